@@ -1,0 +1,584 @@
+"""CPU oracle for the SAC / SAC-EO update hot path.
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path (``sac-expert_amd/``)
+may import this module; only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` use it, and only as the checker / the
+timed CPU port.
+
+What it is
+----------
+A NumPy restatement of the reference's TensorFlow-eager update math, written
+from the reference sources (all citations relative to noc-lab/sac-expert):
+
+* replay sampling / gather          sac_eo/common/buffers.py:126-144
+* normaliser                        sac_eo/common/normalizer.py:26-58
+* Keras Dense MLP                   sac_eo/common/nn_utils.py:59-138
+* squashed Gaussian evaluate/sample sac_eo/actors/continuous_actors.py:270-379
+* Q critic _forward / value         sac_eo/critics/critics.py:84-103
+* twin-Q target                     sac_eo/algs/SAC_expert.py:211-229
+* critic update                     sac_eo/algs/SAC_expert.py:232-259
+* actor (+ expert term) and alpha   sac_eo/algs/SAC_expert.py:262-356 (SAC.py:178-217)
+* Polyak sync                       sac_eo/algs/SAC_expert.py:362-373
+* one gradient step                 sac_eo/algs/SAC_expert.py:463-477 (SAC.py:236-250)
+* world-model sample / loss         sac_eo/models/continuous_models.py:244-302
+* model-fit step                    sac_eo/algs/mbrl_onpolicy_alg.py:301-319
+* Keras Adam (legacy OptimizerV2, epsilon-hat form, eps=1e-7)
+
+Backward passes are written in closed form (the reference uses
+tf.GradientTape); ``tests/test_oracle.py`` checks them against torch autograd
+in fp64 on the same forward formulas.
+
+Precision modes: ``np.float64`` (reference-quality arithmetic) and
+``np.float32`` (op-by-op emulation of the TF fp32 graph: every elementwise op
+rounds to fp32, constants are cast the way TF casts python / numpy scalars).
+
+Parity status: the random streams are pinned bit-exactly against NumPy's own
+legacy ``RandomState`` (the reference's RNG; see oracle/mt19937.c and
+tests/golden/).  The floating-point math is *parity unpinned* against the
+reference itself: TensorFlow is not installable in this image and the
+reference ships no tests or golden numbers for this path.
+"""
+from __future__ import annotations
+
+import dataclasses
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+LOG_STD_MIN = -5.0   # continuous_actors.py:250
+LOG_STD_MAX = 2.0    # continuous_actors.py:251
+
+
+# ---------------------------------------------------------------------------
+# configuration / state containers
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class Config:
+    S: int = 17
+    A: int = 6
+    hidden: Sequence[int] = (256, 256)
+    act: str = "relu"
+    B: int = 256
+    gamma: float = 0.995          # train_parser.py:160
+    tau: float = 5e-3             # train_parser.py:326
+    lr_q: float = 3e-4            # train_parser.py:310
+    lr_pi: float = 1e-4           # train_parser.py:312
+    lr_alpha: float = 1e-4        # train_parser.py:314
+    init_temperature: float = 0.1  # train_parser.py:308
+    act_limit: float = 1.0
+    per_state_std: bool = False
+    # SAC-EO
+    epsilon: float = 1e-3         # train_parser.py:280
+    model_hidden: Sequence[int] = (512, 512)
+    model_act: str = "relu"
+    lr_model: float = 1e-3
+    reward_loss_coef: float = 1.0
+
+    @property
+    def target_entropy(self) -> float:
+        return -float(self.A)     # SAC_expert.py:46
+
+
+@dataclasses.dataclass
+class Normalizers:
+    """(x - mean) / max(std, 1e-8) per normalizer.py:26-41 ('den' = max(std,1e-8))."""
+    s_mean: np.ndarray
+    s_den: np.ndarray
+    a_mean: np.ndarray
+    a_den: np.ndarray
+    d_mean: np.ndarray
+    d_den: np.ndarray
+    r_mean: float = 0.0
+    r_den: float = 1.0
+    ret_den: float = 1.0
+
+    @staticmethod
+    def identity(S: int, A: int) -> "Normalizers":
+        z = np.zeros
+        o = np.ones
+        return Normalizers(z(S, np.float32), o(S, np.float32), z(A, np.float32),
+                           o(A, np.float32), z(S, np.float32), o(S, np.float32))
+
+    def cast(self, dt):
+        c = lambda x: np.asarray(x, dtype=dt)
+        return Normalizers(c(self.s_mean), c(self.s_den), c(self.a_mean), c(self.a_den),
+                           c(self.d_mean), c(self.d_den), c(self.r_mean), c(self.r_den),
+                           c(self.ret_den))
+
+
+@dataclasses.dataclass
+class AdamState:
+    t: int
+    m: List[np.ndarray]
+    v: List[np.ndarray]
+
+    @staticmethod
+    def zeros_like(params: List[np.ndarray]) -> "AdamState":
+        return AdamState(0, [np.zeros_like(p) for p in params], [np.zeros_like(p) for p in params])
+
+
+@dataclasses.dataclass
+class SACState:
+    """Keras weight-list layout [W0(in,out), b0, W1, b1, W2, b2] per net
+    (pinned by the reference's pickled logs); the actor's global
+    logstd (1,A) variable is kept separately (continuous_actors.py:56-58)."""
+    actor: List[np.ndarray]
+    logstd: np.ndarray
+    q: List[List[np.ndarray]]
+    q_targ: List[List[np.ndarray]]
+    alpha: np.ndarray
+    opt_actor: AdamState
+    opt_q: List[AdamState]
+    opt_alpha: AdamState
+    models: Optional[List[List[np.ndarray]]] = None
+    opt_model: Optional[AdamState] = None
+
+    def copy(self) -> "SACState":
+        cp = lambda L: [x.copy() for x in L]
+        cpo = lambda o: AdamState(o.t, cp(o.m), cp(o.v))
+        return SACState(cp(self.actor), self.logstd.copy(), [cp(x) for x in self.q],
+                        [cp(x) for x in self.q_targ], self.alpha.copy(), cpo(self.opt_actor),
+                        [cpo(o) for o in self.opt_q], cpo(self.opt_alpha),
+                        None if self.models is None else [cp(x) for x in self.models],
+                        None if self.opt_model is None else cpo(self.opt_model))
+
+    def astype(self, dt) -> "SACState":
+        c = lambda L: [np.asarray(x, dtype=dt).copy() for x in L]
+        co = lambda o: AdamState(o.t, c(o.m), c(o.v))
+        return SACState(c(self.actor), np.asarray(self.logstd, dt).copy(), [c(x) for x in self.q],
+                        [c(x) for x in self.q_targ], np.asarray(self.alpha, dt).copy(),
+                        co(self.opt_actor), [co(o) for o in self.opt_q], co(self.opt_alpha),
+                        None if self.models is None else [c(x) for x in self.models],
+                        None if self.opt_model is None else co(self.opt_model))
+
+
+# ---------------------------------------------------------------------------
+# initialisation (orthogonal, nn_utils.py:24-57; TF's RNG is not reproducible,
+# so parity tests inject these weights identically into oracle and device)
+# ---------------------------------------------------------------------------
+def orthogonal(rng: np.random.RandomState, shape, gain: float) -> np.ndarray:
+    rows, cols = int(np.prod(shape[:-1])), int(shape[-1])
+    flat = (rows, cols) if rows >= cols else (cols, rows)
+    a = rng.normal(size=flat)
+    q, r = np.linalg.qr(a)
+    q = q * np.sign(np.diag(r))
+    if rows < cols:
+        q = q.T
+    return (gain * q).reshape(shape).astype(np.float32)
+
+
+def init_mlp(rng, in_dim: int, out_dim: int, hidden: Sequence[int], gain_final: float,
+             bias_scale: float = 0.0) -> List[np.ndarray]:
+    dims = [in_dim] + list(hidden) + [out_dim]
+    params = []
+    for l in range(len(dims) - 1):
+        g = math.sqrt(2.0) if l < len(dims) - 2 else gain_final
+        params.append(orthogonal(rng, (dims[l], dims[l + 1]), g))
+        params.append((bias_scale * rng.normal(size=dims[l + 1])).astype(np.float32))
+    return params
+
+
+def init_state(cfg: Config, seed: int = 1, with_models: bool = False,
+               bias_scale: float = 0.0, actor_gain: float = 0.01, critic_gain: float = 1.0,
+               model_gain: float = 0.01) -> SACState:
+    rng = np.random.RandomState(seed)
+    out_a = 2 * cfg.A if cfg.per_state_std else cfg.A
+    actor = init_mlp(rng, cfg.S, out_a, cfg.hidden, actor_gain, bias_scale)
+    q = [init_mlp(rng, cfg.S + cfg.A, 1, cfg.hidden, critic_gain, bias_scale) for _ in range(2)]
+    q_targ = [[w.copy() for w in net] for net in q]         # init_critic.py:34-35
+    logstd = np.zeros((1, cfg.A), np.float32)
+    alpha = np.asarray(np.log(cfg.init_temperature), np.float32)  # SAC_expert.py:106
+    st = SACState(actor, logstd, q, q_targ, alpha,
+                  AdamState.zeros_like(actor + [logstd]),
+                  [AdamState.zeros_like(n) for n in q], AdamState.zeros_like([alpha]))
+    if with_models:
+        st.models = [init_mlp(rng, cfg.S + cfg.A, cfg.S + 1, cfg.model_hidden, model_gain, bias_scale)
+                     for _ in range(2)]
+        st.opt_model = AdamState.zeros_like(st.models[0] + st.models[1])
+    return st
+
+
+# ---------------------------------------------------------------------------
+# elementwise pieces (TF semantics)
+# ---------------------------------------------------------------------------
+def _F(dt, x):
+    return np.asarray(x, dtype=dt)
+
+
+def act_fwd(z, kind):
+    if kind == "relu":
+        return np.maximum(z, 0)
+    if kind == "tanh":
+        return np.tanh(z)
+    if kind == "elu":            # TF: features<0 ? exp(x)-1 : x
+        return np.where(z < 0, np.exp(np.minimum(z, 0)) - 1, z).astype(z.dtype)
+    raise ValueError(kind)
+
+
+def act_grad(h, kind):
+    """Derivative expressed through the layer OUTPUT (TF ReluGrad / TanhGrad /
+    EluGrad all take the activation output)."""
+    one = np.ones((), h.dtype)
+    if kind == "relu":
+        return (h > 0).astype(h.dtype)
+    if kind == "tanh":
+        return one - h * h
+    if kind == "elu":
+        return np.where(h < 0, h + one, one).astype(h.dtype)
+    raise ValueError(kind)
+
+
+def softplus(x):
+    # TF softplus_op.h: x > -thr ? x : (x < thr ? exp(x) : log1p(exp(x)))
+    thr = x.dtype.type(np.log(np.finfo(x.dtype).eps) + 2.0)      # < 0
+    xc = np.clip(x, thr, -thr)
+    out = np.where(x > -thr, x, np.where(x < thr, np.exp(np.minimum(x, thr)), np.log1p(np.exp(xc))))
+    return out.astype(x.dtype)
+
+
+# ---------------------------------------------------------------------------
+# MLP (Keras Dense: y = act(x @ W + b))
+# ---------------------------------------------------------------------------
+def mlp_forward(params, x, act):
+    hs = []
+    h = x
+    nl = len(params) // 2
+    out = None
+    for l in range(nl):
+        z = h @ params[2 * l] + params[2 * l + 1]
+        if l < nl - 1:
+            h = act_fwd(z, act)
+            hs.append(h)
+        else:
+            out = z
+    return out, hs
+
+
+def mlp_backward(params, x, hs, dout, act, need_dx=False, need_dw=True):
+    nl = len(params) // 2
+    grads = [None] * len(params)
+    d = dout
+    dx = None
+    for l in reversed(range(nl)):
+        inp = x if l == 0 else hs[l - 1]
+        if need_dw:
+            grads[2 * l] = inp.T @ d
+            grads[2 * l + 1] = d.sum(axis=0)
+        if l > 0:
+            d = (d @ params[2 * l].T) * act_grad(hs[l - 1], act)
+        elif need_dx:
+            dx = d @ params[0].T
+    return grads, dx
+
+
+# ---------------------------------------------------------------------------
+# squashed Gaussian head (continuous_actors.py:270-379)
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class HeadCache:
+    x: np.ndarray
+    t: np.ndarray
+    std: np.ndarray
+    u: np.ndarray
+    mask: np.ndarray      # d clip/d logstd_raw (TF clip_by_value: pass inside [min,max] incl.)
+
+
+def split_head(out, logstd_var, cfg: Config):
+    if cfg.per_state_std:
+        return out[:, :cfg.A], out[:, cfg.A:]       # no softplus (:334-336)
+    return out, np.broadcast_to(logstd_var, out.shape)
+
+
+def head_evaluate(mu, logstd_raw, u, lim, dt):
+    """evaluate(): returns (pi, neglogp_adjusted, cache).  u is the N(0,1)
+    draw already cast to the compute dtype (TF casts numpy f64 -> f32)."""
+    l = np.clip(logstd_raw, _F(dt, LOG_STD_MIN), _F(dt, LOG_STD_MAX)).astype(dt)
+    std = np.exp(l)
+    x = mu + std * u
+    z = (x - mu) / np.exp(l)
+    vec = z * z + _F(dt, 2) * l + _F(dt, np.log(_F(dt, 2 * np.pi)))
+    nlp = _F(dt, 0.5) * vec.sum(axis=-1)
+    corr = _F(dt, 2.0) * (_F(dt, np.log(2.0)) - x - softplus(_F(dt, -2.0) * x))
+    nlp_adj = nlp + corr.sum(axis=-1)
+    t = np.tanh(x)
+    pi = _F(dt, lim) * t
+    mask = ((logstd_raw >= LOG_STD_MIN) & (logstd_raw <= LOG_STD_MAX)).astype(dt)
+    return pi, nlp_adj, HeadCache(x, t, std, u, mask)
+
+
+def head_sample(mu, logstd_raw, u, lim, dt):
+    """sample(deterministic=False) (continuous_actors.py:270-306)."""
+    l = np.clip(logstd_raw, _F(dt, LOG_STD_MIN), _F(dt, LOG_STD_MAX)).astype(dt)
+    std = np.exp(l)
+    x = mu + std * u
+    t = np.tanh(x)
+    mask = ((logstd_raw >= LOG_STD_MIN) & (logstd_raw <= LOG_STD_MAX)).astype(dt)
+    return _F(dt, lim) * t, HeadCache(x, t, std, u, mask)
+
+
+def head_backward(g_pi, c, cache: HeadCache, lim, dt):
+    """Closed-form gradient of pi (and, for evaluate, of neglogp_adjusted with
+    per-row weight c) w.r.t. mu and the unclipped logstd."""
+    one = _F(dt, 1)
+    gx = g_pi * _F(dt, lim) * (one - cache.t * cache.t)
+    if c is not None:
+        gx = gx - _F(dt, 2) * c[:, None] * cache.t
+    dmu = gx
+    dl = gx * cache.std * cache.u
+    if c is not None:
+        dl = dl + c[:, None]
+    dl = dl * cache.mask
+    return dmu, dl
+
+
+# ---------------------------------------------------------------------------
+# Keras Adam (legacy OptimizerV2 / ResourceApplyAdam) and NumPy Polyak
+# ---------------------------------------------------------------------------
+def adam_step(params: List[np.ndarray], grads: List[np.ndarray], opt: AdamState, lr: float, dt):
+    opt.t += 1
+    b1, b2, eps = _F(dt, 0.9), _F(dt, 0.999), _F(dt, 1e-7)
+    tt = _F(dt, opt.t)
+    b1p = np.power(b1, tt)
+    b2p = np.power(b2, tt)
+    one = _F(dt, 1)
+    alpha_t = _F(dt, lr) * np.sqrt(one - b2p) / (one - b1p)
+    for i, (p, g) in enumerate(zip(params, grads)):
+        m, v = opt.m[i], opt.v[i]
+        m += (g - m) * (one - b1)
+        v += (g * g - v) * (one - b2)
+        p -= (m * alpha_t) / (np.sqrt(v) + eps)
+
+
+def polyak(targ: List[np.ndarray], src: List[np.ndarray], tau: float, dt):
+    """SAC_expert.py:362-373 -- two fp32 roundings then an add, no FMA."""
+    c1, c2 = _F(dt, 1.0 - tau), _F(dt, tau)
+    for t, s in zip(targ, src):
+        t[...] = t * c1 + s * c2
+
+
+# ---------------------------------------------------------------------------
+# one SAC / SAC-EO gradient step
+# ---------------------------------------------------------------------------
+@dataclasses.dataclass
+class Expert:
+    s1: np.ndarray
+    sp1: np.ndarray
+    s2: np.ndarray
+    sp2: np.ndarray
+    noise1: np.ndarray
+    noise2: np.ndarray
+    epsilon: float
+
+
+def _norm(x, mean, den):
+    return (x - mean) / den
+
+
+def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, noise_pi, noise_alpha,
+               expert: Optional[Expert] = None, do_polyak: bool = True, keep: Optional[dict] = None):
+    """One ``_update`` (SAC_expert.py:463-477 / SAC.py:236-250), in place on
+    ``st``.  ``batch`` = (s, a, sp, r, d) raw rows; noises are (n, A) arrays.
+    Returns the step statistics.  ``keep`` (optional dict) receives the
+    intermediates used by the stage-level GPU parity tests."""
+    dt = st.alpha.dtype.type
+    F = lambda x: _F(dt, x)
+    nrm = nrm.cast(dt)
+    s, a, sp, r, d = [np.asarray(x, dt) for x in batch]
+    n1, n2, n3 = [np.asarray(x, dt) for x in (noise_t, noise_pi, noise_alpha)]
+    B, S = s.shape
+    lim = cfg.act_limit
+    alpha = st.alpha.copy()
+    actor_all = st.actor
+    stats = {}
+
+    # ---------------- target (_get_Q_target, SAC_expert.py:211-229)
+    sp_n = _norm(sp, nrm.s_mean, nrm.s_den)
+    out_t, hs_t = mlp_forward(actor_all, sp_n, cfg.act)
+    mu_t, ls_t = split_head(out_t, st.logstd, cfg)
+    a_t, nlp_t, _ = head_evaluate(mu_t, ls_t, n1, lim, dt)
+    xq_t = np.concatenate([sp_n, _norm(a_t, nrm.a_mean, nrm.a_den)], axis=1)
+    qt = [mlp_forward(net, xq_t, cfg.act)[0][:, 0] * nrm.ret_den for net in st.q_targ]
+    next_value = np.minimum(qt[0], qt[1]) + alpha * nlp_t
+    y = r + F(cfg.gamma) * ((F(1) - d) * next_value)
+    if keep is not None:
+        keep.update(sp_n=sp_n, actor_h_t=hs_t, mu_t=mu_t, a_t=a_t, nlp_t=nlp_t, qt=qt, y=y)
+
+    # ---------------- critic (_update_critic, :232-259)
+    s_n = _norm(s, nrm.s_mean, nrm.s_den)
+    xq = np.concatenate([s_n, _norm(a, nrm.a_mean, nrm.a_den)], axis=1)
+    for k in range(2):
+        q, hs = mlp_forward(st.q[k], xq, cfg.act)
+        e = q[:, 0] - y
+        stats["q%d_loss" % (k + 1)] = float(np.mean(F(0.5) * e * e))
+        dq = (e * F(1.0 / B))[:, None]
+        grads, _ = mlp_backward(st.q[k], xq, hs, dq, cfg.act)
+        if keep is not None:
+            keep["q%d_h" % k] = hs
+            keep["q%d_out" % k] = q[:, 0]
+            keep["q%d_grads" % k] = grads
+        adam_step(st.q[k], grads, st.opt_q[k], cfg.lr_q, dt)
+
+    # ---------------- actor (_update_actor_and_alpha, :262-338)
+    out_p, hs_p = mlp_forward(actor_all, s_n, cfg.act)
+    mu_p, ls_p = split_head(out_p, st.logstd, cfg)
+    a_p, nlp_p, cache_p = head_evaluate(mu_p, ls_p, n2, lim, dt)
+    xq_p = np.concatenate([s_n, _norm(a_p, nrm.a_mean, nrm.a_den)], axis=1)
+    fq = [mlp_forward(net, xq_p, cfg.act) for net in st.q]
+    q1p, q2p = fq[0][0][:, 0], fq[1][0][:, 0]
+    minq = np.minimum(q1p, q2p)
+    p_loss = np.mean(-alpha * nlp_p - minq)
+    w_sac = F(1.0 - expert.epsilon) if expert is not None else F(1)
+    # d p / d minQ_i = -1/B, split on ties (TF _MinOrMaxGrad)
+    gmin = -w_sac * F(1.0 / B)
+    sel1 = np.where(q1p < q2p, F(1), np.where(q1p == q2p, F(0.5), F(0)))
+    sel2 = np.where(q2p < q1p, F(1), np.where(q1p == q2p, F(0.5), F(0)))
+    dxa = None
+    for k, sel in enumerate((sel1, sel2)):
+        _, dx = mlp_backward(st.q[k], xq_p, fq[k][1], (gmin * sel)[:, None], cfg.act,
+                             need_dx=True, need_dw=False)
+        part = dx[:, S:] / nrm.a_den
+        dxa = part if dxa is None else dxa + part
+    c = np.full(B, -w_sac * alpha * F(1.0 / B), dt)
+    dmu, dl = head_backward(dxa, c, cache_p, lim, dt)
+    rows_x = [s_n]
+    rows_h = [hs_p]
+    rows_dmu = [dmu]
+    rows_dl = [dl]
+    mse = None
+    if expert is not None:
+        eps = F(expert.epsilon)
+        halves = [(expert.s1, expert.sp1, expert.noise1), (expert.s2, expert.sp2, expert.noise2)]
+        diffs = []
+        caches = []
+        for k, (se, spe, ne) in enumerate(halves):
+            se, spe, ne = np.asarray(se, dt), np.asarray(spe, dt), np.asarray(ne, dt)
+            se_n = _norm(se, nrm.s_mean, nrm.s_den)
+            out_e, hs_e = mlp_forward(actor_all, se_n, cfg.act)
+            mu_e, ls_e = split_head(out_e, st.logstd, cfg)
+            ca, cache_e = head_sample(mu_e, ls_e, ne, lim, dt)
+            xm = np.concatenate([se_n, _norm(ca, nrm.a_mean, nrm.a_den)], axis=1)
+            om, hsm = mlp_forward(st.models[k], xm, cfg.model_act)
+            sp_hat = se + (om[:, :S] * nrm.d_den + nrm.d_mean)
+            diffs.append(spe - sp_hat)
+            caches.append((se_n, hs_e, cache_e, xm, hsm, spe, sp_hat))
+        dl_e = F(0.5) * ((diffs[0] ** 2).sum(-1) + (diffs[1] ** 2).sum(-1))
+        mse = np.mean(dl_e)
+        p_loss = (F(1) - eps) * p_loss + eps * mse
+        ne_half = diffs[0].shape[0]
+        for k, (se_n, hs_e, cache_e, xm, hsm, spe, sp_hat) in enumerate(caches):
+            dsp = -eps * F(1.0 / ne_half) * diffs[k]
+            dout = np.zeros((ne_half, S + 1), dt)
+            dout[:, :S] = dsp * nrm.d_den
+            _, dxm = mlp_backward(st.models[k], xm, hsm, dout, cfg.model_act,
+                                  need_dx=True, need_dw=False)
+            dca = dxm[:, S:] / nrm.a_den
+            dmu_e, dl_ee = head_backward(dca, None, cache_e, lim, dt)
+            rows_x.append(se_n)
+            rows_h.append(hs_e)
+            rows_dmu.append(dmu_e)
+            rows_dl.append(dl_ee)
+        stats["mse_loss"] = float(mse)
+    X = np.concatenate(rows_x, 0)
+    Hs = [np.concatenate([h[l] for h in rows_h], 0) for l in range(len(rows_h[0]))]
+    DMU = np.concatenate(rows_dmu, 0)
+    DL = np.concatenate(rows_dl, 0)
+    if cfg.per_state_std:
+        dout_a = np.concatenate([DMU, DL], axis=1)
+        g_logstd = np.zeros_like(st.logstd)
+    else:
+        dout_a = DMU
+        g_logstd = DL.sum(axis=0, keepdims=True)
+    grads_a, _ = mlp_backward(actor_all, X, Hs, dout_a, cfg.act)
+    if keep is not None:
+        keep.update(actor_h_p=hs_p, mu_p=mu_p, a_p=a_p, nlp_p=nlp_p, q1p=q1p, q2p=q2p,
+                    dxa=dxa, dmu=DMU, dl=DL, actor_grads=grads_a, g_logstd=g_logstd)
+    stats["p_loss"] = float(p_loss)
+    adam_step(st.actor + [st.logstd], grads_a + [g_logstd], st.opt_actor, cfg.lr_pi, dt)
+
+    # ---------------- alpha (:340-348)
+    out_3, _ = mlp_forward(st.actor, s_n, cfg.act)
+    mu_3, ls_3 = split_head(out_3, st.logstd, cfg)
+    _, nlp_3, _ = head_evaluate(mu_3, ls_3, n3, lim, dt)
+    m_ent = np.mean(-nlp_3 + F(cfg.target_entropy))
+    stats["alpha_loss"] = float(-alpha * m_ent)
+    g_alpha = np.asarray(-m_ent, dt)
+    al = [st.alpha]
+    adam_step(al, [g_alpha], st.opt_alpha, cfg.lr_alpha, dt)
+    st.alpha = np.maximum(st.alpha, F(1e-5)).astype(dt)
+    stats["alpha"] = float(st.alpha)
+    if keep is not None:
+        keep.update(nlp_3=nlp_3, g_alpha=g_alpha)
+
+    # ---------------- Polyak (:362-373)
+    if do_polyak:
+        for k in range(2):
+            polyak(st.q_targ[k], st.q[k], cfg.tau, dt)
+    return stats
+
+
+# ---------------------------------------------------------------------------
+# world model: loss and one fitting step (continuous_models.py:280-302,
+# mbrl_onpolicy_alg.py:301-319)
+# ---------------------------------------------------------------------------
+def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches):
+    """``batches`` = [(s, a, sp, r)] per model (independent minibatches,
+    SAC_expert.py:519-543).  Sum of the per-model mean losses, one Adam over
+    all model variables.  Returns the summed loss."""
+    dt = st.alpha.dtype.type
+    F = lambda x: _F(dt, x)
+    nrm = nrm.cast(dt)
+    S = cfg.S
+    grads_all = []
+    loss_all = F(0)
+    for k, (s, a, sp, r) in enumerate(batches):
+        s, a, sp, r = [np.asarray(x, dt) for x in (s, a, sp, r)]
+        n = s.shape[0]
+        xm = np.concatenate([_norm(s, nrm.s_mean, nrm.s_den), _norm(a, nrm.a_mean, nrm.a_den)], 1)
+        out, hs = mlp_forward(st.models[k], xm, cfg.model_act)
+        dpred, rpred = out[:, :S], out[:, S]
+        dn = ((sp - s) - nrm.d_mean) / nrm.d_den
+        rn = (r - nrm.r_mean) / nrm.r_den
+        ed = dn - dpred
+        er = rn - rpred
+        per = F(0.5) * (ed * ed).sum(-1) + F(cfg.reward_loss_coef) * (F(0.5) * er * er)
+        loss_all = loss_all + np.mean(per)
+        dout = np.zeros_like(out)
+        dout[:, :S] = -ed * F(1.0 / n)
+        dout[:, S] = -er * F(cfg.reward_loss_coef / n)
+        g, _ = mlp_backward(st.models[k], xm, hs, dout, cfg.model_act)
+        grads_all += g
+    adam_step(st.models[0] + st.models[1], grads_all, st.opt_model, cfg.lr_model, dt)
+    return float(loss_all)
+
+
+# ---------------------------------------------------------------------------
+# RNG consumption in the reference's order ("RNG consumption
+# order"): the global legacy NumPy stream feeds the sampler and every noise
+# draw; the expert split uses the algorithm's Generator (base_onpolicy_alg.py:109).
+# ---------------------------------------------------------------------------
+def draw_step_randoms(rs, cur_size: int, B: int, A: int, n_expert: int = 0, gen=None):
+    idx = rs.randint(cur_size, size=B)                          # buffers.py:136
+    n1 = rs.normal(size=(B, A))                                 # target evaluate(sp)
+    n2 = rs.normal(size=(B, A))                                 # actor evaluate(s)
+    out = {"idx": idx, "noise_t": n1, "noise_pi": n2}
+    if n_expert:
+        perm = np.arange(n_expert)
+        gen.shuffle(perm)                                       # SAC_expert.py:301-303
+        sec = np.array_split(perm, 2)
+        out["perm"] = perm
+        out["sections"] = sec
+        out["noise_e1"] = rs.normal(size=(len(sec[0]), A))      # sample(s_expert_one)
+        out["noise_e2"] = rs.normal(size=(len(sec[1]), A))      # sample(s_expert_two)
+    out["noise_alpha"] = rs.normal(size=(B, A))                 # alpha evaluate(s)
+    return out
+
+
+def gather(buf, idx):
+    """buffers.py:137-141: rows s, a, sp, r, d at idx (logical order)."""
+    return buf["s"][idx], buf["a"][idx], buf["sp"][idx], buf["r"][idx], buf["d"][idx]
+
+
+def f32_noise(x):
+    """TF converts the float64 numpy draw to float32 (round to nearest)."""
+    return np.asarray(x, np.float64).astype(np.float32)

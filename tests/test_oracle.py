@@ -1,0 +1,233 @@
+"""Pins the CPU oracle (test infrastructure) before it is trusted.
+
+* the C MT19937 restatement vs NumPy's legacy RandomState (the reference's
+  RNG, sac_eo/common/buffers.py:136, continuous_actors.py:351) and vs the
+  committed golden vectors (tests/golden/rng_golden.npz);
+* the closed-form backward of sac_oracle vs torch autograd (fp64) on the same
+  forward formulas (reference: tf.GradientTape in SAC_expert.py:238-347);
+* fp32 emulation vs fp64 reference over a short trajectory.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import sac_oracle as O
+from mt_oracle import MTOracle
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# ----------------------------------------------------------------- RNG
+@pytest.mark.parametrize("seed", [0, 2773201285, 2590541744])
+def test_mt_oracle_matches_numpy(seed):
+    rs = np.random.RandomState(seed)
+    mo = MTOracle(seed)
+    for high in [1, 2, 3, 777, 5000, 2 ** 20, 10 ** 6, 4 * 10 ** 6, 2 ** 31]:
+        assert np.array_equal(rs.randint(high, size=301), mo.randint(high, 301))
+        assert np.array_equal(rs.normal(size=(7, 3)), mo.normal((7, 3)))   # odd: exercises the cache
+    a, b = rs.get_state(), mo.get_state()
+    assert np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+
+
+def test_mt_oracle_set_state_roundtrip():
+    rs = np.random.RandomState(7)
+    rs.normal(size=3)          # leaves a cached gaussian
+    mo = MTOracle()
+    mo.set_state(rs.get_state())
+    assert np.array_equal(rs.normal(size=11), mo.normal(11))
+    assert np.array_equal(rs.randint(999_999, size=64), mo.randint(999_999, 64))
+
+
+def test_rng_golden_vectors():
+    g = np.load(os.path.join(GOLD, "rng_golden.npz"))
+    for key in [k for k in g.files if k.startswith("seed_") and k.endswith("_normal")]:
+        name = key[: -len("_normal")]
+        seed = int(name.split("_")[1])
+        for high in g["highs"]:
+            assert np.array_equal(MTOracle(seed).randint(int(high), 256), g[f"{name}_int_{int(high)}"])
+        assert np.array_equal(MTOracle(seed).normal((256, 6)), g[f"{name}_normal"])
+    mo = MTOracle(2590541744)
+    assert np.array_equal(mo.randint(10 ** 6, 256), g["step_idx"])
+    for k in ("noise_t", "noise_pi", "noise_alpha"):
+        assert np.array_equal(mo.normal((256, 6)), g["step_" + k])
+
+
+def test_seed_derivation_known_answer():
+    """sac_eo/train.py:118-128 with --seed 0 (values recorded in the reference's
+    sac_eo/logs/TEMPLOG_0 param.setup_kwargs)."""
+    seeds = np.random.SeedSequence(0).generate_state(5)
+    got = [int(np.random.SeedSequence(seeds[k]).generate_state(1)[0]) for k in range(5)]
+    assert got[:4] == [2773201285, 397334063, 3968933684, 2590541744]
+    assert got[4] == 3892593679
+
+
+# ----------------------------------------------------------------- backward vs autograd
+torch = pytest.importorskip("torch")
+
+
+def _t(x):
+    return torch.tensor(np.asarray(x, np.float64), dtype=torch.float64)
+
+
+def _mlp(params, x, act):
+    h = x
+    n = len(params) // 2
+    hs = []
+    for l in range(n):
+        z = h @ params[2 * l] + params[2 * l + 1]
+        if l < n - 1:
+            h = {"relu": torch.relu, "tanh": torch.tanh,
+                 "elu": torch.nn.functional.elu}[act](z)
+            hs.append(h)
+        else:
+            h = z
+    return h
+
+
+def _head_eval(mu, lraw, u):
+    l = torch.clamp(lraw, -5.0, 2.0)
+    std = torch.exp(l)
+    x = mu + std * u
+    z = (x - mu) / torch.exp(l)
+    nlp = 0.5 * (z * z + 2 * l + np.log(2 * np.pi)).sum(-1)
+    nlp = nlp + (2.0 * (np.log(2.0) - x - torch.nn.functional.softplus(-2.0 * x))).sum(-1)
+    return torch.tanh(x), nlp
+
+
+def _make(cfg, seed=3, bias_scale=0.1):
+    st = O.init_state(cfg, seed=seed, with_models=True, bias_scale=bias_scale,
+                      actor_gain=0.5, model_gain=0.3).astype(np.float64)
+    rs = np.random.RandomState(seed + 10)
+    B, S, A = cfg.B, cfg.S, cfg.A
+    batch = (rs.normal(size=(B, S)), rs.uniform(-1, 1, (B, A)), rs.normal(size=(B, S)),
+             rs.normal(size=B), (rs.uniform(size=B) < 0.2).astype(np.float64))
+    noises = [rs.normal(size=(B, A)) for _ in range(3)]
+    nrm = O.Normalizers(rs.normal(size=S) * 0.1, rs.uniform(0.5, 2, S), rs.normal(size=A) * 0.1,
+                        rs.uniform(0.5, 2, A), rs.normal(size=S) * 0.1, rs.uniform(0.5, 2, S),
+                        0.0, 1.0, 1.0).cast(np.float64)
+    ne = 6
+    ex = O.Expert(rs.normal(size=(ne // 2, S)), rs.normal(size=(ne // 2, S)),
+                  rs.normal(size=(ne // 2, S)), rs.normal(size=(ne // 2, S)),
+                  rs.normal(size=(ne // 2, A)), rs.normal(size=(ne // 2, A)), 0.3)
+    return st, batch, noises, nrm, ex
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "elu"])
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_oracle_backward_matches_autograd(act, use_expert):
+    cfg = O.Config(S=5, A=3, hidden=(16, 12), act=act, B=32, model_hidden=(20, 18))
+    st0, batch, noises, nrm, ex = _make(cfg)
+    st1 = st0.copy()
+    keep = {}
+    O.sac_update(st1, cfg, nrm, batch, *noises, expert=ex if use_expert else None, keep=keep)
+    s, a, sp, r, d = [_t(x) for x in batch]
+    S = cfg.S
+    nm = lambda x, m, dd: (x - _t(m)) / _t(dd)
+
+    # critic grads (pre-Adam) vs autograd; target y from the oracle's own value
+    y = _t(keep["y"])
+    for k in range(2):
+        P = [_t(w).requires_grad_() for w in st0.q[k]]
+        q = _mlp(P, torch.cat([nm(s, nrm.s_mean, nrm.s_den), nm(a, nrm.a_mean, nrm.a_den)], 1), act)
+        loss = torch.mean(0.5 * ((q - y[:, None]) ** 2).sum(-1))
+        g = torch.autograd.grad(loss, P)
+        for gg, mine in zip(g, keep["q%d_grads" % k]):
+            np.testing.assert_allclose(mine, gg.numpy(), rtol=1e-9, atol=1e-12)
+
+    # actor grads with the UPDATED critics and the PRE-update actor/alpha
+    PA = [_t(w).requires_grad_() for w in st0.actor]
+    LS = _t(st0.logstd).requires_grad_()
+    Q = [[_t(w) for w in net] for net in st1.q]
+    s_n = nm(s, nrm.s_mean, nrm.s_den)
+    mu = _mlp(PA, s_n, act)
+    pi, nlp = _head_eval(mu, LS.expand_as(mu), _t(noises[1]))
+    xq = torch.cat([s_n, nm(pi, nrm.a_mean, nrm.a_den)], 1)
+    minq = torch.minimum(_mlp(Q[0], xq, act), _mlp(Q[1], xq, act))
+    alpha = float(st0.alpha)
+    p = torch.mean(-alpha * nlp[:, None] - minq)
+    if use_expert:
+        M = [[_t(w) for w in net] for net in st0.models]
+        sq = []
+        for k, (se, spe, ne) in enumerate([(ex.s1, ex.sp1, ex.noise1), (ex.s2, ex.sp2, ex.noise2)]):
+            se_n = nm(_t(se), nrm.s_mean, nrm.s_den)
+            mue = _mlp(PA, se_n, act)
+            ca = torch.tanh(mue + torch.exp(torch.clamp(LS, -5, 2)) * _t(ne))
+            om = _mlp(M[k], torch.cat([se_n, nm(ca, nrm.a_mean, nrm.a_den)], 1), cfg.model_act)
+            sp_hat = _t(se) + (om[:, :S] * _t(nrm.d_den) + _t(nrm.d_mean))
+            sq.append(((_t(spe) - sp_hat) ** 2).sum(-1))
+        mse = torch.mean(0.5 * (sq[0] + sq[1]))
+        p = (1 - ex.epsilon) * p + ex.epsilon * mse
+    g = torch.autograd.grad(p, PA + [LS])
+    for gg, mine in zip(g[:-1], keep["actor_grads"]):
+        np.testing.assert_allclose(mine, gg.numpy(), rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(keep["g_logstd"], g[-1].numpy(), rtol=1e-7, atol=1e-10)
+
+    # alpha grad: d(-alpha*mean(-nlp + H))/dalpha with the UPDATED actor
+    mu3 = _mlp([_t(w) for w in st1.actor], s_n, act)
+    _, nlp3 = _head_eval(mu3, _t(st1.logstd).expand_as(mu3), _t(noises[2]))
+    al = torch.tensor(alpha, dtype=torch.float64, requires_grad=True)
+    (ga,) = torch.autograd.grad(-al * torch.mean(-nlp3 + cfg.target_entropy), al)
+    np.testing.assert_allclose(float(keep["g_alpha"]), ga.item(), rtol=1e-10)
+
+
+def test_min_tie_split():
+    """TF _MinOrMaxGrad splits the gradient of reduce_min equally on ties."""
+    cfg = O.Config(S=3, A=1, hidden=(8, 8), B=8)
+    st = O.init_state(cfg, seed=2).astype(np.float64)
+    st.q[1] = [w.copy() for w in st.q[0]]          # identical critics -> every row ties
+    st.opt_q[1] = O.AdamState.zeros_like(st.q[1])
+    rs = np.random.RandomState(0)
+    batch = (rs.normal(size=(8, 3)), rs.uniform(-1, 1, (8, 1)), rs.normal(size=(8, 3)),
+             rs.normal(size=8), np.zeros(8))
+    keep = {}
+    O.sac_update(st, cfg, O.Normalizers.identity(3, 1).cast(np.float64), batch,
+                 *[rs.normal(size=(8, 1)) for _ in range(3)], keep=keep)
+    assert np.array_equal(keep["q1p"], keep["q2p"])
+
+
+def test_fp32_emulation_tracks_fp64():
+    cfg = O.Config(S=17, A=6, B=64)
+    st64 = O.init_state(cfg, seed=1).astype(np.float64)
+    st32 = O.init_state(cfg, seed=1)
+    rs = np.random.RandomState(0)
+    N = 500
+    buf = dict(s=rs.normal(size=(N, 17)).astype(np.float32), a=rs.uniform(-1, 1, (N, 6)).astype(np.float32),
+               sp=rs.normal(size=(N, 17)).astype(np.float32), r=rs.normal(size=N).astype(np.float32),
+               d=np.zeros(N))
+    nrm = O.Normalizers.identity(17, 6)
+    g64, g32 = np.random.RandomState(3), np.random.RandomState(3)
+    for _ in range(30):
+        R1 = O.draw_step_randoms(g64, N, 64, 6)
+        R2 = O.draw_step_randoms(g32, N, 64, 6)
+        n = [O.f32_noise(R1[k]) for k in ("noise_t", "noise_pi", "noise_alpha")]
+        s64 = O.sac_update(st64, cfg, nrm, O.gather(buf, R1["idx"]), *n)
+        s32 = O.sac_update(st32, cfg, nrm, O.gather(buf, R2["idx"]), *n)
+        for k in ("q1_loss", "q2_loss"):
+            assert abs(s64[k] - s32[k]) <= 1e-4 * abs(s64[k]) + 1e-7
+
+
+def test_model_fit_step_matches_autograd():
+    cfg = O.Config(S=4, A=2, hidden=(8, 8), B=16, model_hidden=(10, 12))
+    st = O.init_state(cfg, seed=5, with_models=True, bias_scale=0.1, model_gain=0.5).astype(np.float64)
+    rs = np.random.RandomState(1)
+    nrm = O.Normalizers(rs.normal(size=4) * .1, rs.uniform(.5, 2, 4), rs.normal(size=2) * .1,
+                        rs.uniform(.5, 2, 2), rs.normal(size=4) * .1, rs.uniform(.5, 2, 4), 0.2, 1.5, 1.0)
+    batches = [(rs.normal(size=(9, 4)), rs.uniform(-1, 1, (9, 2)), rs.normal(size=(9, 4)),
+                rs.normal(size=9)) for _ in range(2)]
+    M = [[_t(w).requires_grad_() for w in net] for net in st.models]
+    tot = 0
+    for k, (s, a, sp, r) in enumerate(batches):
+        x = torch.cat([(_t(s) - _t(nrm.s_mean)) / _t(nrm.s_den), (_t(a) - _t(nrm.a_mean)) / _t(nrm.a_den)], 1)
+        out = _mlp(M[k], x, "relu")
+        dn = ((_t(sp) - _t(s)) - _t(nrm.d_mean)) / _t(nrm.d_den)
+        rn = (_t(r) - nrm.r_mean) / nrm.r_den
+        tot = tot + torch.mean(0.5 * ((dn - out[:, :4]) ** 2).sum(-1) + 0.5 * (rn - out[:, 4]) ** 2)
+    g = torch.autograd.grad(tot, M[0] + M[1])
+    # reproduce the oracle's first Adam step from the autograd gradients
+    ref = st.copy()
+    O.adam_step(ref.models[0] + ref.models[1], [x.numpy() for x in g], ref.opt_model, cfg.lr_model, np.float64)
+    loss = O.model_fit_step(st, cfg, nrm, batches)
+    assert abs(loss - tot.item()) < 1e-12
+    for w1, w2 in zip(st.models[0] + st.models[1], ref.models[0] + ref.models[1]):
+        np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=1e-14)
