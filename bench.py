@@ -1,0 +1,229 @@
+"""SAC gradient-steps/sec on MI355X (BASELINE.json metric, configs[1]).
+
+Workload (default ``--config hc``): HalfCheetah-v3-shaped synthetic replay
+buffer (obs 17, act 6, 1e6 rows resident in HBM), plain SAC twin-Q + actor +
+alpha update (alg ``sac``, no world model), batch 256, 256x2 relu MLPs, fp32.
+A step = one ``_update`` (SAC.py:236-250): sampler + gather, target, both
+critic Adams, actor Adam, alpha Adam, Polyak.
+
+Multi-GPU: one process per GPU (torch.distributed.run), each an independent
+learner with its own seed -- the reference's ``--runs N`` spawn-pool
+parallelism (train.py:118-152).  No data-path collective; ``value`` is the
+sum of steps over ranks divided by the max-over-ranks wall time (weak scaling).
+
+Extra JSON fields: ``roofline`` for the dominant kernel (HIP-event timed in
+this process) and ``cpu_baseline`` (the CPU oracle port on the host cores,
+rank 0 at N=1, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sac-expert_amd"))
+
+CONFIGS = {
+    # BASELINE.json configs[1]
+    "hc": dict(workload="HalfCheetah-v3-shaped synthetic buffer, SAC twin-Q + actor + alpha update (no model), fp32",
+               S=17, A=6, B=256, hidden=(256, 256), buffer=1_000_000, use_expert=False),
+    # configs[2]-shaped (SAC-EO expert term; model fitting is a separate call)
+    "humanoid_eo": dict(workload="Humanoid-v3-shaped synthetic buffer, SAC-EO update incl. world-model expert term, fp32",
+                        S=376, A=17, B=1024, hidden=(256, 256), buffer=1_000_000, use_expert=True),
+}
+
+FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+HBM_PEAK_GBS = 8000.0
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def build_engine(cfgd, seed, device):
+    import torch
+    from sac_eo.engine import Engine, EngineConfig
+    from sac_eo.nets import create_nn_weights
+    S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
+    ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
+                        buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
+                        expert_capacity=20, graph_steps=8)
+    eng = Engine(ecfg, device=device)
+    rng = np.random.default_rng(seed)
+    eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
+    for k in range(2):
+        w = create_nn_weights(rng, S + A, 1, cfgd["hidden"], 1.0)
+        eng.set_net(f"q{k}", w)
+        eng.set_net(f"t{k}", w)
+    if cfgd["use_expert"]:
+        for k in range(2):
+            eng.set_net(f"m{k}", create_nn_weights(rng, S + A, S + 1, (512, 512), 0.01))
+    # synthetic HalfCheetah-shaped rows generated on the device
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    N = cfgd["buffer"]
+    sig = torch.rand(S, device=device, generator=g) * 4.9 + 0.1
+    s = torch.randn(N, S, device=device, generator=g) * sig
+    sp = torch.randn(N, S, device=device, generator=g) * sig
+    a = torch.rand(N, A, device=device, generator=g) * 2 - 1
+    r = torch.randn(N, device=device, generator=g)
+    d = torch.zeros(N, device=device)
+    eng.append(s, a, r, sp, d)
+    del s, sp, a, r, d
+    if cfgd["use_expert"]:
+        ers = np.random.RandomState(seed + 1)
+        eng.set_expert(ers.normal(size=(20, S)), ers.normal(size=(20, S)), 1e-3)
+        gen = np.random.default_rng(seed + 2)
+        perms = np.stack([gen.permutation(20) for _ in range(4096)])
+        eng.push_perms(perms)
+    eng.rng_seed(seed)
+    eng.sync()
+    return eng
+
+
+def roofline(eng, n_prof=20):
+    info = eng.plan_info()
+    ms = eng.profile(n_prof)          # eager, HIP events around each launch on the engine stream
+    fam = {}
+    for i, L in enumerate(info):
+        f = fam.setdefault(L["kernel"], dict(ms=0.0, flops=0.0, bytes=0.0, launches=0))
+        f["ms"] += ms[i]
+        f["flops"] += L["flops"]
+        f["bytes"] += L["bytes"]
+        f["launches"] += 1
+    dom = max(fam, key=lambda k: fam[k]["ms"])
+    f = fam[dom]
+    avg_s = f["ms"] / f["launches"] * 1e-3
+    flops_per_launch = f["flops"] / f["launches"]
+    achieved = flops_per_launch / avg_s / 1e12
+    per_stage = {L["name"]: round(float(ms[i]) * 1e3, 2) for i, L in enumerate(info)}
+    return {
+        "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
+        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": None,
+        "avg_launch_us": round(avg_s * 1e6, 3), "launches_per_step": f["launches"],
+        "flops_per_launch": flops_per_launch,
+        "step_us_eager_events": round(float(ms.sum()) * 1e3, 2),
+        "stage_us": per_stage,
+    }, fam
+
+
+def cpu_baseline(cfgd, seconds=10.0):
+    """The CPU oracle (numpy fp32 port of the reference update) on the host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sac_oracle as O
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    try:
+        from threadpoolctl import threadpool_limits
+        ctx = threadpool_limits(limits=threads)
+    except Exception:  # pragma: no cover
+        ctx = None
+    S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
+    ocfg = O.Config(S=S, A=A, B=B, hidden=cfgd["hidden"], act="relu")
+    st = O.init_state(ocfg, seed=1)
+    rs = np.random.RandomState(0)
+    N = 100_000   # sample of the buffer; gather cost is independent of N
+    buf = dict(s=rs.normal(size=(N, S)).astype(np.float32), a=rs.uniform(-1, 1, (N, A)).astype(np.float32),
+               sp=rs.normal(size=(N, S)).astype(np.float32), r=rs.normal(size=N).astype(np.float32),
+               d=np.zeros(N))
+    nrm = O.Normalizers.identity(S, A)
+    g = np.random.RandomState(1)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        R = O.draw_step_randoms(g, N, B, A)
+        O.sac_update(st, ocfg, nrm, O.gather(buf, R["idx"]), O.f32_noise(R["noise_t"]),
+                     O.f32_noise(R["noise_pi"]), O.f32_noise(R["noise_alpha"]))
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds and n >= 5:
+            break
+    if ctx is not None:
+        ctx.unregister() if hasattr(ctx, "unregister") else None
+    return {"value": round(n / el, 3), "unit": "gradient-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n} updates of the numpy fp32 oracle (oracle/sac_oracle.py) at the bench shapes, "
+                      f"{el:.1f}s, BLAS threads={threads}; TensorFlow reference not installable"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--config", default="hc", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    ws, rank, local = dist_env()
+    cfgd = CONFIGS[args.config]
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+    eng = build_engine(cfgd, seed=1000 + rank, device=device)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if dist is not None:
+            dist.barrier()
+            torch.cuda.synchronize(device)
+
+    eng.step(args.warmup, num_timesteps=0, ts_increment=1)
+    eng.sync()
+    barrier()
+    t0 = time.perf_counter()
+    eng.step(args.steps, num_timesteps=args.warmup, ts_increment=1)
+    eng.sync()
+    t1 = time.perf_counter()
+    barrier()
+    el = t1 - t0
+    if dist is not None:
+        t = torch.tensor([el], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    stats = eng.stats(1)[0]
+    finite = bool(np.all(np.isfinite(stats)))
+    value = args.steps * ws / el
+    roof = None
+    if rank == 0 and not args.no_roofline:
+        roof, _ = roofline(eng)
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(cfgd, args.cpu_seconds)
+    if rank == 0:
+        line = {
+            "metric": "SAC gradient-steps/sec (batch=256, 256x2 MLP)" if args.config == "hc"
+            else "SAC-EO gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)",
+            "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (HalfCheetah-shaped replay rows generated on device; random orthogonal init)",
+            "config": {"workload": cfgd["workload"], "obs_dim": cfgd["S"], "act_dim": cfgd["A"],
+                       "batch": cfgd["B"], "hidden": list(cfgd["hidden"]), "buffer_rows": cfgd["buffer"],
+                       "parallelism": f"replicas x{ws} (independent seeds, no collective)",
+                       "sampler": "NumPy-legacy MT19937 stream on device (bit-exact indices)"},
+            "finite_stats": finite,
+            "last_stats": {k: float(v) for k, v in zip(
+                ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss", "nlp_mean", "step"], stats)},
+            "roofline": roof, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

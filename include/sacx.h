@@ -1,0 +1,152 @@
+/*
+ * sacx.h -- C ABI of libsacx, the MI355X-native SAC / SAC-EO update engine.
+ *
+ * The reference (noc-lab/sac-expert, TensorFlow-eager Python) has no FFI: its
+ * hot path sits behind duck-typed Python objects.  This ABI is the boundary a
+ * binding (ctypes here) calls in place of the reference
+ * functions named next to each entry.  Everything is plain C: opaque handle,
+ * plain pointers and sizes, int status codes (0 = OK, < 0 = error, message in
+ * sacx_last_error).  No torch types cross the boundary.
+ *
+ * Memory model: the caller allocates ONE device arena (any allocator, e.g. a
+ * torch uint8 CUDA tensor), binds it with sacx_bind(), and addresses named
+ * tensors inside it through the segment table (sacx_layout).  Weights use the
+ * Keras (in, out) row-major layout with the bias stored as one extra row
+ * (W_ext = [W ; b]), so reference get_weights()/set_weights() lists map onto
+ * views (sac_eo/common/nn_utils.py:59-76).  Every call is asynchronous on the
+ * bound HIP stream unless stated otherwise.  A handle is not re-entrant; use
+ * one handle per learner (per GPU / per seed).
+ */
+#ifndef SACX_H
+#define SACX_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SACX_ABI_VERSION 1
+
+typedef struct sacx_handle sacx_handle;
+
+enum sacx_activation { SACX_ACT_RELU = 0, SACX_ACT_TANH = 1, SACX_ACT_ELU = 2 };
+enum sacx_dtype { SACX_F32 = 0, SACX_I32 = 1, SACX_I64 = 2, SACX_U32 = 3, SACX_F64 = 4 };
+enum sacx_role { SACX_ROLE_WORK = 0, SACX_ROLE_PARAM = 1, SACX_ROLE_TARGET = 2, SACX_ROLE_STATE = 3 };
+
+/* Flags for sacx_sac_step. */
+#define SACX_STEP_EXTERNAL_RANDOMS 1  /* skip the device sampler: caller filled slot0.idx / slot0.noise */
+#define SACX_STEP_EAGER 2             /* launch kernels directly instead of replaying a hipGraph */
+
+/* Hyper-parameters; names follow sac_eo/common/train_parser.py. */
+typedef struct sacx_config {
+    int32_t abi_version;        /* = SACX_ABI_VERSION */
+    int32_t s_dim;              /* observation dim (HalfCheetah 17, Humanoid 376) */
+    int32_t a_dim;              /* action dim (6, 17) */
+    int32_t hidden[2];          /* --actor_layers / --critic_layers (same for both) */
+    int32_t activation;         /* --actor_activations / --critic_activations */
+    int32_t batch;              /* --sac_batch_size */
+    int64_t buffer_capacity;    /* --env_buffer_size (ring capacity, rows) */
+    int32_t per_state_std;      /* --actor_per_state_std */
+    int32_t use_expert;         /* alg_type sac_imit (SAC-EO expert regulariser) */
+    int32_t expert_capacity;    /* --expert_buffer_size */
+    int32_t expert_batch;       /* rows of expert data per update (even) */
+    int32_t model_hidden[2];    /* --model_layers */
+    int32_t model_activation;   /* --model_activations */
+    int32_t model_batch;        /* --model_batch_size */
+    int32_t target_update_int;  /* --target_update_int */
+    int32_t graph_steps;        /* updates per captured hipGraph (0 -> 8) */
+    int32_t stats_capacity;     /* rows of the per-update statistics ring (0 -> 4096) */
+    int32_t perm_capacity;      /* per-update expert permutations held on device (0 -> 4096) */
+    float gamma;                /* --gamma */
+    float tau;                  /* --soft_tau */
+    float lr_q;                 /* --q_crit_lr */
+    float lr_pi;                /* --mbpo_actor_lr */
+    float lr_alpha;             /* --mbpo_alpha_lr */
+    float lr_model;             /* --model_lr */
+    float init_temperature;     /* --init_temperature (alpha var = log of it) */
+    float target_entropy;       /* -len(action) (SAC_expert.py:46) */
+    float act_limit;            /* action_space.high (continuous_actors.py:252) */
+    float epsilon;              /* --epsilon (expert weight) */
+    float reward_loss_coef;     /* --reward_loss_coef */
+} sacx_config;
+
+typedef struct sacx_segment {
+    char name[48];
+    uint64_t offset;            /* bytes from arena base */
+    int64_t rows;
+    int64_t cols;
+    int32_t dtype;              /* enum sacx_dtype */
+    int32_t role;               /* enum sacx_role */
+} sacx_segment;
+
+typedef struct sacx_launch_info {
+    char name[32];              /* stage name, e.g. "critic.dW+adam" */
+    char kernel[32];            /* kernel symbol family, e.g. "k_gemm" */
+    int32_t grid;               /* workgroups */
+    int32_t block;              /* threads per workgroup */
+    double flops;               /* algorithmic FLOPs of the launch (unpadded shapes) */
+    double bytes;               /* algorithmic HBM/L2 bytes of the launch */
+} sacx_launch_info;
+
+/* Statistics row written per update into the stats ring (float32 x 8). */
+enum sacx_stat { SACX_STAT_Q1_LOSS = 0, SACX_STAT_Q2_LOSS, SACX_STAT_P_LOSS, SACX_STAT_ALPHA_LOSS,
+                 SACX_STAT_ALPHA, SACX_STAT_MSE_LOSS, SACX_STAT_NLP_MEAN, SACX_STAT_STEP };
+
+/* --- lifecycle ------------------------------------------------------------ */
+/* Replaces the construction done by init_actor / init_critics / init_alg
+ * (sac_eo/actors/init_actor.py:8-30, sac_eo/critics/init_critic.py:5-38,
+ * sac_eo/algs/init_alg.py:9-34): validates the config, computes the layout. */
+int sacx_create(const sacx_config* cfg, sacx_handle** out);
+void sacx_destroy(sacx_handle* h);
+const char* sacx_last_error(const sacx_handle* h);   /* NULL handle: error of the last failed create */
+int64_t sacx_arena_bytes(const sacx_handle* h);
+int sacx_layout(const sacx_handle* h, sacx_segment* segs, int32_t cap, int32_t* n_out);
+/* Binds the caller-owned arena (>= sacx_arena_bytes, 256-B aligned) and the HIP
+ * stream (hipStream_t as void*, NULL = default stream); builds the launch plan.
+ * The caller zero-fills the arena and writes weights / normalisers / RNG state
+ * through the segment views before the first step. */
+int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream);
+
+/* --- data path ------------------------------------------------------------ */
+/* TrajectoryBuffer.add (sac_eo/common/buffers.py:41-71): appends n rows at the
+ * ring head with FIFO truncation to buffer_capacity.  Device pointers, rows of
+ * s[n,S], a[n,A], r[n], sp[n,S], d[n] (0/1 as float). */
+int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const float* r,
+                       const float* sp, const float* d, int64_t n);
+/* expert_reg of _expert_preprocess (sac_eo/algs/SAC_expert.py:375-424): the
+ * expert rows (device pointers s_e[n,S], sp_e[n,S]) used by every following
+ * update, and the regulariser weight epsilon. */
+int sacx_expert_set(sacx_handle* h, const float* s_e, const float* sp_e, int32_t n, float epsilon);
+/* Host array perms[n_steps, expert_batch]: the self.rng.shuffle permutations
+ * (sac_eo/algs/SAC_expert.py:301-303) for the next n_steps updates. */
+int sacx_perm_push(sacx_handle* h, const int32_t* perms, int64_t n_steps);
+
+/* --- RNG (the reference's global NumPy legacy MT19937 stream) ------------- */
+/* np.random.seed / RandomState.set_state / get_state (sac_eo/common/seeding.py:12).
+ * set/get are synchronous with respect to the bound stream. */
+int sacx_rng_seed(sacx_handle* h, uint32_t seed);
+int sacx_rng_set_state(sacx_handle* h, const uint32_t key[624], int32_t pos, int32_t has_gauss, double gauss);
+int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t* has_gauss, double* gauss);
+
+/* --- the hot path ---------------------------------------------------------- */
+/* n_steps x SAC_exp._update / SAC._update (sac_eo/algs/SAC_expert.py:463-477,
+ * sac_eo/algs/SAC.py:236-250): sample + gather, twin-Q target, Q1/Q2 Adam,
+ * actor (+ expert term) Adam, alpha Adam + clamp, Polyak.  ts_increment is
+ * added to num_timesteps after every update (1 = SAC_exp.train, 0 = repeated
+ * updates at one env step as in SAC.train). */
+int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment,
+                  int32_t flags);
+int sacx_sync(sacx_handle* h);
+
+/* --- measurement ----------------------------------------------------------- */
+int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);
+/* Runs n_steps updates eagerly with a HIP event around every launch on the
+ * bound stream and returns the summed device milliseconds per launch index
+ * (array of length n_launches from sacx_plan_info).  Synchronous. */
+int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SACX_H */

@@ -1,0 +1,913 @@
+// libsacx host side: arena layout, launch plan of one SAC / SAC-EO update,
+// hipGraph capture and the C ABI declared in include/sacx.h.
+//
+// One update (SAC_expert.py:463-477) is planned as this launch sequence
+// (reference function each stage restates in brackets):
+//   rng            sampler: randint + all normals of the update   [buffers.py:136, continuous_actors.py:351]
+//   gather         replay rows -> normalised staging               [buffers.py:137-141, normalizer.py:36-41]
+//   actor.fwd0/1   actor MLP on [sp ; s ; s_expert]               [continuous_actors.py:327-331]
+//   actor.head     evaluate(sp), evaluate(s), sample(s_expert)     [continuous_actors.py:270-379]
+//   q.fwd0/1       target nets on (sp,a'), critics on (s,a), models on (s_e, c_a)
+//   q.head         min target, TD target, critic loss grads, expert MSE  [SAC_expert.py:211-250, 321-334]
+//   critic.bwd1    dX through critic layer 2 (+ model layer 2)
+//   critic.adam    dW of q0/q1 + Keras Adam + Polyak into t0/t1  [SAC_expert.py:243,250,362-373]
+//   pi.q.fwd0/1    updated critics on (s, pi(s))                  [SAC_expert.py:314-317]
+//   pi.q.head      min + policy loss grads                        [SAC_expert.py:317-319]
+//   pi.q.bwd1      dX through critic layer 2
+//   actor.head.bwd action grads -> tanh-Gaussian backward -> actor layer 3 dX
+//   actor.bwd1     dX through actor layer 2
+//   actor.adam     dW of the actor (+ logstd) + Keras Adam        [SAC_expert.py:336-338]
+//   alpha.fwd0/1   updated actor on s                              [SAC_expert.py:341-343]
+//   alpha.head     evaluate + alpha loss + Adam + clamp + stats   [SAC_expert.py:345-356]
+#include "sacx.h"
+#include "sacx_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstddef>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+using namespace sacx;
+
+namespace {
+
+std::string g_create_error;
+
+inline int64_t r4(int64_t x) { return (x + 3) & ~int64_t(3); }
+
+struct SegInfo {
+    std::string name;
+    uint64_t off;
+    int64_t rows, cols;
+    int dtype, role;
+};
+
+struct Launch {
+    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD } kind;
+    std::string name;
+    RngArgs rng;
+    GatherArgs gather;
+    GemmArgs gemm;
+    HeadArgs head;
+    FinalArgs fin;
+    QHeadArgs qh;
+    ActorBwdArgs ab;
+    int grid = 0, block = 256;
+    double flops = 0, bytes = 0;
+    int gemm_first = 0;  // index of the first problem in the host table (GEMM)
+};
+
+const char* kernel_family(Launch::Kind k) {
+    switch (k) {
+        case Launch::RNG: return "k_rng";
+        case Launch::GATHER: return "k_gather";
+        case Launch::GEMM: return "k_gemm";
+        case Launch::AHEAD: return "k_actor_head";
+        case Launch::QHEAD: return "k_qhead";
+        case Launch::ABWD: return "k_actor_bwd";
+    }
+    return "?";
+}
+
+}  // namespace
+
+struct sacx_handle {
+    sacx_config cfg{};
+    std::string err;
+    // dims
+    int S = 0, A = 0, H0 = 0, H1 = 0, B = 0, Aout = 0, ne = 0, Hm0 = 0, Hm1 = 0, ecap = 0;
+    int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0, act = 0, mact = 0;
+    int64_t cap = 0;
+    int graph_steps = 8, stats_cap = 4096, perm_cap = 4096;
+    // layout
+    std::vector<SegInfo> segs;
+    std::map<std::string, size_t> seg_index;
+    uint64_t arena_bytes = 0;
+    uint64_t param_off = 0;
+    int64_t p_stride = 0;  // floats
+    // binding
+    char* arena = nullptr;
+    hipStream_t stream = nullptr;
+    hipStream_t cap_stream = nullptr, rng_stream = nullptr;
+    bool bound = false;
+    std::vector<Launch> plan[2];
+    std::vector<GemmProb> probs;
+    GemmProb* d_probs = nullptr;
+    std::map<std::pair<int, int>, hipGraphExec_t> graphs;
+    std::vector<hipEvent_t> events;
+    int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
+
+    uint64_t add(const std::string& name, int64_t rows, int64_t cols, int dtype, int role) {
+        const int esz = (dtype == SACX_I64 || dtype == SACX_F64) ? 8 : 4;
+        const uint64_t off = (arena_bytes + 255) & ~uint64_t(255);
+        segs.push_back({name, off, rows, cols, dtype, role});
+        seg_index[name] = segs.size() - 1;
+        arena_bytes = off + (uint64_t)(rows * cols * esz);
+        return off;
+    }
+    void alias(const std::string& name, uint64_t off, int64_t rows, int64_t cols, int dtype, int role) {
+        segs.push_back({name, off, rows, cols, dtype, role});
+        seg_index[name] = segs.size() - 1;
+    }
+    const SegInfo& seg(const std::string& n) const { return segs.at(seg_index.at(n)); }
+    template <class T>
+    T* ptr(const std::string& n) const { return reinterpret_cast<T*>(arena + seg(n).off); }
+    float* f(const std::string& n) const { return ptr<float>(n); }
+    Ctl* ctl() const { return ptr<Ctl>("ctl"); }
+};
+
+namespace {
+
+int fail(sacx_handle* h, const std::string& msg) {
+    if (h) h->err = msg;
+    return -1;
+}
+
+#define HIPCHK(h, x)                                                                    \
+    do {                                                                                \
+        hipError_t e_ = (x);                                                            \
+        if (e_ != hipSuccess) return fail((h), std::string(#x " -> ") + hipGetErrorString(e_)); \
+    } while (0)
+
+void build_layout(sacx_handle* h) {
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B;
+    const int F = SACX_F32;
+    // ---------------- parameters (Keras W_ext = [W ; b] per Dense layer)
+    h->arena_bytes = 0;
+    auto net = [&](const std::string& n, int in, int out, int role, int h0, int h1) {
+        h->add(n + ".l0", in + 1, h0, F, role);
+        h->add(n + ".l1", h0 + 1, h1, F, role);
+        h->add(n + ".l2", h1 + 1, out, F, role);
+    };
+    net("actor", S, h->Aout, SACX_ROLE_PARAM, H0, H1);
+    h->add("actor.logstd", 1, A, F, SACX_ROLE_PARAM);
+    net("q0", S + A, 1, SACX_ROLE_PARAM, H0, H1);
+    net("q1", S + A, 1, SACX_ROLE_PARAM, H0, H1);
+    net("t0", S + A, 1, SACX_ROLE_TARGET, H0, H1);
+    net("t1", S + A, 1, SACX_ROLE_TARGET, H0, H1);
+    h->add("alpha", 1, 1, F, SACX_ROLE_PARAM);
+    if (h->cfg.use_expert) {
+        net("m0", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
+        net("m1", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
+    }
+    const uint64_t pbytes = (h->arena_bytes + 255) & ~uint64_t(255);
+    h->param_off = 0;
+    h->p_stride = (int64_t)(pbytes / 4);
+    h->alias("params", 0, 1, h->p_stride, F, SACX_ROLE_PARAM);
+    h->arena_bytes = pbytes;
+    h->add("adam_m", 1, h->p_stride, F, SACX_ROLE_STATE);
+    h->add("adam_v", 1, h->p_stride, F, SACX_ROLE_STATE);
+    // ---------------- normalisers (normalizer.py: (x - mean) / max(std, 1e-8))
+    h->add("norm.s_mean", 1, S, F, SACX_ROLE_STATE);
+    h->add("norm.s_den", 1, S, F, SACX_ROLE_STATE);
+    h->add("norm.a_mean", 1, A, F, SACX_ROLE_STATE);
+    h->add("norm.a_den", 1, A, F, SACX_ROLE_STATE);
+    h->add("norm.d_mean", 1, S, F, SACX_ROLE_STATE);
+    h->add("norm.d_den", 1, S, F, SACX_ROLE_STATE);
+    h->add("norm.r", 1, 2, F, SACX_ROLE_STATE);  // r_mean, r_den
+    h->add("norm.ret_den", 1, 1, F, SACX_ROLE_STATE);
+    // ---------------- control + RNG
+    h->add("ctl", 1, 32, SACX_I64, SACX_ROLE_STATE);
+    const uint64_t roff = h->add("rng", 1, sizeof(RngState) / 4, SACX_U32, SACX_ROLE_STATE);
+    h->alias("rng.key", roff, 1, 624, SACX_U32, SACX_ROLE_STATE);
+    h->alias("rng.pos", roff + offsetof(RngState, pos), 1, 2, SACX_I32, SACX_ROLE_STATE);
+    h->alias("rng.gauss", roff + offsetof(RngState, gauss), 1, 1, SACX_F64, SACX_ROLE_STATE);
+    for (int s = 0; s < 2; ++s) {
+        h->add("slot" + std::to_string(s) + ".idx", 1, B, SACX_I32, SACX_ROLE_WORK);
+        h->add("slot" + std::to_string(s) + ".noise", 1, h->n_norm, F, SACX_ROLE_WORK);
+    }
+    // ---------------- data
+    h->add("replay", h->cap, h->stride, F, SACX_ROLE_STATE);
+    const int ecap = std::max(1, h->ecap), ne1 = std::max(1, h->ne);
+    h->add("expert.s", ecap, S, F, SACX_ROLE_STATE);
+    h->add("expert.sp", ecap, S, F, SACX_ROLE_STATE);
+    h->add("perm", h->perm_cap, ne1, SACX_I32, SACX_ROLE_STATE);
+    h->add("stats", h->stats_cap, 8, F, SACX_ROLE_STATE);
+    h->add("red", 1, 1024, F, SACX_ROLE_WORK);
+    // ---------------- workspace
+    const int Ra = h->Ra, Rb = h->Rb, Hm0 = std::max(1, h->Hm0), Hm1 = std::max(1, h->Hm1);
+    h->add("ws.Xa", Ra, h->ldS, F, 0);
+    h->add("ws.Xq", B, h->ldQ, F, 0);
+    h->add("ws.Xt", B, h->ldQ, F, 0);
+    h->add("ws.Xp", B, h->ldQ, F, 0);
+    h->add("ws.Xm", ne1, h->ldQ, F, 0);
+    h->add("ws.r", 1, B, F, 0);
+    h->add("ws.d", 1, B, F, 0);
+    h->add("ws.se_raw", ne1, S, F, 0);
+    h->add("ws.spe_raw", ne1, S, F, 0);
+    h->add("ws.Ha1", Ra, H0, F, 0);
+    h->add("ws.Ha2", Ra, H1, F, 0);
+    h->add("ws.c_t", Rb, A, F, 0);
+    h->add("ws.c_std", Rb, A, F, 0);
+    h->add("ws.c_u", Rb, A, F, 0);
+    h->add("ws.c_mask", Rb, A, F, 0);
+    h->add("ws.nlp_t", 1, B, F, 0);
+    h->add("ws.nlp_p", 1, B, F, 0);
+    h->add("ws.nlp3", 1, B, F, 0);
+    h->add("ws.Hq1", 4 * B, H0, F, 0);
+    h->add("ws.Hq2", 4 * B, H1, F, 0);
+    h->add("ws.Dq2", 2 * B, H1, F, 0);
+    h->add("ws.Dq1", 2 * B, H0, F, 0);
+    h->add("ws.gq", 2, B, F, 0);
+    h->add("ws.lq", 2, B, F, 0);
+    h->add("ws.Hp1", 2 * B, H0, F, 0);
+    h->add("ws.Hp2", 2 * B, H1, F, 0);
+    h->add("ws.Dp2", 2 * B, H1, F, 0);
+    h->add("ws.Dp1", 2 * B, H0, F, 0);
+    h->add("ws.lp", 1, B, F, 0);
+    h->add("ws.Hm1", ne1, Hm0, F, 0);
+    h->add("ws.Hm2", ne1, Hm1, F, 0);
+    h->add("ws.Dm2", ne1, Hm1, F, 0);
+    h->add("ws.Dm1", ne1, Hm0, F, 0);
+    h->add("ws.mse", 1, ne1, F, 0);
+    h->add("ws.Da3", Rb, h->Aout, F, 0);
+    h->add("ws.Da2", Rb, H1, F, 0);
+    h->add("ws.Da1", Rb, H0, F, 0);
+    h->add("ws.E", Rb, A, F, 0);
+    h->add("ws.Hl1", B, H0, F, 0);
+    h->add("ws.Hl2", B, H1, F, 0);
+    h->arena_bytes = (h->arena_bytes + 255) & ~uint64_t(255);
+}
+
+// ---------------------------------------------------------------- GEMM problem helpers
+GemmProb prob_fwd(const float* X, int ldx, int M, int K, const float* Wext, int N, float* C, int act) {
+    GemmProb p{};
+    p.A = X; p.lda = ldx; p.a_kc = 1; p.ones_row = -1;
+    p.B = Wext; p.ldb = N; p.b_kc = 0;
+    p.M = M; p.N = N; p.K = K;
+    p.bias = Wext + (size_t)K * N;
+    p.C = C; p.ldc = N;
+    p.epi = EPI_FWD; p.act = act;
+    return p;
+}
+
+// C = (D * W^T) (.) act'(Hprev), W_ext is [(K_in+1) x N_out]; C is [M x K_in]
+GemmProb prob_dx(const float* D, int M, int Nout, const float* Wext, int Kin, const float* Hprev, float* C, int act) {
+    GemmProb p{};
+    p.A = D; p.lda = Nout; p.a_kc = 1; p.ones_row = -1;
+    p.B = Wext; p.ldb = Nout; p.b_kc = 1;   // B[k][n] = W[n][k]
+    p.M = M; p.N = Kin; p.K = Nout;
+    p.H = Hprev; p.ldh = Kin;
+    p.C = C; p.ldc = Kin;
+    p.epi = EPI_DACT; p.act = act;
+    return p;
+}
+
+// dW_ext = [X | 1]^T * D over R rows, then Adam (+ Polyak into T)
+GemmProb prob_dw(const float* X, int ldx, int Kin, int R, const float* D, int Nout, float* P, float* T, int group) {
+    GemmProb p{};
+    p.A = X; p.lda = ldx; p.a_kc = 0; p.ones_row = Kin;
+    p.B = D; p.ldb = Nout; p.b_kc = 0;
+    p.M = Kin + 1; p.N = Nout; p.K = R;
+    p.P = P; p.T = T; p.ldp = Nout;
+    p.epi = EPI_ADAM; p.group = group; p.grad_scale = 1.f;
+    return p;
+}
+
+double gemm_flops(const GemmProb& p) { return 2.0 * p.M * p.N * p.K; }
+double gemm_bytes(const GemmProb& p) {
+    double b = 4.0 * ((double)p.M * p.K + (double)p.K * p.N + (double)p.M * p.N);
+    if (p.epi == EPI_ADAM) b += 4.0 * p.M * p.N * (p.T ? 8 : 6) - 4.0 * p.M * p.N;
+    if (p.epi == EPI_DACT) b += 4.0 * p.M * p.N;
+    return b;
+}
+
+void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name, std::vector<GemmProb> ps,
+              bool record_probs) {
+    Launch L{};
+    L.kind = Launch::GEMM;
+    L.name = name;
+    int tiles = 0;
+    for (auto& p : ps) {
+        p.tiles_n = (p.N + 15) / 16;
+        p.tile_begin = tiles;
+        tiles += ((p.M + 15) / 16) * p.tiles_n;
+        L.flops += gemm_flops(p);
+        L.bytes += gemm_bytes(p);
+    }
+    L.gemm_first = (int)h->probs.size();
+    if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
+    L.gemm.nprob = (int)ps.size();
+    L.gemm.total_tiles = tiles;
+    L.gemm.p_stride = h->p_stride;
+    L.gemm.ctl = h->ctl();
+    L.gemm.adam.lr[GRP_Q] = h->cfg.lr_q;
+    L.gemm.adam.lr[GRP_PI] = h->cfg.lr_pi;
+    L.gemm.adam.lr[GRP_ALPHA] = h->cfg.lr_alpha;
+    L.gemm.adam.lr[GRP_MODEL] = h->cfg.lr_model;
+    L.gemm.adam.tau_keep = (float)(1.0 - (double)h->cfg.tau);
+    L.gemm.adam.tau_take = h->cfg.tau;
+    L.gemm.adam.target_update_int = h->cfg.target_update_int;
+    L.grid = tiles;
+    plan.push_back(L);
+}
+
+void build_plan(sacx_handle* h, int slot, bool record_probs) {
+    std::vector<Launch>& plan = h->plan[slot];
+    plan.clear();
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
+    const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
+    const int ldS = h->ldS, ldQ = h->ldQ, act = h->act, mact = h->mact;
+    const bool eo = h->cfg.use_expert != 0;
+    const std::string sl = "slot" + std::to_string(slot);
+    int32_t* idx = h->ptr<int32_t>(sl + ".idx");
+    float* noise = h->f(sl + ".noise");
+    float* noise_t = noise;
+    float* noise_pi = noise + (size_t)B * A;
+    float* noise_e = noise + (size_t)2 * B * A;
+    float* noise_al = noise + (size_t)(2 * B + ne) * A;
+    auto W = [&](const std::string& n) { return h->f(n); };
+    float *Xa = W("ws.Xa"), *Xq = W("ws.Xq"), *Xt = W("ws.Xt"), *Xp = W("ws.Xp"), *Xm = W("ws.Xm");
+    float *Ha1 = W("ws.Ha1"), *Ha2 = W("ws.Ha2");
+    float *Hq1 = W("ws.Hq1"), *Hq2 = W("ws.Hq2"), *Dq1 = W("ws.Dq1"), *Dq2 = W("ws.Dq2");
+    float *Hp1 = W("ws.Hp1"), *Hp2 = W("ws.Hp2"), *Dp1 = W("ws.Dp1"), *Dp2 = W("ws.Dp2");
+    float *Hm1b = W("ws.Hm1"), *Hm2b = W("ws.Hm2"), *Dm1 = W("ws.Dm1"), *Dm2 = W("ws.Dm2");
+    float *Da1 = W("ws.Da1"), *Da2 = W("ws.Da2"), *Da3 = W("ws.Da3"), *E = W("ws.E");
+    float *Hl1 = W("ws.Hl1"), *Hl2 = W("ws.Hl2");
+    const char* qn[4] = {"t0", "t1", "q0", "q1"};
+
+    // ---- sampler
+    {
+        Launch L{};
+        L.kind = Launch::RNG;
+        L.name = "rng";
+        L.rng.st = h->ptr<RngState>("rng");
+        L.rng.ctl = h->ctl();
+        L.rng.n_int = B;
+        L.rng.n_norm = h->n_norm;
+        L.rng.out_idx = idx;
+        L.rng.out_norm = noise;
+        L.grid = 1;
+        L.block = 1024;
+        L.bytes = 4.0 * (B + h->n_norm) + 2.0 * sizeof(RngState);
+        plan.push_back(L);
+    }
+    // ---- gather
+    {
+        Launch L{};
+        L.kind = Launch::GATHER;
+        L.name = "gather";
+        GatherArgs& g = L.gather;
+        g.replay = W("replay"); g.cap = h->cap; g.stride = h->stride;
+        g.S = S; g.A = A; g.B = B; g.ne = ne; g.idx = idx; g.ctl = h->ctl();
+        g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den");
+        g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
+        g.Xa = Xa; g.ldS = ldS; g.Xq = Xq; g.Xt = Xt; g.Xp = Xp; g.Xm = Xm; g.ldQ = ldQ;
+        g.r = W("ws.r"); g.d = W("ws.d");
+        g.exp_s = W("expert.s"); g.exp_sp = W("expert.sp");
+        g.perm_ring = h->ptr<int32_t>("perm"); g.perm_cap = h->perm_cap;
+        g.se_raw = W("ws.se_raw"); g.spe_raw = W("ws.spe_raw");
+        L.grid = (B + ne + 3) / 4;
+        L.bytes = 4.0 * (B * (2.0 * S + A + 2) + ne * 2.0 * S) + 4.0 * (B * (2.0 * ldS + 3.0 * ldQ + 2));
+        plan.push_back(L);
+    }
+    // ---- actor forward on [sp ; s ; s_e]
+    add_gemm(h, plan, "actor.fwd0", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)}, record_probs);
+    add_gemm(h, plan, "actor.fwd1", {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, record_probs);
+    // ---- actor head
+    {
+        Launch L{};
+        L.kind = Launch::AHEAD;
+        L.name = "actor.head";
+        HeadArgs& a = L.head;
+        a.H2 = Ha2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.nseg = eo ? 3 : 2;
+        a.seg[0] = {0, B, 0, 0, noise_t, Xt, W("ws.nlp_t")};
+        a.seg[1] = {B, 2 * B, 0, 0, noise_pi, Xp, W("ws.nlp_p")};
+        a.seg[2] = {2 * B, 2 * B + ne, 1, 0, noise_e, Xm, nullptr};
+        a.total_rows = h->Ra;
+        a.cache_row0 = B;
+        a.c_t = W("ws.c_t"); a.c_std = W("ws.c_std"); a.c_u = W("ws.c_u"); a.c_mask = W("ws.c_mask");
+        a.alpha_mode = 0;
+        L.grid = (h->Ra + 3) / 4;
+        L.flops = 2.0 * h->Ra * H1 * Aout;
+        L.bytes = 4.0 * h->Ra * (H1 + 6.0 * A);
+        plan.push_back(L);
+    }
+    // ---- target / critic / model forward
+    {
+        std::vector<GemmProb> p0, p1;
+        for (int k = 0; k < 4; ++k) {
+            const std::string n = qn[k];
+            p0.push_back(prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, act));
+            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act));
+        }
+        if (eo) {
+            for (int k = 0; k < 2; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                p0.push_back(prob_fwd(Xm + (size_t)k * half * ldQ, ldQ, half, S + A, W(n + ".l0"), Hm0,
+                                      Hm1b + (size_t)k * half * Hm0, mact));
+                p1.push_back(prob_fwd(Hm1b + (size_t)k * half * Hm0, Hm0, half, Hm0, W(n + ".l1"), Hm1,
+                                      Hm2b + (size_t)k * half * Hm1, mact));
+            }
+        }
+        add_gemm(h, plan, "q.fwd0", p0, record_probs);
+        add_gemm(h, plan, "q.fwd1", p1, record_probs);
+    }
+    // ---- q.head: target, critic loss grads, expert MSE
+    {
+        Launch L{};
+        L.kind = Launch::QHEAD;
+        L.name = "q.head";
+        QHeadArgs& q = L.qh;
+        q.mode = 0; q.B = B; q.H1 = H1; q.H2 = Hq2;
+        for (int k = 0; k < 4; ++k) q.W3[k] = W(std::string(qn[k]) + ".l2");
+        q.act = act; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
+        q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = W("ws.r"); q.d = W("ws.d");
+        q.gamma = h->cfg.gamma; q.ret_den = W("norm.ret_den"); q.w_sac = 1.f;
+        q.ne = ne; q.Hm1 = Hm1; q.S = S; q.Hm2 = Hm2b;
+        q.Wm3[0] = eo ? W("m0.l2") : nullptr;
+        q.Wm3[1] = eo ? W("m1.l2") : nullptr;
+        q.mact = mact; q.se_raw = W("ws.se_raw"); q.spe_raw = W("ws.spe_raw");
+        q.d_mean = W("norm.d_mean"); q.d_den = W("norm.d_den"); q.ctl = h->ctl();
+        q.Dm2 = Dm2; q.mse_rows = W("ws.mse");
+        L.grid = (B + ne + 3) / 4;
+        L.flops = 2.0 * B * H1 * 4 + 2.0 * B * H1 * 2 + 4.0 * ne * Hm1 * S;
+        L.bytes = 4.0 * (4.0 * B * H1 + 2.0 * B * H1 * 2);
+        plan.push_back(L);
+    }
+    // ---- critic backward + Adam + Polyak
+    {
+        std::vector<GemmProb> pb;
+        for (int k = 0; k < 2; ++k) {
+            const std::string n = "q" + std::to_string(k);
+            pb.push_back(prob_dx(Dq2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hq1 + (size_t)(2 + k) * B * H0,
+                                 Dq1 + (size_t)k * B * H0, act));
+        }
+        if (eo) {
+            for (int k = 0; k < 2; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                pb.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, half, Hm1, W(n + ".l1"), Hm0,
+                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
+            }
+        }
+        add_gemm(h, plan, "critic.bwd1", pb, record_probs);
+        std::vector<GemmProb> pw;
+        for (int k = 0; k < 2; ++k) {
+            const std::string n = "q" + std::to_string(k), t = "t" + std::to_string(k);
+            pw.push_back(prob_dw(Xq, ldQ, S + A, B, Dq1 + (size_t)k * B * H0, H0, W(n + ".l0"), W(t + ".l0"), GRP_Q));
+            pw.push_back(prob_dw(Hq1 + (size_t)(2 + k) * B * H0, H0, H0, B, Dq2 + (size_t)k * B * H1, H1, W(n + ".l1"),
+                                 W(t + ".l1"), GRP_Q));
+            pw.push_back(prob_dw(Hq2 + (size_t)(2 + k) * B * H1, H1, H1, B, W("ws.gq") + (size_t)k * B, 1,
+                                 W(n + ".l2"), W(t + ".l2"), GRP_Q));
+        }
+        add_gemm(h, plan, "critic.adam", pw, record_probs);
+    }
+    // ---- policy loss through the updated critics
+    {
+        std::vector<GemmProb> p0, p1;
+        for (int k = 0; k < 2; ++k) {
+            const std::string n = "q" + std::to_string(k);
+            p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), H0, Hp1 + (size_t)k * B * H0, act));
+            p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, act));
+        }
+        add_gemm(h, plan, "pi.q.fwd0", p0, record_probs);
+        add_gemm(h, plan, "pi.q.fwd1", p1, record_probs);
+        Launch L{};
+        L.kind = Launch::QHEAD;
+        L.name = "pi.q.head";
+        QHeadArgs& q = L.qh;
+        q.mode = 1; q.B = B; q.H1 = H1; q.H2 = Hp2;
+        q.W3[0] = W("q0.l2"); q.W3[1] = W("q1.l2"); q.W3[2] = nullptr; q.W3[3] = nullptr;
+        q.act = act; q.D2 = Dp2; q.g = nullptr; q.loss_rows = W("ws.lp");
+        q.alpha = W("alpha"); q.nlp = W("ws.nlp_p");
+        q.w_sac = eo ? (float)(1.0 - (double)h->cfg.epsilon) : 1.f;
+        q.ret_den = W("norm.ret_den");
+        q.ne = 0; q.ctl = h->ctl();
+        L.grid = (B + 3) / 4;
+        L.flops = 2.0 * B * H1 * 2 * 2;
+        L.bytes = 4.0 * (2.0 * B * H1 * 2);
+        plan.push_back(L);
+        std::vector<GemmProb> pb;
+        for (int k = 0; k < 2; ++k) {
+            const std::string n = "q" + std::to_string(k);
+            pb.push_back(prob_dx(Dp2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hp1 + (size_t)k * B * H0,
+                                 Dp1 + (size_t)k * B * H0, act));
+        }
+        add_gemm(h, plan, "pi.q.bwd1", pb, record_probs);
+    }
+    // ---- actor backward
+    {
+        Launch L{};
+        L.kind = Launch::ABWD;
+        L.name = "actor.head.bwd";
+        ActorBwdArgs& b = L.ab;
+        b.B = B; b.ne = ne; b.S = S; b.A = A; b.Aout = Aout; b.H0 = H0; b.H1 = H1; b.Hm0 = Hm0;
+        b.per_state_std = h->cfg.per_state_std; b.lim = h->cfg.act_limit;
+        b.Dp1 = Dp1; b.Wq1[0] = W("q0.l0"); b.Wq1[1] = W("q1.l0");
+        b.Dm1 = Dm1; b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W("m1.l0") : nullptr;
+        b.a_den = W("norm.a_den"); b.alpha = W("alpha"); b.ctl = h->ctl(); b.use_expert = eo;
+        b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
+        b.W3a = W("actor.l2"); b.Ha2 = Ha2 + (size_t)B * H1; b.act = act;
+        b.Da3 = Da3; b.Da2 = Da2; b.E = E;
+        L.grid = (h->Rb + 3) / 4;
+        L.flops = 2.0 * B * 2 * H0 * A + 2.0 * ne * Hm0 * A + 2.0 * h->Rb * H1 * Aout;
+        L.bytes = 4.0 * (2.0 * B * H0 + ne * Hm0 + 2.0 * h->Rb * H1);
+        plan.push_back(L);
+        const int Rb = h->Rb;
+        add_gemm(h, plan, "actor.bwd1",
+                 {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, act)}, record_probs);
+        std::vector<GemmProb> pw;
+        pw.push_back(prob_dw(Xa + (size_t)B * ldS, ldS, S, Rb, Da1, H0, W("actor.l0"), nullptr, GRP_PI));
+        pw.push_back(prob_dw(Ha1 + (size_t)B * H0, H0, H0, Rb, Da2, H1, W("actor.l1"), nullptr, GRP_PI));
+        pw.push_back(prob_dw(Ha2 + (size_t)B * H1, H1, H1, Rb, Da3, Aout, W("actor.l2"), nullptr, GRP_PI));
+        if (!h->cfg.per_state_std) {
+            GemmProb p = prob_dw(nullptr, 1, 0, Rb, E, A, W("actor.logstd"), nullptr, GRP_PI);
+            p.ones_row = 0;   // single all-ones row: column sums of E
+            pw.push_back(p);
+        }
+        add_gemm(h, plan, "actor.adam", pw, record_probs);
+    }
+    // ---- alpha: updated actor on s, evaluate, Adam on alpha, statistics
+    add_gemm(h, plan, "alpha.fwd0", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
+             record_probs);
+    add_gemm(h, plan, "alpha.fwd1", {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, record_probs);
+    {
+        Launch L{};
+        L.kind = Launch::AHEAD;
+        L.name = "alpha.head";
+        HeadArgs& a = L.head;
+        a.H2 = Hl2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.nseg = 1;
+        a.seg[0] = {0, B, 0, 0, noise_al, nullptr, W("ws.nlp3")};
+        a.total_rows = B;
+        a.cache_row0 = 1 << 30;
+        a.c_t = nullptr;
+        a.alpha_mode = 1;
+        FinalArgs& f = L.fin;
+        f.alpha = W("alpha"); f.alpha_m = f.alpha + h->p_stride; f.alpha_v = f.alpha + 2 * h->p_stride;
+        f.ctl = h->ctl();
+        f.adam = plan.back().gemm.adam;
+        f.target_entropy = h->cfg.target_entropy;
+        f.B = B; f.ne = ne; f.use_expert = eo;
+        f.lq = W("ws.lq"); f.lp = W("ws.lp"); f.mse_rows = W("ws.mse"); f.red = W("red");
+        f.stats = W("stats"); f.stats_cap = h->stats_cap;
+        L.grid = (B + 3) / 4;
+        L.flops = 2.0 * B * H1 * Aout;
+        L.bytes = 4.0 * B * H1;
+        plan.push_back(L);
+    }
+}
+
+void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
+    switch (L.kind) {
+        case Launch::RNG: launch_rng(L.rng, s); break;
+        case Launch::GATHER: launch_gather(L.gather, s); break;
+        case Launch::GEMM: {
+            GemmArgs g = L.gemm;
+            g.probs = h->d_probs + L.gemm_first;
+            launch_gemm(g, s);
+            break;
+        }
+        case Launch::AHEAD: launch_actor_head(L.head, L.fin, s); break;
+        case Launch::QHEAD: launch_qhead(L.qh, s); break;
+        case Launch::ABWD: launch_actor_bwd(L.ab, s); break;
+    }
+}
+
+void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
+    for (const Launch& L : h->plan[slot]) {
+        if (L.kind == Launch::RNG && !with_rng) continue;
+        enqueue(L, h, s);
+    }
+}
+
+int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
+    auto key = std::make_pair(G, with_rng ? 1 : 0);
+    auto it = h->graphs.find(key);
+    if (it != h->graphs.end()) {
+        *out = it->second;
+        return 0;
+    }
+    hipStream_t cs = h->cap_stream, rs = h->rng_stream;
+    if ((int)h->events.size() < 2 * G + 1) {
+        for (int i = (int)h->events.size(); i < 2 * G + 1; ++i) {
+            hipEvent_t e;
+            HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            h->events.push_back(e);
+        }
+    }
+    hipEvent_t* evR = h->events.data();
+    hipEvent_t* evS = h->events.data() + G;
+    hipEvent_t evFork = h->events[2 * G];
+    HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    if (with_rng && G > 1) {
+        // sampler chain on a forked stream: RNG(j) overlaps update j-1; RNG(j+2)
+        // waits for update j (the last reader of its slot).
+        const Launch& R0 = h->plan[0][0];
+        const Launch& R1 = h->plan[1][0];
+        HIPCHK(h, hipEventRecord(evFork, cs));
+        HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
+        enqueue(R0, h, rs);
+        HIPCHK(h, hipEventRecord(evR[0], rs));
+        enqueue(R1, h, rs);
+        HIPCHK(h, hipEventRecord(evR[1], rs));
+        for (int j = 0; j < G; ++j) {
+            HIPCHK(h, hipStreamWaitEvent(cs, evR[j], 0));
+            enqueue_step(h, j & 1, false, cs);
+            HIPCHK(h, hipEventRecord(evS[j], cs));
+            if (j + 2 < G) {
+                HIPCHK(h, hipStreamWaitEvent(rs, evS[j], 0));
+                enqueue(h->plan[j & 1][0], h, rs);
+                HIPCHK(h, hipEventRecord(evR[j + 2], rs));
+            }
+        }
+    } else {
+        for (int j = 0; j < G; ++j) enqueue_step(h, 0, with_rng, cs);
+    }
+    hipGraph_t graph;
+    HIPCHK(h, hipStreamEndCapture(cs, &graph));
+    hipGraphExec_t exec;
+    HIPCHK(h, hipGraphInstantiateWithFlags(&exec, graph, 0));
+    HIPCHK(h, hipGraphDestroy(graph));
+    h->graphs[key] = exec;
+    *out = exec;
+    return 0;
+}
+
+}  // namespace
+
+// ============================================================================ C ABI
+extern "C" {
+
+int sacx_create(const sacx_config* cfg, sacx_handle** out) {
+    g_create_error.clear();
+    if (!cfg || !out) {
+        g_create_error = "null argument";
+        return -1;
+    }
+    auto bad = [&](const char* m) {
+        g_create_error = m;
+        return -2;
+    };
+    if (cfg->abi_version != SACX_ABI_VERSION) return bad("abi_version mismatch");
+    if (cfg->s_dim <= 0 || cfg->a_dim <= 0 || cfg->a_dim > 32) return bad("s_dim/a_dim out of range (a_dim <= 32)");
+    if (cfg->hidden[0] <= 0 || cfg->hidden[1] <= 0) return bad("hidden sizes must be positive");
+    if (cfg->activation < 0 || cfg->activation > 2) return bad("activation must be relu/tanh/elu");
+    if (cfg->batch <= 0 || cfg->buffer_capacity <= 0) return bad("batch/buffer_capacity must be positive");
+    if (cfg->buffer_capacity >= (int64_t(1) << 31)) return bad("buffer_capacity must be < 2^31");
+    if (cfg->use_expert) {
+        if (cfg->expert_batch <= 0 || (cfg->expert_batch & 1))
+            return bad("expert_batch must be positive and even (SAC_expert.py:329-332 adds equal halves)");
+        if (cfg->expert_capacity < cfg->expert_batch) return bad("expert_capacity < expert_batch");
+        if (cfg->model_hidden[0] <= 0 || cfg->model_hidden[1] <= 0) return bad("model sizes must be positive");
+        if (cfg->model_activation < 0 || cfg->model_activation > 2) return bad("model activation invalid");
+        if (cfg->s_dim + 1 > 512) return bad("s_dim > 511 unsupported by the model MSE head");
+    }
+    auto* h = new sacx_handle();
+    h->cfg = *cfg;
+    h->S = cfg->s_dim;
+    h->A = cfg->a_dim;
+    h->H0 = cfg->hidden[0];
+    h->H1 = cfg->hidden[1];
+    h->B = cfg->batch;
+    h->cap = cfg->buffer_capacity;
+    h->act = cfg->activation;
+    h->Aout = cfg->per_state_std ? 2 * h->A : h->A;
+    h->ne = cfg->use_expert ? cfg->expert_batch : 0;
+    h->ecap = cfg->use_expert ? cfg->expert_capacity : 0;
+    h->Hm0 = cfg->use_expert ? cfg->model_hidden[0] : 0;
+    h->Hm1 = cfg->use_expert ? cfg->model_hidden[1] : 0;
+    h->mact = cfg->model_activation;
+    h->ldS = (int)r4(h->S);
+    h->ldQ = (int)r4(h->S + h->A);
+    h->stride = (int)r4(2 * h->S + h->A + 2);
+    h->Ra = 2 * h->B + h->ne;
+    h->Rb = h->B + h->ne;
+    h->n_norm = (3 * h->B + h->ne) * h->A;
+    if (cfg->graph_steps > 0) h->graph_steps = cfg->graph_steps;
+    if (h->graph_steps > 64) h->graph_steps = 64;
+    if (h->graph_steps > 1 && (h->graph_steps & 1)) h->graph_steps += 1;
+    if (cfg->stats_capacity > 0) h->stats_cap = cfg->stats_capacity;
+    if (cfg->perm_capacity > 0) h->perm_cap = cfg->perm_capacity;
+    if (h->Aout > 64) {
+        delete h;
+        return bad("action output > 64 unsupported");
+    }
+    build_layout(h);
+    *out = h;
+    return 0;
+}
+
+void sacx_destroy(sacx_handle* h) {
+    if (!h) return;
+    for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto e : h->events) (void)hipEventDestroy(e);
+    if (h->d_probs) (void)hipFree(h->d_probs);
+    if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+    if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
+    delete h;
+}
+
+const char* sacx_last_error(const sacx_handle* h) {
+    if (!h) return g_create_error.c_str();
+    return h->err.c_str();
+}
+
+int64_t sacx_arena_bytes(const sacx_handle* h) { return h ? (int64_t)h->arena_bytes : -1; }
+
+int sacx_layout(const sacx_handle* h, sacx_segment* segs, int32_t cap, int32_t* n_out) {
+    if (!h || !n_out) return -1;
+    *n_out = (int32_t)h->segs.size();
+    if (!segs) return 0;
+    for (int i = 0; i < (int)h->segs.size() && i < cap; ++i) {
+        const SegInfo& s = h->segs[i];
+        std::memset(&segs[i], 0, sizeof(sacx_segment));
+        std::strncpy(segs[i].name, s.name.c_str(), sizeof(segs[i].name) - 1);
+        segs[i].offset = s.off;
+        segs[i].rows = s.rows;
+        segs[i].cols = s.cols;
+        segs[i].dtype = s.dtype;
+        segs[i].role = s.role;
+    }
+    return 0;
+}
+
+int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
+    if (!h) return -1;
+    if (!arena || bytes < h->arena_bytes) return fail(h, "arena missing or too small");
+    if (((uintptr_t)arena) & 255) return fail(h, "arena must be 256-byte aligned");
+    if (h->bound) return fail(h, "handle already bound");
+    h->arena = static_cast<char*>(arena);
+    h->stream = static_cast<hipStream_t>(stream);
+    h->probs.clear();
+    build_plan(h, 0, true);
+    build_plan(h, 1, false);
+    HIPCHK(h, hipMalloc(&h->d_probs, sizeof(GemmProb) * std::max<size_t>(1, h->probs.size())));
+    HIPCHK(h, hipMemcpy(h->d_probs, h->probs.data(), sizeof(GemmProb) * h->probs.size(), hipMemcpyHostToDevice));
+    HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
+    HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
+    h->bound = true;
+    return 0;
+}
+
+int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const float* r, const float* sp,
+                       const float* d, int64_t n) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n <= 0) return 0;
+    if (!s || !a || !r || !sp || !d) return fail(h, "null row pointer");
+    AppendArgs g{};
+    g.replay = h->f("replay"); g.cap = h->cap; g.stride = h->stride; g.S = h->S; g.A = h->A;
+    g.s = s; g.a = a; g.r = r; g.sp = sp; g.d = d; g.n = n; g.ctl = h->ctl();
+    launch_append(g, h->stream);
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int sacx_expert_set(sacx_handle* h, const float* s_e, const float* sp_e, int32_t n, float epsilon) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert");
+    if (n != h->ne) return fail(h, "expert rows must equal expert_batch");
+    const size_t bytes = sizeof(float) * (size_t)n * h->S;
+    HIPCHK(h, hipMemcpyAsync(h->f("expert.s"), s_e, bytes, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->f("expert.sp"), sp_e, bytes, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    Ctl* c = h->ctl();
+    const int64_t nn = n;
+    HIPCHK(h, hipMemcpy(&c->n_expert, &nn, sizeof(nn), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(&c->epsilon, &epsilon, sizeof(float), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int sacx_perm_push(sacx_handle* h, const int32_t* perms, int64_t n_steps) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return 0;
+    if (n_steps > h->perm_cap) return fail(h, "n_steps exceeds perm_capacity");
+    int32_t* ring = h->ptr<int32_t>("perm");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    for (int64_t j = 0; j < n_steps; ++j) {
+        const int64_t slot = (h->seq_host + j) % h->perm_cap;
+        HIPCHK(h, hipMemcpy(ring + slot * h->ne, perms + j * h->ne, sizeof(int32_t) * h->ne, hipMemcpyHostToDevice));
+    }
+    return 0;
+}
+
+int sacx_rng_seed(sacx_handle* h, uint32_t seed) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    RngState st{};
+    for (int pos = 0; pos < 624; ++pos) {       // init_genrand (seeding.py:12 -> np.random.seed)
+        st.key[pos] = seed;
+        seed = 1812433253U * (seed ^ (seed >> 30)) + (uint32_t)pos + 1U;
+    }
+    st.pos = 624;
+    st.has_gauss = 0;
+    st.gauss = 0.0;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(h->ptr<RngState>("rng"), &st, sizeof(st), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int sacx_rng_set_state(sacx_handle* h, const uint32_t key[624], int32_t pos, int32_t has_gauss, double gauss) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (pos < 0 || pos > 624) return fail(h, "pos out of range");
+    RngState st{};
+    std::memcpy(st.key, key, sizeof(st.key));
+    st.pos = pos;
+    st.has_gauss = has_gauss;
+    st.gauss = gauss;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(h->ptr<RngState>("rng"), &st, sizeof(st), hipMemcpyHostToDevice));
+    return 0;
+}
+
+int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t* has_gauss, double* gauss) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    RngState st{};
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(&st, h->ptr<RngState>("rng"), sizeof(st), hipMemcpyDeviceToHost));
+    std::memcpy(key, st.key, sizeof(st.key));
+    *pos = st.pos;
+    *has_gauss = st.has_gauss;
+    *gauss = st.gauss;
+    return 0;
+}
+
+int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment, int32_t flags) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n_steps <= 0) return 0;
+    launch_set_ctl(h->ctl(), num_timesteps, ts_increment, h->stream);
+    const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
+    if (flags & SACX_STEP_EAGER) {
+        for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
+        HIPCHK(h, hipGetLastError());
+    } else {
+        const int G = ext ? 1 : h->graph_steps;
+        int64_t q = n_steps / G, r = n_steps % G;
+        if (q > 0) {
+            hipGraphExec_t g;
+            if (get_graph(h, G, !ext, &g)) return -1;
+            for (int64_t i = 0; i < q; ++i) HIPCHK(h, hipGraphLaunch(g, h->stream));
+        }
+        if (r > 0) {
+            hipGraphExec_t g1;
+            if (get_graph(h, 1, !ext, &g1)) return -1;
+            for (int64_t i = 0; i < r; ++i) HIPCHK(h, hipGraphLaunch(g1, h->stream));
+        }
+    }
+    h->seq_host += n_steps;
+    return 0;
+}
+
+int sacx_sync(sacx_handle* h) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out) {
+    if (!h || !n_out) return -1;
+    if (!h->bound) {
+        *n_out = 0;
+        return -1;
+    }
+    const auto& plan = h->plan[0];
+    *n_out = (int32_t)plan.size();
+    if (!out) return 0;
+    for (int i = 0; i < (int)plan.size() && i < cap; ++i) {
+        std::memset(&out[i], 0, sizeof(sacx_launch_info));
+        std::strncpy(out[i].name, plan[i].name.c_str(), sizeof(out[i].name) - 1);
+        std::strncpy(out[i].kernel, kernel_family(plan[i].kind), sizeof(out[i].kernel) - 1);
+        out[i].grid = plan[i].grid;
+        out[i].block = plan[i].block;
+        out[i].flops = plan[i].flops;
+        out[i].bytes = plan[i].bytes;
+    }
+    return 0;
+}
+
+int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t cap) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    const auto& plan = h->plan[0];
+    const int n = (int)plan.size();
+    std::vector<hipEvent_t> ev(n + 1);
+    for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
+    std::vector<double> acc(n, 0.0);
+    for (int64_t s = 0; s < n_steps; ++s) {
+        HIPCHK(h, hipEventRecord(ev[0], h->stream));
+        for (int i = 0; i < n; ++i) {
+            enqueue(plan[i], h, h->stream);
+            HIPCHK(h, hipEventRecord(ev[i + 1], h->stream));
+        }
+        HIPCHK(h, hipEventSynchronize(ev[n]));
+        for (int i = 0; i < n; ++i) {
+            float ms = 0.f;
+            HIPCHK(h, hipEventElapsedTime(&ms, ev[i], ev[i + 1]));
+            acc[i] += ms;
+        }
+    }
+    for (auto& e : ev) (void)hipEventDestroy(e);
+    h->seq_host += n_steps;
+    for (int i = 0; i < n && i < cap; ++i) ms_per_launch[i] = acc[i];
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,208 @@
+// Internal structures shared by the host plan builder (sacx.cpp) and the
+// gfx950 kernels (k_*.hip).  Not part of the public ABI.
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace sacx {
+
+enum Act { ACT_RELU = 0, ACT_TANH = 1, ACT_ELU = 2, ACT_NONE = 3 };
+
+// Device control block (lives in the arena, segment "ctl", int64 x 32).
+struct Ctl {
+    int64_t t_sac;          // completed updates (Adam iterations of q / pi / alpha optimisers)
+    int64_t t_model;        // model optimiser iterations
+    int64_t num_timesteps;  // SAC_expert.py:475 gating of the Polyak sync
+    int64_t ts_increment;
+    int64_t cur_size;       // TrajectoryBuffer.current_size
+    int64_t start;          // physical ring index of logical row 0
+    int64_t step_seq;       // update sequence number (stats / perm ring index)
+    int64_t n_expert;       // expert rows currently set
+    int32_t red_counter[8]; // last-arriver tickets (self-resetting)
+    float epsilon;          // expert weight
+    float pad_f[3];
+    int64_t reserved[14];
+};
+static_assert(sizeof(Ctl) <= 32 * 8, "ctl segment is 32 int64");
+
+struct RngState {          // NumPy legacy RandomState (MT19937) state
+    uint32_t key[624];
+    int32_t pos;
+    int32_t has_gauss;
+    double gauss;
+};
+
+// Adam constants for the optimiser groups.
+enum { GRP_Q = 0, GRP_PI = 1, GRP_ALPHA = 2, GRP_MODEL = 3 };
+struct AdamConsts {
+    float lr[4];
+    float tau_keep;   // f32(1 - tau)
+    float tau_take;   // f32(tau)
+    int32_t target_update_int;
+    int32_t pad;
+};
+
+// ---------------------------------------------------------------- grouped GEMM
+// C[M,N] = A[M,K] * B[K,N] on 16x16 output tiles, fp32 MFMA (v_mfma_f32_16x16x4_f32),
+// K split over the 4 waves of a 256-thread workgroup and reduced through LDS.
+enum Epi { EPI_FWD = 0, EPI_DACT = 1, EPI_ADAM = 2, EPI_STORE = 3 };
+
+struct GemmProb {
+    const float* A;        // a_kc: A[m*lda + k]   else A[k*lda + m] (row ones_row = 1.0)
+    const float* B;        // b_kc: B[n*ldb + k]   else B[k*ldb + n]
+    float* C;
+    const float* bias;     // EPI_FWD
+    const float* H;        // EPI_DACT: activation output whose derivative multiplies
+    float* P;              // EPI_ADAM: parameter tile base (m/v at +P_stride, +2*P_stride floats)
+    float* T;              // EPI_ADAM: Polyak target (nullable)
+    int32_t lda, ldb, ldc, ldh, ldp;
+    int32_t M, N, K;
+    int32_t a_kc, b_kc, ones_row;
+    int32_t epi, act, group;
+    int32_t tiles_n, tile_begin;
+    float grad_scale;
+    int32_t pad;
+};
+
+struct GemmArgs {
+    const GemmProb* probs;
+    int32_t nprob;
+    int32_t total_tiles;
+    int64_t p_stride;      // floats between params / adam_m / adam_v blocks
+    const Ctl* ctl;
+    AdamConsts adam;
+};
+
+// ---------------------------------------------------------------- sampler + gather
+struct RngArgs {
+    RngState* st;
+    const Ctl* ctl;        // reads cur_size at run time
+    int32_t n_int;
+    int32_t n_norm;
+    int32_t* out_idx;
+    float* out_norm;
+};
+
+struct GatherArgs {
+    const float* replay;   // [cap, stride]
+    int64_t cap;
+    int32_t stride;
+    int32_t S, A, B, ne;
+    const int32_t* idx;
+    const Ctl* ctl;
+    const float *s_mean, *s_den, *a_mean, *a_den;
+    float* Xa;  int32_t ldS;   // actor rows [sp(B) ; s(B) ; s_e(ne)]
+    float* Xq;  float* Xt; float* Xp; float* Xm; int32_t ldQ;
+    float* r; float* d;
+    const float* exp_s; const float* exp_sp; const int32_t* perm_ring; int32_t perm_cap;
+    float* se_raw; float* spe_raw;
+};
+
+// ---------------------------------------------------------------- actor head rows
+struct HeadSeg {
+    int32_t r0, r1;        // actor rows [r0, r1)
+    int32_t mode;          // 0 = evaluate (neglogp), 1 = sample (no neglogp)
+    int32_t xq_row0;       // first row in xq_out
+    const float* noise;    // [r1-r0, A]
+    float* xq_out;         // normalised action -> xq_out[(xq_row0 + i) * ldQ + S + j]
+    float* nlp_out;        // [r1-r0] (evaluate)
+};
+
+struct HeadArgs {
+    const float* H2; int32_t ldh;
+    const float* W3;       // W3_ext [(H1+1), Aout]
+    const float* logstd;   // [A] global logstd (per_state_std == 0)
+    int32_t H1, A, Aout, S, ldQ, per_state_std;
+    float lim;
+    const float *a_mean, *a_den;
+    int32_t nseg;
+    HeadSeg seg[3];
+    int32_t total_rows;
+    // backward cache (rows >= cache_row0 are cached at [row - cache_row0])
+    int32_t cache_row0;
+    float* c_t; float* c_std; float* c_u; float* c_mask;
+    // alpha mode: reduce sum(-nlp + target_entropy) and finalise the update
+    int32_t alpha_mode;
+};
+
+// ---------------------------------------------------------------- Q heads
+struct QHeadArgs {
+    // target/critic mode (mode 0): nets t0,t1 on H2 slabs [0],[1]; q0,q1 on slabs [2],[3]
+    // actor-loss mode (mode 1): q0,q1 on slabs [0],[1]
+    int32_t mode;
+    int32_t B, H1;
+    const float* H2;        // [nslab, B, H1]
+    const float* W3[4];     // W3_ext of the nets, [(H1+1) x 1]
+    int32_t act;
+    float* D2;              // [2, B, H1] delta at the layer-2 output of the trained / differentiated nets
+    float* g;               // [2, B]     delta at the output (mode 0)
+    float* loss_rows;       // mode 0: [2, B] 0.5 e^2 ; mode 1: [B] -alpha*nlp - minQ
+    const float* alpha;
+    const float* nlp;       // mode 0: nlp of the target actions; mode 1: nlp of the policy actions
+    const float* r; const float* d;
+    float gamma, ret_den_unused;
+    const float* ret_den;
+    float w_sac;            // (1 - epsilon) for SAC-EO, 1 for SAC
+    // SAC-EO model rows (mode 0 only): rows [B, B+ne) handle the expert MSE
+    int32_t ne, Hm1, S;
+    const float* Hm2;       // [ne, Hm1]
+    const float* Wm3[2];    // [(Hm1+1), S+1]
+    int32_t mact;
+    const float* se_raw; const float* spe_raw;
+    const float *d_mean, *d_den;
+    const Ctl* ctl;         // epsilon
+    float* Dm2;             // [ne, Hm1]
+    float* mse_rows;        // [ne]
+};
+
+// ---------------------------------------------------------------- actor backward head
+struct ActorBwdArgs {
+    int32_t B, ne, S, A, Aout, H0, H1, Hm0, per_state_std;
+    float lim;
+    const float* Dp1;       // [2, B, H0]
+    const float* Wq1[2];    // W1_ext of q0, q1 [(S+A+1), H0]
+    const float* Dm1;       // [ne, Hm0]
+    const float* Wm1[2];    // W1_ext of the models [(S+A+1), Hm0]
+    const float *a_den;
+    const float* alpha;
+    const Ctl* ctl;         // epsilon
+    int32_t use_expert;
+    const float *c_t, *c_std, *c_u, *c_mask;   // cache rows [0, B+ne)
+    const float* W3a;       // [(H1+1), Aout]
+    const float* Ha2;       // actor layer-2 outputs of rows [B, ...) ; row i at Ha2[i*H1]
+    int32_t act;
+    float* Da3; float* Da2; float* E;
+};
+
+// ---------------------------------------------------------------- finalize (alpha + stats)
+struct FinalArgs {
+    float* alpha; float* alpha_m; float* alpha_v;
+    Ctl* ctl;
+    AdamConsts adam;
+    float target_entropy;
+    int32_t B, ne, use_expert;
+    const float* lq;        // [2, B]
+    const float* lp;        // [B]
+    const float* mse_rows;  // [ne]
+    float* red;             // partial slots
+    float* stats; int32_t stats_cap;
+};
+
+struct AppendArgs {
+    float* replay; int64_t cap; int32_t stride; int32_t S, A;
+    const float *s, *a, *r, *sp, *d;
+    int64_t n;
+    Ctl* ctl;
+};
+
+// launchers (defined in k_sac.hip)
+void launch_gemm(const GemmArgs& a, hipStream_t s);
+void launch_rng(const RngArgs& a, hipStream_t s);
+void launch_gather(const GatherArgs& a, hipStream_t s);
+void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s);
+void launch_qhead(const QHeadArgs& a, hipStream_t s);
+void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s);
+void launch_append(const AppendArgs& a, hipStream_t s);
+void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s);
+
+}  // namespace sacx

@@ -1,0 +1,133 @@
+"""ctypes binding of libsacx (include/sacx.h).
+
+This is the product path's only way to the GPU: there is no CPU fallback.  If
+the shared library is missing the import raises, loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
+
+SACX_ABI_VERSION = 1
+ACT = {"relu": 0, "tanh": 1, "elu": 2}
+DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
+STEP_EXTERNAL_RANDOMS = 1
+STEP_EAGER = 2
+STAT_NAMES = ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss", "nlp_mean", "step"]
+
+# every symbol include/sacx.h declares (checked by tests/test_abi.py)
+EXPORTS = [
+    "sacx_create", "sacx_destroy", "sacx_last_error", "sacx_arena_bytes", "sacx_layout", "sacx_bind",
+    "sacx_buffer_append", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
+    "sacx_rng_get_state", "sacx_sac_step", "sacx_sync", "sacx_plan_info", "sacx_profile",
+]
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("s_dim", ctypes.c_int32),
+        ("a_dim", ctypes.c_int32),
+        ("hidden", ctypes.c_int32 * 2),
+        ("activation", ctypes.c_int32),
+        ("batch", ctypes.c_int32),
+        ("buffer_capacity", ctypes.c_int64),
+        ("per_state_std", ctypes.c_int32),
+        ("use_expert", ctypes.c_int32),
+        ("expert_capacity", ctypes.c_int32),
+        ("expert_batch", ctypes.c_int32),
+        ("model_hidden", ctypes.c_int32 * 2),
+        ("model_activation", ctypes.c_int32),
+        ("model_batch", ctypes.c_int32),
+        ("target_update_int", ctypes.c_int32),
+        ("graph_steps", ctypes.c_int32),
+        ("stats_capacity", ctypes.c_int32),
+        ("perm_capacity", ctypes.c_int32),
+        ("gamma", ctypes.c_float),
+        ("tau", ctypes.c_float),
+        ("lr_q", ctypes.c_float),
+        ("lr_pi", ctypes.c_float),
+        ("lr_alpha", ctypes.c_float),
+        ("lr_model", ctypes.c_float),
+        ("init_temperature", ctypes.c_float),
+        ("target_entropy", ctypes.c_float),
+        ("act_limit", ctypes.c_float),
+        ("epsilon", ctypes.c_float),
+        ("reward_loss_coef", ctypes.c_float),
+    ]
+
+
+class Segment(ctypes.Structure):
+    _fields_ = [
+        ("name", ctypes.c_char * 48),
+        ("offset", ctypes.c_uint64),
+        ("rows", ctypes.c_int64),
+        ("cols", ctypes.c_int64),
+        ("dtype", ctypes.c_int32),
+        ("role", ctypes.c_int32),
+    ]
+
+
+class LaunchInfo(ctypes.Structure):
+    _fields_ = [
+        ("name", ctypes.c_char * 32),
+        ("kernel", ctypes.c_char * 32),
+        ("grid", ctypes.c_int32),
+        ("block", ctypes.c_int32),
+        ("flops", ctypes.c_double),
+        ("bytes", ctypes.c_double),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    """Loads libsacx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libsacx.so not found at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(the HIP engine is required; there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u32, f32, f64 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                                   ctypes.c_float, ctypes.c_double)
+    P = ctypes.POINTER
+    sig = {
+        "sacx_create": (ctypes.c_int, [P(Config), P(vp)]),
+        "sacx_destroy": (None, [vp]),
+        "sacx_last_error": (ctypes.c_char_p, [vp]),
+        "sacx_arena_bytes": (i64, [vp]),
+        "sacx_layout": (ctypes.c_int, [vp, P(Segment), i32, P(i32)]),
+        "sacx_bind": (ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
+        "sacx_buffer_append": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64]),
+        "sacx_expert_set": (ctypes.c_int, [vp, vp, vp, i32, f32]),
+        "sacx_perm_push": (ctypes.c_int, [vp, vp, i64]),
+        "sacx_rng_seed": (ctypes.c_int, [vp, u32]),
+        "sacx_rng_set_state": (ctypes.c_int, [vp, vp, i32, i32, f64]),
+        "sacx_rng_get_state": (ctypes.c_int, [vp, vp, P(i32), P(i32), P(f64)]),
+        "sacx_sac_step": (ctypes.c_int, [vp, i64, i64, i32, i32]),
+        "sacx_sync": (ctypes.c_int, [vp]),
+        "sacx_plan_info": (ctypes.c_int, [vp, P(LaunchInfo), i32, P(i32)]),
+        "sacx_profile": (ctypes.c_int, [vp, i64, P(f64), i32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = L
+    return L
+
+
+class SacxError(RuntimeError):
+    pass
+
+
+def check(rc: int, handle=None, what: str = "") -> None:
+    if rc != 0:
+        msg = lib().sacx_last_error(handle)
+        raise SacxError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,277 @@
+"""Device engine: one libsacx handle + its HBM arena, viewed as torch tensors.
+
+PyTorch-ROCm is plumbing here: it allocates the arena, supplies the HIP
+stream and gives named views for setting weights / reading results.  All
+update arithmetic runs in the hand-written gfx950 kernels behind the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+import math
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+_TORCH_DT = {0: torch.float32, 1: torch.int32, 2: torch.int64, 3: torch.int32, 4: torch.float64}
+_ESZ = {0: 4, 1: 4, 2: 8, 3: 4, 4: 8}
+
+# ctl field indices (int64 slots, see csrc/sacx_internal.h struct Ctl)
+CTL = {"t_sac": 0, "t_model": 1, "num_timesteps": 2, "ts_increment": 3, "cur_size": 4, "start": 5,
+       "step_seq": 6, "n_expert": 7}
+
+
+@dataclasses.dataclass
+class EngineConfig:
+    s_dim: int
+    a_dim: int
+    hidden: Sequence[int] = (256, 256)
+    activation: str = "relu"
+    batch: int = 256
+    buffer_capacity: int = 1_000_000
+    per_state_std: bool = False
+    use_expert: bool = False
+    expert_capacity: int = 20
+    expert_batch: int = 20
+    model_hidden: Sequence[int] = (512, 512)
+    model_activation: str = "relu"
+    model_batch: int = 200
+    target_update_int: int = 1
+    graph_steps: int = 8
+    stats_capacity: int = 4096
+    perm_capacity: int = 4096
+    gamma: float = 0.995
+    tau: float = 5e-3
+    lr_q: float = 3e-4
+    lr_pi: float = 1e-4
+    lr_alpha: float = 1e-4
+    lr_model: float = 1e-3
+    init_temperature: float = 0.1
+    target_entropy: Optional[float] = None
+    act_limit: float = 1.0
+    epsilon: float = 1e-3
+    reward_loss_coef: float = 1.0
+
+    def to_c(self) -> N.Config:
+        c = N.Config()
+        c.abi_version = N.SACX_ABI_VERSION
+        c.s_dim, c.a_dim = int(self.s_dim), int(self.a_dim)
+        c.hidden[0], c.hidden[1] = int(self.hidden[0]), int(self.hidden[1])
+        c.activation = N.ACT[self.activation]
+        c.batch = int(self.batch)
+        c.buffer_capacity = int(self.buffer_capacity)
+        c.per_state_std = int(bool(self.per_state_std))
+        c.use_expert = int(bool(self.use_expert))
+        c.expert_capacity = int(self.expert_capacity)
+        c.expert_batch = int(self.expert_batch)
+        c.model_hidden[0], c.model_hidden[1] = int(self.model_hidden[0]), int(self.model_hidden[1])
+        c.model_activation = N.ACT[self.model_activation]
+        c.model_batch = int(self.model_batch)
+        c.target_update_int = int(self.target_update_int)
+        c.graph_steps = int(self.graph_steps)
+        c.stats_capacity = int(self.stats_capacity)
+        c.perm_capacity = int(self.perm_capacity)
+        c.gamma, c.tau = self.gamma, self.tau
+        c.lr_q, c.lr_pi, c.lr_alpha, c.lr_model = self.lr_q, self.lr_pi, self.lr_alpha, self.lr_model
+        c.init_temperature = self.init_temperature
+        c.target_entropy = float(-self.a_dim if self.target_entropy is None else self.target_entropy)
+        c.act_limit = self.act_limit
+        c.epsilon = self.epsilon
+        c.reward_loss_coef = self.reward_loss_coef
+        return c
+
+
+class Engine:
+    """One SAC / SAC-EO learner on one GPU (one handle, one arena)."""
+
+    NETS = ("actor", "q0", "q1", "t0", "t1", "m0", "m1")
+
+    def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None, stream=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("sac_eo.engine needs a ROCm GPU (no CPU fallback)")
+        self.cfg = cfg
+        self.lib = N.lib()
+        self.device = torch.device(device or "cuda")
+        h = ctypes.c_void_p()
+        c = cfg.to_c()
+        N.check(self.lib.sacx_create(ctypes.byref(c), ctypes.byref(h)), None, "sacx_create")
+        self.h = h
+        nbytes = int(self.lib.sacx_arena_bytes(h))
+        self._raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
+        off = (-self._raw.data_ptr()) % 256
+        self.arena = self._raw[off: off + nbytes]
+        self.nbytes = nbytes
+        n = ctypes.c_int32()
+        self.lib.sacx_layout(h, None, 0, ctypes.byref(n))
+        segs = (N.Segment * n.value)()
+        self.lib.sacx_layout(h, segs, n.value, ctypes.byref(n))
+        self.segments: Dict[str, dict] = {}
+        self.v: Dict[str, torch.Tensor] = {}
+        for s in segs:
+            name = s.name.decode()
+            nb = int(s.rows * s.cols * _ESZ[s.dtype])
+            t = self.arena[s.offset: s.offset + nb].view(_TORCH_DT[s.dtype]).view(int(s.rows), int(s.cols))
+            self.segments[name] = dict(offset=int(s.offset), rows=int(s.rows), cols=int(s.cols),
+                                       dtype=N.DTYPES[s.dtype], role=int(s.role))
+            self.v[name] = t
+        with torch.cuda.device(self.device):
+            self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        N.check(self.lib.sacx_bind(h, ctypes.c_void_p(self.arena.data_ptr()), nbytes,
+                                   ctypes.c_void_p(self.stream.cuda_stream)), h, "sacx_bind")
+        self._init_state()
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if getattr(self, "h", None) is not None:
+            self.sync()
+            self.lib.sacx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _init_state(self):
+        cfg = self.cfg
+        v = self.v
+        for k in ("norm.s_den", "norm.a_den", "norm.d_den", "norm.ret_den"):
+            v[k].fill_(1.0)
+        v["norm.r"][0, 1] = 1.0
+        v["alpha"].fill_(float(np.float32(np.log(cfg.init_temperature))))   # SAC_expert.py:106
+        self.rng_seed(0)
+
+    # ------------------------------------------------------------------ weights
+    def _layers(self, net: str) -> List[torch.Tensor]:
+        return [self.v[f"{net}.l{i}"] for i in range(3)]
+
+    def set_net(self, net: str, weights: Sequence[np.ndarray]):
+        """Keras get_weights() list [W0, b0, W1, b1, W2, b2] -> W_ext views."""
+        for i, t in enumerate(self._layers(net)):
+            W = torch.as_tensor(np.asarray(weights[2 * i], np.float32))
+            b = torch.as_tensor(np.asarray(weights[2 * i + 1], np.float32)).reshape(1, -1)
+            if tuple(W.shape) != (t.shape[0] - 1, t.shape[1]):
+                raise ValueError(f"{net}.l{i}: expected {(t.shape[0] - 1, t.shape[1])}, got {tuple(W.shape)}")
+            t.copy_(torch.cat([W, b], 0).to(self.device))
+
+    def get_net(self, net: str) -> List[np.ndarray]:
+        out = []
+        for t in self._layers(net):
+            a = t.detach().cpu().numpy()
+            out += [a[:-1].copy(), a[-1].copy()]
+        return out
+
+    def set_logstd(self, logstd):
+        self.v["actor.logstd"].copy_(torch.as_tensor(np.asarray(logstd, np.float32).reshape(1, -1)))
+
+    def set_alpha(self, alpha: float):
+        self.v["alpha"].fill_(float(np.float32(alpha)))
+
+    def alpha(self) -> float:
+        return float(self.v["alpha"].item())
+
+    def set_normalizers(self, s_mean, s_den, a_mean, a_den, d_mean=None, d_den=None,
+                        r_mean=0.0, r_den=1.0, ret_den=1.0):
+        """Values of RunningNormalizer.normalize: mean and max(std, 1e-8) (normalizer.py:26-41)."""
+        v = self.v
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        put = lambda k, x, n: v[k].copy_(torch.as_tensor(np.asarray(x, np.float32).reshape(1, n)))
+        put("norm.s_mean", s_mean, S)
+        put("norm.s_den", s_den, S)
+        put("norm.a_mean", a_mean, A)
+        put("norm.a_den", a_den, A)
+        put("norm.d_mean", np.zeros(S) if d_mean is None else d_mean, S)
+        put("norm.d_den", np.ones(S) if d_den is None else d_den, S)
+        v["norm.r"].copy_(torch.tensor([[np.float32(r_mean), np.float32(r_den)]]))
+        v["norm.ret_den"].fill_(float(np.float32(ret_den)))
+
+    def reset_optimizers(self):
+        self.v["adam_m"].zero_()
+        self.v["adam_v"].zero_()
+        self.v["ctl"][0, CTL["t_sac"]] = 0
+
+    # ------------------------------------------------------------------ RNG (global NumPy stream)
+    def rng_seed(self, seed: int):
+        N.check(self.lib.sacx_rng_seed(self.h, ctypes.c_uint32(int(seed) & 0xFFFFFFFF)), self.h, "rng_seed")
+
+    def rng_set_state(self, state):
+        """Accepts np.random.get_state() / RandomState.get_state()."""
+        _, key, pos, has_gauss, gauss = state[:5]
+        key = np.ascontiguousarray(key, dtype=np.uint32)
+        N.check(self.lib.sacx_rng_set_state(self.h, key.ctypes.data, int(pos), int(has_gauss), float(gauss)),
+                self.h, "rng_set_state")
+
+    def rng_get_state(self):
+        key = np.zeros(624, np.uint32)
+        pos, hg, g = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_double()
+        N.check(self.lib.sacx_rng_get_state(self.h, key.ctypes.data, ctypes.byref(pos), ctypes.byref(hg),
+                                            ctypes.byref(g)), self.h, "rng_get_state")
+        return ("MT19937", key, pos.value, hg.value, g.value)
+
+    # ------------------------------------------------------------------ data
+    def _dev(self, x, shape) -> torch.Tensor:
+        t = torch.as_tensor(x, dtype=torch.float32, device=self.device).reshape(shape).contiguous()
+        return t
+
+    def append(self, s, a, r, sp, d):
+        """TrajectoryBuffer.add (buffers.py:41-71) into the device ring."""
+        n = int(np.shape(r)[0]) if not torch.is_tensor(r) else int(r.shape[0])
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        ts = [self._dev(s, (n, S)), self._dev(a, (n, A)), self._dev(r, (n,)), self._dev(sp, (n, S)),
+              self._dev(d, (n,))]
+        N.check(self.lib.sacx_buffer_append(self.h, *[ctypes.c_void_p(t.data_ptr()) for t in ts], n),
+                self.h, "buffer_append")
+        self._keep = ts   # keep sources alive until the stream consumes them
+        return n
+
+    def set_expert(self, s_e, sp_e, epsilon: float):
+        n = int(np.shape(s_e)[0])
+        S = self.cfg.s_dim
+        a, b = self._dev(s_e, (n, S)), self._dev(sp_e, (n, S))
+        N.check(self.lib.sacx_expert_set(self.h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()),
+                                         n, float(epsilon)), self.h, "expert_set")
+
+    def push_perms(self, perms: np.ndarray):
+        perms = np.ascontiguousarray(perms, dtype=np.int32)
+        N.check(self.lib.sacx_perm_push(self.h, perms.ctypes.data, int(perms.shape[0])), self.h, "perm_push")
+
+    # ------------------------------------------------------------------ hot path
+    def step(self, n: int = 1, num_timesteps: int = 0, ts_increment: int = 1, external: bool = False,
+             eager: bool = False):
+        flags = (N.STEP_EXTERNAL_RANDOMS if external else 0) | (N.STEP_EAGER if eager else 0)
+        N.check(self.lib.sacx_sac_step(self.h, int(n), int(num_timesteps), int(ts_increment), flags),
+                self.h, "sac_step")
+
+    def sync(self):
+        N.check(self.lib.sacx_sync(self.h), self.h, "sync")
+
+    def ctl(self) -> Dict[str, int]:
+        c = self.v["ctl"][0].cpu().numpy()
+        return {k: int(c[i]) for k, i in CTL.items()}
+
+    def stats(self, n_last: int) -> np.ndarray:
+        """Last n_last rows of the per-update statistics ring, oldest first."""
+        seq = self.ctl()["step_seq"]
+        cap = self.cfg.stats_capacity
+        st = self.v["stats"].cpu().numpy()
+        idx = [(seq - n_last + i) % cap for i in range(n_last)]
+        return st[idx]
+
+    # ------------------------------------------------------------------ measurement
+    def plan_info(self) -> List[dict]:
+        n = ctypes.c_int32()
+        self.lib.sacx_plan_info(self.h, None, 0, ctypes.byref(n))
+        arr = (N.LaunchInfo * n.value)()
+        N.check(self.lib.sacx_plan_info(self.h, arr, n.value, ctypes.byref(n)), self.h, "plan_info")
+        return [dict(name=a.name.decode(), kernel=a.kernel.decode(), grid=a.grid, block=a.block,
+                     flops=a.flops, bytes=a.bytes) for a in arr]
+
+    def profile(self, n_steps: int) -> np.ndarray:
+        k = len(self.plan_info())
+        out = (ctypes.c_double * k)()
+        N.check(self.lib.sacx_profile(self.h, int(n_steps), out, k), self.h, "profile")
+        return np.array(list(out)) / n_steps

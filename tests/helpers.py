@@ -1,0 +1,83 @@
+"""Shared setup for the parity tests: one oracle state (tests' checker) and
+the same state loaded into the device engine (the product)."""
+from __future__ import annotations
+
+import numpy as np
+
+import sac_oracle as O
+
+B1 = np.float32(1.0) - np.float32(0.9)   # Keras (1 - beta_1) in fp32: m_1 = g * B1
+
+
+def synthetic_buffer(rs: np.random.RandomState, N: int, S: int, A: int, done_p: float = 0.0):
+    """SURVEY.md §8(d) synthetic data: per-dim scales U(0.1, 5), a ~ U(-1, 1)."""
+    sig = rs.uniform(0.1, 5.0, size=S)
+    buf = dict(s=(rs.normal(size=(N, S)) * sig).astype(np.float32),
+               a=rs.uniform(-1, 1, size=(N, A)).astype(np.float32),
+               sp=(rs.normal(size=(N, S)) * sig).astype(np.float32),
+               r=rs.normal(size=N).astype(np.float32),
+               d=(rs.uniform(size=N) < done_p).astype(np.float64))
+    return buf
+
+
+def nontrivial_normalizers(rs, S, A):
+    return O.Normalizers(
+        (rs.normal(size=S) * 0.2).astype(np.float32), rs.uniform(0.5, 3.0, S).astype(np.float32),
+        (rs.normal(size=A) * 0.05).astype(np.float32), rs.uniform(0.8, 1.2, A).astype(np.float32),
+        (rs.normal(size=S) * 0.1).astype(np.float32), rs.uniform(0.5, 2.0, S).astype(np.float32),
+        0.0, 1.0, 1.0)
+
+
+def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
+              use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
+              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1):
+    """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
+    from sac_eo.engine import Engine, EngineConfig
+    ocfg = O.Config(S=S, A=A, hidden=hidden, act=act, B=B, per_state_std=per_state_std,
+                    model_hidden=model_hidden, epsilon=epsilon)
+    st = O.init_state(ocfg, seed=seed + 1, with_models=use_expert, bias_scale=bias_scale,
+                      actor_gain=actor_gain, model_gain=0.3)
+    rs = np.random.RandomState(seed + 100)
+    buf = synthetic_buffer(rs, N, S, A, done_p)
+    nrm = O.Normalizers.identity(S, A) if normalizers == "identity" else nontrivial_normalizers(rs, S, A)
+    ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
+                        per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
+                        expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon)
+    eng = Engine(ecfg)
+    eng.set_net("actor", st.actor)
+    eng.set_logstd(st.logstd)
+    for k in range(2):
+        eng.set_net(f"q{k}", st.q[k])
+        eng.set_net(f"t{k}", st.q_targ[k])
+    if use_expert:
+        for k in range(2):
+            eng.set_net(f"m{k}", st.models[k])
+    eng.set_alpha(float(st.alpha))
+    eng.set_normalizers(nrm.s_mean, nrm.s_den, nrm.a_mean, nrm.a_den, nrm.d_mean, nrm.d_den,
+                        nrm.r_mean, nrm.r_den, nrm.ret_den)
+    eng.append(buf["s"], buf["a"], buf["r"], buf["sp"], buf["d"].astype(np.float32))
+    expert = None
+    if use_expert:
+        ers = np.random.RandomState(seed + 200)
+        sig = ers.uniform(0.1, 5.0, size=S)
+        expert = dict(s=(ers.normal(size=(ne, S)) * sig).astype(np.float32),
+                      sp=(ers.normal(size=(ne, S)) * sig).astype(np.float32))
+        eng.set_expert(expert["s"], expert["sp"], epsilon)
+    return eng, ocfg, st.astype(np.float64), buf, nrm, expert
+
+
+def oracle_step(st, ocfg, nrm, buf, R, expert=None, keep=None):
+    """One oracle update with the randoms R drawn in the reference order."""
+    n = [O.f32_noise(R[k]) for k in ("noise_t", "noise_pi", "noise_alpha")]
+    ex = None
+    if expert is not None:
+        sec = R["sections"]
+        ex = O.Expert(expert["s"][sec[0]], expert["sp"][sec[0]], expert["s"][sec[1]], expert["sp"][sec[1]],
+                      O.f32_noise(R["noise_e1"]), O.f32_noise(R["noise_e2"]), ocfg.epsilon)
+    return O.sac_update(st, ocfg, nrm, O.gather(buf, R["idx"]), *n, expert=ex, keep=keep)
+
+
+def relerr(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b)) / max(np.max(np.abs(b)), 1e-30))

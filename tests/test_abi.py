@@ -1,0 +1,59 @@
+"""CPU-side checks of the drop-in boundary: libsacx.so loads and exports every
+symbol include/sacx.h declares; the ctypes structs match the C layout.  No
+compute calls (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_symbols():
+    txt = open(os.path.join(ROOT, "include", "sacx.h")).read()
+    return sorted(set(re.findall(r"\b(sacx_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_exports_header_symbols():
+    from sac_eo import _native as N
+    L = N.lib()
+    syms = _header_symbols()
+    assert len(syms) >= 16
+    for s in syms:
+        assert hasattr(L, s), s
+    assert sorted(N.EXPORTS) == syms
+
+
+def test_struct_layouts():
+    from sac_eo import _native as N
+    # offsets fixed by include/sacx.h (natural alignment)
+    assert N.Config.buffer_capacity.offset == 32
+    assert ctypes.sizeof(N.Config) == 136          # gcc: sizeof(sacx_config)
+    assert N.Config.reward_loss_coef.offset == 128
+    assert ctypes.sizeof(N.Segment) == 48 + 8 + 8 + 8 + 4 + 4
+    assert ctypes.sizeof(N.LaunchInfo) == 32 + 32 + 4 + 4 + 8 + 8
+
+
+def test_create_validates_without_gpu():
+    """sacx_create / layout are host-only; bad configs fail with a message."""
+    from sac_eo import _native as N
+    from sac_eo.engine import EngineConfig
+    L = N.lib()
+    h = ctypes.c_void_p()
+    c = EngineConfig(s_dim=17, a_dim=6).to_c()
+    assert L.sacx_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    n = ctypes.c_int32()
+    L.sacx_layout(h, None, 0, ctypes.byref(n))
+    segs = (N.Segment * n.value)()
+    L.sacx_layout(h, segs, n.value, ctypes.byref(n))
+    names = {s.name.decode(): s for s in segs}
+    for k in ("actor.l0", "q0.l2", "t1.l1", "alpha", "adam_m", "adam_v", "replay", "rng", "ctl"):
+        assert k in names
+    assert names["actor.l0"].rows == 18 and names["actor.l0"].cols == 256     # [W;b] Keras layout
+    assert names["replay"].rows == 1_000_000 and names["replay"].cols == 44
+    assert L.sacx_arena_bytes(h) > 176_000_000
+    L.sacx_destroy(h)
+    bad = EngineConfig(s_dim=17, a_dim=6, use_expert=True, expert_batch=7).to_c()
+    assert L.sacx_create(ctypes.byref(bad), ctypes.byref(h)) != 0
+    assert b"even" in L.sacx_last_error(None)

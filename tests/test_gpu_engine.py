@@ -1,0 +1,201 @@
+"""Device parity tests: the HIP engine (through the C ABI) against the CPU
+oracle on identical seeded inputs.  Run on the MI355X box (-m gpu).
+
+Tolerances (fp32 device vs fp64 oracle):
+  * sampler indices: bit-exact; noise: bit-exact after the f64->f32 cast
+  * per-stage activations / losses: 2e-5 relative to the tensor's max
+  * gradients (read back through Adam's first moment): 2e-4 relative to max
+  * Q-loss trajectory over 100 updates: 1e-4 relative (BASELINE.json north_star)
+"""
+import numpy as np
+import pytest
+
+import sac_oracle as O
+from helpers import B1, make_pair, oracle_step, relerr
+
+pytestmark = pytest.mark.gpu
+
+
+def _draw(seed, N, B, A, ne=0):
+    rs = np.random.RandomState(seed)
+    gen = np.random.default_rng(seed + 7) if ne else None
+    return rs, gen
+
+
+def test_rng_matches_numpy(gpu_available):
+    eng, ocfg, st, buf, nrm, _ = make_pair(S=5, A=3, hidden=(32, 32), B=37, N=777)
+    for seed in (0, 2590541744, 12345):
+        rs = np.random.RandomState(seed)
+        rs.normal(size=1)                                    # leave a cached gaussian (has_gauss)
+        eng.rng_set_state(rs.get_state())
+        for _ in range(3):
+            eng.step(1, eager=True)
+            eng.sync()
+            idx = rs.randint(777, size=37)
+            noise = rs.normal(size=(3 * 37 * 3,))
+            assert np.array_equal(eng.v["slot0.idx"][0].cpu().numpy(), idx)
+            assert np.array_equal(eng.v["slot0.noise"][0].cpu().numpy(), noise.astype(np.float32))
+        got = eng.rng_get_state()
+        ref = rs.get_state()
+        assert np.array_equal(got[1], ref[1]) and got[2] == ref[2] and got[3] == ref[3] and got[4] == ref[4]
+    eng.close()
+
+
+def test_rng_big_draws(gpu_available):
+    """Many twists per update (B*A large) and a near-power-of-two bound."""
+    eng, *_ = make_pair(S=4, A=17, hidden=(16, 16), B=1024, N=(1 << 20) + 3)
+    rs = np.random.RandomState(99)
+    eng.rng_set_state(rs.get_state())
+    eng.step(2, eager=True)
+    eng.sync()
+    for _ in range(2):
+        idx = rs.randint((1 << 20) + 3, size=1024)
+        nz = rs.normal(size=3 * 1024 * 17).astype(np.float32)
+    assert np.array_equal(eng.v["slot0.idx"][0].cpu().numpy(), idx)
+    assert np.array_equal(eng.v["slot0.noise"][0].cpu().numpy(), nz)
+    eng.close()
+
+
+def test_replay_ring_fifo(gpu_available):
+    """TrajectoryBuffer.add truncation (buffers.py:60-66) on the device ring."""
+    from sac_eo.engine import Engine, EngineConfig
+    eng = Engine(EngineConfig(s_dim=3, a_dim=2, hidden=(16, 16), batch=4, buffer_capacity=10))
+    rs = np.random.RandomState(0)
+    ref = {k: np.zeros((0,) + sh, np.float32) for k, sh in (("s", (3,)), ("a", (2,)), ("r", ()), ("sp", (3,)), ("d", ()))}
+    for n in (4, 5, 3, 12, 1):
+        rows = dict(s=rs.normal(size=(n, 3)), a=rs.normal(size=(n, 2)), r=rs.normal(size=n),
+                    sp=rs.normal(size=(n, 3)), d=(rs.uniform(size=n) < .5).astype(np.float64))
+        eng.append(rows["s"], rows["a"], rows["r"], rows["sp"], rows["d"])
+        for k in ref:
+            ref[k] = np.concatenate([ref[k], rows[k].astype(np.float32)])[-10:]
+    c = eng.ctl()
+    assert c["cur_size"] == 10
+    rep = eng.v["replay"].cpu().numpy()
+    phys = (c["start"] + np.arange(10)) % 10
+    assert np.array_equal(rep[phys, 0:3], ref["s"])
+    assert np.array_equal(rep[phys, 3:5], ref["a"])
+    assert np.array_equal(rep[phys, 5:8], ref["sp"])
+    assert np.array_equal(rep[phys, 8], ref["r"])
+    assert np.array_equal(rep[phys, 9], ref["d"])
+    eng.close()
+
+
+def _one_step_compare(act, normalizers="identity", per_state_std=False, use_expert=False, B=256, seed=0,
+                      done_p=0.05):
+    eng, ocfg, st, buf, nrm, expert = make_pair(act=act, normalizers=normalizers, per_state_std=per_state_std,
+                                               use_expert=use_expert, B=B, seed=seed, done_p=done_p)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(seed + 5)
+    gen = np.random.default_rng(seed + 6)
+    eng.rng_set_state(rs.get_state())
+    R = O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=20 if use_expert else 0, gen=gen)
+    if use_expert:
+        eng.push_perms(R["perm"][None, :])
+    keep = {}
+    st0 = st.copy()
+    stats = oracle_step(st, ocfg, nrm, buf, R, expert, keep)
+    eng.step(1, eager=True)
+    eng.sync()
+    v = {k: t.cpu().numpy() for k, t in eng.v.items()}
+    S, A = ocfg.S, ocfg.A
+    # sampler: bit-exact
+    assert np.array_equal(v["slot0.idx"][0], R["idx"])
+    # forward stages
+    assert relerr(v["ws.Xa"][:B, :S], keep["sp_n"]) < 1e-6
+    assert relerr(v["ws.Ha1"][:B], keep["actor_h_t"][0]) < 2e-5
+    assert relerr(v["ws.Ha2"][B:2 * B], keep["actor_h_p"][1]) < 2e-5
+    assert relerr(v["ws.nlp_t"][0], keep["nlp_t"]) < 2e-5
+    assert relerr(v["ws.nlp_p"][0], keep["nlp_p"]) < 2e-5
+    assert relerr(v["ws.Hq2"][2 * B:3 * B], keep["q0_h"][1]) < 2e-5
+    # losses (stats ring)
+    row = eng.stats(1)[0]
+    for i, k in enumerate(("q1_loss", "q2_loss", "p_loss", "alpha_loss")):
+        assert abs(row[i] - stats[k]) <= 2e-5 * abs(stats[k]) + 1e-7, (k, row[i], stats[k])
+    assert abs(row[4] - stats["alpha"]) <= 1e-6 * abs(stats["alpha"])
+    # gradients through Adam's first moment (m_1 = g * (1 - beta1))
+    def grads_of(net):
+        m = eng.v["adam_m"][0]
+        out = []
+        for i in range(3):
+            seg = eng.segments[f"{net}.l{i}"]
+            off = seg["offset"] // 4
+            n = seg["rows"] * seg["cols"]
+            w = m[off: off + n].cpu().numpy().reshape(seg["rows"], seg["cols"]) / B1
+            out += [w[:-1], w[-1]]
+        return out
+    for k in range(2):
+        for gd, go in zip(grads_of(f"q{k}"), keep[f"q{k}_grads"]):
+            assert relerr(gd, go) < 2e-4
+    for gd, go in zip(grads_of("actor"), keep["actor_grads"]):
+        assert relerr(gd, go) < 2e-4, (relerr(gd, go))
+    if not per_state_std:
+        seg = eng.segments["actor.logstd"]
+        gl = eng.v["adam_m"][0][seg["offset"] // 4: seg["offset"] // 4 + A].cpu().numpy() / B1
+        assert relerr(gl, keep["g_logstd"][0]) < 2e-4
+    # Polyak: targets = keep*f32(1-tau) + updated q * f32(tau)
+    for k in range(2):
+        tgt = eng.get_net(f"t{k}")
+        for a_, b_ in zip(tgt, st.q_targ[k]):
+            assert np.max(np.abs(a_ - b_)) < 1e-5
+    eng.close()
+    return True
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "elu"])
+def test_one_update_matches_oracle(gpu_available, act):
+    _one_step_compare(act)
+
+
+def test_one_update_nontrivial_normalizers(gpu_available):
+    _one_step_compare("tanh", normalizers="random", seed=3)
+
+
+def test_one_update_per_state_std(gpu_available):
+    _one_step_compare("relu", per_state_std=True, seed=4)
+
+
+def test_one_update_sac_eo(gpu_available):
+    _one_step_compare("relu", use_expert=True, seed=5)
+
+
+def test_one_update_small_batch(gpu_available):
+    _one_step_compare("relu", B=37, seed=6)
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_qloss_trajectory_100(gpu_available, use_expert):
+    """Q-loss trajectory over 100 updates within 1e-4 relative (north_star)."""
+    B = 256
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=11, use_expert=use_expert, done_p=0.01)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(123)
+    gen = np.random.default_rng(77)
+    eng.rng_set_state(rs.get_state())
+    steps = 100
+    Rs = [O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=20 if use_expert else 0, gen=gen) for _ in range(steps)]
+    if use_expert:
+        eng.push_perms(np.stack([R["perm"] for R in Rs]))
+    eng.step(steps, num_timesteps=0, ts_increment=1)     # graph replay path
+    eng.sync()
+    dev = eng.stats(steps)
+    ref = np.array([[oracle_step(st, ocfg, nrm, buf, R, expert)[k] for k in ("q1_loss", "q2_loss")] for R in Rs])
+    rel = np.abs(dev[:, :2] - ref) / np.abs(ref)
+    assert rel.max() < 1e-4, rel.max()
+    got = eng.rng_get_state()
+    exp = rs.get_state()
+    assert np.array_equal(got[1], exp[1]) and got[2] == exp[2]
+    eng.close()
+
+
+def test_graph_equals_eager(gpu_available):
+    """hipGraph replay (sampler forked on a side stream) is bit-identical to eager launches."""
+    outs = []
+    for eager in (True, False):
+        eng, ocfg, st, buf, nrm, _ = make_pair(act="tanh", B=128, seed=21)
+        eng.rng_set_state(np.random.RandomState(5).get_state())
+        eng.step(16, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(16).copy(), eng.v["params"].cpu().numpy().copy()))
+        eng.close()
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])
