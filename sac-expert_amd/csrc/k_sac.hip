@@ -86,6 +86,41 @@ __device__ __forceinline__ float adam_update(float* p, float* m, float* v, float
     return pn;
 }
 
+// ---------------------------------------------------------------- row helpers
+// A row of a hidden layer (width H <= 64*MAXQ) is held as hv[q] = h[lane + 64 q];
+// all loads of a row are issued before any reduction so the wave's memory
+// latency overlaps instead of serialising behind each butterfly.
+#define MAXQ 8
+__device__ __forceinline__ void load_row(const float* __restrict__ h, int H, float (&hv)[MAXQ]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+        const int k = lane + 64 * q;
+        hv[q] = (k < H) ? h[k] : 0.f;
+    }
+}
+
+// out[u] = sum_k hv(k) * W[k*ldw + o0 + u] for u < 8 (o0+u < O); broadcast to all lanes
+__device__ __forceinline__ void rowdot8(const float (&hv)[MAXQ], const float* __restrict__ W, int H, int ldw,
+                                        int o0, int O, float (&out)[8]) {
+    const int lane = threadIdx.x & 63;
+    float p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) p[u] = 0.f;
+#pragma unroll
+    for (int q = 0; q < MAXQ; ++q) {
+        const int k = lane + 64 * q;
+        if (k < H) {
+            const float* wr = W + (size_t)k * ldw + o0;
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (o0 + u < O) p[u] = fmaf(hv[q], wr[u], p[u]);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) out[u] = wave_sum(p[u]);
+}
+
 // ==================================================================== k_gemm
 __device__ __forceinline__ void load_a(const GemmProb& g, int m, bool mok, int k0, bool vec, float (&a)[4]) {
     if (g.a_kc) {
@@ -564,14 +599,22 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         for (int i = 1; i < h.nseg; ++i)
             if (row >= h.seg[i].r0) sidx = i;
         const HeadSeg sg = h.seg[sidx];
-        const float* h2 = h.H2 + (size_t)row * h.ldh;
+        float hv[MAXQ];
+        load_row(h.H2 + (size_t)row * h.ldh, h.H1, hv);
+        const float* bias = h.W3 + (size_t)h.H1 * h.Aout;
         float mu = 0.f, lraw = 0.f;
-        for (int o = 0; o < h.Aout; ++o) {
-            float p = 0.f;
-            for (int k = lane; k < h.H1; k += 64) p = fmaf(h2[k], h.W3[(size_t)k * h.Aout + o], p);
-            const float s = wave_sum(p) + h.W3[(size_t)h.H1 * h.Aout + o];
-            if (lane == o) mu = s;
-            if (h.per_state_std && lane + h.A == o) lraw = s;
+        for (int o0 = 0; o0 < h.Aout; o0 += 8) {
+            float s8[8];
+            rowdot8(hv, h.W3, h.H1, h.Aout, o0, h.Aout, s8);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int o = o0 + u;
+                if (o < h.Aout) {
+                    const float sv = s8[u] + bias[o];
+                    if (lane == o) mu = sv;
+                    if (h.per_state_std && lane + h.A == o) lraw = sv;
+                }
+            }
         }
         float nlp_vec = 0.f, nlp_corr = 0.f;
         if (lane < h.A) {
@@ -641,17 +684,30 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
     const int B = q.B, H1 = q.H1;
     if (row < B) {
         const int nnet = (q.mode == 0) ? 4 : 2;
-        float out[4];
-        for (int k = 0; k < nnet; ++k) {
-            const float* hr = q.H2 + ((size_t)k * B + row) * H1;
-            const float* w = q.W3[k];
-            float p = 0.f;
-            for (int i = lane; i < H1; i += 64) p = fmaf(hr[i], w[i], p);
-            out[k] = wave_sum(p) + w[H1];
+        float hv[4][MAXQ];
+        float wv[4][MAXQ];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (k < nnet) {
+                load_row(q.H2 + ((size_t)k * B + row) * H1, H1, hv[k]);
+                load_row(q.W3[k], H1, wv[k]);
+            }
         }
+        float out[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            float p = 0.f;
+            if (k < nnet) {
+#pragma unroll
+                for (int i = 0; i < MAXQ; ++i) p = fmaf(hv[k][i], wv[k][i], p);
+            }
+            out[k] = wave_sum(p);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (k < nnet) out[k] = out[k] + q.W3[k][H1];
         const float alpha = *q.alpha;
         float g0, g1;
-        int dn0, dn1;  // slab of the differentiated nets
         if (q.mode == 0) {
             const float rd = *q.ret_den;
             const float v0 = out[0] * rd, v1 = out[1] * rd;
@@ -667,8 +723,6 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
                 q.g[row] = g0;
                 q.g[B + row] = g1;
             }
-            dn0 = 2;
-            dn1 = 3;
         } else {
             const float q0 = out[0], q1 = out[1];
             const float minq = fminf(q0, q1);
@@ -678,18 +732,22 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
             const float s1 = q1 < q0 ? 1.f : (q0 == q1 ? 0.5f : 0.f);
             g0 = gmin * s0;
             g1 = gmin * s1;
-            dn0 = 0;
-            dn1 = 1;
         }
-        const float* w0 = q.W3[dn0];
-        const float* w1 = q.W3[dn1];
-        const float* h0 = q.H2 + ((size_t)dn0 * B + row) * H1;
-        const float* h1 = q.H2 + ((size_t)dn1 * B + row) * H1;
+        // differentiated nets: slabs 2,3 (mode 0) or 0,1 (mode 1)
+        const int dn0 = q.mode == 0 ? 2 : 0;
         float* d0 = q.D2 + (size_t)row * H1;
         float* d1 = q.D2 + ((size_t)B + row) * H1;
-        for (int i = lane; i < H1; i += 64) {
-            d0[i] = (g0 * w0[i]) * dact_f(h0[i], q.act);
-            d1[i] = (g1 * w1[i]) * dact_f(h1[i], q.act);
+#pragma unroll
+        for (int i = 0; i < MAXQ; ++i) {
+            const int k = lane + 64 * i;
+            if (k < H1) {
+                const float a0 = dn0 == 2 ? hv[2][i] : hv[0][i];
+                const float a1 = dn0 == 2 ? hv[3][i] : hv[1][i];
+                const float w0 = dn0 == 2 ? wv[2][i] : wv[0][i];
+                const float w1 = dn0 == 2 ? wv[3][i] : wv[1][i];
+                d0[k] = (g0 * w0) * dact_f(a0, q.act);
+                d1[k] = (g1 * w1) * dact_f(a1, q.act);
+            }
         }
         return;
     }
@@ -749,24 +807,51 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const float eps = b.use_expert ? b.ctl->epsilon : 0.f;
     const float w_sac = 1.f - eps;
     const float c = -w_sac * (*b.alpha) * (1.f / (float)B);
+    // action gradient: ga_j = sum over the input rows S+j of W1 of the row's layer-1 delta
     float ga = 0.f;
-    for (int j = 0; j < A; ++j) {
-        float p = 0.f;
-        if (pol) {
-            for (int k = 0; k < 2; ++k) {
-                const float* dr = b.Dp1 + ((size_t)k * B + row) * b.H0;
-                const float* w = b.Wq1[k] + (size_t)(S + j) * b.H0;
-                for (int i = lane; i < b.H0; i += 64) p = fmaf(dr[i], w[i], p);
+    float dv0[MAXQ], dv1[MAXQ];
+    const float* Wa;
+    const float* Wb;
+    int Hd;
+    if (pol) {
+        Hd = b.H0;
+        load_row(b.Dp1 + (size_t)row * b.H0, Hd, dv0);
+        load_row(b.Dp1 + ((size_t)B + row) * b.H0, Hd, dv1);
+        Wa = b.Wq1[0];
+        Wb = b.Wq1[1];
+    } else {
+        const int e = row - B;
+        const int k = e < b.ne / 2 ? 0 : 1;
+        Hd = b.Hm0;
+        load_row(b.Dm1 + (size_t)e * b.Hm0, Hd, dv0);
+#pragma unroll
+        for (int i = 0; i < MAXQ; ++i) dv1[i] = 0.f;
+        Wa = b.Wm1[k];
+        Wb = b.Wm1[k];
+    }
+    for (int j0 = 0; j0 < A; j0 += 8) {
+        float p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            p[u] = 0.f;
+            if (j0 + u < A) {
+                const float* wa = Wa + (size_t)(S + j0 + u) * Hd;
+                const float* wb = Wb + (size_t)(S + j0 + u) * Hd;
+#pragma unroll
+                for (int i = 0; i < MAXQ; ++i) {
+                    const int k = lane + 64 * i;
+                    if (k < Hd) {
+                        p[u] = fmaf(dv0[i], wa[k], p[u]);
+                        if (pol) p[u] = fmaf(dv1[i], wb[k], p[u]);
+                    }
+                }
             }
-        } else {
-            const int e = row - B;
-            const int k = e < b.ne / 2 ? 0 : 1;
-            const float* dr = b.Dm1 + (size_t)e * b.Hm0;
-            const float* w = b.Wm1[k] + (size_t)(S + j) * b.Hm0;
-            for (int i = lane; i < b.Hm0; i += 64) p = fmaf(dr[i], w[i], p);
         }
-        const float s = wave_sum(p);
-        if (lane == j) ga = s / b.a_den[j];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float sj = wave_sum(p[u]);
+            if (j0 + u < A && lane == j0 + u) ga = sj / b.a_den[j0 + u];
+        }
     }
     float gx = 0.f, dl = 0.f;
     if (lane < A) {

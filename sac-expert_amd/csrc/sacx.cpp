@@ -96,6 +96,7 @@ struct sacx_handle {
     bool bound = false;
     std::vector<Launch> plan[2];
     std::vector<GemmProb> probs;
+    int probs_cursor = 0;
     GemmProb* d_probs = nullptr;
     std::map<std::pair<int, int>, hipGraphExec_t> graphs;
     std::vector<hipEvent_t> events;
@@ -289,7 +290,9 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         L.flops += gemm_flops(p);
         L.bytes += gemm_bytes(p);
     }
-    L.gemm_first = (int)h->probs.size();
+    // both slot plans address the same (slot-independent) problem table
+    L.gemm_first = h->probs_cursor;
+    h->probs_cursor += (int)ps.size();
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
     L.gemm.nprob = (int)ps.size();
     L.gemm.total_tiles = tiles;
@@ -309,6 +312,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
 void build_plan(sacx_handle* h, int slot, bool record_probs) {
     std::vector<Launch>& plan = h->plan[slot];
     plan.clear();
+    h->probs_cursor = 0;
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
     const int ldS = h->ldS, ldQ = h->ldQ, act = h->act, mact = h->mact;
@@ -518,7 +522,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         pw.push_back(prob_dw(Ha1 + (size_t)B * H0, H0, H0, Rb, Da2, H1, W("actor.l1"), nullptr, GRP_PI));
         pw.push_back(prob_dw(Ha2 + (size_t)B * H1, H1, H1, Rb, Da3, Aout, W("actor.l2"), nullptr, GRP_PI));
         if (!h->cfg.per_state_std) {
-            GemmProb p = prob_dw(nullptr, 1, 0, Rb, E, A, W("actor.logstd"), nullptr, GRP_PI);
+            GemmProb p = prob_dw(E, 1, 0, Rb, E, A, W("actor.logstd"), nullptr, GRP_PI);
             p.ones_row = 0;   // single all-ones row: column sums of E
             pw.push_back(p);
         }
@@ -651,6 +655,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     if (cfg->abi_version != SACX_ABI_VERSION) return bad("abi_version mismatch");
     if (cfg->s_dim <= 0 || cfg->a_dim <= 0 || cfg->a_dim > 32) return bad("s_dim/a_dim out of range (a_dim <= 32)");
     if (cfg->hidden[0] <= 0 || cfg->hidden[1] <= 0) return bad("hidden sizes must be positive");
+    if (cfg->hidden[0] > 512 || cfg->hidden[1] > 512) return bad("hidden sizes > 512 unsupported (row kernels hold a row in 8 regs/lane)");
     if (cfg->activation < 0 || cfg->activation > 2) return bad("activation must be relu/tanh/elu");
     if (cfg->batch <= 0 || cfg->buffer_capacity <= 0) return bad("batch/buffer_capacity must be positive");
     if (cfg->buffer_capacity >= (int64_t(1) << 31)) return bad("buffer_capacity must be < 2^31");
@@ -659,6 +664,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
             return bad("expert_batch must be positive and even (SAC_expert.py:329-332 adds equal halves)");
         if (cfg->expert_capacity < cfg->expert_batch) return bad("expert_capacity < expert_batch");
         if (cfg->model_hidden[0] <= 0 || cfg->model_hidden[1] <= 0) return bad("model sizes must be positive");
+        if (cfg->model_hidden[0] > 512 || cfg->model_hidden[1] > 512) return bad("model hidden sizes > 512 unsupported");
         if (cfg->model_activation < 0 || cfg->model_activation > 2) return bad("model activation invalid");
         if (cfg->s_dim + 1 > 512) return bad("s_dim > 511 unsupported by the model MSE head");
     }
@@ -741,6 +747,12 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->probs.clear();
     build_plan(h, 0, true);
     build_plan(h, 1, false);
+    if (h->plan[0].size() != h->plan[1].size()) return fail(h, "internal: slot plans differ");
+    for (size_t i = 0; i < h->plan[0].size(); ++i)
+        if (h->plan[0][i].kind == Launch::GEMM &&
+            (h->plan[0][i].gemm_first != h->plan[1][i].gemm_first ||
+             h->plan[0][i].gemm_first + h->plan[0][i].gemm.nprob > (int)h->probs.size()))
+            return fail(h, "internal: GEMM problem table mismatch");
     HIPCHK(h, hipMalloc(&h->d_probs, sizeof(GemmProb) * std::max<size_t>(1, h->probs.size())));
     HIPCHK(h, hipMemcpy(h->d_probs, h->probs.data(), sizeof(GemmProb) * h->probs.size(), hipMemcpyHostToDevice));
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));

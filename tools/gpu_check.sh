@@ -15,4 +15,11 @@ rc=$?; echo "smoke rc=$rc"; tail -5 gpurun_out/smoke.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -5 gpurun_out/bench.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+if [ -n "${PROF:-}" ]; then
+  export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof" -o "$PROF" \
+      -- python bench.py --steps 1000 --warmup 100 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1
+  rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof_bench.log; find gpurun_out/prof -name "*stats*" | head
+fi
 exit $rc
