@@ -25,6 +25,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstddef>
 #include <cstring>
 #include <map>
@@ -603,7 +604,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
     hipEvent_t* evS = h->events.data() + G;
     hipEvent_t evFork = h->events[2 * G];
     HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    if (with_rng && G > 1) {
+    const bool fork = with_rng && G > 1 && std::getenv("SACX_NO_FORK") == nullptr;
+    if (fork) {
         // sampler chain on a forked stream: RNG(j) overlaps update j-1; RNG(j+2)
         // waits for update j (the last reader of its slot).
         const Launch& R0 = h->plan[0][0];
