@@ -178,7 +178,11 @@ def test_qloss_trajectory_100(gpu_available, use_expert):
     eng.step(steps, num_timesteps=0, ts_increment=1)     # graph replay path
     eng.sync()
     dev = eng.stats(steps)
-    ref = np.array([[oracle_step(st, ocfg, nrm, buf, R, expert)[k] for k in ("q1_loss", "q2_loss")] for R in Rs])
+    ref = []
+    for R in Rs:
+        o = oracle_step(st, ocfg, nrm, buf, R, expert)      # one oracle update per step
+        ref.append([o["q1_loss"], o["q2_loss"]])
+    ref = np.array(ref)
     rel = np.abs(dev[:, :2] - ref) / np.abs(ref)
     assert rel.max() < 1e-4, rel.max()
     got = eng.rng_get_state()
