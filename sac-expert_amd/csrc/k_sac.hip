@@ -59,10 +59,24 @@ __device__ __forceinline__ float softplus_f(float x) {
 
 // butterfly sum over the 64 lanes; lane 0's value is broadcast so every lane
 // holds the bit-identical result
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+// quad xor-1, xor-2, then row rotate 4 and 8 (DPP, full-rate VALU): every lane of
+// a 16-lane row holds the row sum; the four row sums are read from lanes
+// 0/16/32/48 and added in a fixed order, so the result is wave-uniform and
+// bit-identical on every lane.
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-    return __shfl(v, 0, 64);
+    v = v + dpp<0xB1>(v);
+    v = v + dpp<0x4E>(v);
+    v = v + dpp<0x124>(v);
+    v = v + dpp<0x128>(v);
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return (r0 + r1) + (r2 + r3);
 }
 
 __device__ __forceinline__ float adam_lr(const AdamConsts& c, int group, int64_t t) {
@@ -177,15 +191,40 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     __shared__ float red[4][4][64];
     const int tile = blockIdx.x;
     int p = 0;
-    for (int i = 1; i < ga.nprob; ++i)
-        if (tile >= ga.probs[i].tile_begin) p = i;
-    const GemmProb g = ga.probs[p];
+#pragma unroll
+    for (int i = 1; i < GEMM_MAXP; ++i)
+        if (i < ga.nprob && tile >= ga.probs[i].tile_begin) p = i;
+    const GemmProb& g = ga.probs[p];
     const int lt = tile - g.tile_begin;
     const int tm = lt / g.tiles_n;
     const int tn = lt - tm * g.tiles_n;
     const int m0 = tm * 16, n0 = tn * 16;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = lane & 15, grp = lane >> 4;
+
+    // ---- epilogue operands first: this thread's output element is known now,
+    //      so its loads overlap the operand loads instead of following the MFMAs
+    const int t = threadIdx.x;
+    const int row = t >> 4, col = t & 15;
+    const int mm = m0 + row, nn = n0 + col;
+    const bool out_ok = (mm < g.M) && (nn < g.N);
+    const int epi = g.epi;
+    float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
+    size_t pidx = 0;
+    if (out_ok) {
+        if (epi == EPI_FWD) {
+            e0 = g.bias[nn];
+        } else if (epi == EPI_DACT) {
+            e0 = g.H[(size_t)mm * g.ldh + nn];
+        } else if (epi == EPI_ADAM) {
+            pidx = (size_t)mm * g.ldp + nn;
+            e0 = g.P[pidx];
+            e1 = g.P[pidx + ga.p_stride];
+            e2 = g.P[pidx + 2 * ga.p_stride];
+            if (g.T != nullptr) e3 = g.T[pidx];
+        }
+    }
+
     const int nIt = (g.K + 15) >> 4;
     const int per = (nIt + 3) >> 2;
     const int it0 = wave * per;
@@ -223,23 +262,18 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     for (int q = 0; q < 4; ++q) red[wave][q][lane] = acc[q];
     __syncthreads();
 
-    // one output element per thread: (row = t>>4, col = t&15); lane (row>>2)*16+col, reg row&3
-    const int t = threadIdx.x;
-    const int row = t >> 4, col = t & 15;
+    // (row, col) lives in lane (row>>2)*16+col, register row&3 of each wave's tile
     const int L = ((row >> 2) << 4) | col, R = row & 3;
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
-    const int mm = m0 + row, nn = n0 + col;
-    if (mm >= g.M || nn >= g.N) return;
-    switch (g.epi) {
-        case EPI_FWD: {
-            const float z = v + g.bias[nn];
-            g.C[(size_t)mm * g.ldc + nn] = act_f(z, g.act);
+    if (!out_ok) return;
+    switch (epi) {
+        case EPI_FWD:
+            g.C[(size_t)mm * g.ldc + nn] = act_f(v + e0, g.act);
             break;
-        }
         case EPI_DACT:
-            g.C[(size_t)mm * g.ldc + nn] = v * dact_f(g.H[(size_t)mm * g.ldh + nn], g.act);
+            g.C[(size_t)mm * g.ldc + nn] = v * dact_f(e0, g.act);
             break;
         case EPI_STORE:
             g.C[(size_t)mm * g.ldc + nn] = v;
@@ -248,15 +282,17 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
             const Ctl* ctl = ga.ctl;
             const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
             const float lr_t = adam_lr(ga.adam, g.group, tstep);
-            const size_t idx = (size_t)mm * g.ldp + nn;
-            float* P = g.P + idx;
-            const float pn = adam_update(P, P + ga.p_stride, P + 2 * ga.p_stride, v * g.grad_scale, lr_t);
+            const float gr = v * g.grad_scale;
+            const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+            const float mm1 = e1 + (gr - e1) * (1.f - b1);
+            const float vv1 = e2 + (gr * gr - e2) * (1.f - b2);
+            const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
+            g.P[pidx] = pn;
+            g.P[pidx + ga.p_stride] = mm1;
+            g.P[pidx + 2 * ga.p_stride] = vv1;
             if (g.T != nullptr) {
                 const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-                if (ctl->num_timesteps % tui == 0) {
-                    float* T = g.T + idx;
-                    *T = *T * ga.adam.tau_keep + pn * ga.adam.tau_take;
-                }
+                if (ctl->num_timesteps % tui == 0) g.T[pidx] = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
             }
             break;
         }
@@ -601,6 +637,13 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         const HeadSeg sg = h.seg[sidx];
         float hv[MAXQ];
         load_row(h.H2 + (size_t)row * h.ldh, h.H1, hv);
+        float u_pf = 0.f, ls_pf = 0.f, am_pf = 0.f, ad_pf = 1.f;
+        if (lane < h.A) {
+            u_pf = sg.noise[(size_t)(row - sg.r0) * h.A + lane];
+            if (!h.per_state_std) ls_pf = h.logstd[lane];
+            am_pf = h.a_mean[lane];
+            ad_pf = h.a_den[lane];
+        }
         const float* bias = h.W3 + (size_t)h.H1 * h.Aout;
         float mu = 0.f, lraw = 0.f;
         for (int o0 = 0; o0 < h.Aout; o0 += 8) {
@@ -619,10 +662,10 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         float nlp_vec = 0.f, nlp_corr = 0.f;
         if (lane < h.A) {
             const int j = lane;
-            if (!h.per_state_std) lraw = h.logstd[j];
+            if (!h.per_state_std) lraw = ls_pf;
             const float l = fminf(fmaxf(lraw, -5.f), 2.f);
             const float sd = expf(l);
-            const float u = sg.noise[(size_t)(row - sg.r0) * h.A + j];
+            const float u = u_pf;
             const float x = mu + sd * u;
             const float t = tanhf(x);
             const float pi = h.lim * t;
@@ -632,7 +675,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
                 nlp_corr = 2.f * ((LN2_F - x) - softplus_f(-2.f * x));
             }
             if (sg.xq_out != nullptr)
-                sg.xq_out[(size_t)(sg.xq_row0 + row - sg.r0) * h.ldQ + h.S + j] = (pi - h.a_mean[j]) / h.a_den[j];
+                sg.xq_out[(size_t)(sg.xq_row0 + row - sg.r0) * h.ldQ + h.S + j] = (pi - am_pf) / ad_pf;
             if (row >= h.cache_row0 && h.c_t != nullptr) {
                 const size_t ci = (size_t)(row - h.cache_row0) * h.A + j;
                 h.c_t[ci] = t;
@@ -677,13 +720,22 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
 }
 
 // ==================================================================== k_qhead
+template <int MODE>
 __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
     __shared__ float buf[4][512];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = q.B, H1 = q.H1;
     if (row < B) {
-        const int nnet = (q.mode == 0) ? 4 : 2;
+        constexpr int nnet = (MODE == 0) ? 4 : 2;
+        const float alpha = *q.alpha;
+        const float nlp_r = q.nlp[row];
+        float r_r = 0.f, d_r = 0.f, rd = 1.f;
+        if (MODE == 0) {
+            r_r = q.r[row];
+            d_r = q.d[row];
+            rd = *q.ret_den;
+        }
         float hv[4][MAXQ];
         float wv[4][MAXQ];
 #pragma unroll
@@ -706,13 +758,11 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             if (k < nnet) out[k] = out[k] + q.W3[k][H1];
-        const float alpha = *q.alpha;
         float g0, g1;
-        if (q.mode == 0) {
-            const float rd = *q.ret_den;
+        if (MODE == 0) {
             const float v0 = out[0] * rd, v1 = out[1] * rd;
-            const float nv = fminf(v0, v1) + alpha * q.nlp[row];
-            const float y = q.r[row] + q.gamma * ((1.f - q.d[row]) * nv);
+            const float nv = fminf(v0, v1) + alpha * nlp_r;
+            const float y = r_r + q.gamma * ((1.f - d_r) * nv);
             const float e0 = out[2] - y, e1 = out[3] - y;
             const float invB = 1.f / (float)B;
             g0 = e0 * invB;
@@ -726,7 +776,7 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
         } else {
             const float q0 = out[0], q1 = out[1];
             const float minq = fminf(q0, q1);
-            if (lane == 0) q.loss_rows[row] = (-alpha) * q.nlp[row] - minq;
+            if (lane == 0) q.loss_rows[row] = (-alpha) * nlp_r - minq;
             const float gmin = -q.w_sac * (1.f / (float)B);
             const float s0 = q0 < q1 ? 1.f : (q0 == q1 ? 0.5f : 0.f);
             const float s1 = q1 < q0 ? 1.f : (q0 == q1 ? 0.5f : 0.f);
@@ -734,7 +784,7 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
             g1 = gmin * s1;
         }
         // differentiated nets: slabs 2,3 (mode 0) or 0,1 (mode 1)
-        const int dn0 = q.mode == 0 ? 2 : 0;
+        constexpr int dn0 = MODE == 0 ? 2 : 0;
         float* d0 = q.D2 + (size_t)row * H1;
         float* d1 = q.D2 + ((size_t)B + row) * H1;
 #pragma unroll
@@ -752,13 +802,13 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
         return;
     }
     // ---- SAC-EO: world-model L3 on the expert rows + MSE and its gradient
-    if (q.mode != 0 || row >= B + q.ne) return;
+    if (MODE != 0 || row >= B + q.ne) return;
     const int e = row - B;
     const int half = q.ne / 2;
     const int k = e < half ? 0 : 1;
     const int S = q.S, Hm = q.Hm1, O = S + 1;
     const float* hr = q.Hm2 + (size_t)e * Hm;
-    const float* W = q.Wm3[k];
+    const float* W = k ? q.Wm3[1] : q.Wm3[0];
     float* ob = buf[wave];
     for (int j = 0; j < S; ++j) {
         float p = 0.f;
@@ -790,7 +840,8 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
 
 void launch_qhead(const QHeadArgs& a, hipStream_t s) {
     const int rows = a.B + (a.mode == 0 ? a.ne : 0);
-    hipLaunchKernelGGL(k_qhead, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+    if (a.mode == 0) hipLaunchKernelGGL(k_qhead<0>, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_qhead<1>, dim3((rows + 3) / 4), dim3(256), 0, s, a);
 }
 
 // ==================================================================== k_actor_bwd
@@ -805,8 +856,19 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     if (row >= B + b.ne) return;
     const bool pol = row < B;
     const float eps = b.use_expert ? b.ctl->epsilon : 0.f;
+    const float alpha = *b.alpha;
+    float t_pf = 0.f, sd_pf = 0.f, u_pf = 0.f, mk_pf = 0.f;
+    if (lane < A) {
+        const size_t ci = (size_t)row * A + lane;
+        t_pf = b.c_t[ci];
+        sd_pf = b.c_std[ci];
+        u_pf = b.c_u[ci];
+        mk_pf = b.c_mask[ci];
+    }
+    float h2v[MAXQ];
+    load_row(b.Ha2 + (size_t)row * b.H1, b.H1, h2v);
     const float w_sac = 1.f - eps;
-    const float c = -w_sac * (*b.alpha) * (1.f / (float)B);
+    const float c = -w_sac * alpha * (1.f / (float)B);
     // action gradient: ga_j = sum over the input rows S+j of W1 of the row's layer-1 delta
     float ga = 0.f;
     float dv0[MAXQ], dv1[MAXQ];
@@ -856,7 +918,7 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     float gx = 0.f, dl = 0.f;
     if (lane < A) {
         const size_t ci = (size_t)row * A + lane;
-        const float t = b.c_t[ci], sd = b.c_std[ci], u = b.c_u[ci], mask = b.c_mask[ci];
+        const float t = t_pf, sd = sd_pf, u = u_pf, mask = mk_pf;
         gx = ga * b.lim * (1.f - t * t);
         if (pol) gx = gx - (2.f * c) * t;
         dl = (gx * sd) * u;
@@ -866,9 +928,11 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
         if (b.per_state_std) b.Da3[(size_t)row * b.Aout + A + lane] = dl;
         else b.E[ci] = dl;
     }
-    const float* h2 = b.Ha2 + (size_t)row * b.H1;
-    for (int i0 = 0; i0 < b.H1; i0 += 64) {
+#pragma unroll
+    for (int qq = 0; qq < MAXQ; ++qq) {
+        const int i0 = qq * 64;
         const int i = i0 + lane;
+        if (i0 >= b.H1) break;
         float p = 0.f;
         for (int o = 0; o < A; ++o) {
             const float d3 = __shfl(gx, o, 64);
@@ -880,7 +944,7 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
                 if (i < b.H1) p = fmaf(d3, b.W3a[(size_t)i * b.Aout + A + o], p);
             }
         }
-        if (i < b.H1) b.Da2[(size_t)row * b.H1 + i] = p * dact_f(h2[i], b.act);
+        if (i < b.H1) b.Da2[(size_t)row * b.H1 + i] = p * dact_f(h2v[qq], b.act);
     }
 }
 

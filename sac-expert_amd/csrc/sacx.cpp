@@ -98,7 +98,6 @@ struct sacx_handle {
     std::vector<Launch> plan[2];
     std::vector<GemmProb> probs;
     int probs_cursor = 0;
-    GemmProb* d_probs = nullptr;
     std::map<std::pair<int, int>, hipGraphExec_t> graphs;
     std::vector<hipEvent_t> events;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
@@ -295,6 +294,8 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     L.gemm_first = h->probs_cursor;
     h->probs_cursor += (int)ps.size();
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
+    if (ps.size() > GEMM_MAXP) { fprintf(stderr, "sacx: too many GEMM problems in %s\n", name.c_str()); abort(); }
+    for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
     L.gemm.nprob = (int)ps.size();
     L.gemm.total_tiles = tiles;
     L.gemm.p_stride = h->p_stride;
@@ -566,12 +567,7 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
     switch (L.kind) {
         case Launch::RNG: launch_rng(L.rng, s); break;
         case Launch::GATHER: launch_gather(L.gather, s); break;
-        case Launch::GEMM: {
-            GemmArgs g = L.gemm;
-            g.probs = h->d_probs + L.gemm_first;
-            launch_gemm(g, s);
-            break;
-        }
+        case Launch::GEMM: launch_gemm(L.gemm, s); break;
         case Launch::AHEAD: launch_actor_head(L.head, L.fin, s); break;
         case Launch::QHEAD: launch_qhead(L.qh, s); break;
         case Launch::ABWD: launch_actor_bwd(L.ab, s); break;
@@ -709,7 +705,6 @@ void sacx_destroy(sacx_handle* h) {
     if (!h) return;
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : h->events) (void)hipEventDestroy(e);
-    if (h->d_probs) (void)hipFree(h->d_probs);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     delete h;
@@ -755,8 +750,6 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
             (h->plan[0][i].gemm_first != h->plan[1][i].gemm_first ||
              h->plan[0][i].gemm_first + h->plan[0][i].gemm.nprob > (int)h->probs.size()))
             return fail(h, "internal: GEMM problem table mismatch");
-    HIPCHK(h, hipMalloc(&h->d_probs, sizeof(GemmProb) * std::max<size_t>(1, h->probs.size())));
-    HIPCHK(h, hipMemcpy(h->d_probs, h->probs.data(), sizeof(GemmProb) * h->probs.size(), hipMemcpyHostToDevice));
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
     h->bound = true;

@@ -64,8 +64,9 @@ struct GemmProb {
     int32_t pad;
 };
 
+#define GEMM_MAXP 8
 struct GemmArgs {
-    const GemmProb* probs;
+    GemmProb probs[GEMM_MAXP];   // by value: no dependent global load to find a tile's problem
     int32_t nprob;
     int32_t total_tiles;
     int64_t p_stride;      // floats between params / adam_m / adam_v blocks
