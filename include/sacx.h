@@ -137,6 +137,14 @@ int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t*
  * updates at one env step as in SAC.train). */
 int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment,
                   int32_t flags);
+/* n_steps x _apply_model_grads (sac_eo/algs/mbrl_onpolicy_alg.py:301-319) as
+ * called by SAC_exp._update_models (sac_eo/algs/SAC_expert.py:519-550): each
+ * step fits both world models on their own minibatch and applies one Keras
+ * Adam over all model variables.  idx: host array [n_steps, 2, model_batch]
+ * of replay-logical row indices (the caller's np.random.shuffle minibatches
+ * of model_data, mapped into the replay ring).  Per-step summed loss goes to
+ * the "mstats" ring.  Requires use_expert. */
+int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t flags);
 int sacx_sync(sacx_handle* h);
 
 /* --- measurement ----------------------------------------------------------- */

@@ -1005,3 +1005,80 @@ void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipSt
     hipLaunchKernelGGL(k_set_ctl, dim3(1), dim3(64), 0, s, ctl, num_timesteps, ts_increment);
 }
 }  // namespace sacx
+
+namespace sacx {
+// ==================================================================== world-model fitting
+// MSEModel.get_loss (continuous_models.py:280-302) summed over the two models
+// and one Keras Adam over all their variables (mbrl_onpolicy_alg.py:301-319).
+__global__ __launch_bounds__(256) void k_mgather(MGatherArgs g) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= 2 * g.mb) return;
+    const int S = g.S, A = g.A;
+    const int64_t slot = g.ctl->mfit_seq % g.idx_cap;
+    const int64_t li = g.idx_ring[slot * 2 * g.mb + row];
+    const int64_t phys = (g.ctl->start + li) % g.cap;
+    const float* rec = g.replay + phys * (int64_t)g.stride;
+    for (int c = lane; c < g.ldQ; c += 64) {
+        float x = 0.f;
+        if (c < S) x = (rec[c] - g.s_mean[c]) / g.s_den[c];
+        else if (c < S + A) x = (rec[c] - g.a_mean[c - S]) / g.a_den[c - S];
+        g.X[(size_t)row * g.ldQ + c] = x;
+    }
+    for (int c = lane; c <= S; c += 64) {
+        float y;
+        if (c < S) y = ((rec[S + A + c] - rec[c]) - g.d_mean[c]) / g.d_den[c];
+        else y = (rec[2 * S + A] - g.r_norm[0]) / g.r_norm[1];
+        g.T[(size_t)row * (S + 1) + c] = y;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_mloss(MLossArgs g) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + wave;
+    if (row >= 2 * g.mb) return;
+    const int S = g.S, O = S + 1;
+    const float inv = 1.f / (float)g.mb;
+    float sq = 0.f, er = 0.f;
+    for (int c = lane; c <= S; c += 64) {
+        const float e = g.T[(size_t)row * O + c] - g.O[(size_t)row * O + c];
+        if (c < S) {
+            sq = sq + e * e;
+            g.D3[(size_t)row * O + c] = -e * inv;
+        } else {
+            er = e;
+            g.D3[(size_t)row * O + c] = -e * (g.reward_coef * inv);
+        }
+    }
+    const float tot = wave_sum(sq);
+    const float e_r = wave_sum(er);
+    if (lane == 0) g.loss_rows[row] = 0.5f * tot + g.reward_coef * (0.5f * (e_r * e_r));
+}
+
+__global__ __launch_bounds__(64) void k_mfinal(MFinalArgs f) {
+    const int lane = threadIdx.x & 63;
+    float s0 = 0.f, s1 = 0.f;
+    for (int i = lane; i < f.mb; i += 64) {
+        s0 += f.loss_rows[i];
+        s1 += f.loss_rows[f.mb + i];
+    }
+    const float l0 = wave_sum(s0) / (float)f.mb, l1 = wave_sum(s1) / (float)f.mb;
+    if (lane == 0) {
+        const int64_t seq = f.ctl->mfit_seq;
+        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = l0 + l1;
+        f.mstats[(size_t)(seq % f.mstats_cap) * 2 + 1] = (float)seq;
+        f.ctl->t_model += 1;
+        f.ctl->mfit_seq = seq + 1;
+    }
+}
+
+void launch_mgather(const MGatherArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_mgather, dim3((2 * a.mb + 3) / 4), dim3(256), 0, s, a);
+}
+void launch_mloss(const MLossArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_mloss, dim3((2 * a.mb + 3) / 4), dim3(256), 0, s, a);
+}
+void launch_mfinal(const MFinalArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_mfinal, dim3(1), dim3(64), 0, s, a);
+}
+}  // namespace sacx

@@ -48,7 +48,7 @@ struct SegInfo {
 };
 
 struct Launch {
-    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD } kind;
+    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, MGATHER, MLOSS, MFINAL } kind;
     std::string name;
     RngArgs rng;
     GatherArgs gather;
@@ -57,6 +57,9 @@ struct Launch {
     FinalArgs fin;
     QHeadArgs qh;
     ActorBwdArgs ab;
+    MGatherArgs mg;
+    MLossArgs ml;
+    MFinalArgs mf;
     int grid = 0, block = 256;
     double flops = 0, bytes = 0;
     int gemm_first = 0;  // index of the first problem in the host table (GEMM)
@@ -70,6 +73,9 @@ const char* kernel_family(Launch::Kind k) {
         case Launch::AHEAD: return "k_actor_head";
         case Launch::QHEAD: return "k_qhead";
         case Launch::ABWD: return "k_actor_bwd";
+        case Launch::MGATHER: return "k_mgather";
+        case Launch::MLOSS: return "k_mloss";
+        case Launch::MFINAL: return "k_mfinal";
     }
     return "?";
 }
@@ -83,7 +89,7 @@ struct sacx_handle {
     int S = 0, A = 0, H0 = 0, H1 = 0, B = 0, Aout = 0, ne = 0, Hm0 = 0, Hm1 = 0, ecap = 0;
     int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0, act = 0, mact = 0;
     int64_t cap = 0;
-    int graph_steps = 8, stats_cap = 4096, perm_cap = 4096;
+    int graph_steps = 8, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
     // layout
     std::vector<SegInfo> segs;
     std::map<std::string, size_t> seg_index;
@@ -96,6 +102,9 @@ struct sacx_handle {
     hipStream_t cap_stream = nullptr, rng_stream = nullptr;
     bool bound = false;
     std::vector<Launch> plan[2];
+    std::vector<Launch> mplan;
+    hipGraphExec_t mgraph = nullptr;
+    int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
     std::vector<GemmProb> probs;
     int probs_cursor = 0;
     std::map<std::pair<int, int>, hipGraphExec_t> graphs;
@@ -231,6 +240,20 @@ void build_layout(sacx_handle* h) {
     h->add("ws.E", Rb, A, F, 0);
     h->add("ws.Hl1", B, H0, F, 0);
     h->add("ws.Hl2", B, H1, F, 0);
+    if (h->cfg.use_expert) {          // world-model fitting (A16)
+        const int R2 = 2 * h->mb, O = S + 1;
+        h->add("mfit.idx", h->mfit_cap, R2, SACX_I32, SACX_ROLE_WORK);
+        h->add("mstats", h->stats_cap, 2, F, SACX_ROLE_STATE);
+        h->add("ws.Xf", R2, h->ldQ, F, 0);
+        h->add("ws.Tf", R2, O, F, 0);
+        h->add("ws.Hf1", R2, Hm0, F, 0);
+        h->add("ws.Hf2", R2, Hm1, F, 0);
+        h->add("ws.Of", R2, O, F, 0);
+        h->add("ws.Df3", R2, O, F, 0);
+        h->add("ws.Df2", R2, Hm1, F, 0);
+        h->add("ws.Df1", R2, Hm0, F, 0);
+        h->add("ws.lf", 1, R2, F, 0);
+    }
     h->arena_bytes = (h->arena_bytes + 255) & ~uint64_t(255);
 }
 
@@ -563,6 +586,70 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     }
 }
 
+// one world-model fitting step: gather -> 3 fwd GEMMs -> loss grads -> 2 dX GEMMs -> dW + Adam -> finalize
+void build_model_plan(sacx_handle* h) {
+    std::vector<Launch>& plan = h->mplan;
+    plan.clear();
+    if (!h->cfg.use_expert) return;
+    const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ, mact = h->mact;
+    auto W = [&](const std::string& n) { return h->f(n); };
+    float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Hf1 = W("ws.Hf1"), *Hf2 = W("ws.Hf2"), *Of = W("ws.Of");
+    float *Df3 = W("ws.Df3"), *Df2 = W("ws.Df2"), *Df1 = W("ws.Df1");
+    {
+        Launch L{};
+        L.kind = Launch::MGATHER;
+        L.name = "model.gather";
+        MGatherArgs& g = L.mg;
+        g.replay = W("replay"); g.cap = h->cap; g.stride = h->stride; g.S = S; g.A = A; g.mb = mb;
+        g.idx_ring = h->ptr<int32_t>("mfit.idx"); g.idx_cap = h->mfit_cap; g.ctl = h->ctl();
+        g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den"); g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
+        g.d_mean = W("norm.d_mean"); g.d_den = W("norm.d_den"); g.r_norm = W("norm.r");
+        g.X = Xf; g.ldQ = ldQ; g.T = Tf;
+        L.grid = (2 * mb + 3) / 4;
+        L.bytes = 4.0 * 2 * mb * (2.0 * S + A + 1 + ldQ + O);
+        plan.push_back(L);
+    }
+    std::vector<GemmProb> f0, f1, f2, b2, b1, w;
+    for (int k = 0; k < 2; ++k) {
+        const std::string n = "m" + std::to_string(k);
+        const size_t r0 = (size_t)k * mb;
+        f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, mact));
+        f1.push_back(prob_fwd(Hf1 + r0 * Hm0, Hm0, mb, Hm0, W(n + ".l1"), Hm1, Hf2 + r0 * Hm1, mact));
+        f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), O, Of + r0 * O, ACT_NONE));
+        b2.push_back(prob_dx(Df3 + r0 * O, mb, O, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, mact));
+        b1.push_back(prob_dx(Df2 + r0 * Hm1, mb, Hm1, W(n + ".l1"), Hm0, Hf1 + r0 * Hm0, Df1 + r0 * Hm0, mact));
+        w.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Df1 + r0 * Hm0, Hm0, W(n + ".l0"), nullptr, GRP_MODEL));
+        w.push_back(prob_dw(Hf1 + r0 * Hm0, Hm0, Hm0, mb, Df2 + r0 * Hm1, Hm1, W(n + ".l1"), nullptr, GRP_MODEL));
+        w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * O, O, W(n + ".l2"), nullptr, GRP_MODEL));
+    }
+    add_gemm(h, plan, "model.fwd0", f0, false);
+    add_gemm(h, plan, "model.fwd1", f1, false);
+    add_gemm(h, plan, "model.fwd2", f2, false);
+    {
+        Launch L{};
+        L.kind = Launch::MLOSS;
+        L.name = "model.loss";
+        L.ml.S = S; L.ml.mb = mb; L.ml.T = Tf; L.ml.O = Of; L.ml.D3 = Df3; L.ml.loss_rows = W("ws.lf");
+        L.ml.reward_coef = h->cfg.reward_loss_coef;
+        L.grid = (2 * mb + 3) / 4;
+        L.bytes = 4.0 * 2 * mb * O * 3;
+        plan.push_back(L);
+    }
+    add_gemm(h, plan, "model.bwd2", b2, false);
+    add_gemm(h, plan, "model.bwd1", b1, false);
+    add_gemm(h, plan, "model.adam", w, false);
+    {
+        Launch L{};
+        L.kind = Launch::MFINAL;
+        L.name = "model.final";
+        L.mf.ctl = h->ctl(); L.mf.loss_rows = W("ws.lf"); L.mf.mb = mb;
+        L.mf.mstats = W("mstats"); L.mf.mstats_cap = h->stats_cap;
+        L.grid = 1;
+        L.block = 64;
+        plan.push_back(L);
+    }
+}
+
 void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
     switch (L.kind) {
         case Launch::RNG: launch_rng(L.rng, s); break;
@@ -571,6 +658,9 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::AHEAD: launch_actor_head(L.head, L.fin, s); break;
         case Launch::QHEAD: launch_qhead(L.qh, s); break;
         case Launch::ABWD: launch_actor_bwd(L.ab, s); break;
+        case Launch::MGATHER: launch_mgather(L.mg, s); break;
+        case Launch::MLOSS: launch_mloss(L.ml, s); break;
+        case Launch::MFINAL: launch_mfinal(L.mf, s); break;
     }
 }
 
@@ -681,6 +771,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->Hm0 = cfg->use_expert ? cfg->model_hidden[0] : 0;
     h->Hm1 = cfg->use_expert ? cfg->model_hidden[1] : 0;
     h->mact = cfg->model_activation;
+    h->mb = cfg->use_expert ? (cfg->model_batch > 0 ? cfg->model_batch : 200) : 0;
     h->ldS = (int)r4(h->S);
     h->ldQ = (int)r4(h->S + h->A);
     h->stride = (int)r4(2 * h->S + h->A + 2);
@@ -704,6 +795,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
 void sacx_destroy(sacx_handle* h) {
     if (!h) return;
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
+    if (h->mgraph) (void)hipGraphExecDestroy(h->mgraph);
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
@@ -750,6 +842,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
             (h->plan[0][i].gemm_first != h->plan[1][i].gemm_first ||
              h->plan[0][i].gemm_first + h->plan[0][i].gemm.nprob > (int)h->probs.size()))
             return fail(h, "internal: GEMM problem table mismatch");
+    build_model_plan(h);
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
     h->bound = true;
@@ -860,6 +953,41 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
         }
     }
     h->seq_host += n_steps;
+    return 0;
+}
+
+int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t flags) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert (no world models)");
+    if (n_steps <= 0) return 0;
+    if (!idx) return fail(h, "null index array");
+    const int R2 = 2 * h->mb;
+    int32_t* ring = h->ptr<int32_t>("mfit.idx");
+    for (int64_t done = 0; done < n_steps;) {
+        const int64_t chunk = std::min<int64_t>(n_steps - done, h->mfit_cap);
+        HIPCHK(h, hipStreamSynchronize(h->stream));   // ring slots of earlier chunks are consumed
+        for (int64_t j = 0; j < chunk; ++j) {
+            const int64_t slot = (h->mfit_host + done + j) % h->mfit_cap;
+            HIPCHK(h, hipMemcpy(ring + slot * R2, idx + (done + j) * R2, sizeof(int32_t) * R2, hipMemcpyHostToDevice));
+        }
+        if (flags & SACX_STEP_EAGER) {
+            for (int64_t j = 0; j < chunk; ++j)
+                for (const Launch& L : h->mplan) enqueue(L, h, h->stream);
+            HIPCHK(h, hipGetLastError());
+        } else {
+            if (!h->mgraph) {
+                HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+                for (const Launch& L : h->mplan) enqueue(L, h, h->cap_stream);
+                hipGraph_t graph;
+                HIPCHK(h, hipStreamEndCapture(h->cap_stream, &graph));
+                HIPCHK(h, hipGraphInstantiateWithFlags(&h->mgraph, graph, 0));
+                HIPCHK(h, hipGraphDestroy(graph));
+            }
+            for (int64_t j = 0; j < chunk; ++j) HIPCHK(h, hipGraphLaunch(h->mgraph, h->stream));
+        }
+        done += chunk;
+    }
+    h->mfit_host += n_steps;
     return 0;
 }
 

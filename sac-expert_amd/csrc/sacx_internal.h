@@ -21,7 +21,8 @@ struct Ctl {
     int32_t red_counter[8]; // last-arriver tickets (self-resetting)
     float epsilon;          // expert weight
     float pad_f[3];
-    int64_t reserved[14];
+    int64_t mfit_seq;       // model-fit step sequence (index ring / stats)
+    int64_t reserved[13];
 };
 static_assert(sizeof(Ctl) <= 32 * 8, "ctl segment is 32 int64");
 
@@ -196,6 +197,29 @@ struct AppendArgs {
     Ctl* ctl;
 };
 
+// ---------------------------------------------------------------- world-model fitting
+struct MGatherArgs {        // rows [0, 2*mb): model k = row / mb
+    const float* replay; int64_t cap; int32_t stride;
+    int32_t S, A, mb;
+    const int32_t* idx_ring; int32_t idx_cap;   // [idx_cap, 2*mb] replay-logical rows
+    const Ctl* ctl;
+    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den)
+    float* X; int32_t ldQ;      // [2mb, ldQ] = [s_n | a_n | 0]
+    float* T;                   // [2mb, S+1] = [norm(sp - s) | norm(r)]
+};
+struct MLossArgs {
+    int32_t S, mb;
+    const float* T; const float* O;   // [2mb, S+1]
+    float* D3;                        // dL/dout [2mb, S+1]
+    float* loss_rows;                 // [2mb]
+    float reward_coef;
+};
+struct MFinalArgs {
+    Ctl* ctl;
+    const float* loss_rows; int32_t mb;
+    float* mstats; int32_t mstats_cap;
+};
+
 // launchers (defined in k_sac.hip)
 void launch_gemm(const GemmArgs& a, hipStream_t s);
 void launch_rng(const RngArgs& a, hipStream_t s);
@@ -204,6 +228,9 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s);
 void launch_qhead(const QHeadArgs& a, hipStream_t s);
 void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s);
 void launch_append(const AppendArgs& a, hipStream_t s);
+void launch_mgather(const MGatherArgs& a, hipStream_t s);
+void launch_mloss(const MLossArgs& a, hipStream_t s);
+void launch_mfinal(const MFinalArgs& a, hipStream_t s);
 void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s);
 
 }  // namespace sacx

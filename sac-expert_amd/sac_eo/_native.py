@@ -22,7 +22,7 @@ STAT_NAMES = ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss",
 EXPORTS = [
     "sacx_create", "sacx_destroy", "sacx_last_error", "sacx_arena_bytes", "sacx_layout", "sacx_bind",
     "sacx_buffer_append", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
-    "sacx_rng_get_state", "sacx_sac_step", "sacx_sync", "sacx_plan_info", "sacx_profile",
+    "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
 ]
 
 
@@ -111,6 +111,7 @@ def lib():
         "sacx_rng_set_state": (ctypes.c_int, [vp, vp, i32, i32, f64]),
         "sacx_rng_get_state": (ctypes.c_int, [vp, vp, P(i32), P(i32), P(f64)]),
         "sacx_sac_step": (ctypes.c_int, [vp, i64, i64, i32, i32]),
+        "sacx_model_fit": (ctypes.c_int, [vp, vp, i64, i32]),
         "sacx_sync": (ctypes.c_int, [vp]),
         "sacx_plan_info": (ctypes.c_int, [vp, P(LaunchInfo), i32, P(i32)]),
         "sacx_profile": (ctypes.c_int, [vp, i64, P(f64), i32]),
