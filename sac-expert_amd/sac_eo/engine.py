@@ -21,7 +21,7 @@ _ESZ = {0: 4, 1: 4, 2: 8, 3: 4, 4: 8}
 
 # ctl field indices (int64 slots, see csrc/sacx_internal.h struct Ctl)
 CTL = {"t_sac": 0, "t_model": 1, "num_timesteps": 2, "ts_increment": 3, "cur_size": 4, "start": 5,
-       "step_seq": 6, "n_expert": 7}
+       "step_seq": 6, "n_expert": 7, "mfit_seq": 14}
 
 
 @dataclasses.dataclass
@@ -245,6 +245,32 @@ class Engine:
         flags = (N.STEP_EXTERNAL_RANDOMS if external else 0) | (N.STEP_EAGER if eager else 0)
         N.check(self.lib.sacx_sac_step(self.h, int(n), int(num_timesteps), int(ts_increment), flags),
                 self.h, "sac_step")
+
+    def model_fit(self, idx: np.ndarray, eager: bool = False):
+        """``idx[n, 2, model_batch]``: replay-logical rows of each model's minibatch per step
+        (SAC_expert.py:519-543 -> _apply_model_grads)."""
+        idx = np.ascontiguousarray(idx, dtype=np.int32)
+        if idx.ndim != 3 or idx.shape[1] != 2 or idx.shape[2] != self.cfg.model_batch:
+            raise ValueError(f"idx must be [n, 2, {self.cfg.model_batch}]")
+        N.check(self.lib.sacx_model_fit(self.h, idx.ctypes.data, int(idx.shape[0]), N.STEP_EAGER if eager else 0),
+                self.h, "model_fit")
+
+    def model_stats(self, n_last: int) -> np.ndarray:
+        """Summed model loss of the last n_last fitting steps, oldest first."""
+        seq = self.ctl()["mfit_seq"]
+        cap = self.cfg.stats_capacity
+        st = self.v["mstats"].cpu().numpy()
+        return st[[(seq - n_last + i) % cap for i in range(n_last)], 0]
+
+    def reset_model_optimizer(self):
+        """--reset_model_optimizer (SAC_expert.py:553-555): fresh Adam state for the models."""
+        for net in ("m0", "m1"):
+            for i in range(3):
+                seg = self.segments[f"{net}.l{i}"]
+                o, n = seg["offset"] // 4, seg["rows"] * seg["cols"]
+                self.v["adam_m"][0, o:o + n] = 0
+                self.v["adam_v"][0, o:o + n] = 0
+        self.v["ctl"][0, CTL["t_model"]] = 0
 
     def sync(self):
         N.check(self.lib.sacx_sync(self.h), self.h, "sync")

@@ -203,3 +203,29 @@ def test_graph_equals_eager(gpu_available):
         eng.close()
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("eager", [True, False])
+def test_model_fit_matches_oracle(gpu_available, eager):
+    """World-model fitting steps (mbrl_onpolicy_alg.py:301-319) vs oracle.model_fit_step."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=31, use_expert=True, normalizers="random")
+    N = buf["r"].shape[0]
+    mb = eng.cfg.model_batch
+    rs = np.random.RandomState(9)
+    steps = 5
+    idx = rs.randint(N, size=(steps, 2, mb))
+    eng.model_fit(idx, eager=eager)
+    eng.sync()
+    dev = eng.model_stats(steps)
+    ref = []
+    for j in range(steps):
+        batches = [(buf["s"][idx[j, k]], buf["a"][idx[j, k]], buf["sp"][idx[j, k]], buf["r"][idx[j, k]])
+                   for k in range(2)]
+        ref.append(O.model_fit_step(st, ocfg, nrm, batches))
+    ref = np.array(ref)
+    assert np.max(np.abs(dev - ref) / np.abs(ref)) < 1e-4, (dev, ref)
+    for k in range(2):
+        for a_, b_ in zip(eng.get_net(f"m{k}"), st.models[k]):
+            assert np.max(np.abs(a_ - b_)) < 5e-5
+    assert eng.ctl()["t_model"] == steps
+    eng.close()
