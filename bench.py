@@ -55,7 +55,7 @@ def build_engine(cfgd, seed, device):
     S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
-                        expert_capacity=20, graph_steps=8)
+                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "8")))
     eng = Engine(ecfg, device=device)
     rng = np.random.default_rng(seed)
     eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))

@@ -32,12 +32,40 @@ typedef float floatx4 __attribute__((ext_vector_type(4)));
 #define SOFTPLUS_THR -0x1.be2804p+3f  // log(FLT_EPSILON) + 2 (TF softplus_op.h)
 
 // ------------------------------------------------------------------ helpers
+template <int ACT>
+__device__ __forceinline__ float act_t(float z) {
+    if constexpr (ACT == ACT_RELU) return z > 0.f ? z : 0.f;
+    else if constexpr (ACT == ACT_TANH) return tanhf(z);
+    else if constexpr (ACT == ACT_ELU) return z < 0.f ? expf(z) - 1.f : z;
+    else return z;
+}
+
 __device__ __forceinline__ float act_f(float z, int act) {
     switch (act) {
-        case ACT_RELU: return z > 0.f ? z : 0.f;
-        case ACT_TANH: return tanhf(z);
-        case ACT_ELU: return z < 0.f ? expf(z) - 1.f : z;
+        case ACT_RELU: return act_t<ACT_RELU>(z);
+        case ACT_TANH: return act_t<ACT_TANH>(z);
+        case ACT_ELU: return act_t<ACT_ELU>(z);
         default: return z;
+    }
+}
+
+// act over a whole register block under ONE wave-uniform branch
+template <int N>
+__device__ __forceinline__ void act_block(float (&h)[N], int act) {
+    switch (act) {
+        case ACT_RELU:
+#pragma unroll
+            for (int i = 0; i < N; ++i) h[i] = act_t<ACT_RELU>(h[i]);
+            break;
+        case ACT_TANH:
+#pragma unroll
+            for (int i = 0; i < N; ++i) h[i] = act_t<ACT_TANH>(h[i]);
+            break;
+        case ACT_ELU:
+#pragma unroll
+            for (int i = 0; i < N; ++i) h[i] = act_t<ACT_ELU>(h[i]);
+            break;
+        default: break;
     }
 }
 
@@ -100,101 +128,139 @@ __device__ __forceinline__ float adam_update(float* p, float* m, float* v, float
     return pn;
 }
 
+// Raw buffer loads.  Out-of-range elements get an offset past the resource's
+// num_records and the hardware returns 0, so every load is unconditional and no
+// select follows it (a select on a load result is turned back into a branch
+// around the load by the compiler, and a load under a branch ends in vmcnt(0)
+// at the block boundary).  Offsets are 32-bit: every tensor read this way is
+// < 2 GiB (the replay ring is read with global loads).
+#define SACX_BUF_OOB 0x80000000u
+#define SACX_RSRC_WORD3 0x00020000
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, (int)bytes, SACX_RSRC_WORD3);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+__device__ __forceinline__ float4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rs(const float* p) { return make_rsrc(p, p ? 0x7fffffffu : 0u); }
+// The empty asm hides the select from the optimiser, which would otherwise
+// split load(select(ok, off, OOB)) back into two loads under branches.
+__device__ __forceinline__ uint32_t boff(bool ok, int elem) {
+    uint32_t o = ok ? (uint32_t)elem * 4u : SACX_BUF_OOB;
+    asm("" : "+v"(o));
+    return o;
+}
+// wave index as a scalar (lets per-row pointers and branches stay in SGPRs)
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
+
 // ---------------------------------------------------------------- row helpers
 // A row of a hidden layer (width H <= 64*MAXQ) is held as hv[q] = h[lane + 64 q];
 // all loads of a row are issued before any reduction so the wave's memory
 // latency overlaps instead of serialising behind each butterfly.
 #define MAXQ 8
-__device__ __forceinline__ void load_row(const float* __restrict__ h, int H, float (&hv)[MAXQ]) {
+// hv[q] = h[base + lane + 64 q] (0 beyond H)
+__device__ __forceinline__ void load_row(__amdgpu_buffer_rsrc_t r, int base, int H, float (&hv)[MAXQ]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < MAXQ; ++q) {
         const int k = lane + 64 * q;
-        hv[q] = (k < H) ? h[k] : 0.f;
+        hv[q] = bload(r, boff(k < H, base + k));
     }
 }
 
-// out[u] = sum_k hv(k) * W[k*ldw + o0 + u] for u < 8 (o0+u < O); broadcast to all lanes
-__device__ __forceinline__ void rowdot8(const float (&hv)[MAXQ], const float* __restrict__ W, int H, int ldw,
+// out[u] = sum_k hv(k) * W[k*ldw + o0 + u] for u < 8 (0 for o0+u >= O); broadcast to all lanes.
+__device__ __forceinline__ void rowdot8(const float (&hv)[MAXQ], __amdgpu_buffer_rsrc_t rW, int H, int ldw,
                                         int o0, int O, float (&out)[8]) {
     const int lane = threadIdx.x & 63;
-    float p[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) p[u] = 0.f;
+    float w[MAXQ][8];
 #pragma unroll
     for (int q = 0; q < MAXQ; ++q) {
         const int k = lane + 64 * q;
-        if (k < H) {
-            const float* wr = W + (size_t)k * ldw + o0;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (o0 + u < O) p[u] = fmaf(hv[q], wr[u], p[u]);
-        }
+        for (int u = 0; u < 8; ++u) w[q][u] = bload(rW, boff(k < H && o0 + u < O, k * ldw + o0 + u));
+    }
+    float p[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        p[u] = 0.f;
+#pragma unroll
+        for (int q = 0; q < MAXQ; ++q) p[u] = fmaf(hv[q], w[q][u], p[u]);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) out[u] = wave_sum(p[u]);
 }
 
 // ==================================================================== k_gemm
-__device__ __forceinline__ void load_a(const GemmProb& g, int m, bool mok, int k0, bool vec, float (&a)[4]) {
-    if (g.a_kc) {
-        if (mok) {
-            const float* src = g.A + (size_t)m * g.lda + k0;
-            if (vec && k0 + 3 < g.K) {
-                const float4 v = *reinterpret_cast<const float4*>(src);
-                a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) a[j] = (k0 + j < g.K) ? src[j] : 0.f;
-            }
+template <bool KC, bool VEC>
+__device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t ra, const GemmProb& g, int m, bool mok, int k0,
+                                       float (&a)[4]) {
+    if constexpr (KC) {
+        if constexpr (VEC) {
+            const uint32_t off = boff(mok && k0 < g.K, m * g.lda + k0);
+            const float4 v = bload4(ra, off);
+            a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] = 0.f;
+            for (int j = 0; j < 4; ++j) {
+                const int k = k0 + j;
+                a[j] = bload(ra, boff(mok && k < g.K, m * g.lda + k));
+            }
         }
     } else {
-        const bool ones = (m == g.ones_row);
+        // A[m][k] = X[k][m]; logical row ones_row is all ones (bias-gradient row)
+        const float one = (m == g.ones_row) ? 1.f : 0.f;
+        const bool rd = mok && (m != g.ones_row);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int k = k0 + j;
-            float x = 0.f;
-            if (mok && k < g.K) x = ones ? 1.f : g.A[(size_t)k * g.lda + m];
-            a[j] = x;
+            const bool kok = k < g.K;
+            a[j] = bload(ra, boff(rd && kok, k * g.lda + m)) + (kok ? one : 0.f);
         }
     }
 }
 
-__device__ __forceinline__ void load_b(const GemmProb& g, int n, bool nok, int k0, bool vec, float (&b)[4]) {
-    if (g.b_kc) {
-        if (nok) {
-            const float* src = g.B + (size_t)n * g.ldb + k0;
-            if (vec && k0 + 3 < g.K) {
-                const float4 v = *reinterpret_cast<const float4*>(src);
-                b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) b[j] = (k0 + j < g.K) ? src[j] : 0.f;
-            }
+template <bool KC, bool VEC>
+__device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb& g, int n, bool nok, int k0,
+                                       float (&b)[4]) {
+    if constexpr (KC) {
+        if constexpr (VEC) {
+            const uint32_t off = boff(nok && k0 < g.K, n * g.ldb + k0);
+            const float4 v = bload4(rb, off);
+            b[0] = v.x; b[1] = v.y; b[2] = v.z; b[3] = v.w;
         } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = 0.f;
+            for (int j = 0; j < 4; ++j) {
+                const int k = k0 + j;
+                b[j] = bload(rb, boff(nok && k < g.K, n * g.ldb + k));
+            }
         }
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int k = k0 + j;
-            b[j] = (nok && k < g.K) ? g.B[(size_t)k * g.ldb + n] : 0.f;
+            b[j] = bload(rb, boff(nok && k < g.K, k * g.ldb + n));
         }
     }
 }
 
+// MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
+// act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
+template <int MODE, int VEC>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
+    constexpr bool AKC = (MODE != GM_DW);
+    constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
     const int tile = blockIdx.x;
     int p = 0;
 #pragma unroll
     for (int i = 1; i < GEMM_MAXP; ++i)
         if (i < ga.nprob && tile >= ga.probs[i].tile_begin) p = i;
-    const GemmProb& g = ga.probs[p];
+    const GemmProb g = ga.probs[p];   // by value: every field loads once, up front (speculatable)
     const int lt = tile - g.tile_begin;
     const int tm = lt / g.tiles_n;
     const int tn = lt - tm * g.tiles_n;
@@ -202,27 +268,24 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int r = lane & 15, grp = lane >> 4;
 
-    // ---- epilogue operands first: this thread's output element is known now,
-    //      so its loads overlap the operand loads instead of following the MFMAs
+    // ---- epilogue operands first (this thread's output element is known now)
     const int t = threadIdx.x;
     const int row = t >> 4, col = t & 15;
     const int mm = m0 + row, nn = n0 + col;
     const bool out_ok = (mm < g.M) && (nn < g.N);
-    const int epi = g.epi;
+    const int mmc = min(mm, g.M - 1), nnc = min(nn, g.N - 1);
     float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
-    size_t pidx = 0;
-    if (out_ok) {
-        if (epi == EPI_FWD) {
-            e0 = g.bias[nn];
-        } else if (epi == EPI_DACT) {
-            e0 = g.H[(size_t)mm * g.ldh + nn];
-        } else if (epi == EPI_ADAM) {
-            pidx = (size_t)mm * g.ldp + nn;
-            e0 = g.P[pidx];
-            e1 = g.P[pidx + ga.p_stride];
-            e2 = g.P[pidx + 2 * ga.p_stride];
-            if (g.T != nullptr) e3 = g.T[pidx];
-        }
+    const size_t pidx = (size_t)mmc * g.ldp + nnc;
+    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+        e0 = g.bias[nnc];
+    } else if constexpr (MODE == GM_DX) {
+        e0 = g.H[(size_t)mmc * g.ldh + nnc];
+    } else {
+        e0 = g.P[pidx];
+        e1 = g.P[pidx + ga.p_stride];
+        e2 = g.P[pidx + 2 * ga.p_stride];
+        // no target: a zero-sized resource reads 0 without a branch
+        e3 = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
     }
 
     const int nIt = (g.K + 15) >> 4;
@@ -231,24 +294,91 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const int it1 = min(nIt, it0 + per);
     const int m = m0 + r, n = n0 + r;
     const bool mok = m < g.M, nok = n < g.N;
-    const bool avec = g.a_kc && ((g.lda & 3) == 0) && ((((uintptr_t)g.A) & 15) == 0);
-    const bool bvec = g.b_kc && ((g.ldb & 3) == 0) && ((((uintptr_t)g.B) & 15) == 0);
 
+    // operand extents in bytes (offsets are 32-bit: every operand < 2 GiB, checked on the host)
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B, 0x7fffffffu);
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
     floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
-    for (int it = it0; it < it1; it += 4) {
+    if constexpr (MODE == GM_FWD2) {
+        // layer 0 per 16-wide hidden chunk hb: D' = W0^T[hb.., :] X^T[:, m0..] leaves lane
+        // (r, grp) holding H1[m0+r][hb+4grp+v] in register v -- exactly the A operand of the
+        // layer-1 MFMA v with k = hb+4grp+v, so H1 never leaves registers.
+        constexpr int NK0 = VEC;   // layer-0 K steps of 4, rounded up to even (host-checked)
+        const int H0 = g.K;
+        const __amdgpu_buffer_rsrc_t rw0 = make_rsrc(g.W0, 0x7fffffffu);
+        float xv[NK0];
+#pragma unroll
+        for (int s = 0; s < NK0; ++s) {
+            const int k = 4 * s + grp;
+            xv[s] = bload(ra, boff(mok && k < g.K0, m * g.lda + k));
+        }
+        const bool store_h1 = (tn == 0) && mok;
+        // groups of 4 chunks, every load of a group issued before its first MFMA
+        // (a loop-carried register copy would force vmcnt(0) per chunk)
+        for (int c0 = it0; c0 < it1; c0 += 4) {
+            float w0v[4][NK0], b0v[4][4], w1v[4][4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int it = c0 + c;
+                const int hb = it * 16;
+                const bool hok = (it < it1) && (hb + r < H0);
+#pragma unroll
+                for (int s = 0; s < NK0; ++s) {
+                    const int k = 4 * s + grp;
+                    w0v[c][s] = bload(rw0, boff(hok && k < g.K0, k * H0 + hb + r));
+                }
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    const int hk = hb + 4 * grp + v;
+                    const bool kok = (it < it1) && (hk < H0);
+                    b0v[c][v] = bload(rw0, boff(kok, g.K0 * H0 + hk));
+                    w1v[c][v] = bload(rb, boff(kok && nok, hk * g.ldb + n));
+                }
+            }
+            __builtin_amdgcn_sched_barrier(0);   // all loads of the group in flight before any MFMA
+            floatx4 d[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[c] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int s = 0; s < NK0; ++s)
+#pragma unroll
+                for (int c = 0; c < 4; ++c) d[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0v[c][s], xv[s], d[c], 0, 0, 0);
+            float hh[16];
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+#pragma unroll
+                for (int v = 0; v < 4; ++v) hh[4 * c + v] = d[c][v] + b0v[c][v];
+            act_block(hh, g.act);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const int it = c0 + c;
+                const float h[4] = {hh[4 * c], hh[4 * c + 1], hh[4 * c + 2], hh[4 * c + 3]};
+                if (store_h1 && it < it1) {
+                    const int hk = it * 16 + 4 * grp;
+#pragma unroll
+                    for (int v = 0; v < 4; ++v)
+                        if (hk + v < H0) g.C0[(size_t)m * H0 + hk + v] = h[v];
+                }
+                // chunks past it1 have w1 = 0: they add exact zeros
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[0], w1v[c][0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[1], w1v[c][1], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[2], w1v[c][2], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[3], w1v[c][3], acc1, 0, 0, 0);
+            }
+        }
+    }
+    for (int it = it0; MODE != GM_FWD2 && it < it1; it += 4) {
         float a[4][4], b[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if (it + u < it1) {
-                const int k0 = (it + u) * 16 + grp * 4;
-                load_a(g, m, mok, k0, avec, a[u]);
-                load_b(g, n, nok, k0, bvec, b[u]);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) { a[u][j] = 0.f; b[u][j] = 0.f; }
-            }
+            // iterations past it1 read a clamped (valid) slab and are zeroed
+            const int k0 = (it + u) * 16 + grp * 4;
+            const int k0e = (it + u < it1) ? k0 : (1 << 30);
+            load_a<AKC, VEC && AKC>(ra, g, m, mok, k0e, a[u]);
+            load_b<BKC, VEC && BKC>(rb, g, n, nok, k0e, b[u]);
         }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
@@ -268,39 +398,55 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     v = v + red[2][R][L];
     v = v + red[3][R][L];
     if (!out_ok) return;
-    switch (epi) {
-        case EPI_FWD:
-            g.C[(size_t)mm * g.ldc + nn] = act_f(v + e0, g.act);
-            break;
-        case EPI_DACT:
-            g.C[(size_t)mm * g.ldc + nn] = v * dact_f(e0, g.act);
-            break;
-        case EPI_STORE:
-            g.C[(size_t)mm * g.ldc + nn] = v;
-            break;
-        case EPI_ADAM: {
-            const Ctl* ctl = ga.ctl;
-            const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
-            const float lr_t = adam_lr(ga.adam, g.group, tstep);
-            const float gr = v * g.grad_scale;
-            const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
-            const float mm1 = e1 + (gr - e1) * (1.f - b1);
-            const float vv1 = e2 + (gr * gr - e2) * (1.f - b2);
-            const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
-            g.P[pidx] = pn;
-            g.P[pidx + ga.p_stride] = mm1;
-            g.P[pidx + 2 * ga.p_stride] = vv1;
-            if (g.T != nullptr) {
-                const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-                if (ctl->num_timesteps % tui == 0) g.T[pidx] = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
-            }
-            break;
+    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+        g.C[(size_t)mm * g.ldc + nn] = act_f(v + e0, g.act);
+    } else if constexpr (MODE == GM_DX) {
+        g.C[(size_t)mm * g.ldc + nn] = v * dact_f(e0, g.act);
+    } else {
+        const Ctl* ctl = ga.ctl;
+        const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
+        const float lr_t = adam_lr(ga.adam, g.group, tstep);
+        const float gr = v * g.grad_scale;
+        const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+        const float mm1 = e1 + (gr - e1) * (1.f - b1);
+        const float vv1 = e2 + (gr * gr - e2) * (1.f - b2);
+        const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
+        g.P[pidx] = pn;
+        g.P[pidx + ga.p_stride] = mm1;
+        g.P[pidx + 2 * ga.p_stride] = vv1;
+        if (g.T != nullptr) {
+            const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
+            if (ctl->num_timesteps % tui == 0) g.T[pidx] = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
         }
     }
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_gemm, dim3(a.total_tiles), dim3(256), 0, s, a);
+    const dim3 grid(a.total_tiles), block(256);
+    switch (a.mode) {
+    case GM_FWD:
+        if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_gemm<GM_FWD, 0>), grid, block, 0, s, a);
+        break;
+    case GM_DX:
+        if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_gemm<GM_DX, 0>), grid, block, 0, s, a);
+        break;
+    case GM_FWD2:
+        switch (a.vec) {
+        case 2: hipLaunchKernelGGL((k_gemm<GM_FWD2, 2>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gemm<GM_FWD2, 4>), grid, block, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_gemm<GM_FWD2, 6>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((k_gemm<GM_FWD2, 8>), grid, block, 0, s, a); break;
+        case 10: hipLaunchKernelGGL((k_gemm<GM_FWD2, 10>), grid, block, 0, s, a); break;
+        case 12: hipLaunchKernelGGL((k_gemm<GM_FWD2, 12>), grid, block, 0, s, a); break;
+        case 14: hipLaunchKernelGGL((k_gemm<GM_FWD2, 14>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_gemm<GM_FWD2, 16>), grid, block, 0, s, a); break;
+        }
+        break;
+    default:
+        hipLaunchKernelGGL((k_gemm<GM_DW, 0>), grid, block, 0, s, a);
+    }
 }
 
 // ==================================================================== k_rng
@@ -499,6 +645,10 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
         a.st->pos = pos;
         a.st->has_gauss = sh_has;
         a.st->gauss = sh_gauss;
+        // the update these randoms belong to (the sampler runs ahead of the updates)
+        const int64_t seq = a.reset_seq ? a.ctl->step_seq : a.ctl->rng_seq;
+        a.ctl->pseq[a.slot] = seq;
+        a.ctl->rng_seq = seq + 1;
     }
 }
 
@@ -509,54 +659,56 @@ void launch_rng(const RngArgs& a, hipStream_t s) {
 // ==================================================================== k_gather
 // one wave per sampled row (then per expert row); rows are [s | a | sp | r | d]
 __global__ __launch_bounds__(256) void k_gather(GatherArgs g) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int S = g.S, A = g.A;
+    const __amdgpu_buffer_rsrc_t rsm = rs(g.s_mean), rsd = rs(g.s_den), ram = rs(g.a_mean), rad = rs(g.a_den);
     if (row < g.B) {
         const int64_t li = g.idx[row];
         const int64_t phys = (g.ctl->start + li) % g.cap;
-        const float* rec = g.replay + phys * (int64_t)g.stride;
+        // resource based at the record: the ring itself may exceed 32-bit offsets
+        const __amdgpu_buffer_rsrc_t rR = make_rsrc(g.replay + phys * (int64_t)g.stride, (uint32_t)g.stride * 4u);
+        const float r_v = bload(rR, (uint32_t)(2 * S + A) * 4u);
+        const float d_v = bload(rR, (uint32_t)(2 * S + A + 1) * 4u);
         for (int c = lane; c < g.ldQ; c += 64) {
-            float sn = 0.f, spn = 0.f, an = 0.f;
-            if (c < S) {
-                sn = (rec[c] - g.s_mean[c]) / g.s_den[c];
-                spn = (rec[S + A + c] - g.s_mean[c]) / g.s_den[c];
-            } else if (c < S + A) {
-                an = (rec[c] - g.a_mean[c - S]) / g.a_den[c - S];
-            }
+            const bool cs = c < S, ca = c >= S && c < S + A;
+            const float xs = bload(rR, boff(cs, c)), xsp = bload(rR, boff(cs, S + A + c));
+            const float xa = bload(rR, boff(ca, c));
+            const float ms = bload(rsm, boff(cs, c)), ds = bload(rsd, boff(cs, c));
+            const float ma = bload(ram, boff(ca, c - S)), da = bload(rad, boff(ca, c - S));
+            const float sn = cs ? (xs - ms) / ds : 0.f;
+            const float spn = cs ? (xsp - ms) / ds : 0.f;
+            const float an = ca ? (xa - ma) / da : 0.f;
             if (c < g.ldS) {
                 g.Xa[(size_t)row * g.ldS + c] = spn;
                 g.Xa[(size_t)(g.B + row) * g.ldS + c] = sn;
             }
-            g.Xq[(size_t)row * g.ldQ + c] = (c < S) ? sn : an;
-            if (c < S) {
+            g.Xq[(size_t)row * g.ldQ + c] = cs ? sn : an;
+            if (!ca) {
                 g.Xt[(size_t)row * g.ldQ + c] = spn;
                 g.Xp[(size_t)row * g.ldQ + c] = sn;
-            } else if (c >= S + A) {
-                g.Xt[(size_t)row * g.ldQ + c] = 0.f;
-                g.Xp[(size_t)row * g.ldQ + c] = 0.f;
             }
         }
         if (lane == 0) {
-            g.r[row] = rec[2 * S + A];
-            g.d[row] = rec[2 * S + A + 1];
+            g.r[row] = r_v;
+            g.d[row] = d_v;
         }
     } else if (row < g.B + g.ne) {
         const int e = row - g.B;
-        const int64_t slot = g.ctl->step_seq % g.perm_cap;
+        const int64_t slot = g.ctl->pseq[g.slot] % g.perm_cap;
         const int src = g.perm_ring[slot * g.ne + e];
-        const float* s_e = g.exp_s + (size_t)src * S;
-        const float* sp_e = g.exp_sp + (size_t)src * S;
+        const __amdgpu_buffer_rsrc_t rse = rs(g.exp_s + (size_t)src * S), rspe = rs(g.exp_sp + (size_t)src * S);
         for (int c = lane; c < g.ldQ; c += 64) {
-            float sn = 0.f;
-            if (c < S) {
-                sn = (s_e[c] - g.s_mean[c]) / g.s_den[c];
-                g.se_raw[(size_t)e * S + c] = s_e[c];
-                g.spe_raw[(size_t)e * S + c] = sp_e[c];
+            const bool cs = c < S;
+            const float xs = bload(rse, boff(cs, c)), xsp = bload(rspe, boff(cs, c));
+            const float ms = bload(rsm, boff(cs, c)), ds = bload(rsd, boff(cs, c));
+            const float sn = cs ? (xs - ms) / ds : 0.f;
+            if (cs) {
+                g.se_raw[(size_t)e * S + c] = xs;
+                g.spe_raw[(size_t)e * S + c] = xsp;
             }
             if (c < g.ldS) g.Xa[(size_t)(2 * g.B + e) * g.ldS + c] = sn;
-            if (c < S) g.Xm[(size_t)e * g.ldQ + c] = sn;
-            else if (c >= S + A) g.Xm[(size_t)e * g.ldQ + c] = 0.f;
+            if (c < S || c >= S + A) g.Xm[(size_t)e * g.ldQ + c] = sn;
         }
     }
 }
@@ -567,7 +719,7 @@ void launch_gather(const GatherArgs& a, hipStream_t s) {
 }
 
 // ==================================================================== finalize
-// alpha Adam + clamp and the per-update statistics (last-arriving workgroup).
+// alpha Adam + clamp and the per-update statistics.
 __device__ float mean_rows(const float* x, int n) {
     // deterministic: lane-strided partials then butterfly (wave 0 only)
     const int lane = threadIdx.x & 63;
@@ -576,8 +728,7 @@ __device__ float mean_rows(const float* x, int n) {
     return wave_sum(s) / (float)n;
 }
 
-__device__ void finalize_update(const FinalArgs& f, int nred, float nlp_sum_total_unused) {
-    (void)nlp_sum_total_unused;
+__device__ void finalize_update(const FinalArgs& f, int nred) {
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x & 63;
     float s = 0.f;
@@ -621,13 +772,19 @@ __device__ void finalize_update(const FinalArgs& f, int nred, float nlp_sum_tota
     }
 }
 
+// one wave: alpha Adam + clamp and the statistics row of the update
+__global__ __launch_bounds__(64) void k_alpha_final(FinalArgs f) { finalize_update(f, f.nred); }
+
+void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
+    hipLaunchKernelGGL(k_alpha_final, dim3(1), dim3(64), 0, s, f);
+}
+
 // ==================================================================== k_actor_head
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
 __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     __shared__ float red_s[4];
-    __shared__ int last_s;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     float row_ent = 0.f;
     if (row < h.total_rows) {
@@ -635,34 +792,34 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         for (int i = 1; i < h.nseg; ++i)
             if (row >= h.seg[i].r0) sidx = i;
         const HeadSeg sg = h.seg[sidx];
+        const int A = h.A, Aout = h.Aout;
+        const bool jok = lane < A;
+        // everything this row reads is issued up front
         float hv[MAXQ];
-        load_row(h.H2 + (size_t)row * h.ldh, h.H1, hv);
-        float u_pf = 0.f, ls_pf = 0.f, am_pf = 0.f, ad_pf = 1.f;
-        if (lane < h.A) {
-            u_pf = sg.noise[(size_t)(row - sg.r0) * h.A + lane];
-            if (!h.per_state_std) ls_pf = h.logstd[lane];
-            am_pf = h.a_mean[lane];
-            ad_pf = h.a_den[lane];
-        }
-        const float* bias = h.W3 + (size_t)h.H1 * h.Aout;
+        load_row(rs(h.H2), row * h.ldh, h.H1, hv);
+        const __amdgpu_buffer_rsrc_t rW = rs(h.W3);
+        const float u_pf = bload(rs(sg.noise), boff(jok, (row - sg.r0) * A + lane));
+        const float ls_pf = bload(rs(h.logstd), boff(jok && !h.per_state_std, lane));
+        const float am_pf = bload(rs(h.a_mean), boff(jok, lane));
+        const float ad_pf = bload(rs(h.a_den), boff(jok, lane));
+        const float bmu = bload(rW, boff(jok, h.H1 * Aout + lane));
+        const float bls = bload(rW, boff(jok && h.per_state_std, h.H1 * Aout + A + lane));
         float mu = 0.f, lraw = 0.f;
-        for (int o0 = 0; o0 < h.Aout; o0 += 8) {
+        for (int o0 = 0; o0 < Aout; o0 += 8) {
             float s8[8];
-            rowdot8(hv, h.W3, h.H1, h.Aout, o0, h.Aout, s8);
+            rowdot8(hv, rW, h.H1, Aout, o0, Aout, s8);
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
                 const int o = o0 + u;
-                if (o < h.Aout) {
-                    const float sv = s8[u] + bias[o];
-                    if (lane == o) mu = sv;
-                    if (h.per_state_std && lane + h.A == o) lraw = sv;
-                }
+                mu = (lane == o) ? s8[u] : mu;
+                lraw = (lane + A == o) ? s8[u] : lraw;
             }
         }
+        mu = mu + bmu;
+        lraw = h.per_state_std ? lraw + bls : ls_pf;
         float nlp_vec = 0.f, nlp_corr = 0.f;
-        if (lane < h.A) {
+        if (jok) {
             const int j = lane;
-            if (!h.per_state_std) lraw = ls_pf;
             const float l = fminf(fmaxf(lraw, -5.f), 2.f);
             const float sd = expf(l);
             const float u = u_pf;
@@ -677,7 +834,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
             if (sg.xq_out != nullptr)
                 sg.xq_out[(size_t)(sg.xq_row0 + row - sg.r0) * h.ldQ + h.S + j] = (pi - am_pf) / ad_pf;
             if (row >= h.cache_row0 && h.c_t != nullptr) {
-                const size_t ci = (size_t)(row - h.cache_row0) * h.A + j;
+                const size_t ci = (size_t)(row - h.cache_row0) * A + j;
                 h.c_t[ci] = t;
                 h.c_std[ci] = sd;
                 h.c_u[ci] = u;
@@ -691,7 +848,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         }
     }
     if (!h.alpha_mode) return;
-    // ---- alpha: block partial of sum(-nlp + H), then the last arriver finalises
+    // ---- alpha: block partial of sum(-nlp + H); k_alpha_final reduces them
     if (lane == 0) red_s[wave] = row_ent;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -699,20 +856,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         part = part + red_s[2];
         part = part + red_s[3];
         f.red[blockIdx.x] = part;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int tk = __hip_atomic_fetch_add(&f.ctl->red_counter[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int is_last = (tk == (int)gridDim.x - 1);
-        if (is_last) {
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(&f.ctl->red_counter[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        last_s = is_last;
     }
-    __syncthreads();
-    if (!last_s) return;
-    finalize_update(f, (int)gridDim.x, 0.f);
 }
 
 void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
@@ -723,7 +867,7 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
 template <int MODE>
 __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
     __shared__ float buf[4][512];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = q.B, H1 = q.H1;
     if (row < B) {
@@ -738,28 +882,25 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
         }
         float hv[4][MAXQ];
         float wv[4][MAXQ];
+        float bias[4];
+        const __amdgpu_buffer_rsrc_t rH = rs(q.H2);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (k < nnet) {
-                load_row(q.H2 + ((size_t)k * B + row) * H1, H1, hv[k]);
-                load_row(q.W3[k], H1, wv[k]);
-            }
+        for (int k = 0; k < nnet; ++k) {
+            load_row(rH, (k * B + row) * H1, H1, hv[k]);
+            const __amdgpu_buffer_rsrc_t rW = rs(q.W3[k]);
+            load_row(rW, 0, H1, wv[k]);
+            bias[k] = bload(rW, (uint32_t)H1 * 4u);
         }
         float out[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
+        for (int k = 0; k < nnet; ++k) {
             float p = 0.f;
-            if (k < nnet) {
 #pragma unroll
-                for (int i = 0; i < MAXQ; ++i) p = fmaf(hv[k][i], wv[k][i], p);
-            }
-            out[k] = wave_sum(p);
+            for (int i = 0; i < MAXQ; ++i) p = fmaf(hv[k][i], wv[k][i], p);
+            out[k] = wave_sum(p) + bias[k];
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            if (k < nnet) out[k] = out[k] + q.W3[k][H1];
         float g0, g1;
-        if (MODE == 0) {
+        if constexpr (MODE == 0) {
             const float v0 = out[0] * rd, v1 = out[1] * rd;
             const float nv = fminf(v0, v1) + alpha * nlp_r;
             const float y = r_r + q.gamma * ((1.f - d_r) * nv);
@@ -784,19 +925,15 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
             g1 = gmin * s1;
         }
         // differentiated nets: slabs 2,3 (mode 0) or 0,1 (mode 1)
-        constexpr int dn0 = MODE == 0 ? 2 : 0;
+        constexpr int dn = MODE == 0 ? 2 : 0;
         float* d0 = q.D2 + (size_t)row * H1;
         float* d1 = q.D2 + ((size_t)B + row) * H1;
 #pragma unroll
         for (int i = 0; i < MAXQ; ++i) {
             const int k = lane + 64 * i;
             if (k < H1) {
-                const float a0 = dn0 == 2 ? hv[2][i] : hv[0][i];
-                const float a1 = dn0 == 2 ? hv[3][i] : hv[1][i];
-                const float w0 = dn0 == 2 ? wv[2][i] : wv[0][i];
-                const float w1 = dn0 == 2 ? wv[3][i] : wv[1][i];
-                d0[k] = (g0 * w0) * dact_f(a0, q.act);
-                d1[k] = (g1 * w1) * dact_f(a1, q.act);
+                d0[k] = (g0 * wv[dn][i]) * dact_f(hv[dn][i], q.act);
+                d1[k] = (g1 * wv[dn + 1][i]) * dact_f(hv[dn + 1][i], q.act);
             }
         }
         return;
@@ -807,14 +944,17 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
     const int half = q.ne / 2;
     const int k = e < half ? 0 : 1;
     const int S = q.S, Hm = q.Hm1, O = S + 1;
-    const float* hr = q.Hm2 + (size_t)e * Hm;
-    const float* W = k ? q.Wm3[1] : q.Wm3[0];
+    const __amdgpu_buffer_rsrc_t rW = rs(k ? q.Wm3[1] : q.Wm3[0]);
+    float hv[MAXQ];
+    load_row(rs(q.Hm2), e * Hm, Hm, hv);
     float* ob = buf[wave];
-    for (int j = 0; j < S; ++j) {
-        float p = 0.f;
-        for (int i = lane; i < Hm; i += 64) p = fmaf(hr[i], W[(size_t)i * O + j], p);
-        const float s = wave_sum(p);
-        if (lane == 0) ob[j] = s + W[(size_t)Hm * O + j];
+    for (int j0 = 0; j0 < S; j0 += 8) {
+        float s8[8];
+        rowdot8(hv, rW, Hm, O, j0, S, s8);
+        const float bj = bload(rW, boff(j0 + lane < S, Hm * O + j0 + lane));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (lane == u && j0 + u < S) ob[j0 + u] = s8[u] + bj;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -831,10 +971,29 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
     if (lane == 0) q.mse_rows[e] = tot;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    for (int i = lane; i < Hm; i += 64) {
-        float p = 0.f;
-        for (int j = 0; j < S; ++j) p = fmaf(ob[j], W[(size_t)i * O + j], p);
-        q.Dm2[(size_t)e * Hm + i] = p * dact_f(hr[i], q.mact);
+    // Dm2[e][i] = (sum_j ob[j] W[i][j]) * act'(h[i]); j in ascending order, 8 loads in flight
+    float pacc[MAXQ];
+#pragma unroll
+    for (int qq = 0; qq < MAXQ; ++qq) pacc[qq] = 0.f;
+    for (int j0 = 0; j0 < S; j0 += 8) {
+        float w[MAXQ][8];
+#pragma unroll
+        for (int qq = 0; qq < MAXQ; ++qq) {
+            const int i = lane + 64 * qq;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[qq][u] = bload(rW, boff(i < Hm && j0 + u < S, i * O + j0 + u));
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float ou = ob[min(j0 + u, S - 1)];
+#pragma unroll
+            for (int qq = 0; qq < MAXQ; ++qq) pacc[qq] = (j0 + u < S) ? fmaf(ou, w[qq][u], pacc[qq]) : pacc[qq];
+        }
+    }
+#pragma unroll
+    for (int qq = 0; qq < MAXQ; ++qq) {
+        const int i = lane + 64 * qq;
+        if (i < Hm) q.Dm2[(size_t)e * Hm + i] = pacc[qq] * dact_f(hv[qq], q.mact);
     }
 }
 
@@ -850,74 +1009,68 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 // (SURVEY.md §8a A5), then the Dense(H1 -> Aout) backward with the activation
 // derivative.  Per-column values live in lane j and are broadcast by shuffles.
 __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = b.B, S = b.S, A = b.A;
     if (row >= B + b.ne) return;
     const bool pol = row < B;
+    const bool jok = lane < A;
     const float eps = b.use_expert ? b.ctl->epsilon : 0.f;
     const float alpha = *b.alpha;
-    float t_pf = 0.f, sd_pf = 0.f, u_pf = 0.f, mk_pf = 0.f;
-    if (lane < A) {
-        const size_t ci = (size_t)row * A + lane;
-        t_pf = b.c_t[ci];
-        sd_pf = b.c_std[ci];
-        u_pf = b.c_u[ci];
-        mk_pf = b.c_mask[ci];
-    }
+    const int ci = row * A + lane;
+    const float t_pf = bload(rs(b.c_t), boff(jok, ci));
+    const float sd_pf = bload(rs(b.c_std), boff(jok, ci));
+    const float u_pf = bload(rs(b.c_u), boff(jok, ci));
+    const float mk_pf = bload(rs(b.c_mask), boff(jok, ci));
+    const float ad_pf = bload(rs(b.a_den), boff(jok, lane));
     float h2v[MAXQ];
-    load_row(b.Ha2 + (size_t)row * b.H1, b.H1, h2v);
+    load_row(rs(b.Ha2), row * b.H1, b.H1, h2v);
     const float w_sac = 1.f - eps;
     const float c = -w_sac * alpha * (1.f / (float)B);
     // action gradient: ga_j = sum over the input rows S+j of W1 of the row's layer-1 delta
-    float ga = 0.f;
+    // (policy rows: both critics' deltas; expert rows: its world model's delta, no second term)
+    const int e = row - B;
+    const int km = e < b.ne / 2 ? 0 : 1;
+    const int Hd = pol ? b.H0 : b.Hm0;
     float dv0[MAXQ], dv1[MAXQ];
-    const float* Wa;
-    const float* Wb;
-    int Hd;
-    if (pol) {
-        Hd = b.H0;
-        load_row(b.Dp1 + (size_t)row * b.H0, Hd, dv0);
-        load_row(b.Dp1 + ((size_t)B + row) * b.H0, Hd, dv1);
-        Wa = b.Wq1[0];
-        Wb = b.Wq1[1];
-    } else {
-        const int e = row - B;
-        const int k = e < b.ne / 2 ? 0 : 1;
-        Hd = b.Hm0;
-        load_row(b.Dm1 + (size_t)e * b.Hm0, Hd, dv0);
-#pragma unroll
-        for (int i = 0; i < MAXQ; ++i) dv1[i] = 0.f;
-        Wa = b.Wm1[k];
-        Wb = b.Wm1[k];
-    }
+    load_row(rs(pol ? b.Dp1 : b.Dm1), pol ? row * b.H0 : e * b.Hm0, Hd, dv0);
+    load_row(rs(b.Dp1), (B + row) * b.H0, pol ? Hd : 0, dv1);
+    const __amdgpu_buffer_rsrc_t rWa = rs(pol ? b.Wq1[0] : b.Wm1[km]);
+    const __amdgpu_buffer_rsrc_t rWb = rs(b.Wq1[1]);
+    const int Hb = pol ? Hd : 0;
+    float ga = 0.f;
     for (int j0 = 0; j0 < A; j0 += 8) {
+        float w0[8][MAXQ], w1[8][MAXQ];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const bool uok = j0 + u < A;
+            const int jr = S + j0 + u;
+#pragma unroll
+            for (int i = 0; i < MAXQ; ++i) {
+                const int k = lane + 64 * i;
+                w0[u][i] = bload(rWa, boff(uok && k < Hd, jr * Hd + k));
+                w1[u][i] = bload(rWb, boff(uok && k < Hb, jr * Hd + k));
+            }
+        }
         float p[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             p[u] = 0.f;
-            if (j0 + u < A) {
-                const float* wa = Wa + (size_t)(S + j0 + u) * Hd;
-                const float* wb = Wb + (size_t)(S + j0 + u) * Hd;
 #pragma unroll
-                for (int i = 0; i < MAXQ; ++i) {
-                    const int k = lane + 64 * i;
-                    if (k < Hd) {
-                        p[u] = fmaf(dv0[i], wa[k], p[u]);
-                        if (pol) p[u] = fmaf(dv1[i], wb[k], p[u]);
-                    }
-                }
+            for (int i = 0; i < MAXQ; ++i) {
+                p[u] = fmaf(dv0[i], w0[u][i], p[u]);
+                p[u] = fmaf(dv1[i], w1[u][i], p[u]);
             }
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const float sj = wave_sum(p[u]);
-            if (j0 + u < A && lane == j0 + u) ga = sj / b.a_den[j0 + u];
+            ga = (lane == j0 + u) ? sj : ga;
         }
     }
+    ga = ga / ad_pf;
     float gx = 0.f, dl = 0.f;
-    if (lane < A) {
-        const size_t ci = (size_t)row * A + lane;
+    if (jok) {
         const float t = t_pf, sd = sd_pf, u = u_pf, mask = mk_pf;
         gx = ga * b.lim * (1.f - t * t);
         if (pol) gx = gx - (2.f * c) * t;
@@ -928,23 +1081,35 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
         if (b.per_state_std) b.Da3[(size_t)row * b.Aout + A + lane] = dl;
         else b.E[ci] = dl;
     }
+    // Da2[row][i] = (sum_o Da3[row][o] W3a[i][o]) * act'(Ha2[row][i]); columns o live in lanes
+    const __amdgpu_buffer_rsrc_t rW3 = rs(b.W3a);
+    float pacc[MAXQ];
+#pragma unroll
+    for (int qq = 0; qq < MAXQ; ++qq) pacc[qq] = 0.f;
+    for (int o0 = 0; o0 < b.Aout; o0 += 8) {
+        float w[MAXQ][8];
+#pragma unroll
+        for (int qq = 0; qq < MAXQ; ++qq) {
+            const int i = qq * 64 + lane;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) w[qq][u] = bload(rW3, boff(i < b.H1 && o0 + u < b.Aout, i * b.Aout + o0 + u));
+        }
+        float d3[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int o = o0 + u;
+            const float src = (o < A) ? __shfl(gx, min(o, 63), 64) : __shfl(dl, min(max(o - A, 0), 63), 64);
+            d3[u] = (o < b.Aout) ? src : 0.f;
+        }
+#pragma unroll
+        for (int qq = 0; qq < MAXQ; ++qq)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) pacc[qq] = fmaf(d3[u], w[qq][u], pacc[qq]);
+    }
 #pragma unroll
     for (int qq = 0; qq < MAXQ; ++qq) {
-        const int i0 = qq * 64;
-        const int i = i0 + lane;
-        if (i0 >= b.H1) break;
-        float p = 0.f;
-        for (int o = 0; o < A; ++o) {
-            const float d3 = __shfl(gx, o, 64);
-            if (i < b.H1) p = fmaf(d3, b.W3a[(size_t)i * b.Aout + o], p);
-        }
-        if (b.per_state_std) {
-            for (int o = 0; o < A; ++o) {
-                const float d3 = __shfl(dl, o, 64);
-                if (i < b.H1) p = fmaf(d3, b.W3a[(size_t)i * b.Aout + A + o], p);
-            }
-        }
-        if (i < b.H1) b.Da2[(size_t)row * b.H1 + i] = p * dact_f(h2v[qq], b.act);
+        const int i = qq * 64 + lane;
+        if (i < b.H1) b.Da2[(size_t)row * b.H1 + i] = pacc[qq] * dact_f(h2v[qq], b.act);
     }
 }
 
@@ -995,6 +1160,12 @@ void launch_append(const AppendArgs& a, hipStream_t s) {
 
 namespace sacx {
 // per-call control values as kernel arguments (graph/stream ordered, no host buffer lifetime issues)
+__global__ void k_set_pseq(Ctl* ctl, int slot) { ctl->pseq[slot] = ctl->step_seq; }
+
+void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_pseq, dim3(1), dim3(1), 0, s, ctl, slot);
+}
+
 __global__ void k_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
         ctl->num_timesteps = num_timesteps;

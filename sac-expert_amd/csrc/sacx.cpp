@@ -48,7 +48,7 @@ struct SegInfo {
 };
 
 struct Launch {
-    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, MGATHER, MLOSS, MFINAL } kind;
+    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, FINAL, MGATHER, MLOSS, MFINAL } kind;
     std::string name;
     RngArgs rng;
     GatherArgs gather;
@@ -63,6 +63,7 @@ struct Launch {
     int grid = 0, block = 256;
     double flops = 0, bytes = 0;
     int gemm_first = 0;  // index of the first problem in the host table (GEMM)
+    bool after_final = false;  // graph: waits for the previous update's alpha.final
 };
 
 const char* kernel_family(Launch::Kind k) {
@@ -73,6 +74,7 @@ const char* kernel_family(Launch::Kind k) {
         case Launch::AHEAD: return "k_actor_head";
         case Launch::QHEAD: return "k_qhead";
         case Launch::ABWD: return "k_actor_bwd";
+        case Launch::FINAL: return "k_alpha_final";
         case Launch::MGATHER: return "k_mgather";
         case Launch::MLOSS: return "k_mloss";
         case Launch::MFINAL: return "k_mfinal";
@@ -99,7 +101,7 @@ struct sacx_handle {
     // binding
     char* arena = nullptr;
     hipStream_t stream = nullptr;
-    hipStream_t cap_stream = nullptr, rng_stream = nullptr;
+    hipStream_t cap_stream = nullptr, rng_stream = nullptr, fin_stream = nullptr;
     bool bound = false;
     std::vector<Launch> plan[2];
     std::vector<Launch> mplan;
@@ -186,29 +188,33 @@ void build_layout(sacx_handle* h) {
     h->alias("rng.key", roff, 1, 624, SACX_U32, SACX_ROLE_STATE);
     h->alias("rng.pos", roff + offsetof(RngState, pos), 1, 2, SACX_I32, SACX_ROLE_STATE);
     h->alias("rng.gauss", roff + offsetof(RngState, gauss), 1, 1, SACX_F64, SACX_ROLE_STATE);
+    // per-slot update inputs: the sampler + gather of update j+2 run while update j+1
+    // executes, so everything they write is double buffered
+    const int ne1 = std::max(1, h->ne);
     for (int s = 0; s < 2; ++s) {
-        h->add("slot" + std::to_string(s) + ".idx", 1, B, SACX_I32, SACX_ROLE_WORK);
-        h->add("slot" + std::to_string(s) + ".noise", 1, h->n_norm, F, SACX_ROLE_WORK);
+        const std::string sl = "slot" + std::to_string(s);
+        h->add(sl + ".idx", 1, B, SACX_I32, SACX_ROLE_WORK);
+        h->add(sl + ".noise", 1, h->n_norm, F, SACX_ROLE_WORK);
+        h->add(sl + ".Xa", h->Ra, h->ldS, F, 0);   // actor rows [sp ; s ; s_e] (normalised)
+        h->add(sl + ".Xq", B, h->ldQ, F, 0);       // critic rows [s | a]
+        h->add(sl + ".Xt", B, h->ldQ, F, 0);       // target rows [sp | pi(sp)]
+        h->add(sl + ".Xp", B, h->ldQ, F, 0);       // policy rows [s | pi(s)]
+        h->add(sl + ".Xm", ne1, h->ldQ, F, 0);     // expert rows [s_e | pi(s_e)]
+        h->add(sl + ".r", 1, B, F, 0);
+        h->add(sl + ".d", 1, B, F, 0);
+        h->add(sl + ".se_raw", ne1, S, F, 0);
+        h->add(sl + ".spe_raw", ne1, S, F, 0);
     }
     // ---------------- data
     h->add("replay", h->cap, h->stride, F, SACX_ROLE_STATE);
-    const int ecap = std::max(1, h->ecap), ne1 = std::max(1, h->ne);
+    const int ecap = std::max(1, h->ecap);
     h->add("expert.s", ecap, S, F, SACX_ROLE_STATE);
     h->add("expert.sp", ecap, S, F, SACX_ROLE_STATE);
     h->add("perm", h->perm_cap, ne1, SACX_I32, SACX_ROLE_STATE);
     h->add("stats", h->stats_cap, 8, F, SACX_ROLE_STATE);
-    h->add("red", 1, 1024, F, SACX_ROLE_WORK);
+    h->add("red", 1, std::max(1024, (B + 3) / 4), F, SACX_ROLE_WORK);
     // ---------------- workspace
     const int Ra = h->Ra, Rb = h->Rb, Hm0 = std::max(1, h->Hm0), Hm1 = std::max(1, h->Hm1);
-    h->add("ws.Xa", Ra, h->ldS, F, 0);
-    h->add("ws.Xq", B, h->ldQ, F, 0);
-    h->add("ws.Xt", B, h->ldQ, F, 0);
-    h->add("ws.Xp", B, h->ldQ, F, 0);
-    h->add("ws.Xm", ne1, h->ldQ, F, 0);
-    h->add("ws.r", 1, B, F, 0);
-    h->add("ws.d", 1, B, F, 0);
-    h->add("ws.se_raw", ne1, S, F, 0);
-    h->add("ws.spe_raw", ne1, S, F, 0);
     h->add("ws.Ha1", Ra, H0, F, 0);
     h->add("ws.Ha2", Ra, H1, F, 0);
     h->add("ws.c_t", Rb, A, F, 0);
@@ -269,6 +275,16 @@ GemmProb prob_fwd(const float* X, int ldx, int M, int K, const float* Wext, int 
     return p;
 }
 
+// two chained Dense layers (GM_FWD2): C1 = act(X W0 + b0) [M x H0], C = act(C1 W1 + b1) [M x N]
+GemmProb prob_fwd2(const float* X, int ldx, int M, int K0, const float* W0ext, int H0, float* C1,
+                   const float* W1ext, int N, float* C, int act) {
+    GemmProb p = prob_fwd(X, ldx, M, H0, W1ext, N, C, act);
+    p.K0 = K0;
+    p.W0 = W0ext;
+    p.C0 = C1;
+    return p;
+}
+
 // C = (D * W^T) (.) act'(Hprev), W_ext is [(K_in+1) x N_out]; C is [M x K_in]
 GemmProb prob_dx(const float* D, int M, int Nout, const float* Wext, int Kin, const float* Hprev, float* C, int act) {
     GemmProb p{};
@@ -292,8 +308,12 @@ GemmProb prob_dw(const float* X, int ldx, int Kin, int R, const float* D, int No
     return p;
 }
 
-double gemm_flops(const GemmProb& p) { return 2.0 * p.M * p.N * p.K; }
+// algorithmic counts (the fused layer 0 counted once, not per column tile)
+double gemm_flops(const GemmProb& p) { return 2.0 * p.M * p.N * p.K + (p.W0 ? 2.0 * p.M * p.K * p.K0 : 0.0); }
 double gemm_bytes(const GemmProb& p) {
+    if (p.W0)   // X, W0, H1 out, W1, H2 out
+        return 4.0 * ((double)p.M * p.K0 + (p.K0 + 1.0) * p.K + (double)p.M * p.K + (p.K + 1.0) * p.N +
+                      (double)p.M * p.N);
     double b = 4.0 * ((double)p.M * p.K + (double)p.K * p.N + (double)p.M * p.N);
     if (p.epi == EPI_ADAM) b += 4.0 * p.M * p.N * (p.T ? 8 : 6) - 4.0 * p.M * p.N;
     if (p.epi == EPI_DACT) b += 4.0 * p.M * p.N;
@@ -318,6 +338,33 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     h->probs_cursor += (int)ps.size();
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
     if (ps.size() > GEMM_MAXP) { fprintf(stderr, "sacx: too many GEMM problems in %s\n", name.c_str()); abort(); }
+    // every problem of a launch must share the operand/epilogue mode (k_gemm template)
+    auto mode_of = [](const GemmProb& p) {
+        return p.epi == EPI_ADAM ? GM_DW : (p.epi == EPI_DACT ? GM_DX : (p.W0 ? GM_FWD2 : GM_FWD));
+    };
+    const int mode = mode_of(ps[0]);
+    bool vec = mode != GM_DW;
+    int k0max = 0;
+    for (auto& p : ps) {
+        if (mode == GM_FWD2 && (p.K0 < 1 || p.K0 > FWD2_MAX_K0)) {
+            fprintf(stderr, "sacx: fused layer-0 K %d out of range in %s\n", p.K0, name.c_str());
+            abort();
+        }
+        k0max = std::max(k0max, p.K0);
+        // 32-bit buffer offsets: every operand the GEMM reads must stay below 2 GiB
+        const double ext = 4.0 * ((double)p.M * p.lda + (double)p.K * p.ldb + p.N);
+        if (ext >= 2147483648.0) { fprintf(stderr, "sacx: operand too large in %s\n", name.c_str()); abort(); }
+    }
+    for (auto& p : ps) {
+        if (mode_of(p) != mode) { fprintf(stderr, "sacx: mixed GEMM modes in %s\n", name.c_str()); abort(); }
+        const bool akc = p.a_kc != 0, bkc = p.b_kc != 0;
+        if (akc != (mode != GM_DW) || bkc != (mode == GM_DX)) { fprintf(stderr, "sacx: bad operand layout in %s\n", name.c_str()); abort(); }
+        const bool v_a = (p.lda % 4 == 0) && ((((uintptr_t)p.A) & 15) == 0);
+        const bool v_b = mode == GM_DX ? ((p.ldb % 4 == 0) && ((((uintptr_t)p.B) & 15) == 0)) : true;
+        if (!(v_a && v_b && p.K % 4 == 0 && p.K >= 4)) vec = false;
+    }
+    L.gemm.mode = mode;
+    L.gemm.vec = mode == GM_FWD2 ? ((k0max + 7) / 8) * 2 : (vec ? 1 : 0);
     for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
     L.gemm.nprob = (int)ps.size();
     L.gemm.total_tiles = tiles;
@@ -350,7 +397,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     float* noise_e = noise + (size_t)2 * B * A;
     float* noise_al = noise + (size_t)(2 * B + ne) * A;
     auto W = [&](const std::string& n) { return h->f(n); };
-    float *Xa = W("ws.Xa"), *Xq = W("ws.Xq"), *Xt = W("ws.Xt"), *Xp = W("ws.Xp"), *Xm = W("ws.Xm");
+    float *Xa = W(sl + ".Xa"), *Xq = W(sl + ".Xq"), *Xt = W(sl + ".Xt"), *Xp = W(sl + ".Xp"), *Xm = W(sl + ".Xm");
+    float *r_in = W(sl + ".r"), *d_in = W(sl + ".d"), *se_raw = W(sl + ".se_raw"), *spe_raw = W(sl + ".spe_raw");
     float *Ha1 = W("ws.Ha1"), *Ha2 = W("ws.Ha2");
     float *Hq1 = W("ws.Hq1"), *Hq2 = W("ws.Hq2"), *Dq1 = W("ws.Dq1"), *Dq2 = W("ws.Dq2");
     float *Hp1 = W("ws.Hp1"), *Hp2 = W("ws.Hp2"), *Dp1 = W("ws.Dp1"), *Dp2 = W("ws.Dp2");
@@ -370,6 +418,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.rng.n_norm = h->n_norm;
         L.rng.out_idx = idx;
         L.rng.out_norm = noise;
+        L.rng.slot = slot;
+        L.rng.reset_seq = 1;   // cleared for the chained launches of a captured graph
         L.grid = 1;
         L.block = 1024;
         L.bytes = 4.0 * (B + h->n_norm) + 2.0 * sizeof(RngState);
@@ -386,17 +436,39 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den");
         g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
         g.Xa = Xa; g.ldS = ldS; g.Xq = Xq; g.Xt = Xt; g.Xp = Xp; g.Xm = Xm; g.ldQ = ldQ;
-        g.r = W("ws.r"); g.d = W("ws.d");
+        g.r = r_in; g.d = d_in; g.slot = slot;
         g.exp_s = W("expert.s"); g.exp_sp = W("expert.sp");
         g.perm_ring = h->ptr<int32_t>("perm"); g.perm_cap = h->perm_cap;
-        g.se_raw = W("ws.se_raw"); g.spe_raw = W("ws.spe_raw");
+        g.se_raw = se_raw; g.spe_raw = spe_raw;
         L.grid = (B + ne + 3) / 4;
         L.bytes = 4.0 * (B * (2.0 * S + A + 2) + ne * 2.0 * S) + 4.0 * (B * (2.0 * ldS + 3.0 * ldQ + 2));
         plan.push_back(L);
     }
     // ---- actor forward on [sp ; s ; s_e]
-    add_gemm(h, plan, "actor.fwd0", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)}, record_probs);
-    add_gemm(h, plan, "actor.fwd1", {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, record_probs);
+    // Layer 0 has a small K (S, S+A): fuse it into layer 1 (GM_FWD2) when it fits and the
+    // launch is at most one workgroup round (<= 512 tiles at 2 WGs/CU; measured: 512-tile
+    // fused launches beat the pair, the 1024-tile one is slower).  SACX_FUSE=0/1 overrides.
+    const char* fenv = std::getenv("SACX_FUSE");
+    const int fuse_mode = fenv ? std::atoi(fenv) : -1;
+    const bool fuse_a = S <= FWD2_MAX_K0, fuse_q = S + A <= FWD2_MAX_K0;
+    auto fwd_pair = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1,
+                        bool fuse) {
+        int tiles = 0;
+        for (auto& p : p1) tiles += ((p.M + 15) / 16) * ((p.N + 15) / 16);
+        if (fuse_mode == 0 || (fuse_mode < 0 && tiles > 512)) fuse = false;
+        if (!fuse) {
+            add_gemm(h, plan, name + "0", p0, record_probs);
+            add_gemm(h, plan, name + "1", p1, record_probs);
+            return;
+        }
+        std::vector<GemmProb> pf;
+        for (size_t i = 0; i < p0.size(); ++i)
+            pf.push_back(prob_fwd2(p0[i].A, p0[i].lda, p0[i].M, p0[i].K, p0[i].B, p0[i].N, p0[i].C, p1[i].B,
+                                   p1[i].N, p1[i].C, p1[i].act));
+        add_gemm(h, plan, name, pf, record_probs);
+    };
+    fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
+             {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a);
     // ---- actor head
     {
         Launch L{};
@@ -436,24 +508,24 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                       Hm2b + (size_t)k * half * Hm1, mact));
             }
         }
-        add_gemm(h, plan, "q.fwd0", p0, record_probs);
-        add_gemm(h, plan, "q.fwd1", p1, record_probs);
+        fwd_pair("q.fwd", p0, p1, fuse_q);
     }
     // ---- q.head: target, critic loss grads, expert MSE
     {
         Launch L{};
         L.kind = Launch::QHEAD;
         L.name = "q.head";
+        L.after_final = true;   // first reader of alpha / the update counters
         QHeadArgs& q = L.qh;
         q.mode = 0; q.B = B; q.H1 = H1; q.H2 = Hq2;
         for (int k = 0; k < 4; ++k) q.W3[k] = W(std::string(qn[k]) + ".l2");
         q.act = act; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
-        q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = W("ws.r"); q.d = W("ws.d");
+        q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = r_in; q.d = d_in;
         q.gamma = h->cfg.gamma; q.ret_den = W("norm.ret_den"); q.w_sac = 1.f;
         q.ne = ne; q.Hm1 = Hm1; q.S = S; q.Hm2 = Hm2b;
         q.Wm3[0] = eo ? W("m0.l2") : nullptr;
         q.Wm3[1] = eo ? W("m1.l2") : nullptr;
-        q.mact = mact; q.se_raw = W("ws.se_raw"); q.spe_raw = W("ws.spe_raw");
+        q.mact = mact; q.se_raw = se_raw; q.spe_raw = spe_raw;
         q.d_mean = W("norm.d_mean"); q.d_den = W("norm.d_den"); q.ctl = h->ctl();
         q.Dm2 = Dm2; q.mse_rows = W("ws.mse");
         L.grid = (B + ne + 3) / 4;
@@ -496,8 +568,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), H0, Hp1 + (size_t)k * B * H0, act));
             p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, act));
         }
-        add_gemm(h, plan, "pi.q.fwd0", p0, record_probs);
-        add_gemm(h, plan, "pi.q.fwd1", p1, record_probs);
+        fwd_pair("pi.q.fwd", p0, p1, fuse_q);
         Launch L{};
         L.kind = Launch::QHEAD;
         L.name = "pi.q.head";
@@ -554,9 +625,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, "actor.adam", pw, record_probs);
     }
     // ---- alpha: updated actor on s, evaluate, Adam on alpha, statistics
-    add_gemm(h, plan, "alpha.fwd0", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
-             record_probs);
-    add_gemm(h, plan, "alpha.fwd1", {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, record_probs);
+    fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
+             {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, fuse_a);
     {
         Launch L{};
         L.kind = Launch::AHEAD;
@@ -571,17 +641,30 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         a.cache_row0 = 1 << 30;
         a.c_t = nullptr;
         a.alpha_mode = 1;
+        L.fin.red = W("red");                       // per-workgroup partials of sum(-nlp + H)
+        L.fin.target_entropy = h->cfg.target_entropy;
+        L.grid = (B + 3) / 4;
+        L.flops = 2.0 * B * H1 * Aout;
+        L.bytes = 4.0 * B * H1;
+        plan.push_back(L);
+    }
+    {
+        const Launch& AH = plan.back();
+        Launch L{};
+        L.kind = Launch::FINAL;
+        L.name = "alpha.final";
         FinalArgs& f = L.fin;
+        f.nred = AH.grid;
         f.alpha = W("alpha"); f.alpha_m = f.alpha + h->p_stride; f.alpha_v = f.alpha + 2 * h->p_stride;
         f.ctl = h->ctl();
-        f.adam = plan.back().gemm.adam;
+        f.adam = plan[plan.size() - 2].gemm.adam;   // alpha.fwd's Adam constants
         f.target_entropy = h->cfg.target_entropy;
         f.B = B; f.ne = ne; f.use_expert = eo;
         f.lq = W("ws.lq"); f.lp = W("ws.lp"); f.mse_rows = W("ws.mse"); f.red = W("red");
         f.stats = W("stats"); f.stats_cap = h->stats_cap;
-        L.grid = (B + 3) / 4;
-        L.flops = 2.0 * B * H1 * Aout;
-        L.bytes = 4.0 * B * H1;
+        L.grid = 1;
+        L.block = 64;
+        L.bytes = 4.0 * (f.nred + 3.0 * B + ne);
         plan.push_back(L);
     }
 }
@@ -658,19 +741,28 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::AHEAD: launch_actor_head(L.head, L.fin, s); break;
         case Launch::QHEAD: launch_qhead(L.qh, s); break;
         case Launch::ABWD: launch_actor_bwd(L.ab, s); break;
+        case Launch::FINAL: launch_alpha_final(L.fin, s); break;
         case Launch::MGATHER: launch_mgather(L.mg, s); break;
         case Launch::MLOSS: launch_mloss(L.ml, s); break;
         case Launch::MFINAL: launch_mfinal(L.mf, s); break;
     }
 }
 
+// the sampler + gather launches of a slot (the update's inputs)
+bool is_prologue(const Launch& L) { return L.kind == Launch::RNG || L.kind == Launch::GATHER; }
+
 void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
+    if (!with_rng) launch_set_pseq(h->ctl(), slot, s);   // caller-provided randoms: perm of this update
     for (const Launch& L : h->plan[slot]) {
         if (L.kind == Launch::RNG && !with_rng) continue;
         enqueue(L, h, s);
     }
 }
 
+// Captured chain of G updates on three streams:
+//   rs: sampler + gather of update j (j >= 2 waits for update j-2, the last reader of its slot)
+//   cs: the update body (waits for its inputs; q.head waits for the previous alpha.final)
+//   fs: alpha.final of update j (alpha Adam + statistics), off the critical path
 int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
     auto key = std::make_pair(G, with_rng ? 1 : 0);
     auto it = h->graphs.find(key);
@@ -678,40 +770,55 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
         *out = it->second;
         return 0;
     }
-    hipStream_t cs = h->cap_stream, rs = h->rng_stream;
-    if ((int)h->events.size() < 2 * G + 1) {
-        for (int i = (int)h->events.size(); i < 2 * G + 1; ++i) {
-            hipEvent_t e;
-            HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            h->events.push_back(e);
-        }
+    hipStream_t cs = h->cap_stream, rs = h->rng_stream, fs = h->fin_stream;
+    const int nev = 3 * G + 1;
+    for (int i = (int)h->events.size(); i < nev; ++i) {
+        hipEvent_t e;
+        HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        h->events.push_back(e);
     }
-    hipEvent_t* evR = h->events.data();
-    hipEvent_t* evS = h->events.data() + G;
-    hipEvent_t evFork = h->events[2 * G];
+    hipEvent_t* evR = h->events.data();          // inputs of update j ready
+    hipEvent_t* evS = h->events.data() + G;      // update j's body done
+    hipEvent_t* evF = h->events.data() + 2 * G;  // alpha.final of update j done
+    hipEvent_t evFork = h->events[3 * G];
     HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    const bool fork = with_rng && G > 1 && std::getenv("SACX_NO_FORK") == nullptr;
+    const bool fork = with_rng && std::getenv("SACX_NO_FORK") == nullptr;
+    // diagnostics: keep alpha.final / gather on the main stream
+    const bool final_main = std::getenv("SACX_FINAL_MAIN") != nullptr;
+    const bool gather_main = std::getenv("SACX_GATHER_MAIN") != nullptr;
     if (fork) {
-        // sampler chain on a forked stream: RNG(j) overlaps update j-1; RNG(j+2)
-        // waits for update j (the last reader of its slot).
-        const Launch& R0 = h->plan[0][0];
-        const Launch& R1 = h->plan[1][0];
         HIPCHK(h, hipEventRecord(evFork, cs));
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
-        enqueue(R0, h, rs);
-        HIPCHK(h, hipEventRecord(evR[0], rs));
-        enqueue(R1, h, rs);
-        HIPCHK(h, hipEventRecord(evR[1], rs));
+        auto prologue = [&](int j) {
+            for (const Launch& L : h->plan[j & 1]) {
+                if (!is_prologue(L) || (gather_main && L.kind == Launch::GATHER)) continue;
+                Launch C = L;
+                if (C.kind == Launch::RNG) C.rng.reset_seq = (j == 0);
+                enqueue(C, h, rs);
+            }
+            return hipEventRecord(evR[j], rs);
+        };
+        HIPCHK(h, prologue(0));
+        if (G > 1) HIPCHK(h, prologue(1));
         for (int j = 0; j < G; ++j) {
             HIPCHK(h, hipStreamWaitEvent(cs, evR[j], 0));
-            enqueue_step(h, j & 1, false, cs);
+            const Launch* fin = nullptr;
+            for (const Launch& L : h->plan[j & 1]) {
+                if (L.kind == Launch::RNG || (L.kind == Launch::GATHER && !gather_main)) continue;
+                if (L.kind == Launch::FINAL && !final_main) { fin = &L; continue; }
+                if (L.after_final && j > 0) HIPCHK(h, hipStreamWaitEvent(cs, evF[j - 1], 0));
+                enqueue(L, h, cs);
+            }
             HIPCHK(h, hipEventRecord(evS[j], cs));
+            HIPCHK(h, hipStreamWaitEvent(fs, evS[j], 0));
+            if (fin) enqueue(*fin, h, fs);
+            HIPCHK(h, hipEventRecord(evF[j], fs));
             if (j + 2 < G) {
                 HIPCHK(h, hipStreamWaitEvent(rs, evS[j], 0));
-                enqueue(h->plan[j & 1][0], h, rs);
-                HIPCHK(h, hipEventRecord(evR[j + 2], rs));
+                HIPCHK(h, prologue(j + 2));
             }
         }
+        HIPCHK(h, hipStreamWaitEvent(cs, evF[G - 1], 0));   // join the side streams
     } else {
         for (int j = 0; j < G; ++j) enqueue_step(h, 0, with_rng, cs);
     }
@@ -799,6 +906,7 @@ void sacx_destroy(sacx_handle* h) {
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
+    if (h->fin_stream) (void)hipStreamDestroy(h->fin_stream);
     delete h;
 }
 
@@ -845,6 +953,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     build_model_plan(h);
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
+    HIPCHK(h, hipStreamCreateWithFlags(&h->fin_stream, hipStreamNonBlocking));
     h->bound = true;
     return 0;
 }

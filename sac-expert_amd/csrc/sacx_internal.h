@@ -22,7 +22,9 @@ struct Ctl {
     float epsilon;          // expert weight
     float pad_f[3];
     int64_t mfit_seq;       // model-fit step sequence (index ring / stats)
-    int64_t reserved[13];
+    int64_t rng_seq;        // update number the next sampler launch draws for
+    int64_t pseq[2];        // update number whose randoms slot 0 / 1 holds (expert perm ring index)
+    int64_t reserved[10];
 };
 static_assert(sizeof(Ctl) <= 32 * 8, "ctl segment is 32 int64");
 
@@ -47,6 +49,12 @@ struct AdamConsts {
 // C[M,N] = A[M,K] * B[K,N] on 16x16 output tiles, fp32 MFMA (v_mfma_f32_16x16x4_f32),
 // K split over the 4 waves of a 256-thread workgroup and reduced through LDS.
 enum Epi { EPI_FWD = 0, EPI_DACT = 1, EPI_ADAM = 2, EPI_STORE = 3 };
+// launch-uniform operand/epilogue mode of k_gemm (template parameter)
+// GM_FWD2: two chained Dense layers, H2 = act(act(X W0 + b0) W1 + b1), for a
+// small layer-0 K (<= 64): the layer-0 output is recomputed per column tile in
+// registers and never round-trips through memory (column tile 0 stores it).
+enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2, GM_FWD2 = 3 };
+#define FWD2_MAX_K0 64
 
 struct GemmProb {
     const float* A;        // a_kc: A[m*lda + k]   else A[k*lda + m] (row ones_row = 1.0)
@@ -62,13 +70,18 @@ struct GemmProb {
     int32_t epi, act, group;
     int32_t tiles_n, tile_begin;
     float grad_scale;
-    int32_t pad;
+    int32_t K0;            // GM_FWD2: layer-0 inner dim (A is then X[M x K0], K is the hidden width)
+    const float* W0;       // GM_FWD2: layer-0 W_ext [(K0+1) x K]
+    float* C0;             // GM_FWD2: layer-0 output H1 [M x K] (row stride K)
 };
 
 #define GEMM_MAXP 8
 struct GemmArgs {
     GemmProb probs[GEMM_MAXP];   // by value: no dependent global load to find a tile's problem
     int32_t nprob;
+    int32_t mode;          // GemmMode, uniform over the launch's problems
+    int32_t vec;           // GM_FWD/GM_DX: float4 loads along k (ld % 4 == 0, K % 4 == 0, aligned);
+                           // GM_FWD2: layer-0 K steps of 4, rounded up to even (2..16)
     int32_t total_tiles;
     int64_t p_stride;      // floats between params / adam_m / adam_v blocks
     const Ctl* ctl;
@@ -78,11 +91,13 @@ struct GemmArgs {
 // ---------------------------------------------------------------- sampler + gather
 struct RngArgs {
     RngState* st;
-    const Ctl* ctl;        // reads cur_size at run time
+    Ctl* ctl;              // reads cur_size at run time; advances rng_seq / pseq
     int32_t n_int;
     int32_t n_norm;
     int32_t* out_idx;
     float* out_norm;
+    int32_t slot;          // writes ctl->pseq[slot]
+    int32_t reset_seq;     // first sampler launch of a chain: rng_seq = step_seq
 };
 
 struct GatherArgs {
@@ -92,6 +107,7 @@ struct GatherArgs {
     int32_t S, A, B, ne;
     const int32_t* idx;
     const Ctl* ctl;
+    int32_t slot;          // expert permutation of update ctl->pseq[slot]
     const float *s_mean, *s_den, *a_mean, *a_den;
     float* Xa;  int32_t ldS;   // actor rows [sp(B) ; s(B) ; s_e(ne)]
     float* Xq;  float* Xt; float* Xp; float* Xm; int32_t ldQ;
@@ -187,6 +203,7 @@ struct FinalArgs {
     const float* lp;        // [B]
     const float* mse_rows;  // [ne]
     float* red;             // partial slots
+    int32_t nred;           // number of partials (alpha.head workgroups)
     float* stats; int32_t stats_cap;
 };
 
@@ -232,5 +249,7 @@ void launch_mgather(const MGatherArgs& a, hipStream_t s);
 void launch_mloss(const MLossArgs& a, hipStream_t s);
 void launch_mfinal(const MFinalArgs& a, hipStream_t s);
 void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s);
+void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s);
+void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 
 }  // namespace sacx

@@ -101,7 +101,7 @@ def _one_step_compare(act, normalizers="identity", per_state_std=False, use_expe
     # sampler: bit-exact
     assert np.array_equal(v["slot0.idx"][0], R["idx"])
     # forward stages
-    assert relerr(v["ws.Xa"][:B, :S], keep["sp_n"]) < 1e-6
+    assert relerr(v["slot0.Xa"][:B, :S], keep["sp_n"]) < 1e-6
     assert relerr(v["ws.Ha1"][:B], keep["actor_h_t"][0]) < 2e-5
     assert relerr(v["ws.Ha2"][B:2 * B], keep["actor_h_p"][1]) < 2e-5
     assert relerr(v["ws.nlp_t"][0], keep["nlp_t"]) < 2e-5
@@ -191,15 +191,21 @@ def test_qloss_trajectory_100(gpu_available, use_expert):
     eng.close()
 
 
-def test_graph_equals_eager(gpu_available):
-    """hipGraph replay (sampler forked on a side stream) is bit-identical to eager launches."""
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_graph_equals_eager(gpu_available, use_expert):
+    """hipGraph replay (sampler + gather forked ahead on a side stream, alpha.final on a
+    third) is bit-identical to eager launches; 19 = two 8-update graphs + 3 single ones."""
     outs = []
+    n = 19
     for eager in (True, False):
-        eng, ocfg, st, buf, nrm, _ = make_pair(act="tanh", B=128, seed=21)
+        eng, ocfg, st, buf, nrm, _ = make_pair(act="tanh", B=128, seed=21, use_expert=use_expert)
         eng.rng_set_state(np.random.RandomState(5).get_state())
-        eng.step(16, eager=eager)
+        if use_expert:
+            rs = np.random.RandomState(8)
+            eng.push_perms(np.stack([rs.permutation(eng.cfg.expert_batch) for _ in range(n)]))
+        eng.step(n, eager=eager)
         eng.sync()
-        outs.append((eng.stats(16).copy(), eng.v["params"].cpu().numpy().copy()))
+        outs.append((eng.stats(n).copy(), eng.v["params"].cpu().numpy().copy()))
         eng.close()
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])

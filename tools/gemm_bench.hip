@@ -1,0 +1,90 @@
+// Ablation harness for k_gemm: per-launch time (graph replay) by shape/epilogue.
+#include "../sac-expert_amd/csrc/k_sac.hip"
+#include <chrono>
+#include <cstdio>
+#include <functional>
+using namespace sacx;
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+static double tgraph(hipStream_t s, int n, std::function<void(int)> launch) {
+    hipGraph_t g; hipGraphExec_t ge;
+    (void)hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    for (int i = 0; i < n; ++i) launch(i);
+    (void)hipStreamEndCapture(s, &g);
+    (void)hipGraphInstantiateWithFlags(&ge, g, 0);
+    (void)hipGraphLaunch(ge, s); (void)hipStreamSynchronize(s);
+    auto t0 = std::chrono::high_resolution_clock::now();
+    for (int r = 0; r < 5; ++r) (void)hipGraphLaunch(ge, s);
+    (void)hipStreamSynchronize(s);
+    auto t1 = std::chrono::high_resolution_clock::now();
+    (void)hipGraphExecDestroy(ge); (void)hipGraphDestroy(g);
+    return std::chrono::duration<double, std::micro>(t1 - t0).count() / (5.0 * n);
+}
+
+int main() {
+    hipStream_t s; CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    const size_t NF = 8 << 20;
+    float *X0, *X1, *W, *P; Ctl* ctl;
+    CK(hipMalloc(&X0, NF * 4)); CK(hipMalloc(&X1, NF * 4)); CK(hipMalloc(&W, NF * 4)); CK(hipMalloc(&P, 3 * NF * 4));
+    CK(hipMalloc(&ctl, sizeof(Ctl)));
+    CK(hipMemset(X0, 0, NF * 4)); CK(hipMemset(X1, 0, NF * 4)); CK(hipMemset(W, 0, NF * 4)); CK(hipMemset(P, 0, 3 * NF * 4));
+    CK(hipMemset(ctl, 0, sizeof(Ctl)));
+    auto fwd = [&](const float* A, float* C, int M, int N, int K) {
+        GemmArgs ga{}; GemmProb p{};
+        p.A = A; p.lda = K; p.a_kc = 1; p.ones_row = -1; p.B = W; p.ldb = N; p.b_kc = 0; p.M = M; p.N = N; p.K = K;
+        p.bias = W + (size_t)K * N; p.C = C; p.ldc = N; p.epi = EPI_FWD; p.act = ACT_RELU;
+        p.tiles_n = (N + 15) / 16; p.tile_begin = 0;
+        ga.probs[0] = p; ga.nprob = 1; ga.total_tiles = ((M + 15) / 16) * p.tiles_n; ga.p_stride = NF; ga.ctl = ctl;
+        ga.mode = GM_FWD; ga.vec = (K % 4 == 0);
+        ga.adam.lr[0] = ga.adam.lr[1] = ga.adam.lr[2] = ga.adam.lr[3] = 1e-4f;
+        return ga;
+    };
+    const int n = 100;
+    struct V { const char* name; int M, N, K; bool dep; };
+    V vs[] = {{"fwd 512x256 K=256 warm", 512, 256, 256, false}, {"fwd 512x256 K=256 dep", 512, 256, 256, true},
+              {"fwd 512x256 K=16 warm", 512, 256, 16, false},   {"fwd 512x256 K=16 dep", 512, 256, 16, true},
+              {"fwd 64x64 K=16 warm", 64, 64, 16, false},       {"fwd 16x16 K=16 warm", 16, 16, 16, false},
+              {"fwd 1024x256 K=256 dep", 1024, 256, 256, true}};
+    for (auto& v : vs) {
+        GemmArgs a0 = fwd(X0, X1, v.M, v.N, v.K), a1 = fwd(X1, X0, v.M, v.N, v.K);
+        double us = tgraph(s, n, [&](int i) { launch_gemm(v.dep ? ((i & 1) ? a1 : a0) : a0, s); });
+        printf("%-28s %4d tiles: %.2f us/launch\n", v.name, a0.total_tiles, us);
+    }
+    // fused two-layer forward (GM_FWD2) vs the two single-layer launches it replaces
+    for (int M : {512, 1024}) {
+        const int K0 = M == 512 ? 17 : 23, H0 = 256, N = 256;
+        GemmArgs f2{}; GemmProb p{};
+        p.A = X0; p.lda = 24; p.a_kc = 1; p.ones_row = -1; p.B = W + 100000; p.ldb = N; p.b_kc = 0;
+        p.M = M; p.N = N; p.K = H0; p.bias = W + 100000 + (size_t)H0 * N; p.C = X1; p.ldc = N;
+        p.epi = EPI_FWD; p.act = ACT_RELU; p.tiles_n = N / 16; p.tile_begin = 0;
+        p.K0 = K0; p.W0 = W; p.C0 = X1 + 2000000;
+        f2.probs[0] = p; f2.nprob = 1; f2.total_tiles = (M / 16) * (N / 16); f2.p_stride = NF; f2.ctl = ctl;
+        f2.mode = GM_FWD2; f2.vec = ((K0 + 7) / 8) * 2;
+        char nm[64];
+        snprintf(nm, sizeof nm, "fwd2 %dx%d K0=%d", M, N, K0);
+        printf("%-28s %4d tiles: %.2f us/launch\n", nm, f2.total_tiles, tgraph(s, n, [&](int) { launch_gemm(f2, s); }));
+        GemmArgs a0 = fwd(X0, X1 + 2000000, M, H0, K0);
+        a0.probs[0].lda = 24; a0.vec = 0;
+        GemmArgs a1 = fwd(X1 + 2000000, X1, M, N, H0);
+        snprintf(nm, sizeof nm, "fwd0+fwd1 %dx%d K0=%d", M, N, K0);
+        printf("%-28s %4d tiles: %.2f us/pair\n", nm, a0.total_tiles + a1.total_tiles,
+               2 * tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); }));
+    }
+    // Adam epilogue on a 257x256 grad tile set (dW of a 256x256 layer, K = batch 256)
+    {
+        GemmArgs ga{}; GemmProb p{};
+        p.A = X0; p.lda = 256; p.a_kc = 0; p.ones_row = 256; p.B = X1; p.ldb = 256; p.b_kc = 0;
+        p.M = 257; p.N = 256; p.K = 256; p.P = P; p.T = nullptr; p.ldp = 256; p.epi = EPI_ADAM; p.group = 0; p.grad_scale = 1.f;
+        p.tiles_n = 16; p.tile_begin = 0;
+        ga.probs[0] = p; ga.nprob = 1; ga.total_tiles = 17 * 16; ga.p_stride = NF; ga.ctl = ctl; ga.mode = GM_DW; ga.vec = 0;
+        ga.adam.lr[0] = 3e-4f; ga.adam.tau_keep = 0.995f; ga.adam.tau_take = 0.005f; ga.adam.target_update_int = 1;
+        printf("%-28s %4d tiles: %.2f us/launch\n", "dW+adam 257x256 K=256", ga.total_tiles, tgraph(s, n, [&](int) { launch_gemm(ga, s); }));
+        // dX (k-contig A and B^T), the critic backward shape: 512x256, K=256
+        GemmArgs gx{}; GemmProb q{};
+        q.A = X0; q.lda = 256; q.a_kc = 1; q.ones_row = -1; q.B = W; q.ldb = 257 * 0 + 256; q.b_kc = 1; q.M = 512; q.N = 256; q.K = 256;
+        q.H = X1; q.ldh = 256; q.C = X1 + 2000000; q.ldc = 256; q.epi = EPI_DACT; q.act = ACT_RELU; q.tiles_n = 16; q.tile_begin = 0;
+        gx.probs[0] = q; gx.nprob = 1; gx.total_tiles = 32 * 16; gx.p_stride = NF; gx.ctl = ctl; gx.mode = GM_DX; gx.vec = 1;
+        printf("%-28s %4d tiles: %.2f us/launch\n", "dX 512x256 K=256", gx.total_tiles, tgraph(s, n, [&](int) { launch_gemm(gx, s); }));
+    }
+    return 0;
+}

@@ -24,6 +24,18 @@ __global__ void k_clock(unsigned long long* o) {
     if (threadIdx.x == 0 && blockIdx.x == 0) { o[0] = t1 - t0; o[1] = r1 - r0; o[2] = (unsigned long long)x; }
 }
 
+struct BigArgs { int v[256]; };
+__global__ void k_karg_chain(BigArgs a, int* out, int hops) {
+    int j = threadIdx.x & 255;
+    for (int h = 0; h < hops; ++h) j = a.v[j];
+    if (j == -1) out[0] = j;
+}
+__global__ void k_gchain_uniform(const int* __restrict__ nxt, int* out, int hops) {
+    int j = 0;                       // wave-uniform chain -> scalar loads from global
+    for (int h = 0; h < hops; ++h) j = nxt[j];
+    if (j == -1) out[0] = j;
+}
+
 template <class F>
 double time_graph(hipStream_t s, int n, F launch) {
     hipGraph_t g; hipGraphExec_t ge;
@@ -55,6 +67,11 @@ int main() {
     printf("pingpong 512x256: %.2f us/launch\n", time_graph(s, N, [&] { static int f = 0; if (f ^= 1) k_load<<<512, 256, 0, s>>>(a, b); else k_load<<<512, 256, 0, s>>>(b, a); }));
     for (int hops : {1, 2, 4, 8, 16})
         printf("chain %2d hops 512x256: %.2f us/launch\n", hops, time_graph(s, N, [&] { k_chain<<<512, 256, 0, s>>>(nxt, pi, hops); }));
+    BigArgs ba; for (int i = 0; i < 256; ++i) ba.v[i] = (i * 37 + 11) & 255;
+    for (int hops : {1, 4, 16})
+        printf("karg chain %2d hops 512x256: %.2f us/launch\n", hops, time_graph(s, N, [&] { k_karg_chain<<<512, 256, 0, s>>>(ba, pi, hops); }));
+    for (int hops : {1, 4, 16})
+        printf("global uniform chain %2d hops 512x256: %.2f us/launch\n", hops, time_graph(s, N, [&] { k_gchain_uniform<<<512, 256, 0, s>>>(nxt, pi, hops); }));
     k_clock<<<256, 64, 0, s>>>(clk); CK(hipStreamSynchronize(s));
     unsigned long long hc[3]; CK(hipMemcpy(hc, clk, 24, hipMemcpyDeviceToHost));
     printf("clock (1 wave/CU busy loop): %.0f MHz (memtime %llu / realtime %llu @100MHz)\n", 100.0 * hc[0] / hc[1], hc[0], hc[1]);
