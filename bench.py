@@ -55,7 +55,7 @@ def build_engine(cfgd, seed, device):
     S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
-                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "8")))
+                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "32")))
     eng = Engine(ecfg, device=device)
     rng = np.random.default_rng(seed)
     eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
@@ -89,9 +89,34 @@ def build_engine(cfgd, seed, device):
     return eng
 
 
-def roofline(eng, n_prof=20):
+def pmc_traffic(kernel, config):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this config
+    (tools/pmc_summary.py over tools/gpu_pmc.sh output: 2 x FETCH_SIZE + WRITE_SIZE,
+    the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md section HBM), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        k = d["kernels"][kernel]
+        return k["traffic_bytes_per_launch"], os.path.relpath(path, ROOT)
+    except (OSError, KeyError, ValueError):
+        return None, None
+
+
+def roofline(eng, config, n_prof=20, n_replays=20):
+    """Roofline of the dominant kernel family.
+
+    Its average in-pipeline launch duration is measured with HIP events on the
+    engine's stream around replays of the captured update graph, once complete
+    and once with that family's launches left out (sacx_time_graph): the chain
+    is serial with no gaps between kernels, so the difference divided by the
+    family's launches per update is its average launch duration -- the number
+    rocprofv3 --kernel-trace --stats reports for it (profiles/).  Must run after
+    the timed region: the ablated replays leave meaningless state behind.
+    The per-stage eager numbers (HIP events around every eager launch) include
+    ~4 us of per-event GPU overhead each and only rank the stages."""
     info = eng.plan_info()
-    ms = eng.profile(n_prof)          # eager, HIP events around each launch on the engine stream
+    ms = eng.profile(n_prof)
     fam = {}
     for i, L in enumerate(info):
         f = fam.setdefault(L["kernel"], dict(ms=0.0, flops=0.0, bytes=0.0, launches=0))
@@ -101,18 +126,25 @@ def roofline(eng, n_prof=20):
         f["launches"] += 1
     dom = max(fam, key=lambda k: fam[k]["ms"])
     f = fam[dom]
-    avg_s = f["ms"] / f["launches"] * 1e-3
+    t_full = eng.time_graph(n_replays)           # ms per update, whole graph
+    t_wo = eng.time_graph(n_replays, dom)        # ms per update, family left out
+    avg_s = (t_full - t_wo) / f["launches"] * 1e-3
     flops_per_launch = f["flops"] / f["launches"]
     achieved = flops_per_launch / avg_s / 1e12
-    per_stage = {L["name"]: round(float(ms[i]) * 1e3, 2) for i, L in enumerate(info)}
-    return {
+    traffic, src = pmc_traffic(dom, config)
+    out = {
         "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
-        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5), "traffic": None,
+        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
+        "traffic": traffic, "traffic_source": src,
         "avg_launch_us": round(avg_s * 1e6, 3), "launches_per_step": f["launches"],
         "flops_per_launch": flops_per_launch,
-        "step_us_eager_events": round(float(ms.sum()) * 1e3, 2),
-        "stage_us": per_stage,
-    }, fam
+        "algorithmic_bytes_per_launch": f["bytes"] / f["launches"],
+        "timing": "HIP events over graph replays, with vs without the family (sacx_time_graph)",
+        "graph_us_per_update": round(t_full * 1e3, 3),
+        "graph_us_per_update_without": round(t_wo * 1e3, 3),
+        "stage_us_eager_events": {L["name"]: round(float(ms[i]) * 1e3, 2) for i, L in enumerate(info)},
+    }
+    return out, fam
 
 
 def cpu_baseline(cfgd, seconds=10.0):
@@ -198,7 +230,7 @@ def main():
     value = args.steps * ws / el
     roof = None
     if rank == 0 and not args.no_roofline:
-        roof, _ = roofline(eng)
+        roof, _ = roofline(eng, args.config)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(cfgd, args.cpu_seconds)

@@ -55,7 +55,7 @@ typedef struct sacx_config {
     int32_t model_activation;   /* --model_activations */
     int32_t model_batch;        /* --model_batch_size */
     int32_t target_update_int;  /* --target_update_int */
-    int32_t graph_steps;        /* updates per captured hipGraph (0 -> 8) */
+    int32_t graph_steps;        /* updates per captured hipGraph (0 -> 32, max 64) */
     int32_t stats_capacity;     /* rows of the per-update statistics ring (0 -> 4096) */
     int32_t perm_capacity;      /* per-update expert permutations held on device (0 -> 4096) */
     float gamma;                /* --gamma */
@@ -151,8 +151,18 @@ int sacx_sync(sacx_handle* h);
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);
 /* Runs n_steps updates eagerly with a HIP event around every launch on the
  * bound stream and returns the summed device milliseconds per launch index
- * (array of length n_launches from sacx_plan_info).  Synchronous. */
+ * (array of length n_launches from sacx_plan_info).  Each step is queued
+ * behind a ~3 ms device-side wait so the deltas are back-to-back device time,
+ * not host launch latency.  Synchronous. */
 int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t cap);
+
+/* Replays the captured update graph (graph_steps updates, device sampler) n_replays
+ * times between two HIP events on the bound stream and returns the elapsed ms.
+ * skip_kernel names a kernel family (sacx_launch_info.kernel, e.g. "k_gemm") whose
+ * launches are left out of the graph: the difference of the two timings is that
+ * family's in-pipeline time.  With a family skipped the updates are meaningless and
+ * the state must be discarded (measurement only).  Synchronous. */
+int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, double* ms_out);
 
 #ifdef __cplusplus
 }

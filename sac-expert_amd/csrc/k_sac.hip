@@ -1160,6 +1160,17 @@ void launch_append(const AppendArgs& a, hipStream_t s) {
 
 namespace sacx {
 // per-call control values as kernel arguments (graph/stream ordered, no host buffer lifetime issues)
+// busy-waits ~us microseconds (100 MHz realtime counter): lets the host queue a whole
+// step of launches + events behind it, so the event deltas are device back-to-back time
+__global__ void k_spin(int64_t ticks) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while ((int64_t)(__builtin_amdgcn_s_memrealtime() - t0) < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void launch_spin(double us, hipStream_t s) {
+    hipLaunchKernelGGL(k_spin, dim3(1), dim3(1), 0, s, (int64_t)(us * 100.0));
+}
+
 __global__ void k_set_pseq(Ctl* ctl, int slot) { ctl->pseq[slot] = ctl->step_seq; }
 
 void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s) {

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <tuple>
 #include <vector>
 
 using namespace sacx;
@@ -91,7 +92,7 @@ struct sacx_handle {
     int S = 0, A = 0, H0 = 0, H1 = 0, B = 0, Aout = 0, ne = 0, Hm0 = 0, Hm1 = 0, ecap = 0;
     int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0, act = 0, mact = 0;
     int64_t cap = 0;
-    int graph_steps = 8, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
+    int graph_steps = 32, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
     // layout
     std::vector<SegInfo> segs;
     std::map<std::string, size_t> seg_index;
@@ -109,7 +110,7 @@ struct sacx_handle {
     int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
     std::vector<GemmProb> probs;
     int probs_cursor = 0;
-    std::map<std::pair<int, int>, hipGraphExec_t> graphs;
+    std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;   // (G, with_rng, skipped kind)
     std::vector<hipEvent_t> events;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
 
@@ -763,8 +764,9 @@ void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
 //   rs: sampler + gather of update j (j >= 2 waits for update j-2, the last reader of its slot)
 //   cs: the update body (waits for its inputs; q.head waits for the previous alpha.final)
 //   fs: alpha.final of update j (alpha Adam + statistics), off the critical path
-int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
-    auto key = std::make_pair(G, with_rng ? 1 : 0);
+// skip_kind >= 0 leaves that launch kind out (measurement only: sacx_time_graph)
+int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1) {
+    auto key = std::make_tuple(G, with_rng ? 1 : 0, skip_kind);
     auto it = h->graphs.find(key);
     if (it != h->graphs.end()) {
         *out = it->second;
@@ -805,6 +807,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
             const Launch* fin = nullptr;
             for (const Launch& L : h->plan[j & 1]) {
                 if (L.kind == Launch::RNG || (L.kind == Launch::GATHER && !gather_main)) continue;
+                if ((int)L.kind == skip_kind) continue;
                 if (L.kind == Launch::FINAL && !final_main) { fin = &L; continue; }
                 if (L.after_final && j > 0) HIPCHK(h, hipStreamWaitEvent(cs, evF[j - 1], 0));
                 enqueue(L, h, cs);
@@ -820,6 +823,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out) {
         }
         HIPCHK(h, hipStreamWaitEvent(cs, evF[G - 1], 0));   // join the side streams
     } else {
+        if (skip_kind >= 0) return fail(h, "kernel ablation needs the forked sampler graph");
         for (int j = 0; j < G; ++j) enqueue_step(h, 0, with_rng, cs);
     }
     hipGraph_t graph;
@@ -1136,6 +1140,7 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
     for (auto& e : ev) HIPCHK(h, hipEventCreate(&e));
     std::vector<double> acc(n, 0.0);
     for (int64_t s = 0; s < n_steps; ++s) {
+        launch_spin(3000.0, h->stream);   // the host queues the whole step while the GPU waits
         HIPCHK(h, hipEventRecord(ev[0], h->stream));
         for (int i = 0; i < n; ++i) {
             enqueue(plan[i], h, h->stream);
@@ -1151,6 +1156,35 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
     for (auto& e : ev) (void)hipEventDestroy(e);
     h->seq_host += n_steps;
     for (int i = 0; i < n && i < cap; ++i) ms_per_launch[i] = acc[i];
+    return 0;
+}
+
+int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, double* ms_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!ms_out || n_replays <= 0) return fail(h, "bad arguments");
+    int skip = -1;
+    if (skip_kernel && skip_kernel[0]) {
+        for (int k = Launch::RNG; k <= Launch::MFINAL; ++k)
+            if (std::strcmp(kernel_family((Launch::Kind)k), skip_kernel) == 0) skip = k;
+        if (skip < 0 || skip == Launch::RNG || skip == Launch::GATHER)
+            return fail(h, "unknown or non-removable kernel family");
+    }
+    hipGraphExec_t g;
+    if (get_graph(h, h->graph_steps, true, &g, skip)) return -1;
+    hipEvent_t e0, e1;
+    HIPCHK(h, hipEventCreate(&e0));
+    HIPCHK(h, hipEventCreate(&e1));
+    HIPCHK(h, hipGraphLaunch(g, h->stream));   // warm
+    HIPCHK(h, hipEventRecord(e0, h->stream));
+    for (int64_t i = 0; i < n_replays; ++i) HIPCHK(h, hipGraphLaunch(g, h->stream));
+    HIPCHK(h, hipEventRecord(e1, h->stream));
+    HIPCHK(h, hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *ms_out = ms;
+    h->seq_host += (n_replays + 1) * h->graph_steps;
     return 0;
 }
 

@@ -250,6 +250,7 @@ void launch_mloss(const MLossArgs& a, hipStream_t s);
 void launch_mfinal(const MFinalArgs& a, hipStream_t s);
 void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s);
 void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s);
+void launch_spin(double us, hipStream_t s);
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 
 }  // namespace sacx

@@ -40,7 +40,7 @@ class EngineConfig:
     model_activation: str = "relu"
     model_batch: int = 200
     target_update_int: int = 1
-    graph_steps: int = 8
+    graph_steps: int = 32
     stats_capacity: int = 4096
     perm_capacity: int = 4096
     gamma: float = 0.995
@@ -295,6 +295,14 @@ class Engine:
         N.check(self.lib.sacx_plan_info(self.h, arr, n.value, ctypes.byref(n)), self.h, "plan_info")
         return [dict(name=a.name.decode(), kernel=a.kernel.decode(), grid=a.grid, block=a.block,
                      flops=a.flops, bytes=a.bytes) for a in arr]
+
+    def time_graph(self, n_replays: int, skip_kernel: str = None) -> float:
+        """ms per update of graph replays (HIP events); skip_kernel leaves a kernel family
+        out (the state is meaningless afterwards)."""
+        ms = ctypes.c_double(0.0)
+        arg = skip_kernel.encode() if skip_kernel else None
+        N.check(self.lib.sacx_time_graph(self.h, int(n_replays), arg, ctypes.byref(ms)), self.h, "time_graph")
+        return ms.value / (n_replays * self.cfg.graph_steps)
 
     def profile(self, n_steps: int) -> np.ndarray:
         k = len(self.plan_info())

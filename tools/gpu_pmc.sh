@@ -1,17 +1,18 @@
 #!/bin/bash
-# PMC passes (one counter group per run, kernel-trace only) over a short bench.
+# PMC passes (one counter group per run, kernel-trace only) over a short bench of
+# config ${CONFIG:-hc}; summary -> profiles/pmc_<config>.json (+ copy in gpurun_out/).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+CONFIG=${CONFIG:-hc}
+OUT=gpurun_out/pmc_$CONFIG
+mkdir -p $OUT
 export TMPDIR=/tmp
 i=0
-for grp in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-           "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_IFETCH" \
-           "FETCH_SIZE" "WRITE_SIZE" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$PWD/gpurun_out/pmc" -o "p$i" \
-      -- python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-roofline > gpurun_out/pmc/p$i.log 2>&1
-  rc=$?; echo "pass $i ($grp) rc=$rc"; tail -2 gpurun_out/pmc/p$i.log
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$PWD/$OUT" -o "p$i" \
+      -- python bench.py --config $CONFIG --steps 200 --warmup 20 --no-cpu-baseline --no-roofline > $OUT/p$i.log 2>&1
+  rc=$?; echo "pass $i ($grp) rc=$rc"; tail -1 $OUT/p$i.log
   [ $rc -eq 0 ] || exit $rc
 done
-ls gpurun_out/pmc
+python tools/pmc_summary.py $OUT $CONFIG "${PMC_TAG:-$CONFIG}" gpurun_out/pmc_$CONFIG.json
