@@ -41,14 +41,8 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak,
 HBM_PEAK_GBS = 8000.0
 
 
-def dist_env():
-    ws = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    return ws, rank, local
-
-
-def build_engine(cfgd, seed, device):
+def build_engine(cfgd, seeds, device):
+    """seeds: this replica's reference-style seeds (sac_eo.common.seeding.derive_seeds)."""
     import torch
     from sac_eo.engine import Engine, EngineConfig
     from sac_eo.nets import create_nn_weights
@@ -57,7 +51,7 @@ def build_engine(cfgd, seed, device):
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
                         expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "32")))
     eng = Engine(ecfg, device=device)
-    rng = np.random.default_rng(seed)
+    rng = np.random.default_rng(seeds["setup"])        # weights (init_seeds(setup_seed) then nets)
     eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
     for k in range(2):
         w = create_nn_weights(rng, S + A, 1, cfgd["hidden"], 1.0)
@@ -68,7 +62,7 @@ def build_engine(cfgd, seed, device):
             eng.set_net(f"m{k}", create_nn_weights(rng, S + A, S + 1, (512, 512), 0.01))
     # synthetic HalfCheetah-shaped rows generated on the device
     g = torch.Generator(device=device)
-    g.manual_seed(seed)
+    g.manual_seed(int(seeds["sim"]))                   # synthetic replay rows
     N = cfgd["buffer"]
     sig = torch.rand(S, device=device, generator=g) * 4.9 + 0.1
     s = torch.randn(N, S, device=device, generator=g) * sig
@@ -79,12 +73,12 @@ def build_engine(cfgd, seed, device):
     eng.append(s, a, r, sp, d)
     del s, sp, a, r, d
     if cfgd["use_expert"]:
-        ers = np.random.RandomState(seed + 1)
+        ers = np.random.RandomState(seeds["eval"])
         eng.set_expert(ers.normal(size=(20, S)), ers.normal(size=(20, S)), 1e-3)
-        gen = np.random.default_rng(seed + 2)
+        gen = np.random.default_rng(seeds["algorithm"])  # SAC_exp's self.rng (alg_seed)
         perms = np.stack([gen.permutation(20) for _ in range(4096)])
         eng.push_perms(perms)
-    eng.rng_seed(seed)
+    eng.rng_seed(seeds["expert"])                    # global stream: last np.random.seed (train.py:95-97)
     eng.sync()
     return eng
 
@@ -196,21 +190,12 @@ def main():
     args = ap.parse_args()
 
     import torch
-    ws, rank, local = dist_env()
+    from sac_eo.common.replicas import init_replica
+    rep = init_replica()                      # one learner per GPU, RCCL only for barrier / max time
+    ws, rank, device = rep.world_size, rep.rank, rep.device
     cfgd = CONFIGS[args.config]
-    device = torch.device("cuda", local)
-    torch.cuda.set_device(device)
-    dist = None
-    if ws > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
-    eng = build_engine(cfgd, seed=1000 + rank, device=device)
-
-    def barrier():
-        torch.cuda.synchronize(device)
-        if dist is not None:
-            dist.barrier()
-            torch.cuda.synchronize(device)
+    eng = build_engine(cfgd, rep.seeds(0), device=device)
+    barrier = rep.barrier
 
     eng.step(args.warmup, num_timesteps=0, ts_increment=1)
     eng.sync()
@@ -220,11 +205,7 @@ def main():
     eng.sync()
     t1 = time.perf_counter()
     barrier()
-    el = t1 - t0
-    if dist is not None:
-        t = torch.tensor([el], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = rep.max_over_ranks(t1 - t0)
     stats = eng.stats(1)[0]
     finite = bool(np.all(np.isfinite(stats)))
     value = args.steps * ws / el
@@ -253,8 +234,7 @@ def main():
         }
         print(json.dumps(line), flush=True)
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    rep.close()
 
 
 if __name__ == "__main__":
