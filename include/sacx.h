@@ -145,6 +145,12 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
  * of model_data, mapped into the replay ring).  Per-step summed loss goes to
  * the "mstats" ring.  Requires use_expert. */
 int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t flags);
+/* SquashedGaussianActor.sample (sac_eo/actors/continuous_actors.py:270-306) on n device
+ * rows obs[n,S] -> act_out[n,A] (device): normalise, MLP, a = act_limit*tanh(mu + std*u).
+ * deterministic != 0: u = 0 and the RNG is untouched (the reference draws nothing);
+ * otherwise u = np.random.normal(size=(n,A)) from the device copy of the global stream,
+ * in the order the reference would draw it.  Behaviour-policy inference for the env loop. */
+int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
 int sacx_sync(sacx_handle* h);
 
 /* --- measurement ----------------------------------------------------------- */

@@ -646,9 +646,11 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
         a.st->has_gauss = sh_has;
         a.st->gauss = sh_gauss;
         // the update these randoms belong to (the sampler runs ahead of the updates)
-        const int64_t seq = a.reset_seq ? a.ctl->step_seq : a.ctl->rng_seq;
-        a.ctl->pseq[a.slot] = seq;
-        a.ctl->rng_seq = seq + 1;
+        if (a.slot >= 0) {
+            const int64_t seq = a.reset_seq ? a.ctl->step_seq : a.ctl->rng_seq;
+            a.ctl->pseq[a.slot] = seq;
+            a.ctl->rng_seq = seq + 1;
+        }
     }
 }
 
@@ -833,6 +835,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
             }
             if (sg.xq_out != nullptr)
                 sg.xq_out[(size_t)(sg.xq_row0 + row - sg.r0) * h.ldQ + h.S + j] = (pi - am_pf) / ad_pf;
+            if (sg.pi_out != nullptr) sg.pi_out[(size_t)(row - sg.r0) * A + j] = pi;
             if (row >= h.cache_row0 && h.c_t != nullptr) {
                 const size_t ci = (size_t)(row - h.cache_row0) * A + j;
                 h.c_t[ci] = t;
@@ -1169,6 +1172,22 @@ __global__ void k_spin(int64_t ticks) {
 
 void launch_spin(double us, hipStream_t s) {
     hipLaunchKernelGGL(k_spin, dim3(1), dim3(1), 0, s, (int64_t)(us * 100.0));
+}
+
+// BaseActor._transform_state (base_actor.py:35-39): X[i][c] = (obs[i][c] - mean[c]) / den[c], 0 in the pad
+__global__ __launch_bounds__(256) void k_obs_norm(const float* obs, int64_t n, int S, const float* mean,
+                                                  const float* den, float* X, int ldX) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n * ldX) return;
+    const int64_t i = t / ldX;
+    const int c = (int)(t - i * ldX);
+    X[t] = c < S ? (obs[i * S + c] - mean[c]) / den[c] : 0.f;
+}
+
+void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, const float* den, float* X, int ldX,
+                     hipStream_t s) {
+    const int64_t tot = n * ldX;
+    hipLaunchKernelGGL(k_obs_norm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, obs, n, S, mean, den, X, ldX);
 }
 
 __global__ void k_set_pseq(Ctl* ctl, int slot) { ctl->pseq[slot] = ctl->step_seq; }

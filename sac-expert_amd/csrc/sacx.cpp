@@ -146,6 +146,8 @@ int fail(sacx_handle* h, const std::string& msg) {
         if (e_ != hipSuccess) return fail((h), std::string(#x " -> ") + hipGetErrorString(e_)); \
     } while (0)
 
+constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
+
 void build_layout(sacx_handle* h) {
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B;
     const int F = SACX_F32;
@@ -247,6 +249,11 @@ void build_layout(sacx_handle* h) {
     h->add("ws.E", Rb, A, F, 0);
     h->add("ws.Hl1", B, H0, F, 0);
     h->add("ws.Hl2", B, H1, F, 0);
+    // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
+    h->add("act.X", ACT_CAP, h->ldS, F, 0);
+    h->add("act.H1", ACT_CAP, H0, F, 0);
+    h->add("act.H2", ACT_CAP, H1, F, 0);
+    h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
     if (h->cfg.use_expert) {          // world-model fitting (A16)
         const int R2 = 2 * h->mb, O = S + 1;
         h->add("mfit.idx", h->mfit_cap, R2, SACX_I32, SACX_ROLE_WORK);
@@ -1156,6 +1163,43 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
     for (auto& e : ev) (void)hipEventDestroy(e);
     h->seq_host += n_steps;
     for (int i = 0; i < n && i < cap; ++i) ms_per_launch[i] = acc[i];
+    return 0;
+}
+
+int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS;
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    for (int64_t done = 0; done < n; done += ACT_CAP) {
+        const int m = (int)std::min<int64_t>(ACT_CAP, n - done);
+        float* noise = deterministic ? nullptr : W("act.noise");
+        if (!deterministic) {          // u = np.random.normal(size=(m, A)) from the global stream
+            RngArgs r{};
+            r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
+            r.n_int = 0; r.n_norm = m * A; r.out_idx = nullptr; r.out_norm = noise;
+            r.slot = -1; r.reset_seq = 0;
+            launch_rng(r, h->stream);
+        }
+        launch_obs_norm(obs + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
+        std::vector<Launch> pl;
+        add_gemm(h, pl, "act.fwd0", {prob_fwd(W("act.X"), ldS, m, S, W("actor.l0"), H0, W("act.H1"), h->act)}, false);
+        add_gemm(h, pl, "act.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W("actor.l1"), H1, W("act.H2"), h->act)}, false);
+        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+        h->probs_cursor -= 2;          // host table bookkeeping of add_gemm (these launches are not in a plan)
+        HeadArgs a{};
+        a.H2 = W("act.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.nseg = 1;
+        a.seg[0] = {0, m, 1, 0, noise, nullptr, nullptr, act_out + done * A};
+        a.total_rows = m;
+        a.cache_row0 = 1 << 30;
+        a.alpha_mode = 0;
+        FinalArgs f{};
+        launch_actor_head(a, f, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
     return 0;
 }
 

@@ -96,7 +96,7 @@ struct RngArgs {
     int32_t n_norm;
     int32_t* out_idx;
     float* out_norm;
-    int32_t slot;          // writes ctl->pseq[slot]
+    int32_t slot;          // writes ctl->pseq[slot]; -1: a draw outside the updates (no stamp)
     int32_t reset_seq;     // first sampler launch of a chain: rng_seq = step_seq
 };
 
@@ -124,6 +124,7 @@ struct HeadSeg {
     const float* noise;    // [r1-r0, A]
     float* xq_out;         // normalised action -> xq_out[(xq_row0 + i) * ldQ + S + j]
     float* nlp_out;        // [r1-r0] (evaluate)
+    float* pi_out;         // raw action lim*tanh(x) -> pi_out[(i) * A + j] (nullable)
 };
 
 struct HeadArgs {
@@ -251,6 +252,8 @@ void launch_mfinal(const MFinalArgs& a, hipStream_t s);
 void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s);
 void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s);
 void launch_spin(double us, hipStream_t s);
+void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, const float* den, float* X, int ldX,
+                     hipStream_t s);
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 
 }  // namespace sacx

@@ -1,0 +1,100 @@
+"""SquashedGaussianActor (reference ``sac_eo/actors/continuous_actors.py:237-379``).
+
+Holds the actor's hyper-parameters and, until an algorithm binds it, its weights
+in the Keras ``get_weights()`` order ``[W0, b0, W1, b1, W2, b2] (+ logstd (1, A))``.
+Once bound (``_bind``), the weights live in the engine's HBM arena: get/set go
+through the engine and ``sample`` runs on the GPU (``sacx_actor_act``).  There is
+no CPU execution path.
+"""
+import numpy as np
+
+from ..nets import create_nn_weights
+
+
+class _Out(np.ndarray):
+    """ndarray with the ``.numpy()`` the reference calls on TF tensors."""
+
+    def numpy(self):
+        return np.asarray(self)
+
+
+def _as_out(x):
+    return np.asarray(x).view(_Out)
+
+
+class SquashedGaussianActor:
+    def __init__(self, env, layers, activations, gain, init_type, layer_norm, std_mult=1.0, per_state_std=False,
+                 output_norm=False, rng=None):
+        self.s_dim = int(np.prod(env.observation_space.shape))
+        self.a_dim = int(np.prod(env.action_space.shape))
+        self.layers = list(layers)
+        acts = list(activations)
+        self.activation = acts[0]
+        if any(a != self.activation for a in acts):
+            raise NotImplementedError("one activation for all hidden layers")
+        if layer_norm:
+            raise NotImplementedError("actor_layer_norm is not built (off by default)")
+        if output_norm:
+            raise NotImplementedError("actor_output_norm is not built (off by default)")
+        self.gain, self.init_type = gain, init_type
+        self.per_state_std = bool(per_state_std)
+        self.std_mult = std_mult
+        self.act_low = np.asarray(env.action_space.low, np.float32)
+        self.act_high = np.asarray(env.action_space.high, np.float32)
+        self.act_limit = self.act_high
+        self.min_log_std, self.max_log_std = -5, 2
+        out_dim = 2 * self.a_dim if self.per_state_std else self.a_dim
+        rng = rng if rng is not None else np.random.default_rng(np.random.randint(2 ** 31))
+        self._w = create_nn_weights(rng, self.s_dim, out_dim, self.layers, gain)
+        self._logstd = np.zeros((1, self.a_dim), np.float32)     # tf.Variable(zeros), :56-58
+        self._engine = None
+        self._net = None
+
+    # ------------------------------------------------------------------ binding
+    def _bind(self, engine, net="actor", with_logstd=True):
+        """Moves the weights into ``engine`` (net name) and serves them from there."""
+        engine.set_net(net, self._w)
+        if with_logstd and not self.per_state_std:
+            engine.set_logstd(self._logstd)
+        self._engine, self._net = engine, net
+
+    @property
+    def trainable(self):
+        return self.get_weights()
+
+    def get_weights(self):
+        if self._engine is not None:
+            w = self._engine.get_net(self._net)
+            if not self.per_state_std:
+                w.append(self._engine.v["actor.logstd"].cpu().numpy().copy())
+            return w
+        return [x.copy() for x in self._w] + ([] if self.per_state_std else [self._logstd.copy()])
+
+    def set_weights(self, weights):
+        weights = [np.asarray(x, np.float32) for x in weights]
+        nw = len(self._w)
+        self._w = weights[:nw]
+        if not self.per_state_std and len(weights) > nw:
+            self._logstd = weights[nw].reshape(1, -1)
+        if self._engine is not None:
+            self._engine.set_net(self._net, self._w)
+            if not self.per_state_std:
+                self._engine.set_logstd(self._logstd)
+
+    def set_rms(self, normalizer):
+        self.s_rms = normalizer.get_rms()[0]
+
+    # ------------------------------------------------------------------ acting
+    def sample(self, s, deterministic=False):
+        """act_limit * tanh(mu + std * u) on the GPU; u from the global NumPy stream's
+        device copy unless deterministic (continuous_actors.py:270-306)."""
+        if self._engine is None:
+            raise RuntimeError("actor is not bound to a device engine (build the algorithm first)")
+        out = self._engine.act(np.asarray(s, np.float32), deterministic=deterministic)
+        return _as_out(out.cpu().numpy())
+
+    def clip(self, a):
+        return np.clip(a, self.act_low, self.act_high)
+
+    def tf_clip(self, a):
+        return self.clip(a)

@@ -1,0 +1,42 @@
+"""SAC (reference ``sac_eo/algs/SAC.py``): the train loop of ``:253-390``; every
+``_update`` (``:236-250``) is one device gradient step (``sacx_sac_step``)."""
+import numpy as np
+
+from .base import SACBase
+
+
+class SAC(SACBase):
+    use_expert = False
+
+    def train(self, total_timesteps, params):
+        self._set_rms()
+        checkpoints = self._checkpoints(total_timesteps)
+        ck = 0
+        num_timesteps = 0
+        num_timesteps += self._collect_env_data(num_timesteps, update_normalizers=self.update_normalizers,
+                                                only_model_normalizer=self.only_model_normalizer)
+        episode_step, episode, episode_reward, done = 0, 0, 0.0, True
+        obs = None
+        while num_timesteps < total_timesteps:
+            if done:
+                if episode > 0:
+                    self.logger.log_train({"J_tot": episode_reward, "steps": episode_step, "traj": 1})
+                obs = self.env.reset()
+                done, episode_reward, episode_step = False, 0.0, 0
+                episode += 1
+            a = self.actor.sample(obs, deterministic=not self.random_act).numpy()
+            if episode_step % int(self.repeat_after_real_steps) == 0:
+                for _ in range(self.G):          # G updates at one env step: num_timesteps unchanged
+                    self._update(num_timesteps, ts_increment=0)
+            next_obs, r, done, _ = self.env.step(self.actor.clip(a))
+            done_no_max = False if episode_step + 1 == self._max_episode_steps else done
+            episode_reward += r
+            self._add(obs[None], a[None], [r], next_obs[None], [float(done_no_max)])
+            obs = next_obs
+            episode_step += 1
+            num_timesteps += 1
+            if num_timesteps >= checkpoints[ck]:
+                self._dump_and_save(params)
+                ck = min(ck + 1, len(checkpoints) - 1)
+        self._dump_and_save(params)
+        return self.checkpoint_name

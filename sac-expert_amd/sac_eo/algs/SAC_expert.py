@@ -1,0 +1,174 @@
+"""SAC_exp — SAC-EO (reference ``sac_eo/algs/SAC_expert.py``).
+
+* ``_update`` (``:463-477``): one device gradient step; the expert term's
+  ``self.rng.shuffle`` permutation (``:301-303``) is drawn here on the host from the
+  same Generator and handed to the device (``sacx_perm_push``).
+* ``_update_models`` (``:480-552``): the epoch / minibatch loop with the reference's
+  ``np.random.shuffle`` draws (under ``_host_rng``), each minibatch pair fitted on the
+  device (``sacx_model_fit``).  The expert-MSE diagnostics of ``:554-608`` draw the
+  same counterfactual actions (so the stream stays aligned) but their model
+  evaluations are SURVEY F3 (not built this round) and are logged as NaN.
+* ``_collect_expert_data`` (``:156-208``): rollouts of the expert actor (its own
+  inference-only engine) in ``env_expert``.
+"""
+import time
+
+import numpy as np
+
+from ..common.normalizer import RunningNormalizers
+from ..common.samplers import trajectory_sampler
+from ..engine import Engine, EngineConfig
+from .base import SACBase
+
+
+class SAC_exp(SACBase):
+    use_expert = True
+
+    def __init__(self, idx, env, env_eval, env_expert, actor, expert, init_expert_rms_stats, v_critic, q_targets,
+                 q_critics, models, alg_kwargs, mf_update_kwargs):
+        if len(models) != 2:
+            raise NotImplementedError("SAC-EO is built for num_models = 2 (the default)")
+        super().__init__(idx, env, env_eval, actor, v_critic, q_targets, q_critics, models, alg_kwargs,
+                         mf_update_kwargs)
+        self.env_expert = env_expert
+        self.expert = expert
+        self.expert_normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, init_expert_rms_stats)
+        self.use_expert_actions = alg_kwargs.get("use_expert_actions", False)
+        for flag in ("scale_epsilon_by_true_MSE", "scale_max_disc", "scale_median_disc", "scale_total_disc"):
+            if alg_kwargs.get(flag):
+                raise NotImplementedError(f"{flag}: adaptive epsilon is SURVEY F3, not built this round")
+        self.model_MSE_on_expert_data = []
+        self.model_MSE_on_expert_counterfactual_action = []
+        self._expert_engine = None
+        self.s_expert = self.sp_expert = None
+
+    # ------------------------------------------------------------------ expert
+    def _expert_engine_for(self):
+        if self._expert_engine is None:
+            ex = self.expert
+            cfg = EngineConfig(s_dim=self.s_dim, a_dim=self.a_dim, hidden=tuple(ex.layers), activation=ex.activation,
+                               batch=1, buffer_capacity=1, per_state_std=ex.per_state_std, graph_steps=1,
+                               act_limit=float(np.max(ex.act_limit)))
+            self._expert_engine = Engine(cfg)
+            ex._bind(self._expert_engine, "actor")
+            self.expert_normalizer.push_to(self._expert_engine)
+        return self._expert_engine
+
+    def _set_rms(self):
+        super()._set_rms()
+        self.expert.set_rms(self.expert_normalizer)
+
+    def _collect_expert_data(self):
+        t0 = time.time()
+        self._expert_engine_for()
+        s_all, sp_all, J_all, cur = [], [], [], 0
+        while cur < self.expert_buffer_size:
+            horizon = min(self.expert_buffer_size - cur, self.env_horizon)
+            s, a, r, sp, d, J = trajectory_sampler(self.env_expert, self.expert, horizon, eval=True,
+                                                   deterministic=True)
+            s_all.append(s)
+            sp_all.append(sp)
+            cur += len(r)
+            if horizon == self.env_horizon:
+                J_all.append(J)
+        self.s_expert = np.concatenate(s_all)[-self.expert_buffer_size:]
+        self.sp_expert = np.concatenate(sp_all)[-self.expert_buffer_size:]
+        self.expert_reward = float(np.mean(J_all)) if J_all else float("nan")
+        self.logger.log_train({"expert_J_tot": self.expert_reward, "expert_steps": cur,
+                               "expert_time": time.time() - t0})
+
+    def _expert_preprocess(self):
+        """Default path of :375-424: epsilon_coef = epsilon over the whole expert buffer."""
+        eps = self.epsilon
+        s_e, sp_e = self.s_expert, self.sp_expert
+        if self.expert_batch_size:
+            with self._host_rng():               # get_model_info(batch_size), buffers.py:116-122
+                pick = np.random.randint(len(s_e), size=int(self.expert_batch_size))
+            s_e, sp_e = s_e[pick], sp_e[pick]
+        self.engine.set_expert(s_e, sp_e, eps)
+        return (s_e, None, sp_e, eps, self.use_expert_actions)
+
+    # ------------------------------------------------------------------ update
+    def _update(self, num_timesteps, expert_reg=None, ts_increment=1):
+        n_e = self.engine.cfg.expert_batch
+        idx = np.arange(n_e)
+        self.rng.shuffle(idx)                    # SAC_expert.py:301-303
+        self.engine.push_perms(idx[None, :])
+        self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
+
+    def _update_models(self):
+        t0 = time.time()
+        n_model = min(self.steps_total, self.model_buffer_size)   # model_data = last rows of the env data
+        if n_model < self.model_batch_size:
+            return
+        base = int(self.engine.ctl()["cur_size"]) - n_model
+        batches = []
+        num_updates = 0
+        with self._host_rng():
+            for ep in range(self.model_num_epochs):
+                idx = np.arange(n_model)
+                if self.model_batch_shuffle:
+                    idx = np.tile(idx, (2, 1))
+                    for row in idx:
+                        np.random.shuffle(row)
+                else:
+                    np.random.shuffle(idx)
+                    idx = np.tile(idx, (2, 1))
+                sections = np.arange(0, n_model, self.model_batch_size)[1:]
+                parts = np.array_split(idx, sections, axis=1)
+                if n_model % self.model_batch_size != 0:
+                    parts = parts[:-1]
+                for p in parts:
+                    batches.append(p)
+                    num_updates += 1
+                    if num_updates >= self.model_max_updates:
+                        break
+                if num_updates >= self.model_max_updates:
+                    break
+        if batches:
+            self.engine.model_fit((np.stack(batches) + base).astype(np.int32))
+        if self.reset_model_optimizer:
+            self.engine.reset_model_optimizer()
+        # diagnostics: draw the counterfactual actions the reference draws (stream alignment)
+        if not self.use_expert_actions:
+            self.actor.sample(self.s_expert, deterministic=False)
+        self.model_MSE_on_expert_data.append(float("nan"))
+        self.model_MSE_on_expert_counterfactual_action.append(float("nan"))
+        self.logger.log_train({"time_model_fit": time.time() - t0, "model_loss_epochs": ep + 1,
+                               "model_updates": num_updates,
+                               "model_loss_last": float(self.engine.model_stats(1)[0].sum())})
+
+    # ------------------------------------------------------------------ loop
+    def train(self, total_timesteps, params):
+        self._set_rms()
+        self._collect_expert_data()
+        checkpoints = self._checkpoints(total_timesteps)
+        ck = 0
+        num_timesteps = 0
+        num_timesteps += self._collect_env_data(num_timesteps, update_normalizers=self.update_normalizers,
+                                                only_model_normalizer=self.only_model_normalizer)
+        episode_step, episode, episode_reward, done = 0, 0, 0.0, True
+        obs, expert_reg = None, None
+        while num_timesteps < total_timesteps:
+            if done:
+                if episode > 0:
+                    self.logger.log_train({"J_tot": episode_reward, "steps": episode_step, "traj": 1})
+                obs = self.env.reset()
+                done, episode_reward, episode_step = False, 0.0, 0
+                episode += 1
+                self._update_models()
+                expert_reg = self._expert_preprocess()
+            a = self.actor.sample(obs, deterministic=not self.random_act).numpy()
+            self._update(num_timesteps, expert_reg)
+            next_obs, r, done, _ = self.env.step(self.actor.clip(a))
+            done_no_max = False if episode_step + 1 == self._max_episode_steps else done
+            episode_reward += r
+            self._add(obs[None], a[None], [r], next_obs[None], [float(done_no_max)])
+            obs = next_obs
+            episode_step += 1
+            num_timesteps += 1
+            if num_timesteps >= checkpoints[ck]:
+                self._dump_and_save(params)
+                ck = min(ck + 1, len(checkpoints) - 1)
+        self._dump_and_save(params)
+        return self.checkpoint_name

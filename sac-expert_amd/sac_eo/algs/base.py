@@ -1,0 +1,184 @@
+"""Shared host side of SAC / SAC_exp: builds the device engine from the reference's
+actor / critic / model objects and kwargs, owns the env loop bookkeeping.
+
+The gradient step itself is ``Engine.step`` -> ``sacx_sac_step`` (HIP kernels, HBM
+resident state).  The global NumPy stream is shared between host and device: the
+device keeps the live copy (updates, stochastic actions); host code that draws from
+``np.random`` (model-minibatch shuffles) runs inside ``self._host_rng()``, which
+pulls the device state into NumPy and pushes it back afterwards, so draws happen in
+the reference's order."""
+import contextlib
+import time
+
+import numpy as np
+
+from ..common.logger import Logger
+from ..common.normalizer import RunningNormalizers
+from ..common.samplers import trajectory_sampler
+from ..engine import Engine, EngineConfig
+
+
+class SACBase:
+    use_expert = False
+
+    def __init__(self, idx, env, env_eval, actor, critics, q_targets, q_critics, models, alg_kwargs,
+                 mf_update_kwargs):
+        self.idx = idx
+        self.env, self.env_eval = env, env_eval
+        self.actor, self.critics, self.q_targets, self.q_critics = actor, critics, q_targets, q_critics
+        self.models = models
+        self.s_dim = int(np.prod(env.observation_space.shape))
+        self.a_dim = int(np.prod(env.action_space.shape))
+        self._setup(alg_kwargs)
+        self.logger = Logger()
+        self.rng = np.random.default_rng(self.alg_seed)            # base_onpolicy_alg.py:108-109
+        self.normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, self.init_rms_stats)
+        self.engine = self._build_engine(alg_kwargs)
+        self.steps_total = 0
+        self.traj_total = 0
+        self.checkpoint_name = f"{self.checkpoint_file}_{idx}"
+
+    # ------------------------------------------------------------------ setup
+    def _setup(self, k):
+        self.gamma = k["gamma"]
+        self.alg_seed = k.get("alg_seed")
+        self.init_rms_stats = k.get("init_rms_stats")
+        self.total_timesteps = int(k.get("total_timesteps", 0) or 0)
+        self.env_buffer_size = k.get("env_buffer_size")
+        self.model_buffer_size = int(k.get("model_buffer_size") or 1e5)
+        self.checkpoint_file = k.get("checkpoint_file", "TEMPLOG")
+        self.save_path = k.get("save_path", "./logs")
+        self.save_freq, self.eval_freq = k.get("save_freq"), k.get("eval_freq")
+        self.eval_num_traj = k.get("eval_num_traj", 5)
+        self.env_horizon = k.get("env_horizon", 1000)
+        self.env_batch_type = k.get("env_batch_type", "steps")
+        self.env_batch_size_init = k.get("env_batch_size_init", 5000)
+        self.env_batch_size = k.get("env_batch_size", 3000)
+        self.init_temperature = k["init_temperature"]
+        self.mbpo_lr, self.mbpo_actor_lr, self.mbpo_alpha_lr = k["q_crit_lr"], k["mbpo_actor_lr"], k["mbpo_alpha_lr"]
+        self.G = k.get("mbpo_G", 3)
+        self.sac_batch_size = k["sac_batch_size"]
+        self.soft_tau = k["soft_tau"]
+        self.target_update_int = k["target_update_int"]
+        self.repeat_after_real_steps = k.get("real_step_mod", 3)
+        self.random_act = k.get("random_act", False)
+        self.update_normalizers = k.get("update_normalizers", False)
+        self.only_model_normalizer = k.get("only_model_normalizer", False)
+        self.model_lr = k.get("model_lr", 1e-3)
+        self.model_num_epochs = k.get("model_num_epochs", 10)
+        self.model_batch_size = k.get("model_batch_size", 200)
+        self.model_max_updates = k.get("model_max_updates", 1e5)
+        self.model_batch_shuffle = k.get("model_batch_shuffle", True)
+        self.model_holdout_ratio = k.get("model_holdout_ratio", 0.0)
+        self.reset_model_optimizer = k.get("reset_model_optimizer", False)
+        self.epsilon = k.get("epsilon", 1e-3)
+        self.expert_buffer_size = int(k.get("expert_buffer_size") or 20)
+        self.expert_batch_size = k.get("expert_batch_size")
+        self._max_episode_steps = 1000
+
+    def _capacity(self):
+        if self.env_buffer_size:
+            return int(self.env_buffer_size)
+        # the reference's buffer is unbounded when env_buffer_size is None
+        return max(1, self.total_timesteps + self.env_batch_size_init + self.env_horizon)
+
+    def _build_engine(self, k):
+        hidden = self.actor.layers
+        if len(hidden) != 2 or list(self.q_critics[0].layers) != list(hidden):
+            raise NotImplementedError("the device engine runs 2 hidden layers shared by actor and critics")
+        if self.actor.activation != self.q_critics[0].activation:
+            raise NotImplementedError("actor and critic activations must match")
+        cfg = EngineConfig(
+            s_dim=self.s_dim, a_dim=self.a_dim, hidden=tuple(hidden), activation=self.actor.activation,
+            batch=int(self.sac_batch_size), buffer_capacity=self._capacity(), per_state_std=self.actor.per_state_std,
+            use_expert=self.use_expert, expert_capacity=self.expert_buffer_size,
+            expert_batch=int(self.expert_batch_size or self.expert_buffer_size),
+            model_hidden=tuple(self.models[0].layers) if self.use_expert else (512, 512),
+            model_activation=self.models[0].activation if self.use_expert else "relu",
+            model_batch=int(self.model_batch_size), target_update_int=int(self.target_update_int),
+            graph_steps=1, gamma=self.gamma, tau=self.soft_tau, lr_q=self.mbpo_lr, lr_pi=self.mbpo_actor_lr,
+            lr_alpha=self.mbpo_alpha_lr, lr_model=self.model_lr, init_temperature=self.init_temperature,
+            target_entropy=-float(self.a_dim), act_limit=float(np.max(self.actor.act_limit)),
+            epsilon=float(self.epsilon),
+            reward_loss_coef=self.models[0].reward_loss_coef if self.use_expert else 1.0)
+        eng = Engine(cfg)
+        self.actor._bind(eng, "actor")
+        for i, q in enumerate(self.q_critics):
+            q._bind(eng, f"q{i}")
+        for i, t in enumerate(self.q_targets):
+            t._bind(eng, f"t{i}")
+        if self.use_expert:
+            for i, m in enumerate(self.models[:2]):
+                m._bind(eng, f"m{i}")
+        self.normalizer.push_to(eng)
+        eng.rng_set_state(np.random.get_state())       # adopt the global stream
+        return eng
+
+    # ------------------------------------------------------------------ RNG sharing
+    @contextlib.contextmanager
+    def _host_rng(self):
+        np.random.set_state(self.engine.rng_get_state())
+        try:
+            yield
+        finally:
+            self.engine.rng_set_state(np.random.get_state())
+
+    # ------------------------------------------------------------------ data
+    def _set_rms(self):
+        for obj in [self.actor] + list(self.q_critics) + list(self.q_targets) + list(self.models or []):
+            obj.set_rms(self.normalizer)
+        self.normalizer.push_to(self.engine)
+
+    def _add(self, s, a, r, sp, d):
+        n = self.engine.append(np.asarray(s, np.float32), np.asarray(a, np.float32), np.asarray(r, np.float32),
+                               np.asarray(sp, np.float32), np.asarray(d, np.float32))
+        self.steps_total += n
+
+    def _collect_env_data(self, num_timesteps, update_normalizers=True, only_model_normalizer=False):
+        """SAC_expert.py:625-684: rollouts of the stochastic actor until the batch is full."""
+        t0 = time.time()
+        batch_size = self.env_batch_size_init if num_timesteps == 0 else self.env_batch_size
+        steps_start, J_all, cur = self.steps_total, [], 0
+        while cur < batch_size:
+            horizon = min(batch_size - cur, self.env_horizon) if self.env_batch_type == "steps" else self.env_horizon
+            s, a, r, sp, d, J = trajectory_sampler(self.env, self.actor, horizon, eval=True)
+            if update_normalizers:
+                self.normalizer.update_rms(s, a, r, sp)
+                self.normalizer.push_to(self.engine)
+            self._add(s, a, r, sp, d)
+            self.traj_total += 1
+            if horizon == self.env_horizon:
+                J_all.append(J)
+            cur = self.steps_total - steps_start if self.env_batch_type == "steps" else cur + 1
+        steps_new = self.steps_total - steps_start
+        self.current_reward = float(np.mean(J_all)) if J_all else float("nan")
+        self.logger.log_train({"J_tot": self.current_reward, "steps": steps_new, "traj": 1,
+                               "time_env_data": time.time() - t0})
+        return steps_new
+
+    def _evaluate(self, num_timesteps):
+        J = []
+        for _ in range(self.eval_num_traj):
+            *_, Jt = trajectory_sampler(self.env_eval, self.actor, self.env_horizon, eval=True, deterministic=True)
+            J.append(Jt)
+        self.logger.log_eval({"J_tot": float(np.mean(J)), "steps": num_timesteps})
+
+    # ------------------------------------------------------------------ update
+    def _update(self, num_timesteps, expert_reg=None, ts_increment=1):
+        self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
+
+    def _dump_and_save(self, params):
+        final = {"actor_weights": self.actor.get_weights(),
+                 "critic_weights": [q.get_weights() for q in self.q_critics],
+                 "target_weights": [t.get_weights() for t in self.q_targets],
+                 "alpha": self.engine.alpha(), "rms_stats": self.normalizer.get_rms_stats()}
+        if self.use_expert:
+            final["model_weights"] = [m.get_weights() for m in self.models[:2]]
+        self.logger.log_params(params)
+        self.logger.log_final(final)
+        self.logger.save(self.save_path, self.checkpoint_name)
+
+    def _checkpoints(self, total_timesteps):
+        if self.save_freq is None:
+            return np.array([total_timesteps])
+        return np.concatenate((np.arange(0, total_timesteps, self.save_freq)[1:], [total_timesteps]))

@@ -179,7 +179,7 @@ class Engine:
         """Values of RunningNormalizer.normalize: mean and max(std, 1e-8) (normalizer.py:26-41)."""
         v = self.v
         S, A = self.cfg.s_dim, self.cfg.a_dim
-        put = lambda k, x, n: v[k].copy_(torch.as_tensor(np.asarray(x, np.float32).reshape(1, n)))
+        put = lambda k, x, n: v[k].copy_(torch.as_tensor(np.array(x, np.float32).reshape(1, n)))
         put("norm.s_mean", s_mean, S)
         put("norm.s_den", s_den, S)
         put("norm.a_mean", a_mean, A)
@@ -238,6 +238,20 @@ class Engine:
     def push_perms(self, perms: np.ndarray):
         perms = np.ascontiguousarray(perms, dtype=np.int32)
         N.check(self.lib.sacx_perm_push(self.h, perms.ctypes.data, int(perms.shape[0])), self.h, "perm_push")
+
+    def act(self, obs, deterministic: bool = True) -> "torch.Tensor":
+        """SquashedGaussianActor.sample (continuous_actors.py:270-306) on the device:
+        obs [n, S] or [S] -> actions [n, A] (a CUDA tensor; [A] for a single row).
+        deterministic=False draws u from the device copy of the global NumPy stream."""
+        single = np.ndim(obs) == 1 if not torch.is_tensor(obs) else obs.dim() == 1
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        o = self._dev(obs, (-1, S))
+        n = int(o.shape[0])
+        out = torch.empty((n, A), dtype=torch.float32, device=self.device)
+        N.check(self.lib.sacx_actor_act(self.h, ctypes.c_void_p(o.data_ptr()), n, int(bool(deterministic)),
+                                        ctypes.c_void_p(out.data_ptr())), self.h, "actor_act")
+        self._keep_act = o
+        return out[0] if single else out
 
     # ------------------------------------------------------------------ hot path
     def step(self, n: int = 1, num_timesteps: int = 0, ts_increment: int = 1, external: bool = False,

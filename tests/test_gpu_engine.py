@@ -235,3 +235,26 @@ def test_model_fit_matches_oracle(gpu_available, eager):
             assert np.max(np.abs(a_ - b_)) < 5e-5
     assert eng.ctl()["t_model"] == steps
     eng.close()
+
+
+@pytest.mark.parametrize("deterministic,per_state_std,n", [(True, False, 37), (False, False, 37), (False, True, 5),
+                                                           (False, False, 1)])
+def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n):
+    """Behaviour-policy inference (sample(), continuous_actors.py:270-306) vs the oracle;
+    the stochastic draw advances the device stream exactly as np.random.normal(size=(n, A))."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="tanh", B=64, seed=41, normalizers="random",
+                                           per_state_std=per_state_std)
+    S, A = ocfg.S, ocfg.A
+    obs = np.random.RandomState(3).normal(size=(n, S)) * 2.0
+    eng.rng_set_state(np.random.RandomState(17).get_state())
+    ref_rs = np.random.RandomState(17)
+    got = eng.act(obs[0] if n == 1 else obs, deterministic).cpu().numpy().reshape(n, A)
+    x = (obs.astype(np.float32) - nrm.s_mean) / nrm.s_den
+    out, _ = O.mlp_forward(st.actor, x.astype(np.float64), ocfg.act)
+    mu, lraw = O.split_head(out, st.logstd, ocfg)
+    u = np.zeros((n, A)) if deterministic else O.f32_noise(ref_rs.normal(size=(n, A))).astype(np.float64)
+    pi, _ = O.head_sample(mu, lraw, u, ocfg.act_limit, np.float64)
+    assert relerr(got, pi) < 2e-5, relerr(got, pi)
+    dev, ref = eng.rng_get_state(), ref_rs.get_state()
+    assert np.array_equal(dev[1], ref[1]) and dev[2] == ref[2] and dev[3] == ref[3] and dev[4] == ref[4]
+    eng.close()
