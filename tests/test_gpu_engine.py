@@ -81,9 +81,9 @@ def test_replay_ring_fifo(gpu_available):
 
 
 def _one_step_compare(act, normalizers="identity", per_state_std=False, use_expert=False, B=256, seed=0,
-                      done_p=0.05):
+                      done_p=0.05, S=17, A=6):
     eng, ocfg, st, buf, nrm, expert = make_pair(act=act, normalizers=normalizers, per_state_std=per_state_std,
-                                               use_expert=use_expert, B=B, seed=seed, done_p=done_p)
+                                               use_expert=use_expert, B=B, seed=seed, done_p=done_p, S=S, A=A)
     N = buf["r"].shape[0]
     rs = np.random.RandomState(seed + 5)
     gen = np.random.default_rng(seed + 6)
@@ -160,6 +160,12 @@ def test_one_update_sac_eo(gpu_available):
 
 def test_one_update_small_batch(gpu_available):
     _one_step_compare("relu", B=37, seed=6)
+
+
+def test_one_update_humanoid_shapes(gpu_available):
+    """Config C3 shapes (S=376, A=17, B=1024, SAC-EO): wide layer-0 K (unfused forward),
+    multi-chunk gather rows and the 47-chunk world-model head."""
+    _one_step_compare("relu", use_expert=True, B=1024, seed=7, S=376, A=17, normalizers="random")
 
 
 @pytest.mark.parametrize("use_expert", [False, True])
