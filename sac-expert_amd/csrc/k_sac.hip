@@ -195,6 +195,60 @@ __device__ __forceinline__ void rowdot8(const float (&hv)[MAXQ], __amdgpu_buffer
     for (int u = 0; u < 8; ++u) out[u] = wave_sum(p[u]);
 }
 
+// ==================================================================== finalize
+// alpha Adam + clamp and the per-update statistics.
+__device__ float mean_rows(const float* x, int n) {
+    // deterministic: lane-strided partials then butterfly (wave 0 only)
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+    for (int i = lane; i < n; i += 64) s += x[i];
+    return wave_sum(s) / (float)n;
+}
+
+__device__ void finalize_update(const FinalArgs& f, int nred) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+    for (int i = lane; i < nred; i += 64) s += f.red[i];
+    const float ent_sum = wave_sum(s);          // sum_i (-nlp_i + H)
+    const float m_ent = ent_sum / (float)f.B;   // reduce_mean
+    const float q1 = mean_rows(f.lq, f.B);
+    const float q2 = mean_rows(f.lq + f.B, f.B);
+    float pl = mean_rows(f.lp, f.B);
+    float mse = 0.f;
+    if (f.use_expert && f.ne > 0) {
+        const int h = f.ne / 2;
+        float sm = 0.f;
+        for (int i = lane; i < h; i += 64) sm += 0.5f * (f.mse_rows[i] + f.mse_rows[i + h]);
+        mse = wave_sum(sm) / (float)h;
+        const float eps = f.ctl->epsilon;
+        pl = (1.f - eps) * pl + eps * mse;
+    }
+    if (lane == 0) {
+        Ctl* ctl = f.ctl;
+        const int64_t tnew = ctl->t_sac + 1;
+        const float alpha_old = *f.alpha;
+        const float g = -m_ent;                 // d(-alpha*m)/d alpha
+        const float lr_t = adam_lr(f.adam, GRP_ALPHA, tnew);
+        float an = adam_update(f.alpha, f.alpha_m, f.alpha_v, g, lr_t);
+        an = fmaxf(an, 1e-5f);                  // SAC_expert.py:348
+        *f.alpha = an;
+        const int64_t seq = ctl->step_seq;
+        float* st = f.stats + (size_t)(seq % f.stats_cap) * 8;
+        st[0] = q1;
+        st[1] = q2;
+        st[2] = pl;
+        st[3] = -alpha_old * m_ent;
+        st[4] = an;
+        st[5] = mse;
+        st[6] = -(m_ent - f.target_entropy);    // mean neglogp (diagnostic)
+        st[7] = (float)seq;
+        ctl->t_sac = tnew;
+        ctl->num_timesteps += ctl->ts_increment;
+        ctl->step_seq = seq + 1;
+    }
+}
+
 // ==================================================================== k_gemm
 template <bool KC, bool VEC>
 __device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t ra, const GemmProb& g, int m, bool mok, int k0,
@@ -256,6 +310,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
     const int tile = blockIdx.x;
+    if (tile >= ga.total_tiles) {          // the folded alpha.final of the previous update
+        if (ga.has_final) finalize_update(ga.fin, ga.fin.nred);
+        return;
+    }
     int p = 0;
 #pragma unroll
     for (int i = 1; i < GEMM_MAXP; ++i)
@@ -422,7 +480,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
-    const dim3 grid(a.total_tiles), block(256);
+    const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0)), block(256);
     switch (a.mode) {
     case GM_FWD:
         if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1>), grid, block, 0, s, a);
@@ -720,60 +778,6 @@ void launch_gather(const GatherArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4), dim3(256), 0, s, a);
 }
 
-// ==================================================================== finalize
-// alpha Adam + clamp and the per-update statistics.
-__device__ float mean_rows(const float* x, int n) {
-    // deterministic: lane-strided partials then butterfly (wave 0 only)
-    const int lane = threadIdx.x & 63;
-    float s = 0.f;
-    for (int i = lane; i < n; i += 64) s += x[i];
-    return wave_sum(s) / (float)n;
-}
-
-__device__ void finalize_update(const FinalArgs& f, int nred) {
-    if (threadIdx.x >= 64) return;
-    const int lane = threadIdx.x & 63;
-    float s = 0.f;
-    for (int i = lane; i < nred; i += 64) s += f.red[i];
-    const float ent_sum = wave_sum(s);          // sum_i (-nlp_i + H)
-    const float m_ent = ent_sum / (float)f.B;   // reduce_mean
-    const float q1 = mean_rows(f.lq, f.B);
-    const float q2 = mean_rows(f.lq + f.B, f.B);
-    float pl = mean_rows(f.lp, f.B);
-    float mse = 0.f;
-    if (f.use_expert && f.ne > 0) {
-        const int h = f.ne / 2;
-        float sm = 0.f;
-        for (int i = lane; i < h; i += 64) sm += 0.5f * (f.mse_rows[i] + f.mse_rows[i + h]);
-        mse = wave_sum(sm) / (float)h;
-        const float eps = f.ctl->epsilon;
-        pl = (1.f - eps) * pl + eps * mse;
-    }
-    if (lane == 0) {
-        Ctl* ctl = f.ctl;
-        const int64_t tnew = ctl->t_sac + 1;
-        const float alpha_old = *f.alpha;
-        const float g = -m_ent;                 // d(-alpha*m)/d alpha
-        const float lr_t = adam_lr(f.adam, GRP_ALPHA, tnew);
-        float an = adam_update(f.alpha, f.alpha_m, f.alpha_v, g, lr_t);
-        an = fmaxf(an, 1e-5f);                  // SAC_expert.py:348
-        *f.alpha = an;
-        const int64_t seq = ctl->step_seq;
-        float* st = f.stats + (size_t)(seq % f.stats_cap) * 8;
-        st[0] = q1;
-        st[1] = q2;
-        st[2] = pl;
-        st[3] = -alpha_old * m_ent;
-        st[4] = an;
-        st[5] = mse;
-        st[6] = -(m_ent - f.target_entropy);    // mean neglogp (diagnostic)
-        st[7] = (float)seq;
-        ctl->t_sac = tnew;
-        ctl->num_timesteps += ctl->ts_increment;
-        ctl->step_seq = seq + 1;
-    }
-}
-
 // one wave: alpha Adam + clamp and the statistics row of the update
 __global__ __launch_bounds__(64) void k_alpha_final(FinalArgs f) { finalize_update(f, f.nred); }
 
@@ -789,10 +793,10 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     float row_ent = 0.f;
-    if (row < h.total_rows) {
-        int sidx = 0;
-        for (int i = 1; i < h.nseg; ++i)
-            if (row >= h.seg[i].r0) sidx = i;
+    int sidx = 0;
+    for (int i = 1; i < h.nseg; ++i)
+        if (row >= h.seg[i].r0) sidx = i;
+    if (row < h.total_rows && row < h.seg[sidx].r1) {     // rows in the pad before alpha_row0 idle
         const HeadSeg sg = h.seg[sidx];
         const int A = h.A, Aout = h.Aout;
         const bool jok = lane < A;
@@ -836,7 +840,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
             if (sg.xq_out != nullptr)
                 sg.xq_out[(size_t)(sg.xq_row0 + row - sg.r0) * h.ldQ + h.S + j] = (pi - am_pf) / ad_pf;
             if (sg.pi_out != nullptr) sg.pi_out[(size_t)(row - sg.r0) * A + j] = pi;
-            if (row >= h.cache_row0 && h.c_t != nullptr) {
+            if (row >= h.cache_row0 && row < h.cache_row1 && h.c_t != nullptr) {
                 const size_t ci = (size_t)(row - h.cache_row0) * A + j;
                 h.c_t[ci] = t;
                 h.c_std[ci] = sd;
@@ -850,7 +854,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
             row_ent = -nlp + f.target_entropy;
         }
     }
-    if (!h.alpha_mode) return;
+    if (!h.alpha_mode || (int)blockIdx.x * 4 < h.alpha_row0) return;
     // ---- alpha: block partial of sum(-nlp + H); k_alpha_final reduces them
     if (lane == 0) red_s[wave] = row_ent;
     __syncthreads();
@@ -858,7 +862,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         float part = red_s[0] + red_s[1];
         part = part + red_s[2];
         part = part + red_s[3];
-        f.red[blockIdx.x] = part;
+        f.red[blockIdx.x - h.alpha_row0 / 4] = part;
     }
 }
 

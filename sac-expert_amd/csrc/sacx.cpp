@@ -64,7 +64,8 @@ struct Launch {
     int grid = 0, block = 256;
     double flops = 0, bytes = 0;
     int gemm_first = 0;  // index of the first problem in the host table (GEMM)
-    bool after_final = false;  // graph: waits for the previous update's alpha.final
+    bool after_final = false;  // graph: waits for the previous update's alpha branch
+    bool alpha_branch = false; // graph: runs on the side stream beside the next update's first launches
 };
 
 const char* kernel_family(Launch::Kind k) {
@@ -102,9 +103,9 @@ struct sacx_handle {
     // binding
     char* arena = nullptr;
     hipStream_t stream = nullptr;
-    hipStream_t cap_stream = nullptr, rng_stream = nullptr, fin_stream = nullptr;
+    hipStream_t cap_stream = nullptr, rng_stream = nullptr;
     bool bound = false;
-    std::vector<Launch> plan[2];
+    std::vector<Launch> plan[NSLOT];
     std::vector<Launch> mplan;
     hipGraphExec_t mgraph = nullptr;
     int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
@@ -194,7 +195,7 @@ void build_layout(sacx_handle* h) {
     // per-slot update inputs: the sampler + gather of update j+2 run while update j+1
     // executes, so everything they write is double buffered
     const int ne1 = std::max(1, h->ne);
-    for (int s = 0; s < 2; ++s) {
+    for (int s = 0; s < NSLOT; ++s) {
         const std::string sl = "slot" + std::to_string(s);
         h->add(sl + ".idx", 1, B, SACX_I32, SACX_ROLE_WORK);
         h->add(sl + ".noise", 1, h->n_norm, F, SACX_ROLE_WORK);
@@ -218,8 +219,11 @@ void build_layout(sacx_handle* h) {
     h->add("red", 1, std::max(1024, (B + 3) / 4), F, SACX_ROLE_WORK);
     // ---------------- workspace
     const int Ra = h->Ra, Rb = h->Rb, Hm0 = std::max(1, h->Hm0), Hm1 = std::max(1, h->Hm1);
-    h->add("ws.Ha1", Ra, H0, F, 0);
-    h->add("ws.Ha2", Ra, H1, F, 0);
+    // actor activations; rows [Ra4, Ra4 + B) hold the alpha evaluate() of an update
+    // (aliased ws.Hl1 / ws.Hl2) so one grouped head launch can serve both
+    const int Ra4 = (Ra + 3) & ~3;
+    const uint64_t oHa1 = h->add("ws.Ha1", Ra4 + B, H0, F, 0);
+    const uint64_t oHa2 = h->add("ws.Ha2", Ra4 + B, H1, F, 0);
     h->add("ws.c_t", Rb, A, F, 0);
     h->add("ws.c_std", Rb, A, F, 0);
     h->add("ws.c_u", Rb, A, F, 0);
@@ -247,8 +251,8 @@ void build_layout(sacx_handle* h) {
     h->add("ws.Da2", Rb, H1, F, 0);
     h->add("ws.Da1", Rb, H0, F, 0);
     h->add("ws.E", Rb, A, F, 0);
-    h->add("ws.Hl1", B, H0, F, 0);
-    h->add("ws.Hl2", B, H1, F, 0);
+    h->alias("ws.Hl1", oHa1 + (uint64_t)Ra4 * H0 * 4, B, H0, F, 0);
+    h->alias("ws.Hl2", oHa2 + (uint64_t)Ra4 * H1 * 4, B, H1, F, 0);
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
     h->add("act.H1", ACT_CAP, H0, F, 0);
@@ -460,23 +464,27 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     const int fuse_mode = fenv ? std::atoi(fenv) : -1;
     const bool fuse_a = S <= FWD2_MAX_K0, fuse_q = S + A <= FWD2_MAX_K0;
     auto fwd_pair = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1,
-                        bool fuse) {
-        int tiles = 0;
+                        bool fuse, int forced = -1, int extra_tiles = 0) -> bool {
+        int tiles = extra_tiles;      // tiles of problems folded into the same launch later
         for (auto& p : p1) tiles += ((p.M + 15) / 16) * ((p.N + 15) / 16);
         if (fuse_mode == 0 || (fuse_mode < 0 && tiles > 512)) fuse = false;
+        if (forced >= 0) fuse = fuse && forced;
         if (!fuse) {
             add_gemm(h, plan, name + "0", p0, record_probs);
             add_gemm(h, plan, name + "1", p1, record_probs);
-            return;
+            return false;
         }
         std::vector<GemmProb> pf;
         for (size_t i = 0; i < p0.size(); ++i)
             pf.push_back(prob_fwd2(p0[i].A, p0[i].lda, p0[i].M, p0[i].K, p0[i].B, p0[i].N, p0[i].C, p1[i].B,
                                    p1[i].N, p1[i].C, p1[i].act));
         add_gemm(h, plan, name, pf, record_probs);
+        return true;
     };
-    fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
-             {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a);
+    // the previous update's alpha forward (B rows) is folded into this launch (merged_body)
+    const int alpha_tiles = ((B + 15) / 16) * ((H1 + 15) / 16);
+    const bool actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
+             {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a, -1, alpha_tiles);
     // ---- actor head
     {
         Launch L{};
@@ -492,6 +500,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         a.seg[2] = {2 * B, 2 * B + ne, 1, 0, noise_e, Xm, nullptr};
         a.total_rows = h->Ra;
         a.cache_row0 = B;
+        a.cache_row1 = h->Ra;
         a.c_t = W("ws.c_t"); a.c_std = W("ws.c_std"); a.c_u = W("ws.c_u"); a.c_mask = W("ws.c_mask");
         a.alpha_mode = 0;
         L.grid = (h->Ra + 3) / 4;
@@ -633,8 +642,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, "actor.adam", pw, record_probs);
     }
     // ---- alpha: updated actor on s, evaluate, Adam on alpha, statistics
+    const size_t alpha_first = plan.size();
+    // the alpha forward is folded into the next update's actor forward (merged_body): same fusion
     fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
-             {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, fuse_a);
+             {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, fuse_a, actor_fused ? 1 : 0);
     {
         Launch L{};
         L.kind = Launch::AHEAD;
@@ -674,6 +685,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.block = 64;
         L.bytes = 4.0 * (f.nred + 3.0 * B + ne);
         plan.push_back(L);
+    }
+    // alpha.fwd .. alpha.final only feed the next update's q.head
+    for (size_t i = alpha_first; i < plan.size(); ++i) plan[i].alpha_branch = true;
+    {
     }
 }
 
@@ -767,10 +782,80 @@ void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
     }
 }
 
-// Captured chain of G updates on three streams:
-//   rs: sampler + gather of update j (j >= 2 waits for update j-2, the last reader of its slot)
-//   cs: the update body (waits for its inputs; q.head waits for the previous alpha.final)
-//   fs: alpha.final of update j (alpha Adam + statistics), off the critical path
+// Appends the problems of GEMM launch `b` to launch `a` (same mode; tile ranges follow a's).
+bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
+    if (a.mode != b.mode || a.nprob + b.nprob > GEMM_MAXP) return false;
+    for (int i = 0; i < b.nprob; ++i) {
+        GemmProb p = b.probs[i];
+        p.tile_begin += a.total_tiles;
+        a.probs[a.nprob + i] = p;
+    }
+    a.nprob += b.nprob;
+    a.total_tiles += b.total_tiles;
+    a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec && b.vec);
+    return true;
+}
+
+// The main-stream launches of update `slot` with the alpha branch (alpha.fwd, alpha.head,
+// alpha.final) of the PREVIOUS update (prev_slot >= 0) folded in:
+//   alpha.fwd   -> extra problems of this update's actor forward launch(es);
+//   alpha.head  -> an extra segment (rows from round4(Ra)) of this update's actor.head;
+//   alpha.final -> one extra workgroup of the first GEMM after actor.head (q.fwd).
+// Each folded piece computes exactly what it computed standalone (bit-identical results);
+// the update's own alpha branch is left out (folded into the next update, or the tail).
+// Returns false if the plans do not line up (then the caller keeps the branch separate).
+bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& out) {
+    out.clear();
+    std::vector<const Launch*> pg;
+    const Launch *ph = nullptr, *pf = nullptr;
+    if (prev_slot >= 0)
+        for (const Launch& L : h->plan[prev_slot]) {
+            if (!L.alpha_branch) continue;
+            if (L.kind == Launch::GEMM) pg.push_back(&L);
+            else if (L.kind == Launch::AHEAD) ph = &L;
+            else if (L.kind == Launch::FINAL) pf = &L;
+        }
+    size_t gi = 0;
+    bool head_done = prev_slot < 0, final_done = prev_slot < 0;
+    for (const Launch& L : h->plan[slot]) {
+        if (is_prologue(L) || L.alpha_branch) continue;
+        Launch C = L;
+        if (prev_slot >= 0) {
+            if (C.kind == Launch::GEMM && !head_done && gi < pg.size() && C.name.rfind("actor.fwd", 0) == 0) {
+                if (!merge_gemm(C.gemm, pg[gi]->gemm)) return false;
+                C.name += "+alpha";
+                ++gi;
+            } else if (C.kind == Launch::AHEAD && !head_done && ph) {
+                HeadArgs& a = C.head;
+                const HeadSeg& sg = ph->head.seg[0];
+                if (a.nseg >= 4) return false;
+                const int r0 = (a.total_rows + 3) & ~3;
+                HeadSeg m = sg;
+                m.r0 = r0;
+                m.r1 = r0 + (sg.r1 - sg.r0);
+                a.seg[a.nseg++] = m;
+                a.total_rows = m.r1;
+                a.alpha_mode = 1;
+                a.alpha_row0 = r0;
+                C.fin = ph->fin;
+                C.name += "+alpha";
+                head_done = true;
+            } else if (C.kind == Launch::GEMM && head_done && !final_done && pf &&
+                       (C.gemm.mode == GM_FWD || C.gemm.mode == GM_FWD2)) {
+                C.gemm.has_final = 1;
+                C.gemm.fin = pf->fin;
+                C.name += "+alpha.final";
+                final_done = true;
+            }
+        }
+        out.push_back(C);
+    }
+    return gi == pg.size() && head_done && final_done;
+}
+
+// Captured chain of G updates on two streams (see the fork branch below):
+//   cs: the updates, alpha branches folded one update later (merged_body) + a tail;
+//   rs: sampler + gather, two updates ahead (slot double buffer).
 // skip_kind >= 0 leaves that launch kind out (measurement only: sacx_time_graph)
 int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1) {
     auto key = std::make_tuple(G, with_rng ? 1 : 0, skip_kind);
@@ -779,7 +864,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         *out = it->second;
         return 0;
     }
-    hipStream_t cs = h->cap_stream, rs = h->rng_stream, fs = h->fin_stream;
+    hipStream_t cs = h->cap_stream, rs = h->rng_stream;
     const int nev = 3 * G + 1;
     for (int i = (int)h->events.size(); i < nev; ++i) {
         hipEvent_t e;
@@ -792,14 +877,19 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     hipEvent_t evFork = h->events[3 * G];
     HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     const bool fork = with_rng && std::getenv("SACX_NO_FORK") == nullptr;
-    // diagnostics: keep alpha.final / gather on the main stream
-    const bool final_main = std::getenv("SACX_FINAL_MAIN") != nullptr;
+    // diagnostics: SACX_GATHER_MAIN keeps the gather on the main stream; SACX_MERGE_ALPHA=0
+    // keeps each alpha branch as separate launches
     const bool gather_main = std::getenv("SACX_GATHER_MAIN") != nullptr;
     if (fork) {
+        // cs: the updates, each with the previous update's alpha branch folded into its first
+        //     launches (merged_body), plus the last update's alpha branch as a tail;
+        // rs: sampler + gather of update j+2 into slot (j+2)%3 == (j-1)%3, once update j's
+        //     actor.head (the last reader of that slot, through the folded alpha rows) has run.
+        const bool merge = std::getenv("SACX_MERGE_ALPHA") == nullptr || std::atoi(std::getenv("SACX_MERGE_ALPHA"));
         HIPCHK(h, hipEventRecord(evFork, cs));
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
         auto prologue = [&](int j) {
-            for (const Launch& L : h->plan[j & 1]) {
+            for (const Launch& L : h->plan[j % NSLOT]) {
                 if (!is_prologue(L) || (gather_main && L.kind == Launch::GATHER)) continue;
                 Launch C = L;
                 if (C.kind == Launch::RNG) C.rng.reset_seq = (j == 0);
@@ -809,26 +899,43 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         };
         HIPCHK(h, prologue(0));
         if (G > 1) HIPCHK(h, prologue(1));
+        std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
             HIPCHK(h, hipStreamWaitEvent(cs, evR[j], 0));
-            const Launch* fin = nullptr;
-            for (const Launch& L : h->plan[j & 1]) {
-                if (L.kind == Launch::RNG || (L.kind == Launch::GATHER && !gather_main)) continue;
-                if ((int)L.kind == skip_kind) continue;
-                if (L.kind == Launch::FINAL && !final_main) { fin = &L; continue; }
-                if (L.after_final && j > 0) HIPCHK(h, hipStreamWaitEvent(cs, evF[j - 1], 0));
-                enqueue(L, h, cs);
+            const int slot = j % NSLOT, prev = j > 0 ? (j - 1) % NSLOT : -1;
+            const bool folded = merge && merged_body(h, slot, prev, body);
+            if (!folded) {                    // plain order: previous alpha branch, then this body
+                body.clear();
+                if (prev >= 0)
+                    for (const Launch& L : h->plan[prev])
+                        if (L.alpha_branch) body.push_back(L);
+                for (const Launch& L : h->plan[slot])
+                    if (!is_prologue(L) && !L.alpha_branch) body.push_back(L);
             }
-            HIPCHK(h, hipEventRecord(evS[j], cs));
-            HIPCHK(h, hipStreamWaitEvent(fs, evS[j], 0));
-            if (fin) enqueue(*fin, h, fs);
-            HIPCHK(h, hipEventRecord(evF[j], fs));
-            if (j + 2 < G) {
+            bool slot_free_recorded = false;
+            for (const Launch& L : body) {
+                if ((int)L.kind == skip_kind) {
+                    // ablation: the alpha.final folded into a skipped GEMM still runs
+                    if (L.kind == Launch::GEMM && L.gemm.has_final) launch_alpha_final(L.gemm.fin, cs);
+                    continue;
+                }
+                enqueue(L, h, cs);
+                // slot (j-1)%3 is read last by the folded alpha rows of this update's actor.head
+                if (!slot_free_recorded && L.kind == Launch::AHEAD) {
+                    HIPCHK(h, hipEventRecord(evS[j], cs));
+                    slot_free_recorded = true;
+                }
+            }
+            if (!slot_free_recorded) HIPCHK(h, hipEventRecord(evS[j], cs));
+            if (j + 2 < G) {                  // slot (j+2)%3 == (j-1)%3: free after evS[j]
                 HIPCHK(h, hipStreamWaitEvent(rs, evS[j], 0));
                 HIPCHK(h, prologue(j + 2));
             }
         }
-        HIPCHK(h, hipStreamWaitEvent(cs, evF[G - 1], 0));   // join the side streams
+        for (const Launch& L : h->plan[(G - 1) % NSLOT])   // tail: the last update's alpha branch
+            if (L.alpha_branch && (int)L.kind != skip_kind) enqueue(L, h, cs);
+        HIPCHK(h, hipEventRecord(evF[0], rs));
+        HIPCHK(h, hipStreamWaitEvent(cs, evF[0], 0));    // join the sampler stream
     } else {
         if (skip_kind >= 0) return fail(h, "kernel ablation needs the forked sampler graph");
         for (int j = 0; j < G; ++j) enqueue_step(h, 0, with_rng, cs);
@@ -917,7 +1024,6 @@ void sacx_destroy(sacx_handle* h) {
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
-    if (h->fin_stream) (void)hipStreamDestroy(h->fin_stream);
     delete h;
 }
 
@@ -953,18 +1059,18 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->arena = static_cast<char*>(arena);
     h->stream = static_cast<hipStream_t>(stream);
     h->probs.clear();
-    build_plan(h, 0, true);
-    build_plan(h, 1, false);
-    if (h->plan[0].size() != h->plan[1].size()) return fail(h, "internal: slot plans differ");
-    for (size_t i = 0; i < h->plan[0].size(); ++i)
-        if (h->plan[0][i].kind == Launch::GEMM &&
-            (h->plan[0][i].gemm_first != h->plan[1][i].gemm_first ||
-             h->plan[0][i].gemm_first + h->plan[0][i].gemm.nprob > (int)h->probs.size()))
-            return fail(h, "internal: GEMM problem table mismatch");
+    for (int sl = 0; sl < NSLOT; ++sl) build_plan(h, sl, sl == 0);
+    for (int sl = 1; sl < NSLOT; ++sl) {
+        if (h->plan[0].size() != h->plan[sl].size()) return fail(h, "internal: slot plans differ");
+        for (size_t i = 0; i < h->plan[0].size(); ++i)
+            if (h->plan[0][i].kind == Launch::GEMM &&
+                (h->plan[0][i].gemm_first != h->plan[sl][i].gemm_first ||
+                 h->plan[0][i].gemm_first + h->plan[0][i].gemm.nprob > (int)h->probs.size()))
+                return fail(h, "internal: GEMM problem table mismatch");
+    }
     build_model_plan(h);
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
-    HIPCHK(h, hipStreamCreateWithFlags(&h->fin_stream, hipStreamNonBlocking));
     h->bound = true;
     return 0;
 }

@@ -9,6 +9,10 @@ namespace sacx {
 enum Act { ACT_RELU = 0, ACT_TANH = 1, ACT_ELU = 2, ACT_NONE = 3 };
 
 // Device control block (lives in the arena, segment "ctl", int64 x 32).
+// update-input slots: the sampler + gather run two updates ahead of the update that
+// consumes them, and an update's alpha rows are read one update later (folded launches)
+#define NSLOT 3
+
 struct Ctl {
     int64_t t_sac;          // completed updates (Adam iterations of q / pi / alpha optimisers)
     int64_t t_model;        // model optimiser iterations
@@ -23,8 +27,8 @@ struct Ctl {
     float pad_f[3];
     int64_t mfit_seq;       // model-fit step sequence (index ring / stats)
     int64_t rng_seq;        // update number the next sampler launch draws for
-    int64_t pseq[2];        // update number whose randoms slot 0 / 1 holds (expert perm ring index)
-    int64_t reserved[10];
+    int64_t pseq[NSLOT];    // update number whose randoms slot 0 / 1 / 2 holds (expert perm ring index)
+    int64_t reserved[9];
 };
 static_assert(sizeof(Ctl) <= 32 * 8, "ctl segment is 32 int64");
 
@@ -75,6 +79,20 @@ struct GemmProb {
     float* C0;             // GM_FWD2: layer-0 output H1 [M x K] (row stride K)
 };
 
+struct FinalArgs {
+    float* alpha; float* alpha_m; float* alpha_v;
+    Ctl* ctl;
+    AdamConsts adam;
+    float target_entropy;
+    int32_t B, ne, use_expert;
+    const float* lq;        // [2, B]
+    const float* lp;        // [B]
+    const float* mse_rows;  // [ne]
+    float* red;             // partial slots
+    int32_t nred;           // number of partials (alpha.head workgroups)
+    float* stats; int32_t stats_cap;
+};
+
 #define GEMM_MAXP 8
 struct GemmArgs {
     GemmProb probs[GEMM_MAXP];   // by value: no dependent global load to find a tile's problem
@@ -86,6 +104,10 @@ struct GemmArgs {
     int64_t p_stride;      // floats between params / adam_m / adam_v blocks
     const Ctl* ctl;
     AdamConsts adam;
+    // one extra workgroup (blockIdx == total_tiles) finalises the PREVIOUS update's alpha
+    // (alpha.final folded into a launch of the next update, see get_graph)
+    int32_t has_final;
+    FinalArgs fin;
 };
 
 // ---------------------------------------------------------------- sampler + gather
@@ -135,13 +157,15 @@ struct HeadArgs {
     float lim;
     const float *a_mean, *a_den;
     int32_t nseg;
-    HeadSeg seg[3];
+    HeadSeg seg[4];
     int32_t total_rows;
     // backward cache (rows >= cache_row0 are cached at [row - cache_row0])
-    int32_t cache_row0;
+    int32_t cache_row0, cache_row1;
     float* c_t; float* c_std; float* c_u; float* c_mask;
-    // alpha mode: reduce sum(-nlp + target_entropy) and finalise the update
+    // alpha mode: rows >= alpha_row0 (a multiple of 4: whole workgroups) are the alpha
+    // evaluate() of an update; their workgroups write partials of sum(-nlp + H) to fin.red
     int32_t alpha_mode;
+    int32_t alpha_row0;
 };
 
 // ---------------------------------------------------------------- Q heads
@@ -194,19 +218,7 @@ struct ActorBwdArgs {
 };
 
 // ---------------------------------------------------------------- finalize (alpha + stats)
-struct FinalArgs {
-    float* alpha; float* alpha_m; float* alpha_v;
-    Ctl* ctl;
-    AdamConsts adam;
-    float target_entropy;
-    int32_t B, ne, use_expert;
-    const float* lq;        // [2, B]
-    const float* lp;        // [B]
-    const float* mse_rows;  // [ne]
-    float* red;             // partial slots
-    int32_t nred;           // number of partials (alpha.head workgroups)
-    float* stats; int32_t stats_cap;
-};
+
 
 struct AppendArgs {
     float* replay; int64_t cap; int32_t stride; int32_t S, A;

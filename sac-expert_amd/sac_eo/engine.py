@@ -21,7 +21,7 @@ _ESZ = {0: 4, 1: 4, 2: 8, 3: 4, 4: 8}
 
 # ctl field indices (int64 slots, see csrc/sacx_internal.h struct Ctl)
 CTL = {"t_sac": 0, "t_model": 1, "num_timesteps": 2, "ts_increment": 3, "cur_size": 4, "start": 5,
-       "step_seq": 6, "n_expert": 7, "mfit_seq": 14, "rng_seq": 15, "pseq0": 16, "pseq1": 17}
+       "step_seq": 6, "n_expert": 7, "mfit_seq": 14, "rng_seq": 15, "pseq0": 16, "pseq1": 17, "pseq2": 18}
 
 
 @dataclasses.dataclass

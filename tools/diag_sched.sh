@@ -10,10 +10,6 @@ run() {
   echo "$tag $(grep -o '"value": [0-9.]*' gpurun_out/sched_$tag.log)"
 }
 run base X=1
-run nofork SACX_NO_FORK=1
-run finalmain SACX_FINAL_MAIN=1
-run gathermain SACX_GATHER_MAIN=1
-run bothmain SACX_FINAL_MAIN=1 SACX_GATHER_MAIN=1
-run g16 SACX_GRAPH_STEPS=16
-run g32 SACX_GRAPH_STEPS=32
-run g2 SACX_GRAPH_STEPS=2
+run nomerge SACX_MERGE_ALPHA=0
+run g64 SACX_GRAPH_STEPS=64
+run nofuse SACX_FUSE=0

@@ -1,0 +1,22 @@
+"""Print one update's worth of the kernel trace: queue, start, duration, gap to the previous
+kernel on the same queue.  usage: python tools/trace_view.py <kernel_trace.csv> [n]"""
+import csv
+import sys
+
+rows = [r for r in csv.DictReader(open(sys.argv[1])) if "sacx" in r["Kernel_Name"]]
+for r in rows:
+    r["s"], r["e"] = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+rows.sort(key=lambda r: r["s"])
+n = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+mid = len(rows) * 2 // 3
+w = rows[mid: mid + n]
+t0 = w[0]["s"]
+last = {}
+busy = 0
+for r in w:
+    q = r["Queue_Id"]
+    gap = (r["s"] - last[q]) / 1e3 if q in last else float("nan")
+    last[q] = r["e"]
+    name = r["Kernel_Name"].replace("sacx::", "").replace("void ", "").split("(")[0]
+    print(f"q{q:>3s} {name:22s} start={(r['s'] - t0) / 1e3:8.2f} dur={(r['e'] - r['s']) / 1e3:6.2f} "
+          f"gap={gap:6.2f} grid={int(r['Grid_Size_X']) // int(r['Workgroup_Size_X'])}")
