@@ -49,7 +49,7 @@ def build_engine(cfgd, seeds, device):
     S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
-                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "32")))
+                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "128")))
     eng = Engine(ecfg, device=device)
     rng = np.random.default_rng(seeds["setup"])        # weights (init_seeds(setup_seed) then nets)
     eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))

@@ -55,7 +55,7 @@ typedef struct sacx_config {
     int32_t model_activation;   /* --model_activations */
     int32_t model_batch;        /* --model_batch_size */
     int32_t target_update_int;  /* --target_update_int */
-    int32_t graph_steps;        /* updates per captured hipGraph (0 -> 32, max 64) */
+    int32_t graph_steps;        /* updates per captured hipGraph (0 -> 128, max 256) */
     int32_t stats_capacity;     /* rows of the per-update statistics ring (0 -> 4096) */
     int32_t perm_capacity;      /* per-update expert permutations held on device (0 -> 4096) */
     float gamma;                /* --gamma */

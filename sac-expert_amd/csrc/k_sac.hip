@@ -585,6 +585,10 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
     }
     __syncthreads();
 
+  for (int u = 0; u < a.nupd; ++u) {
+    // update u of the batch: its randint + normals, in stream order, into slot (slot + u)
+    int32_t* const out_idx = a.out_idx ? (int32_t*)((char*)a.out_idx + u * a.slot_bytes) : nullptr;
+    float* const out_norm = (float*)((char*)a.out_norm + u * a.slot_bytes);
     // ---------------- randint(high, n_int)
     if (a.n_int > 0) {
         const uint64_t high = (uint64_t)a.ctl->cur_size;
@@ -595,7 +599,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
         int done = 0;
         while (done < a.n_int) {
             if (rng == 0) {
-                for (int i = t; i < a.n_int; i += RNG_THREADS) a.out_idx[i] = 0;
+                for (int i = t; i < a.n_int; i += RNG_THREADS) out_idx[i] = 0;
                 break;
             }
             if (pos == 624) {
@@ -618,7 +622,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
             int total;
             const int rank = block_rank(acc, wtot, total);
             const int need = a.n_int - done;
-            if (acc && rank < need) a.out_idx[done + rank] = (int32_t)v;
+            if (acc && rank < need) out_idx[done + rank] = (int32_t)v;
             if (acc && rank == need - 1) sh_last = t;
             __syncthreads();
             if (total >= need) {
@@ -635,7 +639,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
     // ---------------- n_norm x gauss
     int oi = 0;
     if (a.n_norm > 0 && sh_has) {
-        if (t == 0) a.out_norm[0] = (float)sh_gauss;
+        if (t == 0) out_norm[0] = (float)sh_gauss;
         oi = 1;
         __syncthreads();
         if (t == 0) { sh_has = 0; sh_gauss = 0.0; }
@@ -669,9 +673,9 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
         const int need_pairs = (need_vals + 1) >> 1;
         if (acc && rank < need_pairs) {
             const int o = oi + 2 * rank;
-            a.out_norm[o] = (float)(f * x2);
+            out_norm[o] = (float)(f * x2);
             if (o + 1 < a.n_norm) {
-                a.out_norm[o + 1] = (float)(f * x1);
+                out_norm[o + 1] = (float)(f * x1);
             } else {
                 sh_gauss = f * x1;
                 sh_has = 1;
@@ -698,6 +702,9 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
         __syncthreads();
     }
 
+    __syncthreads();
+  }
+
     for (int i = t; i < 624; i += RNG_THREADS) a.st->key[i] = mt[i];
     if (t == 0) {
         a.st->pos = pos;
@@ -706,8 +713,8 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
         // the update these randoms belong to (the sampler runs ahead of the updates)
         if (a.slot >= 0) {
             const int64_t seq = a.reset_seq ? a.ctl->step_seq : a.ctl->rng_seq;
-            a.ctl->pseq[a.slot] = seq;
-            a.ctl->rng_seq = seq + 1;
+            for (int u = 0; u < a.nupd; ++u) a.ctl->pseq[a.slot + u] = seq + u;
+            a.ctl->rng_seq = seq + a.nupd;
         }
     }
 }
@@ -718,9 +725,18 @@ void launch_rng(const RngArgs& a, hipStream_t s) {
 
 // ==================================================================== k_gather
 // one wave per sampled row (then per expert row); rows are [s | a | sp | r | d]
-__global__ __launch_bounds__(256) void k_gather(GatherArgs g) {
+__global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
+    // slot (ga.slot + blockIdx.y): every slot buffer sits at a fixed distance from slot 0's
+    GatherArgs g = ga;
+    {
+        const int64_t off = (int64_t)blockIdx.y * ga.slot_bytes;
+        auto sh = [off](auto* p) { return p ? (decltype(p))((char*)p + off) : p; };
+        g.idx = sh(ga.idx); g.Xa = sh(ga.Xa); g.Xq = sh(ga.Xq); g.Xt = sh(ga.Xt); g.Xp = sh(ga.Xp);
+        g.Xm = sh(ga.Xm); g.r = sh(ga.r); g.d = sh(ga.d); g.se_raw = sh(ga.se_raw); g.spe_raw = sh(ga.spe_raw);
+        g.slot = ga.slot + (int)blockIdx.y;
+    }
     const int S = g.S, A = g.A;
     const __amdgpu_buffer_rsrc_t rsm = rs(g.s_mean), rsd = rs(g.s_den), ram = rs(g.a_mean), rad = rs(g.a_den);
     if (row < g.B) {
@@ -775,7 +791,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs g) {
 
 void launch_gather(const GatherArgs& a, hipStream_t s) {
     const int rows = a.B + a.ne;
-    hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4, a.nupd > 0 ? a.nupd : 1), dim3(256), 0, s, a);
 }
 
 // one wave: alpha Adam + clamp and the statistics row of the update

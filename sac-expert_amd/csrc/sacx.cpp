@@ -93,7 +93,7 @@ struct sacx_handle {
     int S = 0, A = 0, H0 = 0, H1 = 0, B = 0, Aout = 0, ne = 0, Hm0 = 0, Hm1 = 0, ecap = 0;
     int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0, act = 0, mact = 0;
     int64_t cap = 0;
-    int graph_steps = 32, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
+    int graph_steps = 128, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
     // layout
     std::vector<SegInfo> segs;
     std::map<std::string, size_t> seg_index;
@@ -106,6 +106,8 @@ struct sacx_handle {
     hipStream_t cap_stream = nullptr, rng_stream = nullptr;
     bool bound = false;
     std::vector<Launch> plan[NSLOT];
+    int64_t slot_bytes = 0;   // distance between consecutive update-input slots
+    int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
     std::vector<Launch> mplan;
     hipGraphExec_t mgraph = nullptr;
     int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
@@ -128,6 +130,7 @@ struct sacx_handle {
         seg_index[name] = segs.size() - 1;
     }
     const SegInfo& seg(const std::string& n) const { return segs.at(seg_index.at(n)); }
+    uint64_t off_of(const std::string& n) const { return seg(n).off; }
     template <class T>
     T* ptr(const std::string& n) const { return reinterpret_cast<T*>(arena + seg(n).off); }
     float* f(const std::string& n) const { return ptr<float>(n); }
@@ -209,6 +212,13 @@ void build_layout(sacx_handle* h) {
         h->add(sl + ".se_raw", ne1, S, F, 0);
         h->add(sl + ".spe_raw", ne1, S, F, 0);
     }
+    h->slot_bytes = (int64_t)(h->off_of("slot1.idx") - h->off_of("slot0.idx"));
+    for (int k = 1; k < NSLOT; ++k)      // the batched sampler / gather address slot k as slot 0 + k * slot_bytes
+        for (const char* nm : {".idx", ".noise", ".Xa", ".Xq", ".Xt", ".Xp", ".Xm", ".r", ".d", ".se_raw", ".spe_raw"})
+            if (h->off_of("slot" + std::to_string(k) + nm) != h->off_of(std::string("slot0") + nm) + k * (uint64_t)h->slot_bytes) {
+                fprintf(stderr, "sacx: slot layout is not uniform\n");
+                abort();
+            }
     // ---------------- data
     h->add("replay", h->cap, h->stride, F, SACX_ROLE_STATE);
     const int ecap = std::max(1, h->ecap);
@@ -432,6 +442,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.rng.out_norm = noise;
         L.rng.slot = slot;
         L.rng.reset_seq = 1;   // cleared for the chained launches of a captured graph
+        L.rng.nupd = 1;
+        L.rng.slot_bytes = h->slot_bytes;
         L.grid = 1;
         L.block = 1024;
         L.bytes = 4.0 * (B + h->n_norm) + 2.0 * sizeof(RngState);
@@ -448,7 +460,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den");
         g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
         g.Xa = Xa; g.ldS = ldS; g.Xq = Xq; g.Xt = Xt; g.Xp = Xp; g.Xm = Xm; g.ldQ = ldQ;
-        g.r = r_in; g.d = d_in; g.slot = slot;
+        g.r = r_in; g.d = d_in; g.slot = slot; g.nupd = 1; g.slot_bytes = h->slot_bytes;
         g.exp_s = W("expert.s"); g.exp_sp = W("expert.sp");
         g.perm_ring = h->ptr<int32_t>("perm"); g.perm_cap = h->perm_cap;
         g.se_raw = se_raw; g.spe_raw = spe_raw;
@@ -888,21 +900,44 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         const bool merge = std::getenv("SACX_MERGE_ALPHA") == nullptr || std::atoi(std::getenv("SACX_MERGE_ALPHA"));
         HIPCHK(h, hipEventRecord(evFork, cs));
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
-        auto prologue = [&](int j) {
-            for (const Launch& L : h->plan[j % NSLOT]) {
+        // Sampler batches [s, e): one k_rng launch draws updates s..e-1 in stream order and one
+        // gather fills their slots.  Sizes ramp 1, 2, 4, 4, ... so the first update of the graph
+        // waits for one update's draws only.  Slot u%nslot is last read through update u's folded
+        // alpha rows in update u+1's actor.head, so batch [s, e) is drawn after the actor.head of
+        // update e-nslot (at graph start when e <= nslot) and must be done before update s.
+        std::vector<std::pair<int, int>> batches;
+        const int nbatch = h->nbatch, nslot = 2 * h->nbatch;
+        for (int s0 = 0, sz = 1; s0 < G; s0 += sz, sz = std::min(nbatch, 2 * sz))
+            batches.push_back({s0, std::min(G, s0 + std::min(nbatch, sz))});
+        for (int b = 0; b + 1 < (int)batches.size(); ++b)      // sizes must follow the ramp exactly
+            if (batches[b + 1].first != batches[b].second) return fail(h, "internal: sampler batches");
+        auto prologue = [&](int b) {
+            const int j0 = batches[b].first, n = batches[b].second - j0;
+            for (const Launch& L : h->plan[j0 % nslot]) {
                 if (!is_prologue(L) || (gather_main && L.kind == Launch::GATHER)) continue;
+                if ((int)L.kind == skip_kind) continue;   // ablation of the sampler (stale randoms)
                 Launch C = L;
-                if (C.kind == Launch::RNG) C.rng.reset_seq = (j == 0);
+                if (C.kind == Launch::RNG) {
+                    C.rng.reset_seq = (b == 0);
+                    C.rng.nupd = n;
+                } else {
+                    C.gather.nupd = n;
+                }
                 enqueue(C, h, rs);
             }
-            return hipEventRecord(evR[j], rs);
+            return hipEventRecord(evR[b], rs);
         };
-        HIPCHK(h, prologue(0));
-        if (G > 1) HIPCHK(h, prologue(1));
+        std::vector<int> batch_of(G, -1), emit_after(batches.size(), -1);
+        for (int b = 0; b < (int)batches.size(); ++b) {
+            batch_of[batches[b].first] = b;
+            emit_after[b] = batches[b].second - nslot;          // < 0: slots fresh at graph start
+        }
+        for (int b = 0; b < (int)batches.size(); ++b)
+            if (emit_after[b] < 0) HIPCHK(h, prologue(b));
         std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
-            HIPCHK(h, hipStreamWaitEvent(cs, evR[j], 0));
-            const int slot = j % NSLOT, prev = j > 0 ? (j - 1) % NSLOT : -1;
+            if (batch_of[j] >= 0) HIPCHK(h, hipStreamWaitEvent(cs, evR[batch_of[j]], 0));
+            const int slot = j % nslot, prev = j > 0 ? (j - 1) % nslot : -1;
             const bool folded = merge && merged_body(h, slot, prev, body);
             if (!folded) {                    // plain order: previous alpha branch, then this body
                 body.clear();
@@ -912,7 +947,10 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 for (const Launch& L : h->plan[slot])
                     if (!is_prologue(L) && !L.alpha_branch) body.push_back(L);
             }
-            bool slot_free_recorded = false;
+            std::vector<int> due;               // batches whose slots this update's actor.head frees
+            for (int b = 0; b < (int)batches.size(); ++b)
+                if (emit_after[b] == j) due.push_back(b);
+            bool recorded = false;
             for (const Launch& L : body) {
                 if ((int)L.kind == skip_kind) {
                     // ablation: the alpha.final folded into a skipped GEMM still runs
@@ -920,19 +958,18 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                     continue;
                 }
                 enqueue(L, h, cs);
-                // slot (j-1)%3 is read last by the folded alpha rows of this update's actor.head
-                if (!slot_free_recorded && L.kind == Launch::AHEAD) {
+                if (!due.empty() && !recorded && L.kind == Launch::AHEAD) {
                     HIPCHK(h, hipEventRecord(evS[j], cs));
-                    slot_free_recorded = true;
+                    recorded = true;
                 }
             }
-            if (!slot_free_recorded) HIPCHK(h, hipEventRecord(evS[j], cs));
-            if (j + 2 < G) {                  // slot (j+2)%3 == (j-1)%3: free after evS[j]
+            if (!due.empty()) {
+                if (!recorded) HIPCHK(h, hipEventRecord(evS[j], cs));
                 HIPCHK(h, hipStreamWaitEvent(rs, evS[j], 0));
-                HIPCHK(h, prologue(j + 2));
+                for (int b : due) HIPCHK(h, prologue(b));
             }
         }
-        for (const Launch& L : h->plan[(G - 1) % NSLOT])   // tail: the last update's alpha branch
+        for (const Launch& L : h->plan[(G - 1) % nslot])   // tail: the last update's alpha branch
             if (L.alpha_branch && (int)L.kind != skip_kind) enqueue(L, h, cs);
         HIPCHK(h, hipEventRecord(evF[0], rs));
         HIPCHK(h, hipStreamWaitEvent(cs, evF[0], 0));    // join the sampler stream
@@ -1004,7 +1041,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->Rb = h->B + h->ne;
     h->n_norm = (3 * h->B + h->ne) * h->A;
     if (cfg->graph_steps > 0) h->graph_steps = cfg->graph_steps;
-    if (h->graph_steps > 64) h->graph_steps = 64;
+    if (h->graph_steps > 256) h->graph_steps = 256;
     if (h->graph_steps > 1 && (h->graph_steps & 1)) h->graph_steps += 1;
     if (cfg->stats_capacity > 0) h->stats_cap = cfg->stats_capacity;
     if (cfg->perm_capacity > 0) h->perm_cap = cfg->perm_capacity;
@@ -1059,6 +1096,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->arena = static_cast<char*>(arena);
     h->stream = static_cast<hipStream_t>(stream);
     h->probs.clear();
+    if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     for (int sl = 0; sl < NSLOT; ++sl) build_plan(h, sl, sl == 0);
     for (int sl = 1; sl < NSLOT; ++sl) {
         if (h->plan[0].size() != h->plan[sl].size()) return fail(h, "internal: slot plans differ");
@@ -1172,10 +1210,14 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
             if (get_graph(h, G, !ext, &g)) return -1;
             for (int64_t i = 0; i < q; ++i) HIPCHK(h, hipGraphLaunch(g, h->stream));
         }
-        if (r > 0) {
-            hipGraphExec_t g1;
-            if (get_graph(h, 1, !ext, &g1)) return -1;
-            for (int64_t i = 0; i < r; ++i) HIPCHK(h, hipGraphLaunch(g1, h->stream));
+        // remainder: cached graphs of decreasing powers of two (each graph pays its own
+        // sampler start-up and alpha tail, so a few long graphs beat many single updates)
+        for (int p = 1 << 30; r > 0 && p >= 1; p >>= 1) {
+            if (p > r || p >= G) continue;
+            hipGraphExec_t gp;
+            if (get_graph(h, p, !ext, &gp)) return -1;
+            HIPCHK(h, hipGraphLaunch(gp, h->stream));
+            r -= p;
         }
     }
     h->seq_host += n_steps;
@@ -1284,7 +1326,7 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
             RngArgs r{};
             r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
             r.n_int = 0; r.n_norm = m * A; r.out_idx = nullptr; r.out_norm = noise;
-            r.slot = -1; r.reset_seq = 0;
+            r.slot = -1; r.reset_seq = 0; r.nupd = 1;
             launch_rng(r, h->stream);
         }
         launch_obs_norm(obs + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
@@ -1316,8 +1358,7 @@ int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, 
     if (skip_kernel && skip_kernel[0]) {
         for (int k = Launch::RNG; k <= Launch::MFINAL; ++k)
             if (std::strcmp(kernel_family((Launch::Kind)k), skip_kernel) == 0) skip = k;
-        if (skip < 0 || skip == Launch::RNG || skip == Launch::GATHER)
-            return fail(h, "unknown or non-removable kernel family");
+        if (skip < 0 || skip == Launch::GATHER) return fail(h, "unknown or non-removable kernel family");
     }
     hipGraphExec_t g;
     if (get_graph(h, h->graph_steps, true, &g, skip)) return -1;

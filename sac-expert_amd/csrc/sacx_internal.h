@@ -9,9 +9,11 @@ namespace sacx {
 enum Act { ACT_RELU = 0, ACT_TANH = 1, ACT_ELU = 2, ACT_NONE = 3 };
 
 // Device control block (lives in the arena, segment "ctl", int64 x 32).
-// update-input slots: the sampler + gather run two updates ahead of the update that
-// consumes them, and an update's alpha rows are read one update later (folded launches)
-#define NSLOT 3
+// update-input slots: the sampler + gather fill them a batch of NBATCH updates at a time,
+// one batch ahead of the updates that consume them (and an update's alpha rows are read
+// one update later by the folded launches), so two batches of slots rotate
+#define NBATCH_MAX 8
+#define NSLOT (2 * NBATCH_MAX)
 
 struct Ctl {
     int64_t t_sac;          // completed updates (Adam iterations of q / pi / alpha optimisers)
@@ -27,8 +29,7 @@ struct Ctl {
     float pad_f[3];
     int64_t mfit_seq;       // model-fit step sequence (index ring / stats)
     int64_t rng_seq;        // update number the next sampler launch draws for
-    int64_t pseq[NSLOT];    // update number whose randoms slot 0 / 1 / 2 holds (expert perm ring index)
-    int64_t reserved[9];
+    int64_t pseq[NSLOT];    // update number whose randoms slot k holds (expert perm ring index)
 };
 static_assert(sizeof(Ctl) <= 32 * 8, "ctl segment is 32 int64");
 
@@ -120,6 +121,8 @@ struct RngArgs {
     float* out_norm;
     int32_t slot;          // writes ctl->pseq[slot]; -1: a draw outside the updates (no stamp)
     int32_t reset_seq;     // first sampler launch of a chain: rng_seq = step_seq
+    int32_t nupd;          // consecutive updates drawn by this launch (slots slot .. slot+nupd-1)
+    int64_t slot_bytes;    // distance between consecutive slots' buffers
 };
 
 struct GatherArgs {
@@ -130,6 +133,8 @@ struct GatherArgs {
     const int32_t* idx;
     const Ctl* ctl;
     int32_t slot;          // expert permutation of update ctl->pseq[slot]
+    int32_t nupd;          // consecutive slots gathered by this launch (blockIdx.y)
+    int64_t slot_bytes;    // distance between consecutive slots' buffers
     const float *s_mean, *s_den, *a_mean, *a_den;
     float* Xa;  int32_t ldS;   // actor rows [sp(B) ; s(B) ; s_e(ne)]
     float* Xq;  float* Xt; float* Xp; float* Xm; int32_t ldQ;

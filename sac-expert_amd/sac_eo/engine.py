@@ -40,7 +40,7 @@ class EngineConfig:
     model_activation: str = "relu"
     model_batch: int = 200
     target_update_int: int = 1
-    graph_steps: int = 32
+    graph_steps: int = 128
     stats_capacity: int = 4096
     perm_capacity: int = 4096
     gamma: float = 0.995

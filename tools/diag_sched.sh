@@ -10,6 +10,8 @@ run() {
   echo "$tag $(grep -o '"value": [0-9.]*' gpurun_out/sched_$tag.log)"
 }
 run base X=1
-run nomerge SACX_MERGE_ALPHA=0
-run g64 SACX_GRAPH_STEPS=64
+run nb2 SACX_NBATCH=2
+run nb8 SACX_NBATCH=8
+run nb8g64 SACX_NBATCH=8 SACX_GRAPH_STEPS=64
+run nb1 SACX_NBATCH=1
 run nofuse SACX_FUSE=0
