@@ -79,6 +79,14 @@ __device__ __forceinline__ float dact_f(float h, int act) {
     }
 }
 
+// dact_f without a branch on the (launch-uniform) activation: every form, then a select
+__device__ __forceinline__ float dact_sel(float h, int act) {
+    const float dr = h > 0.f ? 1.f : 0.f;
+    const float dt = 1.f - h * h;
+    const float de = h < 0.f ? h + 1.f : 1.f;
+    return act == ACT_RELU ? dr : (act == ACT_TANH ? dt : (act == ACT_ELU ? de : 1.f));
+}
+
 __device__ __forceinline__ float softplus_f(float x) {
     if (x > -SOFTPLUS_THR) return x;
     if (x < SOFTPLUS_THR) return expf(x);
@@ -250,9 +258,9 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
 }
 
 // ==================================================================== k_gemm
-template <bool KC, bool VEC>
+template <bool KC, bool VEC, bool GEN = false>
 __device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t ra, const GemmProb& g, int m, bool mok, int k0,
-                                       float (&a)[4]) {
+                                       float (&a)[4], __amdgpu_buffer_rsrc_t rw) {
     if constexpr (KC) {
         if constexpr (VEC) {
             const uint32_t off = boff(mok && k0 < g.K, m * g.lda + k0);
@@ -264,6 +272,19 @@ __device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t ra, const GemmProb
                 const int k = k0 + j;
                 a[j] = bload(ra, boff(mok && k < g.K, m * g.lda + k));
             }
+        }
+        if constexpr (GEN) {       // A = wgen[k] * act'(A) for problems with wgen (else unchanged)
+            float w[4];
+            if constexpr (VEC) {
+                const float4 v = bload4(rw, boff(k0 < g.K, k0));
+                w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) w[j] = bload(rw, boff(k0 + j < g.K, k0 + j));
+            }
+            const bool gen = g.wgen != nullptr;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a[j] = gen ? w[j] * dact_sel(a[j], g.act) : a[j];
         }
     } else {
         // A[m][k] = X[k][m]; logical row ones_row is all ones (bias-gradient row)
@@ -278,7 +299,7 @@ __device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t ra, const GemmProb
     }
 }
 
-template <bool KC, bool VEC>
+template <bool KC, bool VEC, bool SCALE = false>
 __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb& g, int n, bool nok, int k0,
                                        float (&b)[4]) {
     if constexpr (KC) {
@@ -293,6 +314,14 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
                 b[j] = bload(rb, boff(nok && k < g.K, n * g.ldb + k));
             }
         }
+    } else if constexpr (SCALE) {
+        // GM_DW: k is the row of the reduction (a batch row): scale by bscale[k]
+        const __amdgpu_buffer_rsrc_t rs_ = rs(g.bscale);   // host always sets it (ones if unscaled)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = k0 + j;
+            b[j] = bload(rb, boff(nok && k < g.K, k * g.ldb + n)) * bload(rs_, boff(k < g.K, k));
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -304,14 +333,21 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 
 // MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
-template <int MODE, int VEC>
+template <int MODE>
+__device__ void qhead_block(const QHeadArgs& q, int block);
+
+template <int MODE, int VEC, int ROWK = 0>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
     const int tile = blockIdx.x;
-    if (tile >= ga.total_tiles) {          // the folded alpha.final of the previous update
-        if (ga.has_final) finalize_update(ga.fin, ga.fin.nred);
+    if (tile >= ga.total_tiles) {
+        if constexpr (ROWK > 0) {          // horizontally fused head rows
+            qhead_block<ROWK - 1>(ga.qh, tile - ga.total_tiles);
+        } else if (ga.has_final) {         // the folded alpha.final of the previous update
+            finalize_update(ga.fin, ga.fin.nred);
+        }
         return;
     }
     int p = 0;
@@ -356,6 +392,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     // operand extents in bytes (offsets are 32-bit: every operand < 2 GiB, checked on the host)
     const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A, 0x7fffffffu);
     const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rw = rs(g.wgen);
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
     floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
     if constexpr (MODE == GM_FWD2) {
@@ -433,8 +470,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
             // iterations past it1 read a clamped (valid) slab and are zeroed
             const int k0 = (it + u) * 16 + grp * 4;
             const int k0e = (it + u < it1) ? k0 : (1 << 30);
-            load_a<AKC, VEC && AKC>(ra, g, m, mok, k0e, a[u]);
-            load_b<BKC, VEC && BKC>(rb, g, n, nok, k0e, b[u]);
+            load_a<AKC, VEC && AKC, MODE == GM_DX>(ra, g, m, mok, k0e, a[u], rw);
+            load_b<BKC, VEC && BKC, MODE == GM_DW>(rb, g, n, nok, k0e, b[u]);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -486,10 +523,20 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1>), grid, block, 0, s, a);
         else hipLaunchKernelGGL((k_gemm<GM_FWD, 0>), grid, block, 0, s, a);
         break;
-    case GM_DX:
-        if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_gemm<GM_DX, 0>), grid, block, 0, s, a);
+    case GM_DX: {
+        const dim3 gx(a.total_tiles + (a.rowk ? a.row_blocks : 0));
+        if (a.rowk == 1) {
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 1>), gx, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 1>), gx, block, 0, s, a);
+        } else if (a.rowk == 2) {
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 2>), gx, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 2>), gx, block, 0, s, a);
+        } else {
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1>), gx, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_DX, 0>), gx, block, 0, s, a);
+        }
         break;
+    }
     case GM_FWD2:
         switch (a.vec) {
         case 2: hipLaunchKernelGGL((k_gemm<GM_FWD2, 2>), grid, block, 0, s, a); break;
@@ -888,10 +935,10 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
 
 // ==================================================================== k_qhead
 template <int MODE>
-__global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
+__device__ void qhead_block(const QHeadArgs& q, int block) {
     __shared__ float buf[4][512];
     const int wave = wave_id(), lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + wave;
+    const int row = block * 4 + wave;
     const int B = q.B, H1 = q.H1;
     if (row < B) {
         constexpr int nnet = (MODE == 0) ? 4 : 2;
@@ -946,6 +993,11 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
             const float s1 = q1 < q0 ? 1.f : (q0 == q1 ? 0.5f : 0.f);
             g0 = gmin * s0;
             g1 = gmin * s1;
+            if (lane == 0 && q.g != nullptr) {
+                q.g[row] = g0;
+                q.g[B + row] = g1;
+            }
+            if (q.D2 == nullptr) return;   // the dX launch applies g downstream (linearity)
         }
         // differentiated nets: slabs 2,3 (mode 0) or 0,1 (mode 1)
         constexpr int dn = MODE == 0 ? 2 : 0;
@@ -1020,6 +1072,9 @@ __global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) {
     }
 }
 
+template <int MODE>
+__global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) { qhead_block<MODE>(q, blockIdx.x); }
+
 void launch_qhead(const QHeadArgs& a, hipStream_t s) {
     const int rows = a.B + (a.mode == 0 ? a.ne : 0);
     if (a.mode == 0) hipLaunchKernelGGL(k_qhead<0>, dim3((rows + 3) / 4), dim3(256), 0, s, a);
@@ -1058,6 +1113,11 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     float dv0[MAXQ], dv1[MAXQ];
     load_row(rs(pol ? b.Dp1 : b.Dm1), pol ? row * b.H0 : e * b.Hm0, Hd, dv0);
     load_row(rs(b.Dp1), (B + row) * b.H0, pol ? Hd : 0, dv1);
+    // Dp1 is unscaled (linearity): policy rows scale by their q0 / q1 output gradients,
+    // expert rows by 1 (the OOB read gives 0, plus 1)
+    const __amdgpu_buffer_rsrc_t rg = rs(b.gpol);
+    const float gs0 = bload(rg, boff(pol && b.gpol != nullptr, row)) + ((pol && b.gpol != nullptr) ? 0.f : 1.f);
+    const float gs1 = bload(rg, boff(pol && b.gpol != nullptr, B + row)) + ((pol && b.gpol != nullptr) ? 0.f : 1.f);
     const __amdgpu_buffer_rsrc_t rWa = rs(pol ? b.Wq1[0] : b.Wm1[km]);
     const __amdgpu_buffer_rsrc_t rWb = rs(b.Wq1[1]);
     const int Hb = pol ? Hd : 0;
@@ -1081,8 +1141,8 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
             p[u] = 0.f;
 #pragma unroll
             for (int i = 0; i < MAXQ; ++i) {
-                p[u] = fmaf(dv0[i], w0[u][i], p[u]);
-                p[u] = fmaf(dv1[i], w1[u][i], p[u]);
+                p[u] = fmaf(gs0 * dv0[i], w0[u][i], p[u]);
+                p[u] = fmaf(gs1 * dv1[i], w1[u][i], p[u]);
             }
         }
 #pragma unroll

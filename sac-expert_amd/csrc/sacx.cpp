@@ -249,9 +249,10 @@ void build_layout(sacx_handle* h) {
     h->add("ws.lq", 2, B, F, 0);
     h->add("ws.Hp1", 2 * B, H0, F, 0);
     h->add("ws.Hp2", 2 * B, H1, F, 0);
-    h->add("ws.Dp2", 2 * B, H1, F, 0);
     h->add("ws.Dp1", 2 * B, H0, F, 0);
     h->add("ws.lp", 1, B, F, 0);
+    h->add("ws.gp", 2, B, F, 0);                 // policy-row output gradients of q0, q1
+    h->add("ws.ones", 1, std::max(std::max(Rb, B), std::max(1, h->mb)) + 4, F, SACX_ROLE_STATE);
     h->add("ws.Hm1", ne1, Hm0, F, 0);
     h->add("ws.Hm2", ne1, Hm1, F, 0);
     h->add("ws.Dm2", ne1, Hm1, F, 0);
@@ -381,7 +382,9 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         if (mode_of(p) != mode) { fprintf(stderr, "sacx: mixed GEMM modes in %s\n", name.c_str()); abort(); }
         const bool akc = p.a_kc != 0, bkc = p.b_kc != 0;
         if (akc != (mode != GM_DW) || bkc != (mode == GM_DX)) { fprintf(stderr, "sacx: bad operand layout in %s\n", name.c_str()); abort(); }
-        const bool v_a = (p.lda % 4 == 0) && ((((uintptr_t)p.A) & 15) == 0);
+        if (mode == GM_DW && p.bscale == nullptr) p.bscale = h->f("ws.ones");
+        const bool v_a = (p.lda % 4 == 0) && ((((uintptr_t)p.A) & 15) == 0) &&
+                         ((((uintptr_t)p.wgen) & 15) == 0);
         const bool v_b = mode == GM_DX ? ((p.ldb % 4 == 0) && ((((uintptr_t)p.B) & 15) == 0)) : true;
         if (!(v_a && v_b && p.K % 4 == 0 && p.K >= 4)) vec = false;
     }
@@ -423,7 +426,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     float *r_in = W(sl + ".r"), *d_in = W(sl + ".d"), *se_raw = W(sl + ".se_raw"), *spe_raw = W(sl + ".spe_raw");
     float *Ha1 = W("ws.Ha1"), *Ha2 = W("ws.Ha2");
     float *Hq1 = W("ws.Hq1"), *Hq2 = W("ws.Hq2"), *Dq1 = W("ws.Dq1"), *Dq2 = W("ws.Dq2");
-    float *Hp1 = W("ws.Hp1"), *Hp2 = W("ws.Hp2"), *Dp1 = W("ws.Dp1"), *Dp2 = W("ws.Dp2");
+    float *Hp1 = W("ws.Hp1"), *Hp2 = W("ws.Hp2"), *Dp1 = W("ws.Dp1");
     float *Hm1b = W("ws.Hm1"), *Hm2b = W("ws.Hm2"), *Dm1 = W("ws.Dm1"), *Dm2 = W("ws.Dm2");
     float *Da1 = W("ws.Da1"), *Da2 = W("ws.Da2"), *Da3 = W("ws.Da3"), *E = W("ws.E");
     float *Hl1 = W("ws.Hl1"), *Hl2 = W("ws.Hl2");
@@ -539,13 +542,12 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         }
         fwd_pair("q.fwd", p0, p1, fuse_q);
     }
-    // ---- q.head: target, critic loss grads, expert MSE
+    // ---- critic backward.  By linearity Dq1 = g (.) M1 with M1 = ((w3 (.) act'(Hq2)) Wq1^T) (.) act'(Hq1)
+    // independent of the per-row loss gradient g, so the dX GEMM (A generated from Hq2 and w3)
+    // shares one launch with the q.head rows (target, g, loss rows, Dq2, expert MSE + Dm2), and
+    // critic.adam applies g to layer 0 (row-scaled B).
     {
-        Launch L{};
-        L.kind = Launch::QHEAD;
-        L.name = "q.head";
-        L.after_final = true;   // first reader of alpha / the update counters
-        QHeadArgs& q = L.qh;
+        QHeadArgs q{};
         q.mode = 0; q.B = B; q.H1 = H1; q.H2 = Hq2;
         for (int k = 0; k < 4; ++k) q.W3[k] = W(std::string(qn[k]) + ".l2");
         q.act = act; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
@@ -557,31 +559,28 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         q.mact = mact; q.se_raw = se_raw; q.spe_raw = spe_raw;
         q.d_mean = W("norm.d_mean"); q.d_den = W("norm.d_den"); q.ctl = h->ctl();
         q.Dm2 = Dm2; q.mse_rows = W("ws.mse");
-        L.grid = (B + ne + 3) / 4;
-        L.flops = 2.0 * B * H1 * 4 + 2.0 * B * H1 * 2 + 4.0 * ne * Hm1 * S;
-        L.bytes = 4.0 * (4.0 * B * H1 + 2.0 * B * H1 * 2);
-        plan.push_back(L);
-    }
-    // ---- critic backward + Adam + Polyak
-    {
         std::vector<GemmProb> pb;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
-            pb.push_back(prob_dx(Dq2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hq1 + (size_t)(2 + k) * B * H0,
-                                 Dq1 + (size_t)k * B * H0, act));
+            GemmProb p = prob_dx(Hq2 + (size_t)(2 + k) * B * H1, B, H1, W(n + ".l1"), H0,
+                                 Hq1 + (size_t)(2 + k) * B * H0, Dq1 + (size_t)k * B * H0, act);
+            p.wgen = W(n + ".l2");             // w3 column of W3_ext
+            pb.push_back(p);
         }
-        if (eo) {
-            for (int k = 0; k < 2; ++k) {
-                const std::string n = "m" + std::to_string(k);
-                pb.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, half, Hm1, W(n + ".l1"), Hm0,
-                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
-            }
-        }
-        add_gemm(h, plan, "critic.bwd1", pb, record_probs);
+        add_gemm(h, plan, "q.head+critic.bwd1", pb, record_probs);
+        Launch& L = plan.back();
+        L.gemm.rowk = 1;
+        L.gemm.row_blocks = (B + ne + 3) / 4;
+        L.gemm.qh = q;
+        L.grid += L.gemm.row_blocks;
+        L.flops += 2.0 * B * H1 * 4 + 2.0 * B * H1 * 2 + 4.0 * ne * Hm1 * S;
+        L.bytes += 4.0 * (4.0 * B * H1 + 2.0 * B * H1 * 2);
         std::vector<GemmProb> pw;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k), t = "t" + std::to_string(k);
-            pw.push_back(prob_dw(Xq, ldQ, S + A, B, Dq1 + (size_t)k * B * H0, H0, W(n + ".l0"), W(t + ".l0"), GRP_Q));
+            GemmProb p0 = prob_dw(Xq, ldQ, S + A, B, Dq1 + (size_t)k * B * H0, H0, W(n + ".l0"), W(t + ".l0"), GRP_Q);
+            p0.bscale = W("ws.gq") + (size_t)k * B;   // Dq1 = g (.) M1
+            pw.push_back(p0);
             pw.push_back(prob_dw(Hq1 + (size_t)(2 + k) * B * H0, H0, H0, B, Dq2 + (size_t)k * B * H1, H1, W(n + ".l1"),
                                  W(t + ".l1"), GRP_Q));
             pw.push_back(prob_dw(Hq2 + (size_t)(2 + k) * B * H1, H1, H1, B, W("ws.gq") + (size_t)k * B, 1,
@@ -589,7 +588,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         }
         add_gemm(h, plan, "critic.adam", pw, record_probs);
     }
-    // ---- policy loss through the updated critics
+    // ---- policy loss through the updated critics: the same linearity; pi.q.head's rows
+    // (min, tie split, loss rows, g0 / g1) share the unscaled dX launch, actor.head.bwd applies
+    // g0 / g1.  The SAC-EO world-model dX (needs q.head's Dm2) rides in the same launch.
     {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 2; ++k) {
@@ -598,28 +599,37 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, act));
         }
         fwd_pair("pi.q.fwd", p0, p1, fuse_q);
-        Launch L{};
-        L.kind = Launch::QHEAD;
-        L.name = "pi.q.head";
-        QHeadArgs& q = L.qh;
+        QHeadArgs q{};
         q.mode = 1; q.B = B; q.H1 = H1; q.H2 = Hp2;
         q.W3[0] = W("q0.l2"); q.W3[1] = W("q1.l2"); q.W3[2] = nullptr; q.W3[3] = nullptr;
-        q.act = act; q.D2 = Dp2; q.g = nullptr; q.loss_rows = W("ws.lp");
+        q.act = act; q.D2 = nullptr; q.g = W("ws.gp"); q.loss_rows = W("ws.lp");
         q.alpha = W("alpha"); q.nlp = W("ws.nlp_p");
         q.w_sac = eo ? (float)(1.0 - (double)h->cfg.epsilon) : 1.f;
         q.ret_den = W("norm.ret_den");
         q.ne = 0; q.ctl = h->ctl();
-        L.grid = (B + 3) / 4;
-        L.flops = 2.0 * B * H1 * 2 * 2;
-        L.bytes = 4.0 * (2.0 * B * H1 * 2);
-        plan.push_back(L);
         std::vector<GemmProb> pb;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
-            pb.push_back(prob_dx(Dp2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hp1 + (size_t)k * B * H0,
-                                 Dp1 + (size_t)k * B * H0, act));
+            GemmProb p = prob_dx(Hp2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hp1 + (size_t)k * B * H0,
+                                 Dp1 + (size_t)k * B * H0, act);
+            p.wgen = W(n + ".l2");
+            pb.push_back(p);
         }
-        add_gemm(h, plan, "pi.q.bwd1", pb, record_probs);
+        if (eo) {
+            for (int k = 0; k < 2; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                pb.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, half, Hm1, W(n + ".l1"), Hm0,
+                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
+            }
+        }
+        add_gemm(h, plan, "pi.q.head+pi.q.bwd1", pb, record_probs);
+        Launch& L = plan.back();
+        L.gemm.rowk = 2;
+        L.gemm.row_blocks = (B + 3) / 4;
+        L.gemm.qh = q;
+        L.grid += L.gemm.row_blocks;
+        L.flops += 2.0 * B * H1 * 2 * 2;
+        L.bytes += 4.0 * (2.0 * B * H1 * 2);
     }
     // ---- actor backward
     {
@@ -635,6 +645,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
         b.W3a = W("actor.l2"); b.Ha2 = Ha2 + (size_t)B * H1; b.act = act;
         b.Da3 = Da3; b.Da2 = Da2; b.E = E;
+        b.gpol = W("ws.gp");
         L.grid = (h->Rb + 3) / 4;
         L.flops = 2.0 * B * 2 * H0 * A + 2.0 * ne * Hm0 * A + 2.0 * h->Rb * H1 * Aout;
         L.bytes = 4.0 * (2.0 * B * H0 + ne * Hm0 + 2.0 * h->Rb * H1);
@@ -1096,6 +1107,11 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->arena = static_cast<char*>(arena);
     h->stream = static_cast<hipStream_t>(stream);
     h->probs.clear();
+    {   // ws.ones: the B-row scale of unscaled dW problems
+        const SegInfo& so = h->seg("ws.ones");
+        std::vector<float> ones((size_t)(so.rows * so.cols), 1.0f);
+        HIPCHK(h, hipMemcpy(h->arena + so.off, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice));
+    }
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     for (int sl = 0; sl < NSLOT; ++sl) build_plan(h, sl, sl == 0);
     for (int sl = 1; sl < NSLOT; ++sl) {

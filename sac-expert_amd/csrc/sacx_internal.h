@@ -78,6 +78,13 @@ struct GemmProb {
     int32_t K0;            // GM_FWD2: layer-0 inner dim (A is then X[M x K0], K is the hidden width)
     const float* W0;       // GM_FWD2: layer-0 W_ext [(K0+1) x K]
     float* C0;             // GM_FWD2: layer-0 output H1 [M x K] (row stride K)
+    // GM_DX: when set, A is generated on load as wgen[k] * act'(A[m][k]) -- the delta at the
+    // layer-2 output of a scalar-output net for a unit output gradient (the per-row gradient
+    // is applied downstream: the result is linear in it)
+    const float* wgen;
+    // GM_DW: B[k][n] is scaled by bscale[k] on load (per-row output gradient; a ones vector
+    // when unscaled, so every problem takes the same path)
+    const float* bscale;
 };
 
 struct FinalArgs {
@@ -92,6 +99,35 @@ struct FinalArgs {
     float* red;             // partial slots
     int32_t nred;           // number of partials (alpha.head workgroups)
     float* stats; int32_t stats_cap;
+};
+
+struct QHeadArgs {
+    // target/critic mode (mode 0): nets t0,t1 on H2 slabs [0],[1]; q0,q1 on slabs [2],[3]
+    // actor-loss mode (mode 1): q0,q1 on slabs [0],[1]
+    int32_t mode;
+    int32_t B, H1;
+    const float* H2;        // [nslab, B, H1]
+    const float* W3[4];     // W3_ext of the nets, [(H1+1) x 1]
+    int32_t act;
+    float* D2;              // [2, B, H1] delta at the layer-2 output of the trained / differentiated nets
+    float* g;               // [2, B]     delta at the outputs of the two differentiated nets (nullable)
+    float* loss_rows;       // mode 0: [2, B] 0.5 e^2 ; mode 1: [B] -alpha*nlp - minQ
+    const float* alpha;
+    const float* nlp;       // mode 0: nlp of the target actions; mode 1: nlp of the policy actions
+    const float* r; const float* d;
+    float gamma, ret_den_unused;
+    const float* ret_den;
+    float w_sac;            // (1 - epsilon) for SAC-EO, 1 for SAC
+    // SAC-EO model rows (mode 0 only): rows [B, B+ne) handle the expert MSE
+    int32_t ne, Hm1, S;
+    const float* Hm2;       // [ne, Hm1]
+    const float* Wm3[2];    // [(Hm1+1), S+1]
+    int32_t mact;
+    const float* se_raw; const float* spe_raw;
+    const float *d_mean, *d_den;
+    const Ctl* ctl;         // epsilon
+    float* Dm2;             // [ne, Hm1]
+    float* mse_rows;        // [ne]
 };
 
 #define GEMM_MAXP 8
@@ -109,6 +145,10 @@ struct GemmArgs {
     // (alpha.final folded into a launch of the next update, see get_graph)
     int32_t has_final;
     FinalArgs fin;
+    // GM_DX: rowk = 1 / 2 appends row_blocks workgroups running k_qhead<0> / <1> on qh
+    // (horizontal fusion: the heads and the unscaled dX GEMM are independent)
+    int32_t rowk, row_blocks;
+    QHeadArgs qh;
 };
 
 // ---------------------------------------------------------------- sampler + gather
@@ -174,34 +214,7 @@ struct HeadArgs {
 };
 
 // ---------------------------------------------------------------- Q heads
-struct QHeadArgs {
-    // target/critic mode (mode 0): nets t0,t1 on H2 slabs [0],[1]; q0,q1 on slabs [2],[3]
-    // actor-loss mode (mode 1): q0,q1 on slabs [0],[1]
-    int32_t mode;
-    int32_t B, H1;
-    const float* H2;        // [nslab, B, H1]
-    const float* W3[4];     // W3_ext of the nets, [(H1+1) x 1]
-    int32_t act;
-    float* D2;              // [2, B, H1] delta at the layer-2 output of the trained / differentiated nets
-    float* g;               // [2, B]     delta at the output (mode 0)
-    float* loss_rows;       // mode 0: [2, B] 0.5 e^2 ; mode 1: [B] -alpha*nlp - minQ
-    const float* alpha;
-    const float* nlp;       // mode 0: nlp of the target actions; mode 1: nlp of the policy actions
-    const float* r; const float* d;
-    float gamma, ret_den_unused;
-    const float* ret_den;
-    float w_sac;            // (1 - epsilon) for SAC-EO, 1 for SAC
-    // SAC-EO model rows (mode 0 only): rows [B, B+ne) handle the expert MSE
-    int32_t ne, Hm1, S;
-    const float* Hm2;       // [ne, Hm1]
-    const float* Wm3[2];    // [(Hm1+1), S+1]
-    int32_t mact;
-    const float* se_raw; const float* spe_raw;
-    const float *d_mean, *d_den;
-    const Ctl* ctl;         // epsilon
-    float* Dm2;             // [ne, Hm1]
-    float* mse_rows;        // [ne]
-};
+
 
 // ---------------------------------------------------------------- actor backward head
 struct ActorBwdArgs {
@@ -220,6 +233,7 @@ struct ActorBwdArgs {
     const float* Ha2;       // actor layer-2 outputs of rows [B, ...) ; row i at Ha2[i*H1]
     int32_t act;
     float* Da3; float* Da2; float* E;
+    const float* gpol;      // [2, B] output gradients of q0, q1 for the policy rows (Dp1 is unscaled)
 };
 
 // ---------------------------------------------------------------- finalize (alpha + stats)

@@ -3,6 +3,7 @@
 #include <chrono>
 #include <cstdio>
 #include <functional>
+#include <vector>
 using namespace sacx;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
@@ -75,6 +76,13 @@ int main() {
         GemmArgs ga{}; GemmProb p{};
         p.A = X0; p.lda = 256; p.a_kc = 0; p.ones_row = 256; p.B = X1; p.ldb = 256; p.b_kc = 0;
         p.M = 257; p.N = 256; p.K = 256; p.P = P; p.T = nullptr; p.ldp = 256; p.epi = EPI_ADAM; p.group = 0; p.grad_scale = 1.f;
+        {
+            static float* ones = nullptr;
+            std::vector<float> h1(4096, 1.f);
+            CK(hipMalloc(&ones, 4096 * 4));
+            CK(hipMemcpy(ones, h1.data(), 4096 * 4, hipMemcpyHostToDevice));
+            p.bscale = ones;
+        }
         p.tiles_n = 16; p.tile_begin = 0;
         ga.probs[0] = p; ga.nprob = 1; ga.total_tiles = 17 * 16; ga.p_stride = NF; ga.ctl = ctl; ga.mode = GM_DW; ga.vec = 0;
         ga.adam.lr[0] = 3e-4f; ga.adam.tau_keep = 0.995f; ga.adam.tau_take = 0.005f; ga.adam.target_update_int = 1;
