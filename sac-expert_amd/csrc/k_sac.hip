@@ -167,27 +167,29 @@ __device__ __forceinline__ uint32_t boff(bool ok, int elem) {
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
 // ---------------------------------------------------------------- row helpers
-// A row of a hidden layer (width H <= 64*MAXQ) is held as hv[q] = h[lane + 64 q];
+// A row of a hidden layer (width H <= 64*NQ) is held as hv[q] = h[lane + 64 q];
 // all loads of a row are issued before any reduction so the wave's memory
 // latency overlaps instead of serialising behind each butterfly.
 #define MAXQ 8
 // hv[q] = h[base + lane + 64 q] (0 beyond H)
-__device__ __forceinline__ void load_row(__amdgpu_buffer_rsrc_t r, int base, int H, float (&hv)[MAXQ]) {
+template <int NQ>
+__device__ __forceinline__ void load_row(__amdgpu_buffer_rsrc_t r, int base, int H, float (&hv)[NQ]) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < MAXQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
         const int k = lane + 64 * q;
         hv[q] = bload(r, boff(k < H, base + k));
     }
 }
 
 // out[u] = sum_k hv(k) * W[k*ldw + o0 + u] for u < 8 (0 for o0+u >= O); broadcast to all lanes.
-__device__ __forceinline__ void rowdot8(const float (&hv)[MAXQ], __amdgpu_buffer_rsrc_t rW, int H, int ldw,
+template <int NQ>
+__device__ __forceinline__ void rowdot8(const float (&hv)[NQ], __amdgpu_buffer_rsrc_t rW, int H, int ldw,
                                         int o0, int O, float (&out)[8]) {
     const int lane = threadIdx.x & 63;
-    float w[MAXQ][8];
+    float w[NQ][8];
 #pragma unroll
-    for (int q = 0; q < MAXQ; ++q) {
+    for (int q = 0; q < NQ; ++q) {
         const int k = lane + 64 * q;
 #pragma unroll
         for (int u = 0; u < 8; ++u) w[q][u] = bload(rW, boff(k < H && o0 + u < O, k * ldw + o0 + u));
@@ -197,7 +199,7 @@ __device__ __forceinline__ void rowdot8(const float (&hv)[MAXQ], __amdgpu_buffer
     for (int u = 0; u < 8; ++u) {
         p[u] = 0.f;
 #pragma unroll
-        for (int q = 0; q < MAXQ; ++q) p[u] = fmaf(hv[q], w[q][u], p[u]);
+        for (int q = 0; q < NQ; ++q) p[u] = fmaf(hv[q], w[q][u], p[u]);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) out[u] = wave_sum(p[u]);
@@ -333,10 +335,10 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 
 // MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
-template <int MODE>
+template <int MODE, int NQ>
 __device__ void qhead_block(const QHeadArgs& q, int block);
 
-template <int MODE, int VEC, int ROWK = 0>
+template <int MODE, int VEC, int ROWK = 0, int NQ = 4>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const int tile = blockIdx.x;
     if (tile >= ga.total_tiles) {
         if constexpr (ROWK > 0) {          // horizontally fused head rows
-            qhead_block<ROWK - 1>(ga.qh, tile - ga.total_tiles);
+            qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles);
         } else if (ga.has_final) {         // the folded alpha.final of the previous update
             finalize_update(ga.fin, ga.fin.nred);
         }
@@ -525,16 +527,19 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         break;
     case GM_DX: {
         const dim3 gx(a.total_tiles + (a.rowk ? a.row_blocks : 0));
+        const bool q8 = a.rowk && a.qh.H1 > 256;
+#define SACX_DX(V, R, Q) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q>), gx, block, 0, s, a)
         if (a.rowk == 1) {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 1>), gx, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 1>), gx, block, 0, s, a);
+            if (a.vec) { if (q8) SACX_DX(1, 1, 8); else SACX_DX(1, 1, 4); }
+            else { if (q8) SACX_DX(0, 1, 8); else SACX_DX(0, 1, 4); }
         } else if (a.rowk == 2) {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 2>), gx, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 2>), gx, block, 0, s, a);
+            if (a.vec) { if (q8) SACX_DX(1, 2, 8); else SACX_DX(1, 2, 4); }
+            else { if (q8) SACX_DX(0, 2, 8); else SACX_DX(0, 2, 4); }
         } else {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1>), gx, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_DX, 0>), gx, block, 0, s, a);
+            if (a.vec) SACX_DX(1, 0, 4);
+            else SACX_DX(0, 0, 4);
         }
+#undef SACX_DX
         break;
     }
     case GM_FWD2:
@@ -851,6 +856,7 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // ==================================================================== k_actor_head
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
+template <int NQ>
 __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     __shared__ float red_s[4];
     const int wave = wave_id(), lane = threadIdx.x & 63;
@@ -864,7 +870,7 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         const int A = h.A, Aout = h.Aout;
         const bool jok = lane < A;
         // everything this row reads is issued up front
-        float hv[MAXQ];
+        float hv[NQ];
         load_row(rs(h.H2), row * h.ldh, h.H1, hv);
         const __amdgpu_buffer_rsrc_t rW = rs(h.W3);
         const float u_pf = bload(rs(sg.noise), boff(jok, (row - sg.r0) * A + lane));
@@ -930,11 +936,13 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
 }
 
 void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL(k_actor_head, dim3((a.total_rows + 3) / 4), dim3(256), 0, s, a, f);
+    const dim3 grid((a.total_rows + 3) / 4);
+    if (a.H1 <= 256) hipLaunchKernelGGL(k_actor_head<4>, grid, dim3(256), 0, s, a, f);
+    else hipLaunchKernelGGL(k_actor_head<8>, grid, dim3(256), 0, s, a, f);
 }
 
 // ==================================================================== k_qhead
-template <int MODE>
+template <int MODE, int NQ>
 __device__ void qhead_block(const QHeadArgs& q, int block) {
     __shared__ float buf[4][512];
     const int wave = wave_id(), lane = threadIdx.x & 63;
@@ -950,8 +958,8 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
             d_r = q.d[row];
             rd = *q.ret_den;
         }
-        float hv[4][MAXQ];
-        float wv[4][MAXQ];
+        float hv[4][NQ];
+        float wv[4][NQ];
         float bias[4];
         const __amdgpu_buffer_rsrc_t rH = rs(q.H2);
 #pragma unroll
@@ -966,7 +974,7 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
         for (int k = 0; k < nnet; ++k) {
             float p = 0.f;
 #pragma unroll
-            for (int i = 0; i < MAXQ; ++i) p = fmaf(hv[k][i], wv[k][i], p);
+            for (int i = 0; i < NQ; ++i) p = fmaf(hv[k][i], wv[k][i], p);
             out[k] = wave_sum(p) + bias[k];
         }
         float g0, g1;
@@ -1004,7 +1012,7 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
         float* d0 = q.D2 + (size_t)row * H1;
         float* d1 = q.D2 + ((size_t)B + row) * H1;
 #pragma unroll
-        for (int i = 0; i < MAXQ; ++i) {
+        for (int i = 0; i < NQ; ++i) {
             const int k = lane + 64 * i;
             if (k < H1) {
                 d0[k] = (g0 * wv[dn][i]) * dact_f(hv[dn][i], q.act);
@@ -1020,7 +1028,7 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
     const int k = e < half ? 0 : 1;
     const int S = q.S, Hm = q.Hm1, O = S + 1;
     const __amdgpu_buffer_rsrc_t rW = rs(k ? q.Wm3[1] : q.Wm3[0]);
-    float hv[MAXQ];
+    float hv[8];
     load_row(rs(q.Hm2), e * Hm, Hm, hv);
     float* ob = buf[wave];
     for (int j0 = 0; j0 < S; j0 += 8) {
@@ -1047,13 +1055,13 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // Dm2[e][i] = (sum_j ob[j] W[i][j]) * act'(h[i]); j in ascending order, 8 loads in flight
-    float pacc[MAXQ];
+    float pacc[8];
 #pragma unroll
-    for (int qq = 0; qq < MAXQ; ++qq) pacc[qq] = 0.f;
+    for (int qq = 0; qq < 8; ++qq) pacc[qq] = 0.f;
     for (int j0 = 0; j0 < S; j0 += 8) {
-        float w[MAXQ][8];
+        float w[8][8];
 #pragma unroll
-        for (int qq = 0; qq < MAXQ; ++qq) {
+        for (int qq = 0; qq < 8; ++qq) {
             const int i = lane + 64 * qq;
 #pragma unroll
             for (int u = 0; u < 8; ++u) w[qq][u] = bload(rW, boff(i < Hm && j0 + u < S, i * O + j0 + u));
@@ -1062,23 +1070,29 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
         for (int u = 0; u < 8; ++u) {
             const float ou = ob[min(j0 + u, S - 1)];
 #pragma unroll
-            for (int qq = 0; qq < MAXQ; ++qq) pacc[qq] = (j0 + u < S) ? fmaf(ou, w[qq][u], pacc[qq]) : pacc[qq];
+            for (int qq = 0; qq < 8; ++qq) pacc[qq] = (j0 + u < S) ? fmaf(ou, w[qq][u], pacc[qq]) : pacc[qq];
         }
     }
 #pragma unroll
-    for (int qq = 0; qq < MAXQ; ++qq) {
+    for (int qq = 0; qq < 8; ++qq) {
         const int i = lane + 64 * qq;
         if (i < Hm) q.Dm2[(size_t)e * Hm + i] = pacc[qq] * dact_f(hv[qq], q.mact);
     }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) { qhead_block<MODE>(q, blockIdx.x); }
+template <int MODE, int NQ>
+__global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) { qhead_block<MODE, NQ>(q, blockIdx.x); }
 
 void launch_qhead(const QHeadArgs& a, hipStream_t s) {
     const int rows = a.B + (a.mode == 0 ? a.ne : 0);
-    if (a.mode == 0) hipLaunchKernelGGL(k_qhead<0>, dim3((rows + 3) / 4), dim3(256), 0, s, a);
-    else hipLaunchKernelGGL(k_qhead<1>, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+    const dim3 grid((rows + 3) / 4);
+    if (a.H1 <= 256) {
+        if (a.mode == 0) hipLaunchKernelGGL((k_qhead<0, 4>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_qhead<1, 4>), grid, dim3(256), 0, s, a);
+    } else {
+        if (a.mode == 0) hipLaunchKernelGGL((k_qhead<0, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_qhead<1, 8>), grid, dim3(256), 0, s, a);
+    }
 }
 
 // ==================================================================== k_actor_bwd
@@ -1086,6 +1100,7 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 // rows) or world-model (expert rows) input columns, tanh-Gaussian backward
 // (SURVEY.md §8a A5), then the Dense(H1 -> Aout) backward with the activation
 // derivative.  Per-column values live in lane j and are broadcast by shuffles.
+template <int NQ, int NQD>
 __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
@@ -1101,7 +1116,7 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const float u_pf = bload(rs(b.c_u), boff(jok, ci));
     const float mk_pf = bload(rs(b.c_mask), boff(jok, ci));
     const float ad_pf = bload(rs(b.a_den), boff(jok, lane));
-    float h2v[MAXQ];
+    float h2v[NQ];
     load_row(rs(b.Ha2), row * b.H1, b.H1, h2v);
     const float w_sac = 1.f - eps;
     const float c = -w_sac * alpha * (1.f / (float)B);
@@ -1110,7 +1125,7 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const int e = row - B;
     const int km = e < b.ne / 2 ? 0 : 1;
     const int Hd = pol ? b.H0 : b.Hm0;
-    float dv0[MAXQ], dv1[MAXQ];
+    float dv0[NQD], dv1[NQD];
     load_row(rs(pol ? b.Dp1 : b.Dm1), pol ? row * b.H0 : e * b.Hm0, Hd, dv0);
     load_row(rs(b.Dp1), (B + row) * b.H0, pol ? Hd : 0, dv1);
     // Dp1 is unscaled (linearity): policy rows scale by their q0 / q1 output gradients,
@@ -1123,13 +1138,13 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const int Hb = pol ? Hd : 0;
     float ga = 0.f;
     for (int j0 = 0; j0 < A; j0 += 8) {
-        float w0[8][MAXQ], w1[8][MAXQ];
+        float w0[8][NQD], w1[8][NQD];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const bool uok = j0 + u < A;
             const int jr = S + j0 + u;
 #pragma unroll
-            for (int i = 0; i < MAXQ; ++i) {
+            for (int i = 0; i < NQD; ++i) {
                 const int k = lane + 64 * i;
                 w0[u][i] = bload(rWa, boff(uok && k < Hd, jr * Hd + k));
                 w1[u][i] = bload(rWb, boff(uok && k < Hb, jr * Hd + k));
@@ -1140,7 +1155,7 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
         for (int u = 0; u < 8; ++u) {
             p[u] = 0.f;
 #pragma unroll
-            for (int i = 0; i < MAXQ; ++i) {
+            for (int i = 0; i < NQD; ++i) {
                 p[u] = fmaf(gs0 * dv0[i], w0[u][i], p[u]);
                 p[u] = fmaf(gs1 * dv1[i], w1[u][i], p[u]);
             }
@@ -1166,13 +1181,13 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     }
     // Da2[row][i] = (sum_o Da3[row][o] W3a[i][o]) * act'(Ha2[row][i]); columns o live in lanes
     const __amdgpu_buffer_rsrc_t rW3 = rs(b.W3a);
-    float pacc[MAXQ];
+    float pacc[NQ];
 #pragma unroll
-    for (int qq = 0; qq < MAXQ; ++qq) pacc[qq] = 0.f;
+    for (int qq = 0; qq < NQ; ++qq) pacc[qq] = 0.f;
     for (int o0 = 0; o0 < b.Aout; o0 += 8) {
-        float w[MAXQ][8];
+        float w[NQ][8];
 #pragma unroll
-        for (int qq = 0; qq < MAXQ; ++qq) {
+        for (int qq = 0; qq < NQ; ++qq) {
             const int i = qq * 64 + lane;
 #pragma unroll
             for (int u = 0; u < 8; ++u) w[qq][u] = bload(rW3, boff(i < b.H1 && o0 + u < b.Aout, i * b.Aout + o0 + u));
@@ -1185,12 +1200,12 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
             d3[u] = (o < b.Aout) ? src : 0.f;
         }
 #pragma unroll
-        for (int qq = 0; qq < MAXQ; ++qq)
+        for (int qq = 0; qq < NQ; ++qq)
 #pragma unroll
             for (int u = 0; u < 8; ++u) pacc[qq] = fmaf(d3[u], w[qq][u], pacc[qq]);
     }
 #pragma unroll
-    for (int qq = 0; qq < MAXQ; ++qq) {
+    for (int qq = 0; qq < NQ; ++qq) {
         const int i = qq * 64 + lane;
         if (i < b.H1) b.Da2[(size_t)row * b.H1 + i] = pacc[qq] * dact_f(h2v[qq], b.act);
     }
@@ -1198,7 +1213,16 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
 
 void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {
     const int rows = a.B + a.ne;
-    hipLaunchKernelGGL(k_actor_bwd, dim3((rows + 3) / 4), dim3(256), 0, s, a);
+    const dim3 grid((rows + 3) / 4);
+    const int hd = std::max(a.H0, a.use_expert ? a.Hm0 : 0);
+    const bool q8 = a.H1 > 256, d8 = hd > 256;
+    if (q8) {
+        if (d8) hipLaunchKernelGGL((k_actor_bwd<8, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_actor_bwd<8, 4>), grid, dim3(256), 0, s, a);
+    } else {
+        if (d8) hipLaunchKernelGGL((k_actor_bwd<4, 8>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL((k_actor_bwd<4, 4>), grid, dim3(256), 0, s, a);
+    }
 }
 
 // ==================================================================== k_append

@@ -472,11 +472,11 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         plan.push_back(L);
     }
     // ---- actor forward on [sp ; s ; s_e]
-    // Layer 0 has a small K (S, S+A): fuse it into layer 1 (GM_FWD2) when it fits and the
-    // launch is at most one workgroup round (<= 512 tiles at 2 WGs/CU; measured: 512-tile
-    // fused launches beat the pair, the 1024-tile one is slower).  SACX_FUSE=0/1 overrides.
+    // Layer 0 has a small K (S, S+A): it can be fused into layer 1 (GM_FWD2, <= 512 tiles).
+    // Measured on MI355X it no longer pays once the alpha branch is folded and the heads
+    // share launches (12.0k vs 11.9k updates/s), so it is off unless SACX_FUSE=1.
     const char* fenv = std::getenv("SACX_FUSE");
-    const int fuse_mode = fenv ? std::atoi(fenv) : -1;
+    const int fuse_mode = fenv ? (std::atoi(fenv) ? -1 : 0) : 0;
     const bool fuse_a = S <= FWD2_MAX_K0, fuse_q = S + A <= FWD2_MAX_K0;
     auto fwd_pair = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1,
                         bool fuse, int forced = -1, int extra_tiles = 0) -> bool {

@@ -14,4 +14,4 @@ run nb2 SACX_NBATCH=2
 run nb8 SACX_NBATCH=8
 run nb8g64 SACX_NBATCH=8 SACX_GRAPH_STEPS=64
 run nb1 SACX_NBATCH=1
-run nofuse SACX_FUSE=0
+run fuse SACX_FUSE=1
