@@ -98,17 +98,17 @@ def pmc_traffic(kernel, config):
 
 
 def roofline(eng, config, n_prof=20, n_replays=20):
-    """Roofline of the dominant kernel family.
+    """Roofline of the dominant kernel family (by eager device time).
 
-    Its average in-pipeline launch duration is measured with HIP events on the
-    engine's stream around replays of the captured update graph, once complete
-    and once with that family's launches left out (sacx_time_graph): the chain
-    is serial with no gaps between kernels, so the difference divided by the
-    family's launches per update is its average launch duration -- the number
-    rocprofv3 --kernel-trace --stats reports for it (profiles/).  Must run after
-    the timed region: the ablated replays leave meaningless state behind.
-    The per-stage eager numbers (HIP events around every eager launch) include
-    ~4 us of per-event GPU overhead each and only rank the stages."""
+    Its average launch duration is measured in the real pipeline: a replay of the
+    captured update graph in which each launch of the family stores per-workgroup
+    s_memrealtime ticks (sacx_time_kernels); a launch lasts from its first workgroup's
+    start to its last workgroup's end -- the window rocprofv3 --kernel-trace reports
+    for it (profiles/).  HIP events bracket whole graph replays only: an event between
+    two graph nodes costs ~4 us of GPU time and would distort the chain.  Must run after
+    the timed region (these replays are real updates).  Cross-checks kept in the line:
+    the graph time with and without the family (sacx_time_graph) and the eager
+    per-stage event times (each includes ~4 us of event overhead)."""
     info = eng.plan_info()
     ms = eng.profile(n_prof)
     fam = {}
@@ -120,22 +120,25 @@ def roofline(eng, config, n_prof=20, n_replays=20):
         f["launches"] += 1
     dom = max(fam, key=lambda k: fam[k]["ms"])
     f = fam[dom]
-    t_full = eng.time_graph(n_replays)           # ms per update, whole graph
-    t_wo = eng.time_graph(n_replays, dom)        # ms per update, family left out
-    avg_s = (t_full - t_wo) / f["launches"] * 1e-3
-    flops_per_launch = f["flops"] / f["launches"]
-    achieved = flops_per_launch / avg_s / 1e12
+    G = eng.cfg.graph_steps
+    avg_us, us_per_update, n_graph = eng.time_kernels(dom, 3)
+    launches = n_graph / G                       # launches per update in the captured graph
+    flops_per_launch = f["flops"] / launches     # the plan's family FLOPs per update, folded launches included
+    achieved = flops_per_launch / (avg_us * 1e-6) / 1e12
     traffic, src = pmc_traffic(dom, config)
+    t_full = eng.time_graph(n_replays)
+    t_wo = eng.time_graph(n_replays, dom)
     out = {
         "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
         "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
         "traffic": traffic, "traffic_source": src,
-        "avg_launch_us": round(avg_s * 1e6, 3), "launches_per_step": f["launches"],
+        "avg_launch_us": round(avg_us, 3), "launches_per_update": round(launches, 3),
         "flops_per_launch": flops_per_launch,
-        "algorithmic_bytes_per_launch": f["bytes"] / f["launches"],
-        "timing": "HIP events over graph replays, with vs without the family (sacx_time_graph)",
+        "algorithmic_bytes_per_launch": f["bytes"] / launches,
+        "timing": "per-workgroup device timestamps in a replay of the update graph (sacx_time_kernels)",
+        "family_us_per_update": round(us_per_update, 3),
         "graph_us_per_update": round(t_full * 1e3, 3),
-        "graph_us_per_update_without": round(t_wo * 1e3, 3),
+        "graph_us_per_update_without_family": round(t_wo * 1e3, 3),
         "stage_us_eager_events": {L["name"]: round(float(ms[i]) * 1e3, 2) for i, L in enumerate(info)},
     }
     return out, fam

@@ -169,6 +169,13 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
  * family's in-pipeline time.  With a family skipped the updates are meaningless and
  * the state must be discarded (measurement only).  Synchronous. */
 int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, double* ms_out);
+/* Replays a copy of the update graph in which every launch of `kernel` (only "k_gemm")
+ * records per-workgroup start/end device ticks (s_memrealtime, 100 MHz) into its own
+ * slots; returns the mean launch span (first workgroup start .. last workgroup end) in
+ * us, the summed span per update and the launches per graph replay.  The replays are
+ * real updates.  Synchronous. */
+int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, double* avg_us, double* us_per_update,
+                      int64_t* n_launches);
 
 #ifdef __cplusplus
 }

@@ -338,8 +338,8 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 template <int MODE, int NQ>
 __device__ void qhead_block(const QHeadArgs& q, int block);
 
-template <int MODE, int VEC, int ROWK = 0, int NQ = 4>
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
+template <int MODE, int VEC, int ROWK, int NQ>
+__device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
@@ -514,6 +514,21 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
         if (g.T != nullptr) {
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
             if (ctl->num_timesteps % tui == 0) g.T[pidx] = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
+        }
+    }
+}
+
+// ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
+// (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
+template <int MODE, int VEC, int ROWK = 0, int NQ = 4>
+__global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    gemm_core<MODE, VEC, ROWK, NQ>(ga);
+    if (ga.ktime != nullptr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            ga.ktime[2 * blockIdx.x] = t0;
+            ga.ktime[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }

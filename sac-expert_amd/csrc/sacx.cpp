@@ -880,13 +880,38 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
 //   cs: the updates, alpha branches folded one update later (merged_body) + a tail;
 //   rs: sampler + gather, two updates ahead (slot double buffer).
 // skip_kind >= 0 leaves that launch kind out (measurement only: sacx_time_graph)
-int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1) {
+// kt (measurement only, uncached): every k_gemm launch gets its own per-workgroup timestamp
+// slots in kt->base, recorded in kt->spans as (offset, workgroups).
+struct KTimeMap {
+    uint64_t* base = nullptr;
+    int64_t cap = 0, used = 0;
+    std::vector<std::pair<int64_t, int>> spans;
+};
+
+int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1,
+              KTimeMap* kt = nullptr) {
     auto key = std::make_tuple(G, with_rng ? 1 : 0, skip_kind);
-    auto it = h->graphs.find(key);
-    if (it != h->graphs.end()) {
-        *out = it->second;
-        return 0;
+    if (!kt) {
+        auto it = h->graphs.find(key);
+        if (it != h->graphs.end()) {
+            *out = it->second;
+            return 0;
+        }
     }
+    auto emit = [&](const Launch& L, hipStream_t st) {
+        if (kt && L.kind == Launch::GEMM) {
+            Launch C = L;
+            const int nwg = C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0);
+            if (kt->used + 2 * nwg <= kt->cap) {
+                C.gemm.ktime = kt->base + kt->used;
+                kt->spans.push_back({kt->used, nwg});
+                kt->used += 2 * nwg;
+            }
+            enqueue(C, h, st);
+        } else {
+            enqueue(L, h, st);
+        }
+    };
     hipStream_t cs = h->cap_stream, rs = h->rng_stream;
     const int nev = 3 * G + 1;
     for (int i = (int)h->events.size(); i < nev; ++i) {
@@ -968,7 +993,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                     if (L.kind == Launch::GEMM && L.gemm.has_final) launch_alpha_final(L.gemm.fin, cs);
                     continue;
                 }
-                enqueue(L, h, cs);
+                emit(L, cs);
                 if (!due.empty() && !recorded && L.kind == Launch::AHEAD) {
                     HIPCHK(h, hipEventRecord(evS[j], cs));
                     recorded = true;
@@ -981,7 +1006,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             }
         }
         for (const Launch& L : h->plan[(G - 1) % nslot])   // tail: the last update's alpha branch
-            if (L.alpha_branch && (int)L.kind != skip_kind) enqueue(L, h, cs);
+            if (L.alpha_branch && (int)L.kind != skip_kind) emit(L, cs);
         HIPCHK(h, hipEventRecord(evF[0], rs));
         HIPCHK(h, hipStreamWaitEvent(cs, evF[0], 0));    // join the sampler stream
     } else {
@@ -993,7 +1018,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     hipGraphExec_t exec;
     HIPCHK(h, hipGraphInstantiateWithFlags(&exec, graph, 0));
     HIPCHK(h, hipGraphDestroy(graph));
-    h->graphs[key] = exec;
+    if (!kt) h->graphs[key] = exec;
     *out = exec;
     return 0;
 }
@@ -1364,6 +1389,46 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
         launch_actor_head(a, f, h->stream);
     }
     HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, double* avg_us, double* us_per_update,
+                      int64_t* n_launches) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!kernel || std::strcmp(kernel, "k_gemm") != 0) return fail(h, "only k_gemm carries timestamps");
+    if (!avg_us || n_replays <= 0) return fail(h, "bad arguments");
+    const int G = h->graph_steps;
+    KTimeMap kt;
+    kt.cap = (int64_t)G * 16 * 4096 * 2;               // generous: <= 16 GEMM launches x 4096 WGs per update
+    HIPCHK(h, hipMalloc(&kt.base, kt.cap * sizeof(uint64_t)));
+    hipGraphExec_t g = nullptr;
+    int rc = get_graph(h, G, true, &g, -1, &kt);
+    double sum = 0.0;
+    int64_t cnt = 0;
+    std::vector<uint64_t> host((size_t)kt.used);
+    for (int r = 0; rc == 0 && r < n_replays; ++r) {
+        if (hipGraphLaunch(g, h->stream) != hipSuccess || hipStreamSynchronize(h->stream) != hipSuccess ||
+            hipMemcpy(host.data(), kt.base, host.size() * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = fail(h, "timing replay failed");
+            break;
+        }
+        for (const auto& sp : kt.spans) {
+            uint64_t lo = UINT64_MAX, hi = 0;
+            for (int b = 0; b < sp.second; ++b) {
+                lo = std::min(lo, host[sp.first + 2 * b]);
+                hi = std::max(hi, host[sp.first + 2 * b + 1]);
+            }
+            sum += (double)(hi - lo) * 0.01;             // 100 MHz ticks -> us
+            ++cnt;
+        }
+    }
+    if (g) (void)hipGraphExecDestroy(g);
+    (void)hipFree(kt.base);
+    if (rc) return rc;
+    h->seq_host += (int64_t)n_replays * G;
+    *avg_us = cnt ? sum / cnt : 0.0;
+    if (us_per_update) *us_per_update = sum / ((double)n_replays * G);
+    if (n_launches) *n_launches = cnt / n_replays;
     return 0;
 }
 

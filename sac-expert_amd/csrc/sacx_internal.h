@@ -149,6 +149,7 @@ struct GemmArgs {
     // (horizontal fusion: the heads and the unscaled dX GEMM are independent)
     int32_t rowk, row_blocks;
     QHeadArgs qh;
+    uint64_t* ktime;       // measurement only: per-workgroup start / end ticks (nullable)
 };
 
 // ---------------------------------------------------------------- sampler + gather

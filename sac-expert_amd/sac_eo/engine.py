@@ -318,6 +318,14 @@ class Engine:
         N.check(self.lib.sacx_time_graph(self.h, int(n_replays), arg, ctypes.byref(ms)), self.h, "time_graph")
         return ms.value / (n_replays * self.cfg.graph_steps)
 
+    def time_kernels(self, kernel: str = "k_gemm", n_replays: int = 3):
+        """(mean launch span us, summed span us per update, launches per graph) of `kernel`,
+        from per-workgroup device timestamps inside a replay of the update graph."""
+        a, u, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_int64()
+        N.check(self.lib.sacx_time_kernels(self.h, kernel.encode(), int(n_replays), ctypes.byref(a),
+                                           ctypes.byref(u), ctypes.byref(n)), self.h, "time_kernels")
+        return a.value, u.value, int(n.value)
+
     def profile(self, n_steps: int) -> np.ndarray:
         k = len(self.plan_info())
         out = (ctypes.c_double * k)()
