@@ -229,7 +229,15 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
     if (f.use_expert && f.ne > 0) {
         const int h = f.ne / 2;
         float sm = 0.f;
-        for (int i = lane; i < h; i += 64) sm += 0.5f * (f.mse_rows[i] + f.mse_rows[i + h]);
+        const int nt = f.mse_tiles;
+        for (int i = lane; i < h; i += 64) {
+            float a = 0.f, b = 0.f;
+            for (int t = 0; t < nt; ++t) {
+                a += f.mse_rows[i * nt + t];
+                b += f.mse_rows[(i + h) * nt + t];
+            }
+            sm += 0.5f * (a + b);
+        }
         mse = wave_sum(sm) / (float)h;
         const float eps = f.ctl->epsilon;
         pl = (1.f - eps) * pl + eps * mse;
@@ -372,8 +380,14 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     const int mmc = min(mm, g.M - 1), nnc = min(nn, g.N - 1);
     float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
     const size_t pidx = (size_t)mmc * g.ldp + nnc;
+    float e4 = 0.f;
     if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         e0 = g.bias[nnc];
+        // world-model head rows (mse): zero-sized resources when not an mse problem
+        e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
+        e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
+        e3 = bload(rs(g.dmean), boff(g.mse != 0, nnc));
+        e4 = bload(rs(g.dden), boff(g.mse != 0, nnc));
     } else if constexpr (MODE == GM_DX) {
         e0 = g.H[(size_t)mmc * g.ldh + nnc];
     } else {
@@ -494,6 +508,23 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
+    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+        if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
+            const float pred = v + e0;
+            const float sp_hat = e1 + (pred * e4 + e3);
+            const float diff = e2 - sp_hat;
+            const float gscale = -ga.ctl->epsilon * g.grad_scale;
+            float sq = out_ok ? diff * diff : 0.f;
+            sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's tile row
+            sq += __shfl_xor(sq, 4, 16);
+            sq += __shfl_xor(sq, 2, 16);
+            sq += __shfl_xor(sq, 1, 16);
+            if (!out_ok) return;
+            g.C[(size_t)mm * g.ldc + nn] = (gscale * diff) * e4;
+            if (col == 0) g.part[(size_t)mm * g.tiles_n + tn] = sq;
+            return;
+        }
+    }
     if (!out_ok) return;
     if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         g.C[(size_t)mm * g.ldc + nn] = act_f(v + e0, g.act);

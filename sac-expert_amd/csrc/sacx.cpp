@@ -257,7 +257,8 @@ void build_layout(sacx_handle* h) {
     h->add("ws.Hm2", ne1, Hm1, F, 0);
     h->add("ws.Dm2", ne1, Hm1, F, 0);
     h->add("ws.Dm1", ne1, Hm0, F, 0);
-    h->add("ws.mse", 1, ne1, F, 0);
+    h->add("ws.mse", ne1, (S + 15) / 16, F, 0);       // per-column-tile partials of the expert MSE
+    h->add("ws.dout", ne1, S, F, 0);                  // d loss / d model output (expert rows)
     h->add("ws.Da3", Rb, h->Aout, F, 0);
     h->add("ws.Da2", Rb, H1, F, 0);
     h->add("ws.Da1", Rb, H0, F, 0);
@@ -404,6 +405,20 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     L.gemm.adam.target_update_int = h->cfg.target_update_int;
     L.grid = tiles;
     plan.push_back(L);
+}
+
+// Appends the problems of GEMM launch `b` to launch `a` (same mode; tile ranges follow a's).
+bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
+    if (a.mode != b.mode || a.nprob + b.nprob > GEMM_MAXP) return false;
+    for (int i = 0; i < b.nprob; ++i) {
+        GemmProb p = b.probs[i];
+        p.tile_begin += a.total_tiles;
+        a.probs[a.nprob + i] = p;
+    }
+    a.nprob += b.nprob;
+    a.total_tiles += b.total_tiles;
+    a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec && b.vec);
+    return true;
 }
 
 void build_plan(sacx_handle* h, int slot, bool record_probs) {
@@ -553,12 +568,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         q.act = act; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
         q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = r_in; q.d = d_in;
         q.gamma = h->cfg.gamma; q.ret_den = W("norm.ret_den"); q.w_sac = 1.f;
-        q.ne = ne; q.Hm1 = Hm1; q.S = S; q.Hm2 = Hm2b;
-        q.Wm3[0] = eo ? W("m0.l2") : nullptr;
-        q.Wm3[1] = eo ? W("m1.l2") : nullptr;
-        q.mact = mact; q.se_raw = se_raw; q.spe_raw = spe_raw;
-        q.d_mean = W("norm.d_mean"); q.d_den = W("norm.d_den"); q.ctl = h->ctl();
-        q.Dm2 = Dm2; q.mse_rows = W("ws.mse");
+        // the SAC-EO world-model head on the expert rows runs as GEMM problems (mse epilogue)
+        // in the pi.q.fwd0 launch, not as rows here
+        q.ne = 0; q.ctl = h->ctl();
         std::vector<GemmProb> pb;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
@@ -570,10 +582,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, "q.head+critic.bwd1", pb, record_probs);
         Launch& L = plan.back();
         L.gemm.rowk = 1;
-        L.gemm.row_blocks = (B + ne + 3) / 4;
+        L.gemm.row_blocks = (B + 3) / 4;
         L.gemm.qh = q;
         L.grid += L.gemm.row_blocks;
-        L.flops += 2.0 * B * H1 * 4 + 2.0 * B * H1 * 2 + 4.0 * ne * Hm1 * S;
+        L.flops += 2.0 * B * H1 * 4 + 2.0 * B * H1 * 2;
         L.bytes += 4.0 * (4.0 * B * H1 + 2.0 * B * H1 * 2);
         std::vector<GemmProb> pw;
         for (int k = 0; k < 2; ++k) {
@@ -598,7 +610,43 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), H0, Hp1 + (size_t)k * B * H0, act));
             p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, act));
         }
-        fwd_pair("pi.q.fwd", p0, p1, fuse_q);
+        // SAC-EO: world-model layer 2 on the expert rows + MSE epilogue (needs Hm2 from q.fwd1),
+        // riding in the pi.q.fwd0 launch (a launch of its own when that one is fused)
+        std::vector<GemmProb> pm;
+        const int O = S + 1, mtn = (S + 15) / 16;
+        if (eo) {
+            for (int k = 0; k < 2; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                GemmProb p{};
+                p.A = Hm2b + (size_t)k * half * Hm1; p.lda = Hm1; p.a_kc = 1; p.ones_row = -1;
+                p.B = W(n + ".l2"); p.ldb = O; p.b_kc = 0;           // W_ext [(Hm1+1) x (S+1)]
+                p.M = half; p.N = S; p.K = Hm1;                      // delta-s columns only
+                p.bias = W(n + ".l2") + (size_t)Hm1 * O;
+                p.C = W("ws.dout") + (size_t)k * half * S; p.ldc = S;
+                p.epi = EPI_FWD; p.act = ACT_NONE;
+                p.mse = 1; p.grad_scale = 1.f / (float)half;
+                p.se_raw = se_raw + (size_t)k * half * S; p.spe_raw = spe_raw + (size_t)k * half * S;
+                p.dmean = W("norm.d_mean"); p.dden = W("norm.d_den");
+                p.part = W("ws.mse") + (size_t)k * half * mtn;
+                pm.push_back(p);
+            }
+        }
+        const bool pi_fused = fwd_pair("pi.q.fwd", p0, p1, fuse_q);
+        if (eo) {
+            if (pi_fused) {
+                add_gemm(h, plan, "model.head", pm, record_probs);
+            } else {                         // plan.back() is pi.q.fwd1: fold into pi.q.fwd0
+                Launch& F0 = plan[plan.size() - 2];
+                std::vector<Launch> one;
+                add_gemm(h, one, "model.head", pm, false);
+                h->probs_cursor -= (int)pm.size();
+                if (!merge_gemm(F0.gemm, one[0].gemm)) { fprintf(stderr, "sacx: model.head merge\n"); abort(); }
+                F0.name += "+model.head";
+                F0.grid = F0.gemm.total_tiles;
+                F0.flops += one[0].flops;
+                F0.bytes += one[0].bytes;
+            }
+        }
         QHeadArgs q{};
         q.mode = 1; q.B = B; q.H1 = H1; q.H2 = Hp2;
         q.W3[0] = W("q0.l2"); q.W3[1] = W("q1.l2"); q.W3[2] = nullptr; q.W3[3] = nullptr;
@@ -615,21 +663,34 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             p.wgen = W(n + ".l2");
             pb.push_back(p);
         }
-        if (eo) {
+        if (eo) {                            // Dm2 = dout . Wm2[:, :S]^T (.) act'(Hm2)
             for (int k = 0; k < 2; ++k) {
                 const std::string n = "m" + std::to_string(k);
-                pb.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, half, Hm1, W(n + ".l1"), Hm0,
-                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
+                GemmProb p = prob_dx(W("ws.dout") + (size_t)k * half * S, half, S, W(n + ".l2"), Hm1,
+                                     Hm2b + (size_t)k * half * Hm1, Dm2 + (size_t)k * half * Hm1, mact);
+                p.ldb = O;                           // B[n][k] = W_ext[n][k], row stride S+1
+                pb.push_back(p);
             }
         }
         add_gemm(h, plan, "pi.q.head+pi.q.bwd1", pb, record_probs);
-        Launch& L = plan.back();
-        L.gemm.rowk = 2;
-        L.gemm.row_blocks = (B + 3) / 4;
-        L.gemm.qh = q;
-        L.grid += L.gemm.row_blocks;
-        L.flops += 2.0 * B * H1 * 2 * 2;
-        L.bytes += 4.0 * (2.0 * B * H1 * 2);
+        {
+            Launch& L = plan.back();
+            L.gemm.rowk = 2;
+            L.gemm.row_blocks = (B + 3) / 4;
+            L.gemm.qh = q;
+            L.grid += L.gemm.row_blocks;
+            L.flops += 2.0 * B * H1 * 2 * 2;
+            L.bytes += 4.0 * (2.0 * B * H1 * 2);
+        }
+        if (eo) {                            // Dm1 = Dm2 . Wm1^T (.) act'(Hm1), for actor.head.bwd
+            std::vector<GemmProb> pd;
+            for (int k = 0; k < 2; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                pd.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, half, Hm1, W(n + ".l1"), Hm0,
+                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
+            }
+            add_gemm(h, plan, "model.bwd1", pd, record_probs);
+        }
     }
     // ---- actor backward
     {
@@ -703,6 +764,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         f.target_entropy = h->cfg.target_entropy;
         f.B = B; f.ne = ne; f.use_expert = eo;
         f.lq = W("ws.lq"); f.lp = W("ws.lp"); f.mse_rows = W("ws.mse"); f.red = W("red");
+        f.mse_tiles = (S + 15) / 16;
         f.stats = W("stats"); f.stats_cap = h->stats_cap;
         L.grid = 1;
         L.block = 64;
@@ -803,20 +865,6 @@ void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
         if (L.kind == Launch::RNG && !with_rng) continue;
         enqueue(L, h, s);
     }
-}
-
-// Appends the problems of GEMM launch `b` to launch `a` (same mode; tile ranges follow a's).
-bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
-    if (a.mode != b.mode || a.nprob + b.nprob > GEMM_MAXP) return false;
-    for (int i = 0; i < b.nprob; ++i) {
-        GemmProb p = b.probs[i];
-        p.tile_begin += a.total_tiles;
-        a.probs[a.nprob + i] = p;
-    }
-    a.nprob += b.nprob;
-    a.total_tiles += b.total_tiles;
-    a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec && b.vec);
-    return true;
 }
 
 // The main-stream launches of update `slot` with the alpha branch (alpha.fwd, alpha.head,

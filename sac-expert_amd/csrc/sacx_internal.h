@@ -85,6 +85,13 @@ struct GemmProb {
     // GM_DW: B[k][n] is scaled by bscale[k] on load (per-row output gradient; a ones vector
     // when unscaled, so every problem takes the same path)
     const float* bscale;
+    // GM_FWD with mse: the world-model head on expert rows (SAC_expert.py:319-332): the output
+    // is the normalised delta; C receives d loss / d out = (-eps * grad_scale * diff) * d_den,
+    // diff = sp_e - (s_e + out * d_den + d_mean); part[row * tiles_n + tn] = sum of diff^2 over
+    // the tile's columns (row stride of se_raw / spe_raw is N)
+    int32_t mse;
+    const float *se_raw, *spe_raw, *dmean, *dden;
+    float* part;
 };
 
 struct FinalArgs {
@@ -95,9 +102,10 @@ struct FinalArgs {
     int32_t B, ne, use_expert;
     const float* lq;        // [2, B]
     const float* lp;        // [B]
-    const float* mse_rows;  // [ne]
+    const float* mse_rows;  // [ne, mse_tiles] per-column-tile partial sums of diff^2
     float* red;             // partial slots
     int32_t nred;           // number of partials (alpha.head workgroups)
+    int32_t mse_tiles;      // partials per expert row in mse_rows
     float* stats; int32_t stats_cap;
 };
 
