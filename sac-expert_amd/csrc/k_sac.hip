@@ -628,23 +628,19 @@ __device__ __forceinline__ uint32_t mt_tw(uint32_t cur, uint32_t nxt, uint32_t f
     return far ^ (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
 }
 
-__device__ void mt_twist(uint32_t* mt) {
+// out-of-place twist: dst = next block of src.  MT19937's in-place recurrence reads the old
+// words i+1, i+397 for i < 227 and the NEW words i-227 beyond (dst[0] and dst[396] for 623),
+// so three phases with a barrier after each are enough.
+__device__ __forceinline__ void mt_twist_to(const uint32_t* src, uint32_t* dst) {
     const int t = threadIdx.x;
-    uint32_t v = 0;
-    if (t < 227) v = mt_tw(mt[t], mt[t + 1], mt[t + 397]);
+    if (t < 227) dst[t] = mt_tw(src[t], src[t + 1], src[t + 397]);
     __syncthreads();
-    if (t < 227) mt[t] = v;
-    __syncthreads();
-    if (t < 227) v = mt_tw(mt[227 + t], mt[228 + t], mt[t]);
-    __syncthreads();
-    if (t < 227) mt[227 + t] = v;
+    if (t < 227) dst[227 + t] = mt_tw(src[227 + t], src[228 + t], dst[t]);
     __syncthreads();
     if (t < 170) {
         const int i = 454 + t;
-        v = (i < 623) ? mt_tw(mt[i], mt[i + 1], mt[i - 227]) : mt_tw(mt[623], mt[0], mt[396]);
+        dst[i] = (i < 623) ? mt_tw(src[i], src[i + 1], dst[i - 227]) : mt_tw(src[623], dst[0], dst[396]);
     }
-    __syncthreads();
-    if (t < 170) mt[454 + t] = v;
     __syncthreads();
 }
 
@@ -667,148 +663,211 @@ __device__ __forceinline__ int block_rank(bool flag, int* wtot, int& total) {
     return off + below;
 }
 
-__global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
-    __shared__ uint32_t mt[624];
-    __shared__ uint32_t win[628];
-    __shared__ int wtot[RNG_THREADS / 64];
-    __shared__ int sh_last;
-    __shared__ double sh_gauss;
-    __shared__ int sh_has;
+#define RNG_KB 4   // fresh MT blocks twisted ahead per round
+
+// The stream is consumed in rounds.  blk[0] is the current block (next word at pos); a
+// round twists nb <= RNG_KB fresh blocks after it (as many as the expected acceptance
+// needs), lays the tempered words out in win[] behind any carried words, tests all
+// candidates in parallel and ranks the accepted ones.  The block holding the last
+// consumed word becomes blk[0] again, so the state written back is always the NumPy
+// (key = current block, pos) pair.
+struct RngShared {
+    uint32_t blk[RNG_KB + 1][624];
+    uint32_t win[(RNG_KB + 1) * 624 + 4];
+    int wtot[RNG_THREADS / 64];
+    int last;
+    int has;
+    double gauss;
+};
+
+// lays out the stream of this round; returns its length in words (carry included)
+__device__ int rng_fill(RngShared& S, int& pos, int cl, int est_words) {
     const int t = threadIdx.x;
-    for (int i = t; i < 624; i += RNG_THREADS) mt[i] = a.st->key[i];
+    const int avail = cl + (624 - pos);
+    int nb = est_words > avail ? (est_words - avail + 623) / 624 : 0;
+    if (avail == 0 && nb == 0) nb = 1;
+    nb = nb > RNG_KB ? RNG_KB : nb;
+    for (int j = 1; j <= nb; ++j) mt_twist_to(S.blk[j - 1], S.blk[j]);
+    const int f0 = 624 - pos;
+    const int L = cl + f0 + nb * 624;
+    for (int i = t; i < f0 + nb * 624; i += RNG_THREADS) {
+        const uint32_t w = i < f0 ? S.blk[0][pos + i] : S.blk[1 + (i - f0) / 624][(i - f0) % 624];
+        S.win[cl + i] = mt_temper(w);
+    }
+    __syncthreads();
+    return L | (nb << 24);
+}
+
+// after a round that consumed `used` stream words (carry included): the block holding the
+// last consumed word becomes blk[0]
+__device__ void rng_settle(RngShared& S, int& pos, int cl, int used, int nb) {
+    const int t = threadIdx.x;
+    int c = used - cl;                     // fresh words consumed (>= 0: a candidate ends past the carry)
+    const int f0 = 624 - pos;
+    int j = 0, np = pos + c;
+    if (c > f0) {
+        c -= f0;
+        j = 1 + (c - 1) / 624;
+        np = c - (j - 1) * 624;
+    }
+    if (j > 0) {
+        for (int i = t; i < 624; i += RNG_THREADS) S.blk[0][i] = S.blk[j][i];
+        __syncthreads();
+    }
+    pos = np;
+    (void)nb;
+}
+
+__global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
+    __shared__ RngShared S;
+    const int t = threadIdx.x;
+    for (int i = t; i < 624; i += RNG_THREADS) S.blk[0][i] = a.st->key[i];
     int pos = a.st->pos;
     if (t == 0) {
-        sh_has = a.st->has_gauss;
-        sh_gauss = a.st->gauss;
+        S.has = a.st->has_gauss;
+        S.gauss = a.st->gauss;
     }
     __syncthreads();
 
-  for (int u = 0; u < a.nupd; ++u) {
-    // update u of the batch: its randint + normals, in stream order, into slot (slot + u)
-    int32_t* const out_idx = a.out_idx ? (int32_t*)((char*)a.out_idx + u * a.slot_bytes) : nullptr;
-    float* const out_norm = (float*)((char*)a.out_norm + u * a.slot_bytes);
-    // ---------------- randint(high, n_int)
-    if (a.n_int > 0) {
-        const uint64_t high = (uint64_t)a.ctl->cur_size;
-        const uint64_t rng = high > 0 ? high - 1 : 0;
-        uint64_t mask = rng;
-        mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
-        mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
-        int done = 0;
-        while (done < a.n_int) {
+    for (int u = 0; u < a.nupd; ++u) {
+        // update u of the batch: its randint + normals, in stream order, into slot (slot + u)
+        int32_t* const out_idx = a.out_idx ? (int32_t*)((char*)a.out_idx + u * a.slot_bytes) : nullptr;
+        float* const out_norm = (float*)((char*)a.out_norm + u * a.slot_bytes);
+
+        // ---------------- randint(high, n_int): masked rejection, one word per candidate
+        if (a.n_int > 0) {
+            const uint64_t high = (uint64_t)a.ctl->cur_size;
+            const uint64_t rng = high > 0 ? high - 1 : 0;
+            uint64_t mask = rng;
+            mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+            mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
             if (rng == 0) {
                 for (int i = t; i < a.n_int; i += RNG_THREADS) out_idx[i] = 0;
-                break;
-            }
-            if (pos == 624) {
-                mt_twist(mt);
-                pos = 0;
-            }
-            const int L = 624 - pos;
-            bool acc = false;
-            uint32_t v = 0;
-            if (t < L) {
-                const uint32_t w = mt_temper(mt[pos + t]);
-                if (rng == 0xFFFFFFFFULL) {
-                    v = w;
-                    acc = true;
-                } else {
-                    v = w & (uint32_t)mask;
-                    acc = (uint64_t)v <= rng;
+            } else {
+                int done = 0;
+                while (done < a.n_int) {
+                    const int need = a.n_int - done;
+                    // acceptance (rng+1)/(mask+1) >= 1/2
+                    const int est = (int)((double)need * (double)(mask + 1) / (double)(rng + 1) * 1.05) + 16;
+                    const int r = rng_fill(S, pos, 0, est);
+                    const int L = r & 0xffffff, nb = r >> 24;
+                    int used = L;
+                    bool fin = false;
+                    for (int c0 = 0; c0 < L && !fin; c0 += RNG_THREADS) {
+                        const int idx = c0 + t;
+                        bool acc = false;
+                        uint32_t v = 0;
+                        if (idx < L) {
+                            const uint32_t w = S.win[idx];
+                            if (rng == 0xFFFFFFFFULL) { v = w; acc = true; }
+                            else { v = w & (uint32_t)mask; acc = (uint64_t)v <= rng; }
+                        }
+                        int total;
+                        const int rank = block_rank(acc, S.wtot, total);
+                        const int nd = a.n_int - done;
+                        if (acc && rank < nd) out_idx[done + rank] = (int32_t)v;
+                        if (acc && rank == nd - 1) S.last = idx;
+                        __syncthreads();
+                        if (total >= nd) {
+                            used = S.last + 1;
+                            done = a.n_int;
+                            fin = true;
+                        } else {
+                            done += total;
+                        }
+                        __syncthreads();
+                    }
+                    if (fin) {
+                        rng_settle(S, pos, 0, used, nb);
+                    } else {              // every fresh word consumed: the last block is current
+                        rng_settle(S, pos, 0, L, nb);
+                    }
                 }
             }
-            int total;
-            const int rank = block_rank(acc, wtot, total);
-            const int need = a.n_int - done;
-            if (acc && rank < need) out_idx[done + rank] = (int32_t)v;
-            if (acc && rank == need - 1) sh_last = t;
+        }
+
+        // ---------------- n_norm x legacy_gauss (polar method, pairs of 4 words)
+        int oi = 0;
+        if (a.n_norm > 0 && S.has) {
+            if (t == 0) out_norm[0] = (float)S.gauss;
+            oi = 1;
             __syncthreads();
-            if (total >= need) {
-                pos += sh_last + 1;
-                done = a.n_int;
-            } else {
-                pos += L;
-                done += total;
+            if (t == 0) { S.has = 0; S.gauss = 0.0; }
+            __syncthreads();
+        }
+        int cl = 0;                               // carried words at win[0..cl)
+        while (oi < a.n_norm) {
+            const int need_pairs = (a.n_norm - oi + 1) >> 1;
+            const int est = (int)((double)need_pairs * 4.0 * 1.3) + 16;   // acceptance pi/4
+            const int r = rng_fill(S, pos, cl, est);
+            const int L = r & 0xffffff, nb = r >> 24;
+            const int items = L >> 2;
+            int got = 0;
+            bool fin = false;
+            int used = 4 * items;
+            for (int c0 = 0; c0 < items && !fin; c0 += RNG_THREADS) {
+                const int it = c0 + t;
+                bool acc = false;
+                double f = 0.0, x1 = 0.0, x2 = 0.0;
+                if (it < items) {
+                    const uint32_t w0 = S.win[4 * it], w1 = S.win[4 * it + 1], w2 = S.win[4 * it + 2],
+                                   w3 = S.win[4 * it + 3];
+                    const double u1 = ((double)(int32_t)(w0 >> 5) * 67108864.0 + (double)(int32_t)(w1 >> 6)) / 9007199254740992.0;
+                    const double u2 = ((double)(int32_t)(w2 >> 5) * 67108864.0 + (double)(int32_t)(w3 >> 6)) / 9007199254740992.0;
+                    x1 = 2.0 * u1 - 1.0;
+                    x2 = 2.0 * u2 - 1.0;
+                    const double r2 = x1 * x1 + x2 * x2;
+                    acc = (r2 < 1.0) && (r2 != 0.0);
+                    if (acc) f = sqrt(-2.0 * log(r2) / r2);
+                }
+                int total;
+                const int rank = block_rank(acc, S.wtot, total);
+                const int np = need_pairs - got;
+                if (acc && rank < np) {
+                    const int o = oi + 2 * (got + rank);
+                    out_norm[o] = (float)(f * x2);
+                    if (o + 1 < a.n_norm) {
+                        out_norm[o + 1] = (float)(f * x1);
+                    } else {
+                        S.gauss = f * x1;
+                        S.has = 1;
+                    }
+                }
+                if (acc && rank == np - 1) S.last = it;
+                __syncthreads();
+                if (total >= np) {
+                    used = 4 * (S.last + 1);
+                    fin = true;
+                    got = need_pairs;
+                } else {
+                    got += total;
+                }
+                __syncthreads();
             }
-            __syncthreads();
-        }
-    }
-
-    // ---------------- n_norm x gauss
-    int oi = 0;
-    if (a.n_norm > 0 && sh_has) {
-        if (t == 0) out_norm[0] = (float)sh_gauss;
-        oi = 1;
-        __syncthreads();
-        if (t == 0) { sh_has = 0; sh_gauss = 0.0; }
-    }
-    int cl = 0;  // carried words at win[0..cl)
-    while (oi < a.n_norm) {
-        if (pos == 624) {          // only reachable when the previous phase ended exactly on a block edge
-            mt_twist(mt);
-            pos = 0;
-        }
-        const int fresh = 624 - pos;
-        const int L = cl + fresh;
-        if (t < fresh) win[cl + t] = mt_temper(mt[pos + t]);
-        __syncthreads();
-        const int items = L >> 2;
-        bool acc = false;
-        double f = 0.0, x1 = 0.0, x2 = 0.0;
-        if (t < items) {
-            const uint32_t w0 = win[4 * t], w1 = win[4 * t + 1], w2 = win[4 * t + 2], w3 = win[4 * t + 3];
-            const double u1 = ((double)(int32_t)(w0 >> 5) * 67108864.0 + (double)(int32_t)(w1 >> 6)) / 9007199254740992.0;
-            const double u2 = ((double)(int32_t)(w2 >> 5) * 67108864.0 + (double)(int32_t)(w3 >> 6)) / 9007199254740992.0;
-            x1 = 2.0 * u1 - 1.0;
-            x2 = 2.0 * u2 - 1.0;
-            const double r2 = x1 * x1 + x2 * x2;
-            acc = (r2 < 1.0) && (r2 != 0.0);
-            if (acc) f = sqrt(-2.0 * log(r2) / r2);
-        }
-        int total;
-        const int rank = block_rank(acc, wtot, total);
-        const int need_vals = a.n_norm - oi;
-        const int need_pairs = (need_vals + 1) >> 1;
-        if (acc && rank < need_pairs) {
-            const int o = oi + 2 * rank;
-            out_norm[o] = (float)(f * x2);
-            if (o + 1 < a.n_norm) {
-                out_norm[o + 1] = (float)(f * x1);
+            if (fin) {
+                oi = a.n_norm;
+                rng_settle(S, pos, cl, used, nb);
+                cl = 0;
             } else {
-                sh_gauss = f * x1;
-                sh_has = 1;
+                oi += 2 * got;
+                // carry the < 4 words after the last full candidate; the last block is current
+                const int left = L - 4 * items;
+                uint32_t keep = 0;
+                if (t < left) keep = S.win[4 * items + t];
+                rng_settle(S, pos, cl, L, nb);
+                __syncthreads();
+                if (t < left) S.win[t] = keep;
+                cl = left;
+                __syncthreads();
             }
         }
-        if (acc && rank == need_pairs - 1) sh_last = t;
-        __syncthreads();
-        if (total >= need_pairs) {
-            pos = pos + 4 * (sh_last + 1) - cl;
-            cl = 0;
-            oi = a.n_norm;
-        } else {
-            oi += 2 * total;
-            const int used = 4 * items;
-            const int left = L - used;
-            uint32_t keep = 0;
-            if (t < left) keep = win[used + t];
-            __syncthreads();
-            if (t < left) win[t] = keep;
-            cl = left;
-            mt_twist(mt);
-            pos = 0;
-        }
-        __syncthreads();
     }
 
-    __syncthreads();
-  }
-
-    for (int i = t; i < 624; i += RNG_THREADS) a.st->key[i] = mt[i];
+    for (int i = t; i < 624; i += RNG_THREADS) a.st->key[i] = S.blk[0][i];
     if (t == 0) {
         a.st->pos = pos;
-        a.st->has_gauss = sh_has;
-        a.st->gauss = sh_gauss;
-        // the update these randoms belong to (the sampler runs ahead of the updates)
+        a.st->has_gauss = S.has;
+        a.st->gauss = S.gauss;
         if (a.slot >= 0) {
             const int64_t seq = a.reset_seq ? a.ctl->step_seq : a.ctl->rng_seq;
             for (int u = 0; u < a.nupd; ++u) a.ctl->pseq[a.slot + u] = seq + u;
