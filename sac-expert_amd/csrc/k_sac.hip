@@ -346,12 +346,21 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 template <int MODE, int NQ>
 __device__ void qhead_block(const QHeadArgs& q, int block);
 
+// Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
+// so blocks b and b+8 share an L2.  xcd_tile gives the blocks of one XCD a contiguous range of
+// the row-major tile order: whole row blocks, so each A row block is fetched into one L2
+// instead of all eight (B is the small shared operand).  A bijection on [0, T) for any T.
+__device__ __forceinline__ int xcd_tile(int b, int T) {
+    const int x = b & 7, j = b >> 3, q = T >> 3, r = T & 7;
+    return x * q + (x < r ? x : r) + j;
+}
+
 template <int MODE, int VEC, int ROWK, int NQ>
 __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
-    const int tile = blockIdx.x;
+    int tile = blockIdx.x;
     if (tile >= ga.total_tiles) {
         if constexpr (ROWK > 0) {          // horizontally fused head rows
             qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles);
@@ -360,6 +369,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         }
         return;
     }
+    if (ga.xcd_map) tile = xcd_tile(tile, ga.total_tiles);
     int p = 0;
 #pragma unroll
     for (int i = 1; i < GEMM_MAXP; ++i)

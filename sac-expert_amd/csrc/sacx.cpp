@@ -108,6 +108,7 @@ struct sacx_handle {
     std::vector<Launch> plan[NSLOT];
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
     int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
+    int xcd_map = 1;          // GEMM tiles XCD-contiguous (SACX_XCD=0 restores dispatch order)
     std::vector<Launch> mplan;
     hipGraphExec_t mgraph = nullptr;
     int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
@@ -394,6 +395,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
     L.gemm.nprob = (int)ps.size();
     L.gemm.total_tiles = tiles;
+    L.gemm.xcd_map = h->xcd_map;
     L.gemm.p_stride = h->p_stride;
     L.gemm.ctl = h->ctl();
     L.gemm.adam.lr[GRP_Q] = h->cfg.lr_q;
@@ -1185,6 +1187,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
         std::vector<float> ones((size_t)(so.rows * so.cols), 1.0f);
         HIPCHK(h, hipMemcpy(h->arena + so.off, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice));
     }
+    if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     for (int sl = 0; sl < NSLOT; ++sl) build_plan(h, sl, sl == 0);
     for (int sl = 1; sl < NSLOT; ++sl) {

@@ -146,6 +146,7 @@ struct GemmArgs {
     int32_t vec;           // GM_FWD/GM_DX: float4 loads along k (ld % 4 == 0, K % 4 == 0, aligned);
                            // GM_FWD2: layer-0 K steps of 4, rounded up to even (2..16)
     int32_t total_tiles;
+    int32_t xcd_map;       // 1: each XCD takes a contiguous tile range (see xcd_tile)
     int64_t p_stride;      // floats between params / adam_m / adam_v blocks
     const Ctl* ctl;
     AdamConsts adam;
