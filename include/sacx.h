@@ -151,6 +151,18 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
  * otherwise u = np.random.normal(size=(n,A)) from the device copy of the global stream,
  * in the order the reference would draw it.  Behaviour-policy inference for the env loop. */
 int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
+/* batch_simtrajectory_sampler (sac_eo/common/samplers.py:73-122) with world model `model`
+ * as the environment (MSEModel.reset / step, sac_eo/models/continuous_models.py:225-258)
+ * and the actor's sample() (continuous_actors.py:270-306), all on the device.
+ * s_init[n,S] (device) -> s_out[n,H,S], a_out[n,H,A], r_out[n,H], sp_out[n,H,S], d_out[n,H]
+ * (uint8; always 0: MSEModel.step never terminates).  Per step t: a = sample(s_t) drawing
+ * np.random.normal(size=(n, A)) from the device stream (nothing when deterministic);
+ * (delta_n, r_n) = model([norm s_t, norm clip(a)]), clipped to +-delta_clip / +-reward_clip
+ * when > 0 (--delta_clip_pred / --reward_clip_pred); s_{t+1} = s_t + delta_n*den + mean.
+ * Requires use_expert (the models exist only then). */
+int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
+                 int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
+                 float* r_out, float* sp_out, uint8_t* d_out);
 int sacx_sync(sacx_handle* h);
 
 /* --- measurement ----------------------------------------------------------- */

@@ -553,6 +553,50 @@ def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches):
 
 
 # ---------------------------------------------------------------------------
+# world-model rollout (F2): batch_simtrajectory_sampler (samplers.py:73-122) with an
+# MSEModel as the environment (continuous_models.py:225-258)
+# ---------------------------------------------------------------------------
+def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k: int, rs=None,
+            deterministic: bool = False, delta_clip: float = 0.0, reward_clip: float = 0.0):
+    """Returns (s, a, r, sp, d) of shapes [n,H,S], [n,H,A], [n,H], [n,H,S], [n,H].
+
+    Per step (samplers.py:89-116): a = actor.sample(s) (continuous_actors.py:270-306,
+    u = rs.normal(size=(n, A)) cast to f32, none when deterministic); env.step(actor.clip(a))
+    = MSEModel.step: (delta_n, r_n) = _forward(s, clip(a)) with the optional prediction clips
+    (base_world_model.py:65-87), s <- s + delta_rms.denormalize(delta_n), r =
+    r_rms.denormalize(r_n), d = (ones_like(r) == 0) = False; the last step stores
+    d = terminated (all False)."""
+    dt = st.alpha.dtype.type
+    F = lambda x: _F(dt, x)
+    nrm = nrm.cast(dt)
+    S, A = cfg.S, cfg.A
+    s = np.asarray(s_init, dt).reshape(-1, S)
+    n = s.shape[0]
+    out = dict(s=[], a=[], r=[], sp=[], d=[])
+    lim = F(cfg.act_limit)
+    for _ in range(horizon):
+        x = _norm(s, nrm.s_mean, nrm.s_den)
+        o, _ = mlp_forward(st.actor, x, cfg.act)
+        mu, lraw = split_head(o, st.logstd, cfg)
+        u = np.zeros_like(mu) if deterministic else f32_noise(rs.normal(size=mu.shape)).astype(dt)
+        a, _ = head_sample(mu, lraw, u, cfg.act_limit, dt)
+        ac = np.clip(a, -lim, lim)                                # actor.clip (continuous_actors.py:125)
+        xm = np.concatenate([x, _norm(ac, nrm.a_mean, nrm.a_den)], 1)
+        pred, _ = mlp_forward(st.models[k], xm, cfg.model_act)
+        dn, rn = pred[:, :S], pred[:, S]
+        if delta_clip:
+            dn = np.clip(dn, -F(delta_clip), F(delta_clip))
+        if reward_clip:
+            rn = np.clip(rn, -F(reward_clip), F(reward_clip))
+        sp = s + (dn * nrm.d_den + nrm.d_mean)
+        r = rn * nrm.r_den + nrm.r_mean
+        for key, v in (("s", s), ("a", a), ("r", r), ("sp", sp), ("d", np.zeros(n, bool))):
+            out[key].append(v)
+        s = sp
+    return tuple(np.stack(out[key], axis=1) for key in ("s", "a", "r", "sp", "d"))
+
+
+# ---------------------------------------------------------------------------
 # RNG consumption in the reference's order (SURVEY.md §8a, "RNG consumption
 # order"): the global legacy NumPy stream feeds the sampler and every noise
 # draw; the expert split uses the algorithm's Generator (base_onpolicy_alg.py:109).

@@ -1409,6 +1409,50 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
     hipLaunchKernelGGL(k_obs_norm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, obs, n, S, mean, den, X, ldX);
 }
 
+// ==================================================================== k_roll
+// one wave per trajectory row.  mode 0 (prep): s_t (s_init at t = 0, copied to s_out) is
+// normalised into the actor input and the state columns of the model input
+// (BaseActor._transform_state, BaseWorldModel._forward: same s_rms).  mode 1 (finish):
+// MSEModel.step -- s_{t+1} = s_t + denorm_delta(clip(delta_n)), r = denorm_r(clip(r_n)),
+// d = False (tf.ones_like(r) == 0) -- and the stores of samplers.py:98-116.
+__global__ __launch_bounds__(256) void k_roll(RollArgs g) {
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wave;
+    if (i >= g.n) return;
+    const int S = g.S, A = g.A;
+    const int64_t o = (int64_t)i * g.H + g.t;
+    if (g.mode == 0) {
+        const float* src = (g.t == 0 && g.s_init) ? g.s_init + (int64_t)i * S : g.s_out + o * S;
+        for (int j = lane; j < S; j += 64) {
+            const float v = src[j];
+            if (g.t == 0 && g.s_init) g.s_out[o * S + j] = v;
+            const float xn = (v - g.s_mean[j]) / g.s_den[j];
+            g.X[(int64_t)i * g.ldS + j] = xn;
+            g.Xm[(int64_t)i * g.ldQ + j] = xn;
+        }
+        return;
+    }
+    const float* Oi = g.O + (int64_t)i * (S + 1);
+    for (int j = lane; j < S; j += 64) {
+        float dn = Oi[j];
+        if (g.clip_d > 0.f) dn = fminf(fmaxf(dn, -g.clip_d), g.clip_d);
+        const float sp = g.s_out[o * S + j] + (dn * g.d_den[j] + g.d_mean[j]);
+        g.sp_out[o * S + j] = sp;
+        if (g.t + 1 < g.H) g.s_out[(o + 1) * S + j] = sp;
+    }
+    for (int j = lane; j < A; j += 64) g.a_out[o * A + j] = g.a_raw[(int64_t)i * A + j];
+    if (lane == 0) {
+        float rn = Oi[S];
+        if (g.clip_r > 0.f) rn = fminf(fmaxf(rn, -g.clip_r), g.clip_r);
+        g.r_out[o] = rn * g.r_norm[1] + g.r_norm[0];
+        g.d_out[o] = 0;
+    }
+}
+
+void launch_roll(const RollArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_roll, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
+}
+
 __global__ void k_set_pseq(Ctl* ctl, int slot) { ctl->pseq[slot] = ctl->step_seq; }
 
 void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s) {

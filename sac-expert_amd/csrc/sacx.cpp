@@ -152,6 +152,7 @@ int fail(sacx_handle* h, const std::string& msg) {
     } while (0)
 
 constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
+constexpr int ROLL_CAP = 4096;  // trajectories per sacx_rollout launch chain
 
 void build_layout(sacx_handle* h) {
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B;
@@ -284,6 +285,16 @@ void build_layout(sacx_handle* h) {
         h->add("ws.Df2", R2, Hm1, F, 0);
         h->add("ws.Df1", R2, Hm0, F, 0);
         h->add("ws.lf", 1, R2, F, 0);
+        // model rollout (sacx_rollout), up to ROLL_CAP trajectories per launch chain
+        h->add("roll.X", ROLL_CAP, h->ldS, F, 0);
+        h->add("roll.H1", ROLL_CAP, H0, F, 0);
+        h->add("roll.H2", ROLL_CAP, H1, F, 0);
+        h->add("roll.noise", 1, (int64_t)ROLL_CAP * A, F, 0);
+        h->add("roll.A", ROLL_CAP, A, F, 0);
+        h->add("roll.Xm", ROLL_CAP, h->ldQ, F, 0);
+        h->add("roll.M1", ROLL_CAP, Hm0, F, 0);
+        h->add("roll.M2", ROLL_CAP, Hm1, F, 0);
+        h->add("roll.O", ROLL_CAP, O, F, 0);
     }
     h->arena_bytes = (h->arena_bytes + 255) & ~uint64_t(255);
 }
@@ -1438,6 +1449,74 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
         a.alpha_mode = 0;
         FinalArgs f{};
         launch_actor_head(a, f, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
+                 int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
+                 float* r_out, float* sp_out, uint8_t* d_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "rollout needs the world models (use_expert)");
+    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (n < 0 || horizon < 0) return fail(h, "bad arguments");
+    if (n == 0 || horizon == 0) return 0;
+    if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
+    const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    const std::string mn = "m" + std::to_string(model);
+    // steps outer, chunks inner: each step draws normal(size=(n, A)) in row order, exactly the
+    // reference's one draw per step (samplers.py:92) however the rows are chunked
+    for (int t = 0; t < horizon; ++t) {
+        for (int64_t c0 = 0; c0 < n; c0 += ROLL_CAP) {
+            const int m = (int)std::min<int64_t>(ROLL_CAP, n - c0);
+            RollArgs ra{};
+            ra.n = m; ra.S = S; ra.A = A; ra.H = horizon; ra.t = t; ra.ldS = ldS; ra.ldQ = ldQ;
+            ra.s_init = s_init + c0 * S;
+            ra.s_out = s_out + c0 * horizon * S; ra.a_out = a_out + c0 * horizon * A;
+            ra.r_out = r_out + c0 * horizon; ra.sp_out = sp_out + c0 * horizon * S; ra.d_out = d_out + c0 * horizon;
+            ra.O = W("roll.O"); ra.a_raw = W("roll.A"); ra.X = W("roll.X"); ra.Xm = W("roll.Xm");
+            ra.s_mean = W("norm.s_mean"); ra.s_den = W("norm.s_den");
+            ra.d_mean = W("norm.d_mean"); ra.d_den = W("norm.d_den"); ra.r_norm = W("norm.r");
+            ra.clip_d = delta_clip; ra.clip_r = reward_clip;
+            ra.mode = 0;
+            launch_roll(ra, h->stream);
+            float* noise = deterministic ? nullptr : W("roll.noise");
+            if (!deterministic) {      // actor.sample: u = np.random.normal(size=(m, A))
+                RngArgs r{};
+                r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
+                r.n_int = 0; r.n_norm = m * A; r.out_idx = nullptr; r.out_norm = noise;
+                r.slot = -1; r.reset_seq = 0; r.nupd = 1;
+                launch_rng(r, h->stream);
+            }
+            std::vector<Launch> pl;
+            add_gemm(h, pl, "roll.a.fwd0", {prob_fwd(W("roll.X"), ldS, m, S, W("actor.l0"), H0, W("roll.H1"), h->act)}, false);
+            add_gemm(h, pl, "roll.a.fwd1", {prob_fwd(W("roll.H1"), H0, m, H0, W("actor.l1"), H1, W("roll.H2"), h->act)}, false);
+            for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+            pl.clear();
+            HeadArgs a{};
+            a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+            a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
+            a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+            a.nseg = 1;
+            // sample(): raw action to roll.A, normalised clip(a) (= a: |lim tanh| <= lim) into
+            // the action columns of the model input
+            a.seg[0] = {0, m, 1, 0, noise, W("roll.Xm"), nullptr, W("roll.A")};
+            a.total_rows = m;
+            a.cache_row0 = 1 << 30;
+            a.alpha_mode = 0;
+            FinalArgs f{};
+            launch_actor_head(a, f, h->stream);
+            add_gemm(h, pl, "roll.m.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->mact)}, false);
+            add_gemm(h, pl, "roll.m.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->mact)}, false);
+            add_gemm(h, pl, "roll.m.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), O, W("roll.O"), ACT_NONE)}, false);
+            for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+            h->probs_cursor -= 5;      // host table bookkeeping of add_gemm (these launches are not in a plan)
+            ra.mode = 1;
+            launch_roll(ra, h->stream);
+        }
     }
     HIPCHK(h, hipGetLastError());
     return 0;

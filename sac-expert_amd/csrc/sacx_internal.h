@@ -279,6 +279,21 @@ struct MFinalArgs {
     float* mstats; int32_t mstats_cap;
 };
 
+// ---------------------------------------------------------------- model rollout (F2)
+// batch_simtrajectory_sampler (samplers.py:73-122) over MSEModel.step
+// (continuous_models.py:225-242): one chunk of rows, output row i at (i * H + t)
+struct RollArgs {
+    int32_t mode;               // 0: prep step t (s_t -> actor / model inputs), 1: finish step t
+    int32_t n, S, A, H, t, ldS, ldQ;
+    const float* s_init;        // [n, S] (mode 0, t == 0)
+    float* s_out; float* a_out; float* r_out; float* sp_out; uint8_t* d_out;
+    const float* O;             // model output [n, S+1] = [delta_n | r_n]
+    const float* a_raw;         // actor sample [n, A]
+    float* X; float* Xm;        // actor input [n, ldS], model input [n, ldQ] (columns < S)
+    const float *s_mean, *s_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den)
+    float clip_d, clip_r;       // > 0: clip_by_value(-clip, clip) (delta_clip_pred / reward_clip_pred)
+};
+
 // launchers (defined in k_sac.hip)
 void launch_gemm(const GemmArgs& a, hipStream_t s);
 void launch_rng(const RngArgs& a, hipStream_t s);
@@ -296,5 +311,6 @@ void launch_spin(double us, hipStream_t s);
 void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, const float* den, float* X, int ldX,
                      hipStream_t s);
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
+void launch_roll(const RollArgs& a, hipStream_t s);
 
 }  // namespace sacx

@@ -253,6 +253,26 @@ class Engine:
         self._keep_act = o
         return out[0] if single else out
 
+    def rollout(self, model: int, s_init, horizon: int, deterministic: bool = False,
+                delta_clip: float = 0.0, reward_clip: float = 0.0):
+        """batch_simtrajectory_sampler (samplers.py:73-122) with world model `model` as the
+        environment: s_init [n, S] -> (s, a, r, sp, d) of shapes [n,H,S], [n,H,A], [n,H],
+        [n,H,S], [n,H] (CUDA tensors, d bool).  Draws the actor's noise from the device copy
+        of the global NumPy stream, one normal(size=(n, A)) per step."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        s0 = self._dev(s_init, (-1, S))
+        n, H = int(s0.shape[0]), int(horizon)
+        kw = dict(dtype=torch.float32, device=self.device)
+        s, a, r, sp = (torch.empty((n, H, S), **kw), torch.empty((n, H, A), **kw),
+                       torch.empty((n, H), **kw), torch.empty((n, H, S), **kw))
+        d = torch.empty((n, H), dtype=torch.uint8, device=self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        N.check(self.lib.sacx_rollout(self.h, int(model), p(s0), n, H, int(bool(deterministic)),
+                                      float(delta_clip or 0.0), float(reward_clip or 0.0),
+                                      p(s), p(a), p(r), p(sp), p(d)), self.h, "rollout")
+        self._keep_roll = s0
+        return s, a, r, sp, d.bool()
+
     # ------------------------------------------------------------------ hot path
     def step(self, n: int = 1, num_timesteps: int = 0, ts_increment: int = 1, external: bool = False,
              eager: bool = False):

@@ -264,3 +264,29 @@ def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n
     dev, ref = eng.rng_get_state(), ref_rs.get_state()
     assert np.array_equal(dev[1], ref[1]) and dev[2] == ref[2] and dev[3] == ref[3] and dev[4] == ref[4]
     eng.close()
+
+
+@pytest.mark.parametrize("deterministic,n,horizon,clip", [(False, 37, 5, 0.0), (True, 8, 3, 0.0),
+                                                         (False, 4100, 2, 0.05)])
+def test_rollout_matches_oracle(gpu_available, deterministic, n, horizon, clip):
+    """World-model rollout (samplers.py:73-122 over MSEModel.step) vs oracle.rollout: the
+    noise stream bit-exact (one normal(size=(n, A)) per step, chunked at 4096 rows), the
+    trajectories within 1e-4 relative (fp32 device vs fp64 oracle over the horizon)."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="tanh", B=64, seed=51, use_expert=True, normalizers="random")
+    S = ocfg.S
+    s0 = (np.random.RandomState(5).normal(size=(n, S)) * 1.5).astype(np.float32)
+    eng.rng_set_state(np.random.RandomState(23).get_state())
+    ref_rs = np.random.RandomState(23)
+    got = [t.cpu().numpy() for t in eng.rollout(1, s0, horizon, deterministic, delta_clip=clip)]
+    ref = O.rollout(st, ocfg, nrm, s0, horizon, 1, ref_rs, deterministic, delta_clip=clip)
+    for g, r, name in zip(got, ref, ("s", "a", "r", "sp", "d")):
+        assert g.shape == r.shape, (name, g.shape, r.shape)
+        if name == "d":
+            assert not g.any()
+        else:
+            assert relerr(g, r) < 1e-4, (name, relerr(g, r))
+    assert np.array_equal(got[0][:, 0], s0)
+    assert np.array_equal(got[0][:, 1:], got[3][:, :-1])
+    dev, rr = eng.rng_get_state(), ref_rs.get_state()
+    assert np.array_equal(dev[1], rr[1]) and dev[2] == rr[2] and dev[3] == rr[3] and dev[4] == rr[4]
+    eng.close()

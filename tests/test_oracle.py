@@ -231,3 +231,24 @@ def test_model_fit_step_matches_autograd():
     assert abs(loss - tot.item()) < 1e-12
     for w1, w2 in zip(st.models[0] + st.models[1], ref.models[0] + ref.models[1]):
         np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=1e-14)
+
+
+def test_rollout_oracle_consumes_one_draw_per_step():
+    """oracle.rollout (samplers.py:73-122): one normal(size=(n, A)) per step, s_{t+1} = sp_t,
+    d all False; deterministic draws nothing."""
+    cfg = O.Config(S=3, A=2, hidden=(8, 8), act="tanh", B=4, model_hidden=(8, 8))
+    st = O.init_state(cfg, seed=3, with_models=True).astype(np.float64)
+    nrm = O.Normalizers.identity(3, 2)
+    s0 = np.random.RandomState(1).normal(size=(5, 3))
+    rs = np.random.RandomState(7)
+    s, a, r, sp, d = O.rollout(st, cfg, nrm, s0, 4, 0, rs)
+    ref = np.random.RandomState(7)
+    for _ in range(4):
+        ref.normal(size=(5, 2))
+    assert rs.get_state()[2] == ref.get_state()[2] and np.array_equal(rs.get_state()[1], ref.get_state()[1])
+    assert s.shape == (5, 4, 3) and a.shape == (5, 4, 2) and r.shape == (5, 4) and d.shape == (5, 4)
+    assert np.array_equal(s[:, 1:], sp[:, :-1]) and not d.any()
+    assert np.all(np.abs(a) <= 1.0)
+    rs2 = np.random.RandomState(7)
+    O.rollout(st, cfg, nrm, s0, 4, 0, rs2, deterministic=True)
+    assert rs2.get_state()[2] == np.random.RandomState(7).get_state()[2]
