@@ -41,17 +41,20 @@ FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak,
 HBM_PEAK_GBS = 8000.0
 
 
-def build_engine(cfgd, seeds, device):
-    """seeds: this replica's reference-style seeds (sac_eo.common.seeding.derive_seeds)."""
+def build_engine(cfgd, seeds, device, dp=None, batch=None, weight_seed=None):
+    """seeds: this replica's reference-style seeds (sac_eo.common.seeding.derive_seeds).
+    dp: (rccl id, ranks, rank) for the data-parallel mode, with the local `batch` and one
+    `weight_seed` shared by all ranks (identical initial weights)."""
     import torch
     from sac_eo.engine import Engine, EngineConfig
     from sac_eo.nets import create_nn_weights
-    S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
+    S, A = cfgd["S"], cfgd["A"]
+    B = batch or cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
                         expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "128")))
-    eng = Engine(ecfg, device=device)
-    rng = np.random.default_rng(seeds["setup"])        # weights (init_seeds(setup_seed) then nets)
+    eng = Engine(ecfg, device=device, dp=dp)
+    rng = np.random.default_rng(weight_seed if weight_seed is not None else seeds["setup"])
     eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
     for k in range(2):
         w = create_nn_weights(rng, S + A, 1, cfgd["hidden"], 1.0)
@@ -182,6 +185,38 @@ def cpu_baseline(cfgd, seconds=10.0):
                       f"{el:.1f}s, BLAS threads={threads}; TensorFlow reference not installable"}
 
 
+def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):
+    """SAC-EO's world-model calls at the reference defaults (rank 0, after the timed
+    region): model fitting (A16: 2 models x minibatch 200 per step, SAC_expert.py:519-550)
+    and the rollout (F2: --sim_batch_size 10000 over 2 models = 1000 trajectories x
+    --sim_horizon 5 per model, mbrl_onpolicy_alg.py:72-100)."""
+    import torch
+    S, A = cfgd["S"], cfgd["A"]
+    mb = eng.cfg.model_batch
+    idx = np.random.RandomState(3).randint(cfgd["buffer"], size=(n_fit + 10, 2, mb))
+    eng.model_fit(idx[:10])
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.model_fit(idx[10:])
+    eng.sync()
+    fit_s = (time.perf_counter() - t0) / n_fit
+    Hm = 512
+    macs = 3 * ((S + A) * Hm + Hm * Hm + Hm * (S + 1)) - (S + A) * Hm      # SURVEY.md §8d model-fit row
+    fit_flops = 2.0 * macs * 2 * mb
+    s0 = torch.randn(1000, S, device=eng.device)
+    eng.rollout(0, s0, 5)
+    eng.sync()
+    t0 = time.perf_counter()
+    for _ in range(n_roll):
+        eng.rollout(0, s0, 5)
+    eng.sync()
+    roll_s = (time.perf_counter() - t0) / n_roll
+    return ({"steps_per_s": round(1.0 / fit_s, 1), "us_per_step": round(fit_s * 1e6, 2),
+             "tflops": round(fit_flops / fit_s / 1e12, 3), "models": 2, "minibatch": mb, "graph": True},
+            {"n_traj": 1000, "horizon": 5, "ms_per_call": round(roll_s * 1e3, 4),
+             "transitions_per_s": round(5000 / roll_s, 1), "launches_per_step": 9, "graph": False})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -191,6 +226,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--mode", default="replicas", choices=["replicas", "dp"],
+                    help="replicas: one independent learner per GPU (the metric); dp: one learner, "
+                         "global batch split over the GPUs, gradients all-reduced by RCCL (config C4)")
     args = ap.parse_args()
 
     import torch
@@ -198,7 +236,17 @@ def main():
     rep = init_replica()                      # one learner per GPU, RCCL only for barrier / max time
     ws, rank, device = rep.world_size, rep.rank, rep.device
     cfgd = CONFIGS[args.config]
-    eng = build_engine(cfgd, rep.seeds(0), device=device)
+    dp = args.mode == "dp"
+    if dp:
+        from sac_eo.engine import Engine
+        from sac_eo.common.seeding import derive_seeds
+        if cfgd["use_expert"] or cfgd["B"] % ws:
+            raise SystemExit("dp mode: plain SAC configs with batch divisible by the GPU count")
+        uid = rep.broadcast_bytes(Engine.dp_unique_id() if rank == 0 else None)
+        eng = build_engine(cfgd, rep.seeds(0), device=device, dp=(uid, ws, rank), batch=cfgd["B"] // ws,
+                           weight_seed=int(derive_seeds(0, runs=1)["setup"][0]))
+    else:
+        eng = build_engine(cfgd, rep.seeds(0), device=device)
     barrier = rep.barrier
 
     eng.step(args.warmup, num_timesteps=0, ts_increment=1)
@@ -212,12 +260,15 @@ def main():
     el = rep.max_over_ranks(t1 - t0)
     stats = eng.stats(1)[0]
     finite = bool(np.all(np.isfinite(stats)))
-    value = args.steps * ws / el
+    value = args.steps * (1 if dp else ws) / el     # dp: every rank runs the same global update
     roof = None
-    if rank == 0 and not args.no_roofline:
+    if rank == 0 and not args.no_roofline and not dp:
         roof, _ = roofline(eng, args.config)
+    fit = roll = None
+    if rank == 0 and cfgd["use_expert"]:
+        fit, roll = world_model_legs(eng, cfgd)
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline and not dp:
         cpu = cpu_baseline(cfgd, args.cpu_seconds)
     if rank == 0:
         line = {
@@ -225,17 +276,21 @@ def main():
             else "SAC-EO gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)",
             "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "strong" if dp else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (HalfCheetah-shaped replay rows generated on device; random orthogonal init)",
             "config": {"workload": cfgd["workload"], "obs_dim": cfgd["S"], "act_dim": cfgd["A"],
                        "batch": cfgd["B"], "hidden": list(cfgd["hidden"]), "buffer_rows": cfgd["buffer"],
-                       "parallelism": f"replicas x{ws} (independent seeds, no collective)",
+                       "parallelism": (f"dp{ws}: one learner, batch {cfgd['B'] // ws} per GPU, 3 RCCL all-reduces "
+                                       "per update (critic, actor, alpha gradients)") if dp else
+                                      f"replicas x{ws} (independent seeds, no collective)",
                        "sampler": "NumPy-legacy MT19937 stream on device (bit-exact indices)"},
             "finite_stats": finite,
             "last_stats": {k: float(v) for k, v in zip(
                 ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss", "nlp_mean", "step"], stats)},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if fit is not None:
+            line["model_fit"], line["rollout"] = fit, roll
         print(json.dumps(line), flush=True)
     eng.close()
     rep.close()

@@ -165,6 +165,19 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
                  float* r_out, float* sp_out, uint8_t* d_out);
 int sacx_sync(sacx_handle* h);
 
+/* --- data-parallel mode (config C4: one learner over k GPUs) --------------------
+ * Not in the reference (its --runs are independent learners, sac_eo/train.py:118-152):
+ * each rank samples its local batch from its own buffer and stream; the critic, actor
+ * (+logstd) and alpha gradients are summed over the ranks by RCCL inside the update
+ * graph (three all-reduces per update: 2*P_q, P_a + A, 1 floats) and every rank applies
+ * the same Keras Adam with gradient/k, so weights stay identical when they start so.
+ * With batch = B/k this is the B-row update of SAC.py:236-250 (the losses are means).
+ * sacx_dp_unique_id: on one rank, fills id_out (cap >= 128 bytes), returns its size.
+ * sacx_dp_init: on every rank after sacx_create, before sacx_bind, on the rank's device.
+ * Plain SAC only (use_expert = 0). */
+int sacx_dp_unique_id(void* id_out, int32_t cap);
+int sacx_dp_init(sacx_handle* h, const void* id, int32_t nranks, int32_t rank);
+
 /* --- measurement ----------------------------------------------------------- */
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);
 /* Runs n_steps updates eagerly with a HIP event around every launch on the

@@ -376,11 +376,15 @@ def _norm(x, mean, den):
 
 
 def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, noise_pi, noise_alpha,
-               expert: Optional[Expert] = None, do_polyak: bool = True, keep: Optional[dict] = None):
+               expert: Optional[Expert] = None, do_polyak: bool = True, keep: Optional[dict] = None,
+               grad_hook=None):
     """One ``_update`` (SAC_expert.py:463-477 / SAC.py:236-250), in place on
     ``st``.  ``batch`` = (s, a, sp, r, d) raw rows; noises are (n, A) arrays.
     Returns the step statistics.  ``keep`` (optional dict) receives the
-    intermediates used by the stage-level GPU parity tests."""
+    intermediates used by the stage-level GPU parity tests.  ``grad_hook(name, grads)``
+    (optional) maps each optimiser's gradient list before its Adam ("q0", "q1", "actor",
+    "alpha"): the data-parallel mode's all-reduce / ranks (include/sacx.h sacx_dp_init)."""
+    hook = grad_hook if grad_hook is not None else (lambda name, g: g)
     dt = st.alpha.dtype.type
     F = lambda x: _F(dt, x)
     nrm = nrm.cast(dt)
@@ -417,7 +421,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
             keep["q%d_h" % k] = hs
             keep["q%d_out" % k] = q[:, 0]
             keep["q%d_grads" % k] = grads
-        adam_step(st.q[k], grads, st.opt_q[k], cfg.lr_q, dt)
+        adam_step(st.q[k], hook("q%d" % k, grads), st.opt_q[k], cfg.lr_q, dt)
 
     # ---------------- actor (_update_actor_and_alpha, :262-338)
     out_p, hs_p = mlp_forward(actor_all, s_n, cfg.act)
@@ -494,7 +498,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
         keep.update(actor_h_p=hs_p, mu_p=mu_p, a_p=a_p, nlp_p=nlp_p, q1p=q1p, q2p=q2p,
                     dxa=dxa, dmu=DMU, dl=DL, actor_grads=grads_a, g_logstd=g_logstd)
     stats["p_loss"] = float(p_loss)
-    adam_step(st.actor + [st.logstd], grads_a + [g_logstd], st.opt_actor, cfg.lr_pi, dt)
+    adam_step(st.actor + [st.logstd], hook("actor", grads_a + [g_logstd]), st.opt_actor, cfg.lr_pi, dt)
 
     # ---------------- alpha (:340-348)
     out_3, _ = mlp_forward(st.actor, s_n, cfg.act)
@@ -504,7 +508,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     stats["alpha_loss"] = float(-alpha * m_ent)
     g_alpha = np.asarray(-m_ent, dt)
     al = [st.alpha]
-    adam_step(al, [g_alpha], st.opt_alpha, cfg.lr_alpha, dt)
+    adam_step(al, hook("alpha", [g_alpha]), st.opt_alpha, cfg.lr_alpha, dt)
     st.alpha = np.maximum(st.alpha, F(1e-5)).astype(dt)
     stats["alpha"] = float(st.alpha)
     if keep is not None:

@@ -247,6 +247,18 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
         const int64_t tnew = ctl->t_sac + 1;
         const float alpha_old = *f.alpha;
         const float g = -m_ent;                 // d(-alpha*m)/d alpha
+        if (f.alpha_g != nullptr) {             // data-parallel: k_alpha_apply finishes after the all-reduce
+            *f.alpha_g = g;
+            float* st = f.stats + (size_t)(ctl->step_seq % f.stats_cap) * 8;
+            st[0] = q1;
+            st[1] = q2;
+            st[2] = pl;
+            st[3] = -alpha_old * m_ent;
+            st[5] = mse;
+            st[6] = -(m_ent - f.target_entropy);
+            st[7] = (float)ctl->step_seq;
+            return;
+        }
         const float lr_t = adam_lr(f.adam, GRP_ALPHA, tnew);
         float an = adam_update(f.alpha, f.alpha_m, f.alpha_v, g, lr_t);
         an = fmaxf(an, 1e-5f);                  // SAC_expert.py:348
@@ -541,6 +553,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     } else if constexpr (MODE == GM_DX) {
         g.C[(size_t)mm * g.ldc + nn] = v * dact_f(e0, g.act);
     } else {
+        if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
+            g.P[pidx + 3 * ga.p_stride] = v * g.grad_scale;
+            return;
+        }
         const Ctl* ctl = ga.ctl;
         const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
         const float lr_t = adam_lr(ga.adam, g.group, tstep);
@@ -1407,6 +1423,55 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
                      hipStream_t s) {
     const int64_t tot = n * ldX;
     hipLaunchKernelGGL(k_obs_norm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, obs, n, S, mean, den, X, ldX);
+}
+
+// ==================================================================== data-parallel Adam
+// k_adam_apply: element i of a parameter range, gradient = all-reduced sum * (1 / ranks);
+// the arithmetic of the fused GM_DW epilogue, so one rank reproduces it bit for bit.
+__global__ __launch_bounds__(256) void k_adam_apply(AdamApplyArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const Ctl* ctl = a.ctl;
+    const int64_t tstep = (a.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
+    const float lr_t = adam_lr(a.adam, a.group, tstep);
+    float* P = a.P + i;
+    const float gr = P[3 * a.p_stride] * a.grad_scale;
+    const float e0 = P[0], e1 = P[a.p_stride], e2 = P[2 * a.p_stride];
+    const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+    const float mm1 = e1 + (gr - e1) * (1.f - b1);
+    const float vv1 = e2 + (gr * gr - e2) * (1.f - b2);
+    const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
+    P[0] = pn;
+    P[a.p_stride] = mm1;
+    P[2 * a.p_stride] = vv1;
+    if (a.t_off != 0) {
+        const int64_t tui = a.adam.target_update_int > 0 ? a.adam.target_update_int : 1;
+        if (ctl->num_timesteps % tui == 0) P[a.t_off] = P[a.t_off] * a.adam.tau_keep + pn * a.adam.tau_take;
+    }
+}
+
+void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_adam_apply, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+// the alpha half of finalize_update that follows the all-reduce of the alpha gradient
+__global__ void k_alpha_apply(FinalArgs f) {
+    if (threadIdx.x != 0) return;
+    Ctl* ctl = f.ctl;
+    const int64_t tnew = ctl->t_sac + 1;
+    const float lr_t = adam_lr(f.adam, GRP_ALPHA, tnew);
+    float an = adam_update(f.alpha, f.alpha_m, f.alpha_v, *f.alpha_g * f.grad_scale, lr_t);
+    an = fmaxf(an, 1e-5f);                      // SAC_expert.py:348
+    *f.alpha = an;
+    const int64_t seq = ctl->step_seq;
+    f.stats[(size_t)(seq % f.stats_cap) * 8 + 4] = an;
+    ctl->t_sac = tnew;
+    ctl->num_timesteps += ctl->ts_increment;
+    ctl->step_seq = seq + 1;
+}
+
+void launch_alpha_apply(const FinalArgs& f, hipStream_t s) {
+    hipLaunchKernelGGL(k_alpha_apply, dim3(1), dim3(64), 0, s, f);
 }
 
 // ==================================================================== k_roll

@@ -22,6 +22,8 @@
 #include "sacx.h"
 #include "sacx_internal.h"
 
+#include <rccl/rccl.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -49,7 +51,7 @@ struct SegInfo {
 };
 
 struct Launch {
-    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, FINAL, MGATHER, MLOSS, MFINAL } kind;
+    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, FINAL, MGATHER, MLOSS, MFINAL, ALLREDUCE, APPLY, AAPPLY } kind;
     std::string name;
     RngArgs rng;
     GatherArgs gather;
@@ -61,6 +63,9 @@ struct Launch {
     MGatherArgs mg;
     MLossArgs ml;
     MFinalArgs mf;
+    AdamApplyArgs ap;          // APPLY
+    float* ar_buf = nullptr;   // ALLREDUCE: in-place sum over the data-parallel ranks
+    int64_t ar_count = 0;
     int grid = 0, block = 256;
     double flops = 0, bytes = 0;
     int gemm_first = 0;  // index of the first problem in the host table (GEMM)
@@ -80,6 +85,9 @@ const char* kernel_family(Launch::Kind k) {
         case Launch::MGATHER: return "k_mgather";
         case Launch::MLOSS: return "k_mloss";
         case Launch::MFINAL: return "k_mfinal";
+        case Launch::ALLREDUCE: return "rccl_allreduce";
+        case Launch::APPLY: return "k_adam_apply";
+        case Launch::AAPPLY: return "k_alpha_apply";
     }
     return "?";
 }
@@ -109,6 +117,11 @@ struct sacx_handle {
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
     int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (SACX_XCD=0 restores dispatch order)
+    // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
+    // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
+    int dp_ranks = 0, dp_rank = 0;
+    ncclComm_t comm = nullptr;
+    bool nccl_failed = false;
     std::vector<Launch> mplan;
     hipGraphExec_t mgraph = nullptr;
     int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
@@ -182,6 +195,7 @@ void build_layout(sacx_handle* h) {
     h->arena_bytes = pbytes;
     h->add("adam_m", 1, h->p_stride, F, SACX_ROLE_STATE);
     h->add("adam_v", 1, h->p_stride, F, SACX_ROLE_STATE);
+    h->add("grad", 1, h->p_stride, F, SACX_ROLE_WORK);   // data-parallel gradients (+3 p_stride)
     // ---------------- normalisers (normalizer.py: (x - mean) / max(std, 1e-8))
     h->add("norm.s_mean", 1, S, F, SACX_ROLE_STATE);
     h->add("norm.s_den", 1, S, F, SACX_ROLE_STATE);
@@ -434,6 +448,41 @@ bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
     return true;
 }
 
+// Data-parallel mode: the dW launch `L` stores its local gradients (+3 p_stride) instead of
+// running Adam; RCCL sums the contiguous gradient range [first, last] over the ranks and
+// k_adam_apply runs the Adam (and Polyak into the same range at `targ`) with scale 1/ranks.
+void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string& first, const std::string& last,
+                   const std::string& targ, int group) {
+    Launch& G = plan.back();
+    for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
+    const std::string base = G.name.substr(0, G.name.find(".adam"));
+    G.name = base + ".grad";
+    const uint64_t o0 = h->off_of(first);
+    const SegInfo& sl = h->seg(last);
+    const int64_t n = (int64_t)((sl.off + (uint64_t)(sl.rows * sl.cols) * 4 - o0) / 4);
+    float* P = h->f(first);
+    Launch R{};
+    R.kind = Launch::ALLREDUCE;
+    R.name = base + ".allreduce";
+    R.ar_buf = P + 3 * h->p_stride;
+    R.ar_count = n;
+    R.grid = 0;
+    R.bytes = 8.0 * n;
+    plan.push_back(R);
+    Launch U{};
+    U.kind = Launch::APPLY;
+    U.name = base + ".adam";
+    AdamApplyArgs& a = U.ap;
+    a.P = P; a.n = n; a.p_stride = h->p_stride; a.group = group;
+    a.t_off = targ.empty() ? 0 : (int64_t)(h->off_of(targ) - o0) / 4;
+    a.grad_scale = (float)(1.0 / (double)h->dp_ranks);
+    a.ctl = h->ctl();
+    a.adam = G.gemm.adam;
+    U.grid = (int)((n + 255) / 256);
+    U.bytes = 4.0 * n * (targ.empty() ? 7 : 9);
+    plan.push_back(U);
+}
+
 void build_plan(sacx_handle* h, int slot, bool record_probs) {
     std::vector<Launch>& plan = h->plan[slot];
     plan.clear();
@@ -612,6 +661,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                  W(n + ".l2"), W(t + ".l2"), GRP_Q));
         }
         add_gemm(h, plan, "critic.adam", pw, record_probs);
+        if (h->dp_ranks > 0) dp_split_adam(h, plan, "q0.l0", "q1.l2", "t0.l0", GRP_Q);
     }
     // ---- policy loss through the updated critics: the same linearity; pi.q.head's rows
     // (min, tie split, loss rows, g0 / g1) share the unscaled dX launch, actor.head.bwd applies
@@ -737,6 +787,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             pw.push_back(p);
         }
         add_gemm(h, plan, "actor.adam", pw, record_probs);
+        if (h->dp_ranks > 0) dp_split_adam(h, plan, "actor.l0", "actor.logstd", "", GRP_PI);
     }
     // ---- alpha: updated actor on s, evaluate, Adam on alpha, statistics
     const size_t alpha_first = plan.size();
@@ -782,7 +833,27 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.grid = 1;
         L.block = 64;
         L.bytes = 4.0 * (f.nred + 3.0 * B + ne);
-        plan.push_back(L);
+        if (h->dp_ranks > 0) {              // alpha gradient: local -> all-reduce -> Adam + counters
+            f.alpha_g = W("alpha") + 3 * h->p_stride;
+            f.grad_scale = (float)(1.0 / (double)h->dp_ranks);
+            L.name = "alpha.grad";
+            plan.push_back(L);
+            Launch R{};
+            R.kind = Launch::ALLREDUCE;
+            R.name = "alpha.allreduce";
+            R.ar_buf = f.alpha_g;
+            R.ar_count = 1;
+            plan.push_back(R);
+            Launch U{};
+            U.kind = Launch::AAPPLY;
+            U.name = "alpha.adam";
+            U.fin = f;
+            U.grid = 1;
+            U.block = 64;
+            plan.push_back(U);
+        } else {
+            plan.push_back(L);
+        }
     }
     // alpha.fwd .. alpha.final only feed the next update's q.head
     for (size_t i = alpha_first; i < plan.size(); ++i) plan[i].alpha_branch = true;
@@ -866,6 +937,12 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::MGATHER: launch_mgather(L.mg, s); break;
         case Launch::MLOSS: launch_mloss(L.ml, s); break;
         case Launch::MFINAL: launch_mfinal(L.mf, s); break;
+        case Launch::ALLREDUCE:
+            if (ncclAllReduce(L.ar_buf, L.ar_buf, (size_t)L.ar_count, ncclFloat32, ncclSum, h->comm, s) != ncclSuccess)
+                h->nccl_failed = true;
+            break;
+        case Launch::APPLY: launch_adam_apply(L.ap, s); break;
+        case Launch::AAPPLY: launch_alpha_apply(L.fin, s); break;
     }
 }
 
@@ -994,7 +1071,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         //     launches (merged_body), plus the last update's alpha branch as a tail;
         // rs: sampler + gather of update j+2 into slot (j+2)%3 == (j-1)%3, once update j's
         //     actor.head (the last reader of that slot, through the folded alpha rows) has run.
-        const bool merge = std::getenv("SACX_MERGE_ALPHA") == nullptr || std::atoi(std::getenv("SACX_MERGE_ALPHA"));
+        const bool merge = h->dp_ranks == 0 &&
+                           (std::getenv("SACX_MERGE_ALPHA") == nullptr || std::atoi(std::getenv("SACX_MERGE_ALPHA")));
         HIPCHK(h, hipEventRecord(evFork, cs));
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
         // Sampler batches [s, e): one k_rng launch draws updates s..e-1 in stream order and one
@@ -1158,6 +1236,7 @@ void sacx_destroy(sacx_handle* h) {
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
+    if (h->comm) (void)ncclCommDestroy(h->comm);
     delete h;
 }
 
@@ -1200,6 +1279,14 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     }
     if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
+    if (h->dp_ranks > 0) {
+        if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
+        const int64_t d = (int64_t)(h->off_of("t0.l0") - h->off_of("q0.l0"));
+        for (const char* l : {".l0", ".l1", ".l2"})
+            for (int k = 0; k < 2; ++k)
+                if ((int64_t)(h->off_of("t" + std::to_string(k) + l) - h->off_of("q" + std::to_string(k) + l)) != d)
+                    return fail(h, "internal: target layout is not a fixed shift of the critics");
+    }
     for (int sl = 0; sl < NSLOT; ++sl) build_plan(h, sl, sl == 0);
     for (int sl = 1; sl < NSLOT; ++sl) {
         if (h->plan[0].size() != h->plan[sl].size()) return fail(h, "internal: slot plans differ");
@@ -1213,6 +1300,29 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
     h->bound = true;
+    return 0;
+}
+
+int sacx_dp_unique_id(void* id_out, int32_t cap) {
+    if (!id_out || cap < (int32_t)sizeof(ncclUniqueId)) return -1;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -2;
+    std::memcpy(id_out, &id, sizeof(id));
+    return (int)sizeof(id);
+}
+
+int sacx_dp_init(sacx_handle* h, const void* id, int32_t nranks, int32_t rank) {
+    if (!h) return -1;
+    if (h->bound) return fail(h, "sacx_dp_init must precede sacx_bind");
+    if (h->comm) return fail(h, "data-parallel communicator already set");
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(h, "bad data-parallel arguments");
+    if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof(uid));
+    const ncclResult_t r = ncclCommInitRank(&h->comm, nranks, uid, rank);
+    if (r != ncclSuccess) return fail(h, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+    h->dp_ranks = nranks;
+    h->dp_rank = rank;
     return 0;
 }
 
@@ -1324,6 +1434,7 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
         }
     }
     h->seq_host += n_steps;
+    if (h->nccl_failed) return fail(h, "ncclAllReduce failed");
     return 0;
 }
 

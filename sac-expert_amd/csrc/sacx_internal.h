@@ -107,6 +107,10 @@ struct FinalArgs {
     int32_t nred;           // number of partials (alpha.head workgroups)
     int32_t mse_tiles;      // partials per expert row in mse_rows
     float* stats; int32_t stats_cap;
+    // data-parallel mode: the local alpha gradient goes here (then an all-reduce and
+    // k_alpha_apply do the Adam, clamp, stats[4] and counters); null: all in place
+    float* alpha_g;
+    float grad_scale;       // k_alpha_apply: 1 / ranks
 };
 
 struct QHeadArgs {
@@ -279,6 +283,18 @@ struct MFinalArgs {
     float* mstats; int32_t mstats_cap;
 };
 
+// ---------------------------------------------------------------- data-parallel Adam (C4)
+// After the gradient all-reduce: Keras Adam over a contiguous parameter range with the
+// summed gradients at +3 p_stride (scaled by 1/ranks), Polyak into P + t_off when t_off != 0.
+struct AdamApplyArgs {
+    float* P;
+    int64_t n, p_stride, t_off;
+    int32_t group;
+    float grad_scale;
+    const Ctl* ctl;
+    AdamConsts adam;
+};
+
 // ---------------------------------------------------------------- model rollout (F2)
 // batch_simtrajectory_sampler (samplers.py:73-122) over MSEModel.step
 // (continuous_models.py:225-242): one chunk of rows, output row i at (i * H + t)
@@ -312,5 +328,7 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
                      hipStream_t s);
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 void launch_roll(const RollArgs& a, hipStream_t s);
+void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s);
+void launch_alpha_apply(const FinalArgs& f, hipStream_t s);
 
 }  // namespace sacx

@@ -24,6 +24,7 @@ EXPORTS = [
     "sacx_buffer_append", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
+    "sacx_dp_unique_id", "sacx_dp_init",
 ]
 
 
@@ -119,6 +120,8 @@ def lib():
         "sacx_time_graph": (ctypes.c_int, [vp, i64, ctypes.c_char_p, P(f64)]),
         "sacx_actor_act": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sacx_time_kernels": (ctypes.c_int, [vp, ctypes.c_char_p, i32, P(f64), P(f64), P(i64)]),
+        "sacx_dp_unique_id": (ctypes.c_int, [vp, i32]),
+        "sacx_dp_init": (ctypes.c_int, [vp, vp, i32, i32]),
         "sacx_rollout": (ctypes.c_int, [vp, i32, vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():

@@ -57,6 +57,14 @@ class Replica:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
 
+    def broadcast_bytes(self, payload: bytes = None) -> bytes:
+        """Rank 0's payload on every rank (e.g. the RCCL unique id of the data-parallel mode)."""
+        if self.dist is None:
+            return payload
+        obj = [payload if self.rank == 0 else None]
+        self.dist.broadcast_object_list(obj, src=0)
+        return obj[0]
+
     def close(self):
         if self.dist is not None:
             self.dist.destroy_process_group()

@@ -89,7 +89,9 @@ class Engine:
 
     NETS = ("actor", "q0", "q1", "t0", "t1", "m0", "m1")
 
-    def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None, stream=None):
+    def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None, stream=None, dp=None):
+        """dp = (unique_id bytes, nranks, rank): data-parallel mode (sacx_dp_init), the
+        gradients of the local batch ``cfg.batch`` are summed over the ranks by RCCL."""
         if not torch.cuda.is_available():
             raise RuntimeError("sac_eo.engine needs a ROCm GPU (no CPU fallback)")
         self.cfg = cfg
@@ -119,9 +121,24 @@ class Engine:
             self.v[name] = t
         with torch.cuda.device(self.device):
             self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+            if dp is not None:
+                uid, nranks, rank = dp
+                buf = ctypes.create_string_buffer(bytes(uid), len(uid))
+                N.check(self.lib.sacx_dp_init(h, buf, int(nranks), int(rank)), h, "sacx_dp_init")
+        self.dp = dp
         N.check(self.lib.sacx_bind(h, ctypes.c_void_p(self.arena.data_ptr()), nbytes,
                                    ctypes.c_void_p(self.stream.cuda_stream)), h, "sacx_bind")
         self._init_state()
+
+    @staticmethod
+    def dp_unique_id() -> bytes:
+        """A fresh RCCL unique id (sacx_dp_unique_id) for Engine(dp=(id, nranks, rank))."""
+        lib = N.lib()
+        buf = ctypes.create_string_buffer(256)
+        n = lib.sacx_dp_unique_id(buf, 256)
+        if n <= 0:
+            raise RuntimeError("sacx_dp_unique_id failed")
+        return buf.raw[:n]
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):

@@ -290,3 +290,26 @@ def test_rollout_matches_oracle(gpu_available, deterministic, n, horizon, clip):
     dev, rr = eng.rng_get_state(), ref_rs.get_state()
     assert np.array_equal(dev[1], rr[1]) and dev[2] == rr[2] and dev[3] == rr[3] and dev[4] == rr[4]
     eng.close()
+
+
+@pytest.mark.parametrize("eager", [True, False])
+def test_dp_single_rank_equals_fused(gpu_available, eager):
+    """Data-parallel mode (sacx_dp_init) with one RCCL rank: local gradients stored, summed
+    by ncclAllReduce inside the update graph, then k_adam_apply / k_alpha_apply -- the same
+    arithmetic as the fused dW+Adam epilogue, so parameters, Adam state, targets and
+    statistics are bit-identical to the fused path over 19 updates (2 graphs + 3 singles)."""
+    from sac_eo.engine import Engine
+    outs = []
+    n = 19
+    for dp in (None, (Engine.dp_unique_id(), 1, 0)):
+        eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=128, seed=61, dp=dp)
+        eng.rng_set_state(np.random.RandomState(6).get_state())
+        eng.step(n, eager=eager)
+        eng.sync()
+        plan = [p["name"] for p in eng.plan_info()]
+        outs.append((eng.stats(n).copy(), eng.arena[:eng.segments["grad"]["offset"]].cpu().numpy().copy(), plan))
+        eng.close()
+    assert "critic.allreduce" in outs[1][2] and "alpha.allreduce" in outs[1][2]
+    assert "critic.allreduce" not in outs[0][2]
+    assert np.array_equal(outs[0][0], outs[1][0])
+    assert np.array_equal(outs[0][1], outs[1][1])       # params, adam_m, adam_v (targets included)

@@ -26,8 +26,9 @@ def _worker(rank, ws, port, q):
     rep.barrier()
     t = rep.max_over_ranks(1.0 + rank)          # each rank's "elapsed"
     total = rep.sum_over_ranks(100.0)           # each rank did 100 updates
+    uid = rep.broadcast_bytes(bytes(range(128)) if rank == 0 else None)   # dp-mode RCCL id hand-off
     rep.close()
-    q.put((rank, seeds, t, total))
+    q.put((rank, seeds, t, total, uid))
 
 
 @pytest.mark.parametrize("ws", [2])
@@ -44,7 +45,8 @@ def test_two_replicas_gloo(ws):
         assert p.exitcode == 0
     out.sort()
     ref = derive_seeds(0, runs=ws)
-    for rank, seeds, t, total in out:
+    for rank, seeds, t, total, uid in out:
+        assert uid == bytes(range(128))
         assert t == float(ws)                   # max over ranks of (1 + rank)
         assert total == 100.0 * ws              # aggregate = sum of per-replica work
         for k, v in seeds.items():
