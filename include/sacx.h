@@ -163,6 +163,19 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
 int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
                  int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
                  float* r_out, float* sp_out, uint8_t* d_out);
+/* Expert diagnostics on the device, n <= 2048 expert rows (device).
+ * flags = 0: model_MSE_on_expert_data and _counterfactual_action (SAC_expert.py:579-608):
+ *   out[0] = mean over the 2 models of mean_i 0.5||model.sample(s_e, a_e) - sp_e||^2,
+ *   out[1] = the same with a = actor.sample(s_e, deterministic=False) (draws n*A normals
+ *   from the device stream), out[2..3] / out[4..5] = per model.
+ * flags & SACX_DIAG_DISC: _calc_disc (:427-460): s_disc_i = ||sp_pred0 - sp_pred1||_2 on
+ *   (s_e, counterfactual a); out[0] = sum, out[1] = max, out[2] = median, out[3 + i] = ratio.
+ * flags & SACX_DIAG_EXPERT_ACTIONS (use_expert_actions): a_e replaces the counterfactual
+ *   action (no draw; out[1] = out[0]).  delta_clip > 0: --delta_clip_pred.  out: device, >= 6
+ *   floats (3 + n with DISC).  The adaptive epsilon of :383-418 is scalar host arithmetic. */
+enum { SACX_DIAG_DISC = 1, SACX_DIAG_EXPERT_ACTIONS = 2 };
+int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const float* sp_e, int32_t n,
+                     int32_t flags, float delta_clip, float* out);
 int sacx_sync(sacx_handle* h);
 
 /* --- data-parallel mode (config C4: one learner over k GPUs) --------------------

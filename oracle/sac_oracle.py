@@ -601,6 +601,61 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
 
 
 # ---------------------------------------------------------------------------
+# expert diagnostics (A17 / F3): SAC_expert.py:579-608 and _calc_disc :427-460
+# ---------------------------------------------------------------------------
+def _model_sample(st, cfg, nrm, k, s, a, delta_clip=0.0):
+    """MSEModel.sample (continuous_models.py:244-254) with _forward(clip=True)."""
+    dt = st.alpha.dtype.type
+    xm = np.concatenate([_norm(s, nrm.s_mean, nrm.s_den), _norm(a, nrm.a_mean, nrm.a_den)], 1)
+    out, _ = mlp_forward(st.models[k], xm, cfg.model_act)
+    dn = out[:, :cfg.S]
+    if delta_clip:
+        dn = np.clip(dn, -_F(dt, delta_clip), _F(dt, delta_clip))
+    return s + (dn * nrm.d_den + nrm.d_mean)
+
+
+def _actor_sample(st, cfg, nrm, s, rs):
+    dt = st.alpha.dtype.type
+    o, _ = mlp_forward(st.actor, _norm(s, nrm.s_mean, nrm.s_den), cfg.act)
+    mu, lraw = split_head(o, st.logstd, cfg)
+    u = f32_noise(rs.normal(size=mu.shape)).astype(dt)
+    return head_sample(mu, lraw, u, cfg.act_limit, dt)[0]
+
+
+def expert_mse_diag(st, cfg, nrm, s_e, a_e, sp_e, rs=None, use_expert_actions=False, delta_clip=0.0):
+    """(model_MSE_on_expert_data, model_MSE_on_expert_counterfactual_action): per model
+    mean_i 0.5 ||model.sample(s_e, a) - sp_e||^2, averaged over the models; a = a_e, then
+    a = actor.sample(s_e, deterministic=False) (one normal(size=(n, A)) draw) unless
+    use_expert_actions."""
+    dt = st.alpha.dtype.type
+    nrm = nrm.cast(dt)
+    s_e, a_e, sp_e = [np.asarray(x, dt) for x in (s_e, a_e, sp_e)]
+
+    def mse(a):
+        per = [np.mean(_F(dt, 0.5) * ((_model_sample(st, cfg, nrm, k, s_e, a, delta_clip) - sp_e) ** 2).sum(-1))
+               for k in range(2)]
+        return float(np.mean(per)), per
+    m_data, per_data = mse(a_e)
+    if use_expert_actions:
+        return m_data, m_data, per_data, per_data
+    m_cf, per_cf = mse(_actor_sample(st, cfg, nrm, s_e, rs))
+    return m_data, m_cf, per_data, per_cf
+
+
+def calc_disc(st, cfg, nrm, s_e, a_e, rs=None, use_expert_actions=False, delta_clip=0.0):
+    """_calc_disc: (disc_ratio, max_disc, median_disc, s_disc_total) of the two models'
+    predictions on (s_e, a) with a = a_e or a fresh actor.sample(s_e) (tf_clip: a no-op)."""
+    dt = st.alpha.dtype.type
+    nrm = nrm.cast(dt)
+    s_e = np.asarray(s_e, dt)
+    a = np.asarray(a_e, dt) if use_expert_actions else _actor_sample(st, cfg, nrm, s_e, rs)
+    diff = _model_sample(st, cfg, nrm, 0, s_e, a, delta_clip) - _model_sample(st, cfg, nrm, 1, s_e, a, delta_clip)
+    s_disc = np.sqrt((diff * diff).sum(axis=1))
+    tot = np.sum(s_disc)
+    return s_disc / tot, float(np.max(s_disc)), float(np.median(s_disc)), float(tot)
+
+
+# ---------------------------------------------------------------------------
 # RNG consumption in the reference's order (SURVEY.md §8a, "RNG consumption
 # order"): the global legacy NumPy stream feeds the sampler and every noise
 # draw; the expert split uses the algorithm's Generator (base_onpolicy_alg.py:109).

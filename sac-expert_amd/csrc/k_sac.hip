@@ -1425,6 +1425,124 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
     hipLaunchKernelGGL(k_obs_norm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, obs, n, S, mean, den, X, ldX);
 }
 
+// ==================================================================== k_diag
+// Expert diagnostics.  mode 0: one wave per row normalises s_e into the actor
+// input and the state columns of the model input, and (a_e != null) a_e into its action
+// columns.  modes 1-3: one workgroup of 1024 threads, n <= 2048 rows.
+#define DIAG_THREADS 1024
+#define DIAG_MAXN 2048
+
+__device__ __forceinline__ float diag_pred(const DiagArgs& g, int k, int i, int j) {
+    float dn = g.O[((int64_t)k * g.n + i) * (g.S + 1) + j];
+    if (g.clip_d > 0.f) dn = fminf(fmaxf(dn, -g.clip_d), g.clip_d);
+    return g.s_e[(int64_t)i * g.S + j] + (dn * g.d_den[j] + g.d_mean[j]);   // MSEModel.sample
+}
+
+__device__ float block_sum_1024(float v, float* sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    float t = 0.f;
+    if (threadIdx.x < 64) t = wave_sum(threadIdx.x < DIAG_THREADS / 64 ? sh[threadIdx.x] : 0.f);
+    if (threadIdx.x == 0) sh[0] = t;
+    __syncthreads();
+    return sh[0];
+}
+
+__global__ __launch_bounds__(256) void k_diag_prep(DiagArgs g) {
+    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int i = blockIdx.x * 4 + wave;
+    if (i >= g.n) return;
+    for (int j = lane; j < g.S; j += 64) {
+        const float xn = (g.s_e[(int64_t)i * g.S + j] - g.s_mean[j]) / g.s_den[j];
+        g.X[(int64_t)i * g.ldS + j] = xn;
+        g.Xm[(int64_t)i * g.ldQ + j] = xn;
+    }
+    if (g.a_e)
+        for (int j = lane; j < g.A; j += 64)
+            g.Xm[(int64_t)i * g.ldQ + g.S + j] = (g.a_e[(int64_t)i * g.A + j] - g.a_mean[j]) / g.a_den[j];
+}
+
+__global__ __launch_bounds__(DIAG_THREADS) void k_diag(DiagArgs g) {
+    __shared__ float sh[DIAG_MAXN];
+    __shared__ float red[DIAG_THREADS / 64];
+    const int n = g.n, S = g.S;
+    if (g.mode == 1 || g.mode == 2) {
+        // per model: mean_i 0.5 sum_j (sp_pred - sp_e)^2; then the mean of the two
+        float m[2];
+        for (int k = 0; k < 2; ++k) {
+            float acc = 0.f;
+            for (int i = threadIdx.x; i < n; i += DIAG_THREADS) {
+                float se = 0.f;
+                for (int j = 0; j < S; ++j) {
+                    const float d = diag_pred(g, k, i, j) - g.sp_e[(int64_t)i * S + j];
+                    se += d * d;
+                }
+                acc += 0.5f * se;
+            }
+            m[k] = block_sum_1024(acc, red) / (float)n;
+        }
+        if (threadIdx.x == 0) {
+            const int o = g.mode == 1 ? 0 : 1;
+            g.out[o] = (m[0] + m[1]) * 0.5f;
+            g.out[2 + 2 * (g.mode - 1)] = m[0];
+            g.out[3 + 2 * (g.mode - 1)] = m[1];
+        }
+        return;
+    }
+    // mode 3: s_disc_i = || sp_pred0 - sp_pred1 ||_2; total, max, median, ratio
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < DIAG_MAXN; i += DIAG_THREADS) {
+        float v = __builtin_inff();
+        if (i < n) {
+            float q = 0.f;
+            for (int j = 0; j < S; ++j) {
+                const float d = diag_pred(g, 0, i, j) - diag_pred(g, 1, i, j);
+                q += d * d;
+            }
+            v = sqrtf(q);
+            acc += v;
+        }
+        sh[i] = v;
+    }
+    const float total = block_sum_1024(acc, red);
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int kk = 2; kk <= n2; kk <<= 1)           // bitonic sort of sh[0, n2) ascending
+        for (int jj = kk >> 1; jj > 0; jj >>= 1) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < n2; i += DIAG_THREADS) {
+                const int l = i ^ jj;
+                if (l > i) {
+                    const float a = sh[i], b = sh[l];
+                    const bool up = (i & kk) == 0;
+                    if ((a > b) == up) { sh[i] = b; sh[l] = a; }
+                }
+            }
+        }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        g.out[0] = total;
+        g.out[1] = sh[n - 1];
+        g.out[2] = (n & 1) ? sh[n / 2] : (sh[n / 2 - 1] + sh[n / 2]) * 0.5f;
+    }
+    for (int i = threadIdx.x; i < n; i += DIAG_THREADS) {
+        float q = 0.f;
+        for (int j = 0; j < S; ++j) {
+            const float d = diag_pred(g, 0, i, j) - diag_pred(g, 1, i, j);
+            q += d * d;
+        }
+        g.out[3 + i] = sqrtf(q) / total;
+    }
+}
+
+void launch_diag(const DiagArgs& a, hipStream_t s) {
+    if (a.mode == 0) hipLaunchKernelGGL(k_diag_prep, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_diag, dim3(1), dim3(DIAG_THREADS), 0, s, a);
+}
+
 // ==================================================================== data-parallel Adam
 // k_adam_apply: element i of a parameter range, gradient = all-reduced sum * (1 / ranks);
 // the arithmetic of the fused GM_DW epilogue, so one rank reproduces it bit for bit.

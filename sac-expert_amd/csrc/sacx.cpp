@@ -1024,6 +1024,7 @@ struct KTimeMap {
     uint64_t* base = nullptr;
     int64_t cap = 0, used = 0;
     std::vector<std::pair<int64_t, int>> spans;
+    std::vector<std::string> names;
 };
 
 int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1,
@@ -1043,6 +1044,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             if (kt->used + 2 * nwg <= kt->cap) {
                 C.gemm.ktime = kt->base + kt->used;
                 kt->spans.push_back({kt->used, nwg});
+                kt->names.push_back(C.name);
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);
@@ -1633,6 +1635,85 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
     return 0;
 }
 
+int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const float* sp_e, int32_t n,
+                     int32_t flags, float delta_clip, float* out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "expert diagnostics need the world models (use_expert)");
+    if (n <= 0 || n > ROLL_CAP / 2) return fail(h, "expert rows must be in [1, 2048]");
+    const bool disc = (flags & SACX_DIAG_DISC) != 0, ea = (flags & SACX_DIAG_EXPERT_ACTIONS) != 0;
+    if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
+    const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    DiagArgs d{};
+    d.n = n; d.S = S; d.A = A; d.ldS = ldS; d.ldQ = ldQ;
+    d.s_e = s_e; d.a_e = a_e; d.sp_e = sp_e; d.O = W("roll.O"); d.X = W("roll.X"); d.Xm = W("roll.Xm");
+    d.s_mean = W("norm.s_mean"); d.s_den = W("norm.s_den"); d.a_mean = W("norm.a_mean"); d.a_den = W("norm.a_den");
+    d.d_mean = W("norm.d_mean"); d.d_den = W("norm.d_den"); d.clip_d = delta_clip; d.out = out;
+    // both models on the same n input rows: model k's rows land at [k n, (k+1) n)
+    auto models = [&]() {
+        std::vector<Launch> pl;
+        std::vector<GemmProb> p0, p1, p2;
+        for (int k = 0; k < 2; ++k) {
+            const std::string mn = "m" + std::to_string(k);
+            float* M1 = W("roll.M1") + (size_t)k * n * Hm0;
+            float* M2 = W("roll.M2") + (size_t)k * n * Hm1;
+            p0.push_back(prob_fwd(W("roll.Xm"), ldQ, n, S + A, W(mn + ".l0"), Hm0, M1, h->mact));
+            p1.push_back(prob_fwd(M1, Hm0, n, Hm0, W(mn + ".l1"), Hm1, M2, h->mact));
+            p2.push_back(prob_fwd(M2, Hm1, n, Hm1, W(mn + ".l2"), O, W("roll.O") + (size_t)k * n * O, ACT_NONE));
+        }
+        add_gemm(h, pl, "diag.m.fwd0", p0, false);
+        add_gemm(h, pl, "diag.m.fwd1", p1, false);
+        add_gemm(h, pl, "diag.m.fwd2", p2, false);
+        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+        h->probs_cursor -= 6;
+    };
+    // actor.sample(s_e, deterministic=False) (continuous_actors.py:270-306) into the action columns
+    auto counterfactual = [&]() {
+        RngArgs r{};
+        r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
+        r.n_int = 0; r.n_norm = n * A; r.out_idx = nullptr; r.out_norm = W("roll.noise");
+        r.slot = -1; r.reset_seq = 0; r.nupd = 1;
+        launch_rng(r, h->stream);
+        std::vector<Launch> pl;
+        add_gemm(h, pl, "diag.a.fwd0", {prob_fwd(W("roll.X"), ldS, n, S, W("actor.l0"), H0, W("roll.H1"), h->act)}, false);
+        add_gemm(h, pl, "diag.a.fwd1", {prob_fwd(W("roll.H1"), H0, n, H0, W("actor.l1"), H1, W("roll.H2"), h->act)}, false);
+        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+        h->probs_cursor -= 2;
+        HeadArgs a{};
+        a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.nseg = 1;
+        a.seg[0] = {0, n, 1, 0, W("roll.noise"), W("roll.Xm"), nullptr, W("roll.A")};
+        a.total_rows = n;
+        a.cache_row0 = 1 << 30;
+        FinalArgs f{};
+        launch_actor_head(a, f, h->stream);
+    };
+    d.mode = 0;
+    d.a_e = (disc && !ea) ? nullptr : a_e;
+    launch_diag(d, h->stream);
+    if (disc) {                      // _calc_disc (SAC_expert.py:427-460)
+        if (!ea) counterfactual();
+        models();
+        d.mode = 3;
+        launch_diag(d, h->stream);
+    } else {                         // SAC_expert.py:579-608
+        models();
+        d.mode = 1;
+        launch_diag(d, h->stream);
+        if (!ea) {
+            counterfactual();
+            models();
+        }
+        d.mode = 2;                  // use_expert_actions: the counterfactual MSE is the data MSE
+        launch_diag(d, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
 int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, double* avg_us, double* us_per_update,
                       int64_t* n_launches) {
     if (!h || !h->bound) return fail(h, "not bound");
@@ -1653,15 +1734,33 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
             rc = fail(h, "timing replay failed");
             break;
         }
-        for (const auto& sp : kt.spans) {
-            uint64_t lo = UINT64_MAX, hi = 0;
+        // diagnostics: SACX_KTIME_DUMP=<file> appends one line per launch of the last replay:
+        // name, span, mean / max workgroup duration, last-start offset, gap to the previous end (us)
+        FILE* dump = nullptr;
+        if (r == n_replays - 1)
+            if (const char* path = std::getenv("SACX_KTIME_DUMP")) dump = std::fopen(path, "a");
+        uint64_t prev_hi = 0;
+        for (size_t si = 0; si < kt.spans.size(); ++si) {
+            const auto& sp = kt.spans[si];
+            uint64_t lo = UINT64_MAX, hi = 0, last_start = 0, wmax = 0;
+            double wsum = 0.0;
             for (int b = 0; b < sp.second; ++b) {
-                lo = std::min(lo, host[sp.first + 2 * b]);
-                hi = std::max(hi, host[sp.first + 2 * b + 1]);
+                const uint64_t t0 = host[sp.first + 2 * b], t1 = host[sp.first + 2 * b + 1];
+                lo = std::min(lo, t0);
+                hi = std::max(hi, t1);
+                last_start = std::max(last_start, t0);
+                wmax = std::max(wmax, t1 - t0);
+                wsum += (double)(t1 - t0);
             }
             sum += (double)(hi - lo) * 0.01;             // 100 MHz ticks -> us
             ++cnt;
+            if (dump)
+                std::fprintf(dump, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f\n", kt.names[si].c_str(), sp.second,
+                             (hi - lo) * 0.01, wsum / sp.second * 0.01, wmax * 0.01, (last_start - lo) * 0.01,
+                             prev_hi ? ((double)lo - (double)prev_hi) * 0.01 : 0.0);
+            prev_hi = hi;
         }
+        if (dump) std::fclose(dump);
     }
     if (g) (void)hipGraphExecDestroy(g);
     (void)hipFree(kt.base);

@@ -310,6 +310,21 @@ struct RollArgs {
     float clip_d, clip_r;       // > 0: clip_by_value(-clip, clip) (delta_clip_pred / reward_clip_pred)
 };
 
+// ---------------------------------------------------------------- expert diagnostics (F3)
+// SAC_expert.py:554-608 (model MSE on expert data / on counterfactual actions) and
+// _calc_disc :427-460 (discrepancy of the two models).  O holds model 0's output on rows
+// [0, n) and model 1's on rows [n, 2n) for the same inputs.
+struct DiagArgs {
+    int32_t mode;               // 0: prep inputs; 1: MSE (expert actions); 2: MSE (counterfactual); 3: disc
+    int32_t n, S, A, ldS, ldQ;
+    const float *s_e, *a_e, *sp_e;
+    const float* O;             // [2n, S+1]
+    float* X; float* Xm;        // actor input [n, ldS]; model input [n, ldQ]
+    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den;
+    float clip_d;
+    float* out;
+};
+
 // launchers (defined in k_sac.hip)
 void launch_gemm(const GemmArgs& a, hipStream_t s);
 void launch_rng(const RngArgs& a, hipStream_t s);
@@ -328,6 +343,7 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
                      hipStream_t s);
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 void launch_roll(const RollArgs& a, hipStream_t s);
+void launch_diag(const DiagArgs& a, hipStream_t s);
 void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s);
 void launch_alpha_apply(const FinalArgs& f, hipStream_t s);
 

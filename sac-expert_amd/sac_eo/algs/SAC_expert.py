@@ -5,9 +5,11 @@
   same Generator and handed to the device (``sacx_perm_push``).
 * ``_update_models`` (``:480-552``): the epoch / minibatch loop with the reference's
   ``np.random.shuffle`` draws (under ``_host_rng``), each minibatch pair fitted on the
-  device (``sacx_model_fit``).  The expert-MSE diagnostics of ``:554-608`` draw the
-  same counterfactual actions (so the stream stays aligned) but their model
-  evaluations are SURVEY F3 (not built this round) and are logged as NaN.
+  device (``sacx_model_fit``).  The expert-MSE diagnostics of ``:579-608`` and the
+  model discrepancy of ``_calc_disc`` (``:427-460``) run on the device
+  (``sacx_expert_diag``), drawing the reference's counterfactual actions from the
+  device stream; the adaptive epsilon of ``_expert_preprocess`` (``:383-418``) is the
+  reference's scalar arithmetic on those results.
 * ``_collect_expert_data`` (``:156-208``): rollouts of the expert actor (its own
   inference-only engine) in ``env_expert``.
 """
@@ -34,13 +36,18 @@ class SAC_exp(SACBase):
         self.expert = expert
         self.expert_normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, init_expert_rms_stats)
         self.use_expert_actions = alg_kwargs.get("use_expert_actions", False)
-        for flag in ("scale_epsilon_by_true_MSE", "scale_max_disc", "scale_median_disc", "scale_total_disc"):
-            if alg_kwargs.get(flag):
-                raise NotImplementedError(f"{flag}: adaptive epsilon is SURVEY F3, not built this round")
+        self.scale_epsilon_by_true_MSE = alg_kwargs.get("scale_epsilon_by_true_MSE", False)
+        self.scale_max_disc = alg_kwargs.get("scale_max_disc", False)
+        self.scale_median_disc = alg_kwargs.get("scale_median_disc", False)
+        self.scale_total_disc = alg_kwargs.get("scale_total_disc", False)
+        self.min_mult = alg_kwargs.get("min_mult", False)
+        self.exp_mult = alg_kwargs.get("exp_mult", False)
+        self.mult_coeff = alg_kwargs.get("mult_coeff", 1.0)
+        self.delta_clip_pred = (mf_update_kwargs or {}).get("delta_clip_pred") or alg_kwargs.get("delta_clip_pred")
         self.model_MSE_on_expert_data = []
         self.model_MSE_on_expert_counterfactual_action = []
         self._expert_engine = None
-        self.s_expert = self.sp_expert = None
+        self.s_expert = self.a_expert = self.sp_expert = None
 
     # ------------------------------------------------------------------ expert
     def _expert_engine_for(self):
@@ -61,25 +68,46 @@ class SAC_exp(SACBase):
     def _collect_expert_data(self):
         t0 = time.time()
         self._expert_engine_for()
-        s_all, sp_all, J_all, cur = [], [], [], 0
+        s_all, a_all, sp_all, J_all, cur = [], [], [], [], 0
         while cur < self.expert_buffer_size:
             horizon = min(self.expert_buffer_size - cur, self.env_horizon)
             s, a, r, sp, d, J = trajectory_sampler(self.env_expert, self.expert, horizon, eval=True,
                                                    deterministic=True)
             s_all.append(s)
+            a_all.append(a)
             sp_all.append(sp)
             cur += len(r)
             if horizon == self.env_horizon:
                 J_all.append(J)
         self.s_expert = np.concatenate(s_all)[-self.expert_buffer_size:]
+        self.a_expert = np.concatenate(a_all)[-self.expert_buffer_size:]
         self.sp_expert = np.concatenate(sp_all)[-self.expert_buffer_size:]
         self.expert_reward = float(np.mean(J_all)) if J_all else float("nan")
         self.logger.log_train({"expert_J_tot": self.expert_reward, "expert_steps": cur,
                                "expert_time": time.time() - t0})
 
+    def _diag(self, disc: bool):
+        return self.engine.expert_diag(self.s_expert, self.a_expert, self.sp_expert, disc=disc,
+                                       use_expert_actions=self.use_expert_actions,
+                                       delta_clip=self.delta_clip_pred or 0.0)
+
     def _expert_preprocess(self):
-        """Default path of :375-424: epsilon_coef = epsilon over the whole expert buffer."""
+        """:375-424: epsilon_coef (adaptive variants on the device diagnostics), then the
+        expert rows (a random batch of them with expert_batch_size)."""
         eps = self.epsilon
+        if self.scale_epsilon_by_true_MSE and self.model_MSE_on_expert_counterfactual_action:
+            eps = 1.0 / (self.epsilon * self.model_MSE_on_expert_counterfactual_action[-1] + 1.0)
+            cur = self.current_reward
+            if cur > 0:
+                if self.min_mult:
+                    eps = eps * (-min(self.mult_coeff * (cur / self.expert_reward) - 1, 0))
+                if self.exp_mult:
+                    eps = eps * np.exp(-self.mult_coeff * cur / self.expert_reward)
+        elif self.scale_max_disc or self.scale_median_disc or self.scale_total_disc:
+            d = self._diag(disc=True)
+            x = d["max_disc"] if self.scale_max_disc else (d["median_disc"] if self.scale_median_disc
+                                                           else d["s_disc_total"])
+            eps = 1.0 / (self.epsilon * x + 1.0)
         s_e, sp_e = self.s_expert, self.sp_expert
         if self.expert_batch_size:
             with self._host_rng():               # get_model_info(batch_size), buffers.py:116-122
@@ -129,12 +157,13 @@ class SAC_exp(SACBase):
             self.engine.model_fit((np.stack(batches) + base).astype(np.int32))
         if self.reset_model_optimizer:
             self.engine.reset_model_optimizer()
-        # diagnostics: draw the counterfactual actions the reference draws (stream alignment)
-        if not self.use_expert_actions:
-            self.actor.sample(self.s_expert, deterministic=False)
-        self.model_MSE_on_expert_data.append(float("nan"))
-        self.model_MSE_on_expert_counterfactual_action.append(float("nan"))
-        self.logger.log_train({"time_model_fit": time.time() - t0, "model_loss_epochs": ep + 1,
+        # model MSE on the expert data and on counterfactual actions (SAC_expert.py:579-608)
+        d = self._diag(disc=False)
+        self.model_MSE_on_expert_data.append(d["mse_expert_data"])
+        self.model_MSE_on_expert_counterfactual_action.append(d["mse_counterfactual"])
+        self.logger.log_train({"model_MSE_on_expert_data": d["mse_expert_data"],
+                               "model_MSE_on_expert_counterfactual_action": d["mse_counterfactual"],
+                               "time_model_fit": time.time() - t0, "model_loss_epochs": ep + 1,
                                "model_updates": num_updates,
                                "model_loss_last": float(self.engine.model_stats(1)[0].sum())})
 

@@ -290,6 +290,26 @@ class Engine:
         self._keep_roll = s0
         return s, a, r, sp, d.bool()
 
+    def expert_diag(self, s_e, a_e, sp_e, disc: bool = False, use_expert_actions: bool = False,
+                    delta_clip: float = 0.0) -> dict:
+        """Expert diagnostics on the device (sacx_expert_diag): the model MSE on expert data and
+        on counterfactual actions (SAC_expert.py:579-608) or, with disc, _calc_disc (:427-460)."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        s0, sp0 = self._dev(s_e, (-1, S)), self._dev(sp_e, (-1, S))
+        n = int(s0.shape[0])
+        a0 = self._dev(a_e, (n, A)) if a_e is not None else None
+        out = torch.zeros(3 + n if disc else 6, dtype=torch.float32, device=self.device)
+        flags = (N.DIAG_DISC if disc else 0) | (N.DIAG_EXPERT_ACTIONS if use_expert_actions else 0)
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
+        N.check(self.lib.sacx_expert_diag(self.h, p(s0), p(a0), p(sp0), n, flags, float(delta_clip or 0.0),
+                                          p(out)), self.h, "expert_diag")
+        o = out.cpu().numpy()
+        if disc:
+            return dict(s_disc_total=float(o[0]), max_disc=float(o[1]), median_disc=float(o[2]),
+                        disc_ratio=o[3:].copy())
+        return dict(mse_expert_data=float(o[0]), mse_counterfactual=float(o[1]),
+                    mse_expert_data_per_model=o[2:4].copy(), mse_counterfactual_per_model=o[4:6].copy())
+
     # ------------------------------------------------------------------ hot path
     def step(self, n: int = 1, num_timesteps: int = 0, ts_increment: int = 1, external: bool = False,
              eager: bool = False):

@@ -313,3 +313,31 @@ def test_dp_single_rank_equals_fused(gpu_available, eager):
     assert "critic.allreduce" not in outs[0][2]
     assert np.array_equal(outs[0][0], outs[1][0])
     assert np.array_equal(outs[0][1], outs[1][1])       # params, adam_m, adam_v (targets included)
+
+
+@pytest.mark.parametrize("use_expert_actions,n", [(False, 20), (True, 7), (False, 1000)])
+def test_expert_diag_matches_oracle(gpu_available, use_expert_actions, n):
+    """Expert diagnostics (SAC_expert.py:579-608, _calc_disc :427-460) vs the oracle; the
+    counterfactual draws advance the device stream exactly like the reference's."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=71, use_expert=True, normalizers="random")
+    S, A = ocfg.S, ocfg.A
+    r = np.random.RandomState(9)
+    s_e = (r.normal(size=(n, S)) * 2).astype(np.float32)
+    a_e = r.uniform(-1, 1, (n, A)).astype(np.float32)
+    sp_e = (s_e + r.normal(size=(n, S)) * 0.1).astype(np.float32)
+    eng.rng_set_state(np.random.RandomState(29).get_state())
+    rs = np.random.RandomState(29)
+    got = eng.expert_diag(s_e, a_e, sp_e, use_expert_actions=use_expert_actions)
+    m_data, m_cf, per_data, per_cf = O.expert_mse_diag(st, ocfg, nrm, s_e, a_e, sp_e, rs, use_expert_actions)
+    assert abs(got["mse_expert_data"] - m_data) <= 1e-4 * abs(m_data)
+    assert abs(got["mse_counterfactual"] - m_cf) <= 1e-4 * abs(m_cf)
+    assert np.max(np.abs(got["mse_counterfactual_per_model"] - per_cf) / np.abs(per_cf)) < 1e-4
+    got_d = eng.expert_diag(s_e, a_e, sp_e, disc=True, use_expert_actions=use_expert_actions)
+    ratio, mx, med, tot = O.calc_disc(st, ocfg, nrm, s_e, a_e, rs, use_expert_actions)
+    assert abs(got_d["s_disc_total"] - tot) <= 1e-4 * tot
+    assert abs(got_d["max_disc"] - mx) <= 1e-4 * mx
+    assert abs(got_d["median_disc"] - med) <= 1e-4 * med
+    assert relerr(got_d["disc_ratio"], ratio) < 1e-4
+    dev, ref = eng.rng_get_state(), rs.get_state()
+    assert np.array_equal(dev[1], ref[1]) and dev[2] == ref[2] and dev[3] == ref[3] and dev[4] == ref[4]
+    eng.close()

@@ -1,0 +1,41 @@
+"""Per-launch workgroup timing of one update-graph replay (diagnostic).
+
+Runs bench.py's engine, replays the timed graph once with SACX_KTIME_DUMP set and prints,
+per k_gemm launch: workgroups, launch span, mean / max workgroup duration, the offset of
+the last workgroup start (dispatch skew) and the gap after the previous k_gemm launch."""
+import os
+import sys
+import tempfile
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "sac-expert_amd"))
+
+
+def main():
+    import bench
+    from sac_eo.common.replicas import init_replica
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "hc"
+    rep = init_replica()
+    eng = bench.build_engine(bench.CONFIGS[cfg], rep.seeds(0), rep.device)
+    eng.step(300)
+    eng.sync()
+    path = os.path.join(tempfile.mkdtemp(), "kt.csv")
+    os.environ["SACX_KTIME_DUMP"] = path
+    eng.time_kernels("k_gemm", 2)
+    rows = [l.strip().split(",") for l in open(path)]
+    G = eng.cfg.graph_steps
+    per = len(rows) // G
+    mid = rows[(G // 2) * per:(G // 2 + 1) * per]      # one update from the middle of the graph
+    print(f"{'launch':34s} {'WGs':>5s} {'span':>6s} {'wg_avg':>6s} {'wg_max':>6s} {'skew':>6s} {'gap':>6s}")
+    for r in mid:
+        print(f"{r[0]:34s} {r[1]:>5s} {r[2]:>6s} {r[3]:>6s} {r[4]:>6s} {r[5]:>6s} {r[6]:>6s}")
+    import numpy as np
+    a = np.array([[float(x) for x in r[2:]] for r in rows])
+    print(f"mean over {len(rows)} launches: span {a[:, 0].mean():.2f} wg_avg {a[:, 1].mean():.2f} "
+          f"wg_max {a[:, 2].mean():.2f} skew {a[:, 3].mean():.2f} gap {a[:, 4].mean():.2f} us")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
