@@ -136,6 +136,20 @@ __device__ __forceinline__ float adam_update(float* p, float* m, float* v, float
     return pn;
 }
 
+// Epilogue stores of the update chain.  Every output is read by the next launch on other
+// XCDs; with SACX_WT_STORES the stores are agent-scope (sc1: written through, the line is
+// dropped from this XCD's L2), so the end-of-kernel release has no dirty lines to write back.
+#ifndef SACX_WT_STORES
+#define SACX_WT_STORES 0
+#endif
+__device__ __forceinline__ void st_out(float* p, float v) {
+#if SACX_WT_STORES
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
+
 // Raw buffer loads.  Out-of-range elements get an offset past the resource's
 // num_records and the hardware returns 0, so every load is unconditional and no
 // select follows it (a select on a load result is turned back into a branch
@@ -215,16 +229,47 @@ __device__ float mean_rows(const float* x, int n) {
     return wave_sum(s) / (float)n;
 }
 
+// Lane-strided partial sums of x[0, n) in increasing i -- the order of mean_rows, so the
+// results are bit-identical -- with the first 4 chunks of 64 (n <= 256) loaded up front by
+// the caller (v0) and the remainder, if any, in further chunks.
+__device__ __forceinline__ float strided_rest(const float* x, int n, const float (&v0)[4]) {
+    const int lane = threadIdx.x & 63;
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) s += v0[u];
+    for (int i = 256 + lane; i < n; i += 64) s += x[i];
+    return s;
+}
+
+__device__ __forceinline__ void strided_head(const float* x, int n, float (&v)[4]) {
+    const int lane = threadIdx.x & 63;
+    const __amdgpu_buffer_rsrc_t r = rs(x);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = bload(r, boff(lane + 64 * u < n, lane + 64 * u));
+}
+
 __device__ void finalize_update(const FinalArgs& f, int nred) {
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x & 63;
-    float s = 0.f;
-    for (int i = lane; i < nred; i += 64) s += f.red[i];
-    const float ent_sum = wave_sum(s);          // sum_i (-nlp_i + H)
+    // every operand of the common case (B <= 256, nred <= 256) is requested before the first
+    // use: one memory round trip instead of one per reduction
+    float vr[4], v1[4], v2[4], vp[4];
+    strided_head(f.red, nred, vr);
+    strided_head(f.lq, f.B, v1);
+    strided_head(f.lq + f.B, f.B, v2);
+    strided_head(f.lp, f.B, vp);
+    float a_old = 0.f, a_m = 0.f, a_v = 0.f;
+    int64_t t_sac = 0, seq0 = 0, nts = 0, tsi = 0;
+    if (lane == 0) {
+        a_old = *f.alpha; a_m = *f.alpha_m; a_v = *f.alpha_v;
+        t_sac = f.ctl->t_sac; seq0 = f.ctl->step_seq;
+        nts = f.ctl->num_timesteps; tsi = f.ctl->ts_increment;
+    }
+    const float ent_sum = wave_sum(strided_rest(f.red, nred, vr));   // sum_i (-nlp_i + H)
     const float m_ent = ent_sum / (float)f.B;   // reduce_mean
-    const float q1 = mean_rows(f.lq, f.B);
-    const float q2 = mean_rows(f.lq + f.B, f.B);
-    float pl = mean_rows(f.lp, f.B);
+    const float q1 = wave_sum(strided_rest(f.lq, f.B, v1)) / (float)f.B;
+    const float q2 = wave_sum(strided_rest(f.lq + f.B, f.B, v2)) / (float)f.B;
+    float pl = wave_sum(strided_rest(f.lp, f.B, vp)) / (float)f.B;
     float mse = 0.f;
     if (f.use_expert && f.ne > 0) {
         const int h = f.ne / 2;
@@ -244,26 +289,32 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
     }
     if (lane == 0) {
         Ctl* ctl = f.ctl;
-        const int64_t tnew = ctl->t_sac + 1;
-        const float alpha_old = *f.alpha;
+        const int64_t tnew = t_sac + 1;
+        const float alpha_old = a_old;
         const float g = -m_ent;                 // d(-alpha*m)/d alpha
         if (f.alpha_g != nullptr) {             // data-parallel: k_alpha_apply finishes after the all-reduce
             *f.alpha_g = g;
-            float* st = f.stats + (size_t)(ctl->step_seq % f.stats_cap) * 8;
+            float* st = f.stats + (size_t)(seq0 % f.stats_cap) * 8;
             st[0] = q1;
             st[1] = q2;
             st[2] = pl;
             st[3] = -alpha_old * m_ent;
             st[5] = mse;
             st[6] = -(m_ent - f.target_entropy);
-            st[7] = (float)ctl->step_seq;
+            st[7] = (float)seq0;
             return;
         }
         const float lr_t = adam_lr(f.adam, GRP_ALPHA, tnew);
-        float an = adam_update(f.alpha, f.alpha_m, f.alpha_v, g, lr_t);
+        // adam_update on the prefetched alpha, m, v (same arithmetic)
+        const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+        const float mm = a_m + (g - a_m) * (1.f - b1);
+        const float vv = a_v + (g * g - a_v) * (1.f - b2);
+        float an = a_old - (mm * lr_t) / (sqrtf(vv) + eps);
+        *f.alpha_m = mm;
+        *f.alpha_v = vv;
         an = fmaxf(an, 1e-5f);                  // SAC_expert.py:348
         *f.alpha = an;
-        const int64_t seq = ctl->step_seq;
+        const int64_t seq = seq0;
         float* st = f.stats + (size_t)(seq % f.stats_cap) * 8;
         st[0] = q1;
         st[1] = q2;
@@ -274,7 +325,7 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
         st[6] = -(m_ent - f.target_entropy);    // mean neglogp (diagnostic)
         st[7] = (float)seq;
         ctl->t_sac = tnew;
-        ctl->num_timesteps += ctl->ts_increment;
+        ctl->num_timesteps = nts + tsi;
         ctl->step_seq = seq + 1;
     }
 }
@@ -372,12 +423,16 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
-    int tile = blockIdx.x;
+    // the folded alpha.final of the previous update is workgroup 0: dispatched first, its
+    // serial reductions overlap the tiles instead of trailing them
+    int tile = (int)blockIdx.x - (ga.has_final ? 1 : 0);
+    if (tile < 0) {
+        finalize_update(ga.fin, ga.fin.nred);
+        return;
+    }
     if (tile >= ga.total_tiles) {
         if constexpr (ROWK > 0) {          // horizontally fused head rows
             qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles);
-        } else if (ga.has_final) {         // the folded alpha.final of the previous update
-            finalize_update(ga.fin, ga.fin.nred);
         }
         return;
     }
@@ -491,7 +546,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                     const int hk = it * 16 + 4 * grp;
 #pragma unroll
                     for (int v = 0; v < 4; ++v)
-                        if (hk + v < H0) g.C0[(size_t)m * H0 + hk + v] = h[v];
+                        if (hk + v < H0) st_out(&g.C0[(size_t)m * H0 + hk + v], h[v]);
                 }
                 // chunks past it1 have w1 = 0: they add exact zeros
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[0], w1v[c][0], acc0, 0, 0, 0);
@@ -542,19 +597,19 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             sq += __shfl_xor(sq, 2, 16);
             sq += __shfl_xor(sq, 1, 16);
             if (!out_ok) return;
-            g.C[(size_t)mm * g.ldc + nn] = (gscale * diff) * e4;
-            if (col == 0) g.part[(size_t)mm * g.tiles_n + tn] = sq;
+            st_out(&g.C[(size_t)mm * g.ldc + nn], (gscale * diff) * e4);
+            if (col == 0) st_out(&g.part[(size_t)mm * g.tiles_n + tn], sq);
             return;
         }
     }
     if (!out_ok) return;
     if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
-        g.C[(size_t)mm * g.ldc + nn] = act_f(v + e0, g.act);
+        st_out(&g.C[(size_t)mm * g.ldc + nn], act_f(v + e0, g.act));
     } else if constexpr (MODE == GM_DX) {
-        g.C[(size_t)mm * g.ldc + nn] = v * dact_f(e0, g.act);
+        st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0, g.act));
     } else {
         if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
-            g.P[pidx + 3 * ga.p_stride] = v * g.grad_scale;
+            st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             return;
         }
         const Ctl* ctl = ga.ctl;
@@ -565,12 +620,12 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         const float mm1 = e1 + (gr - e1) * (1.f - b1);
         const float vv1 = e2 + (gr * gr - e2) * (1.f - b2);
         const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
-        g.P[pidx] = pn;
-        g.P[pidx + ga.p_stride] = mm1;
-        g.P[pidx + 2 * ga.p_stride] = vv1;
+        st_out(&g.P[pidx], pn);
+        st_out(&g.P[pidx + ga.p_stride], mm1);
+        st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
         if (g.T != nullptr) {
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-            if (ctl->num_timesteps % tui == 0) g.T[pidx] = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
+            if (ctl->num_timesteps % tui == 0) st_out(&g.T[pidx], e3 * ga.adam.tau_keep + pn * ga.adam.tau_take);
         }
     }
 }
@@ -988,7 +1043,7 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
 template <int NQ>
-__global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
+__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f) {
     __shared__ float red_s[4];
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
@@ -1064,6 +1119,24 @@ __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
         part = part + red_s[3];
         f.red[blockIdx.x - h.alpha_row0 / 4] = part;
     }
+}
+
+// per-workgroup first / last tick (measurement graphs only), as k_gemm
+__device__ __forceinline__ void ktime_stamp(uint64_t* kt, uint64_t t0) {
+    if (kt != nullptr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            kt[2 * blockIdx.x] = t0;
+            kt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
+template <int NQ>
+__global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    actor_head_body<NQ>(h, f);
+    ktime_stamp(h.ktime, t0);
 }
 
 void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
@@ -1232,7 +1305,7 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 // (SURVEY.md §8a A5), then the Dense(H1 -> Aout) backward with the activation
 // derivative.  Per-column values live in lane j and are broadcast by shuffles.
 template <int NQ, int NQD>
-__global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
+__device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b) {
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = b.B, S = b.S, A = b.A;
@@ -1249,6 +1322,16 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const float ad_pf = bload(rs(b.a_den), boff(jok, lane));
     float h2v[NQ];
     load_row(rs(b.Ha2), row * b.H1, b.H1, h2v);
+    // W3's first 8 output columns (all of them when Aout <= 8) load with the phase-1 operands,
+    // not after the action-gradient reductions: one memory round trip less per row
+    const __amdgpu_buffer_rsrc_t rW3 = rs(b.W3a);
+    float w3n[NQ][8];
+#pragma unroll
+    for (int qq = 0; qq < NQ; ++qq) {
+        const int i = qq * 64 + lane;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w3n[qq][u] = bload(rW3, boff(i < b.H1 && u < b.Aout, i * b.Aout + u));
+    }
     const float w_sac = 1.f - eps;
     const float c = -w_sac * alpha * (1.f / (float)B);
     // action gradient: ga_j = sum over the input rows S+j of W1 of the row's layer-1 delta
@@ -1311,17 +1394,24 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
         else b.E[ci] = dl;
     }
     // Da2[row][i] = (sum_o Da3[row][o] W3a[i][o]) * act'(Ha2[row][i]); columns o live in lanes
-    const __amdgpu_buffer_rsrc_t rW3 = rs(b.W3a);
     float pacc[NQ];
 #pragma unroll
     for (int qq = 0; qq < NQ; ++qq) pacc[qq] = 0.f;
     for (int o0 = 0; o0 < b.Aout; o0 += 8) {
         float w[NQ][8];
+        if (o0 == 0) {
 #pragma unroll
-        for (int qq = 0; qq < NQ; ++qq) {
-            const int i = qq * 64 + lane;
+            for (int qq = 0; qq < NQ; ++qq)
 #pragma unroll
-            for (int u = 0; u < 8; ++u) w[qq][u] = bload(rW3, boff(i < b.H1 && o0 + u < b.Aout, i * b.Aout + o0 + u));
+                for (int u = 0; u < 8; ++u) w[qq][u] = w3n[qq][u];
+        } else {
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) {
+                const int i = qq * 64 + lane;
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    w[qq][u] = bload(rW3, boff(i < b.H1 && o0 + u < b.Aout, i * b.Aout + o0 + u));
+            }
         }
         float d3[8];
 #pragma unroll
@@ -1340,6 +1430,13 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
         const int i = qq * 64 + lane;
         if (i < b.H1) b.Da2[(size_t)row * b.H1 + i] = pacc[qq] * dact_f(h2v[qq], b.act);
     }
+}
+
+template <int NQ, int NQD>
+__global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    actor_bwd_body<NQ, NQD>(b);
+    ktime_stamp(b.ktime, t0);
 }
 
 void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {

@@ -1025,6 +1025,8 @@ struct KTimeMap {
     int64_t cap = 0, used = 0;
     std::vector<std::pair<int64_t, int>> spans;
     std::vector<std::string> names;
+    std::vector<char> is_gemm;
+    bool rows = false;      // also stamp the row kernels (k_actor_head, k_actor_bwd): dump only
 };
 
 int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1,
@@ -1038,13 +1040,20 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         }
     }
     auto emit = [&](const Launch& L, hipStream_t st) {
-        if (kt && L.kind == Launch::GEMM) {
+        const bool timed = kt && (L.kind == Launch::GEMM || (kt->rows && (L.kind == Launch::AHEAD || L.kind == Launch::ABWD)));
+        if (timed) {
             Launch C = L;
-            const int nwg = C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0);
+            const int nwg = L.kind == Launch::GEMM
+                                ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0)
+                                : (L.kind == Launch::AHEAD ? (C.head.total_rows + 3) / 4 : C.grid);
             if (kt->used + 2 * nwg <= kt->cap) {
-                C.gemm.ktime = kt->base + kt->used;
+                uint64_t* p = kt->base + kt->used;
+                if (L.kind == Launch::GEMM) C.gemm.ktime = p;
+                else if (L.kind == Launch::AHEAD) C.head.ktime = p;
+                else C.ab.ktime = p;
                 kt->spans.push_back({kt->used, nwg});
                 kt->names.push_back(C.name);
+                kt->is_gemm.push_back(L.kind == Launch::GEMM);
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);
@@ -1722,6 +1731,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
     const int G = h->graph_steps;
     KTimeMap kt;
     kt.cap = (int64_t)G * 16 * 4096 * 2;               // generous: <= 16 GEMM launches x 4096 WGs per update
+    kt.rows = std::getenv("SACX_KTIME_DUMP") != nullptr;
     HIPCHK(h, hipMalloc(&kt.base, kt.cap * sizeof(uint64_t)));
     hipGraphExec_t g = nullptr;
     int rc = get_graph(h, G, true, &g, -1, &kt);
@@ -1752,8 +1762,10 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
                 wmax = std::max(wmax, t1 - t0);
                 wsum += (double)(t1 - t0);
             }
-            sum += (double)(hi - lo) * 0.01;             // 100 MHz ticks -> us
-            ++cnt;
+            if (kt.is_gemm[si]) {
+                sum += (double)(hi - lo) * 0.01;         // 100 MHz ticks -> us
+                ++cnt;
+            }
             if (dump)
                 std::fprintf(dump, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f\n", kt.names[si].c_str(), sp.second,
                              (hi - lo) * 0.01, wsum / sp.second * 0.01, wmax * 0.01, (last_start - lo) * 0.01,

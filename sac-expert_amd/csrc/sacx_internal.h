@@ -225,6 +225,7 @@ struct HeadArgs {
     // evaluate() of an update; their workgroups write partials of sum(-nlp + H) to fin.red
     int32_t alpha_mode;
     int32_t alpha_row0;
+    uint64_t* ktime;        // measurement only (as GemmArgs::ktime)
 };
 
 // ---------------------------------------------------------------- Q heads
@@ -248,6 +249,7 @@ struct ActorBwdArgs {
     int32_t act;
     float* Da3; float* Da2; float* E;
     const float* gpol;      // [2, B] output gradients of q0, q1 for the policy rows (Dp1 is unscaled)
+    uint64_t* ktime;        // measurement only (as GemmArgs::ktime)
 };
 
 // ---------------------------------------------------------------- finalize (alpha + stats)

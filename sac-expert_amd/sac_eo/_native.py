@@ -9,7 +9,7 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
+LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
 SACX_ABI_VERSION = 1
 ACT = {"relu": 0, "tanh": 1, "elu": 2}

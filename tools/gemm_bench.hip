@@ -51,6 +51,15 @@ int main() {
         double us = tgraph(s, n, [&](int i) { launch_gemm(v.dep ? ((i & 1) ? a1 : a0) : a0, s); });
         printf("%-28s %4d tiles: %.2f us/launch\n", v.name, a0.total_tiles, us);
     }
+    // K sweep at 512x256 (dependent chain): launch cost vs operand bytes read per launch
+    for (int xm : {0, 1})
+        for (int K : {16, 64, 128, 256, 512}) {
+            GemmArgs a0 = fwd(X0, X1, 512, 256, K), a1 = fwd(X1, X0, 512, 256, K);
+            a0.xcd_map = a1.xcd_map = xm;
+            const double mb = 512.0 * 256 * K * 4 * (1.0 / 16 + 1.0 / 16) / 1e6;
+            double us = tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); });
+            printf("sweep xcd=%d 512x256 K=%-4d L2 reads %5.1f MB: %.2f us/launch\n", xm, K, mb, us);
+        }
     // fused two-layer forward (GM_FWD2) vs the two single-layer launches it replaces
     for (int M : {512, 1024}) {
         const int K0 = M == 512 ? 17 : 23, H0 = 256, N = 256;
