@@ -30,3 +30,6 @@ def test_train_entry_point(gpu_available, tmp_path, alg):
     if alg == "sac_imit":
         assert log["train"]["model_updates"][-1] == 2 * 2600 // 50 // 2 or log["train"]["model_updates"][-1] > 0
         assert np.isfinite(log["train"]["model_loss_last"][-1])
+        # expert diagnostics on the device (SAC_expert.py:579-608), no longer NaN placeholders
+        assert np.isfinite(log["train"]["model_MSE_on_expert_data"][-1])
+        assert np.isfinite(log["train"]["model_MSE_on_expert_counterfactual_action"][-1])
