@@ -178,6 +178,11 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
                      int32_t flags, float delta_clip, float* out);
 int sacx_sync(sacx_handle* h);
 
+/* After the caller restored the arena's PARAM / TARGET / STATE segments (a resume
+ * snapshot, sac_eo Engine.load_state): re-reads the host mirrors of the device counters
+ * (update and model-fit sequence numbers that place host-pushed permutations / indices). */
+int sacx_resync(sacx_handle* h);
+
 /* --- data-parallel mode (config C4: one learner over k GPUs) --------------------
  * Not in the reference (its --runs are independent learners, sac_eo/train.py:118-152):
  * each rank samples its local batch from its own buffer and stream; the critic, actor

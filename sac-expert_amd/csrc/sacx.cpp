@@ -1314,6 +1314,16 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     return 0;
 }
 
+int sacx_resync(sacx_handle* h) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    Ctl c{};
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(&c, h->ctl(), sizeof(Ctl), hipMemcpyDeviceToHost));
+    h->seq_host = c.step_seq;
+    h->mfit_host = c.mfit_seq;
+    return 0;
+}
+
 int sacx_dp_unique_id(void* id_out, int32_t cap) {
     if (!id_out || cap < (int32_t)sizeof(ncclUniqueId)) return -1;
     ncclUniqueId id;

@@ -16,6 +16,7 @@ ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1
 STEP_EAGER = 2
+ROLE_WORK, ROLE_PARAM, ROLE_TARGET, ROLE_STATE = 0, 1, 2, 3
 DIAG_DISC = 1
 DIAG_EXPERT_ACTIONS = 2
 STAT_NAMES = ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss", "nlp_mean", "step"]
@@ -26,7 +27,7 @@ EXPORTS = [
     "sacx_buffer_append", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
-    "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag",
+    "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync",
 ]
 
 
@@ -123,6 +124,7 @@ def lib():
         "sacx_actor_act": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sacx_time_kernels": (ctypes.c_int, [vp, ctypes.c_char_p, i32, P(f64), P(f64), P(i64)]),
         "sacx_dp_unique_id": (ctypes.c_int, [vp, i32]),
+        "sacx_resync": (ctypes.c_int, [vp]),
         "sacx_expert_diag": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, f32, vp]),
         "sacx_dp_init": (ctypes.c_int, [vp, vp, i32, i32]),
         "sacx_rollout": (ctypes.c_int, [vp, i32, vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp]),

@@ -7,6 +7,7 @@ update arithmetic runs in the hand-written gfx950 kernels behind the C ABI.
 from __future__ import annotations
 
 import ctypes
+import os
 import dataclasses
 import math
 from typing import Dict, List, Optional, Sequence
@@ -309,6 +310,55 @@ class Engine:
                         disc_ratio=o[3:].copy())
         return dict(mse_expert_data=float(o[0]), mse_counterfactual=float(o[1]),
                     mse_expert_data_per_model=o[2:4].copy(), mse_counterfactual_per_model=o[4:6].copy())
+
+    # ------------------------------------------------------------------ snapshot (F4)
+    def _state_ranges(self):
+        """Merged byte ranges of every PARAM / TARGET / STATE segment (aliases fold in)."""
+        iv = sorted((d["offset"], d["offset"] + int(self.v[n].numel() * self.v[n].element_size()))
+                    for n, d in self.segments.items() if d["role"] != N.ROLE_WORK)
+        out = []
+        for a, b in iv:
+            if out and a <= out[-1][1]:
+                out[-1][1] = max(out[-1][1], b)
+            else:
+                out.append([a, b])
+        return out
+
+    def _layout_sig(self):
+        return [[n, d["offset"], d["rows"], d["cols"], d["role"]] for n, d in sorted(self.segments.items())]
+
+    def save_state(self, path: str):
+        """Full-state snapshot (the reference keeps only final weights and logs,
+        base_onpolicy_alg.py:351-374): weights, targets, alpha, Adam moments, normalisers,
+        counters, the device RNG stream, replay ring, expert rows, permutation and stats
+        rings -- every non-workspace segment, byte for byte.  Resuming continues the run
+        bit-identically (tests/test_gpu_engine.py)."""
+        import json
+        os.makedirs(path, exist_ok=True)
+        self.sync()
+        ranges = self._state_ranges()
+        for a, b in ranges:
+            np.save(os.path.join(path, f"range_{a}.npy"), self.arena[a:b].cpu().numpy())
+        with open(os.path.join(path, "meta.json"), "w") as fh:
+            json.dump({"arena_bytes": self.nbytes, "ranges": ranges, "layout": self._layout_sig(),
+                       "format": "sacx-state-1"}, fh)
+
+    def load_state(self, path: str):
+        """Restores a save_state snapshot into this engine (same configuration)."""
+        import json
+        with open(os.path.join(path, "meta.json")) as fh:
+            meta = json.load(fh)
+        if meta.get("format") != "sacx-state-1" or meta["arena_bytes"] != self.nbytes or \
+                meta["layout"] != self._layout_sig():
+            raise ValueError("snapshot layout does not match this engine's configuration")
+        self.sync()
+        for a, b in meta["ranges"]:
+            src = np.load(os.path.join(path, f"range_{a}.npy"))
+            if src.shape != (b - a,):
+                raise ValueError("snapshot range size mismatch")
+            self.arena[a:b].copy_(torch.from_numpy(src).to(self.device))
+        self.sync()
+        N.check(self.lib.sacx_resync(self.h), self.h, "resync")
 
     # ------------------------------------------------------------------ hot path
     def step(self, n: int = 1, num_timesteps: int = 0, ts_increment: int = 1, external: bool = False,

@@ -341,3 +341,33 @@ def test_expert_diag_matches_oracle(gpu_available, use_expert_actions, n):
     dev, ref = eng.rng_get_state(), rs.get_state()
     assert np.array_equal(dev[1], ref[1]) and dev[2] == ref[2] and dev[3] == ref[3] and dev[4] == ref[4]
     eng.close()
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_snapshot_resume_bit_identical(gpu_available, tmp_path, use_expert):
+    """Full-state snapshot (F4): 11 updates, save, 13 more; a fresh engine loading the
+    snapshot runs the same 13 updates bit-identically (weights, Adam, RNG stream, counters,
+    replay ring, permutation ring, stats)."""
+    def fresh():
+        eng, *_ = make_pair(act="tanh", B=64, seed=81, use_expert=use_expert)
+        return eng
+    eng = fresh()
+    eng.rng_set_state(np.random.RandomState(4).get_state())
+    if use_expert:
+        rs = np.random.RandomState(2)
+        eng.push_perms(np.stack([rs.permutation(eng.cfg.expert_batch) for _ in range(24)]))
+    eng.step(11)
+    eng.save_state(str(tmp_path / "snap"))
+    eng.step(13)
+    eng.sync()
+    ref = (eng.stats(13).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state())
+    eng.close()
+    eng2 = fresh()
+    eng2.load_state(str(tmp_path / "snap"))
+    eng2.step(13)
+    eng2.sync()
+    got = (eng2.stats(13).copy(), eng2.v["params"].cpu().numpy().copy(), eng2.rng_get_state())
+    assert np.array_equal(ref[0], got[0]) and np.array_equal(ref[1], got[1])
+    assert np.array_equal(ref[2][1], got[2][1]) and ref[2][2] == got[2][2]
+    assert eng2.ctl()["step_seq"] == 24
+    eng2.close()
