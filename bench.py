@@ -35,9 +35,17 @@ CONFIGS = {
     # configs[2]-shaped (SAC-EO expert term; model fitting is a separate call)
     "humanoid_eo": dict(workload="Humanoid-v3-shaped synthetic buffer, SAC-EO update incl. world-model expert term, fp32",
                         S=376, A=17, B=1024, hidden=(256, 256), buffer=1_000_000, use_expert=True),
+    # configs[4] per replica: bf16 MFMA operands with fp32 accumulate, 4e6-row buffer in HBM
+    "humanoid_bf16": dict(workload="Humanoid-v3-shaped synthetic 4e6-row buffer, SAC update, bf16 MFMA operands / "
+                                   "fp32 accumulate and master weights",
+                          S=376, A=17, B=1024, hidden=(256, 256), buffer=4_000_000, use_expert=False, bf16=True),
+    # the same shapes in fp32 (the comparison point for humanoid_bf16)
+    "humanoid_sac": dict(workload="Humanoid-v3-shaped synthetic 4e6-row buffer, SAC update, fp32",
+                         S=376, A=17, B=1024, hidden=(256, 256), buffer=4_000_000, use_expert=False),
 }
 
 FP32_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 matrix (= vector) peak, dense
+BF16_PEAK_TFLOPS = 2500.0    # dense BF16 MFMA (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -52,7 +60,8 @@ def build_engine(cfgd, seeds, device, dp=None, batch=None, weight_seed=None):
     B = batch or cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
-                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "128")))
+                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "128")),
+                        gemm_bf16=bool(cfgd.get("bf16", False)))
     eng = Engine(ecfg, device=device, dp=dp)
     rng = np.random.default_rng(weight_seed if weight_seed is not None else seeds["setup"])
     eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
@@ -112,6 +121,7 @@ def roofline(eng, config, n_prof=20, n_replays=20):
     the timed region (these replays are real updates).  Cross-checks kept in the line:
     the graph time with and without the family (sacx_time_graph) and the eager
     per-stage event times (each includes ~4 us of event overhead)."""
+    peak = BF16_PEAK_TFLOPS if CONFIGS[config].get("bf16") else FP32_PEAK_TFLOPS
     info = eng.plan_info()
     ms = eng.profile(n_prof)
     fam = {}
@@ -133,8 +143,8 @@ def roofline(eng, config, n_prof=20, n_replays=20):
     t_full = eng.time_graph(n_replays)
     t_wo = eng.time_graph(n_replays, dom)
     out = {
-        "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": FP32_PEAK_TFLOPS,
-        "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 5),
+        "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
+        "unit": "TFLOP/s", "frac": round(achieved / peak, 5),
         "traffic": traffic, "traffic_source": src,
         "avg_launch_us": round(avg_us, 3), "launches_per_update": round(launches, 3),
         "flops_per_launch": flops_per_launch,
@@ -273,10 +283,12 @@ def main():
     if rank == 0:
         line = {
             "metric": "SAC gradient-steps/sec (batch=256, 256x2 MLP)" if args.config == "hc"
-            else "SAC-EO gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)",
+            else ("SAC-EO gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)" if cfgd["use_expert"]
+                  else "SAC gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)"),
             "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
-            "scaling": "strong" if dp else "weak", "vs_baseline": None, "dtype": "f32",
+            "scaling": "strong" if dp else "weak", "vs_baseline": None,
+            "dtype": "bf16 (MFMA operands), f32 accumulate" if cfgd.get("bf16") else "f32",
             "data": "synthetic (HalfCheetah-shaped replay rows generated on device; random orthogonal init)",
             "config": {"workload": cfgd["workload"], "obs_dim": cfgd["S"], "act_dim": cfgd["A"],
                        "batch": cfgd["B"], "hidden": list(cfgd["hidden"]), "buffer_rows": cfgd["buffer"],

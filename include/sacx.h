@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 1
+#define SACX_ABI_VERSION 2
 
 typedef struct sacx_handle sacx_handle;
 
@@ -69,6 +69,8 @@ typedef struct sacx_config {
     float act_limit;            /* action_space.high (continuous_actors.py:252) */
     float epsilon;              /* --epsilon (expert weight) */
     float reward_loss_coef;     /* --reward_loss_coef */
+    int32_t gemm_bf16;          /* 1: the MLP GEMMs take bf16 operands (rounded on load) with fp32
+                                   accumulation, fp32 master weights / Adam (config C5); 0: fp32 */
 } sacx_config;
 
 typedef struct sacx_segment {

@@ -26,6 +26,10 @@
 namespace sacx {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
+
+// fp32 -> bf16 bits, round to nearest even (v_cvt_pk_bf16_f32 on gfx950)
+__device__ __forceinline__ short bf16_bits(float x) { return __builtin_bit_cast(short, (__bf16)x); }
 
 #define LOG2PI_F 0x1.d67f1ep+0f     // f32 log(f32(2*pi))  (continuous_actors.py:360)
 #define LN2_F 0x1.62e430p-1f        // f32(np.log(2.))     (continuous_actors.py:366)
@@ -418,7 +422,7 @@ __device__ __forceinline__ int xcd_tile(int b, int T) {
     return x * q + (x < r ? x : r) + j;
 }
 
-template <int MODE, int VEC, int ROWK, int NQ>
+template <int MODE, int VEC, int ROWK, int NQ, bool BF = false>
 __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
@@ -569,6 +573,15 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+            if constexpr (BF) {
+                // lane (r, grp) holds k = 4 grp + 0..3 of this 16-wide k slab: exactly the
+                // A / B operand of one v_mfma_f32_16x16x16_bf16
+                const shortx4 av = {bf16_bits(a[u][0]), bf16_bits(a[u][1]), bf16_bits(a[u][2]), bf16_bits(a[u][3])};
+                const shortx4 bv = {bf16_bits(b[u][0]), bf16_bits(b[u][1]), bf16_bits(b[u][2]), bf16_bits(b[u][3])};
+                if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc1, 0, 0, 0);
+                else acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc0, 0, 0, 0);
+                continue;
+            }
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1], b[u][1], acc1, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);
@@ -632,10 +645,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 
 // ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
 // (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
-template <int MODE, int VEC, int ROWK = 0, int NQ = 4>
+template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    gemm_core<MODE, VEC, ROWK, NQ>(ga);
+    gemm_core<MODE, VEC, ROWK, NQ, BF>(ga);
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -649,13 +662,22 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
     const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0)), block(256);
     switch (a.mode) {
     case GM_FWD:
-        if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_gemm<GM_FWD, 0>), grid, block, 0, s, a);
+        if (a.bf16) {
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true>), grid, block, 0, s, a);
+        } else {
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0>), grid, block, 0, s, a);
+        }
         break;
     case GM_DX: {
         const dim3 gx(a.total_tiles + (a.rowk ? a.row_blocks : 0));
         const bool q8 = a.rowk && a.qh.H1 > 256;
-#define SACX_DX(V, R, Q) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q>), gx, block, 0, s, a)
+#define SACX_DX(V, R, Q)                                                                            \
+    do {                                                                                           \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true>), gx, block, 0, s, a);          \
+        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q>), gx, block, 0, s, a);                      \
+    } while (0)
         if (a.rowk == 1) {
             if (a.vec) { if (q8) SACX_DX(1, 1, 8); else SACX_DX(1, 1, 4); }
             else { if (q8) SACX_DX(0, 1, 8); else SACX_DX(0, 1, 4); }
@@ -682,7 +704,8 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         }
         break;
     default:
-        hipLaunchKernelGGL((k_gemm<GM_DW, 0>), grid, block, 0, s, a);
+        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true>), grid, block, 0, s, a);
+        else hipLaunchKernelGGL((k_gemm<GM_DW, 0>), grid, block, 0, s, a);
     }
 }
 

@@ -421,6 +421,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     L.gemm.nprob = (int)ps.size();
     L.gemm.total_tiles = tiles;
     L.gemm.xcd_map = h->xcd_map;
+    L.gemm.bf16 = h->cfg.gemm_bf16 != 0 && mode != GM_FWD2;   // the fused forward stays fp32
     L.gemm.p_stride = h->p_stride;
     L.gemm.ctl = h->ctl();
     L.gemm.adam.lr[GRP_Q] = h->cfg.lr_q;

@@ -151,6 +151,7 @@ struct GemmArgs {
                            // GM_FWD2: layer-0 K steps of 4, rounded up to even (2..16)
     int32_t total_tiles;
     int32_t xcd_map;       // 1: each XCD takes a contiguous tile range (see xcd_tile)
+    int32_t bf16;          // 1: bf16 MFMA operands (rounded on load), fp32 accumulate (config C5)
     int64_t p_stride;      // floats between params / adam_m / adam_v blocks
     const Ctl* ctl;
     AdamConsts adam;

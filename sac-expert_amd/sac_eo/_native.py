@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 1
+SACX_ABI_VERSION = 2
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1
@@ -62,6 +62,7 @@ class Config(ctypes.Structure):
         ("act_limit", ctypes.c_float),
         ("epsilon", ctypes.c_float),
         ("reward_loss_coef", ctypes.c_float),
+        ("gemm_bf16", ctypes.c_int32),
     ]
 
 

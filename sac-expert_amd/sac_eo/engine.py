@@ -55,6 +55,7 @@ class EngineConfig:
     act_limit: float = 1.0
     epsilon: float = 1e-3
     reward_loss_coef: float = 1.0
+    gemm_bf16: bool = False     # config C5: bf16 MFMA operands, fp32 accumulate / master weights
 
     def to_c(self) -> N.Config:
         c = N.Config()
@@ -82,6 +83,7 @@ class EngineConfig:
         c.act_limit = self.act_limit
         c.epsilon = self.epsilon
         c.reward_loss_coef = self.reward_loss_coef
+        c.gemm_bf16 = int(bool(self.gemm_bf16))
         return c
 
 

@@ -30,7 +30,7 @@ def nontrivial_normalizers(rs, S, A):
 
 def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
               use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
-              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None):
+              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False):
     """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
     from sac_eo.engine import Engine, EngineConfig
     ocfg = O.Config(S=S, A=A, hidden=hidden, act=act, B=B, per_state_std=per_state_std,
@@ -42,7 +42,8 @@ def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, p
     nrm = O.Normalizers.identity(S, A) if normalizers == "identity" else nontrivial_normalizers(rs, S, A)
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
                         per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
-                        expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon)
+                        expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon,
+                        gemm_bf16=gemm_bf16)
     eng = Engine(ecfg, dp=dp)
     eng.set_net("actor", st.actor)
     eng.set_logstd(st.logstd)

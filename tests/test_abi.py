@@ -31,6 +31,7 @@ def test_struct_layouts():
     assert N.Config.buffer_capacity.offset == 32
     assert ctypes.sizeof(N.Config) == 136          # gcc: sizeof(sacx_config)
     assert N.Config.reward_loss_coef.offset == 128
+    assert N.Config.gemm_bf16.offset == 132
     assert ctypes.sizeof(N.Segment) == 48 + 8 + 8 + 8 + 4 + 4
     assert ctypes.sizeof(N.LaunchInfo) == 32 + 32 + 4 + 4 + 8 + 8
 

@@ -371,3 +371,48 @@ def test_snapshot_resume_bit_identical(gpu_available, tmp_path, use_expert):
     assert np.array_equal(ref[2][1], got[2][1]) and ref[2][2] == got[2][2]
     assert eng2.ctl()["step_seq"] == 24
     eng2.close()
+
+
+BF16_QLOSS_TOL = 5e-3     # config C5: bf16 operands (8-bit mantissa), fp32 accumulate; measured 1.3e-3
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_bf16_qloss_trajectory(gpu_available, use_expert):
+    """Config C5 (bf16 MFMA MLP path, fp32 accumulate and master weights): the Q-loss
+    trajectory over 100 updates against the fp64 oracle within BF16_QLOSS_TOL relative
+    (the fp32 path's bar is 1e-4; bf16 rounds every GEMM operand to 8 mantissa bits), and
+    the sampler stream still bit-exact."""
+    B = 256
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=11, use_expert=use_expert, done_p=0.01,
+                                                gemm_bf16=True)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(123)
+    gen = np.random.default_rng(77)
+    eng.rng_set_state(rs.get_state())
+    steps = 100
+    Rs = [O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=20 if use_expert else 0, gen=gen) for _ in range(steps)]
+    if use_expert:
+        eng.push_perms(np.stack([R["perm"] for R in Rs]))
+    eng.step(steps)
+    eng.sync()
+    dev = eng.stats(steps)
+    ref = np.array([[o["q1_loss"], o["q2_loss"]] for o in (oracle_step(st, ocfg, nrm, buf, R, expert) for R in Rs)])
+    rel = np.abs(dev[:, :2] - ref) / np.abs(ref)
+    print("bf16 q-loss max rel err", rel.max(), "median", np.median(rel))
+    assert rel.max() < BF16_QLOSS_TOL, rel.max()
+    assert np.all(np.isfinite(dev))
+    got, exp = eng.rng_get_state(), rs.get_state()
+    assert np.array_equal(got[1], exp[1]) and got[2] == exp[2]
+    eng.close()
+
+
+def test_bf16_graph_equals_eager(gpu_available):
+    outs = []
+    for eager in (True, False):
+        eng, *_ = make_pair(act="tanh", B=128, seed=21, gemm_bf16=True)
+        eng.rng_set_state(np.random.RandomState(5).get_state())
+        eng.step(19, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy()))
+        eng.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
