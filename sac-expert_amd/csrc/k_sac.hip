@@ -412,6 +412,8 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
 __device__ void qhead_block(const QHeadArgs& q, int block);
+template <int NQ>
+__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block);
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
 // so blocks b and b+8 share an L2.  xcd_tile gives the blocks of one XCD a contiguous range of
@@ -420,6 +422,95 @@ __device__ void qhead_block(const QHeadArgs& q, int block);
 __device__ __forceinline__ int xcd_tile(int b, int T) {
     const int x = b & 7, j = b >> 3, q = T >> 3, r = T & 7;
     return x * q + (x < r ? x : r) + j;
+}
+
+// actor.head folded into the target tiles of q.fwd0 (GM_FWD, rowk = 3, problem headp): the
+// tile's 16 target rows get evaluate() (continuous_actors.py:327-379) from the actor's
+// layer-2 output -- mu / logstd rows = Ha2[m0.., :] W3 (a 16 x Aout MFMA tile, K = H1 split
+// over the 4 waves) -- and the A tile [state columns of A | normalised actions] is staged in
+// LDS for the main loop.  Column tile 0 stores the rows' neglogp for q.head.  The same
+// arithmetic as k_actor_head, with the 16-lane row sums of the MFMA layout.
+__device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb& g, int m0, int tn,
+                                              float (&As)[16][68], float (&red)[4][4][64]) {
+    const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 15, grp = lane >> 4;
+    const int row = t >> 4, col = t & 15;
+    const int A = hd.A, Aout = hd.Aout, H1 = hd.H1, S = g.K - A;
+    const HeadSeg& sg = hd.seg[0];
+    const bool rok = m0 + row < g.M;
+    // everything the prologue reads is requested first
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.A, 0x7fffffffu);
+    float xs[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) xs[q] = bload(rx, boff(rok && col + 16 * q < S, (m0 + row) * g.lda + col + 16 * q));
+    const bool jok = col < A;
+    const float u = bload(rs(sg.noise), boff(jok && rok, (m0 + row - sg.r0) * A + col));
+    const float ls = bload(rs(hd.logstd), boff(jok && !hd.per_state_std, col));
+    const float am = bload(rs(hd.a_mean), boff(jok, col));
+    const float ad = bload(rs(hd.a_den), boff(jok, col));
+    const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(hd.W3, 0x7fffffffu);
+    const float bias = bload(rw3, boff(col < Aout, H1 * Aout + col));
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(hd.H2, 0x7fffffffu);
+    const int nIt = H1 >> 4, per = (nIt + 3) >> 2, i0 = wave * per, i1 = min(nIt, i0 + per);
+    const bool hm = m0 + r < g.M, wn = r < Aout;
+    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+    for (int it = i0; it < i1; it += 4) {
+        float a[4][4], b[4][4];
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) {
+            const bool ok = it + u4 < i1;
+            const int k0 = (it + u4) * 16 + grp * 4;
+            const float4 v = bload4(rh, boff(ok && hm, (m0 + r) * hd.ldh + k0));
+            a[u4][0] = v.x; a[u4][1] = v.y; a[u4][2] = v.z; a[u4][3] = v.w;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[u4][j] = bload(rw3, boff(ok && wn, (k0 + j) * Aout + r));
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u4 = 0; u4 < 4; ++u4) {
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][0], b[u4][0], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][1], b[u4][1], c1, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][2], b[u4][2], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][3], b[u4][3], c1, 0, 0, 0);
+        }
+    }
+    const floatx4 acc = c0 + c1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) red[wave][q][lane] = acc[q];
+    __syncthreads();
+    const int L = ((row >> 2) << 4) | col, R = row & 3;
+    float v = red[0][R][L] + red[1][R][L];
+    v = v + red[2][R][L];
+    v = v + red[3][R][L];
+    const float mu = v + bias;
+    // per_state_std: logstd_raw of action j sits in column A + j of the same row (same 16 lanes)
+    const float lv = __shfl(mu, (lane & ~15) | min(col + A, 15), 64);
+    const float lraw = hd.per_state_std ? lv : ls;
+    float nv = 0.f, nc = 0.f, pin = 0.f;
+    if (jok) {
+        const float l = fminf(fmaxf(lraw, -5.f), 2.f);
+        const float sd = expf(l);
+        const float x = mu + sd * u;
+        const float th = tanhf(x);
+        const float pi = hd.lim * th;
+        const float z = (x - mu) / expf(l);
+        nv = z * z + 2.f * l + LOG2PI_F;
+        nc = 2.f * ((LN2_F - x) - softplus_f(-2.f * x));
+        pin = (pi - am) / ad;
+    }
+    nv += __shfl_xor(nv, 8, 16);
+    nv += __shfl_xor(nv, 4, 16);
+    nv += __shfl_xor(nv, 2, 16);
+    nv += __shfl_xor(nv, 1, 16);
+    nc += __shfl_xor(nc, 8, 16);
+    nc += __shfl_xor(nc, 4, 16);
+    nc += __shfl_xor(nc, 2, 16);
+    nc += __shfl_xor(nc, 1, 16);
+    if (tn == 0 && col == 0 && rok && sg.nlp_out != nullptr) sg.nlp_out[m0 + row - sg.r0] = 0.5f * nv + nc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (col + 16 * q < S) As[row][col + 16 * q] = xs[q];
+    if (jok) As[row][S + col] = pin;
+    __syncthreads();
 }
 
 template <int MODE, int VEC, int ROWK, int NQ, bool BF = false>
@@ -435,7 +526,9 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         return;
     }
     if (tile >= ga.total_tiles) {
-        if constexpr (ROWK > 0) {          // horizontally fused head rows
+        if constexpr (ROWK == 3) {         // actor.head rows beside the target tiles
+            actor_head_body<NQ>(ga.head, ga.hfin, ga.head_block0 + tile - ga.total_tiles);
+        } else if constexpr (ROWK > 0) {   // horizontally fused Q-head rows
             qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles);
         }
         return;
@@ -492,6 +585,34 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     const __amdgpu_buffer_rsrc_t rw = rs(g.wgen);
     floatx4 acc0 = {0.f, 0.f, 0.f, 0.f};
     floatx4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    __shared__ float As[16][68];
+    bool a_lds = false;
+    if constexpr (MODE == GM_FWD && ROWK == 3) {
+        if (g.headp) {
+            // K <= 64: at most one 16-wide k slab per wave.  Its B operand is requested before
+            // the prologue, so the tile pays one memory round trip, not two.
+            float bp[4];
+            const int k0 = it0 * 16 + grp * 4;
+            load_b<BKC, false, false>(rb, g, n, nok, it0 < it1 ? k0 : (1 << 30), bp);
+            head_prologue(ga.head, g, m0, tn, As, red);
+            if (it0 < it1) {
+                float a[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a[j] = (k0 + j < g.K) ? As[r][k0 + j] : 0.f;
+                if constexpr (BF) {
+                    const shortx4 av = {bf16_bits(a[0]), bf16_bits(a[1]), bf16_bits(a[2]), bf16_bits(a[3])};
+                    const shortx4 bv = {bf16_bits(bp[0]), bf16_bits(bp[1]), bf16_bits(bp[2]), bf16_bits(bp[3])};
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc0, 0, 0, 0);
+                } else {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bp[0], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bp[1], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], bp[2], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], bp[3], acc1, 0, 0, 0);
+                }
+            }
+            a_lds = true;
+        }
+    }
     if constexpr (MODE == GM_FWD2) {
         // layer 0 per 16-wide hidden chunk hb: D' = W0^T[hb.., :] X^T[:, m0..] leaves lane
         // (r, grp) holding H1[m0+r][hb+4grp+v] in register v -- exactly the A operand of the
@@ -560,7 +681,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             }
         }
     }
-    for (int it = it0; MODE != GM_FWD2 && it < it1; it += 4) {
+    for (int it = it0; MODE != GM_FWD2 && !a_lds && it < it1; it += 4) {
         float a[4][4], b[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -658,11 +779,37 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     }
 }
 
+// q.fwd0 with the actor head folded in: 1,024 tiles + 128 head-row workgroups must be
+// resident at once (5 workgroups per CU), so registers are capped at 96 per lane
+template <int VEC, int NQ, bool BF>
+__global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    gemm_core<GM_FWD, VEC, 3, NQ, BF>(ga);
+    if (ga.ktime != nullptr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            ga.ktime[2 * blockIdx.x] = t0;
+            ga.ktime[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
     const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0)), block(256);
     switch (a.mode) {
     case GM_FWD:
-        if (a.bf16) {
+        if (a.rowk == 3) {                 // q.fwd0 with the actor head folded in
+            const dim3 gh(a.total_tiles + (a.has_final ? 1 : 0) + a.row_blocks);
+            const bool h8 = a.head.H1 > 256;
+#define SACX_FH(V, Q)                                                                               \
+    do {                                                                                           \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm_head<V, Q, true>), gh, block, 0, s, a);              \
+        else hipLaunchKernelGGL((k_gemm_head<V, Q, false>), gh, block, 0, s, a);                   \
+    } while (0)
+            if (a.vec) { if (h8) SACX_FH(1, 8); else SACX_FH(1, 4); }
+            else { if (h8) SACX_FH(0, 8); else SACX_FH(0, 4); }
+#undef SACX_FH
+        } else if (a.bf16) {
             if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true>), grid, block, 0, s, a);
         } else {
@@ -1066,10 +1213,10 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
 template <int NQ>
-__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f) {
+__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block) {
     __shared__ float red_s[4];
     const int wave = wave_id(), lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + wave;
+    const int row = block * 4 + wave;
     float row_ent = 0.f;
     int sidx = 0;
     for (int i = 1; i < h.nseg; ++i)
@@ -1132,7 +1279,7 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
             row_ent = -nlp + f.target_entropy;
         }
     }
-    if (!h.alpha_mode || (int)blockIdx.x * 4 < h.alpha_row0) return;
+    if (!h.alpha_mode || block * 4 < h.alpha_row0) return;
     // ---- alpha: block partial of sum(-nlp + H); k_alpha_final reduces them
     if (lane == 0) red_s[wave] = row_ent;
     __syncthreads();
@@ -1140,7 +1287,7 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         float part = red_s[0] + red_s[1];
         part = part + red_s[2];
         part = part + red_s[3];
-        f.red[blockIdx.x - h.alpha_row0 / 4] = part;
+        f.red[block - h.alpha_row0 / 4] = part;
     }
 }
 
@@ -1158,7 +1305,7 @@ __device__ __forceinline__ void ktime_stamp(uint64_t* kt, uint64_t t0) {
 template <int NQ>
 __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    actor_head_body<NQ>(h, f);
+    actor_head_body<NQ>(h, f, (int)blockIdx.x);
     ktime_stamp(h.ktime, t0);
 }
 

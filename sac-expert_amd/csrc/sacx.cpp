@@ -71,6 +71,7 @@ struct Launch {
     int gemm_first = 0;  // index of the first problem in the host table (GEMM)
     bool after_final = false;  // graph: waits for the previous update's alpha branch
     bool alpha_branch = false; // graph: runs on the side stream beside the next update's first launches
+    bool frees_slot = false;   // graph: the launch that carries the folded alpha rows (last reader of a slot)
 };
 
 const char* kernel_family(Launch::Kind k) {
@@ -578,11 +579,32 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     const int alpha_tiles = ((B + 15) / 16) * ((H1 + 15) / 16);
     const bool actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
              {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a, -1, alpha_tiles);
+    // actor.head folded into q.fwd0 (plain SAC): the target tiles compute their rows' actions
+    // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
+    // workgroups of the same launch.  SACX_FUSE_HEAD=0 keeps the separate launch.
+    const char* fh = std::getenv("SACX_FUSE_HEAD");
+    const bool fuse_head = !eo && Aout <= 16 && S + A <= 64 && H1 % 16 == 0 && H1 <= 512 &&
+                           !(fh && std::atoi(fh) == 0);
+    HeadArgs head_fused{};
     // ---- actor head
-    {
+    if (fuse_head) {
+        HeadArgs& a = head_fused;
+        a.H2 = Ha2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.nseg = 2;
+        a.seg[0] = {0, B, 0, 0, noise_t, nullptr, W("ws.nlp_t")};      // in the target tiles
+        a.seg[1] = {B, 2 * B, 0, 0, noise_pi, Xp, W("ws.nlp_p")};       // extra workgroups
+        a.total_rows = h->Ra;
+        a.cache_row0 = B;
+        a.cache_row1 = h->Ra;
+        a.c_t = W("ws.c_t"); a.c_std = W("ws.c_std"); a.c_u = W("ws.c_u"); a.c_mask = W("ws.c_mask");
+        a.alpha_mode = 0;
+    } else {
         Launch L{};
         L.kind = Launch::AHEAD;
         L.name = "actor.head";
+        L.frees_slot = true;
         HeadArgs& a = L.head;
         a.H2 = Ha2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
@@ -602,7 +624,27 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         plan.push_back(L);
     }
     // ---- target / critic / model forward
-    {
+    if (fuse_head) {
+        std::vector<GemmProb> p0, p1;
+        for (int k = 0; k < 4; ++k) {
+            const std::string n = qn[k];
+            GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, act);
+            q0.headp = k < 2;
+            p0.push_back(q0);
+            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act));
+        }
+        add_gemm(h, plan, "q.fwd0+actor.head", p0, record_probs);
+        Launch& L = plan.back();
+        L.gemm.rowk = 3;
+        L.gemm.head = head_fused;
+        L.gemm.head_block0 = B / 4;
+        L.gemm.row_blocks = (h->Ra + 3) / 4 - B / 4;
+        L.grid += L.gemm.row_blocks;
+        L.flops += 2.0 * h->Ra * H1 * Aout;
+        L.bytes += 4.0 * h->Ra * (H1 + 6.0 * A);
+        L.frees_slot = true;
+        add_gemm(h, plan, "q.fwd1", p1, record_probs);
+    } else {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
@@ -987,8 +1029,9 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                 if (!merge_gemm(C.gemm, pg[gi]->gemm)) return false;
                 C.name += "+alpha";
                 ++gi;
-            } else if (C.kind == Launch::AHEAD && !head_done && ph) {
-                HeadArgs& a = C.head;
+            } else if (!head_done && ph && (C.kind == Launch::AHEAD || (C.kind == Launch::GEMM && C.gemm.rowk == 3))) {
+                // the head rows: a standalone actor.head, or the rows folded into q.fwd0
+                HeadArgs& a = C.kind == Launch::AHEAD ? C.head : C.gemm.head;
                 const HeadSeg& sg = ph->head.seg[0];
                 if (a.nseg >= 4) return false;
                 const int r0 = (a.total_rows + 3) & ~3;
@@ -999,7 +1042,14 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                 a.total_rows = m.r1;
                 a.alpha_mode = 1;
                 a.alpha_row0 = r0;
-                C.fin = ph->fin;
+                if (C.kind == Launch::AHEAD) {
+                    C.fin = ph->fin;
+                } else {
+                    C.gemm.hfin = ph->fin;
+                    const int rb = (a.total_rows + 3) / 4 - C.gemm.head_block0;
+                    C.grid += rb - C.gemm.row_blocks;
+                    C.gemm.row_blocks = rb;
+                }
                 C.name += "+alpha";
                 head_done = true;
             } else if (C.kind == Launch::GEMM && head_done && !final_done && pf &&
@@ -1027,6 +1077,7 @@ struct KTimeMap {
     std::vector<std::pair<int64_t, int>> spans;
     std::vector<std::string> names;
     std::vector<char> is_gemm;
+    std::vector<int> tiles;     // GEMM workgroups before the extra row blocks
     bool rows = false;      // also stamp the row kernels (k_actor_head, k_actor_bwd): dump only
 };
 
@@ -1055,6 +1106,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 kt->spans.push_back({kt->used, nwg});
                 kt->names.push_back(C.name);
                 kt->is_gemm.push_back(L.kind == Launch::GEMM);
+                kt->tiles.push_back(L.kind == Launch::GEMM ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) : nwg);
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);
@@ -1145,7 +1197,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                     continue;
                 }
                 emit(L, cs);
-                if (!due.empty() && !recorded && L.kind == Launch::AHEAD) {
+                if (!due.empty() && !recorded && L.frees_slot) {
                     HIPCHK(h, hipEventRecord(evS[j], cs));
                     recorded = true;
                 }
@@ -1763,24 +1815,31 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
         uint64_t prev_hi = 0;
         for (size_t si = 0; si < kt.spans.size(); ++si) {
             const auto& sp = kt.spans[si];
-            uint64_t lo = UINT64_MAX, hi = 0, last_start = 0, wmax = 0;
-            double wsum = 0.0;
+            uint64_t lo = UINT64_MAX, hi = 0, last_start = 0, wmax = 0, rmax = 0;
+            double wsum = 0.0, rsum = 0.0;
+            const int nt = kt.tiles[si];
             for (int b = 0; b < sp.second; ++b) {
                 const uint64_t t0 = host[sp.first + 2 * b], t1 = host[sp.first + 2 * b + 1];
                 lo = std::min(lo, t0);
                 hi = std::max(hi, t1);
                 last_start = std::max(last_start, t0);
-                wmax = std::max(wmax, t1 - t0);
-                wsum += (double)(t1 - t0);
+                if (b < nt) {
+                    wmax = std::max(wmax, t1 - t0);
+                    wsum += (double)(t1 - t0);
+                } else {
+                    rmax = std::max(rmax, t1 - t0);
+                    rsum += (double)(t1 - t0);
+                }
             }
             if (kt.is_gemm[si]) {
                 sum += (double)(hi - lo) * 0.01;         // 100 MHz ticks -> us
                 ++cnt;
             }
             if (dump)
-                std::fprintf(dump, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f\n", kt.names[si].c_str(), sp.second,
-                             (hi - lo) * 0.01, wsum / sp.second * 0.01, wmax * 0.01, (last_start - lo) * 0.01,
-                             prev_hi ? ((double)lo - (double)prev_hi) * 0.01 : 0.0);
+                std::fprintf(dump, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f\n", kt.names[si].c_str(), sp.second,
+                             (hi - lo) * 0.01, wsum / std::max(1, nt) * 0.01, wmax * 0.01, (last_start - lo) * 0.01,
+                             prev_hi ? ((double)lo - (double)prev_hi) * 0.01 : 0.0,
+                             sp.second > nt ? rsum / (sp.second - nt) * 0.01 : 0.0, rmax * 0.01);
             prev_hi = hi;
         }
         if (dump) std::fclose(dump);

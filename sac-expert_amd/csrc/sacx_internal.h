@@ -92,6 +92,10 @@ struct GemmProb {
     int32_t mse;
     const float *se_raw, *spe_raw, *dmean, *dden;
     float* part;
+    // GM_FWD: the A operand's last columns [K - A, K) are the actor's evaluate() actions of the
+    // tile's rows, computed in the tile's prologue from GemmArgs::head (seg[0]); columns
+    // [0, K - A) are read from A as usual (the target rows: actor.head folded into q.fwd0)
+    int32_t headp;
 };
 
 struct FinalArgs {
@@ -142,6 +146,36 @@ struct QHeadArgs {
     float* mse_rows;        // [ne]
 };
 
+struct HeadSeg {
+    int32_t r0, r1;        // actor rows [r0, r1)
+    int32_t mode;          // 0 = evaluate (neglogp), 1 = sample (no neglogp)
+    int32_t xq_row0;       // first row in xq_out
+    const float* noise;    // [r1-r0, A]
+    float* xq_out;         // normalised action -> xq_out[(xq_row0 + i) * ldQ + S + j]
+    float* nlp_out;        // [r1-r0] (evaluate)
+    float* pi_out;         // raw action lim*tanh(x) -> pi_out[(i) * A + j] (nullable)
+};
+
+struct HeadArgs {
+    const float* H2; int32_t ldh;
+    const float* W3;       // W3_ext [(H1+1), Aout]
+    const float* logstd;   // [A] global logstd (per_state_std == 0)
+    int32_t H1, A, Aout, S, ldQ, per_state_std;
+    float lim;
+    const float *a_mean, *a_den;
+    int32_t nseg;
+    HeadSeg seg[4];
+    int32_t total_rows;
+    // backward cache (rows >= cache_row0 are cached at [row - cache_row0])
+    int32_t cache_row0, cache_row1;
+    float* c_t; float* c_std; float* c_u; float* c_mask;
+    // alpha mode: rows >= alpha_row0 (a multiple of 4: whole workgroups) are the alpha
+    // evaluate() of an update; their workgroups write partials of sum(-nlp + H) to fin.red
+    int32_t alpha_mode;
+    int32_t alpha_row0;
+    uint64_t* ktime;        // measurement only (as GemmArgs::ktime)
+};
+
 #define GEMM_MAXP 8
 struct GemmArgs {
     GemmProb probs[GEMM_MAXP];   // by value: no dependent global load to find a tile's problem
@@ -163,6 +197,12 @@ struct GemmArgs {
     // (horizontal fusion: the heads and the unscaled dX GEMM are independent)
     int32_t rowk, row_blocks;
     QHeadArgs qh;
+    // GM_FWD with rowk = 3: the actor head (GemmArgs::head) -- seg[0] in the prologue of the
+    // headp problems, the other rows as row_blocks extra workgroups (from row head_block0 * 4);
+    // hfin: the alpha-row partials (alpha_mode)
+    HeadArgs head;
+    FinalArgs hfin;
+    int32_t head_block0;
     uint64_t* ktime;       // measurement only: per-workgroup start / end ticks (nullable)
 };
 
@@ -199,35 +239,6 @@ struct GatherArgs {
 };
 
 // ---------------------------------------------------------------- actor head rows
-struct HeadSeg {
-    int32_t r0, r1;        // actor rows [r0, r1)
-    int32_t mode;          // 0 = evaluate (neglogp), 1 = sample (no neglogp)
-    int32_t xq_row0;       // first row in xq_out
-    const float* noise;    // [r1-r0, A]
-    float* xq_out;         // normalised action -> xq_out[(xq_row0 + i) * ldQ + S + j]
-    float* nlp_out;        // [r1-r0] (evaluate)
-    float* pi_out;         // raw action lim*tanh(x) -> pi_out[(i) * A + j] (nullable)
-};
-
-struct HeadArgs {
-    const float* H2; int32_t ldh;
-    const float* W3;       // W3_ext [(H1+1), Aout]
-    const float* logstd;   // [A] global logstd (per_state_std == 0)
-    int32_t H1, A, Aout, S, ldQ, per_state_std;
-    float lim;
-    const float *a_mean, *a_den;
-    int32_t nseg;
-    HeadSeg seg[4];
-    int32_t total_rows;
-    // backward cache (rows >= cache_row0 are cached at [row - cache_row0])
-    int32_t cache_row0, cache_row1;
-    float* c_t; float* c_std; float* c_u; float* c_mask;
-    // alpha mode: rows >= alpha_row0 (a multiple of 4: whole workgroups) are the alpha
-    // evaluate() of an update; their workgroups write partials of sum(-nlp + H) to fin.red
-    int32_t alpha_mode;
-    int32_t alpha_row0;
-    uint64_t* ktime;        // measurement only (as GemmArgs::ktime)
-};
 
 // ---------------------------------------------------------------- Q heads
 

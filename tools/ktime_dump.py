@@ -35,10 +35,12 @@ def main():
     agg = {}
     for r in rows:
         agg.setdefault(r[0], []).append([float(x) for x in r[2:]])
-    print(f"\n{'launch (mean over updates)':34s} {'n':>5s} {'span':>6s} {'wg_avg':>6s} {'wg_max':>6s} {'skew':>6s} {'gap':>6s}")
+    print(f"\n{'launch (mean over updates)':34s} {'n':>5s} {'span':>6s} {'wg_avg':>6s} {'wg_max':>6s} {'skew':>6s} "
+          f"{'gap':>6s} {'row_avg':>7s} {'row_max':>7s}")
     for name, v in agg.items():
         v = np.array(v).mean(0)
-        print(f"{name:34s} {len(agg[name]):5d} {v[0]:6.2f} {v[1]:6.2f} {v[2]:6.2f} {v[3]:6.2f} {v[4]:6.2f}")
+        print(f"{name:34s} {len(agg[name]):5d} {v[0]:6.2f} {v[1]:6.2f} {v[2]:6.2f} {v[3]:6.2f} {v[4]:6.2f} "
+              f"{v[5]:7.2f} {v[6]:7.2f}")
     a = np.array([[float(x) for x in r[2:]] for r in rows])
     print(f"mean over {len(rows)} launches: span {a[:, 0].mean():.2f} wg_avg {a[:, 1].mean():.2f} "
           f"wg_max {a[:, 2].mean():.2f} skew {a[:, 3].mean():.2f} gap {a[:, 4].mean():.2f} us")
