@@ -851,8 +851,21 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         }
         break;
     default:
-        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true>), grid, block, 0, s, a);
-        else hipLaunchKernelGGL((k_gemm<GM_DW, 0>), grid, block, 0, s, a);
+        if (a.rowk == 3) {                 // dW + Adam with the policy rows of actor.head beside it
+            const dim3 gh(a.total_tiles + a.row_blocks);
+            const bool h8 = a.head.H1 > 256;
+            if (a.bf16) {
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true>), gh, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true>), gh, block, 0, s, a);
+            } else {
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8>), gh, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4>), gh, block, 0, s, a);
+            }
+        } else if (a.bf16) {
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true>), grid, block, 0, s, a);
+        } else {
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0>), grid, block, 0, s, a);
+        }
     }
 }
 

@@ -592,12 +592,15 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         a.H2 = Ha2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
-        a.nseg = 2;
-        a.seg[0] = {0, B, 0, 0, noise_t, nullptr, W("ws.nlp_t")};      // in the target tiles
-        a.seg[1] = {B, 2 * B, 0, 0, noise_pi, Xp, W("ws.nlp_p")};       // extra workgroups
+        // q.fwd0 carries the target rows (tile prologues) and, folded, the previous update's
+        // alpha rows; the policy rows ride as extra workgroups of critic.adam (policy_head)
+        a.nseg = 1;
+        a.seg[0] = {0, B, 0, 0, noise_t, nullptr, W("ws.nlp_t")};
+        // total_rows = Ra: merged_body appends the previous update's alpha rows at round4(Ra),
+        // where their layer-2 outputs live (ws.Hl2 aliases Ha2 from row round4(Ra))
         a.total_rows = h->Ra;
-        a.cache_row0 = B;
-        a.cache_row1 = h->Ra;
+        a.cache_row0 = 1 << 30;             // no backward cache from these rows (target, alpha)
+        a.cache_row1 = 1 << 30;
         a.c_t = W("ws.c_t"); a.c_std = W("ws.c_std"); a.c_u = W("ws.c_u"); a.c_mask = W("ws.c_mask");
         a.alpha_mode = 0;
     } else {
@@ -637,11 +640,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         Launch& L = plan.back();
         L.gemm.rowk = 3;
         L.gemm.head = head_fused;
-        L.gemm.head_block0 = B / 4;
-        L.gemm.row_blocks = (h->Ra + 3) / 4 - B / 4;
-        L.grid += L.gemm.row_blocks;
-        L.flops += 2.0 * h->Ra * H1 * Aout;
-        L.bytes += 4.0 * h->Ra * (H1 + 6.0 * A);
+        L.gemm.head_block0 = ((h->Ra + 3) & ~3) / 4;
+        L.gemm.row_blocks = 0;              // + the alpha rows when merged_body folds them in
+        L.flops += 2.0 * B * H1 * Aout;
+        L.bytes += 4.0 * B * (H1 + 6.0 * A);
         L.frees_slot = true;
         add_gemm(h, plan, "q.fwd1", p1, record_probs);
     } else {
@@ -704,6 +706,23 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                  W(n + ".l2"), W(t + ".l2"), GRP_Q));
         }
         add_gemm(h, plan, "critic.adam", pw, record_probs);
+        if (fuse_head) {                    // the policy rows of actor.head (read from pi.q.fwd0 on)
+            Launch& L = plan.back();
+            HeadArgs a = head_fused;
+            a.nseg = 1;
+            a.seg[0] = {B, 2 * B, 0, 0, noise_pi, Xp, W("ws.nlp_p")};
+            a.total_rows = 2 * B;
+            a.cache_row0 = B;
+            a.cache_row1 = h->Ra;
+            L.name += "+actor.head";
+            L.gemm.rowk = 3;
+            L.gemm.head = a;
+            L.gemm.head_block0 = B / 4;
+            L.gemm.row_blocks = (2 * B + 3) / 4 - B / 4;
+            L.grid += L.gemm.row_blocks;
+            L.flops += 2.0 * B * H1 * Aout;
+            L.bytes += 4.0 * B * (H1 + 6.0 * A);
+        }
         if (h->dp_ranks > 0) dp_split_adam(h, plan, "q0.l0", "q1.l2", "t0.l0", GRP_Q);
     }
     // ---- policy loss through the updated critics: the same linearity; pi.q.head's rows

@@ -187,10 +187,14 @@ def test_qloss_trajectory_100(gpu_available, use_expert):
     ref = []
     for R in Rs:
         o = oracle_step(st, ocfg, nrm, buf, R, expert)      # one oracle update per step
-        ref.append([o["q1_loss"], o["q2_loss"]])
+        ref.append([o["q1_loss"], o["q2_loss"], o["alpha_loss"]])
     ref = np.array(ref)
-    rel = np.abs(dev[:, :2] - ref) / np.abs(ref)
+    rel = np.abs(dev[:, :2] - ref[:, :2]) / np.abs(ref[:, :2])
     assert rel.max() < 1e-4, rel.max()
+    # the alpha loss (-alpha * mean(-nlp + H) over the alpha rows) catches a wrong alpha
+    # branch that the Q losses barely see once alpha is clamped at 1e-5
+    rel_a = np.abs(dev[:, 3] - ref[:, 2]) / np.abs(ref[:, 2])
+    assert rel_a.max() < 1e-3, rel_a.max()
     got = eng.rng_get_state()
     exp = rs.get_state()
     assert np.array_equal(got[1], exp[1]) and got[2] == exp[2]
