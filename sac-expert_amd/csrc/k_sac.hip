@@ -525,10 +525,17 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         finalize_update(ga.fin, ga.fin.nred);
         return;
     }
+    if constexpr (ROWK == 3) {
+        // actor.head rows beside the tiles: dispatched first, so their serial row work
+        // overlaps the tiles instead of trailing the launch
+        if (tile < ga.row_blocks) {
+            actor_head_body<NQ>(ga.head, ga.hfin, ga.head_block0 + tile);
+            return;
+        }
+        tile -= ga.row_blocks;
+    }
     if (tile >= ga.total_tiles) {
-        if constexpr (ROWK == 3) {         // actor.head rows beside the target tiles
-            actor_head_body<NQ>(ga.head, ga.hfin, ga.head_block0 + tile - ga.total_tiles);
-        } else if constexpr (ROWK > 0) {   // horizontally fused Q-head rows
+        if constexpr (ROWK > 0 && ROWK < 3) {   // horizontally fused Q-head rows
             qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles);
         }
         return;

@@ -1096,7 +1096,7 @@ struct KTimeMap {
     std::vector<std::pair<int64_t, int>> spans;
     std::vector<std::string> names;
     std::vector<char> is_gemm;
-    std::vector<int> tiles;     // GEMM workgroups before the extra row blocks
+    std::vector<std::pair<int, int>> rowspan;   // [first, end) workgroups that run row kernels
     bool rows = false;      // also stamp the row kernels (k_actor_head, k_actor_bwd): dump only
 };
 
@@ -1125,7 +1125,9 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 kt->spans.push_back({kt->used, nwg});
                 kt->names.push_back(C.name);
                 kt->is_gemm.push_back(L.kind == Launch::GEMM);
-                kt->tiles.push_back(L.kind == Launch::GEMM ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) : nwg);
+                if (L.kind != Launch::GEMM) kt->rowspan.push_back({0, 0});
+                else if (C.gemm.rowk == 3) kt->rowspan.push_back({C.gemm.has_final ? 1 : 0, (C.gemm.has_final ? 1 : 0) + C.gemm.row_blocks});
+                else kt->rowspan.push_back({C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0), nwg});
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);
@@ -1836,13 +1838,13 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
             const auto& sp = kt.spans[si];
             uint64_t lo = UINT64_MAX, hi = 0, last_start = 0, wmax = 0, rmax = 0;
             double wsum = 0.0, rsum = 0.0;
-            const int nt = kt.tiles[si];
+            const int rb0 = kt.rowspan[si].first, rb1 = kt.rowspan[si].second, nt = sp.second - (rb1 - rb0);
             for (int b = 0; b < sp.second; ++b) {
                 const uint64_t t0 = host[sp.first + 2 * b], t1 = host[sp.first + 2 * b + 1];
                 lo = std::min(lo, t0);
                 hi = std::max(hi, t1);
                 last_start = std::max(last_start, t0);
-                if (b < nt) {
+                if (b < rb0 || b >= rb1) {
                     wmax = std::max(wmax, t1 - t0);
                     wsum += (double)(t1 - t0);
                 } else {
@@ -1858,7 +1860,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
                 std::fprintf(dump, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f\n", kt.names[si].c_str(), sp.second,
                              (hi - lo) * 0.01, wsum / std::max(1, nt) * 0.01, wmax * 0.01, (last_start - lo) * 0.01,
                              prev_hi ? ((double)lo - (double)prev_hi) * 0.01 : 0.0,
-                             sp.second > nt ? rsum / (sp.second - nt) * 0.01 : 0.0, rmax * 0.01);
+                             rb1 > rb0 ? rsum / (rb1 - rb0) * 0.01 : 0.0, rmax * 0.01);
             prev_hi = hi;
         }
         if (dump) std::fclose(dump);
