@@ -3,7 +3,8 @@
 Per kernel family: mean over dispatches of FETCH_SIZE and WRITE_SIZE (KB), and
 traffic_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 -- on gfx950
 FETCH_SIZE counts 128-B requests at 64 B (MI355X_MICROARCH.md, section HBM).
-Families follow sacx kernel names (template arguments folded: k_gemm<1, 1> -> k_gemm).
+Families follow sacx kernel names (template arguments folded: k_gemm<1, 1> -> k_gemm;
+k_gemm_head -> k_gemm).
 usage: python tools/pmc_summary.py gpurun_out/pmc hc [source-tag] [extra-copy-path]
 """
 import csv
@@ -18,7 +19,10 @@ from collections import defaultdict
 def family(name):
     n = name.replace("void ", "")
     m = re.search(r"sacx::(k_[a-z_]+)", n)
-    return m.group(1) if m else None
+    if not m:
+        return None
+    # k_gemm_head is k_gemm with the actor-head prologue (one launch of the k_gemm family)
+    return "k_gemm" if m.group(1).startswith("k_gemm") else m.group(1)
 
 
 def main():
