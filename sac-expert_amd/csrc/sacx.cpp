@@ -72,6 +72,9 @@ struct Launch {
     bool after_final = false;  // graph: waits for the previous update's alpha branch
     bool alpha_branch = false; // graph: runs on the side stream beside the next update's first launches
     bool frees_slot = false;   // graph: the launch that carries the folded alpha rows (last reader of a slot)
+    // graph: the critics' forward on the buffer rows (s, a) runs on its own stream, between
+    // the previous update's critic.adam (q_release) and this update's q.head (q_consumer)
+    bool side_q = false, q_release = false, q_consumer = false;
 };
 
 const char* kernel_family(Launch::Kind k) {
@@ -112,7 +115,7 @@ struct sacx_handle {
     // binding
     char* arena = nullptr;
     hipStream_t stream = nullptr;
-    hipStream_t cap_stream = nullptr, rng_stream = nullptr;
+    hipStream_t cap_stream = nullptr, rng_stream = nullptr, q_stream = nullptr;
     bool bound = false;
     std::vector<Launch> plan[NSLOT];
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
@@ -482,6 +485,8 @@ void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string&
     a.adam = G.gemm.adam;
     U.grid = (int)((n + 255) / 256);
     U.bytes = 4.0 * n * (targ.empty() ? 7 : 9);
+    U.q_release = G.q_release;          // the weights are final after the apply, not the grad launch
+    G.q_release = false;
     plan.push_back(U);
 }
 
@@ -628,13 +633,25 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     }
     // ---- target / critic / model forward
     if (fuse_head) {
-        std::vector<GemmProb> p0, p1;
+        // SACX_SIDE_Q=1 moves the critics' (s, a) forward onto a third stream, off the chain.
+        // Measured slower on MI355X (9.6k vs 11.8k updates/s): the cross-stream edges of the
+        // replayed graph add ~0.3 us to every launch gap and q.head then waits ~8 us.
+        const char* sq = std::getenv("SACX_SIDE_Q");
+        const bool side_q = sq && std::atoi(sq) != 0;
+        std::vector<GemmProb> p0, p1, s0, s1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
             GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, act);
             q0.headp = k < 2;
-            p0.push_back(q0);
-            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act));
+            GemmProb q1 = prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act);
+            (side_q && k >= 2 ? s0 : p0).push_back(q0);
+            (side_q && k >= 2 ? s1 : p1).push_back(q1);
+        }
+        if (side_q) {
+            add_gemm(h, plan, "qsa.fwd0", s0, record_probs);
+            plan.back().side_q = true;
+            add_gemm(h, plan, "qsa.fwd1", s1, record_probs);
+            plan.back().side_q = true;
         }
         add_gemm(h, plan, "q.fwd0+actor.head", p0, record_probs);
         Launch& L = plan.back();
@@ -688,6 +705,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         }
         add_gemm(h, plan, "q.head+critic.bwd1", pb, record_probs);
         Launch& L = plan.back();
+        L.q_consumer = true;
         L.gemm.rowk = 1;
         L.gemm.row_blocks = (B + 3) / 4;
         L.gemm.qh = q;
@@ -706,6 +724,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                  W(n + ".l2"), W(t + ".l2"), GRP_Q));
         }
         add_gemm(h, plan, "critic.adam", pw, record_probs);
+        plan.back().q_release = true;
         if (fuse_head) {                    // the policy rows of actor.head (read from pi.q.fwd0 on)
             Launch& L = plan.back();
             HeadArgs a = head_fused;
@@ -1135,8 +1154,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             enqueue(L, h, st);
         }
     };
-    hipStream_t cs = h->cap_stream, rs = h->rng_stream;
-    const int nev = 3 * G + 1;
+    hipStream_t cs = h->cap_stream, rs = h->rng_stream, qs = h->q_stream;
+    const int nev = 5 * G + 1;
     for (int i = (int)h->events.size(); i < nev; ++i) {
         hipEvent_t e;
         HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1146,6 +1165,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     hipEvent_t* evS = h->events.data() + G;      // update j's body done
     hipEvent_t* evF = h->events.data() + 2 * G;  // alpha.final of update j done
     hipEvent_t evFork = h->events[3 * G];
+    hipEvent_t* evC = h->events.data() + 3 * G + 1;  // update j's critic weights final (critic.adam)
+    hipEvent_t* evQ = h->events.data() + 4 * G + 1;  // update j's (s, a) critic forward done
     HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
     const bool fork = with_rng && std::getenv("SACX_NO_FORK") == nullptr;
     // diagnostics: SACX_GATHER_MAIN keeps the gather on the main stream; SACX_MERGE_ALPHA=0
@@ -1194,6 +1215,22 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         }
         for (int b = 0; b < (int)batches.size(); ++b)
             if (emit_after[b] < 0) HIPCHK(h, prologue(b));
+        // the (s, a) critic forward of update j on qs: after update j-1's critic.adam (graph
+        // start for j = 0) and update j's inputs; update j's q.head waits for it
+        auto side_q = [&](int j, hipEvent_t after) -> hipError_t {
+            int bj = 0;
+            for (int b = 0; b < (int)batches.size(); ++b)
+                if (batches[b].first <= j && j < batches[b].second) bj = b;
+            hipError_t e = hipStreamWaitEvent(qs, after, 0);
+            if (e == hipSuccess) e = hipStreamWaitEvent(qs, evR[bj], 0);
+            for (const Launch& L : h->plan[j % nslot])
+                if (e == hipSuccess && L.side_q && (int)L.kind != skip_kind) emit(L, qs);
+            if (e == hipSuccess) e = hipEventRecord(evQ[j], qs);
+            return e;
+        };
+        bool has_side = false;
+        for (const Launch& L : h->plan[0]) has_side = has_side || L.side_q;
+        if (has_side) HIPCHK(h, side_q(0, evFork));
         std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
             if (batch_of[j] >= 0) HIPCHK(h, hipStreamWaitEvent(cs, evR[batch_of[j]], 0));
@@ -1212,12 +1249,22 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 if (emit_after[b] == j) due.push_back(b);
             bool recorded = false;
             for (const Launch& L : body) {
+                if (L.side_q) continue;        // on qs (side_q above)
+                if (L.q_consumer && has_side) HIPCHK(h, hipStreamWaitEvent(cs, evQ[j], 0));
                 if ((int)L.kind == skip_kind) {
                     // ablation: the alpha.final folded into a skipped GEMM still runs
                     if (L.kind == Launch::GEMM && L.gemm.has_final) launch_alpha_final(L.gemm.fin, cs);
+                    if (L.q_release && has_side && j + 1 < G) {
+                        HIPCHK(h, hipEventRecord(evC[j], cs));
+                        HIPCHK(h, side_q(j + 1, evC[j]));
+                    }
                     continue;
                 }
                 emit(L, cs);
+                if (L.q_release && has_side && j + 1 < G) {
+                    HIPCHK(h, hipEventRecord(evC[j], cs));
+                    HIPCHK(h, side_q(j + 1, evC[j]));
+                }
                 if (!due.empty() && !recorded && L.frees_slot) {
                     HIPCHK(h, hipEventRecord(evS[j], cs));
                     recorded = true;
@@ -1321,6 +1368,7 @@ void sacx_destroy(sacx_handle* h) {
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
+    if (h->q_stream) (void)hipStreamDestroy(h->q_stream);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     delete h;
 }
@@ -1384,6 +1432,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     build_model_plan(h);
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
+    HIPCHK(h, hipStreamCreateWithFlags(&h->q_stream, hipStreamNonBlocking));
     h->bound = true;
     return 0;
 }
