@@ -81,9 +81,10 @@ def test_replay_ring_fifo(gpu_available):
 
 
 def _one_step_compare(act, normalizers="identity", per_state_std=False, use_expert=False, B=256, seed=0,
-                      done_p=0.05, S=17, A=6):
+                      done_p=0.05, S=17, A=6, hidden=(256, 256)):
     eng, ocfg, st, buf, nrm, expert = make_pair(act=act, normalizers=normalizers, per_state_std=per_state_std,
-                                               use_expert=use_expert, B=B, seed=seed, done_p=done_p, S=S, A=A)
+                                               use_expert=use_expert, B=B, seed=seed, done_p=done_p, S=S, A=A,
+                                               hidden=hidden)
     N = buf["r"].shape[0]
     rs = np.random.RandomState(seed + 5)
     gen = np.random.default_rng(seed + 6)
@@ -156,6 +157,29 @@ def test_one_update_per_state_std(gpu_available):
 
 def test_one_update_sac_eo(gpu_available):
     _one_step_compare("relu", use_expert=True, seed=5)
+
+
+def test_one_update_odd_draws(gpu_available):
+    """A = 1, B = 37: every normal(size=(B, A)) draw is odd, so the legacy gauss cache carries
+    a value from one draw into the next (target -> policy -> alpha noise)."""
+    _one_step_compare("tanh", B=37, S=3, A=1, seed=7)
+
+
+def test_one_update_wide_hidden(gpu_available):
+    """Hidden 320 / 384: row kernels on 8 registers per lane, the folded head with K = 384."""
+    _one_step_compare("relu", hidden=(320, 384), seed=8)
+
+
+def test_one_update_narrow_hidden(gpu_available):
+    """Hidden 100 / 60 (not multiples of 16 or 4): scalar operand loads and the separate
+    actor.head launch (the fold needs H1 % 16 == 0)."""
+    _one_step_compare("elu", hidden=(100, 60), seed=9)
+
+
+def test_one_update_unfused_head(gpu_available, monkeypatch):
+    """SACX_FUSE_HEAD=0: the standalone actor.head launch path of plain SAC."""
+    monkeypatch.setenv("SACX_FUSE_HEAD", "0")
+    _one_step_compare("relu", seed=10)
 
 
 def test_one_update_small_batch(gpu_available):
