@@ -224,7 +224,7 @@ def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):
     return ({"steps_per_s": round(1.0 / fit_s, 1), "us_per_step": round(fit_s * 1e6, 2),
              "tflops": round(fit_flops / fit_s / 1e12, 3), "models": 2, "minibatch": mb, "graph": True},
             {"n_traj": 1000, "horizon": 5, "ms_per_call": round(roll_s * 1e3, 4),
-             "transitions_per_s": round(5000 / roll_s, 1), "launches_per_step": 9, "graph": False})
+             "transitions_per_s": round(5000 / roll_s, 1), "launches_per_step": 9, "graph": True})
 
 
 def main():

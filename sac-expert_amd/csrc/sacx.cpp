@@ -43,6 +43,16 @@ std::string g_create_error;
 
 inline int64_t r4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
+struct RollKey {             // sacx_rollout graph cache key (memcmp'd: no padding holes)
+    int32_t model;
+    int32_t pad0;
+    int64_t n;
+    int32_t horizon, deterministic;
+    float delta_clip, reward_clip;
+    const void* ptrs[6];
+};
+static_assert(sizeof(RollKey) == 4 + 4 + 8 + 4 + 4 + 4 + 4 + 6 * 8, "RollKey is packed");
+
 struct SegInfo {
     std::string name;
     uint64_t off;
@@ -132,6 +142,7 @@ struct sacx_handle {
     std::vector<GemmProb> probs;
     int probs_cursor = 0;
     std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;   // (G, with_rng, skipped kind)
+    std::vector<std::pair<RollKey, hipGraphExec_t>> roll_graphs;     // sacx_rollout replays
     std::vector<hipEvent_t> events;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
 
@@ -1365,6 +1376,7 @@ void sacx_destroy(sacx_handle* h) {
     if (!h) return;
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     if (h->mgraph) (void)hipGraphExecDestroy(h->mgraph);
+    for (auto& kv : h->roll_graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
@@ -1709,15 +1721,10 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
     return 0;
 }
 
-int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
-                 int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
-                 float* r_out, float* sp_out, uint8_t* d_out) {
-    if (!h || !h->bound) return fail(h, "not bound");
-    if (!h->cfg.use_expert) return fail(h, "rollout needs the world models (use_expert)");
-    if (model < 0 || model > 1) return fail(h, "model index out of range");
-    if (n < 0 || horizon < 0) return fail(h, "bad arguments");
-    if (n == 0 || horizon == 0) return 0;
-    if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
+// the launches of one rollout call on stream st (eager, or captured by sacx_rollout)
+static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
+                     int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
+                     float* r_out, float* sp_out, uint8_t* d_out, hipStream_t st) {
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
@@ -1737,19 +1744,19 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
             ra.d_mean = W("norm.d_mean"); ra.d_den = W("norm.d_den"); ra.r_norm = W("norm.r");
             ra.clip_d = delta_clip; ra.clip_r = reward_clip;
             ra.mode = 0;
-            launch_roll(ra, h->stream);
+            launch_roll(ra, st);
             float* noise = deterministic ? nullptr : W("roll.noise");
             if (!deterministic) {      // actor.sample: u = np.random.normal(size=(m, A))
                 RngArgs r{};
                 r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
                 r.n_int = 0; r.n_norm = m * A; r.out_idx = nullptr; r.out_norm = noise;
                 r.slot = -1; r.reset_seq = 0; r.nupd = 1;
-                launch_rng(r, h->stream);
+                launch_rng(r, st);
             }
             std::vector<Launch> pl;
             add_gemm(h, pl, "roll.a.fwd0", {prob_fwd(W("roll.X"), ldS, m, S, W("actor.l0"), H0, W("roll.H1"), h->act)}, false);
             add_gemm(h, pl, "roll.a.fwd1", {prob_fwd(W("roll.H1"), H0, m, H0, W("actor.l1"), H1, W("roll.H2"), h->act)}, false);
-            for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+            for (auto& L : pl) launch_gemm(L.gemm, st);
             pl.clear();
             HeadArgs a{};
             a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
@@ -1763,17 +1770,56 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
             a.cache_row0 = 1 << 30;
             a.alpha_mode = 0;
             FinalArgs f{};
-            launch_actor_head(a, f, h->stream);
+            launch_actor_head(a, f, st);
             add_gemm(h, pl, "roll.m.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->mact)}, false);
             add_gemm(h, pl, "roll.m.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->mact)}, false);
             add_gemm(h, pl, "roll.m.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), O, W("roll.O"), ACT_NONE)}, false);
-            for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+            for (auto& L : pl) launch_gemm(L.gemm, st);
             h->probs_cursor -= 5;      // host table bookkeeping of add_gemm (these launches are not in a plan)
             ra.mode = 1;
-            launch_roll(ra, h->stream);
+            launch_roll(ra, st);
         }
     }
-    HIPCHK(h, hipGetLastError());
+}
+
+int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
+                 int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
+                 float* r_out, float* sp_out, uint8_t* d_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "rollout needs the world models (use_expert)");
+    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (n < 0 || horizon < 0) return fail(h, "bad arguments");
+    if (n == 0 || horizon == 0) return 0;
+    if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
+    // one captured graph per (model, shape, clips, pointers): the Python host keeps its
+    // staging / output buffers per shape, so repeated calls replay (SACX_ROLL_GRAPH=0: eager)
+    const char* rg = std::getenv("SACX_ROLL_GRAPH");
+    if (rg && std::atoi(rg) == 0) {
+        enqueue_rollout(h, model, s_init, n, horizon, deterministic, delta_clip, reward_clip, s_out, a_out, r_out,
+                        sp_out, d_out, h->stream);
+        HIPCHK(h, hipGetLastError());
+        return 0;
+    }
+    RollKey key{model, 0, n, horizon, deterministic, delta_clip, reward_clip, {s_init, s_out, a_out, r_out, sp_out, d_out}};
+    hipGraphExec_t ge = nullptr;
+    for (auto& kv : h->roll_graphs)
+        if (std::memcmp(&kv.first, &key, sizeof(RollKey)) == 0) ge = kv.second;
+    if (!ge) {
+        HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+        enqueue_rollout(h, model, s_init, n, horizon, deterministic, delta_clip, reward_clip, s_out, a_out, r_out,
+                        sp_out, d_out, h->cap_stream);
+        hipGraph_t g;
+        HIPCHK(h, hipStreamEndCapture(h->cap_stream, &g));
+        const hipError_t e = hipGraphInstantiateWithFlags(&ge, g, 0);
+        (void)hipGraphDestroy(g);
+        if (e != hipSuccess) return fail(h, std::string("rollout graph: ") + hipGetErrorString(e));
+        if (h->roll_graphs.size() >= 4) {          // a few shapes live at once; drop the oldest
+            (void)hipGraphExecDestroy(h->roll_graphs.front().second);
+            h->roll_graphs.erase(h->roll_graphs.begin());
+        }
+        h->roll_graphs.push_back({key, ge});
+    }
+    HIPCHK(h, hipGraphLaunch(ge, h->stream));
     return 0;
 }
 

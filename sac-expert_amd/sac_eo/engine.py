@@ -280,18 +280,30 @@ class Engine:
         [n,H,S], [n,H] (CUDA tensors, d bool).  Draws the actor's noise from the device copy
         of the global NumPy stream, one normal(size=(n, A)) per step."""
         S, A = self.cfg.s_dim, self.cfg.a_dim
-        s0 = self._dev(s_init, (-1, S))
-        n, H = int(s0.shape[0]), int(horizon)
-        kw = dict(dtype=torch.float32, device=self.device)
-        s, a, r, sp = (torch.empty((n, H, S), **kw), torch.empty((n, H, A), **kw),
-                       torch.empty((n, H), **kw), torch.empty((n, H, S), **kw))
-        d = torch.empty((n, H), dtype=torch.uint8, device=self.device)
+        src = self._dev(s_init, (-1, S))
+        n, H = int(src.shape[0]), int(horizon)
+        # staging + outputs kept per shape: stable pointers let libsacx replay its captured
+        # rollout graph; the caller gets copies
+        if not hasattr(self, "_roll_bufs"):
+            self._roll_bufs = {}
+        bufs = self._roll_bufs.get((n, H))
+        if bufs is None:
+            kw = dict(dtype=torch.float32, device=self.device)
+            bufs = (torch.empty((n, S), **kw), torch.empty((n, H, S), **kw), torch.empty((n, H, A), **kw),
+                    torch.empty((n, H), **kw), torch.empty((n, H, S), **kw),
+                    torch.empty((n, H), dtype=torch.uint8, device=self.device))
+            if len(self._roll_bufs) >= 4:
+                self._roll_bufs.pop(next(iter(self._roll_bufs)))
+            self._roll_bufs[(n, H)] = bufs
+        s0, s, a, r, sp, d = bufs
+        with torch.cuda.stream(self.stream):
+            s0.copy_(src)
         p = lambda t: ctypes.c_void_p(t.data_ptr())
         N.check(self.lib.sacx_rollout(self.h, int(model), p(s0), n, H, int(bool(deterministic)),
                                       float(delta_clip or 0.0), float(reward_clip or 0.0),
                                       p(s), p(a), p(r), p(sp), p(d)), self.h, "rollout")
-        self._keep_roll = s0
-        return s, a, r, sp, d.bool()
+        with torch.cuda.stream(self.stream):
+            return s.clone(), a.clone(), r.clone(), sp.clone(), d.bool()
 
     def expert_diag(self, s_e, a_e, sp_e, disc: bool = False, use_expert_actions: bool = False,
                     delta_clip: float = 0.0) -> dict:

@@ -444,3 +444,21 @@ def test_bf16_graph_equals_eager(gpu_available):
         outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy()))
         eng.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_rollout_graph_replay_equals_eager(gpu_available, monkeypatch):
+    """The captured rollout graph (replayed on the second call with the same shapes) gives
+    the eager launches' results bit for bit, and advances the stream identically."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=53, use_expert=True, normalizers="random")
+    s0 = (np.random.RandomState(6).normal(size=(50, ocfg.S))).astype(np.float32)
+    outs = []
+    for mode in ("1", "1", "0"):          # capture, replay, eager
+        monkeypatch.setenv("SACX_ROLL_GRAPH", mode)
+        eng.rng_set_state(np.random.RandomState(31).get_state())
+        res = [t.cpu().numpy() for t in eng.rollout(0, s0, 4)]
+        outs.append((res, eng.rng_get_state()))
+    for res, stt in outs[1:]:
+        for x, y in zip(outs[0][0], res):
+            assert np.array_equal(x, y)
+        assert np.array_equal(outs[0][1][1], stt[1]) and outs[0][1][2] == stt[2]
+    eng.close()
