@@ -50,47 +50,53 @@ HBM_PEAK_GBS = 8000.0
 
 
 def build_engine(cfgd, seeds, device, dp=None, batch=None, weight_seed=None):
-    """seeds: this replica's reference-style seeds (sac_eo.common.seeding.derive_seeds).
-    dp: (rccl id, ranks, rank) for the data-parallel mode, with the local `batch` and one
-    `weight_seed` shared by all ranks (identical initial weights)."""
+    """seeds: this replica's reference-style seeds (sac_eo.common.seeding.derive_seeds), one
+    dict of scalars per learner; a list of K dicts builds a packed handle of K seeds (one launch
+    chain for all, grid z = seed).  dp: (rccl id, ranks, rank) for the data-parallel mode, with
+    the local `batch` and one `weight_seed` shared by all ranks (identical initial weights)."""
     import torch
     from sac_eo.engine import Engine, EngineConfig
     from sac_eo.nets import create_nn_weights
+    seed_list = list(seeds) if isinstance(seeds, (list, tuple)) else [seeds]
     S, A = cfgd["S"], cfgd["A"]
     B = batch or cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
                         expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "128")),
-                        gemm_bf16=bool(cfgd.get("bf16", False)))
+                        gemm_bf16=bool(cfgd.get("bf16", False)), seeds=len(seed_list))
     eng = Engine(ecfg, device=device, dp=dp)
-    rng = np.random.default_rng(weight_seed if weight_seed is not None else seeds["setup"])
-    eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
-    for k in range(2):
-        w = create_nn_weights(rng, S + A, 1, cfgd["hidden"], 1.0)
-        eng.set_net(f"q{k}", w)
-        eng.set_net(f"t{k}", w)
-    if cfgd["use_expert"]:
-        for k in range(2):
-            eng.set_net(f"m{k}", create_nn_weights(rng, S + A, S + 1, (512, 512), 0.01))
-    # synthetic HalfCheetah-shaped rows generated on the device (SURVEY.md §8d)
-    g = torch.Generator(device=device)
-    g.manual_seed(int(seeds["sim"]))                   # synthetic replay rows
-    N = cfgd["buffer"]
-    sig = torch.rand(S, device=device, generator=g) * 4.9 + 0.1
-    s = torch.randn(N, S, device=device, generator=g) * sig
-    sp = torch.randn(N, S, device=device, generator=g) * sig
-    a = torch.rand(N, A, device=device, generator=g) * 2 - 1
-    r = torch.randn(N, device=device, generator=g)
-    d = torch.zeros(N, device=device)
-    eng.append(s, a, r, sp, d)
-    del s, sp, a, r, d
-    if cfgd["use_expert"]:
-        ers = np.random.RandomState(seeds["eval"])
-        eng.set_expert(ers.normal(size=(20, S)), ers.normal(size=(20, S)), 1e-3)
-        gen = np.random.default_rng(seeds["algorithm"])  # SAC_exp's self.rng (alg_seed)
-        perms = np.stack([gen.permutation(20) for _ in range(4096)])
-        eng.push_perms(perms)
-    eng.rng_seed(seeds["expert"])                    # global stream: last np.random.seed (train.py:95-97)
+    for k, sd in enumerate(seed_list):
+        eng.select_seed(k)
+        rng = np.random.default_rng(weight_seed if weight_seed is not None else sd["setup"])
+        eng.set_net("actor", create_nn_weights(rng, S, A, cfgd["hidden"], 0.01))
+        for j in range(2):
+            w = create_nn_weights(rng, S + A, 1, cfgd["hidden"], 1.0)
+            eng.set_net(f"q{j}", w)
+            eng.set_net(f"t{j}", w)
+        if cfgd["use_expert"]:
+            for j in range(2):
+                eng.set_net(f"m{j}", create_nn_weights(rng, S + A, S + 1, (512, 512), 0.01))
+        # synthetic HalfCheetah-shaped rows generated on the device (SURVEY.md §8d)
+        g = torch.Generator(device=device)
+        g.manual_seed(int(sd["sim"]))                    # synthetic replay rows
+        N = cfgd["buffer"]
+        sig = torch.rand(S, device=device, generator=g) * 4.9 + 0.1
+        s = torch.randn(N, S, device=device, generator=g) * sig
+        sp = torch.randn(N, S, device=device, generator=g) * sig
+        a = torch.rand(N, A, device=device, generator=g) * 2 - 1
+        r = torch.randn(N, device=device, generator=g)
+        d = torch.zeros(N, device=device)
+        eng.append(s, a, r, sp, d)
+        eng.sync()
+        del s, sp, a, r, d
+        if cfgd["use_expert"]:
+            ers = np.random.RandomState(sd["eval"])
+            eng.set_expert(ers.normal(size=(20, S)), ers.normal(size=(20, S)), 1e-3)
+            gen = np.random.default_rng(sd["algorithm"])  # SAC_exp's self.rng (alg_seed)
+            perms = np.stack([gen.permutation(20) for _ in range(4096)])
+            eng.push_perms(perms)
+        eng.rng_seed(sd["expert"])                     # global stream: last np.random.seed (train.py:95-97)
+    eng.select_seed(0)
     eng.sync()
     return eng
 

@@ -15,7 +15,17 @@
  * (W_ext = [W ; b]), so reference get_weights()/set_weights() lists map onto
  * views (sac_eo/common/nn_utils.py:59-76).  Every call is asynchronous on the
  * bound HIP stream unless stated otherwise.  A handle is not re-entrant; use
- * one handle per learner (per GPU / per seed).
+ * one handle per learner (per GPU / per seed), or one handle of packed seeds.
+ *
+ * Packed seeds (cfg.seeds = K > 1): the handle holds K independent learners --
+ * the reference's --runs (sac_eo/train.py:118-152), each with its own weights,
+ * optimiser state, replay ring and RNG stream -- in K equal arena blocks
+ * sacx_seed_stride() bytes apart, each laid out as sacx_layout() describes.
+ * sacx_sac_step advances all K in the same kernel launches (grid z = seed).
+ * The data-path and RNG calls (append, expert rows, permutations, RNG state,
+ * actor_act, rollout, expert_diag, resync) address the seed chosen with
+ * sacx_seed_select (default 0).  sacx_model_fit and the data-parallel mode
+ * need K = 1.
  */
 #ifndef SACX_H
 #define SACX_H
@@ -26,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 2
+#define SACX_ABI_VERSION 3
 
 typedef struct sacx_handle sacx_handle;
 
@@ -71,6 +81,7 @@ typedef struct sacx_config {
     float reward_loss_coef;     /* --reward_loss_coef */
     int32_t gemm_bf16;          /* 1: the MLP GEMMs take bf16 operands (rounded on load) with fp32
                                    accumulation, fp32 master weights / Adam (config C5); 0: fp32 */
+    int32_t seeds;              /* independent learners packed in this handle (0/1 = one; <= 64) */
 } sacx_config;
 
 typedef struct sacx_segment {
@@ -102,7 +113,11 @@ enum sacx_stat { SACX_STAT_Q1_LOSS = 0, SACX_STAT_Q2_LOSS, SACX_STAT_P_LOSS, SAC
 int sacx_create(const sacx_config* cfg, sacx_handle** out);
 void sacx_destroy(sacx_handle* h);
 const char* sacx_last_error(const sacx_handle* h);   /* NULL handle: error of the last failed create */
-int64_t sacx_arena_bytes(const sacx_handle* h);
+int64_t sacx_arena_bytes(const sacx_handle* h);   /* all seeds */
+/* Bytes between consecutive seeds' arena blocks (packed seeds; = the arena size for one). */
+int64_t sacx_seed_stride(const sacx_handle* h);
+/* Packed seeds: the seed (0 <= seed < cfg.seeds) that the per-seed calls address. */
+int sacx_seed_select(sacx_handle* h, int32_t seed);
 int sacx_layout(const sacx_handle* h, sacx_segment* segs, int32_t cap, int32_t* n_out);
 /* Binds the caller-owned arena (>= sacx_arena_bytes, 256-B aligned) and the HIP
  * stream (hipStream_t as void*, NULL = default stream); builds the launch plan.

@@ -184,6 +184,59 @@ __device__ __forceinline__ uint32_t boff(bool ok, int elem) {
 // wave index as a scalar (lets per-row pointers and branches stay in SGPRs)
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
+// ---------------------------------------------------------------- packed seeds
+// A handle created with cfg.seeds = K holds K independent learners (the reference's --runs)
+// in K equal arena blocks sstride bytes apart.  Every launch of the update graph runs all of
+// them: grid z is the seed, and each arena pointer of the (seed-0) launch arguments moves by
+// blockIdx.z * sstride (a scalar add; null pointers stay null).
+__device__ __forceinline__ int64_t seed_off(int64_t sstride) { return (int64_t)blockIdx.z * sstride; }
+template <class T>
+__device__ __forceinline__ T* sr(T* p, int64_t so) {
+    return p ? reinterpret_cast<T*>(reinterpret_cast<unsigned long long>(p) + (unsigned long long)so) : p;
+}
+__device__ __forceinline__ void reloc(GemmProb& g, int64_t so) {
+    g.A = sr(g.A, so); g.B = sr(g.B, so); g.C = sr(g.C, so); g.bias = sr(g.bias, so); g.H = sr(g.H, so);
+    g.P = sr(g.P, so); g.T = sr(g.T, so); g.W0 = sr(g.W0, so); g.C0 = sr(g.C0, so); g.wgen = sr(g.wgen, so);
+    g.bscale = sr(g.bscale, so); g.se_raw = sr(g.se_raw, so); g.spe_raw = sr(g.spe_raw, so);
+    g.dmean = sr(g.dmean, so); g.dden = sr(g.dden, so); g.part = sr(g.part, so);
+}
+__device__ __forceinline__ void reloc(FinalArgs& f, int64_t so) {
+    f.alpha = sr(f.alpha, so); f.alpha_m = sr(f.alpha_m, so); f.alpha_v = sr(f.alpha_v, so); f.ctl = sr(f.ctl, so);
+    f.lq = sr(f.lq, so); f.lp = sr(f.lp, so); f.mse_rows = sr(f.mse_rows, so); f.red = sr(f.red, so);
+    f.stats = sr(f.stats, so); f.alpha_g = sr(f.alpha_g, so);
+}
+__device__ __forceinline__ void reloc(HeadSeg& g, int64_t so) {
+    g.noise = sr(g.noise, so); g.xq_out = sr(g.xq_out, so); g.nlp_out = sr(g.nlp_out, so); g.pi_out = sr(g.pi_out, so);
+}
+__device__ __forceinline__ void reloc(QHeadArgs& q, int64_t so) {
+    q.H2 = sr(q.H2, so);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) q.W3[k] = sr(q.W3[k], so);
+    q.D2 = sr(q.D2, so); q.g = sr(q.g, so); q.loss_rows = sr(q.loss_rows, so); q.alpha = sr(q.alpha, so);
+    q.nlp = sr(q.nlp, so); q.r = sr(q.r, so); q.d = sr(q.d, so); q.ret_den = sr(q.ret_den, so);
+    q.Hm2 = sr(q.Hm2, so);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) q.Wm3[k] = sr(q.Wm3[k], so);
+    q.se_raw = sr(q.se_raw, so); q.spe_raw = sr(q.spe_raw, so); q.d_mean = sr(q.d_mean, so);
+    q.d_den = sr(q.d_den, so); q.ctl = sr(q.ctl, so); q.Dm2 = sr(q.Dm2, so); q.mse_rows = sr(q.mse_rows, so);
+}
+__device__ __forceinline__ void reloc(ActorBwdArgs& b, int64_t so) {
+    b.Dp1 = sr(b.Dp1, so);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        b.Wq1[k] = sr(b.Wq1[k], so);
+        b.Wm1[k] = sr(b.Wm1[k], so);
+    }
+    b.Dm1 = sr(b.Dm1, so); b.a_den = sr(b.a_den, so); b.alpha = sr(b.alpha, so); b.ctl = sr(b.ctl, so);
+    b.c_t = sr(b.c_t, so); b.c_std = sr(b.c_std, so); b.c_u = sr(b.c_u, so); b.c_mask = sr(b.c_mask, so);
+    b.W3a = sr(b.W3a, so); b.Ha2 = sr(b.Ha2, so); b.Da3 = sr(b.Da3, so); b.Da2 = sr(b.Da2, so); b.E = sr(b.E, so);
+    b.gpol = sr(b.gpol, so);
+}
+// the grid z extent of a launch (1 for the single-seed eager calls, whose nseeds is 0)
+inline unsigned seeds_z(int n) { return n > 1 ? (unsigned)n : 1u; }
+// per-workgroup measurement slot (ktime): workgroups of seed z follow those of seed z-1
+__device__ __forceinline__ int ktime_wg() { return (int)(blockIdx.z * gridDim.x + blockIdx.x); }
+
 // ---------------------------------------------------------------- row helpers
 // A row of a hidden layer (width H <= 64*NQ) is held as hv[q] = h[lane + 64 q];
 // all loads of a row are issued before any reduction so the wave's memory
@@ -411,9 +464,9 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 // MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
-__device__ void qhead_block(const QHeadArgs& q, int block);
+__device__ void qhead_block(const QHeadArgs& q, int block, int64_t so);
 template <int NQ>
-__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block);
+__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so);
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
 // so blocks b and b+8 share an L2.  xcd_tile gives the blocks of one XCD a contiguous range of
@@ -431,11 +484,12 @@ __device__ __forceinline__ int xcd_tile(int b, int T) {
 // LDS for the main loop.  Column tile 0 stores the rows' neglogp for q.head.  The same
 // arithmetic as k_actor_head, with the 16-lane row sums of the MFMA layout.
 __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb& g, int m0, int tn,
-                                              float (&As)[16][68], float (&red)[4][4][64]) {
+                                              float (&As)[16][68], float (&red)[4][4][64], int64_t so) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 15, grp = lane >> 4;
     const int row = t >> 4, col = t & 15;
     const int A = hd.A, Aout = hd.Aout, H1 = hd.H1, S = g.K - A;
-    const HeadSeg& sg = hd.seg[0];
+    HeadSeg sg = hd.seg[0];
+    reloc(sg, so);
     const bool rok = m0 + row < g.M;
     // everything the prologue reads is requested first
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.A, 0x7fffffffu);
@@ -444,12 +498,12 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
     for (int q = 0; q < 4; ++q) xs[q] = bload(rx, boff(rok && col + 16 * q < S, (m0 + row) * g.lda + col + 16 * q));
     const bool jok = col < A;
     const float u = bload(rs(sg.noise), boff(jok && rok, (m0 + row - sg.r0) * A + col));
-    const float ls = bload(rs(hd.logstd), boff(jok && !hd.per_state_std, col));
-    const float am = bload(rs(hd.a_mean), boff(jok, col));
-    const float ad = bload(rs(hd.a_den), boff(jok, col));
-    const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(hd.W3, 0x7fffffffu);
+    const float ls = bload(rs(sr(hd.logstd, so)), boff(jok && !hd.per_state_std, col));
+    const float am = bload(rs(sr(hd.a_mean, so)), boff(jok, col));
+    const float ad = bload(rs(sr(hd.a_den, so)), boff(jok, col));
+    const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(sr(hd.W3, so), 0x7fffffffu);
     const float bias = bload(rw3, boff(col < Aout, H1 * Aout + col));
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(hd.H2, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rh = make_rsrc(sr(hd.H2, so), 0x7fffffffu);
     const int nIt = H1 >> 4, per = (nIt + 3) >> 2, i0 = wave * per, i1 = min(nIt, i0 + per);
     const bool hm = m0 + r < g.M, wn = r < Aout;
     floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
@@ -518,25 +572,28 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
+    const int64_t so = seed_off(ga.sstride);
     // the folded alpha.final of the previous update is workgroup 0: dispatched first, its
     // serial reductions overlap the tiles instead of trailing them
     int tile = (int)blockIdx.x - (ga.has_final ? 1 : 0);
     if (tile < 0) {
-        finalize_update(ga.fin, ga.fin.nred);
+        FinalArgs f = ga.fin;
+        reloc(f, so);
+        finalize_update(f, f.nred);
         return;
     }
     if constexpr (ROWK == 3) {
         // actor.head rows beside the tiles: dispatched first, so their serial row work
         // overlaps the tiles instead of trailing the launch
         if (tile < ga.row_blocks) {
-            actor_head_body<NQ>(ga.head, ga.hfin, ga.head_block0 + tile);
+            actor_head_body<NQ>(ga.head, ga.hfin, ga.head_block0 + tile, so);
             return;
         }
         tile -= ga.row_blocks;
     }
     if (tile >= ga.total_tiles) {
         if constexpr (ROWK > 0 && ROWK < 3) {   // horizontally fused Q-head rows
-            qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles);
+            qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles, so);
         }
         return;
     }
@@ -545,7 +602,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 #pragma unroll
     for (int i = 1; i < GEMM_MAXP; ++i)
         if (i < ga.nprob && tile >= ga.probs[i].tile_begin) p = i;
-    const GemmProb g = ga.probs[p];   // by value: every field loads once, up front (speculatable)
+    GemmProb g = ga.probs[p];   // by value: every field loads once, up front (speculatable)
+    reloc(g, so);
     const int lt = tile - g.tile_begin;
     const int tm = lt / g.tiles_n;
     const int tn = lt - tm * g.tiles_n;
@@ -601,7 +659,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             float bp[4];
             const int k0 = it0 * 16 + grp * 4;
             load_b<BKC, false, false>(rb, g, n, nok, it0 < it1 ? k0 : (1 << 30), bp);
-            head_prologue(ga.head, g, m0, tn, As, red);
+            head_prologue(ga.head, g, m0, tn, As, red, so);
             if (it0 < it1) {
                 float a[4];
 #pragma unroll
@@ -731,7 +789,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             const float pred = v + e0;
             const float sp_hat = e1 + (pred * e4 + e3);
             const float diff = e2 - sp_hat;
-            const float gscale = -ga.ctl->epsilon * g.grad_scale;
+            const float gscale = -sr(ga.ctl, so)->epsilon * g.grad_scale;
             float sq = out_ok ? diff * diff : 0.f;
             sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's tile row
             sq += __shfl_xor(sq, 4, 16);
@@ -753,7 +811,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             return;
         }
-        const Ctl* ctl = ga.ctl;
+        const Ctl* ctl = sr(ga.ctl, so);
         const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
         const float lr_t = adam_lr(ga.adam, g.group, tstep);
         const float gr = v * g.grad_scale;
@@ -780,8 +838,8 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            ga.ktime[2 * blockIdx.x] = t0;
-            ga.ktime[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+            ga.ktime[2 * ktime_wg()] = t0;
+            ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
@@ -795,18 +853,19 @@ __global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            ga.ktime[2 * blockIdx.x] = t0;
-            ga.ktime[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+            ga.ktime[2 * ktime_wg()] = t0;
+            ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
-    const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0)), block(256);
+    const unsigned z = seeds_z(a.nseeds);
+    const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0), 1, z), block(256);
     switch (a.mode) {
     case GM_FWD:
         if (a.rowk == 3) {                 // q.fwd0 with the actor head folded in
-            const dim3 gh(a.total_tiles + (a.has_final ? 1 : 0) + a.row_blocks);
+            const dim3 gh(a.total_tiles + (a.has_final ? 1 : 0) + a.row_blocks, 1, z);
             const bool h8 = a.head.H1 > 256;
 #define SACX_FH(V, Q)                                                                               \
     do {                                                                                           \
@@ -825,7 +884,7 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         }
         break;
     case GM_DX: {
-        const dim3 gx(a.total_tiles + (a.rowk ? a.row_blocks : 0));
+        const dim3 gx(a.total_tiles + (a.rowk ? a.row_blocks : 0), 1, z);
         const bool q8 = a.rowk && a.qh.H1 > 256;
 #define SACX_DX(V, R, Q)                                                                            \
     do {                                                                                           \
@@ -859,7 +918,7 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         break;
     default:
         if (a.rowk == 3) {                 // dW + Adam with the policy rows of actor.head beside it
-            const dim3 gh(a.total_tiles + a.row_blocks);
+            const dim3 gh(a.total_tiles + a.row_blocks, 1, z);
             const bool h8 = a.head.H1 > 256;
             if (a.bf16) {
                 if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true>), gh, block, 0, s, a);
@@ -989,8 +1048,14 @@ __device__ void rng_settle(RngShared& S, int& pos, int cl, int used, int nb) {
     (void)nb;
 }
 
-__global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
+__global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
     __shared__ RngShared S;
+    RngArgs a = a_in;
+    {
+        const int64_t so = seed_off(a_in.sstride);
+        a.st = sr(a_in.st, so); a.ctl = sr(a_in.ctl, so);
+        a.out_idx = sr(a_in.out_idx, so); a.out_norm = sr(a_in.out_norm, so);
+    }
     const int t = threadIdx.x;
     for (int i = t; i < 624; i += RNG_THREADS) S.blk[0][i] = a.st->key[i];
     int pos = a.st->pos;
@@ -1148,7 +1213,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
 }
 
 void launch_rng(const RngArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_rng, dim3(1), dim3(RNG_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_rng, dim3(1, 1, seeds_z(a.nseeds)), dim3(RNG_THREADS), 0, s, a);
 }
 
 // ==================================================================== k_gather
@@ -1159,11 +1224,15 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
     // slot (ga.slot + blockIdx.y): every slot buffer sits at a fixed distance from slot 0's
     GatherArgs g = ga;
     {
-        const int64_t off = (int64_t)blockIdx.y * ga.slot_bytes;
+        const int64_t so = seed_off(ga.sstride);
+        const int64_t off = (int64_t)blockIdx.y * ga.slot_bytes + so;
         auto sh = [off](auto* p) { return p ? (decltype(p))((char*)p + off) : p; };
         g.idx = sh(ga.idx); g.Xa = sh(ga.Xa); g.Xq = sh(ga.Xq); g.Xt = sh(ga.Xt); g.Xp = sh(ga.Xp);
         g.Xm = sh(ga.Xm); g.r = sh(ga.r); g.d = sh(ga.d); g.se_raw = sh(ga.se_raw); g.spe_raw = sh(ga.spe_raw);
         g.slot = ga.slot + (int)blockIdx.y;
+        g.replay = sr(ga.replay, so); g.ctl = sr(ga.ctl, so);
+        g.s_mean = sr(ga.s_mean, so); g.s_den = sr(ga.s_den, so); g.a_mean = sr(ga.a_mean, so); g.a_den = sr(ga.a_den, so);
+        g.exp_s = sr(ga.exp_s, so); g.exp_sp = sr(ga.exp_sp, so); g.perm_ring = sr(ga.perm_ring, so);
     }
     const int S = g.S, A = g.A;
     const __amdgpu_buffer_rsrc_t rsm = rs(g.s_mean), rsd = rs(g.s_den), ram = rs(g.a_mean), rad = rs(g.a_den);
@@ -1219,21 +1288,25 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
 
 void launch_gather(const GatherArgs& a, hipStream_t s) {
     const int rows = a.B + a.ne;
-    hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4, a.nupd > 0 ? a.nupd : 1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4, a.nupd > 0 ? a.nupd : 1, seeds_z(a.nseeds)), dim3(256), 0, s, a);
 }
 
 // one wave: alpha Adam + clamp and the statistics row of the update
-__global__ __launch_bounds__(64) void k_alpha_final(FinalArgs f) { finalize_update(f, f.nred); }
+__global__ __launch_bounds__(64) void k_alpha_final(FinalArgs f_in) {
+    FinalArgs f = f_in;
+    reloc(f, seed_off(f_in.sstride));
+    finalize_update(f, f.nred);
+}
 
 void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL(k_alpha_final, dim3(1), dim3(64), 0, s, f);
+    hipLaunchKernelGGL(k_alpha_final, dim3(1, 1, seeds_z(f.nseeds)), dim3(64), 0, s, f);
 }
 
 // ==================================================================== k_actor_head
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
 template <int NQ>
-__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block) {
+__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
     __shared__ float red_s[4];
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = block * 4 + wave;
@@ -1242,17 +1315,18 @@ __device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block
     for (int i = 1; i < h.nseg; ++i)
         if (row >= h.seg[i].r0) sidx = i;
     if (row < h.total_rows && row < h.seg[sidx].r1) {     // rows in the pad before alpha_row0 idle
-        const HeadSeg sg = h.seg[sidx];
+        HeadSeg sg = h.seg[sidx];
+        reloc(sg, so);
         const int A = h.A, Aout = h.Aout;
         const bool jok = lane < A;
         // everything this row reads is issued up front
         float hv[NQ];
-        load_row(rs(h.H2), row * h.ldh, h.H1, hv);
-        const __amdgpu_buffer_rsrc_t rW = rs(h.W3);
+        load_row(rs(sr(h.H2, so)), row * h.ldh, h.H1, hv);
+        const __amdgpu_buffer_rsrc_t rW = rs(sr(h.W3, so));
         const float u_pf = bload(rs(sg.noise), boff(jok, (row - sg.r0) * A + lane));
-        const float ls_pf = bload(rs(h.logstd), boff(jok && !h.per_state_std, lane));
-        const float am_pf = bload(rs(h.a_mean), boff(jok, lane));
-        const float ad_pf = bload(rs(h.a_den), boff(jok, lane));
+        const float ls_pf = bload(rs(sr(h.logstd, so)), boff(jok && !h.per_state_std, lane));
+        const float am_pf = bload(rs(sr(h.a_mean, so)), boff(jok, lane));
+        const float ad_pf = bload(rs(sr(h.a_den, so)), boff(jok, lane));
         const float bmu = bload(rW, boff(jok, h.H1 * Aout + lane));
         const float bls = bload(rW, boff(jok && h.per_state_std, h.H1 * Aout + A + lane));
         float mu = 0.f, lraw = 0.f;
@@ -1287,10 +1361,10 @@ __device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block
             if (sg.pi_out != nullptr) sg.pi_out[(size_t)(row - sg.r0) * A + j] = pi;
             if (row >= h.cache_row0 && row < h.cache_row1 && h.c_t != nullptr) {
                 const size_t ci = (size_t)(row - h.cache_row0) * A + j;
-                h.c_t[ci] = t;
-                h.c_std[ci] = sd;
-                h.c_u[ci] = u;
-                h.c_mask[ci] = (lraw >= -5.f && lraw <= 2.f) ? 1.f : 0.f;
+                sr(h.c_t, so)[ci] = t;
+                sr(h.c_std, so)[ci] = sd;
+                sr(h.c_u, so)[ci] = u;
+                sr(h.c_mask, so)[ci] = (lraw >= -5.f && lraw <= 2.f) ? 1.f : 0.f;
             }
         }
         if (sg.mode == 0) {
@@ -1307,7 +1381,7 @@ __device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block
         float part = red_s[0] + red_s[1];
         part = part + red_s[2];
         part = part + red_s[3];
-        f.red[block - h.alpha_row0 / 4] = part;
+        sr(f.red, so)[block - h.alpha_row0 / 4] = part;
     }
 }
 
@@ -1316,8 +1390,8 @@ __device__ __forceinline__ void ktime_stamp(uint64_t* kt, uint64_t t0) {
     if (kt != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            kt[2 * blockIdx.x] = t0;
-            kt[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+            kt[2 * ktime_wg()] = t0;
+            kt[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
@@ -1325,20 +1399,22 @@ __device__ __forceinline__ void ktime_stamp(uint64_t* kt, uint64_t t0) {
 template <int NQ>
 __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    actor_head_body<NQ>(h, f, (int)blockIdx.x);
+    actor_head_body<NQ>(h, f, (int)blockIdx.x, seed_off(h.sstride));
     ktime_stamp(h.ktime, t0);
 }
 
 void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
-    const dim3 grid((a.total_rows + 3) / 4);
+    const dim3 grid((a.total_rows + 3) / 4, 1, seeds_z(a.nseeds));
     if (a.H1 <= 256) hipLaunchKernelGGL(k_actor_head<4>, grid, dim3(256), 0, s, a, f);
     else hipLaunchKernelGGL(k_actor_head<8>, grid, dim3(256), 0, s, a, f);
 }
 
 // ==================================================================== k_qhead
 template <int MODE, int NQ>
-__device__ void qhead_block(const QHeadArgs& q, int block) {
+__device__ void qhead_block(const QHeadArgs& q_in, int block, int64_t so) {
     __shared__ float buf[4][512];
+    QHeadArgs q = q_in;
+    reloc(q, so);
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = block * 4 + wave;
     const int B = q.B, H1 = q.H1;
@@ -1475,11 +1551,11 @@ __device__ void qhead_block(const QHeadArgs& q, int block) {
 }
 
 template <int MODE, int NQ>
-__global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) { qhead_block<MODE, NQ>(q, blockIdx.x); }
+__global__ __launch_bounds__(256) void k_qhead(QHeadArgs q) { qhead_block<MODE, NQ>(q, blockIdx.x, seed_off(q.sstride)); }
 
 void launch_qhead(const QHeadArgs& a, hipStream_t s) {
     const int rows = a.B + (a.mode == 0 ? a.ne : 0);
-    const dim3 grid((rows + 3) / 4);
+    const dim3 grid((rows + 3) / 4, 1, seeds_z(a.nseeds));
     if (a.H1 <= 256) {
         if (a.mode == 0) hipLaunchKernelGGL((k_qhead<0, 4>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL((k_qhead<1, 4>), grid, dim3(256), 0, s, a);
@@ -1495,7 +1571,9 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 // (SURVEY.md §8a A5), then the Dense(H1 -> Aout) backward with the activation
 // derivative.  Per-column values live in lane j and are broadcast by shuffles.
 template <int NQ, int NQD>
-__device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b) {
+__device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
+    ActorBwdArgs b = b_in;
+    reloc(b, seed_off(b_in.sstride));
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = b.B, S = b.S, A = b.A;
@@ -1537,7 +1615,7 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b) {
     const __amdgpu_buffer_rsrc_t rg = rs(b.gpol);
     const float gs0 = bload(rg, boff(pol && b.gpol != nullptr, row)) + ((pol && b.gpol != nullptr) ? 0.f : 1.f);
     const float gs1 = bload(rg, boff(pol && b.gpol != nullptr, B + row)) + ((pol && b.gpol != nullptr) ? 0.f : 1.f);
-    const __amdgpu_buffer_rsrc_t rWa = rs(pol ? b.Wq1[0] : b.Wm1[km]);
+    const __amdgpu_buffer_rsrc_t rWa = rs(pol ? b.Wq1[0] : (km ? b.Wm1[1] : b.Wm1[0]));
     const __amdgpu_buffer_rsrc_t rWb = rs(b.Wq1[1]);
     const int Hb = pol ? Hd : 0;
     float ga = 0.f;
@@ -1631,7 +1709,7 @@ __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
 
 void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {
     const int rows = a.B + a.ne;
-    const dim3 grid((rows + 3) / 4);
+    const dim3 grid((rows + 3) / 4, 1, seeds_z(a.nseeds));
     const int hd = std::max(a.H0, a.use_expert ? a.Hm0 : 0);
     const bool q8 = a.H1 > 256, d8 = hd > 256;
     if (q8) {
@@ -1923,20 +2001,26 @@ void launch_roll(const RollArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_roll, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
 }
 
-__global__ void k_set_pseq(Ctl* ctl, int slot) { ctl->pseq[slot] = ctl->step_seq; }
-
-void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s) {
-    hipLaunchKernelGGL(k_set_pseq, dim3(1), dim3(1), 0, s, ctl, slot);
+__global__ void k_set_pseq(Ctl* ctl, int slot, int64_t sstride) {
+    ctl = sr(ctl, seed_off(sstride));
+    ctl->pseq[slot] = ctl->step_seq;
 }
 
-__global__ void k_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment) {
+void launch_set_pseq(Ctl* ctl, int slot, int64_t sstride, int nseeds, hipStream_t s) {
+    hipLaunchKernelGGL(k_set_pseq, dim3(1, 1, seeds_z(nseeds)), dim3(1), 0, s, ctl, slot, sstride);
+}
+
+__global__ void k_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, int64_t sstride) {
     if (threadIdx.x == 0 && blockIdx.x == 0) {
+        ctl = sr(ctl, seed_off(sstride));
         ctl->num_timesteps = num_timesteps;
         ctl->ts_increment = ts_increment;
     }
 }
-void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s) {
-    hipLaunchKernelGGL(k_set_ctl, dim3(1), dim3(64), 0, s, ctl, num_timesteps, ts_increment);
+void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, int64_t sstride, int nseeds,
+                    hipStream_t s) {
+    hipLaunchKernelGGL(k_set_ctl, dim3(1, 1, seeds_z(nseeds)), dim3(64), 0, s, ctl, num_timesteps, ts_increment,
+                       sstride);
 }
 }  // namespace sacx
 

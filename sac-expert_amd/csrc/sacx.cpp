@@ -45,7 +45,7 @@ inline int64_t r4(int64_t x) { return (x + 3) & ~int64_t(3); }
 
 struct RollKey {             // sacx_rollout graph cache key (memcmp'd: no padding holes)
     int32_t model;
-    int32_t pad0;
+    int32_t seed;             // packed seeds: the selected seed (its arena block)
     int64_t n;
     int32_t horizon, deterministic;
     float delta_clip, reward_clip;
@@ -122,6 +122,11 @@ struct sacx_handle {
     uint64_t arena_bytes = 0;
     uint64_t param_off = 0;
     int64_t p_stride = 0;  // floats
+    // packed seeds: K learners in K arena blocks seed_bytes apart; `arena` is the block of the
+    // selected seed (the per-seed calls), arena0 seed 0's (the plans: grid z covers the rest)
+    int seeds = 1, sel = 0;
+    uint64_t seed_bytes = 0;
+    char* arena0 = nullptr;
     // binding
     char* arena = nullptr;
     hipStream_t stream = nullptr;
@@ -164,6 +169,8 @@ struct sacx_handle {
     T* ptr(const std::string& n) const { return reinterpret_cast<T*>(arena + seg(n).off); }
     float* f(const std::string& n) const { return ptr<float>(n); }
     Ctl* ctl() const { return ptr<Ctl>("ctl"); }
+    Ctl* ctl0() const { return reinterpret_cast<Ctl*>(arena0 + seg("ctl").off); }
+    uint64_t total_bytes() const { return seeds > 1 ? (uint64_t)seeds * seed_bytes : arena_bytes; }
 };
 
 namespace {
@@ -462,6 +469,14 @@ bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
     a.total_tiles += b.total_tiles;
     a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec && b.vec);
     return true;
+}
+
+// Packed seeds: every launch of an update plan runs all seeds (grid z), relocating its
+// seed-0 arena pointers by blockIdx.z * seed_bytes.
+void pack_seeds(Launch& L, int64_t stride, int n) {
+    L.rng.sstride = L.gather.sstride = L.gemm.sstride = L.head.sstride = L.fin.sstride = L.qh.sstride =
+        L.ab.sstride = stride;
+    L.rng.nseeds = L.gather.nseeds = L.gemm.nseeds = L.head.nseeds = L.fin.nseeds = L.qh.nseeds = L.ab.nseeds = n;
 }
 
 // Data-parallel mode: the dW launch `L` stores its local gradients (+3 p_stride) instead of
@@ -949,6 +964,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     }
     // alpha.fwd .. alpha.final only feed the next update's q.head
     for (size_t i = alpha_first; i < plan.size(); ++i) plan[i].alpha_branch = true;
+    for (Launch& L : plan) pack_seeds(L, (int64_t)h->seed_bytes, h->seeds);
     {
     }
 }
@@ -1042,7 +1058,8 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
 bool is_prologue(const Launch& L) { return L.kind == Launch::RNG || L.kind == Launch::GATHER; }
 
 void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
-    if (!with_rng) launch_set_pseq(h->ctl(), slot, s);   // caller-provided randoms: perm of this update
+    if (!with_rng)   // caller-provided randoms: perm of this update
+        launch_set_pseq(h->ctl0(), slot, (int64_t)h->seed_bytes, h->seeds, s);
     for (const Launch& L : h->plan[slot]) {
         if (L.kind == Launch::RNG && !with_rng) continue;
         enqueue(L, h, s);
@@ -1144,9 +1161,9 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         const bool timed = kt && (L.kind == Launch::GEMM || (kt->rows && (L.kind == Launch::AHEAD || L.kind == Launch::ABWD)));
         if (timed) {
             Launch C = L;
-            const int nwg = L.kind == Launch::GEMM
-                                ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0)
-                                : (L.kind == Launch::AHEAD ? (C.head.total_rows + 3) / 4 : C.grid);
+            const int nwg = (L.kind == Launch::GEMM
+                                 ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0)
+                                 : (L.kind == Launch::AHEAD ? (C.head.total_rows + 3) / 4 : C.grid)) * h->seeds;
             if (kt->used + 2 * nwg <= kt->cap) {
                 uint64_t* p = kt->base + kt->used;
                 if (L.kind == Launch::GEMM) C.gemm.ktime = p;
@@ -1321,6 +1338,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
         return -2;
     };
     if (cfg->abi_version != SACX_ABI_VERSION) return bad("abi_version mismatch");
+    if (cfg->seeds < 0 || cfg->seeds > 64) return bad("seeds must be in [0, 64]");
     if (cfg->s_dim <= 0 || cfg->a_dim <= 0 || cfg->a_dim > 32) return bad("s_dim/a_dim out of range (a_dim <= 32)");
     if (cfg->hidden[0] <= 0 || cfg->hidden[1] <= 0) return bad("hidden sizes must be positive");
     if (cfg->hidden[0] > 512 || cfg->hidden[1] > 512) return bad("hidden sizes > 512 unsupported (row kernels hold a row in 8 regs/lane)");
@@ -1368,6 +1386,8 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
         return bad("action output > 64 unsupported");
     }
     build_layout(h);
+    h->seeds = cfg->seeds > 1 ? cfg->seeds : 1;
+    h->seed_bytes = h->seeds > 1 ? (h->arena_bytes + 65535) & ~uint64_t(65535) : h->arena_bytes;
     *out = h;
     return 0;
 }
@@ -1390,7 +1410,17 @@ const char* sacx_last_error(const sacx_handle* h) {
     return h->err.c_str();
 }
 
-int64_t sacx_arena_bytes(const sacx_handle* h) { return h ? (int64_t)h->arena_bytes : -1; }
+int64_t sacx_arena_bytes(const sacx_handle* h) { return h ? (int64_t)h->total_bytes() : -1; }
+
+int64_t sacx_seed_stride(const sacx_handle* h) { return h ? (int64_t)h->seed_bytes : -1; }
+
+int sacx_seed_select(sacx_handle* h, int32_t seed) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (seed < 0 || seed >= h->seeds) return fail(h, "seed out of range");
+    h->sel = seed;
+    h->arena = h->arena0 + (uint64_t)seed * h->seed_bytes;
+    return 0;
+}
 
 int sacx_layout(const sacx_handle* h, sacx_segment* segs, int32_t cap, int32_t* n_out) {
     if (!h || !n_out) return -1;
@@ -1411,16 +1441,19 @@ int sacx_layout(const sacx_handle* h, sacx_segment* segs, int32_t cap, int32_t* 
 
 int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (!h) return -1;
-    if (!arena || bytes < h->arena_bytes) return fail(h, "arena missing or too small");
+    if (!arena || bytes < h->total_bytes()) return fail(h, "arena missing or too small");
     if (((uintptr_t)arena) & 255) return fail(h, "arena must be 256-byte aligned");
     if (h->bound) return fail(h, "handle already bound");
-    h->arena = static_cast<char*>(arena);
+    h->arena = h->arena0 = static_cast<char*>(arena);
+    h->sel = 0;
     h->stream = static_cast<hipStream_t>(stream);
     h->probs.clear();
     {   // ws.ones: the B-row scale of unscaled dW problems
         const SegInfo& so = h->seg("ws.ones");
         std::vector<float> ones((size_t)(so.rows * so.cols), 1.0f);
-        HIPCHK(h, hipMemcpy(h->arena + so.off, ones.data(), ones.size() * sizeof(float), hipMemcpyHostToDevice));
+        for (int k = 0; k < h->seeds; ++k)
+            HIPCHK(h, hipMemcpy(h->arena0 + (uint64_t)k * h->seed_bytes + so.off, ones.data(), ones.size() * sizeof(float),
+                                hipMemcpyHostToDevice));
     }
     if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
@@ -1471,6 +1504,7 @@ int sacx_dp_init(sacx_handle* h, const void* id, int32_t nranks, int32_t rank) {
     if (!h) return -1;
     if (h->bound) return fail(h, "sacx_dp_init must precede sacx_bind");
     if (h->comm) return fail(h, "data-parallel communicator already set");
+    if (h->seeds > 1) return fail(h, "data-parallel mode needs seeds = 1");
     if (!id || nranks < 1 || rank < 0 || rank >= nranks) return fail(h, "bad data-parallel arguments");
     if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
     ncclUniqueId uid;
@@ -1566,7 +1600,7 @@ int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t*
 int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (n_steps <= 0) return 0;
-    launch_set_ctl(h->ctl(), num_timesteps, ts_increment, h->stream);
+    launch_set_ctl(h->ctl0(), num_timesteps, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
     if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
@@ -1597,6 +1631,7 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
 int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert (no world models)");
+    if (h->seeds > 1) return fail(h, "model_fit needs seeds = 1");
     if (n_steps <= 0) return 0;
     if (!idx) return fail(h, "null index array");
     const int R2 = 2 * h->mb;
@@ -1800,7 +1835,7 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
         HIPCHK(h, hipGetLastError());
         return 0;
     }
-    RollKey key{model, 0, n, horizon, deterministic, delta_clip, reward_clip, {s_init, s_out, a_out, r_out, sp_out, d_out}};
+    RollKey key{model, h->sel, n, horizon, deterministic, delta_clip, reward_clip, {s_init, s_out, a_out, r_out, sp_out, d_out}};
     hipGraphExec_t ge = nullptr;
     for (auto& kv : h->roll_graphs)
         if (std::memcmp(&kv.first, &key, sizeof(RollKey)) == 0) ge = kv.second;
@@ -1909,7 +1944,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
     if (!avg_us || n_replays <= 0) return fail(h, "bad arguments");
     const int G = h->graph_steps;
     KTimeMap kt;
-    kt.cap = (int64_t)G * 16 * 4096 * 2;               // generous: <= 16 GEMM launches x 4096 WGs per update
+    kt.cap = (int64_t)G * 16 * 4096 * 2 * h->seeds;    // generous: <= 16 GEMM launches x 4096 WGs per update
     kt.rows = std::getenv("SACX_KTIME_DUMP") != nullptr;
     HIPCHK(h, hipMalloc(&kt.base, kt.cap * sizeof(uint64_t)));
     hipGraphExec_t g = nullptr;
@@ -1933,13 +1968,16 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
             const auto& sp = kt.spans[si];
             uint64_t lo = UINT64_MAX, hi = 0, last_start = 0, wmax = 0, rmax = 0;
             double wsum = 0.0, rsum = 0.0;
-            const int rb0 = kt.rowspan[si].first, rb1 = kt.rowspan[si].second, nt = sp.second - (rb1 - rb0);
+            const int rb0 = kt.rowspan[si].first, rb1 = kt.rowspan[si].second;
+            const int nt = sp.second - (rb1 - rb0) * h->seeds;
+            const int per = sp.second / h->seeds;     // workgroups per seed (seed-major slots)
             for (int b = 0; b < sp.second; ++b) {
                 const uint64_t t0 = host[sp.first + 2 * b], t1 = host[sp.first + 2 * b + 1];
                 lo = std::min(lo, t0);
                 hi = std::max(hi, t1);
                 last_start = std::max(last_start, t0);
-                if (b < rb0 || b >= rb1) {
+                const int bx = b % per;
+                if (bx < rb0 || bx >= rb1) {
                     wmax = std::max(wmax, t1 - t0);
                     wsum += (double)(t1 - t0);
                 } else {
@@ -1955,7 +1993,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
                 std::fprintf(dump, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f,%.2f\n", kt.names[si].c_str(), sp.second,
                              (hi - lo) * 0.01, wsum / std::max(1, nt) * 0.01, wmax * 0.01, (last_start - lo) * 0.01,
                              prev_hi ? ((double)lo - (double)prev_hi) * 0.01 : 0.0,
-                             rb1 > rb0 ? rsum / (rb1 - rb0) * 0.01 : 0.0, rmax * 0.01);
+                             rb1 > rb0 ? rsum / ((rb1 - rb0) * h->seeds) * 0.01 : 0.0, rmax * 0.01);
             prev_hi = hi;
         }
         if (dump) std::fclose(dump);

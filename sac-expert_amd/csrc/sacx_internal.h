@@ -115,6 +115,10 @@ struct FinalArgs {
     // k_alpha_apply do the Adam, clamp, stats[4] and counters); null: all in place
     float* alpha_g;
     float grad_scale;       // k_alpha_apply: 1 / ranks
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 struct QHeadArgs {
@@ -144,6 +148,10 @@ struct QHeadArgs {
     const Ctl* ctl;         // epsilon
     float* Dm2;             // [ne, Hm1]
     float* mse_rows;        // [ne]
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 struct HeadSeg {
@@ -174,6 +182,10 @@ struct HeadArgs {
     int32_t alpha_mode;
     int32_t alpha_row0;
     uint64_t* ktime;        // measurement only (as GemmArgs::ktime)
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 #define GEMM_MAXP 8
@@ -204,6 +216,10 @@ struct GemmArgs {
     FinalArgs hfin;
     int32_t head_block0;
     uint64_t* ktime;       // measurement only: per-workgroup start / end ticks (nullable)
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 // ---------------------------------------------------------------- sampler + gather
@@ -218,6 +234,10 @@ struct RngArgs {
     int32_t reset_seq;     // first sampler launch of a chain: rng_seq = step_seq
     int32_t nupd;          // consecutive updates drawn by this launch (slots slot .. slot+nupd-1)
     int64_t slot_bytes;    // distance between consecutive slots' buffers
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 struct GatherArgs {
@@ -236,6 +256,10 @@ struct GatherArgs {
     float* r; float* d;
     const float* exp_s; const float* exp_sp; const int32_t* perm_ring; int32_t perm_cap;
     float* se_raw; float* spe_raw;
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 // ---------------------------------------------------------------- actor head rows
@@ -262,6 +286,10 @@ struct ActorBwdArgs {
     float* Da3; float* Da2; float* E;
     const float* gpol;      // [2, B] output gradients of q0, q1 for the policy rows (Dp1 is unscaled)
     uint64_t* ktime;        // measurement only (as GemmArgs::ktime)
+    // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
+    // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 // ---------------------------------------------------------------- finalize (alpha + stats)
@@ -350,8 +378,8 @@ void launch_append(const AppendArgs& a, hipStream_t s);
 void launch_mgather(const MGatherArgs& a, hipStream_t s);
 void launch_mloss(const MLossArgs& a, hipStream_t s);
 void launch_mfinal(const MFinalArgs& a, hipStream_t s);
-void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, hipStream_t s);
-void launch_set_pseq(Ctl* ctl, int slot, hipStream_t s);
+void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, int64_t sstride, int nseeds, hipStream_t s);
+void launch_set_pseq(Ctl* ctl, int slot, int64_t sstride, int nseeds, hipStream_t s);
 void launch_spin(double us, hipStream_t s);
 void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, const float* den, float* X, int ldX,
                      hipStream_t s);

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 2
+SACX_ABI_VERSION = 3
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1
@@ -27,7 +27,8 @@ EXPORTS = [
     "sacx_buffer_append", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
-    "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync",
+    "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
+    "sacx_seed_select",
 ]
 
 
@@ -63,6 +64,7 @@ class Config(ctypes.Structure):
         ("epsilon", ctypes.c_float),
         ("reward_loss_coef", ctypes.c_float),
         ("gemm_bf16", ctypes.c_int32),
+        ("seeds", ctypes.c_int32),
     ]
 
 
@@ -108,6 +110,8 @@ def lib():
         "sacx_destroy": (None, [vp]),
         "sacx_last_error": (ctypes.c_char_p, [vp]),
         "sacx_arena_bytes": (i64, [vp]),
+        "sacx_seed_stride": (i64, [vp]),
+        "sacx_seed_select": (i32, [vp, i32]),
         "sacx_layout": (ctypes.c_int, [vp, P(Segment), i32, P(i32)]),
         "sacx_bind": (ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
         "sacx_buffer_append": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64]),

@@ -56,6 +56,7 @@ class EngineConfig:
     epsilon: float = 1e-3
     reward_loss_coef: float = 1.0
     gemm_bf16: bool = False     # config C5: bf16 MFMA operands, fp32 accumulate / master weights
+    seeds: int = 1              # independent learners packed in one handle (one launch chain for all)
 
     def to_c(self) -> N.Config:
         c = N.Config()
@@ -84,11 +85,16 @@ class EngineConfig:
         c.epsilon = self.epsilon
         c.reward_loss_coef = self.reward_loss_coef
         c.gemm_bf16 = int(bool(self.gemm_bf16))
+        c.seeds = int(self.seeds)
         return c
 
 
 class Engine:
-    """One SAC / SAC-EO learner on one GPU (one handle, one arena)."""
+    """One SAC / SAC-EO learner on one GPU (one handle, one arena) -- or, with
+    ``cfg.seeds = K``, K independent learners (the reference's ``--runs``) packed into one
+    handle: ``step`` advances all of them in the same launches, and every per-seed method
+    (weights, normalisers, RNG, replay, stats, snapshot) addresses the seed chosen with
+    ``select_seed``."""
 
     NETS = ("actor", "q0", "q1", "t0", "t1", "m0", "m1")
 
@@ -104,24 +110,34 @@ class Engine:
         c = cfg.to_c()
         N.check(self.lib.sacx_create(ctypes.byref(c), ctypes.byref(h)), None, "sacx_create")
         self.h = h
-        nbytes = int(self.lib.sacx_arena_bytes(h))
-        self._raw = torch.zeros(nbytes + 256, dtype=torch.uint8, device=self.device)
+        total = int(self.lib.sacx_arena_bytes(h))
+        self.seeds = max(1, int(cfg.seeds))
+        self.seed_stride = int(self.lib.sacx_seed_stride(h))
+        self._raw = torch.zeros(total + 256, dtype=torch.uint8, device=self.device)
         off = (-self._raw.data_ptr()) % 256
-        self.arena = self._raw[off: off + nbytes]
-        self.nbytes = nbytes
+        self.arena_all = self._raw[off: off + total]
         n = ctypes.c_int32()
         self.lib.sacx_layout(h, None, 0, ctypes.byref(n))
         segs = (N.Segment * n.value)()
         self.lib.sacx_layout(h, segs, n.value, ctypes.byref(n))
         self.segments: Dict[str, dict] = {}
-        self.v: Dict[str, torch.Tensor] = {}
         for s in segs:
-            name = s.name.decode()
-            nb = int(s.rows * s.cols * _ESZ[s.dtype])
-            t = self.arena[s.offset: s.offset + nb].view(_TORCH_DT[s.dtype]).view(int(s.rows), int(s.cols))
-            self.segments[name] = dict(offset=int(s.offset), rows=int(s.rows), cols=int(s.cols),
-                                       dtype=N.DTYPES[s.dtype], role=int(s.role))
-            self.v[name] = t
+            self.segments[s.name.decode()] = dict(offset=int(s.offset), rows=int(s.rows), cols=int(s.cols),
+                                                  dtype=N.DTYPES[s.dtype], role=int(s.role), code=int(s.dtype))
+        # per seed: its arena block and the named views into it
+        self.nbytes = total if self.seeds == 1 else self.seed_stride
+        self._arenas, self._views = [], []
+        for k in range(self.seeds):
+            a = self.arena_all[k * self.seed_stride: k * self.seed_stride + self.nbytes]
+            views = {}
+            for name, d in self.segments.items():
+                nb = d["rows"] * d["cols"] * _ESZ[d["code"]]
+                views[name] = a[d["offset"]: d["offset"] + nb].view(_TORCH_DT[d["code"]]).view(d["rows"], d["cols"])
+            self._arenas.append(a)
+            self._views.append(views)
+        self.seed_index = 0
+        self.arena = self._arenas[0]
+        self.v: Dict[str, torch.Tensor] = self._views[0]
         with torch.cuda.device(self.device):
             self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
             if dp is not None:
@@ -129,9 +145,20 @@ class Engine:
                 buf = ctypes.create_string_buffer(bytes(uid), len(uid))
                 N.check(self.lib.sacx_dp_init(h, buf, int(nranks), int(rank)), h, "sacx_dp_init")
         self.dp = dp
-        N.check(self.lib.sacx_bind(h, ctypes.c_void_p(self.arena.data_ptr()), nbytes,
+        N.check(self.lib.sacx_bind(h, ctypes.c_void_p(self.arena_all.data_ptr()), total,
                                    ctypes.c_void_p(self.stream.cuda_stream)), h, "sacx_bind")
-        self._init_state()
+        for k in range(self.seeds):
+            self.select_seed(k)
+            self._init_state()
+        self.select_seed(0)
+
+    def select_seed(self, k: int):
+        """Packed seeds: the seed the per-seed methods (and libsacx's per-seed calls) address."""
+        k = int(k)
+        N.check(self.lib.sacx_seed_select(self.h, k), self.h, "seed_select")
+        self.seed_index = k
+        self.arena = self._arenas[k]
+        self.v = self._views[k]
 
     @staticmethod
     def dp_unique_id() -> bytes:

@@ -28,11 +28,10 @@ def nontrivial_normalizers(rs, S, A):
         0.0, 1.0, 1.0)
 
 
-def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
-              use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
-              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False):
-    """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
-    from sac_eo.engine import Engine, EngineConfig
+def make_learner(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
+                 use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
+                 bias_scale=0.05, actor_gain=0.5, epsilon=0.1):
+    """The seeded inputs of one learner: (oracle_cfg, oracle_state_f32, buffer, normalizers, expert)."""
     ocfg = O.Config(S=S, A=A, hidden=hidden, act=act, B=B, per_state_std=per_state_std,
                     model_hidden=model_hidden, epsilon=epsilon)
     st = O.init_state(ocfg, seed=seed + 1, with_models=use_expert, bias_scale=bias_scale,
@@ -40,30 +39,46 @@ def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, p
     rs = np.random.RandomState(seed + 100)
     buf = synthetic_buffer(rs, N, S, A, done_p)
     nrm = O.Normalizers.identity(S, A) if normalizers == "identity" else nontrivial_normalizers(rs, S, A)
-    ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
-                        per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
-                        expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon,
-                        gemm_bf16=gemm_bf16)
-    eng = Engine(ecfg, dp=dp)
-    eng.set_net("actor", st.actor)
-    eng.set_logstd(st.logstd)
-    for k in range(2):
-        eng.set_net(f"q{k}", st.q[k])
-        eng.set_net(f"t{k}", st.q_targ[k])
-    if use_expert:
-        for k in range(2):
-            eng.set_net(f"m{k}", st.models[k])
-    eng.set_alpha(float(st.alpha))
-    eng.set_normalizers(nrm.s_mean, nrm.s_den, nrm.a_mean, nrm.a_den, nrm.d_mean, nrm.d_den,
-                        nrm.r_mean, nrm.r_den, nrm.ret_den)
-    eng.append(buf["s"], buf["a"], buf["r"], buf["sp"], buf["d"].astype(np.float32))
     expert = None
     if use_expert:
         ers = np.random.RandomState(seed + 200)
         sig = ers.uniform(0.1, 5.0, size=S)
         expert = dict(s=(ers.normal(size=(ne, S)) * sig).astype(np.float32),
                       sp=(ers.normal(size=(ne, S)) * sig).astype(np.float32))
+    return ocfg, st, buf, nrm, expert
+
+
+def load_learner(eng, st, buf, nrm, expert, epsilon):
+    """Writes one learner's state into the engine's selected seed."""
+    eng.set_net("actor", st.actor)
+    eng.set_logstd(st.logstd)
+    for k in range(2):
+        eng.set_net(f"q{k}", st.q[k])
+        eng.set_net(f"t{k}", st.q_targ[k])
+    if expert is not None:
+        for k in range(2):
+            eng.set_net(f"m{k}", st.models[k])
+    eng.set_alpha(float(st.alpha))
+    eng.set_normalizers(nrm.s_mean, nrm.s_den, nrm.a_mean, nrm.a_den, nrm.d_mean, nrm.d_den,
+                        nrm.r_mean, nrm.r_den, nrm.ret_den)
+    eng.append(buf["s"], buf["a"], buf["r"], buf["sp"], buf["d"].astype(np.float32))
+    if expert is not None:
         eng.set_expert(expert["s"], expert["sp"], epsilon)
+
+
+def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
+              use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
+              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False):
+    """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
+    from sac_eo.engine import Engine, EngineConfig
+    ocfg, st, buf, nrm, expert = make_learner(S, A, hidden, B, act, N, seed, per_state_std, use_expert, ne,
+                                              model_hidden, normalizers, done_p, bias_scale, actor_gain, epsilon)
+    ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
+                        per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
+                        expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon,
+                        gemm_bf16=gemm_bf16)
+    eng = Engine(ecfg, dp=dp)
+    load_learner(eng, st, buf, nrm, expert, epsilon)
     return eng, ocfg, st.astype(np.float64), buf, nrm, expert
 
 

@@ -29,9 +29,10 @@ def test_struct_layouts():
     from sac_eo import _native as N
     # offsets fixed by include/sacx.h (natural alignment)
     assert N.Config.buffer_capacity.offset == 32
-    assert ctypes.sizeof(N.Config) == 136          # gcc: sizeof(sacx_config)
+    assert ctypes.sizeof(N.Config) == 144          # gcc: sizeof(sacx_config)
     assert N.Config.reward_loss_coef.offset == 128
     assert N.Config.gemm_bf16.offset == 132
+    assert N.Config.seeds.offset == 136
     assert ctypes.sizeof(N.Segment) == 48 + 8 + 8 + 8 + 4 + 4
     assert ctypes.sizeof(N.LaunchInfo) == 32 + 32 + 4 + 4 + 8 + 8
 
@@ -58,3 +59,27 @@ def test_create_validates_without_gpu():
     bad = EngineConfig(s_dim=17, a_dim=6, use_expert=True, expert_batch=7).to_c()
     assert L.sacx_create(ctypes.byref(bad), ctypes.byref(h)) != 0
     assert b"even" in L.sacx_last_error(None)
+
+
+def test_packed_seed_layout_without_gpu():
+    """cfg.seeds = K: K arena blocks of one seed's layout, 64 KiB-aligned stride."""
+    from sac_eo import _native as N
+    from sac_eo.engine import EngineConfig
+    L = N.lib()
+    h1, h3 = ctypes.c_void_p(), ctypes.c_void_p()
+    c1 = EngineConfig(s_dim=17, a_dim=6, buffer_capacity=10_000).to_c()
+    c3 = EngineConfig(s_dim=17, a_dim=6, buffer_capacity=10_000, seeds=3).to_c()
+    assert L.sacx_create(ctypes.byref(c1), ctypes.byref(h1)) == 0
+    assert L.sacx_create(ctypes.byref(c3), ctypes.byref(h3)) == 0
+    one = L.sacx_arena_bytes(h1)
+    assert L.sacx_seed_stride(h1) == one
+    st = L.sacx_seed_stride(h3)
+    assert st % 65536 == 0 and one <= st < one + 65536
+    assert L.sacx_arena_bytes(h3) == 3 * st
+    # seed selection needs a bound arena
+    assert L.sacx_seed_select(h3, 1) != 0
+    L.sacx_destroy(h1)
+    L.sacx_destroy(h3)
+    bad = EngineConfig(s_dim=17, a_dim=6, seeds=65).to_c()
+    assert L.sacx_create(ctypes.byref(bad), ctypes.byref(h1)) != 0
+    assert b"seeds" in L.sacx_last_error(None)

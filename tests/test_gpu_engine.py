@@ -11,7 +11,7 @@ import numpy as np
 import pytest
 
 import sac_oracle as O
-from helpers import B1, make_pair, oracle_step, relerr
+from helpers import B1, load_learner, make_learner, make_pair, oracle_step, relerr
 
 pytestmark = pytest.mark.gpu
 
@@ -462,3 +462,53 @@ def test_rollout_graph_replay_equals_eager(gpu_available, monkeypatch):
             assert np.array_equal(x, y)
         assert np.array_equal(outs[0][1][1], stt[1]) and outs[0][1][2] == stt[2]
     eng.close()
+
+
+@pytest.mark.parametrize("use_expert,eager", [(False, False), (True, False), (False, True)])
+def test_packed_seeds_equal_single(gpu_available, use_expert, eager):
+    """cfg.seeds = 3 (the reference's --runs packed into one handle, grid z = seed): every
+    seed ends bit-identical to a one-seed engine fed the same state, buffer, RNG stream and
+    permutations -- stats, every parameter / Adam / target value, and the RNG key.  19
+    updates = two 8-update graphs + remainder graphs."""
+    from sac_eo.engine import Engine, EngineConfig
+    K, n, B, N, eps = 3, 19, 128, 3000, 0.1
+    learners = [make_learner(act="tanh", B=B, N=N, seed=40 + 7 * k, use_expert=use_expert, epsilon=eps)
+                for k in range(K)]
+
+    def cfg(seeds):
+        return EngineConfig(s_dim=17, a_dim=6, activation="tanh", batch=B, buffer_capacity=N, use_expert=use_expert,
+                            expert_capacity=20, expert_batch=20, graph_steps=8, epsilon=eps, seeds=seeds)
+
+    def drive(eng, k):
+        _, st, buf, nrm, ex = learners[k]
+        load_learner(eng, st, buf, nrm, ex, eps)
+        eng.rng_set_state(np.random.RandomState(500 + k).get_state())
+        if use_expert:
+            rs = np.random.RandomState(900 + k)
+            eng.push_perms(np.stack([rs.permutation(20) for _ in range(n)]))
+
+    packed = Engine(cfg(K))
+    for k in range(K):
+        packed.select_seed(k)
+        drive(packed, k)
+    packed.select_seed(0)
+    packed.step(n, eager=eager)
+    packed.sync()
+    got = []
+    for k in range(K):
+        packed.select_seed(k)
+        got.append((packed.stats(n).copy(), packed.v["params"].cpu().numpy().copy(),
+                    packed.v["adam_v"].cpu().numpy().copy(), packed.rng_get_state()[1].copy()))
+    packed.close()
+    for k in range(K):
+        e = Engine(cfg(1))
+        drive(e, k)
+        e.step(n, eager=eager)
+        e.sync()
+        ref = (e.stats(n), e.v["params"].cpu().numpy(), e.v["adam_v"].cpu().numpy(), e.rng_get_state()[1])
+        e.close()
+        for i, (a, b) in enumerate(zip(got[k], ref)):
+            assert np.array_equal(a, b), (k, i)
+    assert np.all(np.isfinite(got[0][0]))
+    assert not np.array_equal(got[0][1], got[1][1])     # the seeds are different learners
+
