@@ -11,6 +11,12 @@ learner with its own seed -- the reference's ``--runs N`` spawn-pool
 parallelism (train.py:118-152).  No data-path collective; ``value`` is the
 sum of steps over ranks divided by the max-over-ranks wall time (weak scaling).
 
+Packed seeds: ``--seeds-per-gpu K`` packs K independent learners into each
+GPU's handle for the timed region (cfg.seeds = K: every launch of the update
+graph runs all K, grid z = seed) and ``value`` counts every seed's updates.
+The default keeps one learner per GPU and adds a ``packed_seeds`` leg (8 seeds
+per GPU for hc) measured after the timed region.
+
 Extra JSON fields: ``roofline`` for the dominant kernel (HIP-event timed in
 this process) and ``cpu_baseline`` (the CPU oracle port on the host cores,
 rank 0 at N=1, bounded sample).
@@ -233,6 +239,55 @@ def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):
              "transitions_per_s": round(5000 / roll_s, 1), "launches_per_step": 9, "graph": True})
 
 
+def replica_seeds(rep, k):
+    """The reference-style seeds of this replica's k learners: run indices rank*k .. rank*k+k-1
+    of derive_seeds (sac_eo/train.py:108-118), one dict per learner."""
+    from sac_eo.common.seeding import derive_seeds
+    if k <= 1:
+        return rep.seeds(0)
+    ds = derive_seeds(0, runs=rep.world_size * k)
+    return [{n: int(v[rep.rank * k + j]) for n, v in ds.items()} for j in range(k)]
+
+
+def packed_leg(cfgd, config, rep, k, steps, with_roofline):
+    """K independent learners packed into one handle per GPU (cfg.seeds = K: every launch of the
+    update graph runs all K, grid z = seed): whole-job updates/s over all seeds and GPUs, timed
+    like the main region (barrier + synchronize, max over ranks).  The k_gemm roofline of the
+    packed chain counts the K seeds' FLOPs per launch."""
+    eng = build_engine(cfgd, replica_seeds(rep, k), device=rep.device)
+    eng.step(256)
+    eng.sync()
+    rep.barrier()
+    t0 = time.perf_counter()
+    eng.step(steps)
+    eng.sync()
+    t1 = time.perf_counter()
+    rep.barrier()
+    el = rep.max_over_ranks(t1 - t0)
+    finite = True
+    for j in range(k):
+        eng.select_seed(j)
+        finite = finite and bool(np.all(np.isfinite(eng.stats(1)[0])))
+    eng.select_seed(0)
+    out = {"seeds_per_gpu": k, "value": round(steps * k * rep.world_size / el, 2), "unit": "gradient-steps/s",
+           "per_seed": round(steps / el, 2), "ms_per_round": round(el / steps * 1e3, 5), "steps": steps,
+           "finite_stats": finite,
+           "note": "independent learners (the reference's --runs) packed into one handle per GPU"}
+    if with_roofline:
+        peak = BF16_PEAK_TFLOPS if cfgd.get("bf16") else FP32_PEAK_TFLOPS
+        info = eng.plan_info()
+        flops = sum(L["flops"] for L in info if L["kernel"] == "k_gemm")     # one seed, per update
+        avg_us, _, n_graph = eng.time_kernels("k_gemm", 3)
+        fpl = k * flops / (n_graph / eng.cfg.graph_steps)
+        out["roofline"] = {"kernel": "k_gemm", "bound": "mfma", "achieved": round(fpl / (avg_us * 1e-6) / 1e12, 3),
+                           "peak": peak, "unit": "TFLOP/s",
+                           "frac": round(fpl / (avg_us * 1e-6) / 1e12 / peak, 5), "avg_launch_us": round(avg_us, 3),
+                           "flops_per_launch": fpl,
+                           "timing": "per-workgroup device timestamps in a replay of the packed update graph"}
+    eng.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -245,6 +300,12 @@ def main():
     ap.add_argument("--mode", default="replicas", choices=["replicas", "dp"],
                     help="replicas: one independent learner per GPU (the metric); dp: one learner, "
                          "global batch split over the GPUs, gradients all-reduced by RCCL (config C4)")
+    ap.add_argument("--seeds-per-gpu", type=int, default=1,
+                    help="independent learners packed into each GPU's handle for the timed region "
+                         "(one launch chain, grid z = seed); value counts the updates of every seed")
+    ap.add_argument("--packed-leg", type=int, default=-1,
+                    help="after the timed region, also time K packed seeds per GPU and report them as "
+                         "packed_seeds (default 8 for hc, 4 for the Humanoid configs; 0 = off)")
     args = ap.parse_args()
 
     import torch
@@ -262,7 +323,8 @@ def main():
         eng = build_engine(cfgd, rep.seeds(0), device=device, dp=(uid, ws, rank), batch=cfgd["B"] // ws,
                            weight_seed=int(derive_seeds(0, runs=1)["setup"][0]))
     else:
-        eng = build_engine(cfgd, rep.seeds(0), device=device)
+        eng = build_engine(cfgd, replica_seeds(rep, args.seeds_per_gpu), device=device)
+    K = 1 if dp else max(1, args.seeds_per_gpu)
     barrier = rep.barrier
 
     eng.step(args.warmup, num_timesteps=0, ts_increment=1)
@@ -276,13 +338,19 @@ def main():
     el = rep.max_over_ranks(t1 - t0)
     stats = eng.stats(1)[0]
     finite = bool(np.all(np.isfinite(stats)))
-    value = args.steps * (1 if dp else ws) / el     # dp: every rank runs the same global update
+    value = args.steps * (1 if dp else ws * K) / el     # dp: every rank runs the same global update
     roof = None
     if rank == 0 and not args.no_roofline and not dp:
         roof, _ = roofline(eng, args.config)
     fit = roll = None
-    if rank == 0 and cfgd["use_expert"]:
+    if rank == 0 and cfgd["use_expert"] and K == 1:
         fit, roll = world_model_legs(eng, cfgd)
+    packed = None
+    nleg = args.packed_leg if args.packed_leg >= 0 else (8 if args.config == "hc" else 4)
+    if not dp and K == 1 and nleg > 1:
+        eng.close()
+        eng = None
+        packed = packed_leg(cfgd, args.config, rep, nleg, min(args.steps, 1024), rank == 0 and not args.no_roofline)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not dp:
         cpu = cpu_baseline(cfgd, args.cpu_seconds)
@@ -300,7 +368,9 @@ def main():
                        "batch": cfgd["B"], "hidden": list(cfgd["hidden"]), "buffer_rows": cfgd["buffer"],
                        "parallelism": (f"dp{ws}: one learner, batch {cfgd['B'] // ws} per GPU, 3 RCCL all-reduces "
                                        "per update (critic, actor, alpha gradients)") if dp else
-                                      f"replicas x{ws} (independent seeds, no collective)",
+                                      (f"replicas x{ws} (independent seeds, no collective)" if K == 1 else
+                                       f"replicas x{ws} x {K} packed seeds per GPU (independent seeds, no collective)"),
+                       "seeds_per_gpu": K,
                        "sampler": "NumPy-legacy MT19937 stream on device (bit-exact indices)"},
             "finite_stats": finite,
             "last_stats": {k: float(v) for k, v in zip(
@@ -309,8 +379,11 @@ def main():
         }
         if fit is not None:
             line["model_fit"], line["rollout"] = fit, roll
+        if packed is not None:
+            line["packed_seeds"] = packed
         print(json.dumps(line), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     rep.close()
 
 

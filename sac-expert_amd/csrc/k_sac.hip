@@ -464,9 +464,9 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 // MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
-__device__ void qhead_block(const QHeadArgs& q, int block, int64_t so);
+__device__ __forceinline__ void qhead_block(const QHeadArgs& q, int block, int64_t so);
 template <int NQ>
-__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so);
+__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so);
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
 // so blocks b and b+8 share an L2.  xcd_tile gives the blocks of one XCD a contiguous range of
@@ -567,12 +567,13 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
     __syncthreads();
 }
 
-template <int MODE, int VEC, int ROWK, int NQ, bool BF = false>
+template <int MODE, int VEC, int ROWK, int NQ, bool BF = false, bool PK = false>
 __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[4][4][64];
-    const int64_t so = seed_off(ga.sstride);
+    // PK: packed seeds (nseeds > 1); a one-seed launch compiles the relocation away (so = 0)
+    const int64_t so = PK ? seed_off(ga.sstride) : 0;
     // the folded alpha.final of the previous update is workgroup 0: dispatched first, its
     // serial reductions overlap the tiles instead of trailing them
     int tile = (int)blockIdx.x - (ga.has_final ? 1 : 0);
@@ -831,10 +832,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 
 // ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
 // (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
-template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false>
+template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    gemm_core<MODE, VEC, ROWK, NQ, BF>(ga);
+    gemm_core<MODE, VEC, ROWK, NQ, BF, PK>(ga);
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -846,10 +847,10 @@ __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
 
 // q.fwd0 with the actor head folded in: 1,024 tiles + 128 head-row workgroups must be
 // resident at once (5 workgroups per CU), so registers are capped at 96 per lane
-template <int VEC, int NQ, bool BF>
+template <int VEC, int NQ, bool BF, bool PK = false>
 __global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    gemm_core<GM_FWD, VEC, 3, NQ, BF>(ga);
+    gemm_core<GM_FWD, VEC, 3, NQ, BF, PK>(ga);
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -859,7 +860,8 @@ __global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
     }
 }
 
-void launch_gemm(const GemmArgs& a, hipStream_t s) {
+template <bool PK>
+static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     const unsigned z = seeds_z(a.nseeds);
     const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0), 1, z), block(256);
     switch (a.mode) {
@@ -869,18 +871,18 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
             const bool h8 = a.head.H1 > 256;
 #define SACX_FH(V, Q)                                                                               \
     do {                                                                                           \
-        if (a.bf16) hipLaunchKernelGGL((k_gemm_head<V, Q, true>), gh, block, 0, s, a);              \
-        else hipLaunchKernelGGL((k_gemm_head<V, Q, false>), gh, block, 0, s, a);                   \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm_head<V, Q, true, PK>), gh, block, 0, s, a);              \
+        else hipLaunchKernelGGL((k_gemm_head<V, Q, false, PK>), gh, block, 0, s, a);                   \
     } while (0)
             if (a.vec) { if (h8) SACX_FH(1, 8); else SACX_FH(1, 4); }
             else { if (h8) SACX_FH(0, 8); else SACX_FH(0, 4); }
 #undef SACX_FH
         } else if (a.bf16) {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true>), grid, block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK>), grid, block, 0, s, a);
         } else {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0>), grid, block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, false, PK>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, false, PK>), grid, block, 0, s, a);
         }
         break;
     case GM_DX: {
@@ -888,8 +890,8 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         const bool q8 = a.rowk && a.qh.H1 > 256;
 #define SACX_DX(V, R, Q)                                                                            \
     do {                                                                                           \
-        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true>), gx, block, 0, s, a);          \
-        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q>), gx, block, 0, s, a);                      \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK>), gx, block, 0, s, a);          \
+        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK>), gx, block, 0, s, a);                      \
     } while (0)
         if (a.rowk == 1) {
             if (a.vec) { if (q8) SACX_DX(1, 1, 8); else SACX_DX(1, 1, 4); }
@@ -906,14 +908,14 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
     }
     case GM_FWD2:
         switch (a.vec) {
-        case 2: hipLaunchKernelGGL((k_gemm<GM_FWD2, 2>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_gemm<GM_FWD2, 4>), grid, block, 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_gemm<GM_FWD2, 6>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((k_gemm<GM_FWD2, 8>), grid, block, 0, s, a); break;
-        case 10: hipLaunchKernelGGL((k_gemm<GM_FWD2, 10>), grid, block, 0, s, a); break;
-        case 12: hipLaunchKernelGGL((k_gemm<GM_FWD2, 12>), grid, block, 0, s, a); break;
-        case 14: hipLaunchKernelGGL((k_gemm<GM_FWD2, 14>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((k_gemm<GM_FWD2, 16>), grid, block, 0, s, a); break;
+        case 2: hipLaunchKernelGGL((k_gemm<GM_FWD2, 2, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        case 4: hipLaunchKernelGGL((k_gemm<GM_FWD2, 4, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        case 6: hipLaunchKernelGGL((k_gemm<GM_FWD2, 6, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        case 8: hipLaunchKernelGGL((k_gemm<GM_FWD2, 8, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        case 10: hipLaunchKernelGGL((k_gemm<GM_FWD2, 10, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        case 12: hipLaunchKernelGGL((k_gemm<GM_FWD2, 12, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        case 14: hipLaunchKernelGGL((k_gemm<GM_FWD2, 14, 0, 4, false, PK>), grid, block, 0, s, a); break;
+        default: hipLaunchKernelGGL((k_gemm<GM_FWD2, 16, 0, 4, false, PK>), grid, block, 0, s, a); break;
         }
         break;
     default:
@@ -921,18 +923,23 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
             const dim3 gh(a.total_tiles + a.row_blocks, 1, z);
             const bool h8 = a.head.H1 > 256;
             if (a.bf16) {
-                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true>), gh, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true>), gh, block, 0, s, a);
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true, PK>), gh, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true, PK>), gh, block, 0, s, a);
             } else {
-                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8>), gh, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4>), gh, block, 0, s, a);
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, false, PK>), gh, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, false, PK>), gh, block, 0, s, a);
             }
         } else if (a.bf16) {
-            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true, PK>), grid, block, 0, s, a);
         } else {
-            hipLaunchKernelGGL((k_gemm<GM_DW, 0>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, false, PK>), grid, block, 0, s, a);
         }
     }
+}
+
+void launch_gemm(const GemmArgs& a, hipStream_t s) {
+    if (a.nseeds > 1) launch_gemm_t<true>(a, s);
+    else launch_gemm_t<false>(a, s);
 }
 
 // ==================================================================== k_rng
@@ -1306,7 +1313,7 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
 template <int NQ>
-__device__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
+__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
     __shared__ float red_s[4];
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = block * 4 + wave;
@@ -1396,22 +1403,28 @@ __device__ __forceinline__ void ktime_stamp(uint64_t* kt, uint64_t t0) {
     }
 }
 
-template <int NQ>
+template <int NQ, bool PK>
 __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    actor_head_body<NQ>(h, f, (int)blockIdx.x, seed_off(h.sstride));
+    actor_head_body<NQ>(h, f, (int)blockIdx.x, PK ? seed_off(h.sstride) : 0);
     ktime_stamp(h.ktime, t0);
 }
 
 void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
     const dim3 grid((a.total_rows + 3) / 4, 1, seeds_z(a.nseeds));
-    if (a.H1 <= 256) hipLaunchKernelGGL(k_actor_head<4>, grid, dim3(256), 0, s, a, f);
-    else hipLaunchKernelGGL(k_actor_head<8>, grid, dim3(256), 0, s, a, f);
+    const bool pk = a.nseeds > 1;
+    if (a.H1 <= 256) {
+        if (pk) hipLaunchKernelGGL((k_actor_head<4, true>), grid, dim3(256), 0, s, a, f);
+        else hipLaunchKernelGGL((k_actor_head<4, false>), grid, dim3(256), 0, s, a, f);
+    } else {
+        if (pk) hipLaunchKernelGGL((k_actor_head<8, true>), grid, dim3(256), 0, s, a, f);
+        else hipLaunchKernelGGL((k_actor_head<8, false>), grid, dim3(256), 0, s, a, f);
+    }
 }
 
 // ==================================================================== k_qhead
 template <int MODE, int NQ>
-__device__ void qhead_block(const QHeadArgs& q_in, int block, int64_t so) {
+__device__ __forceinline__ void qhead_block(const QHeadArgs& q_in, int block, int64_t so) {
     __shared__ float buf[4][512];
     QHeadArgs q = q_in;
     reloc(q, so);
@@ -1570,10 +1583,10 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 // rows) or world-model (expert rows) input columns, tanh-Gaussian backward
 // (SURVEY.md §8a A5), then the Dense(H1 -> Aout) backward with the activation
 // derivative.  Per-column values live in lane j and are broadcast by shuffles.
-template <int NQ, int NQD>
+template <int NQ, int NQD, bool PK>
 __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     ActorBwdArgs b = b_in;
-    reloc(b, seed_off(b_in.sstride));
+    if constexpr (PK) reloc(b, seed_off(b_in.sstride));
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = b.B, S = b.S, A = b.A;
@@ -1700,10 +1713,10 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     }
 }
 
-template <int NQ, int NQD>
+template <int NQ, int NQD, bool PK>
 __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    actor_bwd_body<NQ, NQD>(b);
+    actor_bwd_body<NQ, NQD, PK>(b);
     ktime_stamp(b.ktime, t0);
 }
 
@@ -1712,13 +1725,19 @@ void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {
     const dim3 grid((rows + 3) / 4, 1, seeds_z(a.nseeds));
     const int hd = std::max(a.H0, a.use_expert ? a.Hm0 : 0);
     const bool q8 = a.H1 > 256, d8 = hd > 256;
+#define SACX_AB(Q, D)                                                                              \
+    do {                                                                                           \
+        if (a.nseeds > 1) hipLaunchKernelGGL((k_actor_bwd<Q, D, true>), grid, dim3(256), 0, s, a);   \
+        else hipLaunchKernelGGL((k_actor_bwd<Q, D, false>), grid, dim3(256), 0, s, a);              \
+    } while (0)
     if (q8) {
-        if (d8) hipLaunchKernelGGL((k_actor_bwd<8, 8>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_actor_bwd<8, 4>), grid, dim3(256), 0, s, a);
+        if (d8) SACX_AB(8, 8);
+        else SACX_AB(8, 4);
     } else {
-        if (d8) hipLaunchKernelGGL((k_actor_bwd<4, 8>), grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL((k_actor_bwd<4, 4>), grid, dim3(256), 0, s, a);
+        if (d8) SACX_AB(4, 8);
+        else SACX_AB(4, 4);
     }
+#undef SACX_AB
 }
 
 // ==================================================================== k_append
