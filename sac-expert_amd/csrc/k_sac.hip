@@ -567,11 +567,166 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
     __syncthreads();
 }
 
-template <int MODE, int VEC, int ROWK, int NQ, bool BF = false, bool PK = false>
+// 32x32 output tiles (T32, launches with many tiles: packed seeds).  A workgroup owns a 2x2
+// block of 16x16 MFMA tiles and each wave computes all four over its quarter of K, so a
+// workgroup does 4x the MFMA work of a 16x16 one for 2x the operand loads, and a launch has a
+// quarter of the workgroups.  Every 16x16 sub-tile accumulates exactly as gemm_core's 16x16
+// path does (same k order, same acc0 / acc1 split, same 4-wave reduction order, same
+// epilogue), so both tilings give bit-identical results.
+template <int MODE, int VEC, bool BF>
+__device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
+                                            float (&red)[16][4][64]) {
+    constexpr bool AKC = (MODE != GM_DW);
+    constexpr bool BKC = (MODE == GM_DX);
+    const int tm = lt / g.tiles_n;          // tiles_n counts 32-wide column tiles here
+    const int tn = lt - tm * g.tiles_n;
+    const int m0 = tm * 32, n0 = tn * 32;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int r = lane & 15, grp = lane >> 4;
+    const int t = threadIdx.x, row = t >> 4, col = t & 15;
+
+    // ---- epilogue operands of this thread's four outputs (sub-tile s = 2 i + j: rows +16 i, cols +16 j)
+    float e0[4], e1[4], e2[4], e3[4], e4[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int mm = m0 + 16 * (s >> 1) + row, nn = n0 + 16 * (s & 1) + col;
+        const int mmc = min(mm, g.M - 1), nnc = min(nn, g.N - 1);
+        const size_t pidx = (size_t)mmc * g.ldp + nnc;
+        e0[s] = e1[s] = e2[s] = e3[s] = e4[s] = 0.f;
+        if constexpr (MODE == GM_FWD) {
+            e0[s] = g.bias[nnc];
+            e1[s] = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
+            e2[s] = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
+            e3[s] = bload(rs(g.dmean), boff(g.mse != 0, nnc));
+            e4[s] = bload(rs(g.dden), boff(g.mse != 0, nnc));
+        } else if constexpr (MODE == GM_DX) {
+            e0[s] = g.H[(size_t)mmc * g.ldh + nnc];
+        } else {
+            e0[s] = g.P[pidx];
+            e1[s] = g.P[pidx + ga.p_stride];
+            e2[s] = g.P[pidx + 2 * ga.p_stride];
+            e3[s] = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
+        }
+    }
+
+    const int nIt = (g.K + 15) >> 4;
+    const int per = (nIt + 3) >> 2;
+    const int it0 = wave * per;
+    const int it1 = min(nIt, it0 + per);
+    const int ma = m0 + r, mb = m0 + 16 + r, na = n0 + r, nb = n0 + 16 + r;
+    const bool maok = ma < g.M, mbok = mb < g.M, naok = na < g.N, nbok = nb < g.N;
+    const __amdgpu_buffer_rsrc_t ra = make_rsrc(g.A, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rb = make_rsrc(g.B, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rw = rs(g.wgen);
+    floatx4 acc0[4], acc1[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        acc0[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+        acc1[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    for (int it = it0; it < it1; it += 4) {
+        float a[4][2][4], b[4][2][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k0 = (it + u) * 16 + grp * 4;
+            const int k0e = (it + u < it1) ? k0 : (1 << 30);
+            load_a<AKC, VEC && AKC, MODE == GM_DX>(ra, g, ma, maok, k0e, a[u][0], rw);
+            load_a<AKC, VEC && AKC, MODE == GM_DX>(ra, g, mb, mbok, k0e, a[u][1], rw);
+            load_b<BKC, VEC && BKC, MODE == GM_DW>(rb, g, na, naok, k0e, b[u][0]);
+            load_b<BKC, VEC && BKC, MODE == GM_DW>(rb, g, nb, nbok, k0e, b[u][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if constexpr (BF) {
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    const float (&av)[4] = a[u][s >> 1];
+                    const float (&bv)[4] = b[u][s & 1];
+                    const shortx4 as = {bf16_bits(av[0]), bf16_bits(av[1]), bf16_bits(av[2]), bf16_bits(av[3])};
+                    const shortx4 bs = {bf16_bits(bv[0]), bf16_bits(bv[1]), bf16_bits(bv[2]), bf16_bits(bv[3])};
+                    if (u & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc1[s], 0, 0, 0);
+                    else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc0[s], 0, 0, 0);
+                }
+                continue;
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int s = 0; s < 4; ++s) {
+                    if (j & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][s >> 1][j], b[u][s & 1][j], acc1[s], 0, 0, 0);
+                    else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][s >> 1][j], b[u][s & 1][j], acc0[s], 0, 0, 0);
+                }
+        }
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const floatx4 acc = acc0[s] + acc1[s];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[wave * 4 + s][q][lane] = acc[q];
+    }
+    __syncthreads();
+
+    const int L = ((row >> 2) << 4) | col, R = row & 3;
+    const Ctl* ctl = sr(ga.ctl, so);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        float v = red[s][R][L] + red[4 + s][R][L];
+        v = v + red[8 + s][R][L];
+        v = v + red[12 + s][R][L];
+        const int mm = m0 + 16 * (s >> 1) + row, nn = n0 + 16 * (s & 1) + col;
+        const bool out_ok = (mm < g.M) && (nn < g.N);
+        const int mmc = min(mm, g.M - 1), nnc = min(nn, g.N - 1);
+        const size_t pidx = (size_t)mmc * g.ldp + nnc;
+        if constexpr (MODE == GM_FWD) {
+            if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
+                const float pred = v + e0[s];
+                const float sp_hat = e1[s] + (pred * e4[s] + e3[s]);
+                const float diff = e2[s] - sp_hat;
+                const float gscale = -ctl->epsilon * g.grad_scale;
+                float sq = out_ok ? diff * diff : 0.f;
+                sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's sub-tile row
+                sq += __shfl_xor(sq, 4, 16);
+                sq += __shfl_xor(sq, 2, 16);
+                sq += __shfl_xor(sq, 1, 16);
+                if (out_ok) {
+                    st_out(&g.C[(size_t)mm * g.ldc + nn], (gscale * diff) * e4[s]);
+                    if (col == 0) st_out(&g.part[(size_t)mm * ((g.N + 15) >> 4) + 2 * tn + (s & 1)], sq);
+                }
+                continue;
+            }
+            if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], act_f(v + e0[s], g.act));
+        } else if constexpr (MODE == GM_DX) {
+            if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0[s], g.act));
+        } else {
+            if (!out_ok) continue;
+            if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
+                st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
+                continue;
+            }
+            const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
+            const float lr_t = adam_lr(ga.adam, g.group, tstep);
+            const float gr = v * g.grad_scale;
+            const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+            const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
+            const float vv1 = e2[s] + (gr * gr - e2[s]) * (1.f - b2);
+            const float pn = e0[s] - (mm1 * lr_t) / (sqrtf(vv1) + eps);
+            st_out(&g.P[pidx], pn);
+            st_out(&g.P[pidx + ga.p_stride], mm1);
+            st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+            if (g.T != nullptr) {
+                const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
+                if (ctl->num_timesteps % tui == 0) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
+            }
+        }
+    }
+}
+
+template <int MODE, int VEC, int ROWK, int NQ, bool BF = false, bool PK = false, bool T32 = false>
 __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
-    __shared__ float red[4][4][64];
+    __shared__ float red[T32 ? 16 : 4][4][64];
     // PK: packed seeds (nseeds > 1); a one-seed launch compiles the relocation away (so = 0)
     const int64_t so = PK ? seed_off(ga.sstride) : 0;
     // the folded alpha.final of the previous update is workgroup 0: dispatched first, its
@@ -605,6 +760,11 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         if (i < ga.nprob && tile >= ga.probs[i].tile_begin) p = i;
     GemmProb g = ga.probs[p];   // by value: every field loads once, up front (speculatable)
     reloc(g, so);
+    if constexpr (T32) {
+        static_assert(MODE != GM_FWD2 && !(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
+        gemm_tile32<MODE, VEC, BF>(ga, g, tile - g.tile_begin, so, red);
+        return;
+    }
     const int lt = tile - g.tile_begin;
     const int tm = lt / g.tiles_n;
     const int tn = lt - tm * g.tiles_n;
@@ -832,10 +992,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 
 // ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
 // (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
-template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false>
+template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    gemm_core<MODE, VEC, ROWK, NQ, BF, PK>(ga);
+    gemm_core<MODE, VEC, ROWK, NQ, BF, PK, T32>(ga);
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -860,7 +1020,7 @@ __global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
     }
 }
 
-template <bool PK>
+template <bool PK, bool T32>
 static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     const unsigned z = seeds_z(a.nseeds);
     const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0), 1, z), block(256);
@@ -878,11 +1038,11 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
             else { if (h8) SACX_FH(0, 8); else SACX_FH(0, 4); }
 #undef SACX_FH
         } else if (a.bf16) {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK>), grid, block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK, T32>), grid, block, 0, s, a);
         } else {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, false, PK>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, false, PK>), grid, block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, false, PK, T32>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, false, PK, T32>), grid, block, 0, s, a);
         }
         break;
     case GM_DX: {
@@ -890,8 +1050,8 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
         const bool q8 = a.rowk && a.qh.H1 > 256;
 #define SACX_DX(V, R, Q)                                                                            \
     do {                                                                                           \
-        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK>), gx, block, 0, s, a);          \
-        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK>), gx, block, 0, s, a);                      \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK, T32>), gx, block, 0, s, a);          \
+        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK, T32>), gx, block, 0, s, a);                      \
     } while (0)
         if (a.rowk == 1) {
             if (a.vec) { if (q8) SACX_DX(1, 1, 8); else SACX_DX(1, 1, 4); }
@@ -923,23 +1083,30 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
             const dim3 gh(a.total_tiles + a.row_blocks, 1, z);
             const bool h8 = a.head.H1 > 256;
             if (a.bf16) {
-                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true, PK>), gh, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true, PK>), gh, block, 0, s, a);
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true, PK, T32>), gh, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true, PK, T32>), gh, block, 0, s, a);
             } else {
-                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, false, PK>), gh, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, false, PK>), gh, block, 0, s, a);
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, false, PK, T32>), gh, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, false, PK, T32>), gh, block, 0, s, a);
             }
         } else if (a.bf16) {
-            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true, PK>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true, PK, T32>), grid, block, 0, s, a);
         } else {
-            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, false, PK>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, false, PK, T32>), grid, block, 0, s, a);
         }
     }
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
-    if (a.nseeds > 1) launch_gemm_t<true>(a, s);
-    else launch_gemm_t<false>(a, s);
+    // 32x32 tiles: plain FWD / DX / DW launches only (the host never sets t32 elsewhere)
+    const bool t32 = a.t32 && a.mode != GM_FWD2 && !(a.mode == GM_FWD && a.rowk == 3);
+    if (a.nseeds > 1) {
+        if (t32) launch_gemm_t<true, true>(a, s);
+        else launch_gemm_t<true, false>(a, s);
+    } else {
+        if (t32) launch_gemm_t<false, true>(a, s);
+        else launch_gemm_t<false, false>(a, s);
+    }
 }
 
 // ==================================================================== k_rng

@@ -135,6 +135,7 @@ struct sacx_handle {
     std::vector<Launch> plan[NSLOT];
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
     int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
+    int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (SACX_XCD=0 restores dispatch order)
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
     // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
@@ -397,14 +398,21 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     Launch L{};
     L.kind = Launch::GEMM;
     L.name = name;
+    // 32x32 workgroup tiles for plain FWD / DX / DW launches when the handle asks for them
+    // (packed seeds: many tiles per launch); head-prologue and fused two-layer launches stay 16x16
+    // (tile32 = 2: forward / dX launches only -- the dW + Adam epilogue's registers cost occupancy)
+    bool t32 = h->tile32 > 0;
+    for (auto& p : ps) t32 = t32 && p.headp == 0 && p.W0 == nullptr && !(h->tile32 == 2 && p.epi == EPI_ADAM);
+    const int ts = t32 ? 32 : 16;
     int tiles = 0;
     for (auto& p : ps) {
-        p.tiles_n = (p.N + 15) / 16;
+        p.tiles_n = (p.N + ts - 1) / ts;
         p.tile_begin = tiles;
-        tiles += ((p.M + 15) / 16) * p.tiles_n;
+        tiles += ((p.M + ts - 1) / ts) * p.tiles_n;
         L.flops += gemm_flops(p);
         L.bytes += gemm_bytes(p);
     }
+    L.gemm.t32 = t32 ? 1 : 0;
     // both slot plans address the same (slot-independent) problem table
     L.gemm_first = h->probs_cursor;
     h->probs_cursor += (int)ps.size();
@@ -459,7 +467,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
 
 // Appends the problems of GEMM launch `b` to launch `a` (same mode; tile ranges follow a's).
 bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
-    if (a.mode != b.mode || a.nprob + b.nprob > GEMM_MAXP) return false;
+    if (a.mode != b.mode || a.t32 != b.t32 || a.nprob + b.nprob > GEMM_MAXP) return false;
     for (int i = 0; i < b.nprob; ++i) {
         GemmProb p = b.probs[i];
         p.tile_begin += a.total_tiles;
@@ -614,8 +622,11 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
     // workgroups of the same launch.  SACX_FUSE_HEAD=0 keeps the separate launch.
     const char* fh = std::getenv("SACX_FUSE_HEAD");
+    // Packed seeds (>= 4) keep the separate launch: the prologue recomputes each tile's 16 rows
+    // once per column tile, which a full GPU of seeds pays for (measured 34.3k vs 31.6k updates/s
+    // at 8 seeds); one seed gains the launch it saves.
     const bool fuse_head = !eo && Aout <= 16 && S + A <= 64 && H1 % 16 == 0 && H1 <= 512 &&
-                           !(fh && std::atoi(fh) == 0);
+                           (fh ? std::atoi(fh) != 0 : h->seeds < 4);
     HeadArgs head_fused{};
     // ---- actor head
     if (fuse_head) {
@@ -1161,9 +1172,10 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         const bool timed = kt && (L.kind == Launch::GEMM || (kt->rows && (L.kind == Launch::AHEAD || L.kind == Launch::ABWD)));
         if (timed) {
             Launch C = L;
-            const int nwg = (L.kind == Launch::GEMM
+            const int nwg1 = L.kind == Launch::GEMM
                                  ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0)
-                                 : (L.kind == Launch::AHEAD ? (C.head.total_rows + 3) / 4 : C.grid)) * h->seeds;
+                                 : (L.kind == Launch::AHEAD ? (C.head.total_rows + 3) / 4 : C.grid);
+            const int nwg = nwg1 * h->seeds;   // slots of every seed (seed-major)
             if (kt->used + 2 * nwg <= kt->cap) {
                 uint64_t* p = kt->base + kt->used;
                 if (L.kind == Launch::GEMM) C.gemm.ktime = p;
@@ -1174,7 +1186,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 kt->is_gemm.push_back(L.kind == Launch::GEMM);
                 if (L.kind != Launch::GEMM) kt->rowspan.push_back({0, 0});
                 else if (C.gemm.rowk == 3) kt->rowspan.push_back({C.gemm.has_final ? 1 : 0, (C.gemm.has_final ? 1 : 0) + C.gemm.row_blocks});
-                else kt->rowspan.push_back({C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0), nwg});
+                else kt->rowspan.push_back({C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0), nwg1});
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);
@@ -1456,6 +1468,8 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
                                 hipMemcpyHostToDevice));
     }
     if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
+    h->tile32 = h->seeds >= 4 ? 2 : 0;
+    if (const char* e = std::getenv("SACX_T32")) h->tile32 = std::atoi(e);
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     if (h->dp_ranks > 0) {
         if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");

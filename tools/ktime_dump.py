@@ -17,7 +17,8 @@ def main():
     from sac_eo.common.replicas import init_replica
     cfg = sys.argv[1] if len(sys.argv) > 1 else "hc"
     rep = init_replica()
-    eng = bench.build_engine(bench.CONFIGS[cfg], rep.seeds(0), rep.device)
+    k = int(os.environ.get("KT_SEEDS", "1"))           # packed seeds per handle
+    eng = bench.build_engine(bench.CONFIGS[cfg], bench.replica_seeds(rep, k), rep.device)
     eng.step(300)
     eng.sync()
     path = os.path.join(tempfile.mkdtemp(), "kt.csv")
