@@ -464,14 +464,22 @@ def test_rollout_graph_replay_equals_eager(gpu_available, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("use_expert,eager", [(False, False), (True, False), (False, True)])
-def test_packed_seeds_equal_single(gpu_available, use_expert, eager):
-    """cfg.seeds = 3 (the reference's --runs packed into one handle, grid z = seed): every
+@pytest.mark.parametrize("K,use_expert,eager,t32", [(3, False, False, None), (3, True, False, None),
+                                                   (3, False, True, None), (4, False, False, None),
+                                                   (4, True, False, None), (4, False, False, "1")])
+def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, eager, t32):
+    """cfg.seeds = K (the reference's --runs packed into one handle, grid z = seed): every
     seed ends bit-identical to a one-seed engine fed the same state, buffer, RNG stream and
     permutations -- stats, every parameter / Adam / target value, and the RNG key.  19
-    updates = two 8-update graphs + remainder graphs."""
+    updates = two 8-update graphs + remainder graphs.  At K = 4 the packed plan takes 32x32
+    tiles for its forward / dX launches and the one-seed engines 16x16 (both with the
+    separate actor.head launch): the two tilings must agree bit for bit."""
     from sac_eo.engine import Engine, EngineConfig
-    K, n, B, N, eps = 3, 19, 128, 3000, 0.1
+    n, B, N, eps = 19, 128, 3000, 0.1
+    if K >= 4:
+        monkeypatch.setenv("SACX_FUSE_HEAD", "0")
+    if t32 is not None:                         # "1": the dW + Adam launches on 32x32 tiles too
+        monkeypatch.setenv("SACX_T32", t32)
     learners = [make_learner(act="tanh", B=B, N=N, seed=40 + 7 * k, use_expert=use_expert, epsilon=eps)
                 for k in range(K)]
 
@@ -488,6 +496,8 @@ def test_packed_seeds_equal_single(gpu_available, use_expert, eager):
             eng.push_perms(np.stack([rs.permutation(20) for _ in range(n)]))
 
     packed = Engine(cfg(K))
+    if K >= 4:
+        monkeypatch.setenv("SACX_T32", "0")     # the one-seed references: 16x16 tiles
     for k in range(K):
         packed.select_seed(k)
         drive(packed, k)
