@@ -1468,7 +1468,10 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
                                 hipMemcpyHostToDevice));
     }
     if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
-    h->tile32 = h->seeds >= 4 ? 2 : 0;
+    // 32x32 forward / dX tiles once the launches are wide: seeds x batch >= 1024 rows (packed
+    // seeds; Humanoid B = 1024: SAC-EO +5.6 %, model fit +8 %, SAC +1 %); a handle-level rule, so
+    // the launches merged_body folds together always agree
+    h->tile32 = (int64_t)h->seeds * h->B >= 1024 ? 2 : 0;
     if (const char* e = std::getenv("SACX_T32")) h->tile32 = std::atoi(e);
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     if (h->dp_ranks > 0) {

@@ -476,10 +476,9 @@ def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, ea
     separate actor.head launch): the two tilings must agree bit for bit."""
     from sac_eo.engine import Engine, EngineConfig
     n, B, N, eps = 19, 128, 3000, 0.1
-    if K >= 4:
+    if K >= 4:                                  # the packed plan: 32x32 tiles ("1": dW + Adam too)
         monkeypatch.setenv("SACX_FUSE_HEAD", "0")
-    if t32 is not None:                         # "1": the dW + Adam launches on 32x32 tiles too
-        monkeypatch.setenv("SACX_T32", t32)
+        monkeypatch.setenv("SACX_T32", t32 or "2")
     learners = [make_learner(act="tanh", B=B, N=N, seed=40 + 7 * k, use_expert=use_expert, epsilon=eps)
                 for k in range(K)]
 
