@@ -1110,13 +1110,10 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
 }
 
 // ==================================================================== k_rng
-// NumPy legacy RandomState stream, one workgroup:
-//   phase 1: randint(cur_size, n_int)  masked rejection on 32-bit words
-//   phase 2: n_norm x legacy_gauss     polar method, cached second value
-// Words are consumed straight from the current MT block; items are accepted in
-// parallel and ranked with a block-wide ballot prefix count.  A twist happens
-// only once the block is exhausted (a <4-word gauss remainder is carried), so
-// the state written back is always (current block, position).
+// NumPy legacy RandomState stream, one workgroup, per update of the batch:
+//   randint(cur_size, n_int)  masked rejection on 32-bit words
+//   n_norm x legacy_gauss     polar method, cached second value
+// (mtrand legacy_gauss / random_bounded_uint64_fill restated; bit-exact, tests/test_gpu_engine.py)
 #define RNG_THREADS 1024
 
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
@@ -1130,22 +1127,6 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 __device__ __forceinline__ uint32_t mt_tw(uint32_t cur, uint32_t nxt, uint32_t far) {
     const uint32_t y = (cur & 0x80000000U) | (nxt & 0x7fffffffU);
     return far ^ (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
-}
-
-// out-of-place twist: dst = next block of src.  MT19937's in-place recurrence reads the old
-// words i+1, i+397 for i < 227 and the NEW words i-227 beyond (dst[0] and dst[396] for 623),
-// so three phases with a barrier after each are enough.
-__device__ __forceinline__ void mt_twist_to(const uint32_t* src, uint32_t* dst) {
-    const int t = threadIdx.x;
-    if (t < 227) dst[t] = mt_tw(src[t], src[t + 1], src[t + 397]);
-    __syncthreads();
-    if (t < 227) dst[227 + t] = mt_tw(src[227 + t], src[228 + t], dst[t]);
-    __syncthreads();
-    if (t < 170) {
-        const int i = 454 + t;
-        dst[i] = (i < 623) ? mt_tw(src[i], src[i + 1], dst[i - 227]) : mt_tw(src[623], dst[0], dst[396]);
-    }
-    __syncthreads();
 }
 
 // exclusive rank of `flag` among flagged threads, and the block total
@@ -1167,59 +1148,66 @@ __device__ __forceinline__ int block_rank(bool flag, int* wtot, int& total) {
     return off + below;
 }
 
-#define RNG_KB 4   // fresh MT blocks twisted ahead per round
+// The stream lives in an LDS ring of raw (untempered) MT words: stream word q (words 0..623 =
+// the state's key) sits at ring[q % RNG_RW].  MT19937 as a word recurrence is
+//   x[n] = x[n-227] ^ g(n-624),   g(m) = twist(x[m], x[m+1])      (n >= 624)
+// and unrolled three times
+//   x[n] = x[n-681] ^ g(n-624) ^ g(n-851) ^ g(n-1078),
+// whose operands all lie below n-622: 623 consecutive words are independent, so the whole
+// workgroup produces 623 words per step with one barrier (the first 454 words after the key
+// use the 227-wide form, which needs no history before it).  Consumption is one candidate
+// per thread (a word for randint, 4 words for a polar pair), accepted ones ranked by a
+// block-wide ballot prefix.  The state written back is (block holding the last consumed word,
+// position); the ring keeps that block resident and it is generated to its end first.
+#define RNG_RW 32768          // ring words (a power of two: the index wraps with a mask)
 
-// The stream is consumed in rounds.  blk[0] is the current block (next word at pos); a
-// round twists nb <= RNG_KB fresh blocks after it (as many as the expected acceptance
-// needs), lays the tempered words out in win[] behind any carried words, tests all
-// candidates in parallel and ranks the accepted ones.  The block holding the last
-// consumed word becomes blk[0] again, so the state written back is always the NumPy
-// (key = current block, pos) pair.
 struct RngShared {
-    uint32_t blk[RNG_KB + 1][624];
-    uint32_t win[(RNG_KB + 1) * 624 + 4];
+    uint32_t ring[RNG_RW];
     int wtot[RNG_THREADS / 64];
     int last;
     int has;
     double gauss;
 };
 
-// lays out the stream of this round; returns its length in words (carry included)
-__device__ int rng_fill(RngShared& S, int& pos, int cl, int est_words) {
-    const int t = threadIdx.x;
-    const int avail = cl + (624 - pos);
-    int nb = est_words > avail ? (est_words - avail + 623) / 624 : 0;
-    if (avail == 0 && nb == 0) nb = 1;
-    nb = nb > RNG_KB ? RNG_KB : nb;
-    for (int j = 1; j <= nb; ++j) mt_twist_to(S.blk[j - 1], S.blk[j]);
-    const int f0 = 624 - pos;
-    const int L = cl + f0 + nb * 624;
-    for (int i = t; i < f0 + nb * 624; i += RNG_THREADS) {
-        const uint32_t w = i < f0 ? S.blk[0][pos + i] : S.blk[1 + (i - f0) / 624][(i - f0) % 624];
-        S.win[cl + i] = mt_temper(w);
-    }
-    __syncthreads();
-    return L | (nb << 24);
+__device__ __forceinline__ uint32_t& rng_at(RngShared& S, int q) { return S.ring[(unsigned)q & (RNG_RW - 1u)]; }
+__device__ __forceinline__ uint32_t rng_g(RngShared& S, int m) {
+    const uint32_t y = (rng_at(S, m) & 0x80000000U) | (rng_at(S, m + 1) & 0x7fffffffU);
+    return (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
 }
 
-// after a round that consumed `used` stream words (carry included): the block holding the
-// last consumed word becomes blk[0]
-__device__ void rng_settle(RngShared& S, int& pos, int cl, int used, int nb) {
+// all threads: stream words [w0, w1), w0 >= 624
+__device__ void rng_twist(RngShared& S, int w0, int w1) {
     const int t = threadIdx.x;
-    int c = used - cl;                     // fresh words consumed (>= 0: a candidate ends past the carry)
-    const int f0 = 624 - pos;
-    int j = 0, np = pos + c;
-    if (c > f0) {
-        c -= f0;
-        j = 1 + (c - 1) / 624;
-        np = c - (j - 1) * 624;
-    }
-    if (j > 0) {
-        for (int i = t; i < 624; i += RNG_THREADS) S.blk[0][i] = S.blk[j][i];
+    int n0 = w0;
+    while (n0 < w1 && n0 < 1078) {               // 227-wide steps (history from the key only)
+        const int n1 = min(min(w1, 1078), n0 + 227);
+        const int n = n0 + t;
+        if (n < n1) rng_at(S, n) = rng_at(S, n - 227) ^ rng_g(S, n - 624);
         __syncthreads();
+        n0 = n1;
     }
-    pos = np;
-    (void)nb;
+    while (n0 < w1) {                             // 623-wide steps
+        const int n1 = min(w1, n0 + 623);
+        const int n = n0 + t;
+        if (n < n1) rng_at(S, n) = rng_at(S, n - 681) ^ rng_g(S, n - 624) ^ rng_g(S, n - 851) ^ rng_g(S, n - 1078);
+        __syncthreads();
+        n0 = n1;
+    }
+}
+
+// tools/rng_bench.hip builds with SACX_RNG_PROF: thread 0 accumulates 100 MHz ticks of the
+// twist bursts [0], randint chunks [1], gauss chunks [2], whole kernel [3], bursts [4], chunks [5]
+#ifdef SACX_RNG_PROF
+__device__ unsigned long long g_rng_prof[8];
+#define RNG_PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
+#define RNG_PROF_ADD(i, v) do { if (threadIdx.x == 0) g_rng_prof[i] += (v); } while (0)
+#else
+#define RNG_PROF_T(v)
+#define RNG_PROF_ADD(i, v) do { } while (0)
+#endif
+
+__device__ __forceinline__ uint32_t rng_word(const RngShared& S, int q) {
+    return S.ring[(unsigned)q & (RNG_RW - 1u)];
 }
 
 __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
@@ -1231,151 +1219,148 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         a.out_idx = sr(a_in.out_idx, so); a.out_norm = sr(a_in.out_norm, so);
     }
     const int t = threadIdx.x;
-    for (int i = t; i < 624; i += RNG_THREADS) S.blk[0][i] = a.st->key[i];
-    int pos = a.st->pos;
+    for (int i = t; i < 624; i += RNG_THREADS) S.ring[i] = a.st->key[i];
+    const int pos0 = a.st->pos;
     if (t == 0) {
         S.has = a.st->has_gauss;
         S.gauss = a.st->gauss;
     }
+    // randint(high): masked rejection on 32-bit words (legacy bounded uint64 path, rng < 2^32)
+    const uint64_t high = (uint64_t)a.ctl->cur_size;
+    const uint64_t rng = high > 0 ? high - 1 : 0;
+    uint64_t mask = rng;
+    mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+    mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+    // expected words of the whole launch: bursts twist no further than the batch needs
+    const double ints = (a.n_int > 0 && rng > 0) ? (double)a.n_int * ((double)(mask + 1) / (double)(rng + 1)) : 0.0;
+    const double pairs = (double)((a.n_norm + 1) >> 1) * (4.0 / 0.78539816339744831);
+    int est_rem = (int)(((ints + pairs) * 1.01 + 32.0) * a.nupd);
+    int q = pos0;        // next stream word (block 0 word 0 = 0)
+    int gen = 624;       // stream words [0, gen) exist; [gen - RNG_RW, gen) resident
     __syncthreads();
+
+    // makes words [q, q_end) resident (uniform; q_end - q <= RNG_RW - 1248)
+    auto ensure = [&](int q_end) {
+        if (q_end <= gen) return;
+        RNG_PROF_T(p0);
+        const int keep = q > 0 ? ((q - 1) / 624) * 624 : 0;   // the last consumed word's block stays
+        int tgt = max(q_end, q + est_rem);
+        tgt = min(tgt, keep + RNG_RW);
+        rng_twist(S, gen, tgt);
+        gen = tgt;
+        RNG_PROF_T(p1);
+        RNG_PROF_ADD(0, p1 - p0);
+        RNG_PROF_ADD(4, 1);
+    };
+    RNG_PROF_T(k0);
 
     for (int u = 0; u < a.nupd; ++u) {
         // update u of the batch: its randint + normals, in stream order, into slot (slot + u)
         int32_t* const out_idx = a.out_idx ? (int32_t*)((char*)a.out_idx + u * a.slot_bytes) : nullptr;
         float* const out_norm = (float*)((char*)a.out_norm + u * a.slot_bytes);
+        const int q_upd = q;
 
-        // ---------------- randint(high, n_int): masked rejection, one word per candidate
+        // ---------------- randint(high, n_int): one word per candidate
         if (a.n_int > 0) {
-            const uint64_t high = (uint64_t)a.ctl->cur_size;
-            const uint64_t rng = high > 0 ? high - 1 : 0;
-            uint64_t mask = rng;
-            mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
-            mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
             if (rng == 0) {
                 for (int i = t; i < a.n_int; i += RNG_THREADS) out_idx[i] = 0;
             } else {
                 int done = 0;
                 while (done < a.n_int) {
-                    const int need = a.n_int - done;
-                    // acceptance (rng+1)/(mask+1) >= 1/2
-                    const int est = (int)((double)need * (double)(mask + 1) / (double)(rng + 1) * 1.05) + 16;
-                    const int r = rng_fill(S, pos, 0, est);
-                    const int L = r & 0xffffff, nb = r >> 24;
-                    int used = L;
-                    bool fin = false;
-                    for (int c0 = 0; c0 < L && !fin; c0 += RNG_THREADS) {
-                        const int idx = c0 + t;
-                        bool acc = false;
-                        uint32_t v = 0;
-                        if (idx < L) {
-                            const uint32_t w = S.win[idx];
-                            if (rng == 0xFFFFFFFFULL) { v = w; acc = true; }
-                            else { v = w & (uint32_t)mask; acc = (uint64_t)v <= rng; }
-                        }
-                        int total;
-                        const int rank = block_rank(acc, S.wtot, total);
-                        const int nd = a.n_int - done;
-                        if (acc && rank < nd) out_idx[done + rank] = (int32_t)v;
-                        if (acc && rank == nd - 1) S.last = idx;
-                        __syncthreads();
-                        if (total >= nd) {
-                            used = S.last + 1;
-                            done = a.n_int;
-                            fin = true;
-                        } else {
-                            done += total;
-                        }
-                        __syncthreads();
+                    ensure(q + RNG_THREADS);
+                    RNG_PROF_T(c0);
+                    const uint32_t w = mt_temper(rng_word(S, q + t));
+                    uint32_t v;
+                    bool acc;
+                    if (rng == 0xFFFFFFFFULL) { v = w; acc = true; }
+                    else { v = w & (uint32_t)mask; acc = (uint64_t)v <= rng; }
+                    int total;
+                    const int rank = block_rank(acc, S.wtot, total);
+                    const int nd = a.n_int - done;
+                    if (acc && rank < nd) out_idx[done + rank] = (int32_t)v;
+                    if (acc && rank == nd - 1) S.last = t;
+                    __syncthreads();
+                    if (total >= nd) {
+                        q += S.last + 1;
+                        done = a.n_int;
+                    } else {
+                        q += RNG_THREADS;
+                        done += total;
                     }
-                    if (fin) {
-                        rng_settle(S, pos, 0, used, nb);
-                    } else {              // every fresh word consumed: the last block is current
-                        rng_settle(S, pos, 0, L, nb);
-                    }
+                    RNG_PROF_T(c1);
+                    RNG_PROF_ADD(1, c1 - c0);
+                    RNG_PROF_ADD(5, 1);
                 }
             }
         }
 
-        // ---------------- n_norm x legacy_gauss (polar method, pairs of 4 words)
+        // ---------------- n_norm x legacy_gauss (polar method, 4 words per candidate pair)
         int oi = 0;
-        if (a.n_norm > 0 && S.has) {
-            if (t == 0) out_norm[0] = (float)S.gauss;
+        const bool cached = a.n_norm > 0 && S.has;   // every thread reads before thread 0 clears it
+        __syncthreads();
+        if (cached) {
+            if (t == 0) {
+                out_norm[0] = (float)S.gauss;
+                S.has = 0;
+                S.gauss = 0.0;     // NumPy clears the cached value with the flag
+            }
             oi = 1;
-            __syncthreads();
-            if (t == 0) { S.has = 0; S.gauss = 0.0; }
-            __syncthreads();
         }
-        int cl = 0;                               // carried words at win[0..cl)
-        while (oi < a.n_norm) {
-            const int need_pairs = (a.n_norm - oi + 1) >> 1;
-            const int est = (int)((double)need_pairs * 4.0 * 1.3) + 16;   // acceptance pi/4
-            const int r = rng_fill(S, pos, cl, est);
-            const int L = r & 0xffffff, nb = r >> 24;
-            const int items = L >> 2;
-            int got = 0;
-            bool fin = false;
-            int used = 4 * items;
-            for (int c0 = 0; c0 < items && !fin; c0 += RNG_THREADS) {
-                const int it = c0 + t;
-                bool acc = false;
-                double f = 0.0, x1 = 0.0, x2 = 0.0;
-                if (it < items) {
-                    const uint32_t w0 = S.win[4 * it], w1 = S.win[4 * it + 1], w2 = S.win[4 * it + 2],
-                                   w3 = S.win[4 * it + 3];
-                    const double u1 = ((double)(int32_t)(w0 >> 5) * 67108864.0 + (double)(int32_t)(w1 >> 6)) / 9007199254740992.0;
-                    const double u2 = ((double)(int32_t)(w2 >> 5) * 67108864.0 + (double)(int32_t)(w3 >> 6)) / 9007199254740992.0;
-                    x1 = 2.0 * u1 - 1.0;
-                    x2 = 2.0 * u2 - 1.0;
-                    const double r2 = x1 * x1 + x2 * x2;
-                    acc = (r2 < 1.0) && (r2 != 0.0);
-                    if (acc) f = sqrt(-2.0 * log(r2) / r2);
-                }
-                int total;
-                const int rank = block_rank(acc, S.wtot, total);
-                const int np = need_pairs - got;
-                if (acc && rank < np) {
-                    const int o = oi + 2 * (got + rank);
-                    out_norm[o] = (float)(f * x2);
-                    if (o + 1 < a.n_norm) {
-                        out_norm[o + 1] = (float)(f * x1);
-                    } else {
-                        S.gauss = f * x1;
-                        S.has = 1;
-                    }
-                }
-                if (acc && rank == np - 1) S.last = it;
-                __syncthreads();
-                if (total >= np) {
-                    used = 4 * (S.last + 1);
-                    fin = true;
-                    got = need_pairs;
+        const int need_pairs = (a.n_norm - oi + 1) >> 1;
+        int got = 0;
+        while (got < need_pairs) {
+            ensure(q + 4 * RNG_THREADS);
+            RNG_PROF_T(c0);
+            const int c = q + 4 * t;
+            const uint32_t w0 = mt_temper(rng_word(S, c)), w1 = mt_temper(rng_word(S, c + 1));
+            const uint32_t w2 = mt_temper(rng_word(S, c + 2)), w3 = mt_temper(rng_word(S, c + 3));
+            const double u1 = ((double)(int32_t)(w0 >> 5) * 67108864.0 + (double)(int32_t)(w1 >> 6)) / 9007199254740992.0;
+            const double u2 = ((double)(int32_t)(w2 >> 5) * 67108864.0 + (double)(int32_t)(w3 >> 6)) / 9007199254740992.0;
+            const double x1 = 2.0 * u1 - 1.0;
+            const double x2 = 2.0 * u2 - 1.0;
+            const double r2 = x1 * x1 + x2 * x2;
+            const bool acc = (r2 < 1.0) && (r2 != 0.0);
+            double f = 0.0;
+            if (acc) f = sqrt(-2.0 * log(r2) / r2);
+            int total;
+            const int rank = block_rank(acc, S.wtot, total);
+            const int np = need_pairs - got;
+            if (acc && rank < np) {
+                const int o = oi + 2 * (got + rank);
+                out_norm[o] = (float)(f * x2);
+                if (o + 1 < a.n_norm) {
+                    out_norm[o + 1] = (float)(f * x1);
                 } else {
-                    got += total;
+                    S.gauss = f * x1;
+                    S.has = 1;
                 }
-                __syncthreads();
             }
-            if (fin) {
-                oi = a.n_norm;
-                rng_settle(S, pos, cl, used, nb);
-                cl = 0;
+            if (acc && rank == np - 1) S.last = t;
+            __syncthreads();
+            if (total >= np) {
+                q += 4 * (S.last + 1);
+                got = need_pairs;
             } else {
-                oi += 2 * got;
-                // carry the < 4 words after the last full candidate; the last block is current
-                const int left = L - 4 * items;
-                uint32_t keep = 0;
-                if (t < left) keep = S.win[4 * items + t];
-                rng_settle(S, pos, cl, L, nb);
-                __syncthreads();
-                if (t < left) S.win[t] = keep;
-                cl = left;
-                __syncthreads();
+                q += 4 * RNG_THREADS;
+                got += total;
             }
+            RNG_PROF_T(c1);
+            RNG_PROF_ADD(2, c1 - c0);
+            RNG_PROF_ADD(5, 1);
         }
+        est_rem -= q - q_upd;
     }
 
-    for (int i = t; i < 624; i += RNG_THREADS) a.st->key[i] = S.blk[0][i];
+    RNG_PROF_T(k1);
+    RNG_PROF_ADD(3, k1 - k0);
+    // state: the block holding the last consumed word (generated to its end) and the position
+    if (q > pos0) {
+        const int b = (q - 1) / 624;
+        ensure(624 * (b + 1));
+        for (int i = t; i < 624; i += RNG_THREADS) a.st->key[i] = rng_at(S, 624 * b + i);
+        if (t == 0) a.st->pos = q - b * 624;
+    }
     if (t == 0) {
-        a.st->pos = pos;
         a.st->has_gauss = S.has;
         a.st->gauss = S.gauss;
         if (a.slot >= 0) {
