@@ -252,3 +252,25 @@ def test_rollout_oracle_consumes_one_draw_per_step():
     rs2 = np.random.RandomState(7)
     O.rollout(st, cfg, nrm, s0, 4, 0, rs2, deterministic=True)
     assert rs2.get_state()[2] == np.random.RandomState(7).get_state()[2]
+
+
+def test_mt_unrolled_recurrence():
+    """The device sampler's word recurrence (csrc/k_sac.hip rng_twist): MT19937's raw words
+    satisfy x[n] = x[n-227] ^ g(n-624) and, unrolled, x[n] = x[n-681] ^ g(n-624) ^ g(n-851) ^
+    g(n-1078) with g(m) = twist(x[m], x[m+1]).  Raw blocks come from NumPy's own state after
+    every 624 full-range draws."""
+    rs = np.random.RandomState(2773201285)
+    blocks = []
+    for _ in range(6):
+        rs.randint(0, 2 ** 32, size=624, dtype=np.uint64)   # warm: position at a block edge
+        blocks.append(np.array(rs.get_state()[1], dtype=np.uint64))
+    x = np.concatenate(blocks)
+
+    def g(m):
+        y = (x[m] & 0x80000000) | (x[m + 1] & 0x7FFFFFFF)
+        return (y >> 1) ^ np.where(y & 1, 0x9908B0DF, 0).astype(np.uint64)
+
+    n = np.arange(624, len(x))
+    assert np.array_equal(x[n], x[n - 227] ^ g(n - 624))
+    n = np.arange(1078, len(x))
+    assert np.array_equal(x[n], x[n - 681] ^ g(n - 624) ^ g(n - 851) ^ g(n - 1078))
