@@ -232,6 +232,10 @@ __device__ __forceinline__ void reloc(ActorBwdArgs& b, int64_t so) {
     b.W3a = sr(b.W3a, so); b.Ha2 = sr(b.Ha2, so); b.Da3 = sr(b.Da3, so); b.Da2 = sr(b.Da2, so); b.E = sr(b.E, so);
     b.gpol = sr(b.gpol, so);
 }
+// forces a kernarg value into an SGPR at this point: values pinned together load as one batch
+template <class T>
+__device__ __forceinline__ void pin_s(const T& v) { asm volatile("" ::"s"(v)); }
+
 // the grid z extent of a launch (1 for the single-seed eager calls, whose nseeds is 0)
 inline unsigned seeds_z(int n) { return n > 1 ? (unsigned)n : 1u; }
 // per-workgroup measurement slot (ktime): workgroups of seed z follow those of seed z-1
@@ -729,9 +733,21 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     __shared__ float red[T32 ? 16 : 4][4][64];
     // PK: packed seeds (nseeds > 1); a one-seed launch compiles the relocation away (so = 0)
     const int64_t so = PK ? seed_off(ga.sstride) : 0;
+    // Every scalar that decides this workgroup's role and problem is read in ONE batch of
+    // kernarg loads: left alone, the compiler loads each behind its own branch, a chain of
+    // dependent scalar round trips in front of the first operand load.
+    const int has_final = ga.has_final, row_blocks = ga.row_blocks, total_tiles = ga.total_tiles;
+    const int xcd_map = ga.xcd_map, nprob = ga.nprob;
+    const int64_t p_stride = ga.p_stride;
+    int tb[GEMM_MAXP];
+#pragma unroll
+    for (int i = 0; i < GEMM_MAXP; ++i) tb[i] = ga.probs[i].tile_begin;
+    static_assert(GEMM_MAXP == 8, "one pin per problem's tile_begin");
+    asm volatile("" ::"s"(has_final), "s"(row_blocks), "s"(total_tiles), "s"(xcd_map), "s"(nprob), "s"(p_stride),
+                 "s"(tb[1]), "s"(tb[2]), "s"(tb[3]), "s"(tb[4]), "s"(tb[5]), "s"(tb[6]), "s"(tb[7]));
     // the folded alpha.final of the previous update is workgroup 0: dispatched first, its
     // serial reductions overlap the tiles instead of trailing them
-    int tile = (int)blockIdx.x - (ga.has_final ? 1 : 0);
+    int tile = (int)blockIdx.x - (has_final ? 1 : 0);
     if (tile < 0) {
         FinalArgs f = ga.fin;
         reloc(f, so);
@@ -741,24 +757,37 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     if constexpr (ROWK == 3) {
         // actor.head rows beside the tiles: dispatched first, so their serial row work
         // overlaps the tiles instead of trailing the launch
-        if (tile < ga.row_blocks) {
+        if (tile < row_blocks) {
             actor_head_body<NQ>(ga.head, ga.hfin, ga.head_block0 + tile, so);
             return;
         }
-        tile -= ga.row_blocks;
+        tile -= row_blocks;
     }
-    if (tile >= ga.total_tiles) {
+    if (tile >= total_tiles) {
         if constexpr (ROWK > 0 && ROWK < 3) {   // horizontally fused Q-head rows
-            qhead_block<ROWK - 1, NQ>(ga.qh, tile - ga.total_tiles, so);
+            qhead_block<ROWK - 1, NQ>(ga.qh, tile - total_tiles, so);
         }
         return;
     }
-    if (ga.xcd_map) tile = xcd_tile(tile, ga.total_tiles);
+    if (xcd_map) tile = xcd_tile(tile, total_tiles);
     int p = 0;
 #pragma unroll
     for (int i = 1; i < GEMM_MAXP; ++i)
-        if (i < ga.nprob && tile >= ga.probs[i].tile_begin) p = i;
+        if (i < nprob && tile >= tb[i]) p = i;
     GemmProb g = ga.probs[p];   // by value: every field loads once, up front (speculatable)
+    // the selected problem's fields of this mode, again in one batch (one asm statement: the
+    // loads cannot be split by waits between separate pins)
+    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
+                     "s"(g.dmean), "s"(g.dden), "s"(g.headp));
+    } else if constexpr (MODE == GM_DX) {
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.H), "s"(g.ldh));
+    } else {
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row));
+    }
     reloc(g, so);
     if constexpr (T32) {
         static_assert(MODE != GM_FWD2 && !(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
