@@ -777,7 +777,16 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     GemmProb g = ga.probs[p];   // by value: every field loads once, up front (speculatable)
     // the selected problem's fields of this mode, again in one batch (one asm statement: the
     // loads cannot be split by waits between separate pins)
-    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+    if constexpr (MODE == GM_FWD && ROWK == 3) {
+        // q.fwd0 with the actor head folded in (plain SAC: never an mse problem): the head
+        // prologue's operands ride in the same batch
+        const HeadArgs& hd = ga.head;
+        const HeadSeg& s0 = hd.seg[0];
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.headp), "s"(hd.H2), "s"(hd.W3), "s"(hd.logstd),
+                     "s"(hd.a_mean), "s"(hd.a_den), "s"(hd.ldh), "s"(hd.H1), "s"(hd.A), "s"(hd.Aout),
+                     "s"(hd.per_state_std), "s"(hd.lim), "s"(s0.r0), "s"(s0.noise), "s"(s0.nlp_out));
+    } else if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
                      "s"(g.dmean), "s"(g.dden), "s"(g.headp));
@@ -812,11 +821,13 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float e4 = 0.f;
     if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         e0 = g.bias[nnc];
-        // world-model head rows (mse): zero-sized resources when not an mse problem
-        e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
-        e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
-        e3 = bload(rs(g.dmean), boff(g.mse != 0, nnc));
-        e4 = bload(rs(g.dden), boff(g.mse != 0, nnc));
+        if constexpr (ROWK != 3) {   // the head-fused launch (plain SAC) has no mse problems
+            // world-model head rows (mse): zero-sized resources when not an mse problem
+            e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
+            e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
+            e3 = bload(rs(g.dmean), boff(g.mse != 0, nnc));
+            e4 = bload(rs(g.dden), boff(g.mse != 0, nnc));
+        }
     } else if constexpr (MODE == GM_DX) {
         e0 = g.H[(size_t)mmc * g.ldh + nnc];
     } else {
@@ -974,7 +985,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
-    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+    if constexpr ((MODE == GM_FWD || MODE == GM_FWD2) && ROWK != 3) {
         if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
             const float pred = v + e0;
             const float sp_hat = e1 + (pred * e4 + e3);
@@ -1767,6 +1778,12 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 template <int NQ, int NQD, bool PK>
 __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     ActorBwdArgs b = b_in;
+    // every argument in one batch of kernarg loads (else one dependent batch per branch)
+    asm volatile("" ::"s"(b.B), "s"(b.ne), "s"(b.S), "s"(b.A), "s"(b.Aout), "s"(b.H0), "s"(b.H1), "s"(b.Hm0),
+                 "s"(b.per_state_std), "s"(b.lim), "s"(b.Dp1), "s"(b.Wq1[0]), "s"(b.Wq1[1]), "s"(b.Dm1),
+                 "s"(b.Wm1[0]), "s"(b.Wm1[1]), "s"(b.a_den), "s"(b.alpha), "s"(b.ctl), "s"(b.use_expert),
+                 "s"(b.c_t), "s"(b.c_std), "s"(b.c_u), "s"(b.c_mask), "s"(b.W3a), "s"(b.Ha2), "s"(b.act),
+                 "s"(b.gpol));
     if constexpr (PK) reloc(b, seed_off(b_in.sstride));
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
