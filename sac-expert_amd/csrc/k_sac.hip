@@ -232,6 +232,16 @@ __device__ __forceinline__ void reloc(ActorBwdArgs& b, int64_t so) {
     b.W3a = sr(b.W3a, so); b.Ha2 = sr(b.Ha2, so); b.Da3 = sr(b.Da3, so); b.Da2 = sr(b.Da2, so); b.E = sr(b.E, so);
     b.gpol = sr(b.gpol, so);
 }
+// tools/gemm_bench.hip builds with SACX_GEMM_PHASES: wave 0 of each 16x16 tile workgroup
+// stores s_memrealtime at kernel start [0], problem selected [1], main loop done [2], tile
+// reduced [3] and kernel end [4] (the last launch's workgroups, by blockIdx.x)
+#ifdef SACX_GEMM_PHASES
+__device__ unsigned long long g_gemm_ph[8192][5];
+#define GEMM_PH(i) do { if (threadIdx.x == 0) g_gemm_ph[blockIdx.x][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define GEMM_PH(i) do { } while (0)
+#endif
+
 // forces a kernarg value into an SGPR at this point: values pinned together load as one batch
 template <class T>
 __device__ __forceinline__ void pin_s(const T& v) { asm volatile("" ::"s"(v)); }
@@ -798,6 +808,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row));
     }
     reloc(g, so);
+    GEMM_PH(1);
     if constexpr (T32) {
         static_assert(MODE != GM_FWD2 && !(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
         gemm_tile32<MODE, VEC, BF>(ga, g, tile - g.tile_begin, so, red);
@@ -975,10 +986,12 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][3], b[u][3], acc1, 0, 0, 0);
         }
     }
+    GEMM_PH(2);
     const floatx4 acc = acc0 + acc1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[wave][q][lane] = acc[q];
     __syncthreads();
+    GEMM_PH(3);
 
     // (row, col) lives in lane (row>>2)*16+col, register row&3 of each wave's tile
     const int L = ((row >> 2) << 4) | col, R = row & 3;
@@ -1035,7 +1048,11 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
 __global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#ifdef SACX_GEMM_PHASES
+    if (threadIdx.x == 0) g_gemm_ph[blockIdx.x][0] = t0;
+#endif
     gemm_core<MODE, VEC, ROWK, NQ, BF, PK, T32>(ga);
+    GEMM_PH(4);
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {

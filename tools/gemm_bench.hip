@@ -1,4 +1,7 @@
-// Ablation harness for k_gemm: per-launch time (graph replay) by shape/epilogue.
+// Ablation harness for k_gemm: per-launch time (graph replay) by shape/epilogue, and the
+// per-workgroup phase split of a dependent chain (SACX_GEMM_PHASES build).
+// build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I include -I sac-expert_amd/csrc tools/gemm_bench.hip -o tools/gemm_bench
+#define SACX_GEMM_PHASES 1
 #include "../sac-expert_amd/csrc/k_sac.hip"
 #include <chrono>
 #include <cstdio>
@@ -41,6 +44,24 @@ int main() {
         return ga;
     };
     const int n = 100;
+    // phase split: dependent chain of 512x256 FWD launches, stamps of the last launch
+    for (int K : {24, 256}) {
+        GemmArgs a0 = fwd(X0, X1, 512, 256, K), a1 = fwd(X1, X0, 512, 256, K);
+        const double us = tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); });
+        static unsigned long long ph[8192][5];
+        CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_gemm_ph), sizeof(ph)));
+        const int T = a0.total_tiles;
+        unsigned long long lo = ~0ull, hi = 0;
+        double d[4] = {0, 0, 0, 0};
+        for (int b = 0; b < T; ++b) {
+            lo = std::min(lo, ph[b][0]);
+            hi = std::max(hi, ph[b][4]);
+            for (int j = 0; j < 4; ++j) d[j] += (double)(ph[b][j + 1] - ph[b][j]);
+        }
+        printf("phases fwd 512x256 K=%-3d %.2f us/launch | span %.2f us | mean per WG: select %.2f  loads+mfma %.2f  "
+               "reduce %.2f  epilogue %.2f us\n", K, us, (hi - lo) * 0.01, d[0] * 0.01 / T, d[1] * 0.01 / T,
+               d[2] * 0.01 / T, d[3] * 0.01 / T);
+    }
     struct V { const char* name; int M, N, K; bool dep; };
     V vs[] = {{"fwd 512x256 K=256 warm", 512, 256, 256, false}, {"fwd 512x256 K=256 dep", 512, 256, 256, true},
               {"fwd 512x256 K=16 warm", 512, 256, 16, false},   {"fwd 512x256 K=16 dep", 512, 256, 16, true},

@@ -11,7 +11,7 @@ i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$PWD/$OUT" -o "p$i" \
-      -- python bench.py --config $CONFIG --steps 200 --warmup 20 --no-cpu-baseline --no-roofline > $OUT/p$i.log 2>&1
+      -- python bench.py --config $CONFIG --steps 200 --warmup 20 --no-cpu-baseline --no-roofline --packed-leg 0 > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"; tail -1 $OUT/p$i.log
   [ $rc -eq 0 ] || exit $rc
 done

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 timeout -k 10 400 python bench.py > $OUT/bench_hc.log 2>&1
 rc=$?; echo "bench rc=$rc"; tail -c 400 $OUT/bench_hc.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof" -o hc \
-    -- python bench.py --steps 2000 --warmup 200 --no-cpu-baseline > $OUT/prof_bench.log 2>&1
+    -- python bench.py --steps 2000 --warmup 200 --no-cpu-baseline --packed-leg 0 > $OUT/prof_bench.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 find $OUT/prof -name "*kernel_stats*" | head -3
 bash tools/gpu_pmc.sh
