@@ -94,6 +94,20 @@ int main() {
         char nm[64];
         snprintf(nm, sizeof nm, "fwd2 %dx%d K0=%d", M, N, K0);
         printf("%-28s %4d tiles: %.2f us/launch\n", nm, f2.total_tiles, tgraph(s, n, [&](int) { launch_gemm(f2, s); }));
+        {
+            static unsigned long long ph[8192][5];
+            CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_gemm_ph), sizeof(ph)));
+            const int T = f2.total_tiles;
+            unsigned long long lo = ~0ull, hi = 0;
+            double d[4] = {0, 0, 0, 0};
+            for (int b = 0; b < T; ++b) {
+                lo = std::min(lo, ph[b][0]);
+                hi = std::max(hi, ph[b][4]);
+                for (int j = 0; j < 4; ++j) d[j] += (double)(ph[b][j + 1] - ph[b][j]);
+            }
+            printf("  phases: span %.2f us | mean per WG: select %.2f  loads+mfma %.2f  reduce %.2f  epilogue %.2f us\n",
+                   (hi - lo) * 0.01, d[0] * 0.01 / T, d[1] * 0.01 / T, d[2] * 0.01 / T, d[3] * 0.01 / T);
+        }
         GemmArgs a0 = fwd(X0, X1 + 2000000, M, H0, K0);
         a0.probs[0].lda = 24; a0.vec = 0;
         GemmArgs a1 = fwd(X1 + 2000000, X1, M, N, H0);
