@@ -440,10 +440,14 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         const bool akc = p.a_kc != 0, bkc = p.b_kc != 0;
         if (akc != (mode != GM_DW) || bkc != (mode == GM_DX)) { fprintf(stderr, "sacx: bad operand layout in %s\n", name.c_str()); abort(); }
         if (mode == GM_DW && p.bscale == nullptr) p.bscale = h->f("ws.ones");
-        const bool v_a = (p.lda % 4 == 0) && ((((uintptr_t)p.A) & 15) == 0) &&
+        // float4 loads along k: a K that is not a multiple of 4 (S+A = 23, 393; S = 17) still
+        // qualifies when the row stride holds round4(K) (the zero pad columns of the staging
+        // slabs): the over-read elements meet B values that load_b zeroes past K
+        const int64_t k4 = r4(p.K);
+        const bool v_a = (p.lda % 4 == 0) && (k4 <= p.lda) && ((((uintptr_t)p.A) & 15) == 0) &&
                          ((((uintptr_t)p.wgen) & 15) == 0);
-        const bool v_b = mode == GM_DX ? ((p.ldb % 4 == 0) && ((((uintptr_t)p.B) & 15) == 0)) : true;
-        if (!(v_a && v_b && p.K % 4 == 0 && p.K >= 4)) vec = false;
+        const bool v_b = mode == GM_DX ? ((p.ldb % 4 == 0) && (k4 <= p.ldb) && ((((uintptr_t)p.B) & 15) == 0)) : true;
+        if (!(v_a && v_b && p.K >= 4)) vec = false;
     }
     L.gemm.mode = mode;
     L.gemm.vec = mode == GM_FWD2 ? ((k0max + 7) / 8) * 2 : (vec ? 1 : 0);

@@ -44,9 +44,15 @@ int main() {
         return ga;
     };
     const int n = 100;
-    // phase split: dependent chain of 512x256 FWD launches, stamps of the last launch
-    for (int K : {24, 256}) {
-        GemmArgs a0 = fwd(X0, X1, 512, 256, K), a1 = fwd(X1, X0, 512, 256, K);
+    // phase split: dependent chain of FWD launches (512x256; Humanoid's 1024x256 at K = 393),
+    // stamps of the last launch
+    // (lda = round4(K): the padded staging stride that lets K = 393 take float4 loads)
+    struct PV { int M, K, vec; } pvs[] = {{512, 24, 1}, {512, 256, 1}, {1024, 393, 0}, {1024, 393, 1}, {4096, 393, 1}};
+    for (auto pv : pvs) {
+        const int K = pv.K;
+        GemmArgs a0 = fwd(X0, X1, pv.M, 256, K), a1 = fwd(X1, X0, pv.M, 256, K);
+        a0.probs[0].lda = a1.probs[0].lda = (K + 3) & ~3;
+        a0.vec = a1.vec = pv.vec;
         const double us = tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); });
         static unsigned long long ph[8192][5];
         CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_gemm_ph), sizeof(ph)));
@@ -58,8 +64,8 @@ int main() {
             hi = std::max(hi, ph[b][4]);
             for (int j = 0; j < 4; ++j) d[j] += (double)(ph[b][j + 1] - ph[b][j]);
         }
-        printf("phases fwd 512x256 K=%-3d %.2f us/launch | span %.2f us | mean per WG: select %.2f  loads+mfma %.2f  "
-               "reduce %.2f  epilogue %.2f us\n", K, us, (hi - lo) * 0.01, d[0] * 0.01 / T, d[1] * 0.01 / T,
+        printf("phases fwd %dx256 K=%-3d vec=%d %.2f us/launch | span %.2f us | mean per WG: select %.2f  loads+mfma %.2f  "
+               "reduce %.2f  epilogue %.2f us\n", pv.M, K, pv.vec, us, (hi - lo) * 0.01, d[0] * 0.01 / T, d[1] * 0.01 / T,
                d[2] * 0.01 / T, d[3] * 0.01 / T);
     }
     struct V { const char* name; int M, N, K; bool dep; };
