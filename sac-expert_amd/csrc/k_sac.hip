@@ -1045,8 +1045,12 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 
 // ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
 // (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
+#ifndef SACX_T32_WGS
+#define SACX_T32_WGS 4
+#endif
+#define SACX_T32_OCC ((T32 && MODE != GM_DW) ? SACX_T32_WGS : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
-__global__ __launch_bounds__(256) void k_gemm(GemmArgs ga) {
+__global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SACX_GEMM_PHASES
     if (threadIdx.x == 0) g_gemm_ph[blockIdx.x][0] = t0;
