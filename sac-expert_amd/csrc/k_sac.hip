@@ -290,6 +290,30 @@ __device__ __forceinline__ void rowdot8(const float (&hv)[NQ], __amdgpu_buffer_r
     for (int u = 0; u < 8; ++u) out[u] = wave_sum(p[u]);
 }
 
+// rowdot8 over the whole output row [0, OW) at once, W (H x O, dense) staged in LDS by the
+// workgroup.  Read from memory, lane k's W[k][u] for all u is OW single-dword loads 4*O bytes
+// apart -- 64 cache lines per instruction, which made the per-CU L1 the bottleneck of
+// Humanoid's actor.head (O = 17: 96 scattered loads per row).  Per output the same fmaf
+// order and wave_sum as rowdot8, so the sums are identical.
+template <int NQ, int OW>
+__device__ __forceinline__ void rowdot_lds(const float (&hv)[NQ], const float* Ws, int H, int O, float (&out)[OW]) {
+    const int lane = threadIdx.x & 63;
+    float w[NQ][OW];
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int k = lane + 64 * q;
+#pragma unroll
+        for (int u = 0; u < OW; ++u) w[q][u] = (k < H && u < O) ? Ws[k * O + u] : 0.f;   // stride O: odd O conflict-free
+    }
+#pragma unroll
+    for (int u = 0; u < OW; ++u) {
+        float p = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) p = fmaf(hv[q], w[q][u], p);
+        out[u] = wave_sum(p);
+    }
+}
+
 // ==================================================================== finalize
 // alpha Adam + clamp and the per-update statistics.
 __device__ float mean_rows(const float* x, int n) {
@@ -479,7 +503,7 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
 __device__ __forceinline__ void qhead_block(const QHeadArgs& q, int block, int64_t so);
-template <int NQ>
+template <int NQ, int OW = 0>
 __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so);
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
@@ -1525,9 +1549,24 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // ==================================================================== k_actor_head
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
-template <int NQ>
+template <int NQ, int OW>
 __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
     __shared__ float red_s[4];
+    __shared__ float w3s[OW > 0 ? 256 * OW : 1];
+    if constexpr (OW > 0) {
+        // W3 (H1 x Aout, row-major) copied whole into LDS by the workgroup: contiguous loads,
+        // all in flight together, before any row exits
+        static_assert(NQ == 4, "LDS-staged W3: H1 <= 256");
+        const __amdgpu_buffer_rsrc_t rW0 = rs(sr(h.W3, so));
+        const int n = h.H1 * h.Aout;
+        float wv[OW];
+#pragma unroll
+        for (int c = 0; c < OW; ++c) wv[c] = bload(rW0, boff((int)threadIdx.x + 256 * c < n, threadIdx.x + 256 * c));
+#pragma unroll
+        for (int c = 0; c < OW; ++c)
+            if ((int)threadIdx.x + 256 * c < n) w3s[threadIdx.x + 256 * c] = wv[c];
+        __syncthreads();
+    }
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = block * 4 + wave;
     float row_ent = 0.f;
@@ -1550,14 +1589,24 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         const float bmu = bload(rW, boff(jok, h.H1 * Aout + lane));
         const float bls = bload(rW, boff(jok && h.per_state_std, h.H1 * Aout + A + lane));
         float mu = 0.f, lraw = 0.f;
-        for (int o0 = 0; o0 < Aout; o0 += 8) {
-            float s8[8];
-            rowdot8(hv, rW, h.H1, Aout, o0, Aout, s8);
+        if constexpr (OW > 0) {        // Aout <= OW, H1 <= 256 (host-checked): W3 from LDS
+            float so_[OW];
+            rowdot_lds<NQ, OW>(hv, w3s, h.H1, Aout, so_);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const int o = o0 + u;
-                mu = (lane == o) ? s8[u] : mu;
-                lraw = (lane + A == o) ? s8[u] : lraw;
+            for (int u = 0; u < OW; ++u) {
+                mu = (lane == u) ? so_[u] : mu;
+                lraw = (lane + A == u) ? so_[u] : lraw;
+            }
+        } else {
+            for (int o0 = 0; o0 < Aout; o0 += 8) {
+                float s8[8];
+                rowdot8(hv, rW, h.H1, Aout, o0, Aout, s8);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int o = o0 + u;
+                    mu = (lane == o) ? s8[u] : mu;
+                    lraw = (lane + A == o) ? s8[u] : lraw;
+                }
             }
         }
         mu = mu + bmu;
@@ -1616,10 +1665,10 @@ __device__ __forceinline__ void ktime_stamp(uint64_t* kt, uint64_t t0) {
     }
 }
 
-template <int NQ, bool PK>
+template <int NQ, bool PK, int OW = 0>
 __global__ __launch_bounds__(256) void k_actor_head(HeadArgs h, FinalArgs f) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    actor_head_body<NQ>(h, f, (int)blockIdx.x, PK ? seed_off(h.sstride) : 0);
+    actor_head_body<NQ, OW>(h, f, (int)blockIdx.x, PK ? seed_off(h.sstride) : 0);
     ktime_stamp(h.ktime, t0);
 }
 
@@ -1627,8 +1676,19 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
     const dim3 grid((a.total_rows + 3) / 4, 1, seeds_z(a.nseeds));
     const bool pk = a.nseeds > 1;
     if (a.H1 <= 256) {
-        if (pk) hipLaunchKernelGGL((k_actor_head<4, true>), grid, dim3(256), 0, s, a, f);
-        else hipLaunchKernelGGL((k_actor_head<4, false>), grid, dim3(256), 0, s, a, f);
+        // more than one 8-column chunk: the whole row's W3 loads in one round trip (NQ = 4
+        // keeps w[4][OW] at <= 96 registers)
+        if (a.Aout > 8 && a.Aout <= 16) {
+            if (pk) hipLaunchKernelGGL((k_actor_head<4, true, 16>), grid, dim3(256), 0, s, a, f);
+            else hipLaunchKernelGGL((k_actor_head<4, false, 16>), grid, dim3(256), 0, s, a, f);
+        } else if (a.Aout > 16 && a.Aout <= 24) {
+            if (pk) hipLaunchKernelGGL((k_actor_head<4, true, 24>), grid, dim3(256), 0, s, a, f);
+            else hipLaunchKernelGGL((k_actor_head<4, false, 24>), grid, dim3(256), 0, s, a, f);
+        } else if (pk) {
+            hipLaunchKernelGGL((k_actor_head<4, true>), grid, dim3(256), 0, s, a, f);
+        } else {
+            hipLaunchKernelGGL((k_actor_head<4, false>), grid, dim3(256), 0, s, a, f);
+        }
     } else {
         if (pk) hipLaunchKernelGGL((k_actor_head<8, true>), grid, dim3(256), 0, s, a, f);
         else hipLaunchKernelGGL((k_actor_head<8, false>), grid, dim3(256), 0, s, a, f);
@@ -1796,7 +1856,7 @@ void launch_qhead(const QHeadArgs& a, hipStream_t s) {
 // rows) or world-model (expert rows) input columns, tanh-Gaussian backward
 // (SURVEY.md §8a A5), then the Dense(H1 -> Aout) backward with the activation
 // derivative.  Per-column values live in lane j and are broadcast by shuffles.
-template <int NQ, int NQD, bool PK>
+template <int NQ, int NQD, bool PK, int OW>
 __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     ActorBwdArgs b = b_in;
     // every argument in one batch of kernarg loads (else one dependent batch per branch)
@@ -1806,6 +1866,21 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
                  "s"(b.c_t), "s"(b.c_std), "s"(b.c_u), "s"(b.c_mask), "s"(b.W3a), "s"(b.Ha2), "s"(b.act),
                  "s"(b.gpol));
     if constexpr (PK) reloc(b, seed_off(b_in.sstride));
+    __shared__ float w3s[OW > 0 ? 256 * OW : 1];
+    if constexpr (OW > 0) {
+        // W3a (H1 x Aout) staged in LDS as in actor_head_body: its lane-strided reads below
+        // would be 64 cache lines per load instruction
+        static_assert(NQ == 4, "LDS-staged W3: H1 <= 256");
+        const __amdgpu_buffer_rsrc_t rW0 = rs(b.W3a);
+        const int n = b.H1 * b.Aout;
+        float wv[OW];
+#pragma unroll
+        for (int c = 0; c < OW; ++c) wv[c] = bload(rW0, boff((int)threadIdx.x + 256 * c < n, threadIdx.x + 256 * c));
+#pragma unroll
+        for (int c = 0; c < OW; ++c)
+            if ((int)threadIdx.x + 256 * c < n) w3s[threadIdx.x + 256 * c] = wv[c];
+        __syncthreads();
+    }
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     const int B = b.B, S = b.S, A = b.A;
@@ -1830,7 +1905,7 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     for (int qq = 0; qq < NQ; ++qq) {
         const int i = qq * 64 + lane;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) w3n[qq][u] = bload(rW3, boff(i < b.H1 && u < b.Aout, i * b.Aout + u));
+        for (int u = 0; u < 8; ++u) w3n[qq][u] = OW > 0 ? 0.f : bload(rW3, boff(i < b.H1 && u < b.Aout, i * b.Aout + u));
     }
     const float w_sac = 1.f - eps;
     const float c = -w_sac * alpha * (1.f / (float)B);
@@ -1897,7 +1972,20 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     float pacc[NQ];
 #pragma unroll
     for (int qq = 0; qq < NQ; ++qq) pacc[qq] = 0.f;
-    for (int o0 = 0; o0 < b.Aout; o0 += 8) {
+    if constexpr (OW > 0) {     // all OW columns (zeros past Aout, as the 8-chunks give)
+#pragma unroll
+        for (int u = 0; u < OW; ++u) {
+            const float src = (u < A) ? __shfl(gx, min(u, 63), 64) : __shfl(dl, min(max(u - A, 0), 63), 64);
+            const float d3 = (u < b.Aout) ? src : 0.f;
+#pragma unroll
+            for (int qq = 0; qq < NQ; ++qq) {
+                const int i = qq * 64 + lane;
+                const float w = (i < b.H1 && u < b.Aout) ? w3s[i * b.Aout + u] : 0.f;
+                pacc[qq] = fmaf(d3, w, pacc[qq]);
+            }
+        }
+    }
+    for (int o0 = 0; OW == 0 && o0 < b.Aout; o0 += 8) {
         float w[NQ][8];
         if (o0 == 0) {
 #pragma unroll
@@ -1932,10 +2020,10 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     }
 }
 
-template <int NQ, int NQD, bool PK>
+template <int NQ, int NQD, bool PK, int OW = 0>
 __global__ __launch_bounds__(256) void k_actor_bwd(ActorBwdArgs b) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    actor_bwd_body<NQ, NQD, PK>(b);
+    actor_bwd_body<NQ, NQD, PK, OW>(b);
     ktime_stamp(b.ktime, t0);
 }
 
@@ -1944,14 +2032,17 @@ void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {
     const dim3 grid((rows + 3) / 4, 1, seeds_z(a.nseeds));
     const int hd = std::max(a.H0, a.use_expert ? a.Hm0 : 0);
     const bool q8 = a.H1 > 256, d8 = hd > 256;
-#define SACX_AB(Q, D)                                                                              \
-    do {                                                                                           \
-        if (a.nseeds > 1) hipLaunchKernelGGL((k_actor_bwd<Q, D, true>), grid, dim3(256), 0, s, a);   \
-        else hipLaunchKernelGGL((k_actor_bwd<Q, D, false>), grid, dim3(256), 0, s, a);              \
+#define SACX_AB(Q, D, ...)                                                                                  \
+    do {                                                                                                    \
+        if (a.nseeds > 1) hipLaunchKernelGGL((k_actor_bwd<Q, D, true, ##__VA_ARGS__>), grid, dim3(256), 0, s, a); \
+        else hipLaunchKernelGGL((k_actor_bwd<Q, D, false, ##__VA_ARGS__>), grid, dim3(256), 0, s, a);            \
     } while (0)
     if (q8) {
         if (d8) SACX_AB(8, 8);
         else SACX_AB(8, 4);
+    } else if (a.Aout > 8 && a.Aout <= 24) {   // W3a staged in LDS (see actor_bwd_body)
+        if (d8) SACX_AB(4, 8, 24);
+        else SACX_AB(4, 4, 24);
     } else {
         if (d8) SACX_AB(4, 8);
         else SACX_AB(4, 4);
