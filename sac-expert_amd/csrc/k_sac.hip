@@ -18,6 +18,7 @@
 // rounds like the reference's separate TF ops (dot products use explicit
 // fmaf).  GEMM accumulation is the exact-f32 MFMA (k-ordered fmaf chain).
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <math.h>
 #include "sacx_internal.h"
 
@@ -662,16 +663,18 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         acc0[s] = floatx4{0.f, 0.f, 0.f, 0.f};
         acc1[s] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
+    auto main_loop = [&](auto vt) {   // unswitched on the problem's float4 flag, as gemm_core
+    constexpr bool V = decltype(vt)::value;
     for (int it = it0; it < it1; it += 4) {
         float a[4][2][4], b[4][2][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int k0 = (it + u) * 16 + grp * 4;
             const int k0e = (it + u < it1) ? k0 : (1 << 30);
-            load_a<AKC, VEC && AKC, MODE == GM_DX>(ra, g, ma, maok, k0e, a[u][0], rw);
-            load_a<AKC, VEC && AKC, MODE == GM_DX>(ra, g, mb, mbok, k0e, a[u][1], rw);
-            load_b<BKC, VEC && BKC, MODE == GM_DW>(rb, g, na, naok, k0e, b[u][0]);
-            load_b<BKC, VEC && BKC, MODE == GM_DW>(rb, g, nb, nbok, k0e, b[u][1]);
+            load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, ma, maok, k0e, a[u][0], rw);
+            load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, mb, mbok, k0e, a[u][1], rw);
+            load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, na, naok, k0e, b[u][0]);
+            load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, nb, nbok, k0e, b[u][1]);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -696,6 +699,13 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                     else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][s >> 1][j], b[u][s & 1][j], acc0[s], 0, 0, 0);
                 }
         }
+    }
+    };
+    if constexpr (VEC == 1) {
+        if (g.vec) main_loop(std::true_type{});
+        else main_loop(std::false_type{});
+    } else {
+        main_loop(std::false_type{});
     }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -819,14 +829,14 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.headp), "s"(hd.H2), "s"(hd.W3), "s"(hd.logstd),
                      "s"(hd.a_mean), "s"(hd.a_den), "s"(hd.ldh), "s"(hd.H1), "s"(hd.A), "s"(hd.Aout),
-                     "s"(hd.per_state_std), "s"(hd.lim), "s"(s0.r0), "s"(s0.noise), "s"(s0.nlp_out));
+                     "s"(hd.per_state_std), "s"(hd.lim), "s"(s0.r0), "s"(s0.noise), "s"(s0.nlp_out), "s"(g.vec));
     } else if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
-                     "s"(g.dmean), "s"(g.dden), "s"(g.headp));
+                     "s"(g.dmean), "s"(g.dden), "s"(g.headp), "s"(g.vec));
     } else if constexpr (MODE == GM_DX) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
-                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.H), "s"(g.ldh));
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.H), "s"(g.ldh), "s"(g.vec));
     } else {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row));
@@ -982,6 +992,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             }
         }
     }
+    // float4 operand loads per problem (g.vec): a launch can mix problems with and without
+    // them, and the loop is unswitched on the flag
+    auto main_loop = [&](auto vt) {
+    constexpr bool V = decltype(vt)::value;
     for (int it = it0; MODE != GM_FWD2 && !a_lds && it < it1; it += 4) {
         float a[4][4], b[4][4];
 #pragma unroll
@@ -989,8 +1003,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             // iterations past it1 read a clamped (valid) slab and are zeroed
             const int k0 = (it + u) * 16 + grp * 4;
             const int k0e = (it + u < it1) ? k0 : (1 << 30);
-            load_a<AKC, VEC && AKC, MODE == GM_DX>(ra, g, m, mok, k0e, a[u], rw);
-            load_b<BKC, VEC && BKC, MODE == GM_DW>(rb, g, n, nok, k0e, b[u]);
+            load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, m, mok, k0e, a[u], rw);
+            load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, n, nok, k0e, b[u]);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -1009,6 +1023,13 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][3], b[u][3], acc1, 0, 0, 0);
         }
+    }
+    };
+    if constexpr (VEC == 1) {
+        if (g.vec) main_loop(std::true_type{});
+        else main_loop(std::false_type{});
+    } else {
+        main_loop(std::false_type{});
     }
     GEMM_PH(2);
     const floatx4 acc = acc0 + acc1;

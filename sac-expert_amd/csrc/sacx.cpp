@@ -416,14 +416,13 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     // both slot plans address the same (slot-independent) problem table
     L.gemm_first = h->probs_cursor;
     h->probs_cursor += (int)ps.size();
-    if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
     if (ps.size() > GEMM_MAXP) { fprintf(stderr, "sacx: too many GEMM problems in %s\n", name.c_str()); abort(); }
     // every problem of a launch must share the operand/epilogue mode (k_gemm template)
     auto mode_of = [](const GemmProb& p) {
         return p.epi == EPI_ADAM ? GM_DW : (p.epi == EPI_DACT ? GM_DX : (p.W0 ? GM_FWD2 : GM_FWD));
     };
     const int mode = mode_of(ps[0]);
-    bool vec = mode != GM_DW;
+    bool vec = false;   // any problem with float4 loads (each problem carries its own flag)
     int k0max = 0;
     for (auto& p : ps) {
         if (mode == GM_FWD2 && (p.K0 < 1 || p.K0 > FWD2_MAX_K0)) {
@@ -447,8 +446,10 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         const bool v_a = (p.lda % 4 == 0) && (k4 <= p.lda) && ((((uintptr_t)p.A) & 15) == 0) &&
                          ((((uintptr_t)p.wgen) & 15) == 0);
         const bool v_b = mode == GM_DX ? ((p.ldb % 4 == 0) && (k4 <= p.ldb) && ((((uintptr_t)p.B) & 15) == 0)) : true;
-        if (!(v_a && v_b && p.K >= 4)) vec = false;
+        p.vec = (mode != GM_DW && v_a && v_b && p.K >= 4) ? 1 : 0;
+        vec = vec || p.vec;
     }
+    if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
     L.gemm.mode = mode;
     L.gemm.vec = mode == GM_FWD2 ? ((k0max + 7) / 8) * 2 : (vec ? 1 : 0);
     for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
@@ -479,7 +480,7 @@ bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
     }
     a.nprob += b.nprob;
     a.total_tiles += b.total_tiles;
-    a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec && b.vec);
+    a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec || b.vec);
     return true;
 }
 

@@ -96,6 +96,9 @@ struct GemmProb {
     // tile's rows, computed in the tile's prologue from GemmArgs::head (seg[0]); columns
     // [0, K - A) are read from A as usual (the target rows: actor.head folded into q.fwd0)
     int32_t headp;
+    // GM_FWD / GM_DX: this problem's operands take float4 loads along k (host-checked strides and
+    // alignment); the launch's VEC template only says whether any problem does
+    int32_t vec;
 };
 
 struct FinalArgs {

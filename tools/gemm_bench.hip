@@ -37,7 +37,7 @@ int main() {
         GemmArgs ga{}; GemmProb p{};
         p.A = A; p.lda = K; p.a_kc = 1; p.ones_row = -1; p.B = W; p.ldb = N; p.b_kc = 0; p.M = M; p.N = N; p.K = K;
         p.bias = W + (size_t)K * N; p.C = C; p.ldc = N; p.epi = EPI_FWD; p.act = ACT_RELU;
-        p.tiles_n = (N + 15) / 16; p.tile_begin = 0;
+        p.tiles_n = (N + 15) / 16; p.tile_begin = 0; p.vec = (K % 4 == 0);
         ga.probs[0] = p; ga.nprob = 1; ga.total_tiles = ((M + 15) / 16) * p.tiles_n; ga.p_stride = NF; ga.ctl = ctl;
         ga.mode = GM_FWD; ga.vec = (K % 4 == 0);
         ga.adam.lr[0] = ga.adam.lr[1] = ga.adam.lr[2] = ga.adam.lr[3] = 1e-4f;
@@ -52,7 +52,7 @@ int main() {
         const int K = pv.K;
         GemmArgs a0 = fwd(X0, X1, pv.M, 256, K), a1 = fwd(X1, X0, pv.M, 256, K);
         a0.probs[0].lda = a1.probs[0].lda = (K + 3) & ~3;
-        a0.vec = a1.vec = pv.vec;
+        a0.vec = a1.vec = a0.probs[0].vec = a1.probs[0].vec = pv.vec;
         const double us = tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); });
         static unsigned long long ph[8192][5];
         CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_gemm_ph), sizeof(ph)));
@@ -115,7 +115,7 @@ int main() {
                    (hi - lo) * 0.01, d[0] * 0.01 / T, d[1] * 0.01 / T, d[2] * 0.01 / T, d[3] * 0.01 / T);
         }
         GemmArgs a0 = fwd(X0, X1 + 2000000, M, H0, K0);
-        a0.probs[0].lda = 24; a0.vec = 0;
+        a0.probs[0].lda = 24; a0.vec = a0.probs[0].vec = 0;
         GemmArgs a1 = fwd(X1 + 2000000, X1, M, N, H0);
         snprintf(nm, sizeof nm, "fwd0+fwd1 %dx%d K0=%d", M, N, K0);
         printf("%-28s %4d tiles: %.2f us/pair\n", nm, a0.total_tiles + a1.total_tiles,
@@ -140,7 +140,7 @@ int main() {
         // dX (k-contig A and B^T), the critic backward shape: 512x256, K=256
         GemmArgs gx{}; GemmProb q{};
         q.A = X0; q.lda = 256; q.a_kc = 1; q.ones_row = -1; q.B = W; q.ldb = 257 * 0 + 256; q.b_kc = 1; q.M = 512; q.N = 256; q.K = 256;
-        q.H = X1; q.ldh = 256; q.C = X1 + 2000000; q.ldc = 256; q.epi = EPI_DACT; q.act = ACT_RELU; q.tiles_n = 16; q.tile_begin = 0;
+        q.H = X1; q.ldh = 256; q.C = X1 + 2000000; q.ldc = 256; q.epi = EPI_DACT; q.act = ACT_RELU; q.tiles_n = 16; q.tile_begin = 0; q.vec = 1;
         gx.probs[0] = q; gx.nprob = 1; gx.total_tiles = 32 * 16; gx.p_stride = NF; gx.ctl = ctl; gx.mode = GM_DX; gx.vec = 1;
         printf("%-28s %4d tiles: %.2f us/launch\n", "dX 512x256 K=256", gx.total_tiles, tgraph(s, n, [&](int) { launch_gemm(gx, s); }));
     }
