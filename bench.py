@@ -363,7 +363,8 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
             "scaling": "strong" if dp else "weak", "vs_baseline": None,
             "dtype": "bf16 (MFMA operands), f32 accumulate" if cfgd.get("bf16") else "f32",
-            "data": "synthetic (HalfCheetah-shaped replay rows generated on device; random orthogonal init)",
+            "data": ("synthetic (" + ("HalfCheetah" if args.config == "hc" else "Humanoid")
+                     + "-shaped replay rows generated on device; random orthogonal init)"),
             "config": {"workload": cfgd["workload"], "obs_dim": cfgd["S"], "act_dim": cfgd["A"],
                        "batch": cfgd["B"], "hidden": list(cfgd["hidden"]), "buffer_rows": cfgd["buffer"],
                        "parallelism": (f"dp{ws}: one learner, batch {cfgd['B'] // ws} per GPU, 3 RCCL all-reduces "
