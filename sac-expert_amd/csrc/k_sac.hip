@@ -612,6 +612,9 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
 // quarter of the workgroups.  Every 16x16 sub-tile accumulates exactly as gemm_core's 16x16
 // path does (same k order, same acc0 / acc1 split, same 4-wave reduction order, same
 // epilogue), so both tilings give bit-identical results.
+#ifndef SACX_T32_NS
+#define SACX_T32_NS 2   // k slabs per load group of a 32x32 tile (2: 5 workgroups per CU fit)
+#endif
 template <int MODE, int VEC, bool BF>
 __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
                                             float (&red)[16][4][64]) {
@@ -665,10 +668,10 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
     }
     auto main_loop = [&](auto vt) {   // unswitched on the problem's float4 flag, as gemm_core
     constexpr bool V = decltype(vt)::value;
-    for (int it = it0; it < it1; it += 4) {
-        float a[4][2][4], b[4][2][4];
+    for (int it = it0; it < it1; it += SACX_T32_NS) {
+        float a[SACX_T32_NS][2][4], b[SACX_T32_NS][2][4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < SACX_T32_NS; ++u) {
             const int k0 = (it + u) * 16 + grp * 4;
             const int k0e = (it + u < it1) ? k0 : (1 << 30);
             load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, ma, maok, k0e, a[u][0], rw);
@@ -678,7 +681,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < SACX_T32_NS; ++u) {
             if constexpr (BF) {
 #pragma unroll
                 for (int s = 0; s < 4; ++s) {
@@ -1091,7 +1094,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 // ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
 // (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
 #ifndef SACX_T32_WGS
-#define SACX_T32_WGS 4
+#define SACX_T32_WGS 5
 #endif
 #define SACX_T32_OCC ((T32 && MODE != GM_DW) ? SACX_T32_WGS : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
