@@ -1475,8 +1475,11 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
     // 32x32 forward / dX tiles once the launches are wide: seeds x batch >= 1024 rows (packed
     // seeds; Humanoid B = 1024: SAC-EO +5.6 %, model fit +8 %, SAC +1 %); a handle-level rule, so
-    // the launches merged_body folds together always agree
-    h->tile32 = (int64_t)h->seeds * h->B >= 1024 ? 2 : 0;
+    // the launches merged_body folds together always agree.  From 4,096 rows the dW + Adam
+    // launches take 32x32 tiles too (tools/t32_dw.sh: Humanoid 4 seeds +3.5 %, 8 seeds +5 %,
+    // bf16 4 seeds +8 %, HC 32 seeds +1.9 %; HC 8 / 16 seeds and one Humanoid seed even or worse)
+    const int64_t rows = (int64_t)h->seeds * h->B;
+    h->tile32 = rows >= 4096 ? 1 : rows >= 1024 ? 2 : 0;
     if (const char* e = std::getenv("SACX_T32")) h->tile32 = std::atoi(e);
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     if (h->dp_ranks > 0) {
