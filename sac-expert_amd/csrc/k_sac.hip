@@ -613,7 +613,7 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
 // path does (same k order, same acc0 / acc1 split, same 4-wave reduction order, same
 // epilogue), so both tilings give bit-identical results.
 #ifndef SACX_T32_NS
-#define SACX_T32_NS 2   // k slabs per load group of a 32x32 tile (2: 5 workgroups per CU fit)
+#define SACX_T32_NS 1   // k slabs per load group of a 32x32 tile (1: 6 workgroups per CU fit)
 #endif
 template <int MODE, int VEC, bool BF>
 __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
@@ -1094,7 +1094,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 // ktime (measurement graphs only): workgroup b stores its first / last s_memrealtime tick
 // (100 MHz) at ktime[2b], ktime[2b+1]; the host takes the launch's span from min / max.
 #ifndef SACX_T32_WGS
-#define SACX_T32_WGS 5
+#define SACX_T32_WGS 6
 #endif
 #define SACX_T32_OCC ((T32 && MODE != GM_DW) ? SACX_T32_WGS : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
