@@ -1096,7 +1096,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 #ifndef SACX_T32_WGS
 #define SACX_T32_WGS 6
 #endif
-#define SACX_T32_OCC ((T32 && MODE != GM_DW) ? SACX_T32_WGS : 1)
+#ifndef SACX_T32_DW_WGS
+#define SACX_T32_DW_WGS 1
+#endif
+#define SACX_T32_OCC (T32 ? (MODE != GM_DW ? SACX_T32_WGS : SACX_T32_DW_WGS) : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
 __global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
