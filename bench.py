@@ -170,11 +170,54 @@ def roofline(eng, config, n_prof=20, n_replays=20):
     return out, fam
 
 
+def host_cpu_info():
+    """(os.cpu_count(), cores this process may use, lscpu model name).  On the GPU box
+    os.cpu_count() is the whole machine; the usable share is the affinity set capped by the
+    cgroup CPU quota (cpu.max) and the box's OMP_NUM_THREADS."""
+    total = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else total
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        if q != "max":
+            usable = min(usable, max(1, int(int(q) // int(p))))
+    except (OSError, ValueError):
+        pass
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if omp > 0:
+        usable = min(usable, omp)
+    model = None
+    try:
+        import subprocess
+        for ln in subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout.splitlines():
+            if ln.lower().startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except Exception:  # pragma: no cover
+        pass
+    return total, usable, model
+
+
 def cpu_baseline(cfgd, seconds=10.0):
-    """The CPU oracle (numpy fp32 port of the reference update) on the host cores."""
+    """The CPU oracle (numpy fp32 port of the reference update, oracle/sac_oracle.py) on the
+    host cores: timed at 1 BLAS thread and at every usable core; ``value`` is the faster."""
+    total, usable, model = host_cpu_info()
+    runs = {}
+    for th in sorted({1, usable}):
+        runs[th] = _cpu_port_rate(cfgd, seconds / (2 if usable > 1 else 1), th)
+    best = max(runs, key=lambda t: runs[t][0])
+    v, n, el = runs[best]
+    return {"value": round(v, 3), "unit": "gradient-steps/s", "cores": best, "kind": "port",
+            "value_1thread": round(runs[1][0], 3), "value_all_cores": round(runs[usable][0], 3),
+            "cores_usable": usable, "os_cpu_count": total, "cpu_model": model,
+            "sample": f"{n} updates of the numpy fp32 oracle (oracle/sac_oracle.py) at the bench shapes in "
+                      f"{el:.1f}s at {best} BLAS thread(s) (also timed at 1 and {usable} threads); "
+                      "TensorFlow reference not installable"}
+
+
+def _cpu_port_rate(cfgd, seconds, threads):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import sac_oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
     try:
         from threadpoolctl import threadpool_limits
         ctx = threadpool_limits(limits=threads)
@@ -202,9 +245,34 @@ def cpu_baseline(cfgd, seconds=10.0):
             break
     if ctx is not None:
         ctx.unregister() if hasattr(ctx, "unregister") else None
-    return {"value": round(n / el, 3), "unit": "gradient-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} updates of the numpy fp32 oracle (oracle/sac_oracle.py) at the bench shapes, "
-                      f"{el:.1f}s, BLAS threads={threads}; TensorFlow reference not installable"}
+    return n / el, n, el
+
+
+def drop_in_loop(eng, cfgd, n=300):
+    """The drop-in train loop's rate (algs/base.py: one update per env step, as the
+    reference's SAC_exp.train calls _update at SAC_expert.py:780): per iteration the
+    behaviour action of one observation comes back to the host (actor.sample, B=1), one
+    transition is appended to the device ring, and step(1) runs one update."""
+    import torch
+    S, A = cfgd["S"], cfgd["A"]
+    obs = torch.randn(1, S, device=eng.device)
+    row = lambda k: torch.randn(1, k, device=eng.device)
+    eng.prepare(1)
+
+    def it(j):
+        a = eng.act(obs, deterministic=False).cpu()          # host env gets the action
+        eng.append(obs, a, torch.zeros(1), row(S), torch.zeros(1))
+        eng.step(1, num_timesteps=j, ts_increment=1)
+    for j in range(10):
+        it(j)
+    eng.sync()
+    t0 = time.perf_counter()
+    for j in range(n):
+        it(j)
+    eng.sync()
+    el = time.perf_counter() - t0
+    return {"updates_per_s": round(n / el, 1), "us_per_iteration": round(el / n * 1e6, 2), "iterations": n,
+            "iteration": "act(1 obs, stochastic) -> host, append(1 transition), step(1)"}
 
 
 def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):
@@ -256,6 +324,7 @@ def packed_leg(cfgd, config, rep, k, steps, with_roofline):
     packed chain counts the K seeds' FLOPs per launch."""
     eng = build_engine(cfgd, replica_seeds(rep, k), device=rep.device)
     eng.step(256)
+    cap_s = eng.prepare(steps)          # every graph step(steps) replays, instantiated untimed
     eng.sync()
     rep.barrier()
     t0 = time.perf_counter()
@@ -271,7 +340,7 @@ def packed_leg(cfgd, config, rep, k, steps, with_roofline):
     eng.select_seed(0)
     out = {"seeds_per_gpu": k, "value": round(steps * k * rep.world_size / el, 2), "unit": "gradient-steps/s",
            "per_seed": round(steps / el, 2), "ms_per_round": round(el / steps * 1e3, 5), "steps": steps,
-           "finite_stats": finite,
+           "finite_stats": finite, "graph_prepare_s": round(cap_s, 4),
            "note": "independent learners (the reference's --runs) packed into one handle per GPU"}
     if with_roofline:
         peak = BF16_PEAK_TFLOPS if cfgd.get("bf16") else FP32_PEAK_TFLOPS
@@ -286,6 +355,36 @@ def packed_leg(cfgd, config, rep, k, steps, with_roofline):
                            "timing": "per-workgroup device timestamps in a replay of the packed update graph"}
     eng.close()
     return out
+
+
+def spawn_ranks(n):
+    """Runs this script as n ranks under torch.distributed.run (127.0.0.1 rendezvous) in a
+    child process; returns its exit status.  The parent never initialises the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def plan_only(args):
+    """The launch plan without a GPU: each rank joins a gloo group and reports its rank, the
+    world size the group sees and its learners' seeds (replica_seeds); rank 0 prints one JSON
+    line with every rank's entry (tests/test_replicas.py checks it for --gpus 2)."""
+    from sac_eo.common.replicas import init_replica
+    rep = init_replica(backend="gloo", use_cuda=False)
+    mine = {"rank": rep.rank, "world_size": rep.world_size, "seeds": replica_seeds(rep, args.seeds_per_gpu)}
+    if rep.dist is not None:
+        allr = [None] * rep.world_size
+        rep.dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+    if rep.rank == 0:
+        print(json.dumps({"plan_only": True, "n_gpus": args.gpus, "ranks": allr}), flush=True)
+    rep.close()
 
 
 def main():
@@ -306,7 +405,21 @@ def main():
     ap.add_argument("--packed-leg", type=int, default=-1,
                     help="after the timed region, also time K packed seeds per GPU and report them as "
                          "packed_seeds (default 8 for hc, 4 for the Humanoid configs; 0 = off)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="no GPU: every rank joins a gloo group and prints its rank and seeds (launch check)")
     args = ap.parse_args()
+
+    # --gpus N without a torch.distributed.run environment: relaunch as N ranks (one per GPU)
+    # through torch.distributed.run, from this process before anything touches the GPU, and
+    # exit with the launcher's status.  Under the launcher WORLD_SIZE must equal --gpus.
+    ws_env = os.environ.get("WORLD_SIZE")
+    if ws_env is None and args.gpus > 1:
+        raise SystemExit(spawn_ranks(args.gpus))
+    if int(ws_env or 1) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws_env}")
+    if args.plan_only:
+        plan_only(args)
+        return
 
     import torch
     from sac_eo.common.replicas import init_replica
@@ -328,6 +441,9 @@ def main():
     barrier = rep.barrier
 
     eng.step(args.warmup, num_timesteps=0, ts_increment=1)
+    # capture + instantiate + upload every graph the timed step(steps) replays (untimed;
+    # reported as graph_prepare_s): the timed region launches cached graphs only
+    cap_s = eng.prepare(args.steps)
     eng.sync()
     barrier()
     t0 = time.perf_counter()
@@ -339,12 +455,17 @@ def main():
     stats = eng.stats(1)[0]
     finite = bool(np.all(np.isfinite(stats)))
     value = args.steps * (1 if dp else ws * K) / el     # dp: every rank runs the same global update
-    roof = None
-    if rank == 0 and not args.no_roofline and not dp:
-        roof, _ = roofline(eng, args.config)
+    # secondary legs on rank 0, after the timed region; the roofline leg last (its ablated
+    # graph replay leaves the learner's state meaningless)
+    loop = None
+    if rank == 0 and K == 1 and not dp and not args.no_roofline:
+        loop = drop_in_loop(eng, cfgd)
     fit = roll = None
     if rank == 0 and cfgd["use_expert"] and K == 1:
         fit, roll = world_model_legs(eng, cfgd)
+    roof = None
+    if rank == 0 and not args.no_roofline and not dp:
+        roof, _ = roofline(eng, args.config)
     packed = None
     nleg = args.packed_leg if args.packed_leg >= 0 else (8 if args.config == "hc" else 4)
     if not dp and K == 1 and nleg > 1:
@@ -373,13 +494,15 @@ def main():
                                        f"replicas x{ws} x {K} packed seeds per GPU (independent seeds, no collective)"),
                        "seeds_per_gpu": K,
                        "sampler": "NumPy-legacy MT19937 stream on device (bit-exact indices)"},
-            "finite_stats": finite,
+            "finite_stats": finite, "graph_prepare_s": round(cap_s, 4),
             "last_stats": {k: float(v) for k, v in zip(
                 ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss", "nlp_mean", "step"], stats)},
             "roofline": roof, "cpu_baseline": cpu,
         }
         if fit is not None:
             line["model_fit"], line["rollout"] = fit, roll
+        if loop is not None:
+            line["drop_in_loop"] = loop
         if packed is not None:
             line["packed_seeds"] = packed
         print(json.dumps(line), flush=True)

@@ -154,6 +154,11 @@ int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t*
  * updates at one env step as in SAC.train). */
 int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment,
                   int32_t flags);
+/* Captures, instantiates and uploads every hipGraph that sacx_sac_step(h, n_steps, ..., flags)
+ * will replay (n_steps / graph_steps full graphs + one graph of the remainder), without
+ * running an update, so a following sacx_sac_step(n_steps) launches only cached graphs.
+ * (No reference counterpart: TF-eager has no capture step.)  Synchronous. */
+int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags);
 /* n_steps x _apply_model_grads (sac_eo/algs/mbrl_onpolicy_alg.py:301-319) as
  * called by SAC_exp._update_models (sac_eo/algs/SAC_expert.py:519-550): each
  * step fits both world models on their own minibatch and applies one Keras

@@ -689,7 +689,9 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                     const float (&bv)[4] = b[u][s & 1];
                     const shortx4 as = {bf16_bits(av[0]), bf16_bits(av[1]), bf16_bits(av[2]), bf16_bits(av[3])};
                     const shortx4 bs = {bf16_bits(bv[0]), bf16_bits(bv[1]), bf16_bits(bv[2]), bf16_bits(bv[3])};
-                    if (u & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc1[s], 0, 0, 0);
+                    // slab parity relative to it0, as gemm_core's 16x16 path (its groups of 4
+                    // start at it0): the same slabs land in acc0 / acc1 for any SACX_T32_NS
+                    if ((it + u - it0) & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc1[s], 0, 0, 0);
                     else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc0[s], 0, 0, 0);
                 }
                 continue;

@@ -1334,8 +1334,48 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     hipGraphExec_t exec;
     HIPCHK(h, hipGraphInstantiateWithFlags(&exec, graph, 0));
     HIPCHK(h, hipGraphDestroy(graph));
+    HIPCHK(h, hipGraphUpload(exec, h->stream));   // the first replay does not pay the upload
     if (!kt) h->graphs[key] = exec;
     *out = exec;
+    return 0;
+}
+
+// The graphs sacx_sac_step(n_steps) replays: n_steps / G full graphs of G updates, then the
+// remainder as ONE graph of exactly r updates (each graph pays its own sampler start-up and
+// alpha tail, so one remainder graph beats a chain of power-of-two pieces).  Up to
+// kMaxRemGraphs distinct remainder sizes are cached; beyond that a new remainder is split
+// into cached powers of two.  The returned list is what sacx_sac_step launches and what
+// sacx_prepare instantiates ahead of time.
+constexpr int kMaxRemGraphs = 24;
+
+int step_graph_list(sacx_handle* h, int64_t n_steps, bool ext, std::vector<std::pair<hipGraphExec_t, int64_t>>* out) {
+    out->clear();
+    const int G = ext ? 1 : h->graph_steps;
+    const int64_t q = n_steps / G;
+    int64_t r = n_steps % G;
+    if (q > 0) {
+        hipGraphExec_t g;
+        if (get_graph(h, G, !ext, &g)) return -1;
+        out->push_back({g, q});
+    }
+    if (r == 0) return 0;
+    int n_rem = 0;
+    for (const auto& kv : h->graphs)
+        if (std::get<0>(kv.first) != h->graph_steps && std::get<2>(kv.first) < 0) ++n_rem;
+    const bool exact = h->graphs.count(std::make_tuple((int)r, ext ? 0 : 1, -1)) > 0 || n_rem < kMaxRemGraphs;
+    if (exact) {
+        hipGraphExec_t g;
+        if (get_graph(h, (int)r, !ext, &g)) return -1;
+        out->push_back({g, 1});
+        return 0;
+    }
+    for (int p = 1 << 30; r > 0 && p >= 1; p >>= 1) {
+        if (p > r) continue;
+        hipGraphExec_t g;
+        if (get_graph(h, p, !ext, &g)) return -1;
+        out->push_back({g, 1});
+        r -= p;
+    }
     return 0;
 }
 
@@ -1631,25 +1671,22 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
         HIPCHK(h, hipGetLastError());
     } else {
-        const int G = ext ? 1 : h->graph_steps;
-        int64_t q = n_steps / G, r = n_steps % G;
-        if (q > 0) {
-            hipGraphExec_t g;
-            if (get_graph(h, G, !ext, &g)) return -1;
-            for (int64_t i = 0; i < q; ++i) HIPCHK(h, hipGraphLaunch(g, h->stream));
-        }
-        // remainder: cached graphs of decreasing powers of two (each graph pays its own
-        // sampler start-up and alpha tail, so a few long graphs beat many single updates)
-        for (int p = 1 << 30; r > 0 && p >= 1; p >>= 1) {
-            if (p > r || p >= G) continue;
-            hipGraphExec_t gp;
-            if (get_graph(h, p, !ext, &gp)) return -1;
-            HIPCHK(h, hipGraphLaunch(gp, h->stream));
-            r -= p;
-        }
+        std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
+        if (step_graph_list(h, n_steps, ext, &gl)) return -1;
+        for (const auto& g : gl)
+            for (int64_t i = 0; i < g.second; ++i) HIPCHK(h, hipGraphLaunch(g.first, h->stream));
     }
     h->seq_host += n_steps;
     if (h->nccl_failed) return fail(h, "ncclAllReduce failed");
+    return 0;
+}
+
+int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n_steps <= 0 || (flags & SACX_STEP_EAGER)) return 0;
+    std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
+    if (step_graph_list(h, n_steps, (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0, &gl)) return -1;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
 

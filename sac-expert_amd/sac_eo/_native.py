@@ -28,7 +28,7 @@ EXPORTS = [
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
     "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
-    "sacx_seed_select",
+    "sacx_seed_select", "sacx_prepare",
 ]
 
 
@@ -121,6 +121,7 @@ def lib():
         "sacx_rng_set_state": (ctypes.c_int, [vp, vp, i32, i32, f64]),
         "sacx_rng_get_state": (ctypes.c_int, [vp, vp, P(i32), P(i32), P(f64)]),
         "sacx_sac_step": (ctypes.c_int, [vp, i64, i64, i32, i32]),
+        "sacx_prepare": (ctypes.c_int, [vp, i64, i32]),
         "sacx_model_fit": (ctypes.c_int, [vp, vp, i64, i32]),
         "sacx_sync": (ctypes.c_int, [vp]),
         "sacx_plan_info": (ctypes.c_int, [vp, P(LaunchInfo), i32, P(i32)]),

@@ -408,6 +408,15 @@ class Engine:
         N.check(self.lib.sacx_sac_step(self.h, int(n), int(num_timesteps), int(ts_increment), flags),
                 self.h, "sac_step")
 
+    def prepare(self, n: int, external: bool = False) -> float:
+        """Instantiates every hipGraph a following ``step(n)`` replays (sacx_prepare) without
+        running an update; returns the host seconds it took (graph capture + instantiate)."""
+        import time
+        t0 = time.perf_counter()
+        N.check(self.lib.sacx_prepare(self.h, int(n), N.STEP_EXTERNAL_RANDOMS if external else 0),
+                self.h, "prepare")
+        return time.perf_counter() - t0
+
     def model_fit(self, idx: np.ndarray, eager: bool = False):
         """``idx[n, 2, model_batch]``: replay-logical rows of each model's minibatch per step
         (SAC_expert.py:519-543 -> _apply_model_grads)."""

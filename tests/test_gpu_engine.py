@@ -464,16 +464,19 @@ def test_rollout_graph_replay_equals_eager(gpu_available, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("K,use_expert,eager,t32", [(3, False, False, None), (3, True, False, None),
-                                                   (3, False, True, None), (4, False, False, None),
-                                                   (4, True, False, None), (4, False, False, "1")])
-def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, eager, t32):
+@pytest.mark.parametrize("K,use_expert,eager,t32,bf16", [(3, False, False, None, False), (3, True, False, None, False),
+                                                        (3, False, True, None, False), (4, False, False, None, False),
+                                                        (4, True, False, None, False), (4, False, False, "1", False),
+                                                        (4, False, False, "1", True), (4, False, False, "2", True)])
+def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, eager, t32, bf16):
     """cfg.seeds = K (the reference's --runs packed into one handle, grid z = seed): every
     seed ends bit-identical to a one-seed engine fed the same state, buffer, RNG stream and
     permutations -- stats, every parameter / Adam / target value, and the RNG key.  19
     updates = two 8-update graphs + remainder graphs.  At K = 4 the packed plan takes 32x32
     tiles for its forward / dX launches and the one-seed engines 16x16 (both with the
-    separate actor.head launch): the two tilings must agree bit for bit."""
+    separate actor.head launch): the two tilings must agree bit for bit -- in fp32 and with
+    bf16 MFMA operands (config C5: the 32x32 tiles split the k slabs over acc0 / acc1 exactly
+    as the 16x16 path does)."""
     from sac_eo.engine import Engine, EngineConfig
     n, B, N, eps = 19, 128, 3000, 0.1
     if K >= 4:                                  # the packed plan: 32x32 tiles ("1": dW + Adam too)
@@ -484,7 +487,8 @@ def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, ea
 
     def cfg(seeds):
         return EngineConfig(s_dim=17, a_dim=6, activation="tanh", batch=B, buffer_capacity=N, use_expert=use_expert,
-                            expert_capacity=20, expert_batch=20, graph_steps=8, epsilon=eps, seeds=seeds)
+                            expert_capacity=20, expert_batch=20, graph_steps=8, epsilon=eps, seeds=seeds,
+                            gemm_bf16=bf16)
 
     def drive(eng, k):
         _, st, buf, nrm, ex = learners[k]

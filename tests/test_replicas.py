@@ -66,3 +66,35 @@ def test_seed_derivation_known_answers():
     s2 = derive_seeds(0, runs=3)
     s3 = derive_seeds(0, runs=2, runs_start=1)
     assert np.array_equal(s2["setup"][1:], s3["setup"])
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """bench.py --gpus 2 (no launcher environment) relaunches itself as two ranks through
+    torch.distributed.run; each rank's learner seeds are run index = rank of the reference's
+    derivation (sac_eo/train.py:108-128).  --plan-only keeps it on the CPU (gloo)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--plan-only"],
+                         capture_output=True, text=True, timeout=240, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    ranks = sorted(line["ranks"], key=lambda r: r["rank"])
+    assert [r["rank"] for r in ranks] == [0, 1] and all(r["world_size"] == 2 for r in ranks)
+    ref = derive_seeds(0, runs=2)
+    for r in ranks:
+        for k, v in r["seeds"].items():
+            assert v == int(ref[k][r["rank"]])
+
+
+def test_bench_gpus_mismatch_fails_loudly():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "1", "--plan-only"],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert out.returncode != 0 and "WORLD_SIZE=2" in out.stderr
