@@ -173,6 +173,31 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
  * otherwise u = np.random.normal(size=(n,A)) from the device copy of the global stream,
  * in the order the reference would draw it.  Behaviour-policy inference for the env loop. */
 int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
+
+/* --- the reference objects' standalone network calls (device rows in, device rows out) -- */
+/* SquashedGaussianActor.evaluate (sac_eo/actors/continuous_actors.py:327-379) on s[n,S]:
+ * u = np.random.normal(size=(n, A)) from the device copy of the global stream, x = mu + std*u,
+ * pi_out[n,A] = act_limit*tanh(x), nlp_out[n] = neglogp_adjusted. */
+int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out, float* nlp_out);
+/* QCritic._forward / value (sac_eo/critics/critics.py:84-103) of net 0 / 1 (q_critics) or
+ * 2 / 3 (q_targets) on s[n,S], a[n,A]: out[n] = the [n,1] net output (value = 0), or that
+ * times max(ret_rms.std, 1e-8) (value = 1). */
+int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float* a, int64_t n, int32_t value,
+                        float* out);
+/* BaseWorldModel._forward + MSEModel.sample / step (sac_eo/models/base_world_model.py:65-87,
+ * sac_eo/models/continuous_models.py:225-254) of world model `model` on s[n,S], a[n,A].
+ * delta_clip / reward_clip > 0: --delta_clip_pred / --reward_clip_pred.  Outputs (each
+ * nullable): pred_out[n,S+1] = [delta_n | r_n] after the clips, sp_out[n,S] = s +
+ * delta_rms.denormalize(delta_n) (sample), r_out[n] = r_rms.denormalize(r_n) (step).
+ * Requires use_expert. */
+int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n, float delta_clip,
+                       float reward_clip, float* pred_out, float* sp_out, float* r_out);
+/* MSEModel.get_loss (continuous_models.py:280-302) of world model `model` on s, sp [n,S],
+ * a [n,A], r [n]: loss_out[0] = mean_i 0.5||clip(norm(sp-s)) - delta_pred||^2 +
+ * reward_loss_coef * 0.5 (clip(norm(r)) - r_pred)^2, the clips > 0 being --delta_clip_loss /
+ * --reward_clip_loss.  loss_out is device memory.  Requires use_expert. */
+int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* sp, const float* a, const float* r,
+                    int64_t n, float delta_clip_loss, float reward_clip_loss, float* loss_out);
 /* batch_simtrajectory_sampler (sac_eo/common/samplers.py:73-122) with world model `model`
  * as the environment (MSEModel.reset / step, sac_eo/models/continuous_models.py:225-258)
  * and the actor's sample() (continuous_actors.py:270-306), all on the device.

@@ -656,6 +656,67 @@ def calc_disc(st, cfg, nrm, s_e, a_e, rs=None, use_expert_actions=False, delta_c
 
 
 # ---------------------------------------------------------------------------
+# the reference objects' standalone network calls (the methods a caller
+# of the actor / critic / model objects uses)
+# ---------------------------------------------------------------------------
+def actor_evaluate(st, cfg, nrm, s, rs):
+    """SquashedGaussianActor.evaluate (continuous_actors.py:327-379): (pi, neglogp_adjusted)
+    with u = rs.normal(size=(n, A)) cast to f32."""
+    dt = st.alpha.dtype.type
+    nrm = nrm.cast(dt)
+    o, _ = mlp_forward(st.actor, _norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den), cfg.act)
+    mu, lraw = split_head(o, st.logstd, cfg)
+    u = f32_noise(rs.normal(size=mu.shape)).astype(dt)
+    pi, nlp, _ = head_evaluate(mu, lraw, u, cfg.act_limit, dt)
+    return pi, nlp
+
+
+def critic_forward(params, cfg, nrm, s, a, value=False):
+    """QCritic._forward ([n, 1]) / value (squeeze * max(ret std, 1e-8)) (critics.py:84-103)."""
+    dt = params[0].dtype.type
+    nrm = nrm.cast(dt)
+    x = np.concatenate([_norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den),
+                        _norm(np.asarray(a, dt), nrm.a_mean, nrm.a_den)], 1)
+    out, _ = mlp_forward(params, x, cfg.act)
+    return out[:, 0] * _F(dt, nrm.ret_den) if value else out
+
+
+def model_forward(st, cfg, nrm, k, s, a, delta_clip=0.0, reward_clip=0.0):
+    """BaseWorldModel._forward with the prediction clips (base_world_model.py:65-87) and what
+    MSEModel.sample / step make of it (continuous_models.py:225-254): (pred [n, S+1] after the
+    clips, sp = s + delta_rms.denormalize(delta_n), r = r_rms.denormalize(r_n))."""
+    dt = st.alpha.dtype.type
+    nrm = nrm.cast(dt)
+    s, a = np.asarray(s, dt), np.asarray(a, dt)
+    xm = np.concatenate([_norm(s, nrm.s_mean, nrm.s_den), _norm(a, nrm.a_mean, nrm.a_den)], 1)
+    out, _ = mlp_forward(st.models[k], xm, cfg.model_act)
+    dn, rn = out[:, :cfg.S].copy(), out[:, cfg.S].copy()
+    if delta_clip:
+        dn = np.clip(dn, -_F(dt, delta_clip), _F(dt, delta_clip))
+    if reward_clip:
+        rn = np.clip(rn, -_F(dt, reward_clip), _F(dt, reward_clip))
+    return (np.concatenate([dn, rn[:, None]], 1), s + (dn * nrm.d_den + nrm.d_mean), rn * nrm.r_den + nrm.r_mean)
+
+
+def model_loss(st, cfg, nrm, k, s, sp, a, r, delta_clip_loss=0.0, reward_clip_loss=0.0):
+    """MSEModel.get_loss (continuous_models.py:280-302): _forward(clip=False), the loss clips
+    on the normalised targets, mean over rows."""
+    dt = st.alpha.dtype.type
+    nrm = nrm.cast(dt)
+    s, sp, a, r = [np.asarray(x, dt) for x in (s, sp, a, r)]
+    pred, _, _ = model_forward(st, cfg, nrm, k, s, a)
+    dn = ((sp - s) - nrm.d_mean) / nrm.d_den
+    if delta_clip_loss:
+        dn = np.clip(dn, -_F(dt, delta_clip_loss), _F(dt, delta_clip_loss))
+    rn = (r - nrm.r_mean) / nrm.r_den
+    if reward_clip_loss:
+        rn = np.clip(rn, -_F(dt, reward_clip_loss), _F(dt, reward_clip_loss))
+    per = _F(dt, 0.5) * ((dn - pred[:, :cfg.S]) ** 2).sum(-1) + _F(dt, cfg.reward_loss_coef) * (
+        _F(dt, 0.5) * (rn - pred[:, cfg.S]) ** 2)
+    return float(np.mean(per))
+
+
+# ---------------------------------------------------------------------------
 # RNG consumption in the reference's order (SURVEY.md §8a, "RNG consumption
 # order"): the global legacy NumPy stream feeds the sampler and every noise
 # draw; the expert split uses the algorithm's Generator (base_onpolicy_alg.py:109).

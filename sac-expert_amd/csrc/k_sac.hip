@@ -2359,6 +2359,97 @@ void launch_roll(const RollArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_roll, dim3((a.n + 3) / 4), dim3(256), 0, s, a);
 }
 
+// ==================================================================== k_net_io
+// The reference objects' standalone network calls around the GEMM launches:
+//   mode 0: [s_rms.normalize(s) | a_rms.normalize(a) | 0] -> X (QCritic._forward,
+//           critics.py:89-94; BaseWorldModel._forward, base_world_model.py:67-70; the actor's
+//           _transform_state with a == null), one thread per element;
+//   mode 1: QCritic._forward -> [n, 1], value -> squeeze * max(ret_std, 1e-8)
+//           (critics.py:96-103), one thread per row;
+//   mode 2: BaseWorldModel._forward's clips + MSEModel.sample / step
+//           (continuous_models.py:225-254): sp = s + delta_rms.denormalize(delta_n),
+//           r = r_rms.denormalize(r_n); one wave per row;
+//   mode 3: MSEModel.get_loss (continuous_models.py:280-302) over a chunk of rows, one
+//           workgroup; the chunk sums chain through out0 in stream order, the last chunk
+//           writes reduce_mean to out1.
+__global__ __launch_bounds__(256) void k_net_io_elem(NetIOArgs g) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g.mode == 0) {
+        if (t >= (int64_t)g.n * g.ldX) return;
+        const int64_t i = t / g.ldX;
+        const int c = (int)(t - i * g.ldX);
+        float x = 0.f;
+        if (c < g.S) x = (g.s[i * g.S + c] - g.s_mean[c]) / g.s_den[c];
+        else if (g.a != nullptr && c < g.S + g.A) x = (g.a[i * g.A + (c - g.S)] - g.a_mean[c - g.S]) / g.a_den[c - g.S];
+        g.X[t] = x;
+        return;
+    }
+    if (t >= g.n) return;                   // mode 1
+    const float q = g.O[t * g.ldO];
+    g.out0[t] = g.value ? q * g.ret_den[0] : q;
+}
+
+__global__ __launch_bounds__(256) void k_net_io_rows(NetIOArgs g) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int S = g.S, O = S + 1;
+    if (g.mode == 2) {
+        const int64_t i = (int64_t)blockIdx.x * 4 + wave;
+        if (i >= g.n) return;
+        const float* Oi = g.O + i * g.ldO;
+        for (int j = lane; j <= S; j += 64) {
+            float v = Oi[j];
+            const float cl = j < S ? g.clip_d : g.clip_r;
+            if (cl > 0.f) v = fminf(fmaxf(v, -cl), cl);
+            if (g.out0 != nullptr) g.out0[i * O + j] = v;
+            if (j < S) {
+                if (g.out1 != nullptr) g.out1[i * S + j] = g.s[i * S + j] + (v * g.d_den[j] + g.d_mean[j]);
+            } else if (g.out2 != nullptr) {
+                g.out2[i] = v * g.r_norm[1] + g.r_norm[0];
+            }
+        }
+        return;
+    }
+    // mode 3: 0.5 ||clip(norm(sp - s)) - delta_pred||^2 + coef * 0.5 (clip(norm(r)) - r_pred)^2
+    __shared__ float part[4];
+    float acc = 0.f;
+    for (int64_t i = wave; i < g.n; i += 4) {
+        const float* Oi = g.O + i * g.ldO;
+        float sq = 0.f;
+        for (int j = lane; j < S; j += 64) {
+            float dn = ((g.sp[i * S + j] - g.s[i * S + j]) - g.d_mean[j]) / g.d_den[j];
+            if (g.clip_d > 0.f) dn = fminf(fmaxf(dn, -g.clip_d), g.clip_d);
+            const float e = dn - Oi[j];
+            sq = sq + e * e;
+        }
+        const float tot = wave_sum(sq);
+        float rn = (g.r[i] - g.r_norm[0]) / g.r_norm[1];
+        if (g.clip_r > 0.f) rn = fminf(fmaxf(rn, -g.clip_r), g.clip_r);
+        const float er = rn - Oi[S];
+        acc = acc + (0.5f * tot + g.reward_coef * (0.5f * (er * er)));
+    }
+    if (lane == 0) part[wave] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float sum = (part[0] + part[1]) + (part[2] + part[3]);
+        const float run = g.first ? sum : g.out0[0] + sum;
+        g.out0[0] = run;
+        if (g.last) g.out1[0] = run / (float)g.n_total;
+    }
+}
+
+void launch_net_io(const NetIOArgs& a, hipStream_t s) {
+    if (a.mode == 0) {
+        const int64_t tot = (int64_t)a.n * a.ldX;
+        hipLaunchKernelGGL(k_net_io_elem, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a);
+    } else if (a.mode == 1) {
+        hipLaunchKernelGGL(k_net_io_elem, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+    } else if (a.mode == 2) {
+        hipLaunchKernelGGL(k_net_io_rows, dim3((unsigned)((a.n + 3) / 4)), dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_net_io_rows, dim3(1), dim3(256), 0, s, a);
+    }
+}
+
 __global__ void k_set_pseq(Ctl* ctl, int slot, int64_t sstride) {
     ctl = sr(ctl, seed_off(sstride));
     ctl->pseq[slot] = ctl->step_seq;

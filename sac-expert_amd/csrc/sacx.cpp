@@ -309,6 +309,8 @@ void build_layout(sacx_handle* h) {
     h->add("act.H1", ACT_CAP, H0, F, 0);
     h->add("act.H2", ACT_CAP, H1, F, 0);
     h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
+    h->add("act.Xq", ACT_CAP, h->ldQ, F, 0);          // sacx_critic_forward input [norm s | norm a]
+    h->add("act.Q", ACT_CAP, 1, F, 0);                // sacx_critic_forward output
     if (h->cfg.use_expert) {          // world-model fitting (A16)
         const int R2 = 2 * h->mb, O = S + 1;
         h->add("mfit.idx", h->mfit_cap, R2, SACX_I32, SACX_ROLE_WORK);
@@ -1227,16 +1229,26 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         HIPCHK(h, hipEventRecord(evFork, cs));
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
         // Sampler batches [s, e): one k_rng launch draws updates s..e-1 in stream order and one
-        // gather fills their slots.  Sizes ramp 1, 2, 4, 4, ... so the first update of the graph
-        // waits for one update's draws only.  Slot u%nslot is last read through update u's folded
-        // alpha rows in update u+1's actor.head, so batch [s, e) is drawn after the actor.head of
-        // update e-nslot (at graph start when e <= nslot) and must be done before update s.
+        // gather fills their slots s % nslot .. s % nslot + (e - s) - 1 -- consecutive slots (the
+        // kernels address slot + u), so a batch never crosses a multiple of nbatch (nslot =
+        // 2 nbatch is one).  Sizes ramp 1, 2, 4, ... up to nbatch so the first update of the
+        // graph waits for one update's draws only.  Slot u%nslot is last read through update u's
+        // folded alpha rows in update u+1's actor.head, so batch [s, e) is drawn after the
+        // actor.head of update e-nslot (at graph start when e <= nslot) and must be done before
+        // update s.
         std::vector<std::pair<int, int>> batches;
         const int nbatch = h->nbatch, nslot = 2 * h->nbatch;
-        for (int s0 = 0, sz = 1; s0 < G; s0 += sz, sz = std::min(nbatch, 2 * sz))
-            batches.push_back({s0, std::min(G, s0 + std::min(nbatch, sz))});
-        for (int b = 0; b + 1 < (int)batches.size(); ++b)      // sizes must follow the ramp exactly
-            if (batches[b + 1].first != batches[b].second) return fail(h, "internal: sampler batches");
+        for (int s0 = 0, ramp = 1; s0 < G; ramp = std::min(nbatch, 2 * ramp)) {
+            const int sz = std::min({ramp, nbatch - s0 % nbatch, G - s0});
+            batches.push_back({s0, s0 + sz});
+            s0 += sz;
+        }
+        for (int b = 0; b < (int)batches.size(); ++b) {
+            const int s0 = batches[b].first, n = batches[b].second - s0;
+            if ((b + 1 < (int)batches.size() && batches[b + 1].first != batches[b].second) || n < 1 ||
+                s0 % nslot + n > nslot)
+                return fail(h, "internal: sampler batches");
+        }
         auto prologue = [&](int b) {
             const int j0 = batches[b].first, n = batches[b].second - j0;
             for (const Launch& L : h->plan[j0 % nslot]) {
@@ -1813,6 +1825,138 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
         a.alpha_mode = 0;
         FinalArgs f{};
         launch_actor_head(a, f, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+// ---------------------------------------------------------------- reference object methods
+static NetIOArgs netio_base(sacx_handle* h) {
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    NetIOArgs g{};
+    g.S = h->S; g.A = h->A;
+    g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den"); g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
+    g.d_mean = W("norm.d_mean"); g.d_den = W("norm.d_den"); g.r_norm = W("norm.r"); g.ret_den = W("norm.ret_den");
+    g.reward_coef = h->cfg.reward_loss_coef;
+    return g;
+}
+
+int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out, float* nlp_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n < 0 || (n > 0 && (!s || !pi_out || !nlp_out))) return fail(h, "bad arguments");
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS;
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    for (int64_t done = 0; done < n; done += ACT_CAP) {
+        const int m = (int)std::min<int64_t>(ACT_CAP, n - done);
+        RngArgs r{};                   // u = np.random.normal(size=np.shape(a_mean)) (:351)
+        r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
+        r.n_int = 0; r.n_norm = m * A; r.out_idx = nullptr; r.out_norm = W("act.noise");
+        r.slot = -1; r.reset_seq = 0; r.nupd = 1;
+        launch_rng(r, h->stream);
+        launch_obs_norm(s + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
+        std::vector<Launch> pl;
+        add_gemm(h, pl, "eval.fwd0", {prob_fwd(W("act.X"), ldS, m, S, W("actor.l0"), H0, W("act.H1"), h->act)}, false);
+        add_gemm(h, pl, "eval.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W("actor.l1"), H1, W("act.H2"), h->act)}, false);
+        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+        h->probs_cursor -= 2;
+        HeadArgs a{};
+        a.H2 = W("act.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.nseg = 1;
+        a.seg[0] = {0, m, 0, 0, W("act.noise"), nullptr, nlp_out + done, pi_out + done * A};   // mode 0: evaluate
+        a.total_rows = m;
+        a.cache_row0 = 1 << 30;
+        FinalArgs f{};
+        launch_actor_head(a, f, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float* a, int64_t n, int32_t value,
+                        float* out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (net < 0 || net > 3) return fail(h, "net must be 0..3 (q0, q1, t0, t1)");
+    if (n < 0 || (n > 0 && (!s || !a || !out))) return fail(h, "bad arguments");
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldQ = h->ldQ;
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    static const char* names[4] = {"q0", "q1", "t0", "t1"};
+    const std::string nm = names[net];
+    for (int64_t done = 0; done < n; done += ACT_CAP) {
+        const int m = (int)std::min<int64_t>(ACT_CAP, n - done);
+        NetIOArgs g = netio_base(h);
+        g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s + done * S; g.a = a + done * A; g.X = W("act.Xq");
+        launch_net_io(g, h->stream);
+        std::vector<Launch> pl;
+        add_gemm(h, pl, "critic.fwd0", {prob_fwd(W("act.Xq"), ldQ, m, S + A, W(nm + ".l0"), H0, W("act.H1"), h->act)}, false);
+        add_gemm(h, pl, "critic.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W(nm + ".l1"), H1, W("act.H2"), h->act)}, false);
+        add_gemm(h, pl, "critic.fwd2", {prob_fwd(W("act.H2"), H1, m, H1, W(nm + ".l2"), 1, W("act.Q"), ACT_NONE)}, false);
+        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+        h->probs_cursor -= 3;
+        g.mode = 1; g.O = W("act.Q"); g.ldO = 1; g.value = value ? 1 : 0; g.out0 = out + done;
+        launch_net_io(g, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+// the model net on rows [c0, c0 + m) of (s, a): roll.Xm -> roll.M1 -> roll.M2 -> roll.O
+static void model_net_chunk(sacx_handle* h, int32_t model, const float* s, const float* a, int m) {
+    const int S = h->S, A = h->A, ldQ = h->ldQ, Hm0 = h->Hm0, Hm1 = h->Hm1;
+    auto W = [&](const std::string& nm) { return h->f(nm); };
+    const std::string mn = "m" + std::to_string(model);
+    NetIOArgs g = netio_base(h);
+    g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s; g.a = a; g.X = W("roll.Xm");
+    launch_net_io(g, h->stream);
+    std::vector<Launch> pl;
+    add_gemm(h, pl, "model.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->mact)}, false);
+    add_gemm(h, pl, "model.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->mact)}, false);
+    add_gemm(h, pl, "model.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), S + 1, W("roll.O"), ACT_NONE)}, false);
+    for (auto& L : pl) launch_gemm(L.gemm, h->stream);
+    h->probs_cursor -= 3;
+}
+
+int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n, float delta_clip,
+                       float reward_clip, float* pred_out, float* sp_out, float* r_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
+    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (n < 0 || (n > 0 && (!s || !a))) return fail(h, "bad arguments");
+    const int S = h->S;
+    for (int64_t done = 0; done < n; done += ROLL_CAP) {
+        const int m = (int)std::min<int64_t>(ROLL_CAP, n - done);
+        model_net_chunk(h, model, s + done * S, a + done * h->A, m);
+        NetIOArgs g = netio_base(h);
+        g.mode = 2; g.n = m; g.s = s + done * S; g.O = h->f("roll.O"); g.ldO = S + 1;
+        g.clip_d = delta_clip; g.clip_r = reward_clip;
+        g.out0 = pred_out ? pred_out + done * (S + 1) : nullptr;
+        g.out1 = sp_out ? sp_out + done * S : nullptr;
+        g.out2 = r_out ? r_out + done : nullptr;
+        launch_net_io(g, h->stream);
+    }
+    HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* sp, const float* a, const float* r,
+                    int64_t n, float delta_clip_loss, float reward_clip_loss, float* loss_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
+    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (n <= 0 || !s || !sp || !a || !r || !loss_out) return fail(h, "bad arguments");
+    const int S = h->S, A = h->A;
+    for (int64_t done = 0; done < n; done += ROLL_CAP) {
+        const int m = (int)std::min<int64_t>(ROLL_CAP, n - done);
+        model_net_chunk(h, model, s + done * S, a + done * A, m);      // _forward(s, a, clip=False)
+        NetIOArgs g = netio_base(h);
+        g.mode = 3; g.n = m; g.s = s + done * S; g.sp = sp + done * S; g.r = r + done;
+        g.O = h->f("roll.O"); g.ldO = S + 1;
+        g.clip_d = delta_clip_loss; g.clip_r = reward_clip_loss;
+        g.out0 = h->f("roll.noise");           // running sum (workspace scalar)
+        g.out1 = loss_out;
+        g.first = done == 0; g.last = done + m >= n; g.n_total = n;
+        launch_net_io(g, h->stream);
     }
     HIPCHK(h, hipGetLastError());
     return 0;

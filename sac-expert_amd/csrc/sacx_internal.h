@@ -316,6 +316,29 @@ struct MGatherArgs {        // rows [0, 2*mb): model k = row / mb
     float* X; int32_t ldQ;      // [2mb, ldQ] = [s_n | a_n | 0]
     float* T;                   // [2mb, S+1] = [norm(sp - s) | norm(r)]
 };
+// ---------------------------------------------------------------- reference object methods
+// The standalone network calls of the reference's actor / critic / model objects
+// (sacx_critic_forward, sacx_actor_evaluate, sacx_model_forward, sacx_model_loss): the
+// rows a caller hands over, normalised into a GEMM input, and the net output turned into
+// what the reference method returns.
+struct NetIOArgs {
+    int32_t mode;               // 0: prep [norm s | norm a | 0] -> X; 1: critic output; 2: model
+                                // output (sample / step); 3: model loss (get_loss) of a chunk
+    int32_t n, S, A, ldX, ldO;
+    const float *s, *a, *sp, *r;   // caller rows of this chunk (a nullable in mode 0)
+    float* X;                      // mode 0: [n, ldX]
+    const float* O;                // modes 1-3: net output [n, ldO]
+    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den, *r_norm, *ret_den;
+    float clip_d, clip_r;          // > 0: clip_by_value(-clip, clip)
+    float reward_coef;
+    int32_t value;                 // mode 1: 1 = QCritic.value (x ret sigma), 0 = _forward
+    float* out0;                   // mode 1: [n]; mode 2: pred [n, S+1]; mode 3: running sum [1]
+    float* out1;                   // mode 2: sp [n, S]; mode 3: loss [1] (written on the last chunk)
+    float* out2;                   // mode 2: r [n]
+    int32_t first, last;           // mode 3: first / last chunk of the call
+    int64_t n_total;               // mode 3: rows of the whole call (reduce_mean)
+};
+
 struct MLossArgs {
     int32_t S, mb;
     const float* T; const float* O;   // [2mb, S+1]
@@ -389,6 +412,7 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
                      hipStream_t s);
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 void launch_roll(const RollArgs& a, hipStream_t s);
+void launch_net_io(const NetIOArgs& a, hipStream_t s);
 void launch_diag(const DiagArgs& a, hipStream_t s);
 void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s);
 void launch_alpha_apply(const FinalArgs& f, hipStream_t s);

@@ -28,7 +28,8 @@ EXPORTS = [
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
     "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
-    "sacx_seed_select", "sacx_prepare",
+    "sacx_seed_select", "sacx_prepare", "sacx_actor_evaluate", "sacx_critic_forward", "sacx_model_forward",
+    "sacx_model_loss",
 ]
 
 
@@ -128,6 +129,10 @@ def lib():
         "sacx_profile": (ctypes.c_int, [vp, i64, P(f64), i32]),
         "sacx_time_graph": (ctypes.c_int, [vp, i64, ctypes.c_char_p, P(f64)]),
         "sacx_actor_act": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+        "sacx_actor_evaluate": (ctypes.c_int, [vp, vp, i64, vp, vp]),
+        "sacx_critic_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, i32, vp]),
+        "sacx_model_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, f32, f32, vp, vp, vp]),
+        "sacx_model_loss": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, i64, f32, f32, vp]),
         "sacx_time_kernels": (ctypes.c_int, [vp, ctypes.c_char_p, i32, P(f64), P(f64), P(i64)]),
         "sacx_dp_unique_id": (ctypes.c_int, [vp, i32]),
         "sacx_resync": (ctypes.c_int, [vp]),

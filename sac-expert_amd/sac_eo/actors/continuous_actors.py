@@ -93,6 +93,20 @@ class SquashedGaussianActor:
         out = self._engine.act(np.asarray(s, np.float32), deterministic=deterministic)
         return _as_out(out.cpu().numpy())
 
+    def evaluate(self, s):
+        """(pi_action, neglogp_adjusted) of continuous_actors.py:327-379 on the GPU
+        (sacx_actor_evaluate): u = np.random.normal(size=(n, A)) from the device copy of the
+        global stream, x = mu + std * u, pi = act_limit * tanh(x).  One row (s of shape
+        [1, S] or [S]) gives pi [A] and a scalar neglogp, as the reference's squeeze does."""
+        if self._engine is None:
+            raise RuntimeError("actor is not bound to a device engine (build the algorithm first)")
+        x = np.asarray(s, np.float32)
+        pi, nlp = self._engine.evaluate(x.reshape(-1, self.s_dim))
+        pi, nlp = pi.cpu().numpy(), nlp.cpu().numpy()
+        if pi.shape[0] == 1:
+            pi, nlp = pi[0], nlp[0]
+        return _as_out(pi), _as_out(nlp)
+
     def clip(self, a):
         return np.clip(a, self.act_low, self.act_high)
 

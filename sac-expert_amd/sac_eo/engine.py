@@ -300,6 +300,62 @@ class Engine:
         self._keep_act = o
         return out[0] if single else out
 
+    def evaluate(self, s):
+        """SquashedGaussianActor.evaluate (continuous_actors.py:327-379) on the device:
+        s [n, S] -> (pi [n, A], neglogp [n]) CUDA tensors; draws normal(size=(n, A)) from the
+        device copy of the global NumPy stream."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        x = self._dev(s, (-1, S))
+        n = int(x.shape[0])
+        pi = torch.empty((n, A), dtype=torch.float32, device=self.device)
+        nlp = torch.empty((n,), dtype=torch.float32, device=self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        N.check(self.lib.sacx_actor_evaluate(self.h, p(x), n, p(pi), p(nlp)), self.h, "actor_evaluate")
+        self._keep_eval = x
+        return pi, nlp
+
+    def critic_forward(self, net: str, s, a, value: bool = False):
+        """QCritic._forward (value=False: [n, 1]) / value (value=True: [n], x ret sigma)
+        (critics.py:84-103) of net q0 / q1 / t0 / t1 on the device."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        x, u = self._dev(s, (-1, S)), self._dev(a, (-1, A))
+        n = int(x.shape[0])
+        if int(u.shape[0]) != n:
+            raise ValueError("s and a need the same number of rows")
+        out = torch.empty((n,), dtype=torch.float32, device=self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        N.check(self.lib.sacx_critic_forward(self.h, ("q0", "q1", "t0", "t1").index(net), p(x), p(u), n,
+                                             int(bool(value)), p(out)), self.h, "critic_forward")
+        self._keep_q = (x, u)
+        return out if value else out.reshape(n, 1)
+
+    def model_forward(self, model: int, s, a, delta_clip: float = 0.0, reward_clip: float = 0.0):
+        """BaseWorldModel._forward + MSEModel.sample / step (base_world_model.py:65-87,
+        continuous_models.py:225-254): -> (pred [n, S+1] = [delta_n | r_n] after the clips,
+        sp [n, S] = s + denormalised delta, r [n] = denormalised reward)."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        x, u = self._dev(s, (-1, S)), self._dev(a, (-1, A))
+        n = int(x.shape[0])
+        kw = dict(dtype=torch.float32, device=self.device)
+        pred, sp, r = torch.empty((n, S + 1), **kw), torch.empty((n, S), **kw), torch.empty((n,), **kw)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        N.check(self.lib.sacx_model_forward(self.h, int(model), p(x), p(u), n, float(delta_clip or 0.0),
+                                            float(reward_clip or 0.0), p(pred), p(sp), p(r)), self.h, "model_forward")
+        self._keep_m = (x, u)
+        return pred, sp, r
+
+    def model_loss(self, model: int, s, sp, a, r, delta_clip_loss: float = 0.0, reward_clip_loss: float = 0.0):
+        """MSEModel.get_loss (continuous_models.py:280-302) on the device -> float."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        x, y, u = self._dev(s, (-1, S)), self._dev(sp, (-1, S)), self._dev(a, (-1, A))
+        n = int(x.shape[0])
+        rr = self._dev(r, (n,))
+        out = torch.empty((1,), dtype=torch.float32, device=self.device)
+        p = lambda t: ctypes.c_void_p(t.data_ptr())
+        N.check(self.lib.sacx_model_loss(self.h, int(model), p(x), p(y), p(u), p(rr), n, float(delta_clip_loss or 0.0),
+                                         float(reward_clip_loss or 0.0), p(out)), self.h, "model_loss")
+        return float(out.item())
+
     def rollout(self, model: int, s_init, horizon: int, deterministic: bool = False,
                 delta_clip: float = 0.0, reward_clip: float = 0.0):
         """batch_simtrajectory_sampler (samplers.py:73-122) with world model `model` as the
