@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 3
+#define SACX_ABI_VERSION 4
 
 typedef struct sacx_handle sacx_handle;
 
@@ -82,6 +82,19 @@ typedef struct sacx_config {
     int32_t gemm_bf16;          /* 1: the MLP GEMMs take bf16 operands (rounded on load) with fp32
                                    accumulation, fp32 master weights / Adam (config C5); 0: fp32 */
     int32_t seeds;              /* independent learners packed in this handle (0/1 = one; <= 64) */
+    /* --- ABI 4 --- */
+    int32_t actor_gaussian;     /* 0: SquashedGaussianActor (SAC, continuous_actors.py:237-379); 1: GaussianActor
+                                   (:9-123), inference only (sacx_actor_act) -- an expert imported from a log
+                                   (sac_eo/train.py:65-86 builds it without actor_squash) */
+    float actor_std_mult;       /* --actor_std_mult (GaussianActor.logstd_init; 0 -> 1) */
+    int32_t actor_output_norm;  /* --actor_output_norm (GaussianActor mean normalisation) */
+    int32_t actor_layer_norm;   /* --actor_layer_norm: Dense -> LayerNormalization -> tanh on layer 0
+                                   (nn_utils.py:110-119) */
+    int32_t num_models;         /* --num_models for SAC-EO: 1 or 2 world models (0 -> 2) */
+    float model_max_grad_norm;  /* --model_max_grad_norm: clip_by_global_norm(grads, max_norm * num_models)
+                                   of the model fit (mbrl_onpolicy_alg.py:315-317); <= 0: None */
+    float delta_clip_loss;      /* --delta_clip_loss of MSEModel.get_loss in the model fit; <= 0: None */
+    float reward_clip_loss;     /* --reward_clip_loss of MSEModel.get_loss in the model fit; <= 0: None */
 } sacx_config;
 
 typedef struct sacx_segment {

@@ -452,7 +452,11 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     mse = None
     if expert is not None:
         eps = F(expert.epsilon)
-        halves = [(expert.s1, expert.sp1, expert.noise1), (expert.s2, expert.sp2, expert.noise2)]
+        # 2 models: the permuted halves (:301-335); 1 model (expert.s2 None): every expert row
+        # through model 0 (:290-296)
+        halves = [(expert.s1, expert.sp1, expert.noise1)]
+        if expert.s2 is not None:
+            halves.append((expert.s2, expert.sp2, expert.noise2))
         diffs = []
         caches = []
         for k, (se, spe, ne) in enumerate(halves):
@@ -466,7 +470,10 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
             sp_hat = se + (om[:, :S] * nrm.d_den + nrm.d_mean)
             diffs.append(spe - sp_hat)
             caches.append((se_n, hs_e, cache_e, xm, hsm, spe, sp_hat))
-        dl_e = F(0.5) * ((diffs[0] ** 2).sum(-1) + (diffs[1] ** 2).sum(-1))
+        if len(diffs) == 2:
+            dl_e = F(0.5) * ((diffs[0] ** 2).sum(-1) + (diffs[1] ** 2).sum(-1))
+        else:
+            dl_e = F(0.5) * (diffs[0] ** 2).sum(-1)
         mse = np.mean(dl_e)
         p_loss = (F(1) - eps) * p_loss + eps * mse
         ne_half = diffs[0].shape[0]
@@ -525,10 +532,14 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
 # world model: loss and one fitting step (continuous_models.py:280-302,
 # mbrl_onpolicy_alg.py:301-319)
 # ---------------------------------------------------------------------------
-def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches):
+def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches, max_grad_norm=None,
+                   delta_clip_loss=0.0, reward_clip_loss=0.0):
     """``batches`` = [(s, a, sp, r)] per model (independent minibatches,
-    SAC_expert.py:519-543).  Sum of the per-model mean losses, one Adam over
-    all model variables.  Returns the summed loss."""
+    SAC_expert.py:519-543; one entry per world model).  Sum of the per-model mean losses
+    (get_loss with the optional target clips, continuous_models.py:284-296), the optional
+    clip_by_global_norm(grads, max_grad_norm * num_models) (mbrl_onpolicy_alg.py:315-317,
+    TF clip_ops: scale = clip * min(1 / norm, 1 / clip)), one Adam over all model variables.
+    Returns the summed loss."""
     dt = st.alpha.dtype.type
     F = lambda x: _F(dt, x)
     nrm = nrm.cast(dt)
@@ -543,6 +554,10 @@ def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches):
         dpred, rpred = out[:, :S], out[:, S]
         dn = ((sp - s) - nrm.d_mean) / nrm.d_den
         rn = (r - nrm.r_mean) / nrm.r_den
+        if delta_clip_loss:
+            dn = np.clip(dn, -F(delta_clip_loss), F(delta_clip_loss))
+        if reward_clip_loss:
+            rn = np.clip(rn, -F(reward_clip_loss), F(reward_clip_loss))
         ed = dn - dpred
         er = rn - rpred
         per = F(0.5) * (ed * ed).sum(-1) + F(cfg.reward_loss_coef) * (F(0.5) * er * er)
@@ -552,7 +567,14 @@ def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches):
         dout[:, S] = -er * F(cfg.reward_loss_coef / n)
         g, _ = mlp_backward(st.models[k], xm, hs, dout, cfg.model_act)
         grads_all += g
-    adam_step(st.models[0] + st.models[1], grads_all, st.opt_model, cfg.lr_model, dt)
+    nm = len(batches)
+    if max_grad_norm:
+        clip = F(max_grad_norm * nm)
+        norm = np.sqrt(sum(np.sum(g * g) for g in grads_all)).astype(dt)
+        scale = clip * np.minimum(F(1) / norm, F(1) / clip)
+        grads_all = [g * scale for g in grads_all]
+    params = [w for k in range(nm) for w in st.models[k]]
+    adam_step(params, grads_all, st.opt_model, cfg.lr_model, dt)
     return float(loss_all)
 
 
@@ -671,6 +693,26 @@ def actor_evaluate(st, cfg, nrm, s, rs):
     return pi, nlp
 
 
+def gaussian_actor_sample(params, logstd_var, cfg, nrm, s, u, std_mult=1.0, output_norm=False):
+    """GaussianActor.sample (continuous_actors.py:74-123): mean (optionally output-normalised),
+    logstd = log(softplus(out_std)) (per_state_std) or the variable, + logstd_init, floored at
+    log(1e-3); a = mean + exp(logstd) * u (u = 0: deterministic).  No squash."""
+    dt = params[0].dtype.type
+    nrm = nrm.cast(dt)
+    out, _ = mlp_forward(params, _norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den), cfg.act)
+    A = cfg.A
+    if cfg.per_state_std:
+        mean, l = out[:, :A], np.log(softplus(out[:, A:]))
+        init = np.float32(np.log(std_mult) - np.log(np.log(2)))
+    else:
+        mean, l = out, np.broadcast_to(np.asarray(logstd_var, dt), out.shape)
+        init = np.float32(np.log(std_mult))
+    l = np.maximum(l + _F(dt, init), _F(dt, np.log(np.float32(1e-3))))
+    if output_norm:
+        mean = mean / np.maximum(np.mean(np.abs(mean), axis=-1, keepdims=True), _F(dt, 1.0))
+    return mean + np.exp(l) * np.asarray(u, dt)
+
+
 def critic_forward(params, cfg, nrm, s, a, value=False):
     """QCritic._forward ([n, 1]) / value (squeeze * max(ret std, 1e-8)) (critics.py:84-103)."""
     dt = params[0].dtype.type
@@ -721,12 +763,16 @@ def model_loss(st, cfg, nrm, k, s, sp, a, r, delta_clip_loss=0.0, reward_clip_lo
 # order"): the global legacy NumPy stream feeds the sampler and every noise
 # draw; the expert split uses the algorithm's Generator (base_onpolicy_alg.py:109).
 # ---------------------------------------------------------------------------
-def draw_step_randoms(rs, cur_size: int, B: int, A: int, n_expert: int = 0, gen=None):
+def draw_step_randoms(rs, cur_size: int, B: int, A: int, n_expert: int = 0, gen=None, n_models: int = 2):
     idx = rs.randint(cur_size, size=B)                          # buffers.py:136
     n1 = rs.normal(size=(B, A))                                 # target evaluate(sp)
     n2 = rs.normal(size=(B, A))                                 # actor evaluate(s)
     out = {"idx": idx, "noise_t": n1, "noise_pi": n2}
-    if n_expert:
+    if n_expert and n_models == 1:                              # SAC_expert.py:290-291: no shuffle
+        out["sections"] = [np.arange(n_expert)]
+        out["noise_e1"] = rs.normal(size=(n_expert, A))         # sample(s_expert)
+        out["noise_e2"] = None
+    elif n_expert:
         perm = np.arange(n_expert)
         gen.shuffle(perm)                                       # SAC_expert.py:301-303
         sec = np.array_split(perm, 2)

@@ -367,7 +367,20 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
     const float q2 = wave_sum(strided_rest(f.lq + f.B, f.B, v2)) / (float)f.B;
     float pl = wave_sum(strided_rest(f.lp, f.B, vp)) / (float)f.B;
     float mse = 0.f;
-    if (f.use_expert && f.ne > 0) {
+    if (f.use_expert && f.ne > 0 && f.nm == 1) {
+        // one model (SAC_expert.py:293-295): mean over the n_e rows of 0.5 ||sp_e - sp_pred||^2
+        float sm = 0.f;
+        const int nt = f.mse_tiles;
+        for (int i = lane; i < f.ne; i += 64) {
+            float a = 0.f;
+            for (int t = 0; t < nt; ++t) a += f.mse_rows[i * nt + t];
+            sm += 0.5f * a;
+        }
+        mse = wave_sum(sm) / (float)f.ne;
+        const float eps = f.ctl->epsilon;
+        pl = (1.f - eps) * pl + eps * mse;
+    } else if (f.use_expert && f.ne > 0) {
+        // two models (:329-335): row i pairs half 1 row i with half 2 row i
         const int h = f.ne / 2;
         float sm = 0.f;
         const int nt = f.mse_tiles;
@@ -1541,8 +1554,10 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
         }
     } else if (row < g.B + g.ne) {
         const int e = row - g.B;
+        // 2 models: the update's self.rng.shuffle permutation (SAC_expert.py:301-303); one model
+        // takes the expert rows in order (:290-295, no perm ring)
         const int64_t slot = g.ctl->pseq[g.slot] % g.perm_cap;
-        const int src = g.perm_ring[slot * g.ne + e];
+        const int src = g.perm_ring != nullptr ? g.perm_ring[slot * g.ne + e] : e;
         const __amdgpu_buffer_rsrc_t rse = rs(g.exp_s + (size_t)src * S), rspe = rs(g.exp_sp + (size_t)src * S);
         for (int c = lane; c < g.ldQ; c += 64) {
             const bool cs = c < S;
@@ -1640,6 +1655,23 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         }
         mu = mu + bmu;
         lraw = h.per_state_std ? lraw + bls : ls_pf;
+        if (sg.mode == 2) {
+            // GaussianActor.sample (continuous_actors.py:74-123), no squash: optional output
+            // normalisation of the mean, logstd = log(softplus(out)) (per_state_std) or the
+            // variable, + logstd_init, floored at log(1e-3); a = mean + exp(logstd) * u
+            float m = mu;
+            if (h.output_norm) {
+                const float s = wave_sum(jok ? fabsf(mu) : 0.f) / (float)A;
+                m = mu / fmaxf(s, 1.f);
+            }
+            if (jok) {
+                float l = h.per_state_std ? logf(softplus_f(lraw)) : lraw;
+                l = fmaxf(l + h.logstd_init, logf(1e-3f));
+                const float a = m + expf(l) * u_pf;
+                if (sg.pi_out != nullptr) sg.pi_out[(size_t)(row - sg.r0) * A + lane] = a;
+            }
+            return;
+        }
         float nlp_vec = 0.f, nlp_corr = 0.f;
         if (jok) {
             const int j = lane;
@@ -2276,7 +2308,8 @@ __global__ __launch_bounds__(256) void k_adam_apply(AdamApplyArgs a) {
     const int64_t tstep = (a.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
     const float lr_t = adam_lr(a.adam, a.group, tstep);
     float* P = a.P + i;
-    const float gr = P[3 * a.p_stride] * a.grad_scale;
+    float gr = P[3 * a.p_stride] * a.grad_scale;
+    if (a.scale_dev != nullptr) gr = gr * a.scale_dev[0];
     const float e0 = P[0], e1 = P[a.p_stride], e2 = P[2 * a.p_stride];
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
     const float mm1 = e1 + (gr - e1) * (1.f - b1);
@@ -2480,10 +2513,10 @@ namespace sacx {
 __global__ __launch_bounds__(256) void k_mgather(MGatherArgs g) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
-    if (row >= 2 * g.mb) return;
+    if (row >= g.nm * g.mb) return;
     const int S = g.S, A = g.A;
     const int64_t slot = g.ctl->mfit_seq % g.idx_cap;
-    const int64_t li = g.idx_ring[slot * 2 * g.mb + row];
+    const int64_t li = g.idx_ring[slot * g.nm * g.mb + row];
     const int64_t phys = (g.ctl->start + li) % g.cap;
     const float* rec = g.replay + phys * (int64_t)g.stride;
     for (int c = lane; c < g.ldQ; c += 64) {
@@ -2496,6 +2529,8 @@ __global__ __launch_bounds__(256) void k_mgather(MGatherArgs g) {
         float y;
         if (c < S) y = ((rec[S + A + c] - rec[c]) - g.d_mean[c]) / g.d_den[c];
         else y = (rec[2 * S + A] - g.r_norm[0]) / g.r_norm[1];
+        const float cl = c < S ? g.clip_d : g.clip_r;
+        if (cl > 0.f) y = fminf(fmaxf(y, -cl), cl);
         g.T[(size_t)row * (S + 1) + c] = y;
     }
 }
@@ -2503,7 +2538,7 @@ __global__ __launch_bounds__(256) void k_mgather(MGatherArgs g) {
 __global__ __launch_bounds__(256) void k_mloss(MLossArgs g) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
-    if (row >= 2 * g.mb) return;
+    if (row >= g.nm * g.mb) return;
     const int S = g.S, O = S + 1;
     const float inv = 1.f / (float)g.mb;
     float sq = 0.f, er = 0.f;
@@ -2527,12 +2562,12 @@ __global__ __launch_bounds__(64) void k_mfinal(MFinalArgs f) {
     float s0 = 0.f, s1 = 0.f;
     for (int i = lane; i < f.mb; i += 64) {
         s0 += f.loss_rows[i];
-        s1 += f.loss_rows[f.mb + i];
+        if (f.nm > 1) s1 += f.loss_rows[f.mb + i];
     }
     const float l0 = wave_sum(s0) / (float)f.mb, l1 = wave_sum(s1) / (float)f.mb;
     if (lane == 0) {
         const int64_t seq = f.ctl->mfit_seq;
-        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = l0 + l1;
+        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = f.nm > 1 ? l0 + l1 : l0;     // loss_all (:305-312)
         f.mstats[(size_t)(seq % f.mstats_cap) * 2 + 1] = (float)seq;
         f.ctl->t_model += 1;
         f.ctl->mfit_seq = seq + 1;
@@ -2540,10 +2575,39 @@ __global__ __launch_bounds__(64) void k_mfinal(MFinalArgs f) {
 }
 
 void launch_mgather(const MGatherArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_mgather, dim3((2 * a.mb + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_mgather, dim3((a.nm * a.mb + 3) / 4), dim3(256), 0, s, a);
 }
 void launch_mloss(const MLossArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_mloss, dim3((2 * a.mb + 3) / 4), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_mloss, dim3((a.nm * a.mb + 3) / 4), dim3(256), 0, s, a);
+}
+
+// clip_by_global_norm of the model gradients (see GNormArgs): per-chunk sums of squares in a
+// fixed order, then the norm and scale in one wave
+__global__ __launch_bounds__(256) void k_gnorm_part(GNormArgs a) {
+    __shared__ float red[4];
+    const int64_t chunk = (a.n + GNORM_PARTS - 1) / GNORM_PARTS;
+    const int64_t b0 = (int64_t)blockIdx.x * chunk, b1 = min(a.n, b0 + chunk);
+    float acc = 0.f;
+    for (int64_t i = b0 + threadIdx.x; i < b1; i += 256) acc = acc + a.g[i] * a.g[i];
+    const float w = wave_sum(acc);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = w;
+    __syncthreads();
+    if (threadIdx.x == 0) a.part[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(64) void k_gnorm_final(GNormArgs a) {
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < GNORM_PARTS; i += 64) acc = acc + a.part[i];
+    const float tot = wave_sum(acc);
+    if (threadIdx.x == 0) {
+        const float norm = sqrtf(tot);
+        a.scale_out[0] = a.clip * fminf(1.f / norm, 1.f / a.clip) + (norm - norm);
+    }
+}
+
+void launch_gnorm(const GNormArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_gnorm_part, dim3(GNORM_PARTS), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gnorm_final, dim3(1), dim3(64), 0, s, a);
 }
 void launch_mfinal(const MFinalArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_mfinal, dim3(1), dim3(64), 0, s, a);

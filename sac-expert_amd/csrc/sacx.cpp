@@ -61,7 +61,8 @@ struct SegInfo {
 };
 
 struct Launch {
-    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, FINAL, MGATHER, MLOSS, MFINAL, ALLREDUCE, APPLY, AAPPLY } kind;
+    enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, FINAL, MGATHER, MLOSS, MFINAL, ALLREDUCE, APPLY, AAPPLY,
+                GNORM } kind;
     std::string name;
     RngArgs rng;
     GatherArgs gather;
@@ -74,6 +75,7 @@ struct Launch {
     MLossArgs ml;
     MFinalArgs mf;
     AdamApplyArgs ap;          // APPLY
+    GNormArgs gn;              // GNORM
     float* ar_buf = nullptr;   // ALLREDUCE: in-place sum over the data-parallel ranks
     int64_t ar_count = 0;
     int grid = 0, block = 256;
@@ -102,6 +104,7 @@ const char* kernel_family(Launch::Kind k) {
         case Launch::ALLREDUCE: return "rccl_allreduce";
         case Launch::APPLY: return "k_adam_apply";
         case Launch::AAPPLY: return "k_alpha_apply";
+        case Launch::GNORM: return "k_gnorm";
     }
     return "?";
 }
@@ -116,6 +119,7 @@ struct sacx_handle {
     int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0, act = 0, mact = 0;
     int64_t cap = 0;
     int graph_steps = 128, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
+    int nm = 0;               // SAC-EO world models (--num_models: 1 or 2)
     // layout
     std::vector<SegInfo> segs;
     std::map<std::string, size_t> seg_index;
@@ -209,7 +213,7 @@ void build_layout(sacx_handle* h) {
     h->add("alpha", 1, 1, F, SACX_ROLE_PARAM);
     if (h->cfg.use_expert) {
         net("m0", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
-        net("m1", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
+        if (h->nm > 1) net("m1", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
     }
     const uint64_t pbytes = (h->arena_bytes + 255) & ~uint64_t(255);
     h->param_off = 0;
@@ -312,8 +316,9 @@ void build_layout(sacx_handle* h) {
     h->add("act.Xq", ACT_CAP, h->ldQ, F, 0);          // sacx_critic_forward input [norm s | norm a]
     h->add("act.Q", ACT_CAP, 1, F, 0);                // sacx_critic_forward output
     if (h->cfg.use_expert) {          // world-model fitting (A16)
-        const int R2 = 2 * h->mb, O = S + 1;
+        const int R2 = h->nm * h->mb, O = S + 1;
         h->add("mfit.idx", h->mfit_cap, R2, SACX_I32, SACX_ROLE_WORK);
+        h->add("ws.gnorm", 1, GNORM_PARTS + 1, F, 0);   // clip_by_global_norm partials + scale
         h->add("mstats", h->stats_cap, 2, F, SACX_ROLE_STATE);
         h->add("ws.Xf", R2, h->ldQ, F, 0);
         h->add("ws.Tf", R2, O, F, 0);
@@ -537,6 +542,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     h->probs_cursor = 0;
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
+    // expert rows of world model k: [k * half, (k + 1) * half) with 2 models, all with one
+    const int nm = h->nm, mrows = nm == 1 ? ne : half;
     const int ldS = h->ldS, ldQ = h->ldQ, act = h->act, mact = h->mact;
     const bool eo = h->cfg.use_expert != 0;
     const std::string sl = "slot" + std::to_string(slot);
@@ -590,7 +597,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         g.Xa = Xa; g.ldS = ldS; g.Xq = Xq; g.Xt = Xt; g.Xp = Xp; g.Xm = Xm; g.ldQ = ldQ;
         g.r = r_in; g.d = d_in; g.slot = slot; g.nupd = 1; g.slot_bytes = h->slot_bytes;
         g.exp_s = W("expert.s"); g.exp_sp = W("expert.sp");
-        g.perm_ring = h->ptr<int32_t>("perm"); g.perm_cap = h->perm_cap;
+        g.perm_ring = h->nm == 1 ? nullptr : h->ptr<int32_t>("perm"); g.perm_cap = h->perm_cap;
         g.se_raw = se_raw; g.spe_raw = spe_raw;
         L.grid = (B + ne + 3) / 4;
         L.bytes = 4.0 * (B * (2.0 * S + A + 2) + ne * 2.0 * S) + 4.0 * (B * (2.0 * ldS + 3.0 * ldQ + 2));
@@ -715,11 +722,11 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act));
         }
         if (eo) {
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
-                p0.push_back(prob_fwd(Xm + (size_t)k * half * ldQ, ldQ, half, S + A, W(n + ".l0"), Hm0,
+                p0.push_back(prob_fwd(Xm + (size_t)k * half * ldQ, ldQ, mrows, S + A, W(n + ".l0"), Hm0,
                                       Hm1b + (size_t)k * half * Hm0, mact));
-                p1.push_back(prob_fwd(Hm1b + (size_t)k * half * Hm0, Hm0, half, Hm0, W(n + ".l1"), Hm1,
+                p1.push_back(prob_fwd(Hm1b + (size_t)k * half * Hm0, Hm0, mrows, Hm0, W(n + ".l1"), Hm1,
                                       Hm2b + (size_t)k * half * Hm1, mact));
             }
         }
@@ -803,16 +810,16 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> pm;
         const int O = S + 1, mtn = (S + 15) / 16;
         if (eo) {
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
                 GemmProb p{};
                 p.A = Hm2b + (size_t)k * half * Hm1; p.lda = Hm1; p.a_kc = 1; p.ones_row = -1;
                 p.B = W(n + ".l2"); p.ldb = O; p.b_kc = 0;           // W_ext [(Hm1+1) x (S+1)]
-                p.M = half; p.N = S; p.K = Hm1;                      // delta-s columns only
+                p.M = mrows; p.N = S; p.K = Hm1;                     // delta-s columns only
                 p.bias = W(n + ".l2") + (size_t)Hm1 * O;
                 p.C = W("ws.dout") + (size_t)k * half * S; p.ldc = S;
                 p.epi = EPI_FWD; p.act = ACT_NONE;
-                p.mse = 1; p.grad_scale = 1.f / (float)half;
+                p.mse = 1; p.grad_scale = 1.f / (float)mrows;       // MSE_loss = mean over the rows
                 p.se_raw = se_raw + (size_t)k * half * S; p.spe_raw = spe_raw + (size_t)k * half * S;
                 p.dmean = W("norm.d_mean"); p.dden = W("norm.d_den");
                 p.part = W("ws.mse") + (size_t)k * half * mtn;
@@ -852,9 +859,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             pb.push_back(p);
         }
         if (eo) {                            // Dm2 = dout . Wm2[:, :S]^T (.) act'(Hm2)
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
-                GemmProb p = prob_dx(W("ws.dout") + (size_t)k * half * S, half, S, W(n + ".l2"), Hm1,
+                GemmProb p = prob_dx(W("ws.dout") + (size_t)k * half * S, mrows, S, W(n + ".l2"), Hm1,
                                      Hm2b + (size_t)k * half * Hm1, Dm2 + (size_t)k * half * Hm1, mact);
                 p.ldb = O;                           // B[n][k] = W_ext[n][k], row stride S+1
                 pb.push_back(p);
@@ -872,9 +879,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         }
         if (eo) {                            // Dm1 = Dm2 . Wm1^T (.) act'(Hm1), for actor.head.bwd
             std::vector<GemmProb> pd;
-            for (int k = 0; k < 2; ++k) {
+            for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
-                pd.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, half, Hm1, W(n + ".l1"), Hm0,
+                pd.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, mrows, Hm1, W(n + ".l1"), Hm0,
                                      Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
             }
             add_gemm(h, plan, "model.bwd1", pd, record_probs);
@@ -889,7 +896,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.B = B; b.ne = ne; b.S = S; b.A = A; b.Aout = Aout; b.H0 = H0; b.H1 = H1; b.Hm0 = Hm0;
         b.per_state_std = h->cfg.per_state_std; b.lim = h->cfg.act_limit;
         b.Dp1 = Dp1; b.Wq1[0] = W("q0.l0"); b.Wq1[1] = W("q1.l0");
-        b.Dm1 = Dm1; b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W("m1.l0") : nullptr;
+        b.Dm1 = Dm1; b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W(nm > 1 ? "m1.l0" : "m0.l0") : nullptr;
         b.a_den = W("norm.a_den"); b.alpha = W("alpha"); b.ctl = h->ctl(); b.use_expert = eo;
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
         b.W3a = W("actor.l2"); b.Ha2 = Ha2 + (size_t)B * H1; b.act = act;
@@ -951,7 +958,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         f.ctl = h->ctl();
         f.adam = plan[plan.size() - 2].gemm.adam;   // alpha.fwd's Adam constants
         f.target_entropy = h->cfg.target_entropy;
-        f.B = B; f.ne = ne; f.use_expert = eo;
+        f.B = B; f.ne = ne; f.use_expert = eo; f.nm = nm;
         f.lq = W("ws.lq"); f.lp = W("ws.lp"); f.mse_rows = W("ws.mse"); f.red = W("red");
         f.mse_tiles = (S + 15) / 16;
         f.stats = W("stats"); f.stats_cap = h->stats_cap;
@@ -993,6 +1000,7 @@ void build_model_plan(sacx_handle* h) {
     plan.clear();
     if (!h->cfg.use_expert) return;
     const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ, mact = h->mact;
+    const int nm = h->nm;
     auto W = [&](const std::string& n) { return h->f(n); };
     float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Hf1 = W("ws.Hf1"), *Hf2 = W("ws.Hf2"), *Of = W("ws.Of");
     float *Df3 = W("ws.Df3"), *Df2 = W("ws.Df2"), *Df1 = W("ws.Df1");
@@ -1005,13 +1013,14 @@ void build_model_plan(sacx_handle* h) {
         g.idx_ring = h->ptr<int32_t>("mfit.idx"); g.idx_cap = h->mfit_cap; g.ctl = h->ctl();
         g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den"); g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
         g.d_mean = W("norm.d_mean"); g.d_den = W("norm.d_den"); g.r_norm = W("norm.r");
-        g.X = Xf; g.ldQ = ldQ; g.T = Tf;
-        L.grid = (2 * mb + 3) / 4;
-        L.bytes = 4.0 * 2 * mb * (2.0 * S + A + 1 + ldQ + O);
+        g.X = Xf; g.ldQ = ldQ; g.T = Tf; g.nm = nm;
+        g.clip_d = h->cfg.delta_clip_loss; g.clip_r = h->cfg.reward_clip_loss;
+        L.grid = (nm * mb + 3) / 4;
+        L.bytes = 4.0 * nm * mb * (2.0 * S + A + 1 + ldQ + O);
         plan.push_back(L);
     }
     std::vector<GemmProb> f0, f1, f2, b2, b1, w;
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < nm; ++k) {
         const std::string n = "m" + std::to_string(k);
         const size_t r0 = (size_t)k * mb;
         f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, mact));
@@ -1030,20 +1039,51 @@ void build_model_plan(sacx_handle* h) {
         Launch L{};
         L.kind = Launch::MLOSS;
         L.name = "model.loss";
-        L.ml.S = S; L.ml.mb = mb; L.ml.T = Tf; L.ml.O = Of; L.ml.D3 = Df3; L.ml.loss_rows = W("ws.lf");
+        L.ml.S = S; L.ml.mb = mb; L.ml.nm = nm; L.ml.T = Tf; L.ml.O = Of; L.ml.D3 = Df3; L.ml.loss_rows = W("ws.lf");
         L.ml.reward_coef = h->cfg.reward_loss_coef;
-        L.grid = (2 * mb + 3) / 4;
-        L.bytes = 4.0 * 2 * mb * O * 3;
+        L.grid = (nm * mb + 3) / 4;
+        L.bytes = 4.0 * nm * mb * O * 3;
         plan.push_back(L);
     }
     add_gemm(h, plan, "model.bwd2", b2, false);
     add_gemm(h, plan, "model.bwd1", b1, false);
     add_gemm(h, plan, "model.adam", w, false);
+    if (h->cfg.model_max_grad_norm > 0.f) {
+        // --model_max_grad_norm (mbrl_onpolicy_alg.py:315-317): the dW launch stores the
+        // gradients (+3 p_stride); their global norm gives one scale; Adam applies g * scale
+        Launch& G = plan.back();
+        for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
+        G.name = "model.grad";
+        const std::string last = nm > 1 ? "m1.l2" : "m0.l2";
+        const uint64_t o0 = h->off_of("m0.l0");
+        const SegInfo& sl = h->seg(last);
+        const int64_t n = (int64_t)((sl.off + (uint64_t)(sl.rows * sl.cols) * 4 - o0) / 4);
+        float* P = h->f("m0.l0");
+        Launch N{};
+        N.kind = Launch::GNORM;
+        N.name = "model.gnorm";
+        N.gn.g = P + 3 * h->p_stride; N.gn.n = n;
+        N.gn.part = W("ws.gnorm"); N.gn.scale_out = W("ws.gnorm") + GNORM_PARTS;
+        N.gn.clip = (float)((double)h->cfg.model_max_grad_norm * nm);    // max_norm * self.B
+        N.grid = GNORM_PARTS;
+        N.bytes = 4.0 * n;
+        plan.push_back(N);
+        Launch U{};
+        U.kind = Launch::APPLY;
+        U.name = "model.adam";
+        AdamApplyArgs& a = U.ap;
+        a.P = P; a.n = n; a.p_stride = h->p_stride; a.group = GRP_MODEL; a.t_off = 0;
+        a.grad_scale = 1.f; a.scale_dev = N.gn.scale_out;
+        a.ctl = h->ctl(); a.adam = G.gemm.adam;
+        U.grid = (int)((n + 255) / 256);
+        U.bytes = 4.0 * n * 7;
+        plan.push_back(U);
+    }
     {
         Launch L{};
         L.kind = Launch::MFINAL;
         L.name = "model.final";
-        L.mf.ctl = h->ctl(); L.mf.loss_rows = W("ws.lf"); L.mf.mb = mb;
+        L.mf.ctl = h->ctl(); L.mf.loss_rows = W("ws.lf"); L.mf.mb = mb; L.mf.nm = nm;
         L.mf.mstats = W("mstats"); L.mf.mstats_cap = h->stats_cap;
         L.grid = 1;
         L.block = 64;
@@ -1069,6 +1109,7 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
             break;
         case Launch::APPLY: launch_adam_apply(L.ap, s); break;
         case Launch::AAPPLY: launch_alpha_apply(L.fin, s); break;
+        case Launch::GNORM: launch_gnorm(L.gn, s); break;
     }
 }
 
@@ -1415,14 +1456,17 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     if (cfg->batch <= 0 || cfg->buffer_capacity <= 0) return bad("batch/buffer_capacity must be positive");
     if (cfg->buffer_capacity >= (int64_t(1) << 31)) return bad("buffer_capacity must be < 2^31");
     if (cfg->use_expert) {
-        if (cfg->expert_batch <= 0 || (cfg->expert_batch & 1))
-            return bad("expert_batch must be positive and even (SAC_expert.py:329-332 adds equal halves)");
+        if (cfg->expert_batch <= 0 || ((cfg->expert_batch & 1) && cfg->num_models != 1))
+            return bad("expert_batch must be positive and even with 2 models (SAC_expert.py:329-332 adds equal halves)");
         if (cfg->expert_capacity < cfg->expert_batch) return bad("expert_capacity < expert_batch");
         if (cfg->model_hidden[0] <= 0 || cfg->model_hidden[1] <= 0) return bad("model sizes must be positive");
         if (cfg->model_hidden[0] > 512 || cfg->model_hidden[1] > 512) return bad("model hidden sizes > 512 unsupported");
         if (cfg->model_activation < 0 || cfg->model_activation > 2) return bad("model activation invalid");
         if (cfg->s_dim + 1 > 512) return bad("s_dim > 511 unsupported by the model MSE head");
     }
+    if (cfg->num_models < 0 || cfg->num_models > 2) return bad("num_models must be 1 or 2 (0 -> 2)");
+    if (cfg->actor_gaussian && cfg->actor_std_mult < 0.f) return bad("actor_std_mult must be positive");
+    if (cfg->actor_layer_norm) return bad("actor_layer_norm is not built");
     auto* h = new sacx_handle();
     h->cfg = *cfg;
     h->S = cfg->s_dim;
@@ -1439,6 +1483,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->Hm1 = cfg->use_expert ? cfg->model_hidden[1] : 0;
     h->mact = cfg->model_activation;
     h->mb = cfg->use_expert ? (cfg->model_batch > 0 ? cfg->model_batch : 200) : 0;
+    h->nm = cfg->use_expert ? (cfg->num_models > 0 ? cfg->num_models : 2) : 0;
     h->ldS = (int)r4(h->S);
     h->ldQ = (int)r4(h->S + h->A);
     h->stride = (int)r4(2 * h->S + h->A + 2);
@@ -1676,6 +1721,7 @@ int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t*
 
 int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n_steps <= 0) return 0;
     launch_set_ctl(h->ctl0(), num_timesteps, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
@@ -1708,7 +1754,7 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
     if (h->seeds > 1) return fail(h, "model_fit needs seeds = 1");
     if (n_steps <= 0) return 0;
     if (!idx) return fail(h, "null index array");
-    const int R2 = 2 * h->mb;
+    const int R2 = h->nm * h->mb;
     int32_t* ring = h->ptr<int32_t>("mfit.idx");
     for (int64_t done = 0; done < n_steps;) {
         const int64_t chunk = std::min<int64_t>(n_steps - done, h->mfit_cap);
@@ -1819,7 +1865,13 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         a.nseg = 1;
-        a.seg[0] = {0, m, 1, 0, noise, nullptr, nullptr, act_out + done * A};
+        // SquashedGaussianActor.sample (mode 1) or GaussianActor.sample (mode 2)
+        a.seg[0] = {0, m, h->cfg.actor_gaussian ? 2 : 1, 0, noise, nullptr, nullptr, act_out + done * A};
+        if (h->cfg.actor_gaussian) {          // logstd_init (continuous_actors.py:39-44), f32
+            const double sm = h->cfg.actor_std_mult > 0.f ? h->cfg.actor_std_mult : 1.0;
+            a.logstd_init = (float)(std::log(sm) - (h->cfg.per_state_std ? std::log(std::log(2.0)) : 0.0));
+            a.output_norm = h->cfg.actor_output_norm;
+        }
         a.total_rows = m;
         a.cache_row0 = 1 << 30;
         a.alpha_mode = 0;
@@ -1843,6 +1895,7 @@ static NetIOArgs netio_base(sacx_handle* h) {
 
 int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out, float* nlp_out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n < 0 || (n > 0 && (!s || !pi_out || !nlp_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS;
     auto W = [&](const std::string& nm) { return h->f(nm); };
@@ -1921,7 +1974,7 @@ int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const floa
                        float reward_clip, float* pred_out, float* sp_out, float* r_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
-    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (model < 0 || model >= h->nm) return fail(h, "model index out of range (num_models)");
     if (n < 0 || (n > 0 && (!s || !a))) return fail(h, "bad arguments");
     const int S = h->S;
     for (int64_t done = 0; done < n; done += ROLL_CAP) {
@@ -1943,7 +1996,7 @@ int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* 
                     int64_t n, float delta_clip_loss, float reward_clip_loss, float* loss_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
-    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (model < 0 || model >= h->nm) return fail(h, "model index out of range (num_models)");
     if (n <= 0 || !s || !sp || !a || !r || !loss_out) return fail(h, "bad arguments");
     const int S = h->S, A = h->A;
     for (int64_t done = 0; done < n; done += ROLL_CAP) {
@@ -2028,7 +2081,7 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
                  float* r_out, float* sp_out, uint8_t* d_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "rollout needs the world models (use_expert)");
-    if (model < 0 || model > 1) return fail(h, "model index out of range");
+    if (model < 0 || model >= h->nm) return fail(h, "model index out of range (num_models)");
     if (n < 0 || horizon < 0) return fail(h, "bad arguments");
     if (n == 0 || horizon == 0) return 0;
     if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
@@ -2070,6 +2123,7 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     if (!h->cfg.use_expert) return fail(h, "expert diagnostics need the world models (use_expert)");
     if (n <= 0 || n > ROLL_CAP / 2) return fail(h, "expert rows must be in [1, 2048]");
     const bool disc = (flags & SACX_DIAG_DISC) != 0, ea = (flags & SACX_DIAG_EXPERT_ACTIONS) != 0;
+    if (disc && h->nm < 2) return fail(h, "_calc_disc compares two world models (num_models = 2)");
     if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
@@ -2083,8 +2137,8 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     auto models = [&]() {
         std::vector<Launch> pl;
         std::vector<GemmProb> p0, p1, p2;
-        for (int k = 0; k < 2; ++k) {
-            const std::string mn = "m" + std::to_string(k);
+        for (int k = 0; k < 2; ++k) {             // one model: its MSE twice (the mean is exact)
+            const std::string mn = h->nm > 1 ? "m" + std::to_string(k) : std::string("m0");
             float* M1 = W("roll.M1") + (size_t)k * n * Hm0;
             float* M2 = W("roll.M2") + (size_t)k * n * Hm1;
             p0.push_back(prob_fwd(W("roll.Xm"), ldQ, n, S + A, W(mn + ".l0"), Hm0, M1, h->mact));

@@ -112,6 +112,7 @@ struct FinalArgs {
     const float* mse_rows;  // [ne, mse_tiles] per-column-tile partial sums of diff^2
     float* red;             // partial slots
     int32_t nred;           // number of partials (alpha.head workgroups)
+    int32_t nm;             // SAC-EO world models (1: every expert row through model 0)
     int32_t mse_tiles;      // partials per expert row in mse_rows
     float* stats; int32_t stats_cap;
     // data-parallel mode: the local alpha gradient goes here (then an all-reduce and
@@ -159,7 +160,8 @@ struct QHeadArgs {
 
 struct HeadSeg {
     int32_t r0, r1;        // actor rows [r0, r1)
-    int32_t mode;          // 0 = evaluate (neglogp), 1 = sample (no neglogp)
+    int32_t mode;          // 0 = evaluate (neglogp), 1 = sample (no neglogp), 2 = GaussianActor.sample
+                           // (no squash; pi_out only)
     int32_t xq_row0;       // first row in xq_out
     const float* noise;    // [r1-r0, A]
     float* xq_out;         // normalised action -> xq_out[(xq_row0 + i) * ldQ + S + j]
@@ -174,6 +176,8 @@ struct HeadArgs {
     int32_t H1, A, Aout, S, ldQ, per_state_std;
     float lim;
     const float *a_mean, *a_den;
+    float logstd_init;     // mode 2: GaussianActor.logstd_init (continuous_actors.py:39-44)
+    int32_t output_norm;   // mode 2: --actor_output_norm (continuous_actors.py:68-72)
     int32_t nseg;
     HeadSeg seg[4];
     int32_t total_rows;
@@ -315,6 +319,8 @@ struct MGatherArgs {        // rows [0, 2*mb): model k = row / mb
     const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den)
     float* X; int32_t ldQ;      // [2mb, ldQ] = [s_n | a_n | 0]
     float* T;                   // [2mb, S+1] = [norm(sp - s) | norm(r)]
+    int32_t nm;                 // world models fitted (rows [0, nm*mb))
+    float clip_d, clip_r;       // > 0: --delta_clip_loss / --reward_clip_loss on T (get_loss :286-296)
 };
 // ---------------------------------------------------------------- reference object methods
 // The standalone network calls of the reference's actor / critic / model objects
@@ -340,7 +346,7 @@ struct NetIOArgs {
 };
 
 struct MLossArgs {
-    int32_t S, mb;
+    int32_t S, mb, nm;
     const float* T; const float* O;   // [2mb, S+1]
     float* D3;                        // dL/dout [2mb, S+1]
     float* loss_rows;                 // [2mb]
@@ -348,7 +354,7 @@ struct MLossArgs {
 };
 struct MFinalArgs {
     Ctl* ctl;
-    const float* loss_rows; int32_t mb;
+    const float* loss_rows; int32_t mb, nm;
     float* mstats; int32_t mstats_cap;
 };
 
@@ -360,8 +366,20 @@ struct AdamApplyArgs {
     int64_t n, p_stride, t_off;
     int32_t group;
     float grad_scale;
+    const float* scale_dev;     // nullable: gradients also times *scale_dev (clip_by_global_norm)
     const Ctl* ctl;
     AdamConsts adam;
+};
+
+// clip_by_global_norm (mbrl_onpolicy_alg.py:315-317 over TF's clip_ops): k_gnorm_part sums g^2
+// over contiguous chunks of the gradient range, k_gnorm_final forms norm = sqrt(sum) and
+// scale = clip * min(1 / norm, 1 / clip) (+ (norm - norm): NaN when the norm is not finite)
+#define GNORM_PARTS 128
+struct GNormArgs {
+    const float* g; int64_t n;
+    float* part;                // [GNORM_PARTS]
+    float* scale_out;           // [1]
+    float clip;
 };
 
 // ---------------------------------------------------------------- model rollout (F2)
@@ -413,6 +431,7 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
 void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 void launch_roll(const RollArgs& a, hipStream_t s);
 void launch_net_io(const NetIOArgs& a, hipStream_t s);
+void launch_gnorm(const GNormArgs& a, hipStream_t s);
 void launch_diag(const DiagArgs& a, hipStream_t s);
 void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s);
 void launch_alpha_apply(const FinalArgs& f, hipStream_t s);

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 3
+SACX_ABI_VERSION = 4
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1
@@ -66,6 +66,14 @@ class Config(ctypes.Structure):
         ("reward_loss_coef", ctypes.c_float),
         ("gemm_bf16", ctypes.c_int32),
         ("seeds", ctypes.c_int32),
+        ("actor_gaussian", ctypes.c_int32),
+        ("actor_std_mult", ctypes.c_float),
+        ("actor_output_norm", ctypes.c_int32),
+        ("actor_layer_norm", ctypes.c_int32),
+        ("num_models", ctypes.c_int32),
+        ("model_max_grad_norm", ctypes.c_float),
+        ("delta_clip_loss", ctypes.c_float),
+        ("reward_clip_loss", ctypes.c_float),
     ]
 
 

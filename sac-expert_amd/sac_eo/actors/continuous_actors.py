@@ -1,10 +1,14 @@
-"""SquashedGaussianActor (reference ``sac_eo/actors/continuous_actors.py:237-379``).
+"""GaussianActor / SquashedGaussianActor (reference ``sac_eo/actors/continuous_actors.py:9-379``).
 
-Holds the actor's hyper-parameters and, until an algorithm binds it, its weights
-in the Keras ``get_weights()`` order ``[W0, b0, W1, b1, W2, b2] (+ logstd (1, A))``.
-Once bound (``_bind``), the weights live in the engine's HBM arena: get/set go
-through the engine and ``sample`` runs on the GPU (``sacx_actor_act``).  There is
-no CPU execution path.
+Each holds the actor's hyper-parameters and, until an algorithm binds it, its weights in
+the Keras ``get_weights()`` order ``[W0, b0, W1, b1, W2, b2] (+ logstd (1, A))``.  Once
+bound (``_bind``), the weights live in the engine's HBM arena: get/set go through the
+engine and ``sample`` / ``evaluate`` run on the GPU (``sacx_actor_act``,
+``sacx_actor_evaluate``).  There is no CPU execution path.
+
+The SAC learner is the squashed actor.  The plain GaussianActor is what the reference builds
+for an expert imported from a log (``sac_eo/train.py:65-86`` drops ``actor_squash``): its
+device engine is created with ``actor_gaussian`` and serves ``sample`` only.
 """
 import numpy as np
 
@@ -22,7 +26,9 @@ def _as_out(x):
     return np.asarray(x).view(_Out)
 
 
-class SquashedGaussianActor:
+class GaussianActor:
+    squash = False
+
     def __init__(self, env, layers, activations, gain, init_type, layer_norm, std_mult=1.0, per_state_std=False,
                  output_norm=False, rng=None):
         self.s_dim = int(np.prod(env.observation_space.shape))
@@ -34,8 +40,9 @@ class SquashedGaussianActor:
             raise NotImplementedError("one activation for all hidden layers")
         if layer_norm:
             raise NotImplementedError("actor_layer_norm is not built (off by default)")
-        if output_norm:
-            raise NotImplementedError("actor_output_norm is not built (off by default)")
+        if output_norm and self.squash:
+            raise NotImplementedError("actor_output_norm of the squashed actor is not built (off by default)")
+        self.output_norm = bool(output_norm)
         self.gain, self.init_type = gain, init_type
         self.per_state_std = bool(per_state_std)
         self.std_mult = std_mult
@@ -86,12 +93,23 @@ class SquashedGaussianActor:
 
     # ------------------------------------------------------------------ acting
     def sample(self, s, deterministic=False):
-        """act_limit * tanh(mu + std * u) on the GPU; u from the global NumPy stream's
-        device copy unless deterministic (continuous_actors.py:270-306)."""
+        """On the GPU: mu + std * u (GaussianActor, :103-123) or act_limit * tanh(mu + std * u)
+        (SquashedGaussianActor, :270-306); u from the global NumPy stream's device copy unless
+        deterministic."""
         if self._engine is None:
             raise RuntimeError("actor is not bound to a device engine (build the algorithm first)")
         out = self._engine.act(np.asarray(s, np.float32), deterministic=deterministic)
         return _as_out(out.cpu().numpy())
+
+    def clip(self, a):
+        return np.clip(a, self.act_low, self.act_high)
+
+    def tf_clip(self, a):
+        return self.clip(a)
+
+
+class SquashedGaussianActor(GaussianActor):
+    squash = True
 
     def evaluate(self, s):
         """(pi_action, neglogp_adjusted) of continuous_actors.py:327-379 on the GPU
@@ -106,9 +124,3 @@ class SquashedGaussianActor:
         if pi.shape[0] == 1:
             pi, nlp = pi[0], nlp[0]
         return _as_out(pi), _as_out(nlp)
-
-    def clip(self, a):
-        return np.clip(a, self.act_low, self.act_high)
-
-    def tf_clip(self, a):
-        return self.clip(a)

@@ -28,8 +28,8 @@ class SAC_exp(SACBase):
 
     def __init__(self, idx, env, env_eval, env_expert, actor, expert, init_expert_rms_stats, v_critic, q_targets,
                  q_critics, models, alg_kwargs, mf_update_kwargs):
-        if len(models) != 2:
-            raise NotImplementedError("SAC-EO is built for num_models = 2 (the default)")
+        if len(models) not in (1, 2):
+            raise ValueError("SAC-EO uses one or two world models (SAC_expert.py:271-336)")
         super().__init__(idx, env, env_eval, actor, v_critic, q_targets, q_critics, models, alg_kwargs,
                          mf_update_kwargs)
         self.env_expert = env_expert
@@ -45,6 +45,7 @@ class SAC_exp(SACBase):
         self.mult_coeff = alg_kwargs.get("mult_coeff", 1.0)
         self.delta_clip_pred = (mf_update_kwargs or {}).get("delta_clip_pred") or alg_kwargs.get("delta_clip_pred")
         self.model_MSE_on_expert_data = []
+        self._eps_log, self._eps_cur = [], float(self.epsilon)
         self.model_MSE_on_expert_counterfactual_action = []
         self._expert_engine = None
         self.s_expert = self.a_expert = self.sp_expert = None
@@ -53,9 +54,11 @@ class SAC_exp(SACBase):
     def _expert_engine_for(self):
         if self._expert_engine is None:
             ex = self.expert
+            # an imported expert is the reference's plain GaussianActor (train.py:65-86)
             cfg = EngineConfig(s_dim=self.s_dim, a_dim=self.a_dim, hidden=tuple(ex.layers), activation=ex.activation,
                                batch=1, buffer_capacity=1, per_state_std=ex.per_state_std, graph_steps=1,
-                               act_limit=float(np.max(ex.act_limit)))
+                               act_limit=float(np.max(ex.act_limit)), actor_gaussian=not ex.squash,
+                               actor_std_mult=float(ex.std_mult), actor_output_norm=ex.output_norm)
             self._expert_engine = Engine(cfg)
             ex._bind(self._expert_engine, "actor")
             self.expert_normalizer.push_to(self._expert_engine)
@@ -114,15 +117,38 @@ class SAC_exp(SACBase):
                 pick = np.random.randint(len(s_e), size=int(self.expert_batch_size))
             s_e, sp_e = s_e[pick], sp_e[pick]
         self.engine.set_expert(s_e, sp_e, eps)
+        self._eps_cur = float(eps)
         return (s_e, None, sp_e, eps, self.use_expert_actions)
+
+    def _flush_update_logs(self):
+        """The per-update log of _update_actor_and_alpha (SAC_expert.py:351-356): alpha_loss,
+        p_loss, epsilon -- read back from the device statistics ring (q1 / q2 losses too,
+        which the reference computes but does not log)."""
+        n = len(self._eps_log)
+        if n == 0:
+            return
+        cap = self.engine.cfg.stats_capacity
+        if n > cap:
+            raise RuntimeError("more updates than the statistics ring holds between flushes")
+        st = self.engine.stats(n)
+        for i in range(n):
+            self.logger.log_train({"alpha_loss": np.float32(st[i, 3]), "p_loss": np.float32(st[i, 2]),
+                                   "epsilon": self._eps_log[i], "q1_loss": np.float32(st[i, 0]),
+                                   "q2_loss": np.float32(st[i, 1])})
+        self._eps_log = []
+
+    def _dump_and_save(self, params):
+        self._flush_update_logs()
+        super()._dump_and_save(params)
 
     # ------------------------------------------------------------------ update
     def _update(self, num_timesteps, expert_reg=None, ts_increment=1):
-        n_e = self.engine.cfg.expert_batch
-        idx = np.arange(n_e)
-        self.rng.shuffle(idx)                    # SAC_expert.py:301-303
-        self.engine.push_perms(idx[None, :])
+        if len(self.models) > 1:                 # SAC_expert.py:301-303 (one model: no shuffle)
+            idx = np.arange(self.engine.cfg.expert_batch)
+            self.rng.shuffle(idx)
+            self.engine.push_perms(idx[None, :])
         self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
+        self._eps_log.append(self._eps_cur)
 
     def _update_models(self):
         t0 = time.time()
@@ -135,13 +161,14 @@ class SAC_exp(SACBase):
         with self._host_rng():
             for ep in range(self.model_num_epochs):
                 idx = np.arange(n_model)
+                nm = len(self.models)                 # self.B (SAC_expert.py:61)
                 if self.model_batch_shuffle:
-                    idx = np.tile(idx, (2, 1))
+                    idx = np.tile(idx, (nm, 1))
                     for row in idx:
                         np.random.shuffle(row)
                 else:
                     np.random.shuffle(idx)
-                    idx = np.tile(idx, (2, 1))
+                    idx = np.tile(idx, (nm, 1))
                 sections = np.arange(0, n_model, self.model_batch_size)[1:]
                 parts = np.array_split(idx, sections, axis=1)
                 if n_model % self.model_batch_size != 0:
@@ -180,6 +207,7 @@ class SAC_exp(SACBase):
         obs, expert_reg = None, None
         while num_timesteps < total_timesteps:
             if done:
+                self._flush_update_logs()            # before epsilon can change
                 if episode > 0:
                     self.logger.log_train({"J_tot": episode_reward, "steps": episode_step, "traj": 1})
                 obs = self.env.reset()

@@ -68,6 +68,7 @@ class SACBase:
         self.model_num_epochs = k.get("model_num_epochs", 10)
         self.model_batch_size = k.get("model_batch_size", 200)
         self.model_max_updates = k.get("model_max_updates", 1e5)
+        self.model_max_grad_norm = k.get("model_max_grad_norm")
         self.model_batch_shuffle = k.get("model_batch_shuffle", True)
         self.model_holdout_ratio = k.get("model_holdout_ratio", 0.0)
         self.reset_model_optimizer = k.get("reset_model_optimizer", False)
@@ -83,6 +84,8 @@ class SACBase:
         return max(1, self.total_timesteps + self.env_batch_size_init + self.env_horizon)
 
     def _build_engine(self, k):
+        if not getattr(self.actor, "squash", False):
+            raise ValueError("SAC trains the squashed Gaussian actor (--actor_squash)")
         hidden = self.actor.layers
         if len(hidden) != 2 or list(self.q_critics[0].layers) != list(hidden):
             raise NotImplementedError("the device engine runs 2 hidden layers shared by actor and critics")
@@ -100,7 +103,14 @@ class SACBase:
             lr_alpha=self.mbpo_alpha_lr, lr_model=self.model_lr, init_temperature=self.init_temperature,
             target_entropy=-float(self.a_dim), act_limit=float(np.max(self.actor.act_limit)),
             epsilon=float(self.epsilon),
-            reward_loss_coef=self.models[0].reward_loss_coef if self.use_expert else 1.0)
+            reward_loss_coef=self.models[0].reward_loss_coef if self.use_expert else 1.0,
+            num_models=len(self.models) if self.use_expert else 2,
+            model_max_grad_norm=float(self.model_max_grad_norm or 0.0),
+            delta_clip_loss=float(self.models[0].delta_clip_loss or 0.0) if self.use_expert else 0.0,
+            reward_clip_loss=float(self.models[0].reward_clip_loss or 0.0) if self.use_expert else 0.0)
+        if self.use_expert and self.models[0].delta_clip_pred:
+            raise NotImplementedError("delta_clip_pred inside the SAC-EO update's expert term is not built "
+                                      "(the rollout, diagnostics and MSEModel calls take it)")
         eng = Engine(cfg)
         self.actor._bind(eng, "actor")
         for i, q in enumerate(self.q_critics):
@@ -108,7 +118,7 @@ class SACBase:
         for i, t in enumerate(self.q_targets):
             t._bind(eng, f"t{i}")
         if self.use_expert:
-            for i, m in enumerate(self.models[:2]):
+            for i, m in enumerate(self.models):
                 m._bind(eng, f"m{i}")
         self.normalizer.push_to(eng)
         eng.rng_set_state(np.random.get_state())       # adopt the global stream
@@ -167,16 +177,28 @@ class SACBase:
     def _update(self, num_timesteps, expert_reg=None, ts_increment=1):
         self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
 
-    def _dump_and_save(self, params):
+    def _dump_stats(self):
+        """The reference's final dict (base_onpolicy_alg.py:351-364, mbrl_onpolicy_alg.py:321-329):
+        actor weights, the (V) critics' weights, rms stats, model / reward weights -- plus the
+        Q critics, targets and alpha the reference never saves."""
         final = {"actor_weights": self.actor.get_weights(),
-                 "critic_weights": [q.get_weights() for q in self.q_critics],
-                 "target_weights": [t.get_weights() for t in self.q_targets],
-                 "alpha": self.engine.alpha(), "rms_stats": self.normalizer.get_rms_stats()}
+                 "critic_weights": [c.get_weights() for c in self.critics],
+                 "rms_stats": self.normalizer.get_rms_stats(),
+                 "q_critic_weights": [q.get_weights() for q in self.q_critics],
+                 "q_target_weights": [t.get_weights() for t in self.q_targets],
+                 "alpha": self.engine.alpha()}
         if self.use_expert:
-            final["model_weights"] = [m.get_weights() for m in self.models[:2]]
+            final["model_weights"] = [m.get_weights() for m in self.models]
+            final["reward_weights"] = [None for _ in self.models]
+        return final
+
+    def _dump_and_save(self, params):
+        """base_onpolicy_alg.py:366-374: params + final into the logger, appended to the run's
+        checkpoint file, logger reset."""
         self.logger.log_params(params)
-        self.logger.log_final(final)
-        self.logger.save(self.save_path, self.checkpoint_name)
+        self.logger.log_final(self._dump_stats())
+        self.logger.dump_and_save(self.save_path, self.checkpoint_name)
+        self.logger.reset()
 
     def _checkpoints(self, total_timesteps):
         if self.save_freq is None:

@@ -1,56 +1,85 @@
-"""Minimal logger with the reference's dict-of-lists layout (``sac_eo/common/logger.py``);
-checkpoints are written as JSON + NumPy .npz (no pickle)."""
-import json
+"""Logger with the reference's layout (``sac_eo/common/logger.py:5-91``): dict-of-lists
+``train`` data, ``param`` inputs and ``final`` weights / normaliser stats, saved as the
+reference's pickle ``{'param', 'train', 'final'}`` with the train arrays of an existing file
+in front (``dump_and_save``, ``:57-86``), so the reference's analysis tooling reads our logs.
+
+``load_log`` reads such a file (ours, or one the reference wrote) with an allow-list
+unpickler: only containers, scalars and NumPy array / dtype reconstruction are resolved;
+any other global in the file is refused, so loading a log executes nothing from it."""
 import os
+import pickle
 
 import numpy as np
 
+# (module, name) globals a log may reference: NumPy's array / scalar reconstruction
+# (numpy 1.x pickles name numpy.core, numpy 2.x numpy._core)
+_ALLOWED = {(m, n) for m in ("numpy.core.multiarray", "numpy._core.multiarray")
+            for n in ("_reconstruct", "scalar")} | {("numpy", "ndarray"), ("numpy", "dtype")}
+
+
+class _LogUnpickler(pickle.Unpickler):
+    def find_class(self, module, name):
+        if (module, name) in _ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f"log file references {module}.{name}: refused (not a sac_eo log)")
+
+
+def load_log(filename):
+    """A sac_eo log file: the dict of one run's checkpoint, or the list of runs that
+    ``train.py`` aggregates (reference ``sac_eo/train.py:159-186``)."""
+    with open(filename, "rb") as fh:
+        return _LogUnpickler(fh).load()
+
 
 class Logger:
+    """Class for logging data throughout training (reference ``logger.py:5-91``)."""
+
     def __init__(self):
-        self.param_dict = {}
-        self.train_dict = {}
-        self.eval_dict = {}
-        self.final_dict = {}
+        self.param_dict = dict()
+        self.train_dict = dict()
+        self.final_dict = dict()
 
-    def log_params(self, inputs_dict):
-        self.param_dict = inputs_dict
+    def log_train(self, kv):
+        for k, v in kv.items():
+            self.train_dict.setdefault(k, []).append(v)
 
-    def _log(self, d, data):
-        for k, v in data.items():
-            d.setdefault(k, []).append(v)
+    def log_train_ensemble(self, kv_list):
+        ens = dict()
+        for kv in kv_list:
+            for k, v in kv.items():
+                ens.setdefault(k, []).append(v)
+        self.log_train({k: np.array(v) for k, v in ens.items()})
 
-    def log_train(self, data):
-        self._log(self.train_dict, data)
+    def log_eval(self, kv):
+        """_evaluate's record (base_onpolicy_alg.py:190-195: J_tot_eval / steps_eval / time_eval)."""
+        self.log_train({f"{k}_eval": v for k, v in kv.items()})
 
-    def log_eval(self, data):
-        self._log(self.eval_dict, data)
+    def log_params(self, kv):
+        for k, v in kv.items():
+            self.param_dict[k] = v
 
-    def log_final(self, data):
-        self.final_dict.update(data)
+    def log_final(self, kv):
+        for k, v in kv.items():
+            self.final_dict[k] = v
 
     def dump(self):
-        return {"param": self.param_dict, "train": self.train_dict, "eval": self.eval_dict, "final": self.final_dict}
+        return {"param": self.param_dict, "train": {k: np.array(v) for k, v in self.train_dict.items()},
+                "final": self.final_dict}
 
-    def save(self, path, name):
-        os.makedirs(path, exist_ok=True)
-        arrays = {}
+    def dump_and_save(self, log_path, log_name):
+        """Writes ``{'param', 'train', 'final'}``; train arrays already in the file come first."""
+        out = self.dump()
+        os.makedirs(log_path, exist_ok=True)
+        filename = os.path.join(log_path, log_name)
+        if os.path.exists(filename):
+            old = load_log(filename)
+            for k, v in old["train"].items():
+                out["train"][k] = np.concatenate((v, out["train"][k]), axis=0) if k in out["train"] else v
+        with open(filename, "wb") as fh:
+            pickle.dump(out, fh)
+        return filename
 
-        def conv(x, key):
-            if isinstance(x, np.ndarray):
-                arrays[key] = x
-                return {"__npz__": key}
-            if isinstance(x, dict):
-                return {k: conv(v, f"{key}.{k}") for k, v in x.items()}
-            if isinstance(x, (list, tuple)):
-                return [conv(v, f"{key}.{i}") for i, v in enumerate(x)]
-            if isinstance(x, (np.floating, np.integer)):
-                return x.item()
-            return x
-
-        meta = conv(self.dump(), "log")
-        with open(os.path.join(path, name + ".json"), "w") as fh:
-            json.dump(meta, fh, default=str)
-        if arrays:
-            np.savez(os.path.join(path, name + ".npz"), **arrays)
-        return os.path.join(path, name)
+    def reset(self):
+        self.param_dict.clear()
+        self.train_dict.clear()
+        self.final_dict.clear()

@@ -4,9 +4,9 @@ from .critics import QCritic, VCritic
 
 def init_critics(env, critic_layers, critic_activations, critic_gain, critic_weights, num_models, critic_ensemble,
                  critic_init_type, critic_layer_norm, **unused):
-    """Returns (critics, q_targets, q_critics); the targets start as copies of the critics."""
-    if critic_layer_norm:
-        raise NotImplementedError("critic_layer_norm is not built (off by default)")
+    """Returns (critics, q_targets, q_critics); the targets start as copies of the critics.
+    critic_init_type / critic_layer_norm are accepted and ignored, as in the reference
+    (init_critic.py:5-6, critics.py:74 never pass them on)."""
     num_critics = num_models if critic_ensemble else 1
     critics = []
     for idx in range(num_critics):

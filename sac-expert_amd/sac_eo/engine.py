@@ -57,6 +57,14 @@ class EngineConfig:
     reward_loss_coef: float = 1.0
     gemm_bf16: bool = False     # config C5: bf16 MFMA operands, fp32 accumulate / master weights
     seeds: int = 1              # independent learners packed in one handle (one launch chain for all)
+    actor_gaussian: bool = False    # GaussianActor (no squash): inference only (an imported expert)
+    actor_std_mult: float = 1.0
+    actor_output_norm: bool = False
+    actor_layer_norm: bool = False  # Dense -> LayerNorm -> tanh on the actor's layer 0
+    num_models: int = 2             # SAC-EO world models (1 or 2)
+    model_max_grad_norm: float = 0.0    # <= 0: None
+    delta_clip_loss: float = 0.0        # <= 0: None
+    reward_clip_loss: float = 0.0       # <= 0: None
 
     def to_c(self) -> N.Config:
         c = N.Config()
@@ -86,6 +94,14 @@ class EngineConfig:
         c.reward_loss_coef = self.reward_loss_coef
         c.gemm_bf16 = int(bool(self.gemm_bf16))
         c.seeds = int(self.seeds)
+        c.actor_gaussian = int(bool(self.actor_gaussian))
+        c.actor_std_mult = float(self.actor_std_mult)
+        c.actor_output_norm = int(bool(self.actor_output_norm))
+        c.actor_layer_norm = int(bool(self.actor_layer_norm))
+        c.num_models = int(self.num_models)
+        c.model_max_grad_norm = float(self.model_max_grad_norm or 0.0)
+        c.delta_clip_loss = float(self.delta_clip_loss or 0.0)
+        c.reward_clip_loss = float(self.reward_clip_loss or 0.0)
         return c
 
 
@@ -474,11 +490,12 @@ class Engine:
         return time.perf_counter() - t0
 
     def model_fit(self, idx: np.ndarray, eager: bool = False):
-        """``idx[n, 2, model_batch]``: replay-logical rows of each model's minibatch per step
-        (SAC_expert.py:519-543 -> _apply_model_grads)."""
+        """``idx[n, num_models, model_batch]``: replay-logical rows of each model's minibatch per
+        step (SAC_expert.py:519-543 -> _apply_model_grads)."""
         idx = np.ascontiguousarray(idx, dtype=np.int32)
-        if idx.ndim != 3 or idx.shape[1] != 2 or idx.shape[2] != self.cfg.model_batch:
-            raise ValueError(f"idx must be [n, 2, {self.cfg.model_batch}]")
+        nm = int(self.cfg.num_models or 2)
+        if idx.ndim != 3 or idx.shape[1] != nm or idx.shape[2] != self.cfg.model_batch:
+            raise ValueError(f"idx must be [n, {nm}, {self.cfg.model_batch}]")
         N.check(self.lib.sacx_model_fit(self.h, idx.ctypes.data, int(idx.shape[0]), N.STEP_EAGER if eager else 0),
                 self.h, "model_fit")
 

@@ -1,10 +1,14 @@
 """``python -m sac_eo.train`` (reference ``sac_eo/train.py``): same flags, seeds and
-construction sequence, one learner per process.
+construction sequence, one learner per process, the same log files.
 
-Runs are spread over processes: under ``torch.distributed.run`` rank r trains run
-``runs_start + r`` on its local GPU; otherwise the runs execute one after another on
-the current GPU.  No data moves between learners (replicas)."""
+Runs are spread over processes: under ``torch.distributed.run`` rank r trains runs
+``r, r + world, ...`` on its local GPU; otherwise the runs execute one after another on
+the current GPU.  No data moves between learners (replicas).  As in the
+reference (``:159-191``), the runs' checkpoint logs are gathered into one pickled list
+``<env_type>_<env>_<alg_type>_<mf_algo>[_<save_file>]_<date>`` and removed."""
+import copy
 import os
+import pickle
 import sys
 from datetime import datetime
 
@@ -13,7 +17,9 @@ import numpy as np
 from .actors import init_actor
 from .algs import init_alg
 from .common.seeding import derive_seeds, init_seeds
+from .common.logger import load_log
 from .common.train_parser import create_train_parser, gather_inputs
+from .common.train_utils import import_inputs, load_expert
 from .critics import init_critics
 from .envs import init_env
 from .models import init_world_models
@@ -31,10 +37,12 @@ def train(inputs_dict):
     ak = dict(inputs_dict["actor_kwargs"])
     ak.setdefault("actor_weights", None)
     actor = init_actor(env, **ak)
-    expert_kwargs = dict(ak)
-    expert_kwargs["actor_weights"] = None
-    if sk.get("expert_file") is not None:
-        raise NotImplementedError("expert_file import reads a pickle; load expert weights with set_weights instead")
+    if sk.get("expert_file") is not None:        # train.py:65-86
+        expert_kwargs, init_expert_rms_stats = load_expert(sk["expert_path"], sk["expert_file"])
+    else:
+        expert_kwargs = dict(ak)
+        expert_kwargs["actor_weights"] = None
+        init_expert_rms_stats = None
     expert = init_actor(env, **expert_kwargs)
     ck = dict(inputs_dict["critic_kwargs"])
     ck.setdefault("critic_weights", None)
@@ -47,7 +55,7 @@ def train(inputs_dict):
     init_seeds(sk["sim_seed"], env)
     init_seeds(sk["expert_seed"], env_expert)
     alg = init_alg(idx, env, env_eval, env_expert, actor, critics, q_targets, q_critics, models,
-                   inputs_dict["alg_kwargs"], inputs_dict["mf_update_kwargs"], expert, None)
+                   inputs_dict["alg_kwargs"], inputs_dict["mf_update_kwargs"], expert, init_expert_rms_stats)
     return alg.train(inputs_dict["alg_kwargs"]["total_timesteps"], inputs_dict)
 
 
@@ -65,16 +73,42 @@ def main(argv=None):
         rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         runs = runs[rank::ws]
-    names = []
+    names = {}
     for r in runs:
-        d = {g: dict(v) for g, v in inputs_dict.items()}
+        d = copy.deepcopy(inputs_dict)
         d["setup_kwargs"].update(idx=args.runs_start + r, setup_seed=int(seeds["setup"][r]),
                                  sim_seed=int(seeds["sim"][r]), eval_seed=int(seeds["eval"][r]),
                                  expert_seed=int(seeds["expert"][r]), algorithm_seed=int(seeds["algorithm"][r]))
-        names.append(train(d))
-    print(f"done: {names} in {(datetime.now() - start).total_seconds():.1f}s", flush=True)
-    return names
+        d = import_inputs(d)                         # train_utils.py:20-92 (no-op without --import_file)
+        names[r] = train(d)
+    if ws > 1:                                       # every rank's runs are on disk before gathering
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        dist.barrier()
+        allnames = [None] * ws
+        dist.all_gather_object(allnames, names)
+        dist.destroy_process_group()
+        if rank != 0:
+            return None
+        names = {k: v for part in allnames for k, v in part.items()}
+    # gather the runs' logs into one file, in run order (train.py:159-191)
+    outputs = [load_log(os.path.join(args.save_path, names[r])) for r in sorted(names)]
+    save_env = args.env_name.split("-")[0].lower()
+    if args.task_name is not None:
+        save_env = f"{save_env}_{args.task_name.lower()}"
+    date = datetime.today().strftime("%m%d%y_%H%M%S")
+    parts = [args.env_type.lower(), save_env, args.alg_type, args.mf_algo] + \
+        ([args.save_file] if args.save_file is not None else []) + [date]
+    save_filefull = os.path.join(args.save_path, "_".join(parts))
+    with open(save_filefull, "wb") as fh:
+        pickle.dump(outputs, fh)
+    for r in sorted(names):
+        os.remove(os.path.join(args.save_path, names[r]))
+    print(f"done: {save_filefull} in {(datetime.now() - start).total_seconds():.1f}s", flush=True)
+    return save_filefull
 
 
 if __name__ == "__main__":
-    sys.exit(0 if main() else 1)
+    main()
+    sys.exit(0)

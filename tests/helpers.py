@@ -57,7 +57,8 @@ def load_learner(eng, st, buf, nrm, expert, epsilon):
         eng.set_net(f"t{k}", st.q_targ[k])
     if expert is not None:
         for k in range(2):
-            eng.set_net(f"m{k}", st.models[k])
+            if f"m{k}.l0" in eng.segments:      # --num_models 1: model 0 only
+                eng.set_net(f"m{k}", st.models[k])
     eng.set_alpha(float(st.alpha))
     eng.set_normalizers(nrm.s_mean, nrm.s_den, nrm.a_mean, nrm.a_den, nrm.d_mean, nrm.d_den,
                         nrm.r_mean, nrm.r_den, nrm.ret_den)
@@ -68,7 +69,7 @@ def load_learner(eng, st, buf, nrm, expert, epsilon):
 
 def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
               use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
-              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False):
+              graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False, **ekw):
     """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
     from sac_eo.engine import Engine, EngineConfig
     ocfg, st, buf, nrm, expert = make_learner(S, A, hidden, B, act, N, seed, per_state_std, use_expert, ne,
@@ -76,7 +77,7 @@ def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, p
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
                         per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
                         expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon,
-                        gemm_bf16=gemm_bf16)
+                        gemm_bf16=gemm_bf16, **ekw)
     eng = Engine(ecfg, dp=dp)
     load_learner(eng, st, buf, nrm, expert, epsilon)
     return eng, ocfg, st.astype(np.float64), buf, nrm, expert
@@ -88,8 +89,12 @@ def oracle_step(st, ocfg, nrm, buf, R, expert=None, keep=None):
     ex = None
     if expert is not None:
         sec = R["sections"]
-        ex = O.Expert(expert["s"][sec[0]], expert["sp"][sec[0]], expert["s"][sec[1]], expert["sp"][sec[1]],
-                      O.f32_noise(R["noise_e1"]), O.f32_noise(R["noise_e2"]), ocfg.epsilon)
+        if len(sec) == 1:                      # one world model: every expert row, in order
+            ex = O.Expert(expert["s"][sec[0]], expert["sp"][sec[0]], None, None,
+                          O.f32_noise(R["noise_e1"]), None, ocfg.epsilon)
+        else:
+            ex = O.Expert(expert["s"][sec[0]], expert["sp"][sec[0]], expert["s"][sec[1]], expert["sp"][sec[1]],
+                          O.f32_noise(R["noise_e1"]), O.f32_noise(R["noise_e2"]), ocfg.epsilon)
     return O.sac_update(st, ocfg, nrm, O.gather(buf, R["idx"]), *n, expert=ex, keep=keep)
 
 

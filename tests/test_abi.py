@@ -29,10 +29,12 @@ def test_struct_layouts():
     from sac_eo import _native as N
     # offsets fixed by include/sacx.h (natural alignment)
     assert N.Config.buffer_capacity.offset == 32
-    assert ctypes.sizeof(N.Config) == 144          # gcc: sizeof(sacx_config)
+    assert ctypes.sizeof(N.Config) == 176          # gcc: sizeof(sacx_config)
     assert N.Config.reward_loss_coef.offset == 128
     assert N.Config.gemm_bf16.offset == 132
     assert N.Config.seeds.offset == 136
+    assert N.Config.actor_gaussian.offset == 140 and N.Config.num_models.offset == 156
+    assert N.Config.reward_clip_loss.offset == 168
     assert ctypes.sizeof(N.Segment) == 48 + 8 + 8 + 8 + 4 + 4
     assert ctypes.sizeof(N.LaunchInfo) == 32 + 32 + 4 + 4 + 8 + 8
 

@@ -29,8 +29,11 @@ def test_actor_weight_layout_matches_reference():
     q = w[2] / np.sqrt(2)
     assert np.allclose(q.T @ q, np.eye(256), atol=1e-4)
     assert np.isclose(np.linalg.svd(w[4], compute_uv=False).max(), 0.01, rtol=1e-4)
-    with pytest.raises(NotImplementedError):
-        init_actor(env, **dict(ak, actor_weights=None, actor_squash=False))
+    # actor_squash False: the reference's plain GaussianActor (an imported expert, inference only)
+    from sac_eo.actors import GaussianActor, SquashedGaussianActor
+    g = init_actor(env, **dict(ak, actor_weights=w, actor_squash=False))
+    assert type(g) is GaussianActor and not g.squash and isinstance(actor, SquashedGaussianActor)
+    assert all(np.array_equal(a, b) for a, b in zip(g.get_weights(), w))
 
 
 def test_critics_and_models_construction():

@@ -1,0 +1,122 @@
+"""Reference options on the device path, each against the oracle:
+
+* --num_models 1 (SAC_expert.py:273-296): the expert term through one world model on every
+  expert row in order (no shuffle), the mean MSE over the rows; one update per stage and a
+  100-update trajectory on the production schedule; the model fit of one model.
+* --model_max_grad_norm (mbrl_onpolicy_alg.py:315-317: clip_by_global_norm to
+  max_norm * num_models) and --delta_clip_loss / --reward_clip_loss
+  (continuous_models.py:284-296) in the model fit.
+* GaussianActor.sample (continuous_actors.py:74-123, an expert imported from a log:
+  train.py:65-86 builds it without actor_squash), ± per_state_std, ± output_norm.
+"""
+import numpy as np
+import pytest
+
+import sac_oracle as O
+from helpers import make_pair, oracle_step, relerr
+
+pytestmark = pytest.mark.gpu
+
+
+def test_one_model_update_matches_oracle(gpu_available):
+    B, ne = 128, 15                      # one model: an odd expert batch is allowed
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=17, use_expert=True, ne=ne,
+                                                normalizers="random", done_p=0.02, num_models=1)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(90)
+    eng.rng_set_state(rs.get_state())
+    R = O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=ne, n_models=1)
+    keep = {}
+    ref = oracle_step(st, ocfg, nrm, buf, R, expert, keep)
+    eng.step(1, eager=True)
+    eng.sync()
+    row = eng.stats(1)[0]
+    for i, k in enumerate(("q1_loss", "q2_loss", "p_loss", "alpha_loss")):
+        assert abs(row[i] - ref[k]) <= 2e-5 * abs(ref[k]) + 1e-7, (k, row[i], ref[k])
+    assert abs(row[5] - ref["mse_loss"]) <= 2e-5 * abs(ref["mse_loss"])
+    m = eng.v["adam_m"][0]
+    for i in range(3):
+        seg = eng.segments[f"actor.l{i}"]
+        o, n = seg["offset"] // 4, seg["rows"] * seg["cols"]
+        gd = m[o:o + n].cpu().numpy().reshape(seg["rows"], seg["cols"]) / (np.float32(1) - np.float32(0.9))
+        assert relerr(gd[:-1], keep["actor_grads"][2 * i]) < 2e-4
+        assert relerr(gd[-1], keep["actor_grads"][2 * i + 1]) < 2e-4
+    got, exp = eng.rng_get_state(), rs.get_state()
+    assert np.array_equal(got[1], exp[1]) and got[2] == exp[2] and got[3] == exp[3]
+    eng.close()
+
+
+def test_one_model_trajectory(gpu_available):
+    B, ne, steps = 256, 20, 100
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=19, use_expert=True, ne=ne, done_p=0.01,
+                                                graph_steps=128, num_models=1)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(91)
+    eng.rng_set_state(rs.get_state())
+    Rs = [O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=ne, n_models=1) for _ in range(steps)]
+    eng.prepare(steps)
+    eng.step(steps)
+    eng.sync()
+    dev = eng.stats(steps)
+    ref = np.array([[o["q1_loss"], o["q2_loss"], o["p_loss"], o["mse_loss"]]
+                    for o in (oracle_step(st, ocfg, nrm, buf, R, expert) for R in Rs)])
+    assert np.max(np.abs(dev[:, :2] - ref[:, :2]) / np.abs(ref[:, :2])) < 1e-4
+    assert np.max(np.abs(dev[:, 2] - ref[:, 2])) / np.max(np.abs(ref[:, 2])) < 1e-4
+    assert np.max(np.abs(dev[:, 5] - ref[:, 3]) / np.abs(ref[:, 3])) < 1e-4
+    eng.close()
+
+
+@pytest.mark.parametrize("nm,max_norm,dclip,rclip", [(2, 0.05, 0.0, 0.0), (1, 0.0, 0.0, 0.0),
+                                                     (1, 0.02, 0.3, 0.5), (2, 0.0, 0.2, 0.0)])
+def test_model_fit_options(gpu_available, nm, max_norm, dclip, rclip):
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=31, use_expert=True, normalizers="random",
+                                           num_models=nm, model_max_grad_norm=max_norm, delta_clip_loss=dclip,
+                                           reward_clip_loss=rclip)
+    N = buf["r"].shape[0]
+    mb = eng.cfg.model_batch
+    idx = np.random.RandomState(12).randint(N, size=(5, nm, mb))
+    for eager in (True, False):
+        eng.model_fit(idx[:2] if eager else idx[2:], eager=eager)
+    eng.sync()
+    dev = eng.model_stats(5)
+    ref = []
+    for j in range(5):
+        batches = [(buf["s"][idx[j, k]], buf["a"][idx[j, k]], buf["sp"][idx[j, k]], buf["r"][idx[j, k]])
+                   for k in range(nm)]
+        ref.append(O.model_fit_step(st, ocfg, nrm, batches, max_grad_norm=max_norm or None,
+                                    delta_clip_loss=dclip, reward_clip_loss=rclip))
+    ref = np.array(ref)
+    assert np.max(np.abs(dev - ref) / np.abs(ref)) < 1e-4, (dev, ref)
+    for k in range(nm):
+        for a_, b_ in zip(eng.get_net(f"m{k}"), st.models[k]):
+            assert np.max(np.abs(a_ - b_)) < 5e-5
+    eng.close()
+
+
+@pytest.mark.parametrize("per_state_std,output_norm,deterministic", [(False, False, True), (False, True, False),
+                                                                     (True, False, False), (True, True, True)])
+def test_gaussian_actor_sample(gpu_available, per_state_std, output_norm, deterministic):
+    from sac_eo.engine import Engine, EngineConfig
+    S, A, n = 11, 3, 300
+    cfg = O.Config(S=S, A=A, hidden=(64, 64), act="tanh", per_state_std=per_state_std)
+    st = O.init_state(cfg, seed=8, bias_scale=0.2, actor_gain=2.0)
+    st.logstd = np.full((1, A), -0.7, np.float32)
+    eng = Engine(EngineConfig(s_dim=S, a_dim=A, hidden=(64, 64), activation="tanh", batch=1, buffer_capacity=1,
+                              per_state_std=per_state_std, graph_steps=1, actor_gaussian=True, actor_std_mult=0.6,
+                              actor_output_norm=output_norm))
+    eng.set_net("actor", st.actor)
+    eng.set_logstd(st.logstd)
+    nrm = O.Normalizers.identity(S, A)
+    obs = (np.random.RandomState(4).normal(size=(n, S)) * 2).astype(np.float32)
+    eng.rng_set_state(np.random.RandomState(7).get_state())
+    rs = np.random.RandomState(7)
+    got = eng.act(obs, deterministic=deterministic).cpu().numpy()
+    u = np.zeros((n, A)) if deterministic else O.f32_noise(rs.normal(size=(n, A))).astype(np.float64)
+    ref = O.gaussian_actor_sample([w.astype(np.float64) for w in st.actor], st.logstd.astype(np.float64), cfg, nrm,
+                                  obs, u, 0.6, output_norm)
+    assert relerr(got, ref) < 2e-5, relerr(got, ref)
+    if output_norm:                         # the mean is normalised: |a| is not squashed below 1
+        assert np.all(np.isfinite(got))
+    with pytest.raises(Exception):
+        eng.step(1)                         # inference only
+    eng.close()

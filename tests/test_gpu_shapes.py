@@ -1,0 +1,108 @@
+"""BASELINE.json configs exercised at their own shapes on the device.
+
+* C3 (Humanoid-v3, S=376, A=17): the world-model fit (2 models x minibatch 200,
+  mbrl_onpolicy_alg.py:301-319) and the rollout (samplers.py:73-122) vs the oracle.
+* C5 (Humanoid-v3, B=1024, bf16 MFMA operands / fp32 accumulate, 4e6-row buffer in HBM):
+  the Q-loss trajectory of 100 updates vs the fp64 oracle within BF16_QLOSS_TOL (the graph
+  schedule at its production graph_steps = 128), and on a full 4e6-row ring (12.3 GB, byte
+  offsets past 2^32) the device sampler's indices and noise bit-exact against NumPy and the
+  gathered rows equal to the ring rows they name.
+"""
+import numpy as np
+import pytest
+
+import sac_oracle as O
+from helpers import make_pair, oracle_step, relerr
+
+pytestmark = pytest.mark.gpu
+
+HUM = dict(S=376, A=17)
+BF16_QLOSS_TOL = 5e-3       # as tests/test_gpu_engine.py: 8-bit-mantissa operands, fp32 accumulate
+
+
+@pytest.mark.parametrize("eager", [True, False])
+def test_humanoid_model_fit(gpu_available, eager):
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=33, use_expert=True, normalizers="random", **HUM)
+    N = buf["r"].shape[0]
+    mb = eng.cfg.model_batch
+    idx = np.random.RandomState(10).randint(N, size=(4, 2, mb))
+    eng.model_fit(idx, eager=eager)
+    eng.sync()
+    dev = eng.model_stats(4)
+    ref = np.array([O.model_fit_step(st, ocfg, nrm, [(buf["s"][idx[j, k]], buf["a"][idx[j, k]], buf["sp"][idx[j, k]],
+                                                      buf["r"][idx[j, k]]) for k in range(2)]) for j in range(4)])
+    assert np.max(np.abs(dev - ref) / np.abs(ref)) < 1e-4, (dev, ref)
+    for k in range(2):
+        for a_, b_ in zip(eng.get_net(f"m{k}"), st.models[k]):
+            assert np.max(np.abs(a_ - b_)) < 5e-5
+    eng.close()
+
+
+def test_humanoid_rollout(gpu_available):
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=35, use_expert=True, normalizers="random", **HUM)
+    s0 = (np.random.RandomState(7).normal(size=(1000, ocfg.S)) * 0.5).astype(np.float32)
+    eng.rng_set_state(np.random.RandomState(24).get_state())
+    rs = np.random.RandomState(24)
+    got = [t.cpu().numpy() for t in eng.rollout(0, s0, 5)]
+    ref = O.rollout(st, ocfg, nrm, s0, 5, 0, rs)
+    for g, r, name in zip(got, ref, ("s", "a", "r", "sp", "d")):
+        assert g.shape == r.shape
+        if name != "d":
+            assert relerr(g, r) < 1e-4, (name, relerr(g, r))
+    dev, rr = eng.rng_get_state(), rs.get_state()
+    assert np.array_equal(dev[1], rr[1]) and dev[2] == rr[2]
+    eng.close()
+
+
+def test_humanoid_bf16_trajectory(gpu_available):
+    B, steps = 1024, 100
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=B, N=20000, seed=37, done_p=0.01, gemm_bf16=True,
+                                           graph_steps=128, **HUM)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(77)
+    eng.rng_set_state(rs.get_state())
+    Rs = [O.draw_step_randoms(rs, N, B, ocfg.A) for _ in range(steps)]
+    eng.prepare(steps)
+    eng.step(steps)
+    eng.sync()
+    dev = eng.stats(steps)
+    ref = np.array([[o["q1_loss"], o["q2_loss"]] for o in (oracle_step(st, ocfg, nrm, buf, R) for R in Rs)])
+    rel = np.abs(dev[:, :2] - ref) / np.abs(ref)
+    print("humanoid bf16 q-loss max rel err", rel.max(), "median", np.median(rel))
+    assert rel.max() < BF16_QLOSS_TOL, rel.max()
+    got, exp = eng.rng_get_state(), rs.get_state()
+    assert np.array_equal(got[1], exp[1]) and got[2] == exp[2]
+    eng.close()
+
+
+def test_sampler_on_4e6_ring(gpu_available):
+    """Config C5's replay ring: 4e6 Humanoid rows resident in HBM (12.3 GB)."""
+    import torch
+    from sac_eo.engine import Engine, EngineConfig
+    S, A, B, N = 376, 17, 1024, 4_000_000
+    eng = Engine(EngineConfig(s_dim=S, a_dim=A, batch=B, buffer_capacity=N, gemm_bf16=True, graph_steps=1))
+    g = torch.Generator(device=eng.device)
+    g.manual_seed(5)
+    for c0 in range(0, N, 500_000):                   # fill on the device in chunks
+        n = min(500_000, N - c0)
+        s = torch.randn(n, S, device=eng.device, generator=g)
+        eng.append(s, torch.rand(n, A, device=eng.device, generator=g) * 2 - 1,
+                   torch.randn(n, device=eng.device, generator=g), s * 0.5, torch.zeros(n, device=eng.device))
+        eng.sync()
+        del s
+    assert eng.ctl()["cur_size"] == N and eng.ctl()["start"] == 0
+    for seed in (2590541744, 11):
+        rs = np.random.RandomState(seed)
+        eng.rng_set_state(rs.get_state())
+        eng.step(1, external=False, eager=True)
+        eng.sync()
+        idx = rs.randint(N, size=B)
+        noise = rs.normal(size=3 * B * A)
+        assert np.array_equal(eng.v["slot0.idx"][0].cpu().numpy(), idx)
+        assert np.array_equal(eng.v["slot0.noise"][0].cpu().numpy(), noise.astype(np.float32))
+        assert idx.max() > 3_500_000                      # rows past 2^32 bytes into the ring
+        rows = eng.v["replay"][torch.as_tensor(idx, device=eng.device)]
+        xq = eng.v["slot0.Xq"][:B]
+        assert torch.equal(xq[:, :S], rows[:, :S]) and torch.equal(xq[:, S:S + A], rows[:, S:S + A])
+        assert torch.equal(eng.v["slot0.r"][0], rows[:, 2 * S + A])
+    eng.close()

@@ -1,6 +1,5 @@
 """End-to-end ``sac_eo.train`` on the GPU at tiny sizes: the reference's construction
 sequence, env loop, model fitting and checkpoint, through the device engine."""
-import json
 import os
 
 import numpy as np
@@ -17,19 +16,48 @@ def test_train_entry_point(gpu_available, tmp_path, alg):
             "--model_layers", "64", "64", "--total_timesteps", "2600", "--env_batch_size_init", "300",
             "--env_horizon", "200", "--sac_batch_size", "64", "--model_batch_size", "50",
             "--model_num_epochs", "1", "--seed", "3", "--save_path", str(tmp_path)]
-    names = main(argv)
-    assert len(names) == 1
-    with open(os.path.join(tmp_path, names[0] + ".json")) as fh:
-        log = json.load(fh)
-    assert "actor_weights" in log["final"]
-    arrs = np.load(os.path.join(tmp_path, names[0] + ".npz"))
-    w = [arrs[k] for k in arrs.files if k.startswith("log.final.actor_weights")]
-    assert w and all(np.all(np.isfinite(x)) for x in w)
+    path = main(argv)
+    # the reference's gathered log: a list of runs, each {param, train, final} (train.py:159-191)
+    from sac_eo.common.logger import load_log
+    logs = load_log(path)
+    assert isinstance(logs, list) and len(logs) == 1
+    log = logs[0]
+    assert set(log) == {"param", "train", "final"}
+    assert os.listdir(tmp_path) == [os.path.basename(path)]        # per-run checkpoints gathered and removed
+    w = log["final"]["actor_weights"]
+    assert len(w) == 7 and all(np.all(np.isfinite(x)) for x in w)    # [W0, b0, W1, b1, W2, b2, logstd]
     assert np.isfinite(log["final"]["alpha"])
     assert len(log["train"]["J_tot"]) >= 3          # the collection batch + 2 finished 1000-step episodes
     if alg == "sac_imit":
-        assert log["train"]["model_updates"][-1] == 2 * 2600 // 50 // 2 or log["train"]["model_updates"][-1] > 0
+        assert log["train"]["model_updates"][-1] > 0
         assert np.isfinite(log["train"]["model_loss_last"][-1])
-        # expert diagnostics on the device (SAC_expert.py:579-608), no longer NaN placeholders
+        # expert diagnostics on the device (SAC_expert.py:579-608)
         assert np.isfinite(log["train"]["model_MSE_on_expert_data"][-1])
         assert np.isfinite(log["train"]["model_MSE_on_expert_counterfactual_action"][-1])
+        # one alpha_loss / p_loss / epsilon entry per gradient step (SAC_expert.py:351-356)
+        n_upd = 2600 - 300
+        for k in ("alpha_loss", "p_loss", "epsilon"):
+            assert len(log["train"][k]) == n_upd, (k, len(log["train"][k]))
+        assert np.all(np.isfinite(log["train"]["p_loss"]))
+        assert len(log["final"]["model_weights"]) == 2
+
+
+def test_train_one_model_and_imported_expert(gpu_available, tmp_path):
+    """--num_models 1 with --model_max_grad_norm, and --expert_file pointing at a log this
+    build wrote (its actor, built as the reference's plain GaussianActor, collects the expert
+    data)."""
+    from sac_eo.train import main
+    from sac_eo.common.logger import load_log
+    base = ["--env_name", "HalfCheetah-v3", "--actor_layers", "64", "64", "--critic_layers", "64", "64",
+            "--actor_activations", "relu", "--critic_activations", "relu", "--model_layers", "64", "64",
+            "--env_batch_size_init", "300", "--env_horizon", "200", "--sac_batch_size", "64",
+            "--model_batch_size", "50", "--model_num_epochs", "1", "--seed", "5"]
+    exp_dir = tmp_path / "experts"
+    expert_log = main(base + ["--alg_type", "sac", "--total_timesteps", "600", "--save_path", str(exp_dir)])
+    path = main(base + ["--alg_type", "sac_imit", "--num_models", "1", "--model_max_grad_norm", "0.5",
+                        "--total_timesteps", "1600", "--expert_path", str(exp_dir),
+                        "--expert_file", os.path.basename(expert_log), "--save_path", str(tmp_path / "run")])
+    log = load_log(path)[0]
+    assert len(log["final"]["model_weights"]) == 1
+    assert np.all(np.isfinite(log["train"]["p_loss"])) and len(log["train"]["p_loss"]) == 1600 - 300
+    assert np.isfinite(log["train"]["expert_J_tot"][-1])

@@ -274,3 +274,82 @@ def test_mt_unrolled_recurrence():
     assert np.array_equal(x[n], x[n - 227] ^ g(n - 624))
     n = np.arange(1078, len(x))
     assert np.array_equal(x[n], x[n - 681] ^ g(n - 624) ^ g(n - 851) ^ g(n - 1078))
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+def test_oracle_one_model_expert_matches_autograd(act):
+    """--num_models 1 (SAC_expert.py:273-296): every expert row, in order, through model 0;
+    MSE = mean over the rows of 0.5 ||sp_e - sp_pred||^2."""
+    cfg = O.Config(S=5, A=3, hidden=(16, 12), act=act, B=32, model_hidden=(20, 18))
+    st0, batch, noises, nrm, _ = _make(cfg, seed=4)
+    rs = np.random.RandomState(21)
+    ne = 7                                     # odd: one model needs no equal halves
+    ex = O.Expert(rs.normal(size=(ne, 5)), rs.normal(size=(ne, 5)), None, None, rs.normal(size=(ne, 3)), None, 0.4)
+    st1 = st0.copy()
+    keep = {}
+    stats = O.sac_update(st1, cfg, nrm, batch, *noises, expert=ex, keep=keep)
+    s = _t(batch[0])
+    nm = lambda x, m, dd: (x - _t(m)) / _t(dd)
+    PA = [_t(w).requires_grad_() for w in st0.actor]
+    LS = _t(st0.logstd).requires_grad_()
+    Q = [[_t(w) for w in net] for net in st1.q]
+    s_n = nm(s, nrm.s_mean, nrm.s_den)
+    mu = _mlp(PA, s_n, act)
+    pi, nlp = _head_eval(mu, LS.expand_as(mu), _t(noises[1]))
+    xq = torch.cat([s_n, nm(pi, nrm.a_mean, nrm.a_den)], 1)
+    minq = torch.minimum(_mlp(Q[0], xq, act), _mlp(Q[1], xq, act))
+    p = torch.mean(-float(st0.alpha) * nlp[:, None] - minq)
+    se_n = nm(_t(ex.s1), nrm.s_mean, nrm.s_den)
+    ca = torch.tanh(_mlp(PA, se_n, act) + torch.exp(torch.clamp(LS, -5, 2)) * _t(ex.noise1))
+    om = _mlp([_t(w) for w in st0.models[0]], torch.cat([se_n, nm(ca, nrm.a_mean, nrm.a_den)], 1), cfg.model_act)
+    sp_hat = _t(ex.s1) + (om[:, :5] * _t(nrm.d_den) + _t(nrm.d_mean))
+    mse = torch.mean(0.5 * ((_t(ex.sp1) - sp_hat) ** 2).sum(-1))
+    p = (1 - ex.epsilon) * p + ex.epsilon * mse
+    assert abs(stats["mse_loss"] - mse.item()) < 1e-10 and abs(stats["p_loss"] - p.item()) < 1e-10
+    g = torch.autograd.grad(p, PA + [LS])
+    for gg, mine in zip(g[:-1], keep["actor_grads"]):
+        np.testing.assert_allclose(mine, gg.numpy(), rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(keep["g_logstd"], g[-1].numpy(), rtol=1e-7, atol=1e-10)
+
+
+@pytest.mark.parametrize("nmodels,max_norm,dclip,rclip", [(2, 0.05, 0.0, 0.0), (1, 0.02, 0.3, 0.5),
+                                                          (2, 100.0, 0.0, 0.0)])
+def test_model_fit_clips_and_global_norm(nmodels, max_norm, dclip, rclip):
+    """--model_max_grad_norm (mbrl_onpolicy_alg.py:315-317: clip_by_global_norm to
+    max_norm * num_models) and the get_loss target clips (continuous_models.py:284-296),
+    against autograd + TF's clip_by_global_norm formula; a large max_norm leaves the step
+    unchanged."""
+    cfg = O.Config(S=4, A=2, hidden=(8, 8), B=16, model_hidden=(10, 12))
+    st = O.init_state(cfg, seed=6, with_models=True, bias_scale=0.1, model_gain=0.5).astype(np.float64)
+    rs = np.random.RandomState(2)
+    nrm = O.Normalizers(rs.normal(size=4) * .1, rs.uniform(.5, 2, 4), rs.normal(size=2) * .1,
+                        rs.uniform(.5, 2, 2), rs.normal(size=4) * .1, rs.uniform(.5, 2, 4), 0.2, 1.5, 1.0)
+    batches = [(rs.normal(size=(9, 4)), rs.uniform(-1, 1, (9, 2)), rs.normal(size=(9, 4)) * 3,
+                rs.normal(size=9) * 3) for _ in range(nmodels)]
+    M = [[_t(w).requires_grad_() for w in net] for net in st.models[:nmodels]]
+    tot = 0
+    for k, (s, a, sp, r) in enumerate(batches):
+        x = torch.cat([(_t(s) - _t(nrm.s_mean)) / _t(nrm.s_den), (_t(a) - _t(nrm.a_mean)) / _t(nrm.a_den)], 1)
+        out = _mlp(M[k], x, "relu")
+        dn = ((_t(sp) - _t(s)) - _t(nrm.d_mean)) / _t(nrm.d_den)
+        rn = (_t(r) - nrm.r_mean) / nrm.r_den
+        if dclip:
+            dn = torch.clamp(dn, -dclip, dclip)
+        if rclip:
+            rn = torch.clamp(rn, -rclip, rclip)
+        tot = tot + torch.mean(0.5 * ((dn - out[:, :4]) ** 2).sum(-1) + 0.5 * (rn - out[:, 4]) ** 2)
+    flat = [w for net in M for w in net]
+    g = [x.numpy() for x in torch.autograd.grad(tot, flat)]
+    clip = max_norm * nmodels
+    norm = np.sqrt(sum(np.sum(x * x) for x in g))
+    g = [x * (clip * min(1.0 / norm, 1.0 / clip)) for x in g]
+    ref = st.copy()
+    O.adam_step([w for k in range(nmodels) for w in ref.models[k]], g, ref.opt_model, cfg.lr_model, np.float64)
+    loss = O.model_fit_step(st, cfg, nrm, batches, max_grad_norm=max_norm, delta_clip_loss=dclip,
+                            reward_clip_loss=rclip)
+    assert abs(loss - tot.item()) < 1e-12
+    for k in range(nmodels):
+        for w1, w2 in zip(st.models[k], ref.models[k]):
+            np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=1e-14)
+    if nmodels == 1:                            # model 1 untouched
+        assert st.opt_model.t == 1
