@@ -68,6 +68,7 @@ class Config:
     init_temperature: float = 0.1  # train_parser.py:308
     act_limit: float = 1.0
     per_state_std: bool = False
+    layer_norm: bool = False      # --actor_layer_norm: Dense -> LayerNorm -> tanh (nn_utils.py:110-119)
     # SAC-EO
     epsilon: float = 1e-3         # train_parser.py:280
     model_hidden: Sequence[int] = (512, 512)
@@ -185,6 +186,10 @@ def init_state(cfg: Config, seed: int = 1, with_models: bool = False,
     rng = np.random.RandomState(seed)
     out_a = 2 * cfg.A if cfg.per_state_std else cfg.A
     actor = init_mlp(rng, cfg.S, out_a, cfg.hidden, actor_gain, bias_scale)
+    if cfg.layer_norm:            # gamma, beta after b0 (perturbed from 1 / 0 so the test sees them)
+        H0 = cfg.hidden[0]
+        actor = actor[:2] + [(1.0 + 0.1 * rng.normal(size=H0)).astype(np.float32),
+                             (0.1 * rng.normal(size=H0)).astype(np.float32)] + actor[2:]
     q = [init_mlp(rng, cfg.S + cfg.A, 1, cfg.hidden, critic_gain, bias_scale) for _ in range(2)]
     q_targ = [[w.copy() for w in net] for net in q]         # init_critic.py:34-35
     logstd = np.zeros((1, cfg.A), np.float32)
@@ -270,6 +275,41 @@ def mlp_backward(params, x, hs, dout, act, need_dx=False, need_dw=True):
         elif need_dx:
             dx = d @ params[0].T
     return grads, dx
+
+
+# ---------------------------------------------------------------------------
+# the actor's MLP: create_nn with layer_norm (nn_utils.py:108-119) puts Keras
+# LayerNormalization (epsilon 1e-3, gamma, beta) and tanh after the first Dense; its weight
+# list is [W0, b0, gamma, beta, W1, b1, W2, b2].  hs = [H1, H2] (+ [xhat, rstd] with the norm).
+# ---------------------------------------------------------------------------
+LN_EPS = 1e-3
+
+
+def actor_forward(params, x, cfg):
+    if not cfg.layer_norm:
+        return mlp_forward(params, x, cfg.act)
+    dt = x.dtype.type
+    z = x @ params[0] + params[1]
+    mu = z.mean(-1, keepdims=True)
+    d = z - mu
+    rstd = _F(dt, 1) / np.sqrt((d * d).mean(-1, keepdims=True) + _F(dt, LN_EPS))
+    xh = d * rstd
+    h1 = np.tanh(params[2] * xh + params[3])
+    out, hs = mlp_forward(params[4:], h1, cfg.act)
+    return out, [h1] + hs + [xh, rstd]
+
+
+def actor_backward(params, x, hs, dout, cfg):
+    """Gradients of the actor weight list (same order as params)."""
+    if not cfg.layer_norm:
+        return mlp_backward(params, x, hs, dout, cfg.act)[0]
+    h1, h2, xh, rstd = hs
+    g_rest, dh1 = mlp_backward(params[4:], h1, [h2], dout, cfg.act, need_dx=True)
+    one = np.ones((), h1.dtype)
+    dy = dh1 * (one - h1 * h1)
+    gg = dy * params[2]
+    dz = rstd * ((gg - gg.mean(-1, keepdims=True)) - xh * (gg * xh).mean(-1, keepdims=True))
+    return [x.T @ dz, dz.sum(axis=0), (dy * xh).sum(axis=0), dy.sum(axis=0)] + g_rest
 
 
 # ---------------------------------------------------------------------------
@@ -398,7 +438,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
 
     # ---------------- target (_get_Q_target, SAC_expert.py:211-229)
     sp_n = _norm(sp, nrm.s_mean, nrm.s_den)
-    out_t, hs_t = mlp_forward(actor_all, sp_n, cfg.act)
+    out_t, hs_t = actor_forward(actor_all, sp_n, cfg)
     mu_t, ls_t = split_head(out_t, st.logstd, cfg)
     a_t, nlp_t, _ = head_evaluate(mu_t, ls_t, n1, lim, dt)
     xq_t = np.concatenate([sp_n, _norm(a_t, nrm.a_mean, nrm.a_den)], axis=1)
@@ -424,7 +464,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
         adam_step(st.q[k], hook("q%d" % k, grads), st.opt_q[k], cfg.lr_q, dt)
 
     # ---------------- actor (_update_actor_and_alpha, :262-338)
-    out_p, hs_p = mlp_forward(actor_all, s_n, cfg.act)
+    out_p, hs_p = actor_forward(actor_all, s_n, cfg)
     mu_p, ls_p = split_head(out_p, st.logstd, cfg)
     a_p, nlp_p, cache_p = head_evaluate(mu_p, ls_p, n2, lim, dt)
     xq_p = np.concatenate([s_n, _norm(a_p, nrm.a_mean, nrm.a_den)], axis=1)
@@ -462,7 +502,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
         for k, (se, spe, ne) in enumerate(halves):
             se, spe, ne = np.asarray(se, dt), np.asarray(spe, dt), np.asarray(ne, dt)
             se_n = _norm(se, nrm.s_mean, nrm.s_den)
-            out_e, hs_e = mlp_forward(actor_all, se_n, cfg.act)
+            out_e, hs_e = actor_forward(actor_all, se_n, cfg)
             mu_e, ls_e = split_head(out_e, st.logstd, cfg)
             ca, cache_e = head_sample(mu_e, ls_e, ne, lim, dt)
             xm = np.concatenate([se_n, _norm(ca, nrm.a_mean, nrm.a_den)], axis=1)
@@ -500,7 +540,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     else:
         dout_a = DMU
         g_logstd = DL.sum(axis=0, keepdims=True)
-    grads_a, _ = mlp_backward(actor_all, X, Hs, dout_a, cfg.act)
+    grads_a = actor_backward(actor_all, X, Hs, dout_a, cfg)
     if keep is not None:
         keep.update(actor_h_p=hs_p, mu_p=mu_p, a_p=a_p, nlp_p=nlp_p, q1p=q1p, q2p=q2p,
                     dxa=dxa, dmu=DMU, dl=DL, actor_grads=grads_a, g_logstd=g_logstd)
@@ -508,7 +548,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     adam_step(st.actor + [st.logstd], hook("actor", grads_a + [g_logstd]), st.opt_actor, cfg.lr_pi, dt)
 
     # ---------------- alpha (:340-348)
-    out_3, _ = mlp_forward(st.actor, s_n, cfg.act)
+    out_3, _ = actor_forward(st.actor, s_n, cfg)
     mu_3, ls_3 = split_head(out_3, st.logstd, cfg)
     _, nlp_3, _ = head_evaluate(mu_3, ls_3, n3, lim, dt)
     m_ent = np.mean(-nlp_3 + F(cfg.target_entropy))
@@ -602,7 +642,7 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
     lim = F(cfg.act_limit)
     for _ in range(horizon):
         x = _norm(s, nrm.s_mean, nrm.s_den)
-        o, _ = mlp_forward(st.actor, x, cfg.act)
+        o, _ = actor_forward(st.actor, x, cfg)
         mu, lraw = split_head(o, st.logstd, cfg)
         u = np.zeros_like(mu) if deterministic else f32_noise(rs.normal(size=mu.shape)).astype(dt)
         a, _ = head_sample(mu, lraw, u, cfg.act_limit, dt)
@@ -638,7 +678,7 @@ def _model_sample(st, cfg, nrm, k, s, a, delta_clip=0.0):
 
 def _actor_sample(st, cfg, nrm, s, rs):
     dt = st.alpha.dtype.type
-    o, _ = mlp_forward(st.actor, _norm(s, nrm.s_mean, nrm.s_den), cfg.act)
+    o, _ = actor_forward(st.actor, _norm(s, nrm.s_mean, nrm.s_den), cfg)
     mu, lraw = split_head(o, st.logstd, cfg)
     u = f32_noise(rs.normal(size=mu.shape)).astype(dt)
     return head_sample(mu, lraw, u, cfg.act_limit, dt)[0]
@@ -686,7 +726,7 @@ def actor_evaluate(st, cfg, nrm, s, rs):
     with u = rs.normal(size=(n, A)) cast to f32."""
     dt = st.alpha.dtype.type
     nrm = nrm.cast(dt)
-    o, _ = mlp_forward(st.actor, _norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den), cfg.act)
+    o, _ = actor_forward(st.actor, _norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den), cfg)
     mu, lraw = split_head(o, st.logstd, cfg)
     u = f32_noise(rs.normal(size=mu.shape)).astype(dt)
     pi, nlp, _ = head_evaluate(mu, lraw, u, cfg.act_limit, dt)

@@ -2605,6 +2605,87 @@ __global__ __launch_bounds__(64) void k_gnorm_final(GNormArgs a) {
     }
 }
 
+// ==================================================================== k_ln (actor layer norm)
+template <int NQ>
+__global__ __launch_bounds__(256) void k_ln(LNArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t so = seed_off(a.sstride);
+    const int H = a.H;
+    const float inv_h = 1.f / (float)H;
+    int row = blockIdx.x * 4 + wave;
+    const float* gamma = sr(a.gamma, so);
+    if (a.mode == 0) {
+        // rows [r0, r1) then [r2, r3), as one index space
+        const int n0 = a.r[1] - a.r[0];
+        if (row >= n0 + (a.nrange > 1 ? a.r[3] - a.r[2] : 0)) return;
+        row = row < n0 ? a.r[0] + row : a.r[2] + (row - n0);
+        float* z = sr(a.Z, so) + (size_t)row * H;
+        float v[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) v[q] = (lane + 64 * q < H) ? z[lane + 64 * q] : 0.f;
+        float s = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) s += v[q];
+        const float mu = wave_sum(s) * inv_h;
+        float ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const float d = (lane + 64 * q < H) ? v[q] - mu : 0.f;
+            ss += d * d;
+        }
+        const float var = wave_sum(ss) * inv_h;
+        const float rstd = 1.f / sqrtf(var + 1e-3f);     // Keras LayerNormalization epsilon
+        const bool cache = row < a.cache_rows && a.xhat != nullptr;
+        float* xh = cache ? sr(a.xhat, so) + (size_t)row * H : nullptr;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            const int j = lane + 64 * q;
+            if (j < H) {
+                const float x = (v[q] - mu) * rstd;
+                if (cache) xh[j] = x;
+                z[j] = tanhf(gamma[j] * x + gamma[H + j]);
+            }
+        }
+        if (cache && lane == 0) sr(a.rstd, so)[row] = rstd;
+        return;
+    }
+    // mode 1: dY -> dZ = rstd (g - mean(g) - xhat mean(g xhat)), g = dY gamma
+    if (row >= a.r[1]) return;
+    float* d = sr(a.Z, so) + (size_t)row * H;
+    const float* xh = sr(a.xhat, so) + (size_t)(row + a.xrow0) * H;
+    const float rstd = sr(a.rstd, so)[row + a.xrow0];
+    float dy[NQ], x[NQ];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int j = lane + 64 * q;
+        dy[q] = j < H ? d[j] : 0.f;
+        x[q] = j < H ? xh[j] : 0.f;
+        const float g = j < H ? dy[q] * gamma[j] : 0.f;
+        s1 += g;
+        s2 += g * x[q];
+    }
+    const float m1 = wave_sum(s1) * inv_h, m2 = wave_sum(s2) * inv_h;
+    float* gy = sr(a.gy, so) + (size_t)row * H;
+    float* gb = sr(a.gb, so) + (size_t)row * H;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+        const int j = lane + 64 * q;
+        if (j < H) {
+            d[j] = rstd * ((dy[q] * gamma[j] - m1) - x[q] * m2);
+            gy[j] = dy[q] * x[q];
+            gb[j] = dy[q];
+        }
+    }
+}
+
+void launch_ln(const LNArgs& a, hipStream_t s) {
+    const int rows = a.mode == 0 ? (a.r[1] - a.r[0]) + (a.nrange > 1 ? a.r[3] - a.r[2] : 0) : a.r[1];
+    const dim3 grid((rows + 3) / 4, 1, seeds_z(a.nseeds));
+    if (a.H <= 256) hipLaunchKernelGGL(k_ln<4>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(k_ln<8>, grid, dim3(256), 0, s, a);
+}
+
 void launch_gnorm(const GNormArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_gnorm_part, dim3(GNORM_PARTS), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_gnorm_final, dim3(1), dim3(64), 0, s, a);

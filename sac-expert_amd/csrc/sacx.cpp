@@ -62,7 +62,7 @@ struct SegInfo {
 
 struct Launch {
     enum Kind { RNG, GATHER, GEMM, AHEAD, QHEAD, ABWD, FINAL, MGATHER, MLOSS, MFINAL, ALLREDUCE, APPLY, AAPPLY,
-                GNORM } kind;
+                GNORM, LNORM } kind;
     std::string name;
     RngArgs rng;
     GatherArgs gather;
@@ -76,6 +76,7 @@ struct Launch {
     MFinalArgs mf;
     AdamApplyArgs ap;          // APPLY
     GNormArgs gn;              // GNORM
+    LNArgs ln;                 // LNORM
     float* ar_buf = nullptr;   // ALLREDUCE: in-place sum over the data-parallel ranks
     int64_t ar_count = 0;
     int grid = 0, block = 256;
@@ -105,6 +106,7 @@ const char* kernel_family(Launch::Kind k) {
         case Launch::APPLY: return "k_adam_apply";
         case Launch::AAPPLY: return "k_alpha_apply";
         case Launch::GNORM: return "k_gnorm";
+        case Launch::LNORM: return "k_ln";
     }
     return "?";
 }
@@ -120,6 +122,7 @@ struct sacx_handle {
     int64_t cap = 0;
     int graph_steps = 128, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
     int nm = 0;               // SAC-EO world models (--num_models: 1 or 2)
+    bool ln = false;          // --actor_layer_norm: Dense -> LayerNorm -> tanh on the actor's layer 0
     // layout
     std::vector<SegInfo> segs;
     std::map<std::string, size_t> seg_index;
@@ -205,6 +208,7 @@ void build_layout(sacx_handle* h) {
         h->add(n + ".l2", h1 + 1, out, F, role);
     };
     net("actor", S, h->Aout, SACX_ROLE_PARAM, H0, H1);
+    if (h->ln) h->add("actor.ln", 2, H0, F, SACX_ROLE_PARAM);     // LayerNormalization gamma ; beta
     h->add("actor.logstd", 1, A, F, SACX_ROLE_PARAM);
     net("q0", S + A, 1, SACX_ROLE_PARAM, H0, H1);
     net("q1", S + A, 1, SACX_ROLE_PARAM, H0, H1);
@@ -313,6 +317,12 @@ void build_layout(sacx_handle* h) {
     h->add("act.H1", ACT_CAP, H0, F, 0);
     h->add("act.H2", ACT_CAP, H1, F, 0);
     h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
+    if (h->ln) {                      // layer-norm caches of the update's actor rows
+        h->add("ws.ln_xhat", h->Ra, H0, F, 0);
+        h->add("ws.ln_rstd", 1, h->Ra, F, 0);
+        h->add("ws.ln_gy", h->Rb, H0, F, 0);
+        h->add("ws.ln_gb", h->Rb, H0, F, 0);
+    }
     h->add("act.Xq", ACT_CAP, h->ldQ, F, 0);          // sacx_critic_forward input [norm s | norm a]
     h->add("act.Q", ACT_CAP, 1, F, 0);                // sacx_critic_forward output
     if (h->cfg.use_expert) {          // world-model fitting (A16)
@@ -497,6 +507,8 @@ void pack_seeds(Launch& L, int64_t stride, int n) {
     L.rng.sstride = L.gather.sstride = L.gemm.sstride = L.head.sstride = L.fin.sstride = L.qh.sstride =
         L.ab.sstride = stride;
     L.rng.nseeds = L.gather.nseeds = L.gemm.nseeds = L.head.nseeds = L.fin.nseeds = L.qh.nseeds = L.ab.nseeds = n;
+    L.ln.sstride = stride;
+    L.ln.nseeds = n;
 }
 
 // Data-parallel mode: the dW launch `L` stores its local gradients (+3 p_stride) instead of
@@ -630,8 +642,29 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     };
     // the previous update's alpha forward (B rows) is folded into this launch (merged_body)
     const int alpha_tiles = ((B + 15) / 16) * ((H1 + 15) / 16);
-    const bool actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
-             {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a, -1, alpha_tiles);
+    const int Ra4 = (h->Ra + 3) & ~3;       // first row of the alpha rows (ws.Hl1 / ws.Hl2 alias Ha1 / Ha2)
+    // --actor_layer_norm: layer 0 writes the pre-norm Z, k_ln turns it into tanh(LN(Z)) in place
+    auto ln_fwd = [&](const std::string& name, int r0, int r1) {
+        Launch L{};
+        L.kind = Launch::LNORM;
+        L.name = name;
+        LNArgs& a = L.ln;
+        a.mode = 0; a.H = H0; a.Z = Ha1; a.nrange = 1; a.r[0] = r0; a.r[1] = r1;
+        a.gamma = W("actor.ln"); a.xhat = W("ws.ln_xhat"); a.rstd = W("ws.ln_rstd"); a.cache_rows = h->Ra;
+        L.grid = (r1 - r0 + 3) / 4;
+        L.flops = 8.0 * (r1 - r0) * H0;
+        L.bytes = 4.0 * (r1 - r0) * H0 * 3;
+        plan.push_back(L);
+    };
+    bool actor_fused = false;
+    if (h->ln) {
+        add_gemm(h, plan, "actor.fwd0", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, ACT_NONE)}, record_probs);
+        ln_fwd("actor.ln", 0, h->Ra);
+        add_gemm(h, plan, "actor.fwd1", {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, record_probs);
+    } else {
+        actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
+                               {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a, -1, alpha_tiles);
+    }
     // actor.head folded into q.fwd0 (plain SAC): the target tiles compute their rows' actions
     // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
     // workgroups of the same launch.  SACX_FUSE_HEAD=0 keeps the separate launch.
@@ -907,8 +940,22 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.bytes = 4.0 * (2.0 * B * H0 + ne * Hm0 + 2.0 * h->Rb * H1);
         plan.push_back(L);
         const int Rb = h->Rb;
-        add_gemm(h, plan, "actor.bwd1",
-                 {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, act)}, record_probs);
+        add_gemm(h, plan, "actor.bwd1",      // layer-norm layer 0: tanh' at its output
+                 {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, h->ln ? ACT_TANH : act)},
+                 record_probs);
+        if (h->ln) {                          // dY -> dZ through the norm; dY*xhat, dY for gamma / beta
+            Launch N{};
+            N.kind = Launch::LNORM;
+            N.name = "actor.ln.bwd";
+            LNArgs& a = N.ln;
+            a.mode = 1; a.H = H0; a.Z = Da1; a.r[1] = Rb; a.gamma = W("actor.ln");
+            a.xhat = W("ws.ln_xhat"); a.rstd = W("ws.ln_rstd"); a.xrow0 = B;
+            a.gy = W("ws.ln_gy"); a.gb = W("ws.ln_gb");
+            N.grid = (Rb + 3) / 4;
+            N.flops = 8.0 * Rb * H0;
+            N.bytes = 4.0 * Rb * H0 * 5;
+            plan.push_back(N);
+        }
         std::vector<GemmProb> pw;
         pw.push_back(prob_dw(Xa + (size_t)B * ldS, ldS, S, Rb, Da1, H0, W("actor.l0"), nullptr, GRP_PI));
         pw.push_back(prob_dw(Ha1 + (size_t)B * H0, H0, H0, Rb, Da2, H1, W("actor.l1"), nullptr, GRP_PI));
@@ -918,14 +965,29 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             p.ones_row = 0;   // single all-ones row: column sums of E
             pw.push_back(p);
         }
+        if (h->ln) {          // gamma, beta: column sums of dY*xhat and dY
+            for (int k = 0; k < 2; ++k) {
+                float* gsrc = W(k ? "ws.ln_gb" : "ws.ln_gy");
+                GemmProb p = prob_dw(gsrc, 1, 0, Rb, gsrc, H0, W("actor.ln") + (size_t)k * H0, nullptr, GRP_PI);
+                p.ones_row = 0;
+                pw.push_back(p);
+            }
+        }
         add_gemm(h, plan, "actor.adam", pw, record_probs);
         if (h->dp_ranks > 0) dp_split_adam(h, plan, "actor.l0", "actor.logstd", "", GRP_PI);
     }
     // ---- alpha: updated actor on s, evaluate, Adam on alpha, statistics
     const size_t alpha_first = plan.size();
     // the alpha forward is folded into the next update's actor forward (merged_body): same fusion
-    fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
-             {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, fuse_a, actor_fused ? 1 : 0);
+    if (h->ln) {
+        add_gemm(h, plan, "alpha.fwd0", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, ACT_NONE)},
+                 record_probs);
+        ln_fwd("alpha.ln", Ra4, Ra4 + B);
+        add_gemm(h, plan, "alpha.fwd1", {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, record_probs);
+    } else {
+        fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
+                 {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, fuse_a, actor_fused ? 1 : 0);
+    }
     {
         Launch L{};
         L.kind = Launch::AHEAD;
@@ -1110,6 +1172,7 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::APPLY: launch_adam_apply(L.ap, s); break;
         case Launch::AAPPLY: launch_alpha_apply(L.fin, s); break;
         case Launch::GNORM: launch_gnorm(L.gn, s); break;
+        case Launch::LNORM: launch_ln(L.ln, s); break;
     }
 }
 
@@ -1136,16 +1199,17 @@ void enqueue_step(sacx_handle* h, int slot, bool with_rng, hipStream_t s) {
 bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& out) {
     out.clear();
     std::vector<const Launch*> pg;
-    const Launch *ph = nullptr, *pf = nullptr;
+    const Launch *ph = nullptr, *pf = nullptr, *pln = nullptr;
     if (prev_slot >= 0)
         for (const Launch& L : h->plan[prev_slot]) {
             if (!L.alpha_branch) continue;
             if (L.kind == Launch::GEMM) pg.push_back(&L);
             else if (L.kind == Launch::AHEAD) ph = &L;
             else if (L.kind == Launch::FINAL) pf = &L;
+            else if (L.kind == Launch::LNORM) pln = &L;
         }
     size_t gi = 0;
-    bool head_done = prev_slot < 0, final_done = prev_slot < 0;
+    bool head_done = prev_slot < 0, final_done = prev_slot < 0, ln_done = pln == nullptr;
     for (const Launch& L : h->plan[slot]) {
         if (is_prologue(L) || L.alpha_branch) continue;
         Launch C = L;
@@ -1154,6 +1218,14 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                 if (!merge_gemm(C.gemm, pg[gi]->gemm)) return false;
                 C.name += "+alpha";
                 ++gi;
+            } else if (C.kind == Launch::LNORM && !ln_done && C.ln.mode == 0) {
+                // the previous update's alpha rows through the layer norm in the same launch
+                C.ln.nrange = 2;
+                C.ln.r[2] = pln->ln.r[0];
+                C.ln.r[3] = pln->ln.r[1];
+                C.grid += pln->grid;
+                C.name += "+alpha";
+                ln_done = true;
             } else if (!head_done && ph && (C.kind == Launch::AHEAD || (C.kind == Launch::GEMM && C.gemm.rowk == 3))) {
                 // the head rows: a standalone actor.head, or the rows folded into q.fwd0
                 HeadArgs& a = C.kind == Launch::AHEAD ? C.head : C.gemm.head;
@@ -1187,7 +1259,7 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
         }
         out.push_back(C);
     }
-    return gi == pg.size() && head_done && final_done;
+    return gi == pg.size() && head_done && final_done && ln_done;
 }
 
 // Captured chain of G updates on two streams (see the fork branch below):
@@ -1466,7 +1538,6 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     }
     if (cfg->num_models < 0 || cfg->num_models > 2) return bad("num_models must be 1 or 2 (0 -> 2)");
     if (cfg->actor_gaussian && cfg->actor_std_mult < 0.f) return bad("actor_std_mult must be positive");
-    if (cfg->actor_layer_norm) return bad("actor_layer_norm is not built");
     auto* h = new sacx_handle();
     h->cfg = *cfg;
     h->S = cfg->s_dim;
@@ -1484,6 +1555,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->mact = cfg->model_activation;
     h->mb = cfg->use_expert ? (cfg->model_batch > 0 ? cfg->model_batch : 200) : 0;
     h->nm = cfg->use_expert ? (cfg->num_models > 0 ? cfg->num_models : 2) : 0;
+    h->ln = cfg->actor_layer_norm != 0;
     h->ldS = (int)r4(h->S);
     h->ldQ = (int)r4(h->S + h->A);
     h->stride = (int)r4(2 * h->S + h->A + 2);
@@ -1839,10 +1911,28 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
     return 0;
 }
 
+// The actor's hidden layers on m rows of X (row stride ldX) into H1b [m, H0] and H2b [m, H1]:
+// Dense + activation, or with --actor_layer_norm Dense -> LayerNorm -> tanh on layer 0
+// (nn_utils.py:110-119).  Eager launches on st (or captured by the caller).
+static void actor_hidden(sacx_handle* h, const float* X, int ldX, int m, float* H1b, float* H2b, hipStream_t st) {
+    std::vector<Launch> pl;
+    add_gemm(h, pl, "a.fwd0", {prob_fwd(X, ldX, m, h->S, h->f("actor.l0"), h->H0, H1b, h->ln ? ACT_NONE : h->act)},
+             false);
+    add_gemm(h, pl, "a.fwd1", {prob_fwd(H1b, h->H0, m, h->H0, h->f("actor.l1"), h->H1, H2b, h->act)}, false);
+    h->probs_cursor -= 2;          // host table bookkeeping of add_gemm (these launches are not in a plan)
+    launch_gemm(pl[0].gemm, st);
+    if (h->ln) {
+        LNArgs a{};
+        a.mode = 0; a.H = h->H0; a.Z = H1b; a.nrange = 1; a.r[1] = m; a.gamma = h->f("actor.ln");
+        launch_ln(a, st);
+    }
+    launch_gemm(pl[1].gemm, st);
+}
+
 int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
-    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS;
+    const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     for (int64_t done = 0; done < n; done += ACT_CAP) {
         const int m = (int)std::min<int64_t>(ACT_CAP, n - done);
@@ -1855,11 +1945,7 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
             launch_rng(r, h->stream);
         }
         launch_obs_norm(obs + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
-        std::vector<Launch> pl;
-        add_gemm(h, pl, "act.fwd0", {prob_fwd(W("act.X"), ldS, m, S, W("actor.l0"), H0, W("act.H1"), h->act)}, false);
-        add_gemm(h, pl, "act.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W("actor.l1"), H1, W("act.H2"), h->act)}, false);
-        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
-        h->probs_cursor -= 2;          // host table bookkeeping of add_gemm (these launches are not in a plan)
+        actor_hidden(h, W("act.X"), ldS, m, W("act.H1"), W("act.H2"), h->stream);
         HeadArgs a{};
         a.H2 = W("act.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
@@ -1897,7 +1983,7 @@ int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out
     if (!h || !h->bound) return fail(h, "not bound");
     if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n < 0 || (n > 0 && (!s || !pi_out || !nlp_out))) return fail(h, "bad arguments");
-    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS;
+    const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     for (int64_t done = 0; done < n; done += ACT_CAP) {
         const int m = (int)std::min<int64_t>(ACT_CAP, n - done);
@@ -1907,11 +1993,7 @@ int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out
         r.slot = -1; r.reset_seq = 0; r.nupd = 1;
         launch_rng(r, h->stream);
         launch_obs_norm(s + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
-        std::vector<Launch> pl;
-        add_gemm(h, pl, "eval.fwd0", {prob_fwd(W("act.X"), ldS, m, S, W("actor.l0"), H0, W("act.H1"), h->act)}, false);
-        add_gemm(h, pl, "eval.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W("actor.l1"), H1, W("act.H2"), h->act)}, false);
-        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
-        h->probs_cursor -= 2;
+        actor_hidden(h, W("act.X"), ldS, m, W("act.H1"), W("act.H2"), h->stream);
         HeadArgs a{};
         a.H2 = W("act.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
@@ -2019,7 +2101,7 @@ int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* 
 static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
                      int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
                      float* r_out, float* sp_out, uint8_t* d_out, hipStream_t st) {
-    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
+    const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     const std::string mn = "m" + std::to_string(model);
@@ -2047,11 +2129,8 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
                 r.slot = -1; r.reset_seq = 0; r.nupd = 1;
                 launch_rng(r, st);
             }
+            actor_hidden(h, W("roll.X"), ldS, m, W("roll.H1"), W("roll.H2"), st);
             std::vector<Launch> pl;
-            add_gemm(h, pl, "roll.a.fwd0", {prob_fwd(W("roll.X"), ldS, m, S, W("actor.l0"), H0, W("roll.H1"), h->act)}, false);
-            add_gemm(h, pl, "roll.a.fwd1", {prob_fwd(W("roll.H1"), H0, m, H0, W("actor.l1"), H1, W("roll.H2"), h->act)}, false);
-            for (auto& L : pl) launch_gemm(L.gemm, st);
-            pl.clear();
             HeadArgs a{};
             a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
             a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
@@ -2069,7 +2148,7 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
             add_gemm(h, pl, "roll.m.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->mact)}, false);
             add_gemm(h, pl, "roll.m.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), O, W("roll.O"), ACT_NONE)}, false);
             for (auto& L : pl) launch_gemm(L.gemm, st);
-            h->probs_cursor -= 5;      // host table bookkeeping of add_gemm (these launches are not in a plan)
+            h->probs_cursor -= 3;      // host table bookkeeping of add_gemm (these launches are not in a plan)
             ra.mode = 1;
             launch_roll(ra, st);
         }
@@ -2125,7 +2204,7 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     const bool disc = (flags & SACX_DIAG_DISC) != 0, ea = (flags & SACX_DIAG_EXPERT_ACTIONS) != 0;
     if (disc && h->nm < 2) return fail(h, "_calc_disc compares two world models (num_models = 2)");
     if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
-    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
+    const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     DiagArgs d{};
@@ -2158,11 +2237,7 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
         r.n_int = 0; r.n_norm = n * A; r.out_idx = nullptr; r.out_norm = W("roll.noise");
         r.slot = -1; r.reset_seq = 0; r.nupd = 1;
         launch_rng(r, h->stream);
-        std::vector<Launch> pl;
-        add_gemm(h, pl, "diag.a.fwd0", {prob_fwd(W("roll.X"), ldS, n, S, W("actor.l0"), H0, W("roll.H1"), h->act)}, false);
-        add_gemm(h, pl, "diag.a.fwd1", {prob_fwd(W("roll.H1"), H0, n, H0, W("actor.l1"), H1, W("roll.H2"), h->act)}, false);
-        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
-        h->probs_cursor -= 2;
+        actor_hidden(h, W("roll.X"), ldS, n, W("roll.H1"), W("roll.H2"), h->stream);
         HeadArgs a{};
         a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;

@@ -371,6 +371,25 @@ struct AdamApplyArgs {
     AdamConsts adam;
 };
 
+// ---------------------------------------------------------------- actor layer norm (A3)
+// --actor_layer_norm: layer 0 is Dense -> LayerNormalization (epsilon 1e-3, gamma / beta) -> tanh
+// (nn_utils.py:110-119).  The layer-0 GEMM writes the pre-norm Z; k_ln mode 0 turns rows of Z
+// into tanh(gamma xhat + beta) in place (caching xhat, rstd for rows < cache_rows); mode 1 turns
+// dY (the gradient at the norm's output, after tanh') into dZ in place and writes dY*xhat and
+// dY for the gamma / beta column sums.  One wave per row, H <= 512.
+struct LNArgs {
+    int32_t mode;
+    int32_t H;
+    float* Z;                   // [rows, H] (mode 0: Z -> H1; mode 1: dY -> dZ)
+    int32_t nrange, r[4];       // mode 0: row ranges [r0, r1) (+ [r2, r3)); mode 1: rows [0, r1)
+    const float* gamma;         // [H] (beta = gamma + H)
+    float* xhat; float* rstd;   // cache (mode 0 writes rows < cache_rows, mode 1 reads row + xrow0)
+    int32_t cache_rows, xrow0;
+    float* gy; float* gb;       // mode 1: [rows, H] dY * xhat and dY
+    int64_t sstride;
+    int32_t nseeds;
+};
+
 // clip_by_global_norm (mbrl_onpolicy_alg.py:315-317 over TF's clip_ops): k_gnorm_part sums g^2
 // over contiguous chunks of the gradient range, k_gnorm_final forms norm = sqrt(sum) and
 // scale = clip * min(1 / norm, 1 / clip) (+ (norm - norm): NaN when the norm is not finite)
@@ -432,6 +451,7 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s);
 void launch_roll(const RollArgs& a, hipStream_t s);
 void launch_net_io(const NetIOArgs& a, hipStream_t s);
 void launch_gnorm(const GNormArgs& a, hipStream_t s);
+void launch_ln(const LNArgs& a, hipStream_t s);
 void launch_diag(const DiagArgs& a, hipStream_t s);
 void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s);
 void launch_alpha_apply(const FinalArgs& f, hipStream_t s);

@@ -38,8 +38,7 @@ class GaussianActor:
         self.activation = acts[0]
         if any(a != self.activation for a in acts):
             raise NotImplementedError("one activation for all hidden layers")
-        if layer_norm:
-            raise NotImplementedError("actor_layer_norm is not built (off by default)")
+        self.layer_norm = bool(layer_norm)
         if output_norm and self.squash:
             raise NotImplementedError("actor_output_norm of the squashed actor is not built (off by default)")
         self.output_norm = bool(output_norm)
@@ -52,7 +51,7 @@ class GaussianActor:
         self.min_log_std, self.max_log_std = -5, 2
         out_dim = 2 * self.a_dim if self.per_state_std else self.a_dim
         rng = rng if rng is not None else np.random.default_rng(np.random.randint(2 ** 31))
-        self._w = create_nn_weights(rng, self.s_dim, out_dim, self.layers, gain)
+        self._w = create_nn_weights(rng, self.s_dim, out_dim, self.layers, gain, self.layer_norm)
         self._logstd = np.zeros((1, self.a_dim), np.float32)     # tf.Variable(zeros), :56-58
         self._engine = None
         self._net = None

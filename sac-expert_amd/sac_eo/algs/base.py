@@ -104,7 +104,7 @@ class SACBase:
             target_entropy=-float(self.a_dim), act_limit=float(np.max(self.actor.act_limit)),
             epsilon=float(self.epsilon),
             reward_loss_coef=self.models[0].reward_loss_coef if self.use_expert else 1.0,
-            num_models=len(self.models) if self.use_expert else 2,
+            num_models=len(self.models) if self.use_expert else 2, actor_layer_norm=self.actor.layer_norm,
             model_max_grad_norm=float(self.model_max_grad_norm or 0.0),
             delta_clip_loss=float(self.models[0].delta_clip_loss or 0.0) if self.use_expert else 0.0,
             reward_clip_loss=float(self.models[0].reward_clip_loss or 0.0) if self.use_expert else 0.0)

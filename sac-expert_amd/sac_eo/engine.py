@@ -206,6 +206,8 @@ class Engine:
             v[k].fill_(1.0)
         v["norm.r"][0, 1] = 1.0
         v["alpha"].fill_(float(np.float32(np.log(cfg.init_temperature))))   # SAC_expert.py:106
+        if cfg.actor_layer_norm:
+            v["actor.ln"][0].fill_(1.0)                                      # gamma = 1, beta = 0
         self.rng_seed(0)
 
     # ------------------------------------------------------------------ weights
@@ -213,7 +215,13 @@ class Engine:
         return [self.v[f"{net}.l{i}"] for i in range(3)]
 
     def set_net(self, net: str, weights: Sequence[np.ndarray]):
-        """Keras get_weights() list [W0, b0, W1, b1, W2, b2] -> W_ext views."""
+        """Keras get_weights() list [W0, b0, W1, b1, W2, b2] -> W_ext views; the actor with
+        actor_layer_norm has [W0, b0, gamma, beta, W1, ...] (nn_utils.py:110-119)."""
+        weights = list(weights)
+        if net == "actor" and self.cfg.actor_layer_norm:
+            gb = np.stack([np.asarray(weights[2], np.float32).reshape(-1), np.asarray(weights[3], np.float32).reshape(-1)])
+            self.v["actor.ln"].copy_(torch.as_tensor(gb))
+            weights = weights[:2] + weights[4:]
         for i, t in enumerate(self._layers(net)):
             W = torch.as_tensor(np.asarray(weights[2 * i], np.float32))
             b = torch.as_tensor(np.asarray(weights[2 * i + 1], np.float32)).reshape(1, -1)
@@ -226,6 +234,9 @@ class Engine:
         for t in self._layers(net):
             a = t.detach().cpu().numpy()
             out += [a[:-1].copy(), a[-1].copy()]
+        if net == "actor" and self.cfg.actor_layer_norm:
+            gb = self.v["actor.ln"].cpu().numpy()
+            out = out[:2] + [gb[0].copy(), gb[1].copy()] + out[2:]
         return out
 
     def set_logstd(self, logstd):

@@ -27,12 +27,15 @@ def orthogonal(rng: np.random.Generator, shape, gain: float) -> np.ndarray:
 
 
 def create_nn_weights(rng: np.random.Generator, in_dim: int, out_dim: int, layers: Sequence[int],
-                      gain: float) -> List[np.ndarray]:
-    """Keras get_weights() list [W0, b0, ..., W_L, b_L] of create_nn(...)."""
+                      gain: float, layer_norm: bool = False) -> List[np.ndarray]:
+    """Keras get_weights() list [W0, b0, ..., W_L, b_L] of create_nn(...); with layer_norm the
+    LayerNormalization's [gamma (ones), beta (zeros)] follow b0 (nn_utils.py:110-119)."""
     dims = [in_dim] + list(layers) + [out_dim]
     out = []
     for l in range(len(dims) - 1):
         g = math.sqrt(2.0) if l < len(dims) - 2 else gain
         out.append(orthogonal(rng, (dims[l], dims[l + 1]), g))
         out.append(np.zeros(dims[l + 1], np.float32))
+        if l == 0 and layer_norm:
+            out += [np.ones(dims[1], np.float32), np.zeros(dims[1], np.float32)]
     return out

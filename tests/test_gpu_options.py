@@ -120,3 +120,94 @@ def test_gaussian_actor_sample(gpu_available, per_state_std, output_norm, determ
     with pytest.raises(Exception):
         eng.step(1)                         # inference only
     eng.close()
+
+
+def _actor_grads(eng, B1):
+    """The actor's gradients read back through Adam's first moment (m_1 = g (1 - beta1)), in
+    the Keras weight-list order (with the layer norm: [W0, b0, gamma, beta, W1, b1, W2, b2])."""
+    m = eng.v["adam_m"][0]
+    out = []
+    for i in range(3):
+        seg = eng.segments[f"actor.l{i}"]
+        o, n = seg["offset"] // 4, seg["rows"] * seg["cols"]
+        w = m[o:o + n].cpu().numpy().reshape(seg["rows"], seg["cols"]) / B1
+        out += [w[:-1], w[-1]]
+        if i == 0 and "actor.ln" in eng.segments:
+            seg = eng.segments["actor.ln"]
+            o = seg["offset"] // 4
+            gb = m[o:o + 2 * seg["cols"]].cpu().numpy().reshape(2, -1) / B1
+            out += [gb[0], gb[1]]
+    return out
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_layer_norm_update_matches_oracle(gpu_available, use_expert):
+    """--actor_layer_norm: one update per stage vs the oracle, gamma / beta gradients included."""
+    B = 128
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=23, use_expert=use_expert, layer_norm=True,
+                                                normalizers="random", done_p=0.02)
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(93)
+    gen = np.random.default_rng(94)
+    eng.rng_set_state(rs.get_state())
+    R = O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=20 if use_expert else 0, gen=gen)
+    if use_expert:
+        eng.push_perms(R["perm"][None, :])
+    keep = {}
+    ref = oracle_step(st, ocfg, nrm, buf, R, expert, keep)
+    eng.step(1, eager=True)
+    eng.sync()
+    row = eng.stats(1)[0]
+    for i, k in enumerate(("q1_loss", "q2_loss", "p_loss", "alpha_loss")):
+        assert abs(row[i] - ref[k]) <= 2e-5 * abs(ref[k]) + 1e-7, (k, row[i], ref[k])
+    got = _actor_grads(eng, np.float32(1) - np.float32(0.9))
+    assert len(got) == 8
+    for gd, go in zip(got, keep["actor_grads"]):
+        assert relerr(gd, go) < 2e-4, relerr(gd, go)
+    eng.close()
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_layer_norm_trajectory_and_graph(gpu_available, use_expert):
+    """100 updates on the production schedule (the alpha rows' layer norm folded into the next
+    update's) vs the oracle, and graph replay == eager launches bit for bit."""
+    B, steps = 128, 100
+    outs = []
+    for eager in (False, True):
+        eng, ocfg, st, buf, nrm, expert = make_pair(act="tanh", B=B, seed=25, use_expert=use_expert, layer_norm=True,
+                                                    done_p=0.01, graph_steps=128)
+        N = buf["r"].shape[0]
+        rs = np.random.RandomState(95)
+        gen = np.random.default_rng(96)
+        eng.rng_set_state(rs.get_state())
+        Rs = [O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=20 if use_expert else 0, gen=gen) for _ in range(steps)]
+        if use_expert:
+            eng.push_perms(np.stack([R["perm"] for R in Rs]))
+        eng.step(steps, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(steps).copy(), eng.v["params"].cpu().numpy().copy()))
+        eng.close()
+    ref = np.array([[o["q1_loss"], o["q2_loss"], o["p_loss"]] for o in (oracle_step(st, ocfg, nrm, buf, R, expert)
+                                                                        for R in Rs)])
+    dev = outs[0][0]
+    assert np.max(np.abs(dev[:, :2] - ref[:, :2]) / np.abs(ref[:, :2])) < 1e-4
+    assert np.max(np.abs(dev[:, 2] - ref[:, 2])) / np.max(np.abs(ref[:, 2])) < 1e-4
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+def test_layer_norm_inference_paths(gpu_available):
+    """sample / evaluate / rollout through the layer-norm actor."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=27, use_expert=True, layer_norm=True,
+                                           normalizers="random")
+    s = (np.random.RandomState(2).normal(size=(50, ocfg.S)) * 1.5).astype(np.float32)
+    eng.rng_set_state(np.random.RandomState(11).get_state())
+    rs = np.random.RandomState(11)
+    pi, nlp = [t.cpu().numpy() for t in eng.evaluate(s)]
+    rpi, rnlp = O.actor_evaluate(st, ocfg, nrm, s, rs)
+    assert relerr(pi, rpi) < 2e-5 and relerr(nlp, rnlp) < 2e-5
+    got = [t.cpu().numpy() for t in eng.rollout(0, s, 3)]
+    ref = O.rollout(st, ocfg, nrm, s, 3, 0, rs)
+    for g, r, name in zip(got, ref, ("s", "a", "r", "sp", "d")):
+        if name != "d":
+            assert relerr(g, r) < 1e-4, name
+    eng.close()

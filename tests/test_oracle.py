@@ -353,3 +353,45 @@ def test_model_fit_clips_and_global_norm(nmodels, max_norm, dclip, rclip):
             np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=1e-14)
     if nmodels == 1:                            # model 1 untouched
         assert st.opt_model.t == 1
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_oracle_layer_norm_actor_matches_autograd(use_expert):
+    """--actor_layer_norm (nn_utils.py:110-119): Dense -> LayerNormalization(eps 1e-3) -> tanh
+    on the actor's layer 0; the closed-form actor gradients (incl. gamma / beta) vs autograd."""
+    cfg = O.Config(S=5, A=3, hidden=(16, 12), act="relu", B=32, model_hidden=(20, 18), layer_norm=True)
+    st0 = O.init_state(cfg, seed=7, with_models=True, bias_scale=0.1, actor_gain=0.5,
+                       model_gain=0.3).astype(np.float64)
+    _, batch, noises, nrm, ex = _make(O.Config(S=5, A=3, hidden=(16, 12), act="relu", B=32, model_hidden=(20, 18)))
+    st1 = st0.copy()
+    keep = {}
+    O.sac_update(st1, cfg, nrm, batch, *noises, expert=ex if use_expert else None, keep=keep)
+    nm = lambda x, m, dd: (x - _t(m)) / _t(dd)
+
+    def actor(P, x):
+        z = x @ P[0] + P[1]
+        mu = z.mean(-1, keepdim=True)
+        var = ((z - mu) ** 2).mean(-1, keepdim=True)
+        h = torch.tanh(P[2] * (z - mu) / torch.sqrt(var + 1e-3) + P[3])
+        return _mlp(P[4:], h, "relu")
+    PA = [_t(w).requires_grad_() for w in st0.actor]
+    LS = _t(st0.logstd).requires_grad_()
+    Q = [[_t(w) for w in net] for net in st1.q]
+    s_n = nm(_t(batch[0]), nrm.s_mean, nrm.s_den)
+    pi, nlp = _head_eval(actor(PA, s_n), LS.expand(32, 3), _t(noises[1]))
+    xq = torch.cat([s_n, nm(pi, nrm.a_mean, nrm.a_den)], 1)
+    p = torch.mean(-float(st0.alpha) * nlp[:, None] - torch.minimum(_mlp(Q[0], xq, "relu"), _mlp(Q[1], xq, "relu")))
+    if use_expert:
+        M = [[_t(w) for w in net] for net in st0.models]
+        sq = []
+        for k, (se, spe, ne) in enumerate([(ex.s1, ex.sp1, ex.noise1), (ex.s2, ex.sp2, ex.noise2)]):
+            se_n = nm(_t(se), nrm.s_mean, nrm.s_den)
+            ca = torch.tanh(actor(PA, se_n) + torch.exp(torch.clamp(LS, -5, 2)) * _t(ne))
+            om = _mlp(M[k], torch.cat([se_n, nm(ca, nrm.a_mean, nrm.a_den)], 1), cfg.model_act)
+            sq.append(((_t(spe) - (_t(se) + (om[:, :5] * _t(nrm.d_den) + _t(nrm.d_mean)))) ** 2).sum(-1))
+        p = (1 - ex.epsilon) * p + ex.epsilon * torch.mean(0.5 * (sq[0] + sq[1]))
+    g = torch.autograd.grad(p, PA + [LS])
+    assert len(keep["actor_grads"]) == 8
+    for gg, mine in zip(g[:-1], keep["actor_grads"]):
+        np.testing.assert_allclose(mine, gg.numpy(), rtol=1e-7, atol=1e-10)
+    np.testing.assert_allclose(keep["g_logstd"], g[-1].numpy(), rtol=1e-7, atol=1e-10)
