@@ -95,6 +95,11 @@ typedef struct sacx_config {
                                    of the model fit (mbrl_onpolicy_alg.py:315-317); <= 0: None */
     float delta_clip_loss;      /* --delta_clip_loss of MSEModel.get_loss in the model fit; <= 0: None */
     float reward_clip_loss;     /* --reward_clip_loss of MSEModel.get_loss in the model fit; <= 0: None */
+    int32_t act_per_layer;      /* 1: act_layers below give each hidden layer's activation; 0: `activation`
+                                   (actor, critics) and `model_activation` for every hidden layer */
+    int32_t act_layers[3][2];   /* [actor | critics | world models][hidden layer 0, 1]: a sacx_activation
+                                   value; the --actor_activations / --critic_activations / --model_activations
+                                   lists of nn_utils.py:5-22 */
 } sacx_config;
 
 typedef struct sacx_segment {

@@ -69,12 +69,23 @@ class Config:
     act_limit: float = 1.0
     per_state_std: bool = False
     layer_norm: bool = False      # --actor_layer_norm: Dense -> LayerNorm -> tanh (nn_utils.py:110-119)
+    # per-hidden-layer activations (nn_utils.py:5-22); None: `act` for every layer
+    actor_acts: Optional[Sequence[str]] = None
+    critic_acts: Optional[Sequence[str]] = None
     # SAC-EO
     epsilon: float = 1e-3         # train_parser.py:280
     model_hidden: Sequence[int] = (512, 512)
     model_act: str = "relu"
     lr_model: float = 1e-3
     reward_loss_coef: float = 1.0
+
+    @property
+    def aacts(self):
+        return tuple(self.actor_acts) if self.actor_acts else (self.act, self.act)
+
+    @property
+    def cacts(self):
+        return tuple(self.critic_acts) if self.critic_acts else (self.act, self.act)
 
     @property
     def target_entropy(self) -> float:
@@ -253,7 +264,7 @@ def mlp_forward(params, x, act):
     for l in range(nl):
         z = h @ params[2 * l] + params[2 * l + 1]
         if l < nl - 1:
-            h = act_fwd(z, act)
+            h = act_fwd(z, act[l] if isinstance(act, (list, tuple)) else act)
             hs.append(h)
         else:
             out = z
@@ -271,7 +282,7 @@ def mlp_backward(params, x, hs, dout, act, need_dx=False, need_dw=True):
             grads[2 * l] = inp.T @ d
             grads[2 * l + 1] = d.sum(axis=0)
         if l > 0:
-            d = (d @ params[2 * l].T) * act_grad(hs[l - 1], act)
+            d = (d @ params[2 * l].T) * act_grad(hs[l - 1], act[l - 1] if isinstance(act, (list, tuple)) else act)
         elif need_dx:
             dx = d @ params[0].T
     return grads, dx
@@ -287,7 +298,7 @@ LN_EPS = 1e-3
 
 def actor_forward(params, x, cfg):
     if not cfg.layer_norm:
-        return mlp_forward(params, x, cfg.act)
+        return mlp_forward(params, x, cfg.aacts)
     dt = x.dtype.type
     z = x @ params[0] + params[1]
     mu = z.mean(-1, keepdims=True)
@@ -295,16 +306,16 @@ def actor_forward(params, x, cfg):
     rstd = _F(dt, 1) / np.sqrt((d * d).mean(-1, keepdims=True) + _F(dt, LN_EPS))
     xh = d * rstd
     h1 = np.tanh(params[2] * xh + params[3])
-    out, hs = mlp_forward(params[4:], h1, cfg.act)
+    out, hs = mlp_forward(params[4:], h1, cfg.aacts[1:])
     return out, [h1] + hs + [xh, rstd]
 
 
 def actor_backward(params, x, hs, dout, cfg):
     """Gradients of the actor weight list (same order as params)."""
     if not cfg.layer_norm:
-        return mlp_backward(params, x, hs, dout, cfg.act)[0]
+        return mlp_backward(params, x, hs, dout, cfg.aacts)[0]
     h1, h2, xh, rstd = hs
-    g_rest, dh1 = mlp_backward(params[4:], h1, [h2], dout, cfg.act, need_dx=True)
+    g_rest, dh1 = mlp_backward(params[4:], h1, [h2], dout, cfg.aacts[1:], need_dx=True)
     one = np.ones((), h1.dtype)
     dy = dh1 * (one - h1 * h1)
     gg = dy * params[2]
@@ -442,7 +453,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     mu_t, ls_t = split_head(out_t, st.logstd, cfg)
     a_t, nlp_t, _ = head_evaluate(mu_t, ls_t, n1, lim, dt)
     xq_t = np.concatenate([sp_n, _norm(a_t, nrm.a_mean, nrm.a_den)], axis=1)
-    qt = [mlp_forward(net, xq_t, cfg.act)[0][:, 0] * nrm.ret_den for net in st.q_targ]
+    qt = [mlp_forward(net, xq_t, cfg.cacts)[0][:, 0] * nrm.ret_den for net in st.q_targ]
     next_value = np.minimum(qt[0], qt[1]) + alpha * nlp_t
     y = r + F(cfg.gamma) * ((F(1) - d) * next_value)
     if keep is not None:
@@ -452,11 +463,11 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     s_n = _norm(s, nrm.s_mean, nrm.s_den)
     xq = np.concatenate([s_n, _norm(a, nrm.a_mean, nrm.a_den)], axis=1)
     for k in range(2):
-        q, hs = mlp_forward(st.q[k], xq, cfg.act)
+        q, hs = mlp_forward(st.q[k], xq, cfg.cacts)
         e = q[:, 0] - y
         stats["q%d_loss" % (k + 1)] = float(np.mean(F(0.5) * e * e))
         dq = (e * F(1.0 / B))[:, None]
-        grads, _ = mlp_backward(st.q[k], xq, hs, dq, cfg.act)
+        grads, _ = mlp_backward(st.q[k], xq, hs, dq, cfg.cacts)
         if keep is not None:
             keep["q%d_h" % k] = hs
             keep["q%d_out" % k] = q[:, 0]
@@ -468,7 +479,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     mu_p, ls_p = split_head(out_p, st.logstd, cfg)
     a_p, nlp_p, cache_p = head_evaluate(mu_p, ls_p, n2, lim, dt)
     xq_p = np.concatenate([s_n, _norm(a_p, nrm.a_mean, nrm.a_den)], axis=1)
-    fq = [mlp_forward(net, xq_p, cfg.act) for net in st.q]
+    fq = [mlp_forward(net, xq_p, cfg.cacts) for net in st.q]
     q1p, q2p = fq[0][0][:, 0], fq[1][0][:, 0]
     minq = np.minimum(q1p, q2p)
     p_loss = np.mean(-alpha * nlp_p - minq)
@@ -479,7 +490,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     sel2 = np.where(q2p < q1p, F(1), np.where(q1p == q2p, F(0.5), F(0)))
     dxa = None
     for k, sel in enumerate((sel1, sel2)):
-        _, dx = mlp_backward(st.q[k], xq_p, fq[k][1], (gmin * sel)[:, None], cfg.act,
+        _, dx = mlp_backward(st.q[k], xq_p, fq[k][1], (gmin * sel)[:, None], cfg.cacts,
                              need_dx=True, need_dw=False)
         part = dx[:, S:] / nrm.a_den
         dxa = part if dxa is None else dxa + part
@@ -739,7 +750,7 @@ def gaussian_actor_sample(params, logstd_var, cfg, nrm, s, u, std_mult=1.0, outp
     log(1e-3); a = mean + exp(logstd) * u (u = 0: deterministic).  No squash."""
     dt = params[0].dtype.type
     nrm = nrm.cast(dt)
-    out, _ = mlp_forward(params, _norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den), cfg.act)
+    out, _ = mlp_forward(params, _norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den), cfg.aacts)
     A = cfg.A
     if cfg.per_state_std:
         mean, l = out[:, :A], np.log(softplus(out[:, A:]))
@@ -759,7 +770,7 @@ def critic_forward(params, cfg, nrm, s, a, value=False):
     nrm = nrm.cast(dt)
     x = np.concatenate([_norm(np.asarray(s, dt), nrm.s_mean, nrm.s_den),
                         _norm(np.asarray(a, dt), nrm.a_mean, nrm.a_den)], 1)
-    out, _ = mlp_forward(params, x, cfg.act)
+    out, _ = mlp_forward(params, x, cfg.cacts)
     return out[:, 0] * _F(dt, nrm.ret_den) if value else out
 
 

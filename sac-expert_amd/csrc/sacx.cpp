@@ -118,7 +118,10 @@ struct sacx_handle {
     std::string err;
     // dims
     int S = 0, A = 0, H0 = 0, H1 = 0, B = 0, Aout = 0, ne = 0, Hm0 = 0, Hm1 = 0, ecap = 0;
-    int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0, act = 0, mact = 0;
+    int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0;
+    // hidden-layer activations per net and layer (nn_utils.py:5-22 create_activations): actor,
+    // critics, world models
+    int aact[2] = {0, 0}, cact[2] = {0, 0}, macts[2] = {0, 0};
     int64_t cap = 0;
     int graph_steps = 128, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
     int nm = 0;               // SAC-EO world models (--num_models: 1 or 2)
@@ -556,7 +559,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
     // expert rows of world model k: [k * half, (k + 1) * half) with 2 models, all with one
     const int nm = h->nm, mrows = nm == 1 ? ne : half;
-    const int ldS = h->ldS, ldQ = h->ldQ, act = h->act, mact = h->mact;
+    const int ldS = h->ldS, ldQ = h->ldQ;
+    const int a0 = h->aact[0], a1 = h->aact[1], c0 = h->cact[0], c1 = h->cact[1], m0 = h->macts[0], m1 = h->macts[1];
     const bool eo = h->cfg.use_expert != 0;
     const std::string sl = "slot" + std::to_string(slot);
     int32_t* idx = h->ptr<int32_t>(sl + ".idx");
@@ -621,7 +625,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // share launches (12.0k vs 11.9k updates/s), so it is off unless SACX_FUSE=1.
     const char* fenv = std::getenv("SACX_FUSE");
     const int fuse_mode = fenv ? (std::atoi(fenv) ? -1 : 0) : 0;
-    const bool fuse_a = S <= FWD2_MAX_K0, fuse_q = S + A <= FWD2_MAX_K0;
+    // the fused two-layer forward applies one activation to both layers
+    const bool fuse_a = S <= FWD2_MAX_K0 && a0 == a1 && !h->ln, fuse_q = S + A <= FWD2_MAX_K0 && c0 == c1;
     auto fwd_pair = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1,
                         bool fuse, int forced = -1, int extra_tiles = 0) -> bool {
         int tiles = extra_tiles;      // tiles of problems folded into the same launch later
@@ -660,10 +665,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     if (h->ln) {
         add_gemm(h, plan, "actor.fwd0", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, ACT_NONE)}, record_probs);
         ln_fwd("actor.ln", 0, h->Ra);
-        add_gemm(h, plan, "actor.fwd1", {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, record_probs);
+        add_gemm(h, plan, "actor.fwd1", {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, a1)}, record_probs);
     } else {
-        actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, act)},
-                               {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, act)}, fuse_a, -1, alpha_tiles);
+        actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, a0)},
+                               {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, a1)}, fuse_a, -1, alpha_tiles);
     }
     // actor.head folded into q.fwd0 (plain SAC): the target tiles compute their rows' actions
     // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
@@ -725,9 +730,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> p0, p1, s0, s1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
-            GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, act);
+            GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, c0);
             q0.headp = k < 2;
-            GemmProb q1 = prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act);
+            GemmProb q1 = prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, c1);
             (side_q && k >= 2 ? s0 : p0).push_back(q0);
             (side_q && k >= 2 ? s1 : p1).push_back(q1);
         }
@@ -751,16 +756,16 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
-            p0.push_back(prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, act));
-            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, act));
+            p0.push_back(prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, c0));
+            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, c1));
         }
         if (eo) {
             for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
                 p0.push_back(prob_fwd(Xm + (size_t)k * half * ldQ, ldQ, mrows, S + A, W(n + ".l0"), Hm0,
-                                      Hm1b + (size_t)k * half * Hm0, mact));
+                                      Hm1b + (size_t)k * half * Hm0, m0));
                 p1.push_back(prob_fwd(Hm1b + (size_t)k * half * Hm0, Hm0, mrows, Hm0, W(n + ".l1"), Hm1,
-                                      Hm2b + (size_t)k * half * Hm1, mact));
+                                      Hm2b + (size_t)k * half * Hm1, m1));
             }
         }
         fwd_pair("q.fwd", p0, p1, fuse_q);
@@ -773,7 +778,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         QHeadArgs q{};
         q.mode = 0; q.B = B; q.H1 = H1; q.H2 = Hq2;
         for (int k = 0; k < 4; ++k) q.W3[k] = W(std::string(qn[k]) + ".l2");
-        q.act = act; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
+        q.act = c1; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
         q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = r_in; q.d = d_in;
         q.gamma = h->cfg.gamma; q.ret_den = W("norm.ret_den"); q.w_sac = 1.f;
         // the SAC-EO world-model head on the expert rows runs as GEMM problems (mse epilogue)
@@ -783,7 +788,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
             GemmProb p = prob_dx(Hq2 + (size_t)(2 + k) * B * H1, B, H1, W(n + ".l1"), H0,
-                                 Hq1 + (size_t)(2 + k) * B * H0, Dq1 + (size_t)k * B * H0, act);
+                                 Hq1 + (size_t)(2 + k) * B * H0, Dq1 + (size_t)k * B * H0, c0);
             p.wgen = W(n + ".l2");             // w3 column of W3_ext
             pb.push_back(p);
         }
@@ -835,8 +840,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
-            p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), H0, Hp1 + (size_t)k * B * H0, act));
-            p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, act));
+            p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), H0, Hp1 + (size_t)k * B * H0, c0));
+            p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, c1));
         }
         // SAC-EO: world-model layer 2 on the expert rows + MSE epilogue (needs Hm2 from q.fwd1),
         // riding in the pi.q.fwd0 launch (a launch of its own when that one is fused)
@@ -878,7 +883,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         QHeadArgs q{};
         q.mode = 1; q.B = B; q.H1 = H1; q.H2 = Hp2;
         q.W3[0] = W("q0.l2"); q.W3[1] = W("q1.l2"); q.W3[2] = nullptr; q.W3[3] = nullptr;
-        q.act = act; q.D2 = nullptr; q.g = W("ws.gp"); q.loss_rows = W("ws.lp");
+        q.act = c1; q.D2 = nullptr; q.g = W("ws.gp"); q.loss_rows = W("ws.lp");
         q.alpha = W("alpha"); q.nlp = W("ws.nlp_p");
         q.w_sac = eo ? (float)(1.0 - (double)h->cfg.epsilon) : 1.f;
         q.ret_den = W("norm.ret_den");
@@ -887,7 +892,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
             GemmProb p = prob_dx(Hp2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hp1 + (size_t)k * B * H0,
-                                 Dp1 + (size_t)k * B * H0, act);
+                                 Dp1 + (size_t)k * B * H0, c0);
             p.wgen = W(n + ".l2");
             pb.push_back(p);
         }
@@ -895,7 +900,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
                 GemmProb p = prob_dx(W("ws.dout") + (size_t)k * half * S, mrows, S, W(n + ".l2"), Hm1,
-                                     Hm2b + (size_t)k * half * Hm1, Dm2 + (size_t)k * half * Hm1, mact);
+                                     Hm2b + (size_t)k * half * Hm1, Dm2 + (size_t)k * half * Hm1, m1);
                 p.ldb = O;                           // B[n][k] = W_ext[n][k], row stride S+1
                 pb.push_back(p);
             }
@@ -915,7 +920,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
                 pd.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, mrows, Hm1, W(n + ".l1"), Hm0,
-                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, mact));
+                                     Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, m0));
             }
             add_gemm(h, plan, "model.bwd1", pd, record_probs);
         }
@@ -932,7 +937,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.Dm1 = Dm1; b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W(nm > 1 ? "m1.l0" : "m0.l0") : nullptr;
         b.a_den = W("norm.a_den"); b.alpha = W("alpha"); b.ctl = h->ctl(); b.use_expert = eo;
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
-        b.W3a = W("actor.l2"); b.Ha2 = Ha2 + (size_t)B * H1; b.act = act;
+        b.W3a = W("actor.l2"); b.Ha2 = Ha2 + (size_t)B * H1; b.act = a1;
         b.Da3 = Da3; b.Da2 = Da2; b.E = E;
         b.gpol = W("ws.gp");
         L.grid = (h->Rb + 3) / 4;
@@ -941,7 +946,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         plan.push_back(L);
         const int Rb = h->Rb;
         add_gemm(h, plan, "actor.bwd1",      // layer-norm layer 0: tanh' at its output
-                 {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, h->ln ? ACT_TANH : act)},
+                 {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, h->ln ? ACT_TANH : a0)},
                  record_probs);
         if (h->ln) {                          // dY -> dZ through the norm; dY*xhat, dY for gamma / beta
             Launch N{};
@@ -983,10 +988,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, "alpha.fwd0", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, ACT_NONE)},
                  record_probs);
         ln_fwd("alpha.ln", Ra4, Ra4 + B);
-        add_gemm(h, plan, "alpha.fwd1", {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, record_probs);
+        add_gemm(h, plan, "alpha.fwd1", {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, a1)}, record_probs);
     } else {
-        fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, act)},
-                 {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, act)}, fuse_a, actor_fused ? 1 : 0);
+        fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, a0)},
+                 {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, a1)}, fuse_a, actor_fused ? 1 : 0);
     }
     {
         Launch L{};
@@ -1061,7 +1066,8 @@ void build_model_plan(sacx_handle* h) {
     std::vector<Launch>& plan = h->mplan;
     plan.clear();
     if (!h->cfg.use_expert) return;
-    const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ, mact = h->mact;
+    const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ;
+    const int m0 = h->macts[0], m1 = h->macts[1];
     const int nm = h->nm;
     auto W = [&](const std::string& n) { return h->f(n); };
     float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Hf1 = W("ws.Hf1"), *Hf2 = W("ws.Hf2"), *Of = W("ws.Of");
@@ -1085,11 +1091,11 @@ void build_model_plan(sacx_handle* h) {
     for (int k = 0; k < nm; ++k) {
         const std::string n = "m" + std::to_string(k);
         const size_t r0 = (size_t)k * mb;
-        f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, mact));
-        f1.push_back(prob_fwd(Hf1 + r0 * Hm0, Hm0, mb, Hm0, W(n + ".l1"), Hm1, Hf2 + r0 * Hm1, mact));
+        f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, m0));
+        f1.push_back(prob_fwd(Hf1 + r0 * Hm0, Hm0, mb, Hm0, W(n + ".l1"), Hm1, Hf2 + r0 * Hm1, m1));
         f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), O, Of + r0 * O, ACT_NONE));
-        b2.push_back(prob_dx(Df3 + r0 * O, mb, O, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, mact));
-        b1.push_back(prob_dx(Df2 + r0 * Hm1, mb, Hm1, W(n + ".l1"), Hm0, Hf1 + r0 * Hm0, Df1 + r0 * Hm0, mact));
+        b2.push_back(prob_dx(Df3 + r0 * O, mb, O, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, m1));
+        b1.push_back(prob_dx(Df2 + r0 * Hm1, mb, Hm1, W(n + ".l1"), Hm0, Hf1 + r0 * Hm0, Df1 + r0 * Hm0, m0));
         w.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Df1 + r0 * Hm0, Hm0, W(n + ".l0"), nullptr, GRP_MODEL));
         w.push_back(prob_dw(Hf1 + r0 * Hm0, Hm0, Hm0, mb, Df2 + r0 * Hm1, Hm1, W(n + ".l1"), nullptr, GRP_MODEL));
         w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * O, O, W(n + ".l2"), nullptr, GRP_MODEL));
@@ -1537,6 +1543,10 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
         if (cfg->s_dim + 1 > 512) return bad("s_dim > 511 unsupported by the model MSE head");
     }
     if (cfg->num_models < 0 || cfg->num_models > 2) return bad("num_models must be 1 or 2 (0 -> 2)");
+    if (cfg->act_per_layer)
+        for (int n = 0; n < 3; ++n)
+            for (int l = 0; l < 2; ++l)
+                if (cfg->act_layers[n][l] < 0 || cfg->act_layers[n][l] > 2) return bad("act_layers must be relu/tanh/elu");
     if (cfg->actor_gaussian && cfg->actor_std_mult < 0.f) return bad("actor_std_mult must be positive");
     auto* h = new sacx_handle();
     h->cfg = *cfg;
@@ -1546,13 +1556,16 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->H1 = cfg->hidden[1];
     h->B = cfg->batch;
     h->cap = cfg->buffer_capacity;
-    h->act = cfg->activation;
+    for (int l = 0; l < 2; ++l) {           // per-layer activations, or the one of each net
+        h->aact[l] = cfg->act_per_layer ? cfg->act_layers[0][l] : cfg->activation;
+        h->cact[l] = cfg->act_per_layer ? cfg->act_layers[1][l] : cfg->activation;
+        h->macts[l] = cfg->act_per_layer ? cfg->act_layers[2][l] : cfg->model_activation;
+    }
     h->Aout = cfg->per_state_std ? 2 * h->A : h->A;
     h->ne = cfg->use_expert ? cfg->expert_batch : 0;
     h->ecap = cfg->use_expert ? cfg->expert_capacity : 0;
     h->Hm0 = cfg->use_expert ? cfg->model_hidden[0] : 0;
     h->Hm1 = cfg->use_expert ? cfg->model_hidden[1] : 0;
-    h->mact = cfg->model_activation;
     h->mb = cfg->use_expert ? (cfg->model_batch > 0 ? cfg->model_batch : 200) : 0;
     h->nm = cfg->use_expert ? (cfg->num_models > 0 ? cfg->num_models : 2) : 0;
     h->ln = cfg->actor_layer_norm != 0;
@@ -1916,9 +1929,9 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
 // (nn_utils.py:110-119).  Eager launches on st (or captured by the caller).
 static void actor_hidden(sacx_handle* h, const float* X, int ldX, int m, float* H1b, float* H2b, hipStream_t st) {
     std::vector<Launch> pl;
-    add_gemm(h, pl, "a.fwd0", {prob_fwd(X, ldX, m, h->S, h->f("actor.l0"), h->H0, H1b, h->ln ? ACT_NONE : h->act)},
+    add_gemm(h, pl, "a.fwd0", {prob_fwd(X, ldX, m, h->S, h->f("actor.l0"), h->H0, H1b, h->ln ? ACT_NONE : h->aact[0])},
              false);
-    add_gemm(h, pl, "a.fwd1", {prob_fwd(H1b, h->H0, m, h->H0, h->f("actor.l1"), h->H1, H2b, h->act)}, false);
+    add_gemm(h, pl, "a.fwd1", {prob_fwd(H1b, h->H0, m, h->H0, h->f("actor.l1"), h->H1, H2b, h->aact[1])}, false);
     h->probs_cursor -= 2;          // host table bookkeeping of add_gemm (these launches are not in a plan)
     launch_gemm(pl[0].gemm, st);
     if (h->ln) {
@@ -2024,8 +2037,10 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
         g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s + done * S; g.a = a + done * A; g.X = W("act.Xq");
         launch_net_io(g, h->stream);
         std::vector<Launch> pl;
-        add_gemm(h, pl, "critic.fwd0", {prob_fwd(W("act.Xq"), ldQ, m, S + A, W(nm + ".l0"), H0, W("act.H1"), h->act)}, false);
-        add_gemm(h, pl, "critic.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W(nm + ".l1"), H1, W("act.H2"), h->act)}, false);
+        add_gemm(h, pl, "critic.fwd0", {prob_fwd(W("act.Xq"), ldQ, m, S + A, W(nm + ".l0"), H0, W("act.H1"), h->cact[0])},
+                 false);
+        add_gemm(h, pl, "critic.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W(nm + ".l1"), H1, W("act.H2"), h->cact[1])},
+                 false);
         add_gemm(h, pl, "critic.fwd2", {prob_fwd(W("act.H2"), H1, m, H1, W(nm + ".l2"), 1, W("act.Q"), ACT_NONE)}, false);
         for (auto& L : pl) launch_gemm(L.gemm, h->stream);
         h->probs_cursor -= 3;
@@ -2045,8 +2060,10 @@ static void model_net_chunk(sacx_handle* h, int32_t model, const float* s, const
     g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s; g.a = a; g.X = W("roll.Xm");
     launch_net_io(g, h->stream);
     std::vector<Launch> pl;
-    add_gemm(h, pl, "model.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->mact)}, false);
-    add_gemm(h, pl, "model.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->mact)}, false);
+    add_gemm(h, pl, "model.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->macts[0])},
+             false);
+    add_gemm(h, pl, "model.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->macts[1])},
+             false);
     add_gemm(h, pl, "model.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), S + 1, W("roll.O"), ACT_NONE)}, false);
     for (auto& L : pl) launch_gemm(L.gemm, h->stream);
     h->probs_cursor -= 3;
@@ -2144,8 +2161,10 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
             a.alpha_mode = 0;
             FinalArgs f{};
             launch_actor_head(a, f, st);
-            add_gemm(h, pl, "roll.m.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->mact)}, false);
-            add_gemm(h, pl, "roll.m.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->mact)}, false);
+            add_gemm(h, pl, "roll.m.fwd0",
+                     {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->macts[0])}, false);
+            add_gemm(h, pl, "roll.m.fwd1",
+                     {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->macts[1])}, false);
             add_gemm(h, pl, "roll.m.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), O, W("roll.O"), ACT_NONE)}, false);
             for (auto& L : pl) launch_gemm(L.gemm, st);
             h->probs_cursor -= 3;      // host table bookkeeping of add_gemm (these launches are not in a plan)
@@ -2220,8 +2239,8 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
             const std::string mn = h->nm > 1 ? "m" + std::to_string(k) : std::string("m0");
             float* M1 = W("roll.M1") + (size_t)k * n * Hm0;
             float* M2 = W("roll.M2") + (size_t)k * n * Hm1;
-            p0.push_back(prob_fwd(W("roll.Xm"), ldQ, n, S + A, W(mn + ".l0"), Hm0, M1, h->mact));
-            p1.push_back(prob_fwd(M1, Hm0, n, Hm0, W(mn + ".l1"), Hm1, M2, h->mact));
+            p0.push_back(prob_fwd(W("roll.Xm"), ldQ, n, S + A, W(mn + ".l0"), Hm0, M1, h->macts[0]));
+            p1.push_back(prob_fwd(M1, Hm0, n, Hm0, W(mn + ".l1"), Hm1, M2, h->macts[1]));
             p2.push_back(prob_fwd(M2, Hm1, n, Hm1, W(mn + ".l2"), O, W("roll.O") + (size_t)k * n * O, ACT_NONE));
         }
         add_gemm(h, pl, "diag.m.fwd0", p0, false);

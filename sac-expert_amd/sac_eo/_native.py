@@ -74,6 +74,8 @@ class Config(ctypes.Structure):
         ("model_max_grad_norm", ctypes.c_float),
         ("delta_clip_loss", ctypes.c_float),
         ("reward_clip_loss", ctypes.c_float),
+        ("act_per_layer", ctypes.c_int32),
+        ("act_layers", (ctypes.c_int32 * 2) * 3),
     ]
 
 

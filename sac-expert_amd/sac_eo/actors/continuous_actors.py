@@ -34,10 +34,8 @@ class GaussianActor:
         self.s_dim = int(np.prod(env.observation_space.shape))
         self.a_dim = int(np.prod(env.action_space.shape))
         self.layers = list(layers)
-        acts = list(activations)
-        self.activation = acts[0]
-        if any(a != self.activation for a in acts):
-            raise NotImplementedError("one activation for all hidden layers")
+        self.activations = list(activations)          # one name for all layers, or one per layer
+        self.activation = self.activations[0]
         self.layer_norm = bool(layer_norm)
         if output_norm and self.squash:
             raise NotImplementedError("actor_output_norm of the squashed actor is not built (off by default)")

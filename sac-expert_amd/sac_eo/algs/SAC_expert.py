@@ -59,7 +59,7 @@ class SAC_exp(SACBase):
                                batch=1, buffer_capacity=1, per_state_std=ex.per_state_std, graph_steps=1,
                                act_limit=float(np.max(ex.act_limit)), actor_gaussian=not ex.squash,
                                actor_std_mult=float(ex.std_mult), actor_output_norm=ex.output_norm,
-                               actor_layer_norm=ex.layer_norm)
+                               actor_layer_norm=ex.layer_norm, actor_activations=ex.activations)
             self._expert_engine = Engine(cfg)
             ex._bind(self._expert_engine, "actor")
             self.expert_normalizer.push_to(self._expert_engine)

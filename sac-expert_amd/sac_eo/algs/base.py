@@ -89,8 +89,6 @@ class SACBase:
         hidden = self.actor.layers
         if len(hidden) != 2 or list(self.q_critics[0].layers) != list(hidden):
             raise NotImplementedError("the device engine runs 2 hidden layers shared by actor and critics")
-        if self.actor.activation != self.q_critics[0].activation:
-            raise NotImplementedError("actor and critic activations must match")
         cfg = EngineConfig(
             s_dim=self.s_dim, a_dim=self.a_dim, hidden=tuple(hidden), activation=self.actor.activation,
             batch=int(self.sac_batch_size), buffer_capacity=self._capacity(), per_state_std=self.actor.per_state_std,
@@ -98,6 +96,8 @@ class SACBase:
             expert_batch=int(self.expert_batch_size or self.expert_buffer_size),
             model_hidden=tuple(self.models[0].layers) if self.use_expert else (512, 512),
             model_activation=self.models[0].activation if self.use_expert else "relu",
+            actor_activations=self.actor.activations, critic_activations=self.q_critics[0].activations,
+            model_activations=self.models[0].activations if self.use_expert else None,
             model_batch=int(self.model_batch_size), target_update_int=int(self.target_update_int),
             graph_steps=1, gamma=self.gamma, tau=self.soft_tau, lr_q=self.mbpo_lr, lr_pi=self.mbpo_actor_lr,
             lr_alpha=self.mbpo_alpha_lr, lr_model=self.model_lr, init_temperature=self.init_temperature,

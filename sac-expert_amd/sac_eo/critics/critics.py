@@ -15,7 +15,8 @@ from ..nets import create_nn_weights
 class _Critic:
     def __init__(self, in_dim, out_dim, layers, activations, gain, rng=None):
         self.layers = list(layers)
-        self.activation = list(activations)[0]
+        self.activations = list(activations)
+        self.activation = self.activations[0]
         self.gain = gain
         rng = rng if rng is not None else np.random.default_rng(np.random.randint(2 ** 31))
         self._w = create_nn_weights(rng, in_dim, out_dim, self.layers, gain)

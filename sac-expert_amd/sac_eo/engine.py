@@ -65,6 +65,11 @@ class EngineConfig:
     model_max_grad_norm: float = 0.0    # <= 0: None
     delta_clip_loss: float = 0.0        # <= 0: None
     reward_clip_loss: float = 0.0       # <= 0: None
+    # per-layer activations (the reference's --actor_activations / --critic_activations /
+    # --model_activations lists); None: `activation` / `model_activation` for every layer
+    actor_activations: Optional[Sequence[str]] = None
+    critic_activations: Optional[Sequence[str]] = None
+    model_activations: Optional[Sequence[str]] = None
 
     def to_c(self) -> N.Config:
         c = N.Config()
@@ -102,6 +107,15 @@ class EngineConfig:
         c.model_max_grad_norm = float(self.model_max_grad_norm or 0.0)
         c.delta_clip_loss = float(self.delta_clip_loss or 0.0)
         c.reward_clip_loss = float(self.reward_clip_loss or 0.0)
+        lists = (self.actor_activations, self.critic_activations, self.model_activations)
+        if any(x is not None for x in lists):
+            c.act_per_layer = 1
+            for n, (lst, dflt) in enumerate(zip(lists, (self.activation, self.activation, self.model_activation))):
+                lst = list(lst) if lst is not None else [dflt]
+                lst = lst * 2 if len(lst) == 1 else lst          # nn_utils.py:7-8: one name for all layers
+                if len(lst) != 2:
+                    raise ValueError("two hidden layers: one or two activation names per net")
+                c.act_layers[n][0], c.act_layers[n][1] = N.ACT[lst[0]], N.ACT[lst[1]]
         return c
 
 

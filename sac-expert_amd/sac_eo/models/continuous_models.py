@@ -30,7 +30,8 @@ class MSEModel:
         self.delta_clip_pred = k.get("delta_clip_pred")
         self.reward_clip_pred = k.get("reward_clip_pred")
         self.layers = list(layers)
-        self.activation = list(activations)[0]
+        self.activations = list(activations)
+        self.activation = self.activations[0]
         rng = rng if rng is not None else np.random.default_rng(np.random.randint(2 ** 31))
         self._w = create_nn_weights(rng, self.s_dim + self.a_dim, self.s_dim + 1, self.layers, gain)
         self._engine = None

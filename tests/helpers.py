@@ -30,10 +30,11 @@ def nontrivial_normalizers(rs, S, A):
 
 def make_learner(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
                  use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
-                 bias_scale=0.05, actor_gain=0.5, epsilon=0.1, layer_norm=False):
+                 bias_scale=0.05, actor_gain=0.5, epsilon=0.1, layer_norm=False, actor_acts=None, critic_acts=None):
     """The seeded inputs of one learner: (oracle_cfg, oracle_state_f32, buffer, normalizers, expert)."""
     ocfg = O.Config(S=S, A=A, hidden=hidden, act=act, B=B, per_state_std=per_state_std,
-                    model_hidden=model_hidden, epsilon=epsilon, layer_norm=layer_norm)
+                    model_hidden=model_hidden, epsilon=epsilon, layer_norm=layer_norm, actor_acts=actor_acts,
+                    critic_acts=critic_acts)
     st = O.init_state(ocfg, seed=seed + 1, with_models=use_expert, bias_scale=bias_scale,
                       actor_gain=actor_gain, model_gain=0.3)
     rs = np.random.RandomState(seed + 100)
@@ -70,16 +71,17 @@ def load_learner(eng, st, buf, nrm, expert, epsilon):
 def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
               use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
               graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False, layer_norm=False,
-              **ekw):
+              actor_acts=None, critic_acts=None, **ekw):
     """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
     from sac_eo.engine import Engine, EngineConfig
     ocfg, st, buf, nrm, expert = make_learner(S, A, hidden, B, act, N, seed, per_state_std, use_expert, ne,
                                               model_hidden, normalizers, done_p, bias_scale, actor_gain, epsilon,
-                                              layer_norm)
+                                              layer_norm, actor_acts, critic_acts)
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
                         per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
                         expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon,
-                        gemm_bf16=gemm_bf16, actor_layer_norm=layer_norm, **ekw)
+                        gemm_bf16=gemm_bf16, actor_layer_norm=layer_norm, actor_activations=actor_acts,
+                        critic_activations=critic_acts, **ekw)
     eng = Engine(ecfg, dp=dp)
     load_learner(eng, st, buf, nrm, expert, epsilon)
     return eng, ocfg, st.astype(np.float64), buf, nrm, expert

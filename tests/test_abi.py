@@ -29,7 +29,8 @@ def test_struct_layouts():
     from sac_eo import _native as N
     # offsets fixed by include/sacx.h (natural alignment)
     assert N.Config.buffer_capacity.offset == 32
-    assert ctypes.sizeof(N.Config) == 176          # gcc: sizeof(sacx_config)
+    assert ctypes.sizeof(N.Config) == 200          # gcc: sizeof(sacx_config)
+    assert N.Config.act_per_layer.offset == 172 and N.Config.act_layers.offset == 176
     assert N.Config.reward_loss_coef.offset == 128
     assert N.Config.gemm_bf16.offset == 132
     assert N.Config.seeds.offset == 136
