@@ -466,7 +466,7 @@ __device__ __forceinline__ void load_a(__amdgpu_buffer_rsrc_t ra, const GemmProb
             }
             const bool gen = g.wgen != nullptr;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) a[j] = gen ? w[j] * dact_sel(a[j], g.act) : a[j];
+            for (int j = 0; j < 4; ++j) a[j] = gen ? w[j] * dact_sel(a[j], g.gen_act) : a[j];
         }
     } else {
         // A[m][k] = X[k][m]; logical row ones_row is all ones (bias-gradient row)
@@ -854,7 +854,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                      "s"(g.dmean), "s"(g.dden), "s"(g.headp), "s"(g.vec));
     } else if constexpr (MODE == GM_DX) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
-                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.H), "s"(g.ldh), "s"(g.vec));
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec));
     } else {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row));

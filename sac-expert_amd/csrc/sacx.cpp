@@ -790,6 +790,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             GemmProb p = prob_dx(Hq2 + (size_t)(2 + k) * B * H1, B, H1, W(n + ".l1"), H0,
                                  Hq1 + (size_t)(2 + k) * B * H0, Dq1 + (size_t)k * B * H0, c0);
             p.wgen = W(n + ".l2");             // w3 column of W3_ext
+            p.gen_act = c1;                    // act'(Hq2); the epilogue takes act'(Hq1)
             pb.push_back(p);
         }
         add_gemm(h, plan, "q.head+critic.bwd1", pb, record_probs);
@@ -894,6 +895,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             GemmProb p = prob_dx(Hp2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hp1 + (size_t)k * B * H0,
                                  Dp1 + (size_t)k * B * H0, c0);
             p.wgen = W(n + ".l2");
+            p.gen_act = c1;
             pb.push_back(p);
         }
         if (eo) {                            // Dm2 = dout . Wm2[:, :S]^T (.) act'(Hm2)

@@ -82,6 +82,7 @@ struct GemmProb {
     // layer-2 output of a scalar-output net for a unit output gradient (the per-row gradient
     // is applied downstream: the result is linear in it)
     const float* wgen;
+    int32_t gen_act;       // the activation whose derivative the generated A takes (layer 2's)
     // GM_DW: B[k][n] is scaled by bscale[k] on load (per-row output gradient; a ones vector
     // when unscaled, so every problem takes the same path)
     const float* bscale;
