@@ -469,34 +469,44 @@ class Engine:
         """Full-state snapshot (the reference keeps only final weights and logs,
         base_onpolicy_alg.py:351-374): weights, targets, alpha, Adam moments, normalisers,
         counters, the device RNG stream, replay ring, expert rows, permutation and stats
-        rings -- every non-workspace segment, byte for byte.  Resuming continues the run
+        rings -- every non-workspace segment, byte for byte, of every seed of the handle
+        (packed seeds: one ``seed<k>`` directory each).  Resuming continues the run
         bit-identically (tests/test_gpu_engine.py)."""
         import json
         os.makedirs(path, exist_ok=True)
         self.sync()
         ranges = self._state_ranges()
-        for a, b in ranges:
-            np.save(os.path.join(path, f"range_{a}.npy"), self.arena[a:b].cpu().numpy())
+        for k in range(self.seeds):
+            d = path if self.seeds == 1 else os.path.join(path, f"seed{k}")
+            os.makedirs(d, exist_ok=True)
+            for a, b in ranges:
+                np.save(os.path.join(d, f"range_{a}.npy"), self._arenas[k][a:b].cpu().numpy())
         with open(os.path.join(path, "meta.json"), "w") as fh:
             json.dump({"arena_bytes": self.nbytes, "ranges": ranges, "layout": self._layout_sig(),
-                       "format": "sacx-state-1"}, fh)
+                       "seeds": self.seeds, "format": "sacx-state-1"}, fh)
 
     def load_state(self, path: str):
-        """Restores a save_state snapshot into this engine (same configuration)."""
+        """Restores a save_state snapshot into this engine (same configuration, same seeds)."""
         import json
         with open(os.path.join(path, "meta.json")) as fh:
             meta = json.load(fh)
         if meta.get("format") != "sacx-state-1" or meta["arena_bytes"] != self.nbytes or \
-                meta["layout"] != self._layout_sig():
+                meta["layout"] != self._layout_sig() or int(meta.get("seeds", 1)) != self.seeds:
             raise ValueError("snapshot layout does not match this engine's configuration")
         self.sync()
-        for a, b in meta["ranges"]:
-            src = np.load(os.path.join(path, f"range_{a}.npy"))
-            if src.shape != (b - a,):
-                raise ValueError("snapshot range size mismatch")
-            self.arena[a:b].copy_(torch.from_numpy(src).to(self.device))
+        for k in range(self.seeds):
+            d = path if self.seeds == 1 else os.path.join(path, f"seed{k}")
+            for a, b in meta["ranges"]:
+                src = np.load(os.path.join(d, f"range_{a}.npy"))
+                if src.shape != (b - a,):
+                    raise ValueError("snapshot range size mismatch")
+                self._arenas[k][a:b].copy_(torch.from_numpy(src).to(self.device))
         self.sync()
-        N.check(self.lib.sacx_resync(self.h), self.h, "resync")
+        sel = self.seed_index
+        for k in range(self.seeds):            # host mirrors of the counters (every seed steps together)
+            self.select_seed(k)
+            N.check(self.lib.sacx_resync(self.h), self.h, "resync")
+        self.select_seed(sel)
 
     # ------------------------------------------------------------------ hot path
     def step(self, n: int = 1, num_timesteps: int = 0, ts_increment: int = 1, external: bool = False,
