@@ -25,6 +25,15 @@ def family(name):
     return "k_gemm" if m.group(1).startswith("k_gemm") else m.group(1)
 
 
+def subfamily(name):
+    """k_gemm launches split by operand mode (template argument 0): fwd / dx / dw (+ Adam) / fwd2."""
+    m = re.search(r"sacx::k_gemm(_head)?<(\d+)", name)
+    if not m:
+        return None
+    return "k_gemm." + {"0": "fwd", "1": "dx", "2": "dw_adam", "3": "fwd2"}.get(m.group(2), m.group(2)) + \
+        (".head" if m.group(1) else "")
+
+
 def main():
     d, config = sys.argv[1], sys.argv[2]
     tag = sys.argv[3] if len(sys.argv) > 3 else os.path.basename(os.path.normpath(d))
@@ -35,6 +44,9 @@ def main():
             if fam is None or fam == "k_append":
                 continue
             vals[fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            sub = subfamily(r["Kernel_Name"])
+            if sub is not None:
+                vals[sub][r["Counter_Name"]].append(float(r["Counter_Value"]))
     out = {"config": config, "source": tag, "kernels": {}}
     for fam, cs in sorted(vals.items()):
         k = {c: sum(v) / len(v) for c, v in cs.items()}
