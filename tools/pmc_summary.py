@@ -27,11 +27,12 @@ def family(name):
 
 def subfamily(name):
     """k_gemm launches split by operand mode (template argument 0): fwd / dx / dw (+ Adam) / fwd2."""
-    m = re.search(r"sacx::k_gemm(_head)?<(\d+)", name)
+    if "k_gemm_head" in name:              # the forward launch with the actor-head prologue
+        return "k_gemm.fwd_head"
+    m = re.search(r"sacx::k_gemm<(\d+)", name)
     if not m:
         return None
-    return "k_gemm." + {"0": "fwd", "1": "dx", "2": "dw_adam", "3": "fwd2"}.get(m.group(2), m.group(2)) + \
-        (".head" if m.group(1) else "")
+    return "k_gemm." + {"0": "fwd", "1": "dx", "2": "dw_adam", "3": "fwd2"}.get(m.group(1), m.group(1))
 
 
 def main():
