@@ -24,6 +24,7 @@ rank 0 at N=1, bounded sample).
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import sys
@@ -121,6 +122,15 @@ def pmc_traffic(kernel, config):
         return None, None
 
 
+def pmc_counter(kernel, config, counter):
+    """Mean per-dispatch value of a PMC counter of `kernel` from profiles/pmc_<config>.json."""
+    try:
+        with open(os.path.join(ROOT, "profiles", f"pmc_{config}.json")) as fh:
+            return float(json.load(fh)["kernels"][kernel][counter])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def roofline(eng, config, n_prof=20, n_replays=20):
     """Roofline of the dominant kernel family (by eager device time).
 
@@ -152,13 +162,20 @@ def roofline(eng, config, n_prof=20, n_replays=20):
     flops_per_launch = f["flops"] / launches     # the plan's family FLOPs per update, folded launches included
     achieved = flops_per_launch / (avg_us * 1e-6) / 1e12
     traffic, src = pmc_traffic(dom, config)
+    mfma = pmc_counter(dom, config, "SQ_VALU_MFMA_BUSY_CYCLES")
     t_full = eng.time_graph(n_replays)
     t_wo = eng.time_graph(n_replays, dom)
     out = {
         "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
         "unit": "TFLOP/s", "frac": round(achieved / peak, 5),
         "traffic": traffic, "traffic_source": src,
+        # matrix-pipe busy cycles per launch (PMC, summed over the 1,024 SIMDs) over the launch's
+        # SIMD-cycles at 2.4 GHz: the counter-side view of `frac`
+        "mfma_busy_frac": round(mfma / (avg_us * 1e-6 * 2.4e9 * 1024), 5) if mfma else None,
         "avg_launch_us": round(avg_us, 3), "launches_per_update": round(launches, 3),
+        # per-kernel HBM GB/s and MFMA busy for every kernel (k_gather, k_rng, DW+Adam ...)
+        "kernel_table": next((os.path.relpath(p, ROOT) for p in sorted(
+            glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_kernel_table_*.md")))[-1:]), None),
         "flops_per_launch": flops_per_launch,
         "algorithmic_bytes_per_launch": f["bytes"] / launches,
         "timing": "per-workgroup device timestamps in a replay of the update graph (sacx_time_kernels)",

@@ -39,9 +39,14 @@ def make_rng():
     np.savez_compressed(os.path.join(HERE, "rng_golden.npz"), **out)
 
 
-def make_sac():
+SAC_RNG_SEED = 11     # global MT19937 stream of the trajectory
+SAC_STEPS = 10
+
+
+def sac_inputs():
+    """The golden trajectory's inputs: (cfg, fp32 initial state, buffer, normalisers)."""
     cfg = O.Config(S=5, A=2, hidden=(16, 16), act="tanh", B=16)
-    st = O.init_state(cfg, seed=1, bias_scale=0.05).astype(np.float64)
+    st = O.init_state(cfg, seed=1, bias_scale=0.05)
     rs = np.random.RandomState(0)
     N = 64
     buf = dict(s=rs.normal(size=(N, 5)).astype(np.float32),
@@ -49,10 +54,16 @@ def make_sac():
                sp=rs.normal(size=(N, 5)).astype(np.float32),
                r=rs.normal(size=N).astype(np.float32),
                d=(rs.uniform(size=N) < 0.1).astype(np.float64))
-    nrm = O.Normalizers.identity(5, 2)
-    g = np.random.RandomState(11)
+    return cfg, st, buf, O.Normalizers.identity(5, 2)
+
+
+def make_sac():
+    cfg, st, buf, nrm = sac_inputs()
+    st = st.astype(np.float64)
+    N = buf["r"].shape[0]
+    g = np.random.RandomState(SAC_RNG_SEED)
     losses = []
-    for _ in range(10):
+    for _ in range(SAC_STEPS):
         R = O.draw_step_randoms(g, N, cfg.B, cfg.A)
         n = [O.f32_noise(R[k]) for k in ("noise_t", "noise_pi", "noise_alpha")]
         stt = O.sac_update(st, cfg, nrm, O.gather(buf, R["idx"]), *n)
