@@ -200,6 +200,12 @@ __device__ __forceinline__ void reloc(GemmProb& g, int64_t so) {
     g.P = sr(g.P, so); g.T = sr(g.T, so); g.W0 = sr(g.W0, so); g.C0 = sr(g.C0, so); g.wgen = sr(g.wgen, so);
     g.bscale = sr(g.bscale, so); g.se_raw = sr(g.se_raw, so); g.spe_raw = sr(g.spe_raw, so);
     g.dmean = sr(g.dmean, so); g.dden = sr(g.dden, so); g.part = sr(g.part, so);
+    g.pw = sr(g.pw, so); g.ppart = sr(g.ppart, so);
+}
+__device__ __forceinline__ void reloc(HeadBwdArgs& b, int64_t so) {
+    b.part = sr(b.part, so); b.gpol = sr(b.gpol, so); b.a_den = sr(b.a_den, so); b.alpha = sr(b.alpha, so);
+    b.c_t = sr(b.c_t, so); b.c_std = sr(b.c_std, so); b.c_u = sr(b.c_u, so); b.c_mask = sr(b.c_mask, so);
+    b.Da3 = sr(b.Da3, so); b.E = sr(b.E, so); b.Da2 = sr(b.Da2, so);
 }
 __device__ __forceinline__ void reloc(FinalArgs& f, int64_t so) {
     f.alpha = sr(f.alpha, so); f.alpha_m = sr(f.alpha_m, so); f.alpha_v = sr(f.alpha_v, so); f.ctl = sr(f.ctl, so);
@@ -555,39 +561,55 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
     const float ad = bload(rs(sr(hd.a_den, so)), boff(jok, col));
     const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(sr(hd.W3, so), 0x7fffffffu);
     const float bias = bload(rw3, boff(col < Aout, H1 * Aout + col));
-    const __amdgpu_buffer_rsrc_t rh = make_rsrc(sr(hd.H2, so), 0x7fffffffu);
-    const int nIt = H1 >> 4, per = (nIt + 3) >> 2, i0 = wave * per, i1 = min(nIt, i0 + per);
-    const bool hm = m0 + r < g.M, wn = r < Aout;
-    floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
-    for (int it = i0; it < i1; it += 4) {
-        float a[4][4], b[4][4];
+    float mu;
+    if (hd.part != nullptr) {
+        // Ha2 . W3 from actor.fwd1's per-column-tile partials: 4 float4 per (row, output)
+        const __amdgpu_buffer_rsrc_t rp = rs(sr(hd.part, so));
+        const bool pok = rok && col < Aout;
+        float4 pv[4];
 #pragma unroll
-        for (int u4 = 0; u4 < 4; ++u4) {
-            const bool ok = it + u4 < i1;
-            const int k0 = (it + u4) * 16 + grp * 4;
-            const float4 v = bload4(rh, boff(ok && hm, (m0 + r) * hd.ldh + k0));
-            a[u4][0] = v.x; a[u4][1] = v.y; a[u4][2] = v.z; a[u4][3] = v.w;
+        for (int i = 0; i < 4; ++i) pv[i] = bload4(rp, boff(pok && 4 * i < hd.tq, ((m0 + row) * Aout + col) * hd.tq + 4 * i));
+        float v = 0.f;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) b[u4][j] = bload(rw3, boff(ok && wn, (k0 + j) * Aout + r));
+        for (int i = 0; i < 4; ++i) {
+            v = v + pv[i].x; v = v + pv[i].y; v = v + pv[i].z; v = v + pv[i].w;
         }
-        __builtin_amdgcn_sched_barrier(0);
+        mu = v + bias;
+    } else {
+        const __amdgpu_buffer_rsrc_t rh = make_rsrc(sr(hd.H2, so), 0x7fffffffu);
+        const int nIt = H1 >> 4, per = (nIt + 3) >> 2, i0 = wave * per, i1 = min(nIt, i0 + per);
+        const bool hm = m0 + r < g.M, wn = r < Aout;
+        floatx4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+        for (int it = i0; it < i1; it += 4) {
+            float a[4][4], b[4][4];
 #pragma unroll
-        for (int u4 = 0; u4 < 4; ++u4) {
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][0], b[u4][0], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][1], b[u4][1], c1, 0, 0, 0);
-            c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][2], b[u4][2], c0, 0, 0, 0);
-            c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][3], b[u4][3], c1, 0, 0, 0);
+            for (int u4 = 0; u4 < 4; ++u4) {
+                const bool ok = it + u4 < i1;
+                const int k0 = (it + u4) * 16 + grp * 4;
+                const float4 v = bload4(rh, boff(ok && hm, (m0 + r) * hd.ldh + k0));
+                a[u4][0] = v.x; a[u4][1] = v.y; a[u4][2] = v.z; a[u4][3] = v.w;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) b[u4][j] = bload(rw3, boff(ok && wn, (k0 + j) * Aout + r));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u4 = 0; u4 < 4; ++u4) {
+                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][0], b[u4][0], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][1], b[u4][1], c1, 0, 0, 0);
+                c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][2], b[u4][2], c0, 0, 0, 0);
+                c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u4][3], b[u4][3], c1, 0, 0, 0);
+            }
         }
+        const floatx4 acc = c0 + c1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[wave][q][lane] = acc[q];
+        __syncthreads();
+        const int L = ((row >> 2) << 4) | col, R = row & 3;
+        float v = red[0][R][L] + red[1][R][L];
+        v = v + red[2][R][L];
+        v = v + red[3][R][L];
+        mu = v + bias;
     }
-    const floatx4 acc = c0 + c1;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) red[wave][q][lane] = acc[q];
-    __syncthreads();
-    const int L = ((row >> 2) << 4) | col, R = row & 3;
-    float v = red[0][R][L] + red[1][R][L];
-    v = v + red[2][R][L];
-    v = v + red[3][R][L];
-    const float mu = v + bias;
     // per_state_std: logstd_raw of action j sits in column A + j of the same row (same 16 lanes)
     const float lv = __shfl(mu, (lane & ~15) | min(col + A, 15), 64);
     const float lraw = hd.per_state_std ? lv : ls;
@@ -616,6 +638,64 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
     for (int q = 0; q < 4; ++q)
         if (col + 16 * q < S) As[row][col + 16 * q] = xs[q];
     if (jok) As[row][S + col] = pin;
+    __syncthreads();
+}
+
+// actor.head.bwd folded into actor.bwd1 (rowk 4): the policy-row work of k_actor_bwd for the
+// tile's 16 rows (SAC_expert.py:262-296 through continuous_actors.py:327-379).
+// Thread (row, col) owns action col of row m0 + row: the action gradient is the sum of the
+// critics' partial dots (written by the pi.q.bwd1 tiles) scaled by the rows' output gradients,
+// then the tanh-Gaussian backward; d3s[row][o] receives Da3 (o < Aout, zeros past it) for the
+// A-operand generation, and column tile 0 stores Da3 / E for actor.adam.
+__device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn, float (&d3s)[16][17], int64_t so) {
+    reloc(hb, so);
+    const int t = threadIdx.x, lane = t & 63, row = t >> 4, col = t & 15;
+    const int B = hb.B, A = hb.A, tq = hb.tq;
+    const int m = m0 + row;
+    const bool rok = m < B, jok = col < A, ok = rok && jok;
+    const int ci = m * A + col;
+    const float ct = bload(rs(hb.c_t), boff(ok, ci));
+    const float sd = bload(rs(hb.c_std), boff(ok, ci));
+    const float u = bload(rs(hb.c_u), boff(ok, ci));
+    const float mk = bload(rs(hb.c_mask), boff(ok, ci));
+    const float ad = bload(rs(hb.a_den), boff(jok, col));
+    const __amdgpu_buffer_rsrc_t rg = rs(hb.gpol);
+    const float g0 = bload(rg, boff(rok, m));
+    const float g1 = bload(rg, boff(rok, B + m));
+    const float alpha = bload(rs(hb.alpha), 0u);
+    // partials [critic][row][action][tq] (host: tq <= 16, tq % 4 == 0): 4 float4 per critic
+    const __amdgpu_buffer_rsrc_t rp = rs(hb.part);
+    float4 v0[4], v1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const bool iok = ok && 4 * i < tq;
+        v0[i] = bload4(rp, boff(iok, (m * A + col) * tq + 4 * i));
+        v1[i] = bload4(rp, boff(iok, ((B + m) * A + col) * tq + 4 * i));
+    }
+    float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        p0 = p0 + v0[i].x; p0 = p0 + v0[i].y; p0 = p0 + v0[i].z; p0 = p0 + v0[i].w;
+        p1 = p1 + v1[i].x; p1 = p1 + v1[i].y; p1 = p1 + v1[i].z; p1 = p1 + v1[i].w;
+    }
+    const float c = -alpha * (1.f / (float)B);
+    float gx = 0.f, dl = 0.f;
+    if (jok) {
+        const float ga = (g0 * p0 + g1 * p1) / ad;
+        gx = ga * hb.lim * (1.f - ct * ct);
+        gx = gx - (2.f * c) * ct;
+        dl = (gx * sd) * u;
+        dl = dl + c;
+        dl = dl * mk;
+    }
+    // per_state_std: the logstd rows' gradients follow the mean rows (column A + j <- lane j)
+    const float dlv = __shfl(dl, (lane & ~15) | max(col - A, 0), 64);
+    d3s[row][col] = col < A ? gx : ((hb.per_state_std && col < hb.Aout) ? dlv : 0.f);
+    if (tn == 0 && ok) {
+        hb.Da3[(size_t)m * hb.Aout + col] = gx;
+        if (hb.per_state_std) hb.Da3[(size_t)m * hb.Aout + A + col] = dl;
+        else hb.E[ci] = dl;
+    }
     __syncthreads();
 }
 
@@ -847,11 +927,20 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.headp), "s"(hd.H2), "s"(hd.W3), "s"(hd.logstd),
                      "s"(hd.a_mean), "s"(hd.a_den), "s"(hd.ldh), "s"(hd.H1), "s"(hd.A), "s"(hd.Aout),
-                     "s"(hd.per_state_std), "s"(hd.lim), "s"(s0.r0), "s"(s0.noise), "s"(s0.nlp_out), "s"(g.vec));
+                     "s"(hd.per_state_std), "s"(hd.lim), "s"(s0.r0), "s"(s0.noise), "s"(s0.nlp_out), "s"(g.vec),
+                     "s"(hd.part), "s"(hd.tq));
+    } else if constexpr (MODE == GM_FWD && ROWK == 5) {
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.vec), "s"(g.C), "s"(g.ldc),
+                     "s"(g.pw), "s"(g.ppart), "s"(g.pw_ld), "s"(g.pw_cs), "s"(g.pw_n));
     } else if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
                      "s"(g.dmean), "s"(g.dden), "s"(g.headp), "s"(g.vec));
+    } else if constexpr (MODE == GM_DX && ROWK == 2) {
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec),
+                     "s"(g.pw), "s"(g.ppart), "s"(g.pw_ld), "s"(g.pw_cs), "s"(g.pw_n), "s"(g.C));
     } else if constexpr (MODE == GM_DX) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec));
@@ -884,7 +973,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float e4 = 0.f;
     if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
         e0 = g.bias[nnc];
-        if constexpr (ROWK != 3) {   // the head-fused launch (plain SAC) has no mse problems
+        if constexpr (ROWK != 3 && ROWK != 5) {   // head-fused / actor launches: no mse problems
             // world-model head rows (mse): zero-sized resources when not an mse problem
             e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
             e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
@@ -899,6 +988,14 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         e2 = g.P[pidx + 2 * ga.p_stride];
         // no target: a zero-sized resource reads 0 without a branch
         e3 = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
+    }
+    // partial-dot weights of this thread's output column (zero-sized resource: no partials)
+    constexpr bool PART = (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5);
+    float pwv[8];
+    if constexpr (PART) {
+        const __amdgpu_buffer_rsrc_t rpw = rs(g.pw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pwv[j] = bload(rpw, boff(j < g.pw_n && nn < g.N, j * g.pw_ld + nnc * g.pw_cs));
     }
 
     const int nIt = (g.K + 15) >> 4;
@@ -941,6 +1038,72 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             }
             a_lds = true;
         }
+    }
+    __shared__ float d3s[ROWK == 4 ? 16 : 1][17];
+    if constexpr (MODE == GM_DX && ROWK == 4) {
+        // actor.bwd1 with actor.head.bwd folded in (host: one problem, K = H1 <= 256 and a multiple
+        // of 16 -- at most one group of 4 whole k slabs per wave -- and Aout <= 8).  The slab operands (Ha2, W1^T and
+        // the W3a rows of the generation MFMA) are requested before the prologue, so the tile
+        // pays one memory round trip for both.
+        auto hbw_loop = [&](auto vt) {
+            constexpr bool V = decltype(vt)::value;
+            const int Aout = ga.hbw.Aout;
+            float a[4][4], b[4][4], w[4][2];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int it = it0 + u;
+                const int k0 = it * 16 + grp * 4;
+                const int k0e = it < it1 ? k0 : (1 << 30);
+                load_a<true, V, false>(ra, g, m, mok, k0e, a[u], rw);
+                load_b<true, V>(rb, g, n, nok, k0e, b[u]);
+                // generation A operand: lane (r, grp) holds W3a[16 it + r][4 s + grp]
+                const int kr = it * 16 + r;
+#pragma unroll
+                for (int s = 0; s < 2; ++s)
+                    w[u][s] = bload(rw, boff(it < it1 && kr < g.K && 4 * s + grp < Aout, kr * Aout + 4 * s + grp));
+            }
+            head_bwd_prologue(ga.hbw, m0, tn, d3s, so);
+            // generation B operand: Da3[m0 + r][4 s + grp] (zeros past Aout)
+            float d3[2];
+#pragma unroll
+            for (int s = 0; s < 2; ++s) d3[s] = d3s[r][4 * s + grp];
+            float* Da2 = sr(ga.hbw.Da2, so);
+            const bool store = tn == 0 && mok;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                // D'[k][m] = sum_o W3a[k][o] Da3[m][o]: lane (r, grp) gets rows k = 16 it + 4 grp + j
+                // of column m = m0 + r -- exactly its A operand elements a[u][j]
+                floatx4 pre = {0.f, 0.f, 0.f, 0.f};
+                pre = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u][0], d3[0], pre, 0, 0, 0);
+                pre = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u][1], d3[1], pre, 0, 0, 0);
+                const int k0 = (it0 + u) * 16 + grp * 4;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) a[u][j] = pre[j] * dact_sel(a[u][j], g.gen_act);
+                if (store && it0 + u < it1)
+                    *reinterpret_cast<float4*>(&Da2[(size_t)m * g.K + k0]) = float4{a[u][0], a[u][1], a[u][2], a[u][3]};
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if constexpr (BF) {
+                    const shortx4 av = {bf16_bits(a[u][0]), bf16_bits(a[u][1]), bf16_bits(a[u][2]), bf16_bits(a[u][3])};
+                    const shortx4 bv = {bf16_bits(b[u][0]), bf16_bits(b[u][1]), bf16_bits(b[u][2]), bf16_bits(b[u][3])};
+                    if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc1, 0, 0, 0);
+                    else acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc0, 0, 0, 0);
+                    continue;
+                }
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1], b[u][1], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][3], b[u][3], acc1, 0, 0, 0);
+            }
+        };
+        if constexpr (VEC == 1) {
+            if (g.vec) hbw_loop(std::true_type{});
+            else hbw_loop(std::false_type{});
+        } else {
+            hbw_loop(std::false_type{});
+        }
+        a_lds = true;
     }
     if constexpr (MODE == GM_FWD2) {
         // layer 0 per 16-wide hidden chunk hb: D' = W0^T[hb.., :] X^T[:, m0..] leaves lane
@@ -1061,7 +1224,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
-    if constexpr ((MODE == GM_FWD || MODE == GM_FWD2) && ROWK != 3) {
+    if constexpr ((MODE == GM_FWD || MODE == GM_FWD2) && ROWK != 3 && ROWK != 5) {
         if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
             const float pred = v + e0;
             const float sp_hat = e1 + (pred * e4 + e3);
@@ -1075,6 +1238,30 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             if (!out_ok) return;
             st_out(&g.C[(size_t)mm * g.ldc + nn], (gscale * diff) * e4);
             if (col == 0) st_out(&g.part[(size_t)mm * g.tiles_n + tn], sq);
+            return;
+        }
+    }
+    if constexpr (PART) {
+        if (g.ppart != nullptr) {        // uniform over the problem
+            if (mm >= g.M) return;       // whole 16-lane rows
+            float x;
+            if constexpr (MODE == GM_DX) x = nn < g.N ? v * dact_f(e0, g.act) : 0.f;
+            else x = nn < g.N ? act_f(v + e0, g.act) : 0.f;
+            float mine = 0.f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                // sum over the 16 columns of this thread's tile row (16-lane DPP row); lane j's
+                // association order is fixed, so its stored value is deterministic
+                float s = x * pwv[j];
+                s = s + dpp<0xB1>(s);
+                s = s + dpp<0x4E>(s);
+                s = s + dpp<0x124>(s);
+                s = s + dpp<0x128>(s);
+                mine = col == j ? s : mine;
+            }
+            if (col < g.pw_n) st_out(&g.ppart[((size_t)mm * g.pw_n + col) * g.tiles_n + tn], mine);
+            if (g.C == nullptr || !out_ok) return;
+            st_out(&g.C[(size_t)mm * g.ldc + nn], x);
             return;
         }
     }
@@ -1164,6 +1351,14 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
             if (a.vec) { if (h8) SACX_FH(1, 8); else SACX_FH(1, 4); }
             else { if (h8) SACX_FH(0, 8); else SACX_FH(0, 4); }
 #undef SACX_FH
+        } else if (a.rowk == 5) {          // actor.fwd1 (+alpha) writing the head partials (16x16 only)
+            if (a.bf16) {
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, true, PK, false>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, true, PK, false>), grid, block, 0, s, a);
+            } else {
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, false, PK, false>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, false, PK, false>), grid, block, 0, s, a);
+            }
         } else if (a.bf16) {
             if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK, T32>), grid, block, 0, s, a);
@@ -1173,14 +1368,22 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
         }
         break;
     case GM_DX: {
-        const dim3 gx(a.total_tiles + (a.rowk ? a.row_blocks : 0), 1, z);
+        const dim3 gx(a.total_tiles + (a.rowk && a.rowk < 3 ? a.row_blocks : 0), 1, z);
         const bool q8 = a.rowk && a.qh.H1 > 256;
 #define SACX_DX(V, R, Q)                                                                            \
     do {                                                                                           \
         if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK, T32>), gx, block, 0, s, a);          \
         else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK, T32>), gx, block, 0, s, a);                      \
     } while (0)
-        if (a.rowk == 1) {
+        if (a.rowk == 4) {                 // actor.bwd1 with actor.head.bwd folded in (16x16 only)
+            if (a.bf16) {
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, true, PK, false>), gx, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, true, PK, false>), gx, block, 0, s, a);
+            } else {
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, false, PK, false>), gx, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, false, PK, false>), gx, block, 0, s, a);
+            }
+        } else if (a.rowk == 1) {
             if (a.vec) { if (q8) SACX_DX(1, 1, 8); else SACX_DX(1, 1, 4); }
             else { if (q8) SACX_DX(0, 1, 8); else SACX_DX(0, 1, 4); }
         } else if (a.rowk == 2) {
@@ -1622,9 +1825,18 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         reloc(sg, so);
         const int A = h.A, Aout = h.Aout;
         const bool jok = lane < A;
-        // everything this row reads is issued up front
+        // everything this row reads is issued up front: its H2 row, or (h.part) the per-column-tile
+        // partials of H2 . W3 written by actor.fwd1 -- lane o < Aout sums output o's
+        const bool hp = h.part != nullptr;
         float hv[NQ];
-        load_row(rs(sr(h.H2, so)), row * h.ldh, h.H1, hv);
+        float4 pv[4];
+        if (hp) {
+            const __amdgpu_buffer_rsrc_t rp = rs(sr(h.part, so));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) pv[i] = bload4(rp, boff(lane < Aout && 4 * i < h.tq, (row * Aout + lane) * h.tq + 4 * i));
+        } else {
+            load_row(rs(sr(h.H2, so)), row * h.ldh, h.H1, hv);
+        }
         const __amdgpu_buffer_rsrc_t rW = rs(sr(h.W3, so));
         const float u_pf = bload(rs(sg.noise), boff(jok, (row - sg.r0) * A + lane));
         const float ls_pf = bload(rs(sr(h.logstd, so)), boff(jok && !h.per_state_std, lane));
@@ -1633,7 +1845,15 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         const float bmu = bload(rW, boff(jok, h.H1 * Aout + lane));
         const float bls = bload(rW, boff(jok && h.per_state_std, h.H1 * Aout + A + lane));
         float mu = 0.f, lraw = 0.f;
-        if constexpr (OW > 0) {        // Aout <= OW, H1 <= 256 (host-checked): W3 from LDS
+        if (hp) {
+            float v = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v = v + pv[i].x; v = v + pv[i].y; v = v + pv[i].z; v = v + pv[i].w;
+            }
+            mu = v;
+            lraw = __shfl(v, min(lane + A, 63), 64);
+        } else if constexpr (OW > 0) {        // Aout <= OW, H1 <= 256 (host-checked): W3 from LDS
             float so_[OW];
             rowdot_lds<NQ, OW>(hv, w3s, h.H1, Aout, so_);
 #pragma unroll

@@ -284,6 +284,8 @@ void build_layout(sacx_handle* h) {
     const int Ra4 = (Ra + 3) & ~3;
     const uint64_t oHa1 = h->add("ws.Ha1", Ra4 + B, H0, F, 0);
     const uint64_t oHa2 = h->add("ws.Ha2", Ra4 + B, H1, F, 0);
+    // Ha2 . W3 per 16-column tile of actor.fwd1 (rows as ws.Ha2), summed by the head rows
+    h->add("ws.hpart", Ra4 + B, (int64_t)h->Aout * ((H1 + 15) / 16), F, 0);
     h->add("ws.c_t", Rb, A, F, 0);
     h->add("ws.c_std", Rb, A, F, 0);
     h->add("ws.c_u", Rb, A, F, 0);
@@ -302,6 +304,7 @@ void build_layout(sacx_handle* h) {
     h->add("ws.Dp1", 2 * B, H0, F, 0);
     h->add("ws.lp", 1, B, F, 0);
     h->add("ws.gp", 2, B, F, 0);                 // policy-row output gradients of q0, q1
+    h->add("ws.apart", 2 * B, ((H0 + 15) / 16) * A, F, 0);   // their action-gradient partials (folded head bwd)
     h->add("ws.ones", 1, std::max(std::max(Rb, B), std::max(1, h->mb)) + 4, F, SACX_ROLE_STATE);
     h->add("ws.Hm1", ne1, Hm0, F, 0);
     h->add("ws.Hm2", ne1, Hm1, F, 0);
@@ -422,7 +425,9 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     // (packed seeds: many tiles per launch); head-prologue and fused two-layer launches stay 16x16
     // (tile32 = 2: forward / dX launches only -- the dW + Adam epilogue's registers cost occupancy)
     bool t32 = h->tile32 > 0;
-    for (auto& p : ps) t32 = t32 && p.headp == 0 && p.W0 == nullptr && !(h->tile32 == 2 && p.epi == EPI_ADAM);
+    for (auto& p : ps)
+        t32 = t32 && p.headp == 0 && p.W0 == nullptr && !(h->tile32 == 2 && p.epi == EPI_ADAM) && p.ppart == nullptr &&
+              p.hbw == 0;
     const int ts = t32 ? 32 : 16;
     int tiles = 0;
     for (auto& p : ps) {
@@ -661,14 +666,34 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.bytes = 4.0 * (r1 - r0) * H0 * 3;
         plan.push_back(L);
     };
+    // actor.fwd1 writes the head's Ha2 . W3 as per-column-tile partials (rowk 5), so the head
+    // rows and the target-tile prologues sum 16 values per output instead of re-reading Ha2
+    // rows.  SACX_HEAD_PART=0 keeps the row dots (A/B measurement).
+    const char* hpe = std::getenv("SACX_HEAD_PART");
+    const int tqh = (H1 + 15) / 16;
+    const bool head_part = Aout <= 8 && H1 <= 256 && H1 % 64 == 0 && !(fuse_mode != 0 && fuse_a) &&
+                           (hpe ? std::atoi(hpe) != 0 : true);
+    float* hpart = W("ws.hpart");
+    // layer 1 of the actor on `rows` rows from row r0 of Ha1 / Ha2 (+ the head partials)
+    auto actor_fwd1 = [&](int r0, int rows) {
+        GemmProb p = prob_fwd(Ha1 + (size_t)r0 * H0, H0, rows, H0, W("actor.l1"), H1, Ha2 + (size_t)r0 * H1, a1);
+        if (head_part) {
+            p.pw = W("actor.l2"); p.pw_ld = 1; p.pw_cs = Aout; p.pw_n = Aout;   // W3[n][o] at n * Aout + o
+            p.ppart = hpart + (size_t)r0 * Aout * tqh;
+        }
+        return p;
+    };
+    auto mark_part = [&]() { if (head_part) plan.back().gemm.rowk = 5; };
     bool actor_fused = false;
     if (h->ln) {
         add_gemm(h, plan, "actor.fwd0", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, ACT_NONE)}, record_probs);
         ln_fwd("actor.ln", 0, h->Ra);
-        add_gemm(h, plan, "actor.fwd1", {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, a1)}, record_probs);
+        add_gemm(h, plan, "actor.fwd1", {actor_fwd1(0, h->Ra)}, record_probs);
+        mark_part();
     } else {
         actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, a0)},
-                               {prob_fwd(Ha1, H0, h->Ra, H0, W("actor.l1"), H1, Ha2, a1)}, fuse_a, -1, alpha_tiles);
+                               {actor_fwd1(0, h->Ra)}, fuse_a, -1, alpha_tiles);
+        if (!actor_fused) mark_part();
     }
     // actor.head folded into q.fwd0 (plain SAC): the target tiles compute their rows' actions
     // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
@@ -680,10 +705,18 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     const bool fuse_head = !eo && Aout <= 16 && S + A <= 64 && H1 % 16 == 0 && H1 <= 512 &&
                            (fh ? std::atoi(fh) != 0 : h->seeds < 4);
     HeadArgs head_fused{};
+    // actor.head.bwd folded into actor.bwd1 (plain SAC; the expert rows' model gradients keep
+    // the row kernel): pi.q.bwd1 writes per-tile partial action gradients, actor.bwd1's tiles
+    // finish them.  SACX_FOLD_HBW=0 keeps the separate launch (A/B measurement).
+    const char* fhb = std::getenv("SACX_FOLD_HBW");
+    const int tq = (H0 + 15) / 16;
+    const bool fold_hbw = !eo && Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
+                          (fhb ? std::atoi(fhb) != 0 : true);
     // ---- actor head
     if (fuse_head) {
         HeadArgs& a = head_fused;
         a.H2 = Ha2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.part = head_part ? hpart : nullptr; a.tq = tqh;
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         // q.fwd0 carries the target rows (tile prologues) and, folded, the previous update's
@@ -704,6 +737,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.frees_slot = true;
         HeadArgs& a = L.head;
         a.H2 = Ha2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.part = head_part ? hpart : nullptr; a.tq = tqh;
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         a.nseg = eo ? 3 : 2;
@@ -907,6 +941,17 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 pb.push_back(p);
             }
         }
+        if (fold_hbw) {                      // partial action gradients instead of Dp1 (read by no one else)
+            for (int k = 0; k < 2; ++k) {
+                GemmProb& p = pb[k];
+                p.pw = W("q" + std::to_string(k) + ".l0") + (size_t)S * H0;   // action rows of W_ext
+                p.pw_ld = H0;
+                p.pw_cs = 1;
+                p.pw_n = A;
+                p.ppart = W("ws.apart") + (size_t)k * B * tq * A;
+                p.C = nullptr;
+            }
+        }
         add_gemm(h, plan, "pi.q.head+pi.q.bwd1", pb, record_probs);
         {
             Launch& L = plan.back();
@@ -928,6 +973,27 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         }
     }
     // ---- actor backward
+    if (fold_hbw) {
+        // actor.head.bwd as the tile prologue of actor.bwd1: Da3 from the partials of pi.q.bwd1,
+        // Da2 generated on load (an MFMA from Da3 and W3a), stored by column tile 0
+        const int Rb = h->Rb;
+        GemmProb p = prob_dx(Ha2 + (size_t)B * H1, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1,
+                             h->ln ? ACT_TANH : a0);
+        p.wgen = W("actor.l2");              // W3a [(H1+1) x Aout]
+        p.gen_act = a1;                      // act'(Ha2)
+        p.hbw = 1;
+        add_gemm(h, plan, "actor.head.bwd+actor.bwd1", {p}, record_probs);
+        Launch& L = plan.back();
+        L.gemm.rowk = 4;
+        HeadBwdArgs& b = L.gemm.hbw;
+        b.B = B; b.A = A; b.Aout = Aout; b.per_state_std = h->cfg.per_state_std; b.tq = tq;
+        b.lim = h->cfg.act_limit; b.part = W("ws.apart"); b.gpol = W("ws.gp"); b.a_den = W("norm.a_den");
+        b.alpha = W("alpha");
+        b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
+        b.Da3 = Da3; b.E = E; b.Da2 = Da2;
+        L.flops += 2.0 * B * 2 * H0 * A + 2.0 * Rb * H1 * Aout;
+        L.bytes += 4.0 * (2.0 * B * tq * A + 2.0 * Rb * H1);
+    }
     {
         Launch L{};
         L.kind = Launch::ABWD;
@@ -945,11 +1011,13 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.grid = (h->Rb + 3) / 4;
         L.flops = 2.0 * B * 2 * H0 * A + 2.0 * ne * Hm0 * A + 2.0 * h->Rb * H1 * Aout;
         L.bytes = 4.0 * (2.0 * B * H0 + ne * Hm0 + 2.0 * h->Rb * H1);
-        plan.push_back(L);
         const int Rb = h->Rb;
-        add_gemm(h, plan, "actor.bwd1",      // layer-norm layer 0: tanh' at its output
-                 {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, h->ln ? ACT_TANH : a0)},
-                 record_probs);
+        if (!fold_hbw) {
+            plan.push_back(L);
+            add_gemm(h, plan, "actor.bwd1",      // layer-norm layer 0: tanh' at its output
+                     {prob_dx(Da2, Rb, H1, W("actor.l1"), H0, Ha1 + (size_t)B * H0, Da1, h->ln ? ACT_TANH : a0)},
+                     record_probs);
+        }
         if (h->ln) {                          // dY -> dZ through the norm; dY*xhat, dY for gamma / beta
             Launch N{};
             N.kind = Launch::LNORM;
@@ -990,10 +1058,12 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, "alpha.fwd0", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, ACT_NONE)},
                  record_probs);
         ln_fwd("alpha.ln", Ra4, Ra4 + B);
-        add_gemm(h, plan, "alpha.fwd1", {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, a1)}, record_probs);
+        add_gemm(h, plan, "alpha.fwd1", {actor_fwd1(Ra4, B)}, record_probs);
+        mark_part();
     } else {
-        fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, a0)},
-                 {prob_fwd(Hl1, H0, B, H0, W("actor.l1"), H1, Hl2, a1)}, fuse_a, actor_fused ? 1 : 0);
+        if (!fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, a0)},
+                      {actor_fwd1(Ra4, B)}, fuse_a, actor_fused ? 1 : 0))
+            mark_part();
     }
     {
         Launch L{};
@@ -1001,6 +1071,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.name = "alpha.head";
         HeadArgs& a = L.head;
         a.H2 = Hl2; a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.part = head_part ? hpart + (size_t)Ra4 * Aout * tqh : nullptr; a.tq = tqh;
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         a.nseg = 1;

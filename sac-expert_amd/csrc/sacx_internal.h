@@ -100,6 +100,33 @@ struct GemmProb {
     // GM_FWD / GM_DX: this problem's operands take float4 loads along k (host-checked strides and
     // alignment); the launch's VEC template only says whether any problem does
     int32_t vec;
+    // GM_DX in a q-head launch (rowk 2) / GM_FWD in an actor launch (rowk 5): per-row partial
+    // dots of the tile's output row with the rows of pw -- ppart[(m * pw_n + j) * tiles_n + tn] =
+    // sum over the tile's 16 columns n of C[m][n] * pw[j * pw_ld + n * pw_cs], j < pw_n <= 8.
+    // rowk 2: the policy rows' action gradient through the critic's layer-0 action rows (summed
+    // by the folded actor head backward; C may then be null).  rowk 5: the actor head
+    // mu / logstd rows = Ha2 . W3 (summed, + bias, by the head rows and prologues).
+    const float* pw;
+    float* ppart;
+    int32_t pw_ld, pw_cs, pw_n;
+    // GM_DX with rowk 4: the folded actor head backward problem (GemmArgs::hbw)
+    int32_t hbw;
+};
+
+// rowk 4 (GM_DX, actor.bwd1): the actor head backward (k_actor_bwd's policy-row work) runs as
+// the tile prologue.  Per row: ga = (g0 * sum ppart_q0 + g1 * sum ppart_q1) / a_den, the
+// tanh-Gaussian backward (A5) -> Da3[row][0, Aout) (and E), then the A operand
+// Da2[row][k] = (sum_o Da3[row][o] W3a[k][o]) * act'(Ha2[row][k]) is generated on load by a
+// small MFMA (W3a = the problem's wgen, Ha2 = its A); column tile 0 stores Da2 for actor.adam.
+struct HeadBwdArgs {
+    int32_t B, A, Aout, per_state_std, tq;   // tq: partials per row and critic (H0 / 16 tiles)
+    float lim;
+    const float* part;      // [2, B, A, tq]
+    const float* gpol;      // [2, B] output gradients of q0, q1 (the partials are unscaled)
+    const float* a_den;
+    const float* alpha;
+    const float *c_t, *c_std, *c_u, *c_mask;   // backward cache rows [0, B)
+    float* Da3; float* E; float* Da2;
 };
 
 struct FinalArgs {
@@ -179,6 +206,10 @@ struct HeadArgs {
     const float *a_mean, *a_den;
     float logstd_init;     // mode 2: GaussianActor.logstd_init (continuous_actors.py:39-44)
     int32_t output_norm;   // mode 2: --actor_output_norm (continuous_actors.py:68-72)
+    // nullable: the head's Ha2 . W3 as per-column-tile partials written by actor.fwd1 (rowk 5),
+    // part[(row * Aout + o) * tq + i], i < tq (<= 16, a multiple of 4); row = the H2 row
+    const float* part;
+    int32_t tq;
     int32_t nseg;
     HeadSeg seg[4];
     int32_t total_rows;
@@ -224,12 +255,14 @@ struct GemmArgs {
     HeadArgs head;
     FinalArgs hfin;
     int32_t head_block0;
+    HeadBwdArgs hbw;       // rowk 4 (GM_DX)
     uint64_t* ktime;       // measurement only: per-workgroup start / end ticks (nullable)
     // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
     int64_t sstride;
     int32_t nseeds;
 };
+static_assert(sizeof(GemmArgs) <= 4096, "GemmArgs travels as kernel arguments");
 
 // ---------------------------------------------------------------- sampler + gather
 struct RngArgs {
