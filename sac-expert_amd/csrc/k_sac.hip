@@ -18,6 +18,7 @@
 // rounds like the reference's separate TF ops (dot products use explicit
 // fmaf).  GEMM accumulation is the exact-f32 MFMA (k-ordered fmaf chain).
 #include <hip/hip_runtime.h>
+#include <cstddef>
 #include <type_traits>
 #include <math.h>
 #include "sacx_internal.h"
@@ -124,7 +125,10 @@ __device__ __forceinline__ float adam_lr(const AdamConsts& c, int group, int64_t
     const float b1 = 0.9f, b2 = 0.999f;
     const float tt = (float)t;
     const float b1p = powf(b1, tt), b2p = powf(b2, tt);
-    return c.lr[group] * sqrtf(1.f - b2p) / (1.f - b1p);
+    // selects, not c.lr[group]: a dynamic kernarg index is a scalar load at the use
+    const float lr = group == GRP_Q ? c.lr[GRP_Q] : (group == GRP_PI ? c.lr[GRP_PI] :
+                     (group == GRP_ALPHA ? c.lr[GRP_ALPHA] : c.lr[GRP_MODEL]));
+    return lr * sqrtf(1.f - b2p) / (1.f - b1p);
 }
 
 // Keras Adam (ResourceApplyAdam): m += (g-m)(1-b1); v += (g^2-v)(1-b2);
@@ -182,6 +186,29 @@ __device__ __forceinline__ uint32_t boff(bool ok, int elem) {
     asm("" : "+v"(o));
     return o;
 }
+// The control-block scalars a GEMM epilogue needs (the optimiser step, the Polyak gate, the
+// expert weight), requested with the epilogue operands before the main loop: read after the
+// tile reduction they were two more dependent memory round trips (the kernarg ctl pointer,
+// then the field) on every dW + Adam workgroup.
+struct EpiScalars {
+    int64_t t, nts;
+    float eps;
+};
+__device__ __forceinline__ EpiScalars epi_scalars(const Ctl* ctl, int group) {
+    // per-lane buffer loads (boff hides the uniform offsets): the values stay in VGPRs, where a
+    // uniform load would be moved to SGPRs right away and stall the main loop's loads behind it
+    const __amdgpu_buffer_rsrc_t r = make_rsrc(reinterpret_cast<const float*>(ctl), (uint32_t)sizeof(Ctl));
+    const int ot = (int)((group == GRP_MODEL ? offsetof(Ctl, t_model) : offsetof(Ctl, t_sac)) / 4);
+    const int on = (int)(offsetof(Ctl, num_timesteps) / 4), oe = (int)(offsetof(Ctl, epsilon) / 4);
+    const uint32_t t_lo = __float_as_uint(bload(r, boff(true, ot))), t_hi = __float_as_uint(bload(r, boff(true, ot + 1)));
+    const uint32_t n_lo = __float_as_uint(bload(r, boff(true, on))), n_hi = __float_as_uint(bload(r, boff(true, on + 1)));
+    EpiScalars e;
+    e.t = (int64_t)(((uint64_t)t_hi << 32) | t_lo);
+    e.nts = (int64_t)(((uint64_t)n_hi << 32) | n_lo);
+    e.eps = bload(r, boff(true, oe));
+    return e;
+}
+
 // wave index as a scalar (lets per-row pointers and branches stay in SGPRs)
 __device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
@@ -743,6 +770,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             e3[s] = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
         }
     }
+    const EpiScalars es = epi_scalars(sr(ga.ctl, so), g.group);
 
     const int nIt = (g.K + 15) >> 4;
     const int per = (nIt + 3) >> 2;
@@ -814,7 +842,6 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
     __syncthreads();
 
     const int L = ((row >> 2) << 4) | col, R = row & 3;
-    const Ctl* ctl = sr(ga.ctl, so);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         float v = red[s][R][L] + red[4 + s][R][L];
@@ -829,7 +856,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 const float pred = v + e0[s];
                 const float sp_hat = e1[s] + (pred * e4[s] + e3[s]);
                 const float diff = e2[s] - sp_hat;
-                const float gscale = -ctl->epsilon * g.grad_scale;
+                const float gscale = -es.eps * g.grad_scale;
                 float sq = out_ok ? diff * diff : 0.f;
                 sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's sub-tile row
                 sq += __shfl_xor(sq, 4, 16);
@@ -850,8 +877,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
                 continue;
             }
-            const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
-            const float lr_t = adam_lr(ga.adam, g.group, tstep);
+            const float lr_t = adam_lr(ga.adam, g.group, es.t + 1);
             const float gr = v * g.grad_scale;
             const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
             const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
@@ -862,7 +888,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
             if (g.T != nullptr) {
                 const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-                if (ctl->num_timesteps % tui == 0) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
+                if (es.nts % tui == 0) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
             }
         }
     }
@@ -946,7 +972,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                      "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec));
     } else {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
-                     "s"(g.tile_begin), "s"(g.act), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row));
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row),
+                     "s"(g.group), "s"(g.epi), "s"(g.grad_scale), "s"(ga.adam.lr[0]), "s"(ga.adam.lr[1]),
+                     "s"(ga.adam.lr[2]), "s"(ga.adam.lr[3]), "s"(ga.adam.tau_keep), "s"(ga.adam.tau_take),
+                     "s"(ga.adam.target_update_int));
     }
     reloc(g, so);
     GEMM_PH(1);
@@ -989,6 +1018,9 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         // no target: a zero-sized resource reads 0 without a branch
         e3 = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
     }
+    EpiScalars es{};
+    if constexpr (MODE == GM_DW || ((MODE == GM_FWD || MODE == GM_FWD2) && ROWK != 3 && ROWK != 5))
+        es = epi_scalars(sr(ga.ctl, so), g.group);
     // partial-dot weights of this thread's output column (zero-sized resource: no partials)
     constexpr bool PART = (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5);
     float pwv[8];
@@ -1229,7 +1261,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             const float pred = v + e0;
             const float sp_hat = e1 + (pred * e4 + e3);
             const float diff = e2 - sp_hat;
-            const float gscale = -sr(ga.ctl, so)->epsilon * g.grad_scale;
+            const float gscale = -es.eps * g.grad_scale;
             float sq = out_ok ? diff * diff : 0.f;
             sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's tile row
             sq += __shfl_xor(sq, 4, 16);
@@ -1275,9 +1307,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             return;
         }
-        const Ctl* ctl = sr(ga.ctl, so);
-        const int64_t tstep = (g.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
-        const float lr_t = adam_lr(ga.adam, g.group, tstep);
+        const float lr_t = adam_lr(ga.adam, g.group, es.t + 1);
         const float gr = v * g.grad_scale;
         const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
         const float mm1 = e1 + (gr - e1) * (1.f - b1);
@@ -1288,7 +1318,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
         if (g.T != nullptr) {
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-            if (ctl->num_timesteps % tui == 0) st_out(&g.T[pidx], e3 * ga.adam.tau_keep + pn * ga.adam.tau_take);
+            if (es.nts % tui == 0) st_out(&g.T[pidx], e3 * ga.adam.tau_keep + pn * ga.adam.tau_take);
         }
     }
 }
