@@ -341,6 +341,9 @@ def packed_leg(cfgd, config, rep, k, steps, with_roofline):
     packed chain counts the K seeds' FLOPs per launch."""
     eng = build_engine(cfgd, replica_seeds(rep, k), device=rep.device)
     eng.step(256)
+    # a steady-state figure whatever --steps says: at least 4 full 128-update graphs (a 20-step
+    # region is two graph launches and two sampler ramps, not the packed chain's rate)
+    steps = max(steps, 512)
     cap_s = eng.prepare(steps)          # every graph step(steps) replays, instantiated untimed
     eng.sync()
     rep.barrier()

@@ -125,10 +125,9 @@ __device__ __forceinline__ float adam_lr(const AdamConsts& c, int group, int64_t
     const float b1 = 0.9f, b2 = 0.999f;
     const float tt = (float)t;
     const float b1p = powf(b1, tt), b2p = powf(b2, tt);
-    // selects, not c.lr[group]: a dynamic kernarg index is a scalar load at the use
-    const float lr = group == GRP_Q ? c.lr[GRP_Q] : (group == GRP_PI ? c.lr[GRP_PI] :
-                     (group == GRP_ALPHA ? c.lr[GRP_ALPHA] : c.lr[GRP_MODEL]));
-    return lr * sqrtf(1.f - b2p) / (1.f - b1p);
+    // c.lr[group], not a chain of selects: the selects made the compiler copy the whole kernarg
+    // block into scratch in the 32x32 dW variants
+    return c.lr[group] * sqrtf(1.f - b2p) / (1.f - b1p);
 }
 
 // Keras Adam (ResourceApplyAdam): m += (g-m)(1-b1); v += (g^2-v)(1-b2);
@@ -842,6 +841,15 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
     __syncthreads();
 
     const int L = ((row >> 2) << 4) | col, R = row & 3;
+    // the Polyak gate once per workgroup, as a scalar (a per-lane 64-bit modulo per sub-tile
+    // would be outlined, with a stack frame in scratch)
+    bool polyak = false;
+    if constexpr (MODE == GM_DW) {
+        const int64_t nts = (int64_t)__builtin_amdgcn_readfirstlane((int)(es.nts >> 32)) << 32 |
+                            (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
+        const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
+        polyak = nts % tui == 0;
+    }
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         float v = red[s][R][L] + red[4 + s][R][L];
@@ -886,10 +894,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             st_out(&g.P[pidx], pn);
             st_out(&g.P[pidx + ga.p_stride], mm1);
             st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-            if (g.T != nullptr) {
-                const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-                if (es.nts % tui == 0) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
-            }
+            if (g.T != nullptr && polyak) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
         }
     }
 }
@@ -1317,8 +1322,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         st_out(&g.P[pidx + ga.p_stride], mm1);
         st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
         if (g.T != nullptr) {
+            const int64_t nts = (int64_t)__builtin_amdgcn_readfirstlane((int)(es.nts >> 32)) << 32 |
+                                (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-            if (es.nts % tui == 0) st_out(&g.T[pidx], e3 * ga.adam.tau_keep + pn * ga.adam.tau_take);
+            if (nts % tui == 0) st_out(&g.T[pidx], e3 * ga.adam.tau_keep + pn * ga.adam.tau_take);
         }
     }
 }

@@ -672,7 +672,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     const char* hpe = std::getenv("SACX_HEAD_PART");
     const int tqh = (H1 + 15) / 16;
     const bool head_part = Aout <= 8 && H1 <= 256 && H1 % 64 == 0 && !(fuse_mode != 0 && fuse_a) &&
-                           (hpe ? std::atoi(hpe) != 0 : true);
+                           (hpe ? std::atoi(hpe) != 0 : h->tile32 == 0);
     float* hpart = W("ws.hpart");
     // layer 1 of the actor on `rows` rows from row r0 of Ha1 / Ha2 (+ the head partials)
     auto actor_fwd1 = [&](int r0, int rows) {
@@ -710,8 +710,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // finish them.  SACX_FOLD_HBW=0 keeps the separate launch (A/B measurement).
     const char* fhb = std::getenv("SACX_FOLD_HBW");
     const int tq = (H0 + 15) / 16;
+    // Both folds keep their launches on 16x16 tiles: with 32x32 tiles (packed seeds) the tiles
+    // win (HC 8 seeds 43.9k without the folds vs 40.3k with them), so they are off there.
     const bool fold_hbw = !eo && Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
-                          (fhb ? std::atoi(fhb) != 0 : true);
+                          (fhb ? std::atoi(fhb) != 0 : h->tile32 == 0);
     // ---- actor head
     if (fuse_head) {
         HeadArgs& a = head_fused;

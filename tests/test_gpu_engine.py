@@ -482,6 +482,9 @@ def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, ea
     if K >= 4:                                  # the packed plan: 32x32 tiles ("1": dW + Adam too)
         monkeypatch.setenv("SACX_FUSE_HEAD", "0")
         monkeypatch.setenv("SACX_T32", t32 or "2")
+        # without the 16x16-only folds (head partials, folded head backward), as that plan has
+        monkeypatch.setenv("SACX_FOLD_HBW", "0")
+        monkeypatch.setenv("SACX_HEAD_PART", "0")
     learners = [make_learner(act="tanh", B=B, N=N, seed=40 + 7 * k, use_expert=use_expert, epsilon=eps)
                 for k in range(K)]
 

@@ -111,6 +111,10 @@ def test_packed8_production_schedule(gpu_available, monkeypatch):
     from sac_eo.engine import Engine, EngineConfig
     K, n, B, N, eps = 8, 150, 128, 3000, 0.1
     monkeypatch.setenv("SACX_FUSE_HEAD", "0")
+    # the 32x32 plan keeps the separate actor head backward and the row-dot head; so do the
+    # one-seed references (their folds would change the summation order)
+    monkeypatch.setenv("SACX_FOLD_HBW", "0")
+    monkeypatch.setenv("SACX_HEAD_PART", "0")
     learners = [make_learner(act="relu", B=B, N=N, seed=60 + 5 * k) for k in range(K)]
 
     def cfg(seeds, G):
