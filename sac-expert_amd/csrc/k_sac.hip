@@ -223,7 +223,7 @@ __device__ __forceinline__ T* sr(T* p, int64_t so) {
 }
 __device__ __forceinline__ void reloc(GemmProb& g, int64_t so) {
     g.A = sr(g.A, so); g.B = sr(g.B, so); g.C = sr(g.C, so); g.bias = sr(g.bias, so); g.H = sr(g.H, so);
-    g.P = sr(g.P, so); g.T = sr(g.T, so); g.W0 = sr(g.W0, so); g.C0 = sr(g.C0, so); g.wgen = sr(g.wgen, so);
+    g.P = sr(g.P, so); g.T = sr(g.T, so); g.wgen = sr(g.wgen, so);
     g.bscale = sr(g.bscale, so); g.se_raw = sr(g.se_raw, so); g.spe_raw = sr(g.spe_raw, so);
     g.dmean = sr(g.dmean, so); g.dden = sr(g.dden, so); g.part = sr(g.part, so);
     g.pw = sr(g.pw, so); g.ppart = sr(g.ppart, so);
@@ -964,7 +964,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.vec), "s"(g.C), "s"(g.ldc),
                      "s"(g.pw), "s"(g.ppart), "s"(g.pw_ld), "s"(g.pw_cs), "s"(g.pw_n));
-    } else if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+    } else if constexpr (MODE == GM_FWD) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
                      "s"(g.dmean), "s"(g.dden), "s"(g.headp), "s"(g.vec));
@@ -985,7 +985,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     reloc(g, so);
     GEMM_PH(1);
     if constexpr (T32) {
-        static_assert(MODE != GM_FWD2 && !(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
+        static_assert(!(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
         gemm_tile32<MODE, VEC, BF>(ga, g, tile - g.tile_begin, so, red);
         return;
     }
@@ -1005,7 +1005,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float e0 = 0.f, e1 = 0.f, e2 = 0.f, e3 = 0.f;
     const size_t pidx = (size_t)mmc * g.ldp + nnc;
     float e4 = 0.f;
-    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+    if constexpr (MODE == GM_FWD) {
         e0 = g.bias[nnc];
         if constexpr (ROWK != 3 && ROWK != 5) {   // head-fused / actor launches: no mse problems
             // world-model head rows (mse): zero-sized resources when not an mse problem
@@ -1024,7 +1024,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         e3 = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
     }
     EpiScalars es{};
-    if constexpr (MODE == GM_DW || ((MODE == GM_FWD || MODE == GM_FWD2) && ROWK != 3 && ROWK != 5))
+    if constexpr (MODE == GM_DW || (MODE == GM_FWD && ROWK != 3 && ROWK != 5))
         es = epi_scalars(sr(ga.ctl, so), g.group);
     // partial-dot weights of this thread's output column (zero-sized resource: no partials)
     constexpr bool PART = (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5);
@@ -1142,79 +1142,11 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         }
         a_lds = true;
     }
-    if constexpr (MODE == GM_FWD2) {
-        // layer 0 per 16-wide hidden chunk hb: D' = W0^T[hb.., :] X^T[:, m0..] leaves lane
-        // (r, grp) holding H1[m0+r][hb+4grp+v] in register v -- exactly the A operand of the
-        // layer-1 MFMA v with k = hb+4grp+v, so H1 never leaves registers.
-        constexpr int NK0 = VEC;   // layer-0 K steps of 4, rounded up to even (host-checked)
-        const int H0 = g.K;
-        const __amdgpu_buffer_rsrc_t rw0 = make_rsrc(g.W0, 0x7fffffffu);
-        float xv[NK0];
-#pragma unroll
-        for (int s = 0; s < NK0; ++s) {
-            const int k = 4 * s + grp;
-            xv[s] = bload(ra, boff(mok && k < g.K0, m * g.lda + k));
-        }
-        const bool store_h1 = (tn == 0) && mok;
-        // groups of 4 chunks, every load of a group issued before its first MFMA
-        // (a loop-carried register copy would force vmcnt(0) per chunk)
-        for (int c0 = it0; c0 < it1; c0 += 4) {
-            float w0v[4][NK0], b0v[4][4], w1v[4][4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int it = c0 + c;
-                const int hb = it * 16;
-                const bool hok = (it < it1) && (hb + r < H0);
-#pragma unroll
-                for (int s = 0; s < NK0; ++s) {
-                    const int k = 4 * s + grp;
-                    w0v[c][s] = bload(rw0, boff(hok && k < g.K0, k * H0 + hb + r));
-                }
-#pragma unroll
-                for (int v = 0; v < 4; ++v) {
-                    const int hk = hb + 4 * grp + v;
-                    const bool kok = (it < it1) && (hk < H0);
-                    b0v[c][v] = bload(rw0, boff(kok, g.K0 * H0 + hk));
-                    w1v[c][v] = bload(rb, boff(kok && nok, hk * g.ldb + n));
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);   // all loads of the group in flight before any MFMA
-            floatx4 d[4];
-#pragma unroll
-            for (int c = 0; c < 4; ++c) d[c] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int s = 0; s < NK0; ++s)
-#pragma unroll
-                for (int c = 0; c < 4; ++c) d[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(w0v[c][s], xv[s], d[c], 0, 0, 0);
-            float hh[16];
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-                for (int v = 0; v < 4; ++v) hh[4 * c + v] = d[c][v] + b0v[c][v];
-            act_block(hh, g.act);
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int it = c0 + c;
-                const float h[4] = {hh[4 * c], hh[4 * c + 1], hh[4 * c + 2], hh[4 * c + 3]};
-                if (store_h1 && it < it1) {
-                    const int hk = it * 16 + 4 * grp;
-#pragma unroll
-                    for (int v = 0; v < 4; ++v)
-                        if (hk + v < H0) st_out(&g.C0[(size_t)m * H0 + hk + v], h[v]);
-                }
-                // chunks past it1 have w1 = 0: they add exact zeros
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[0], w1v[c][0], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[1], w1v[c][1], acc1, 0, 0, 0);
-                acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[2], w1v[c][2], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(h[3], w1v[c][3], acc1, 0, 0, 0);
-            }
-        }
-    }
     // float4 operand loads per problem (g.vec): a launch can mix problems with and without
     // them, and the loop is unswitched on the flag
     auto main_loop = [&](auto vt) {
     constexpr bool V = decltype(vt)::value;
-    for (int it = it0; MODE != GM_FWD2 && !a_lds && it < it1; it += 4) {
+    for (int it = it0; !a_lds && it < it1; it += 4) {
         float a[4][4], b[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
@@ -1261,7 +1193,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
-    if constexpr ((MODE == GM_FWD || MODE == GM_FWD2) && ROWK != 3 && ROWK != 5) {
+    if constexpr (MODE == GM_FWD && ROWK != 3 && ROWK != 5) {
         if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
             const float pred = v + e0;
             const float sp_hat = e1 + (pred * e4 + e3);
@@ -1303,7 +1235,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         }
     }
     if (!out_ok) return;
-    if constexpr (MODE == GM_FWD || MODE == GM_FWD2) {
+    if constexpr (MODE == GM_FWD) {
         st_out(&g.C[(size_t)mm * g.ldc + nn], act_f(v + e0, g.act));
     } else if constexpr (MODE == GM_DX) {
         st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0, g.act));
@@ -1433,18 +1365,6 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 #undef SACX_DX
         break;
     }
-    case GM_FWD2:
-        switch (a.vec) {
-        case 2: hipLaunchKernelGGL((k_gemm<GM_FWD2, 2, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        case 4: hipLaunchKernelGGL((k_gemm<GM_FWD2, 4, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        case 6: hipLaunchKernelGGL((k_gemm<GM_FWD2, 6, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        case 8: hipLaunchKernelGGL((k_gemm<GM_FWD2, 8, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        case 10: hipLaunchKernelGGL((k_gemm<GM_FWD2, 10, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        case 12: hipLaunchKernelGGL((k_gemm<GM_FWD2, 12, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        case 14: hipLaunchKernelGGL((k_gemm<GM_FWD2, 14, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        default: hipLaunchKernelGGL((k_gemm<GM_FWD2, 16, 0, 4, false, PK>), grid, block, 0, s, a); break;
-        }
-        break;
     default:
         if (a.rowk == 3) {                 // dW + Adam with the policy rows of actor.head beside it
             const dim3 gh(a.total_tiles + a.row_blocks, 1, z);
@@ -1466,7 +1386,7 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
     // 32x32 tiles: plain FWD / DX / DW launches only (the host never sets t32 elsewhere)
-    const bool t32 = a.t32 && a.mode != GM_FWD2 && !(a.mode == GM_FWD && a.rowk == 3);
+    const bool t32 = a.t32 && !(a.mode == GM_FWD && a.rowk == 3);
     if (a.nseeds > 1) {
         if (t32) launch_gemm_t<true, true>(a, s);
         else launch_gemm_t<true, false>(a, s);

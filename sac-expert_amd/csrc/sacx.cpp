@@ -86,8 +86,6 @@ struct Launch {
     bool alpha_branch = false; // graph: runs on the side stream beside the next update's first launches
     bool frees_slot = false;   // graph: the launch that carries the folded alpha rows (last reader of a slot)
     // graph: the critics' forward on the buffer rows (s, a) runs on its own stream, between
-    // the previous update's critic.adam (q_release) and this update's q.head (q_consumer)
-    bool side_q = false, q_release = false, q_consumer = false;
 };
 
 const char* kernel_family(Launch::Kind k) {
@@ -140,13 +138,13 @@ struct sacx_handle {
     // binding
     char* arena = nullptr;
     hipStream_t stream = nullptr;
-    hipStream_t cap_stream = nullptr, rng_stream = nullptr, q_stream = nullptr;
+    hipStream_t cap_stream = nullptr, rng_stream = nullptr;
     bool bound = false;
     std::vector<Launch> plan[NSLOT];
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
     int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
-    int xcd_map = 1;          // GEMM tiles XCD-contiguous (SACX_XCD=0 restores dispatch order)
+    int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
     // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
     int dp_ranks = 0, dp_rank = 0;
@@ -371,16 +369,6 @@ GemmProb prob_fwd(const float* X, int ldx, int M, int K, const float* Wext, int 
     return p;
 }
 
-// two chained Dense layers (GM_FWD2): C1 = act(X W0 + b0) [M x H0], C = act(C1 W1 + b1) [M x N]
-GemmProb prob_fwd2(const float* X, int ldx, int M, int K0, const float* W0ext, int H0, float* C1,
-                   const float* W1ext, int N, float* C, int act) {
-    GemmProb p = prob_fwd(X, ldx, M, H0, W1ext, N, C, act);
-    p.K0 = K0;
-    p.W0 = W0ext;
-    p.C0 = C1;
-    return p;
-}
-
 // C = (D * W^T) (.) act'(Hprev), W_ext is [(K_in+1) x N_out]; C is [M x K_in]
 GemmProb prob_dx(const float* D, int M, int Nout, const float* Wext, int Kin, const float* Hprev, float* C, int act) {
     GemmProb p{};
@@ -405,11 +393,8 @@ GemmProb prob_dw(const float* X, int ldx, int Kin, int R, const float* D, int No
 }
 
 // algorithmic counts (the fused layer 0 counted once, not per column tile)
-double gemm_flops(const GemmProb& p) { return 2.0 * p.M * p.N * p.K + (p.W0 ? 2.0 * p.M * p.K * p.K0 : 0.0); }
+double gemm_flops(const GemmProb& p) { return 2.0 * p.M * p.N * p.K; }
 double gemm_bytes(const GemmProb& p) {
-    if (p.W0)   // X, W0, H1 out, W1, H2 out
-        return 4.0 * ((double)p.M * p.K0 + (p.K0 + 1.0) * p.K + (double)p.M * p.K + (p.K + 1.0) * p.N +
-                      (double)p.M * p.N);
     double b = 4.0 * ((double)p.M * p.K + (double)p.K * p.N + (double)p.M * p.N);
     if (p.epi == EPI_ADAM) b += 4.0 * p.M * p.N * (p.T ? 8 : 6) - 4.0 * p.M * p.N;
     if (p.epi == EPI_DACT) b += 4.0 * p.M * p.N;
@@ -426,7 +411,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     // (tile32 = 2: forward / dX launches only -- the dW + Adam epilogue's registers cost occupancy)
     bool t32 = h->tile32 > 0;
     for (auto& p : ps)
-        t32 = t32 && p.headp == 0 && p.W0 == nullptr && !(h->tile32 == 2 && p.epi == EPI_ADAM) && p.ppart == nullptr &&
+        t32 = t32 && p.headp == 0 && !(h->tile32 == 2 && p.epi == EPI_ADAM) && p.ppart == nullptr &&
               p.hbw == 0;
     const int ts = t32 ? 32 : 16;
     int tiles = 0;
@@ -444,17 +429,11 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     if (ps.size() > GEMM_MAXP) { fprintf(stderr, "sacx: too many GEMM problems in %s\n", name.c_str()); abort(); }
     // every problem of a launch must share the operand/epilogue mode (k_gemm template)
     auto mode_of = [](const GemmProb& p) {
-        return p.epi == EPI_ADAM ? GM_DW : (p.epi == EPI_DACT ? GM_DX : (p.W0 ? GM_FWD2 : GM_FWD));
+        return p.epi == EPI_ADAM ? GM_DW : (p.epi == EPI_DACT ? GM_DX : GM_FWD);
     };
     const int mode = mode_of(ps[0]);
     bool vec = false;   // any problem with float4 loads (each problem carries its own flag)
-    int k0max = 0;
     for (auto& p : ps) {
-        if (mode == GM_FWD2 && (p.K0 < 1 || p.K0 > FWD2_MAX_K0)) {
-            fprintf(stderr, "sacx: fused layer-0 K %d out of range in %s\n", p.K0, name.c_str());
-            abort();
-        }
-        k0max = std::max(k0max, p.K0);
         // 32-bit buffer offsets: every operand the GEMM reads must stay below 2 GiB
         const double ext = 4.0 * ((double)p.M * p.lda + (double)p.K * p.ldb + p.N);
         if (ext >= 2147483648.0) { fprintf(stderr, "sacx: operand too large in %s\n", name.c_str()); abort(); }
@@ -476,12 +455,12 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     }
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
     L.gemm.mode = mode;
-    L.gemm.vec = mode == GM_FWD2 ? ((k0max + 7) / 8) * 2 : (vec ? 1 : 0);
+    L.gemm.vec = vec ? 1 : 0;
     for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
     L.gemm.nprob = (int)ps.size();
     L.gemm.total_tiles = tiles;
     L.gemm.xcd_map = h->xcd_map;
-    L.gemm.bf16 = h->cfg.gemm_bf16 != 0 && mode != GM_FWD2;   // the fused forward stays fp32
+    L.gemm.bf16 = h->cfg.gemm_bf16 != 0;
     L.gemm.p_stride = h->p_stride;
     L.gemm.ctl = h->ctl();
     L.gemm.adam.lr[GRP_Q] = h->cfg.lr_q;
@@ -505,7 +484,7 @@ bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
     }
     a.nprob += b.nprob;
     a.total_tiles += b.total_tiles;
-    a.vec = (a.mode == GM_FWD2) ? std::max(a.vec, b.vec) : (a.vec || b.vec);
+    a.vec = a.vec || b.vec;
     return true;
 }
 
@@ -551,8 +530,6 @@ void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string&
     a.adam = G.gemm.adam;
     U.grid = (int)((n + 255) / 256);
     U.bytes = 4.0 * n * (targ.empty() ? 7 : 9);
-    U.q_release = G.q_release;          // the weights are final after the apply, not the grad launch
-    G.q_release = false;
     plan.push_back(U);
 }
 
@@ -625,33 +602,13 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         plan.push_back(L);
     }
     // ---- actor forward on [sp ; s ; s_e]
-    // Layer 0 has a small K (S, S+A): it can be fused into layer 1 (GM_FWD2, <= 512 tiles).
-    // Measured on MI355X it no longer pays once the alpha branch is folded and the heads
-    // share launches (12.0k vs 11.9k updates/s), so it is off unless SACX_FUSE=1.
-    const char* fenv = std::getenv("SACX_FUSE");
-    const int fuse_mode = fenv ? (std::atoi(fenv) ? -1 : 0) : 0;
-    // the fused two-layer forward applies one activation to both layers
-    const bool fuse_a = S <= FWD2_MAX_K0 && a0 == a1 && !h->ln, fuse_q = S + A <= FWD2_MAX_K0 && c0 == c1;
-    auto fwd_pair = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1,
-                        bool fuse, int forced = -1, int extra_tiles = 0) -> bool {
-        int tiles = extra_tiles;      // tiles of problems folded into the same launch later
-        for (auto& p : p1) tiles += ((p.M + 15) / 16) * ((p.N + 15) / 16);
-        if (fuse_mode == 0 || (fuse_mode < 0 && tiles > 512)) fuse = false;
-        if (forced >= 0) fuse = fuse && forced;
-        if (!fuse) {
-            add_gemm(h, plan, name + "0", p0, record_probs);
-            add_gemm(h, plan, name + "1", p1, record_probs);
-            return false;
-        }
-        std::vector<GemmProb> pf;
-        for (size_t i = 0; i < p0.size(); ++i)
-            pf.push_back(prob_fwd2(p0[i].A, p0[i].lda, p0[i].M, p0[i].K, p0[i].B, p0[i].N, p0[i].C, p1[i].B,
-                                   p1[i].N, p1[i].C, p1[i].act));
-        add_gemm(h, plan, name, pf, record_probs);
-        return true;
+    // the two forward layers of a net as two launches (a fused two-layer tile recomputing
+    // layer 0 per column tile measured slower once the alpha branch and the heads share
+    // launches: 12.06k vs 12.33k updates/s)
+    auto fwd_pair = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1) {
+        add_gemm(h, plan, name + "0", p0, record_probs);
+        add_gemm(h, plan, name + "1", p1, record_probs);
     };
-    // the previous update's alpha forward (B rows) is folded into this launch (merged_body)
-    const int alpha_tiles = ((B + 15) / 16) * ((H1 + 15) / 16);
     const int Ra4 = (h->Ra + 3) & ~3;       // first row of the alpha rows (ws.Hl1 / ws.Hl2 alias Ha1 / Ha2)
     // --actor_layer_norm: layer 0 writes the pre-norm Z, k_ln turns it into tanh(LN(Z)) in place
     auto ln_fwd = [&](const std::string& name, int r0, int r1) {
@@ -671,7 +628,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // rows.  SACX_HEAD_PART=0 keeps the row dots (A/B measurement).
     const char* hpe = std::getenv("SACX_HEAD_PART");
     const int tqh = (H1 + 15) / 16;
-    const bool head_part = Aout <= 8 && H1 <= 256 && H1 % 64 == 0 && !(fuse_mode != 0 && fuse_a) &&
+    const bool head_part = Aout <= 8 && H1 <= 256 && H1 % 64 == 0 &&
                            (hpe ? std::atoi(hpe) != 0 : h->tile32 == 0);
     float* hpart = W("ws.hpart");
     // layer 1 of the actor on `rows` rows from row r0 of Ha1 / Ha2 (+ the head partials)
@@ -684,16 +641,14 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         return p;
     };
     auto mark_part = [&]() { if (head_part) plan.back().gemm.rowk = 5; };
-    bool actor_fused = false;
     if (h->ln) {
         add_gemm(h, plan, "actor.fwd0", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, ACT_NONE)}, record_probs);
         ln_fwd("actor.ln", 0, h->Ra);
         add_gemm(h, plan, "actor.fwd1", {actor_fwd1(0, h->Ra)}, record_probs);
         mark_part();
     } else {
-        actor_fused = fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, a0)},
-                               {actor_fwd1(0, h->Ra)}, fuse_a, -1, alpha_tiles);
-        if (!actor_fused) mark_part();
+        fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, a0)}, {actor_fwd1(0, h->Ra)});
+        mark_part();
     }
     // actor.head folded into q.fwd0 (plain SAC): the target tiles compute their rows' actions
     // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
@@ -758,25 +713,14 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     }
     // ---- target / critic / model forward
     if (fuse_head) {
-        // SACX_SIDE_Q=1 moves the critics' (s, a) forward onto a third stream, off the chain.
-        // Measured slower on MI355X (9.6k vs 11.8k updates/s): the cross-stream edges of the
-        // replayed graph add ~0.3 us to every launch gap and q.head then waits ~8 us.
-        const char* sq = std::getenv("SACX_SIDE_Q");
-        const bool side_q = sq && std::atoi(sq) != 0;
-        std::vector<GemmProb> p0, p1, s0, s1;
+        std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
             GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, c0);
             q0.headp = k < 2;
             GemmProb q1 = prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, c1);
-            (side_q && k >= 2 ? s0 : p0).push_back(q0);
-            (side_q && k >= 2 ? s1 : p1).push_back(q1);
-        }
-        if (side_q) {
-            add_gemm(h, plan, "qsa.fwd0", s0, record_probs);
-            plan.back().side_q = true;
-            add_gemm(h, plan, "qsa.fwd1", s1, record_probs);
-            plan.back().side_q = true;
+            p0.push_back(q0);
+            p1.push_back(q1);
         }
         add_gemm(h, plan, "q.fwd0+actor.head", p0, record_probs);
         Launch& L = plan.back();
@@ -804,7 +748,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                       Hm2b + (size_t)k * half * Hm1, m1));
             }
         }
-        fwd_pair("q.fwd", p0, p1, fuse_q);
+        fwd_pair("q.fwd", p0, p1);
     }
     // ---- critic backward.  By linearity Dq1 = g (.) M1 with M1 = ((w3 (.) act'(Hq2)) Wq1^T) (.) act'(Hq1)
     // independent of the per-row loss gradient g, so the dX GEMM (A generated from Hq2 and w3)
@@ -831,7 +775,6 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         }
         add_gemm(h, plan, "q.head+critic.bwd1", pb, record_probs);
         Launch& L = plan.back();
-        L.q_consumer = true;
         L.gemm.rowk = 1;
         L.gemm.row_blocks = (B + 3) / 4;
         L.gemm.qh = q;
@@ -850,7 +793,6 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                  W(n + ".l2"), W(t + ".l2"), GRP_Q));
         }
         add_gemm(h, plan, "critic.adam", pw, record_probs);
-        plan.back().q_release = true;
         if (fuse_head) {                    // the policy rows of actor.head (read from pi.q.fwd0 on)
             Launch& L = plan.back();
             HeadArgs a = head_fused;
@@ -901,21 +843,17 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 pm.push_back(p);
             }
         }
-        const bool pi_fused = fwd_pair("pi.q.fwd", p0, p1, fuse_q);
-        if (eo) {
-            if (pi_fused) {
-                add_gemm(h, plan, "model.head", pm, record_probs);
-            } else {                         // plan.back() is pi.q.fwd1: fold into pi.q.fwd0
-                Launch& F0 = plan[plan.size() - 2];
-                std::vector<Launch> one;
-                add_gemm(h, one, "model.head", pm, false);
-                h->probs_cursor -= (int)pm.size();
-                if (!merge_gemm(F0.gemm, one[0].gemm)) { fprintf(stderr, "sacx: model.head merge\n"); abort(); }
-                F0.name += "+model.head";
-                F0.grid = F0.gemm.total_tiles;
-                F0.flops += one[0].flops;
-                F0.bytes += one[0].bytes;
-            }
+        fwd_pair("pi.q.fwd", p0, p1);
+        if (eo) {                            // plan.back() is pi.q.fwd1: fold into pi.q.fwd0
+            Launch& F0 = plan[plan.size() - 2];
+            std::vector<Launch> one;
+            add_gemm(h, one, "model.head", pm, false);
+            h->probs_cursor -= (int)pm.size();
+            if (!merge_gemm(F0.gemm, one[0].gemm)) { fprintf(stderr, "sacx: model.head merge\n"); abort(); }
+            F0.name += "+model.head";
+            F0.grid = F0.gemm.total_tiles;
+            F0.flops += one[0].flops;
+            F0.bytes += one[0].bytes;
         }
         QHeadArgs q{};
         q.mode = 1; q.B = B; q.H1 = H1; q.H2 = Hp2;
@@ -1063,9 +1001,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, "alpha.fwd1", {actor_fwd1(Ra4, B)}, record_probs);
         mark_part();
     } else {
-        if (!fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, a0)},
-                      {actor_fwd1(Ra4, B)}, fuse_a, actor_fused ? 1 : 0))
-            mark_part();
+        fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, a0)},
+                 {actor_fwd1(Ra4, B)});
+        mark_part();
     }
     {
         Launch L{};
@@ -1331,7 +1269,7 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                 C.name += "+alpha";
                 head_done = true;
             } else if (C.kind == Launch::GEMM && head_done && !final_done && pf &&
-                       (C.gemm.mode == GM_FWD || C.gemm.mode == GM_FWD2)) {
+                       C.gemm.mode == GM_FWD) {
                 C.gemm.has_final = 1;
                 C.gemm.fin = pf->fin;
                 C.name += "+alpha.final";
@@ -1395,8 +1333,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             enqueue(L, h, st);
         }
     };
-    hipStream_t cs = h->cap_stream, rs = h->rng_stream, qs = h->q_stream;
-    const int nev = 5 * G + 1;
+    hipStream_t cs = h->cap_stream, rs = h->rng_stream;
+    const int nev = 3 * G + 1;
     for (int i = (int)h->events.size(); i < nev; ++i) {
         hipEvent_t e;
         HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -1406,20 +1344,13 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     hipEvent_t* evS = h->events.data() + G;      // update j's body done
     hipEvent_t* evF = h->events.data() + 2 * G;  // alpha.final of update j done
     hipEvent_t evFork = h->events[3 * G];
-    hipEvent_t* evC = h->events.data() + 3 * G + 1;  // update j's critic weights final (critic.adam)
-    hipEvent_t* evQ = h->events.data() + 4 * G + 1;  // update j's (s, a) critic forward done
     HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
-    const bool fork = with_rng && std::getenv("SACX_NO_FORK") == nullptr;
-    // diagnostics: SACX_GATHER_MAIN keeps the gather on the main stream; SACX_MERGE_ALPHA=0
-    // keeps each alpha branch as separate launches
-    const bool gather_main = std::getenv("SACX_GATHER_MAIN") != nullptr;
-    if (fork) {
+    if (with_rng) {
         // cs: the updates, each with the previous update's alpha branch folded into its first
         //     launches (merged_body), plus the last update's alpha branch as a tail;
         // rs: sampler + gather of update j+2 into slot (j+2)%3 == (j-1)%3, once update j's
         //     actor.head (the last reader of that slot, through the folded alpha rows) has run.
-        const bool merge = h->dp_ranks == 0 &&
-                           (std::getenv("SACX_MERGE_ALPHA") == nullptr || std::atoi(std::getenv("SACX_MERGE_ALPHA")));
+        const bool merge = h->dp_ranks == 0;   // the DP mode keeps each alpha branch as its own launches
         HIPCHK(h, hipEventRecord(evFork, cs));
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
         // Sampler batches [s, e): one k_rng launch draws updates s..e-1 in stream order and one
@@ -1446,7 +1377,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         auto prologue = [&](int b) {
             const int j0 = batches[b].first, n = batches[b].second - j0;
             for (const Launch& L : h->plan[j0 % nslot]) {
-                if (!is_prologue(L) || (gather_main && L.kind == Launch::GATHER)) continue;
+                if (!is_prologue(L)) continue;
                 if ((int)L.kind == skip_kind) continue;   // ablation of the sampler (stale randoms)
                 Launch C = L;
                 if (C.kind == Launch::RNG) {
@@ -1466,22 +1397,6 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         }
         for (int b = 0; b < (int)batches.size(); ++b)
             if (emit_after[b] < 0) HIPCHK(h, prologue(b));
-        // the (s, a) critic forward of update j on qs: after update j-1's critic.adam (graph
-        // start for j = 0) and update j's inputs; update j's q.head waits for it
-        auto side_q = [&](int j, hipEvent_t after) -> hipError_t {
-            int bj = 0;
-            for (int b = 0; b < (int)batches.size(); ++b)
-                if (batches[b].first <= j && j < batches[b].second) bj = b;
-            hipError_t e = hipStreamWaitEvent(qs, after, 0);
-            if (e == hipSuccess) e = hipStreamWaitEvent(qs, evR[bj], 0);
-            for (const Launch& L : h->plan[j % nslot])
-                if (e == hipSuccess && L.side_q && (int)L.kind != skip_kind) emit(L, qs);
-            if (e == hipSuccess) e = hipEventRecord(evQ[j], qs);
-            return e;
-        };
-        bool has_side = false;
-        for (const Launch& L : h->plan[0]) has_side = has_side || L.side_q;
-        if (has_side) HIPCHK(h, side_q(0, evFork));
         std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
             if (batch_of[j] >= 0) HIPCHK(h, hipStreamWaitEvent(cs, evR[batch_of[j]], 0));
@@ -1500,22 +1415,12 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 if (emit_after[b] == j) due.push_back(b);
             bool recorded = false;
             for (const Launch& L : body) {
-                if (L.side_q) continue;        // on qs (side_q above)
-                if (L.q_consumer && has_side) HIPCHK(h, hipStreamWaitEvent(cs, evQ[j], 0));
                 if ((int)L.kind == skip_kind) {
                     // ablation: the alpha.final folded into a skipped GEMM still runs
                     if (L.kind == Launch::GEMM && L.gemm.has_final) launch_alpha_final(L.gemm.fin, cs);
-                    if (L.q_release && has_side && j + 1 < G) {
-                        HIPCHK(h, hipEventRecord(evC[j], cs));
-                        HIPCHK(h, side_q(j + 1, evC[j]));
-                    }
                     continue;
                 }
                 emit(L, cs);
-                if (L.q_release && has_side && j + 1 < G) {
-                    HIPCHK(h, hipEventRecord(evC[j], cs));
-                    HIPCHK(h, side_q(j + 1, evC[j]));
-                }
                 if (!due.empty() && !recorded && L.frees_slot) {
                     HIPCHK(h, hipEventRecord(evS[j], cs));
                     recorded = true;
@@ -1674,7 +1579,6 @@ void sacx_destroy(sacx_handle* h) {
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
-    if (h->q_stream) (void)hipStreamDestroy(h->q_stream);
     if (h->comm) (void)ncclCommDestroy(h->comm);
     delete h;
 }
@@ -1729,7 +1633,6 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
             HIPCHK(h, hipMemcpy(h->arena0 + (uint64_t)k * h->seed_bytes + so.off, ones.data(), ones.size() * sizeof(float),
                                 hipMemcpyHostToDevice));
     }
-    if (const char* e = std::getenv("SACX_XCD")) h->xcd_map = std::atoi(e) != 0;
     // 32x32 forward / dX tiles once the launches are wide: seeds x batch >= 1024 rows (packed
     // seeds; Humanoid B = 1024: SAC-EO +5.6 %, model fit +8 %, SAC +1 %); a handle-level rule, so
     // the launches merged_body folds together always agree.  From 4,096 rows the dW + Adam
@@ -1759,7 +1662,6 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     build_model_plan(h);
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
-    HIPCHK(h, hipStreamCreateWithFlags(&h->q_stream, hipStreamNonBlocking));
     h->bound = true;
     return 0;
 }

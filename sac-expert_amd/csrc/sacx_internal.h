@@ -55,11 +55,7 @@ struct AdamConsts {
 // K split over the 4 waves of a 256-thread workgroup and reduced through LDS.
 enum Epi { EPI_FWD = 0, EPI_DACT = 1, EPI_ADAM = 2, EPI_STORE = 3 };
 // launch-uniform operand/epilogue mode of k_gemm (template parameter)
-// GM_FWD2: two chained Dense layers, H2 = act(act(X W0 + b0) W1 + b1), for a
-// small layer-0 K (<= 64): the layer-0 output is recomputed per column tile in
-// registers and never round-trips through memory (column tile 0 stores it).
-enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2, GM_FWD2 = 3 };
-#define FWD2_MAX_K0 64
+enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2 };
 
 struct GemmProb {
     const float* A;        // a_kc: A[m*lda + k]   else A[k*lda + m] (row ones_row = 1.0)
@@ -75,9 +71,6 @@ struct GemmProb {
     int32_t epi, act, group;
     int32_t tiles_n, tile_begin;
     float grad_scale;
-    int32_t K0;            // GM_FWD2: layer-0 inner dim (A is then X[M x K0], K is the hidden width)
-    const float* W0;       // GM_FWD2: layer-0 W_ext [(K0+1) x K]
-    float* C0;             // GM_FWD2: layer-0 output H1 [M x K] (row stride K)
     // GM_DX: when set, A is generated on load as wgen[k] * act'(A[m][k]) -- the delta at the
     // layer-2 output of a scalar-output net for a unit output gradient (the per-row gradient
     // is applied downstream: the result is linear in it)
@@ -233,7 +226,6 @@ struct GemmArgs {
     int32_t nprob;
     int32_t mode;          // GemmMode, uniform over the launch's problems
     int32_t vec;           // GM_FWD/GM_DX: float4 loads along k (ld % 4 == 0, K % 4 == 0, aligned);
-                           // GM_FWD2: layer-0 K steps of 4, rounded up to even (2..16)
     int32_t total_tiles;
     int32_t xcd_map;       // 1: each XCD takes a contiguous tile range (see xcd_tile)
     int32_t bf16;          // 1: bf16 MFMA operands (rounded on load), fp32 accumulate (config C5)

@@ -13,7 +13,7 @@ run() {
 }
 if [ $# -eq 0 ]; then
   set -- base:X=1 nb2:SACX_NBATCH=2 nb8:SACX_NBATCH=8 nb8g64:SACX_NBATCH=8,SACX_GRAPH_STEPS=64 \
-         nb1:SACX_NBATCH=1 fuse:SACX_FUSE=1
+         nb1:SACX_NBATCH=1
 fi
 for v in "$@"; do
   tag="${v%%:*}"; vars="${v#*:}"

@@ -87,40 +87,6 @@ int main() {
             double us = tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); });
             printf("sweep xcd=%d 512x256 K=%-4d L2 reads %5.1f MB: %.2f us/launch\n", xm, K, mb, us);
         }
-    // fused two-layer forward (GM_FWD2) vs the two single-layer launches it replaces
-    for (int M : {512, 1024}) {
-        const int K0 = M == 512 ? 17 : 23, H0 = 256, N = 256;
-        GemmArgs f2{}; GemmProb p{};
-        p.A = X0; p.lda = 24; p.a_kc = 1; p.ones_row = -1; p.B = W + 100000; p.ldb = N; p.b_kc = 0;
-        p.M = M; p.N = N; p.K = H0; p.bias = W + 100000 + (size_t)H0 * N; p.C = X1; p.ldc = N;
-        p.epi = EPI_FWD; p.act = ACT_RELU; p.tiles_n = N / 16; p.tile_begin = 0;
-        p.K0 = K0; p.W0 = W; p.C0 = X1 + 2000000;
-        f2.probs[0] = p; f2.nprob = 1; f2.total_tiles = (M / 16) * (N / 16); f2.p_stride = NF; f2.ctl = ctl;
-        f2.mode = GM_FWD2; f2.vec = ((K0 + 7) / 8) * 2;
-        char nm[64];
-        snprintf(nm, sizeof nm, "fwd2 %dx%d K0=%d", M, N, K0);
-        printf("%-28s %4d tiles: %.2f us/launch\n", nm, f2.total_tiles, tgraph(s, n, [&](int) { launch_gemm(f2, s); }));
-        {
-            static unsigned long long ph[8192][5];
-            CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_gemm_ph), sizeof(ph)));
-            const int T = f2.total_tiles;
-            unsigned long long lo = ~0ull, hi = 0;
-            double d[4] = {0, 0, 0, 0};
-            for (int b = 0; b < T; ++b) {
-                lo = std::min(lo, ph[b][0]);
-                hi = std::max(hi, ph[b][4]);
-                for (int j = 0; j < 4; ++j) d[j] += (double)(ph[b][j + 1] - ph[b][j]);
-            }
-            printf("  phases: span %.2f us | mean per WG: select %.2f  loads+mfma %.2f  reduce %.2f  epilogue %.2f us\n",
-                   (hi - lo) * 0.01, d[0] * 0.01 / T, d[1] * 0.01 / T, d[2] * 0.01 / T, d[3] * 0.01 / T);
-        }
-        GemmArgs a0 = fwd(X0, X1 + 2000000, M, H0, K0);
-        a0.probs[0].lda = 24; a0.vec = a0.probs[0].vec = 0;
-        GemmArgs a1 = fwd(X1 + 2000000, X1, M, N, H0);
-        snprintf(nm, sizeof nm, "fwd0+fwd1 %dx%d K0=%d", M, N, K0);
-        printf("%-28s %4d tiles: %.2f us/pair\n", nm, a0.total_tiles + a1.total_tiles,
-               2 * tgraph(s, n, [&](int i) { launch_gemm((i & 1) ? a1 : a0, s); }));
-    }
     // Adam epilogue on a 257x256 grad tile set (dW of a 256x256 layer, K = batch 256)
     {
         GemmArgs ga{}; GemmProb p{};

@@ -9,4 +9,3 @@ run SACX_T32=0
 run SACX_T32=1
 run SACX_T32=2 SACX_FUSE_HEAD=0
 run SACX_T32=0 SACX_FUSE_HEAD=0
-run SACX_T32=2 SACX_XCD=0
