@@ -86,3 +86,20 @@ def test_packed_seed_layout_without_gpu():
     bad = EngineConfig(s_dim=17, a_dim=6, seeds=65).to_c()
     assert L.sacx_create(ctypes.byref(bad), ctypes.byref(h1)) != 0
     assert b"seeds" in L.sacx_last_error(None)
+
+
+def test_no_kernel_uses_kilobytes_of_scratch():
+    """Build guard (tools/check_scratch.py): every gfx950 kernel in libsacx.so keeps its
+    private segment small -- kilobytes there mean a spilled / copied kernel-argument block."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    so = os.path.join(root, "sac-expert_amd", "lib", "libsacx.so")
+    if not os.path.exists("/opt/rocm/lib/llvm/bin/clang-offload-bundler") or not os.path.exists(so):
+        pytest.skip("ROCm LLVM tools or libsacx.so absent")
+    sys.path.insert(0, os.path.join(root, "tools"))
+    from check_scratch import kernel_scratch
+    sizes = kernel_scratch(so)
+    assert len(sizes) > 50
+    bad = {k: v for k, v in sizes.items() if v > 256}
+    assert not bad, bad
