@@ -734,7 +734,7 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
 #ifndef SACX_T32_NS
 #define SACX_T32_NS 1   // k slabs per load group of a 32x32 tile (1: 6 workgroups per CU fit)
 #endif
-template <int MODE, int VEC, bool BF>
+template <int MODE, int VEC, bool BF, bool PART = false>
 __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
                                             float (&red)[16][4][64]) {
     constexpr bool AKC = (MODE != GM_DW);
@@ -859,6 +859,34 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         const bool out_ok = (mm < g.M) && (nn < g.N);
         const int mmc = min(mm, g.M - 1), nnc = min(nn, g.N - 1);
         const size_t pidx = (size_t)mmc * g.ldp + nnc;
+        if constexpr (PART) {
+            if (g.ppart != nullptr) {     // uniform: the partial head dots of gemm_core's 16x16 path,
+                                          // per 16-column sub-tile (same values, same order)
+                float x;
+                if constexpr (MODE == GM_DX) x = nn < g.N ? v * dact_f(e0[s], g.act) : 0.f;
+                else x = nn < g.N ? act_f(v + e0[s], g.act) : 0.f;
+                if (mm < g.M) {           // whole 16-lane rows
+                    const __amdgpu_buffer_rsrc_t rpw = rs(g.pw);
+                    float w[8];
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) w[j] = bload(rpw, boff(j < g.pw_n && nn < g.N, j * g.pw_ld + nnc * g.pw_cs));
+                    float mine = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        float d = x * w[j];
+                        d = d + dpp<0xB1>(d);
+                        d = d + dpp<0x4E>(d);
+                        d = d + dpp<0x124>(d);
+                        d = d + dpp<0x128>(d);
+                        mine = col == j ? d : mine;
+                    }
+                    if (col < g.pw_n)
+                        st_out(&g.ppart[((size_t)mm * g.pw_n + col) * ((g.N + 15) >> 4) + 2 * tn + (s & 1)], mine);
+                }
+                if (out_ok && g.C != nullptr) st_out(&g.C[(size_t)mm * g.ldc + nn], x);
+                continue;
+            }
+        }
         if constexpr (MODE == GM_FWD) {
             if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
                 const float pred = v + e0[s];
@@ -986,7 +1014,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     GEMM_PH(1);
     if constexpr (T32) {
         static_assert(!(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
-        gemm_tile32<MODE, VEC, BF>(ga, g, tile - g.tile_begin, so, red);
+        gemm_tile32<MODE, VEC, BF, (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5)>(
+            ga, g, tile - g.tile_begin, so, red);
         return;
     }
     const int lt = tile - g.tile_begin;
@@ -1320,13 +1349,13 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
             if (a.vec) { if (h8) SACX_FH(1, 8); else SACX_FH(1, 4); }
             else { if (h8) SACX_FH(0, 8); else SACX_FH(0, 4); }
 #undef SACX_FH
-        } else if (a.rowk == 5) {          // actor.fwd1 (+alpha) writing the head partials (16x16 only)
+        } else if (a.rowk == 5) {          // actor.fwd1 (+alpha) writing the head partials
             if (a.bf16) {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, true, PK, false>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, true, PK, false>), grid, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, true, PK, T32>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, true, PK, T32>), grid, block, 0, s, a);
             } else {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, false, PK, false>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, false, PK, false>), grid, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, false, PK, T32>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, false, PK, T32>), grid, block, 0, s, a);
             }
         } else if (a.bf16) {
             if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, a);

@@ -411,8 +411,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     // (tile32 = 2: forward / dX launches only -- the dW + Adam epilogue's registers cost occupancy)
     bool t32 = h->tile32 > 0;
     for (auto& p : ps)
-        t32 = t32 && p.headp == 0 && !(h->tile32 == 2 && p.epi == EPI_ADAM) && p.ppart == nullptr &&
-              p.hbw == 0;
+        t32 = t32 && p.headp == 0 && !(h->tile32 == 2 && p.epi == EPI_ADAM) && p.hbw == 0;
     const int ts = t32 ? 32 : 16;
     int tiles = 0;
     for (auto& p : ps) {
@@ -665,8 +664,11 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // finish them.  SACX_FOLD_HBW=0 keeps the separate launch (A/B measurement).
     const char* fhb = std::getenv("SACX_FOLD_HBW");
     const int tq = (H0 + 15) / 16;
-    // Both folds keep their launches on 16x16 tiles: with 32x32 tiles (packed seeds) the tiles
-    // win (HC 8 seeds 43.9k without the folds vs 40.3k with them), so they are off there.
+    // The folded launch itself keeps 16x16 tiles (its prologue and generated A operand); the
+    // partial-writing launches may take 32x32 tiles.  On 32x32 (packed) plans both folds are off
+    // by default: there the launches are bound by workgroup residency, not by their number, and
+    // the folds' extra work loses (HC 8 seeds, A/B x2: both on 42.3k, hbw fold only 43.4k, head
+    // partials only 43.1k, both off 43.9k updates/s; tools/pk_ab.sh).
     const bool fold_hbw = !eo && Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
                           (fhb ? std::atoi(fhb) != 0 : h->tile32 == 0);
     // ---- actor head

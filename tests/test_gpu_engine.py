@@ -464,11 +464,13 @@ def test_rollout_graph_replay_equals_eager(gpu_available, monkeypatch):
     eng.close()
 
 
-@pytest.mark.parametrize("K,use_expert,eager,t32,bf16", [(3, False, False, None, False), (3, True, False, None, False),
-                                                        (3, False, True, None, False), (4, False, False, None, False),
-                                                        (4, True, False, None, False), (4, False, False, "1", False),
-                                                        (4, False, False, "1", True), (4, False, False, "2", True)])
-def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, eager, t32, bf16):
+@pytest.mark.parametrize("K,use_expert,eager,t32,bf16,folds",
+                         [(3, False, False, None, False, None), (3, True, False, None, False, None),
+                          (3, False, True, None, False, None), (4, False, False, None, False, "0"),
+                          (4, True, False, None, False, "0"), (4, False, False, "1", False, "0"),
+                          (4, False, False, "1", True, "0"), (4, False, False, "2", True, "0"),
+                          (4, False, False, "2", False, "1"), (4, False, True, "1", True, "1")])
+def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, eager, t32, bf16, folds):
     """cfg.seeds = K (the reference's --runs packed into one handle, grid z = seed): every
     seed ends bit-identical to a one-seed engine fed the same state, buffer, RNG stream and
     permutations -- stats, every parameter / Adam / target value, and the RNG key.  19
@@ -482,9 +484,10 @@ def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, ea
     if K >= 4:                                  # the packed plan: 32x32 tiles ("1": dW + Adam too)
         monkeypatch.setenv("SACX_FUSE_HEAD", "0")
         monkeypatch.setenv("SACX_T32", t32 or "2")
-        # without the 16x16-only folds (head partials, folded head backward), as that plan has
-        monkeypatch.setenv("SACX_FOLD_HBW", "0")
-        monkeypatch.setenv("SACX_HEAD_PART", "0")
+        # the partial-dot folds (off by default on 32x32 plans) set alike in both plans; "1": the
+        # partial epilogues on 32x32 tiles against the one-seed 16x16 ones
+        monkeypatch.setenv("SACX_FOLD_HBW", folds)
+        monkeypatch.setenv("SACX_HEAD_PART", folds)
     learners = [make_learner(act="tanh", B=B, N=N, seed=40 + 7 * k, use_expert=use_expert, epsilon=eps)
                 for k in range(K)]
 
