@@ -1643,6 +1643,11 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     const int64_t rows = (int64_t)h->seeds * h->B;
     h->tile32 = rows >= 4096 ? 1 : rows >= 1024 ? 2 : 0;
     if (const char* e = std::getenv("SACX_T32")) h->tile32 = std::atoi(e);
+    // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
+    // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
+    // an expensive one (Humanoid: 52k normals, 146 us per update) keeps 4, where the graph's
+    // ramp and the sampler's lead over the chain favour smaller batches (5.80k vs 5.62k at 8)
+    h->nbatch = h->n_norm <= 16384 ? 8 : 4;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     if (h->dp_ranks > 0) {
         if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
