@@ -39,6 +39,10 @@ CONFIGS = {
     # BASELINE.json configs[1]
     "hc": dict(workload="HalfCheetah-v3-shaped synthetic buffer, SAC twin-Q + actor + alpha update (no model), fp32",
                S=17, A=6, B=256, hidden=(256, 256), buffer=1_000_000, use_expert=False),
+    # configs[0]-shaped: the reference's default algorithm (SAC-EO: expert term through two
+    # 512x2 world models) at HalfCheetah shapes
+    "hc_eo": dict(workload="HalfCheetah-v3-shaped synthetic buffer, SAC-EO update incl. world-model expert term, fp32",
+                  S=17, A=6, B=256, hidden=(256, 256), buffer=1_000_000, use_expert=True),
     # configs[2]-shaped (SAC-EO expert term; model fitting is a separate call)
     "humanoid_eo": dict(workload="Humanoid-v3-shaped synthetic buffer, SAC-EO update incl. world-model expert term, fp32",
                         S=376, A=17, B=1024, hidden=(256, 256), buffer=1_000_000, use_expert=True),
@@ -497,14 +501,14 @@ def main():
         cpu = cpu_baseline(cfgd, args.cpu_seconds)
     if rank == 0:
         line = {
-            "metric": "SAC gradient-steps/sec (batch=256, 256x2 MLP)" if args.config == "hc"
-            else ("SAC-EO gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)" if cfgd["use_expert"]
-                  else "SAC gradient-steps/sec (Humanoid-shaped, batch=1024, 256x2 MLP)"),
+            "metric": ("SAC" + ("-EO" if cfgd["use_expert"] else "") + " gradient-steps/sec ("
+                       + ("" if cfgd["S"] == 17 else "Humanoid-shaped, ")
+                       + f"batch={cfgd['B']}, 256x2 MLP)"),
             "value": round(value, 2), "unit": "gradient-steps/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5), "higher_is_better": True,
             "scaling": "strong" if dp else "weak", "vs_baseline": None,
             "dtype": "bf16 (MFMA operands), f32 accumulate" if cfgd.get("bf16") else "f32",
-            "data": ("synthetic (" + ("HalfCheetah" if args.config == "hc" else "Humanoid")
+            "data": ("synthetic (" + ("HalfCheetah" if cfgd["S"] == 17 else "Humanoid")
                      + "-shaped replay rows generated on device; random orthogonal init)"),
             "config": {"workload": cfgd["workload"], "obs_dim": cfgd["S"], "act_dim": cfgd["A"],
                        "batch": cfgd["B"], "hidden": list(cfgd["hidden"]), "buffer_rows": cfgd["buffer"],

@@ -232,6 +232,7 @@ __device__ __forceinline__ void reloc(HeadBwdArgs& b, int64_t so) {
     b.part = sr(b.part, so); b.gpol = sr(b.gpol, so); b.a_den = sr(b.a_den, so); b.alpha = sr(b.alpha, so);
     b.c_t = sr(b.c_t, so); b.c_std = sr(b.c_std, so); b.c_u = sr(b.c_u, so); b.c_mask = sr(b.c_mask, so);
     b.Da3 = sr(b.Da3, so); b.E = sr(b.E, so); b.Da2 = sr(b.Da2, so);
+    b.mpart = sr(b.mpart, so); b.ctl = sr(b.ctl, so);
 }
 __device__ __forceinline__ void reloc(FinalArgs& f, int64_t so) {
     f.alpha = sr(f.alpha, so); f.alpha_m = sr(f.alpha_m, so); f.alpha_v = sr(f.alpha_v, so); f.ctl = sr(f.ctl, so);
@@ -676,9 +677,10 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
 __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn, float (&d3s)[16][17], int64_t so) {
     reloc(hb, so);
     const int t = threadIdx.x, lane = t & 63, row = t >> 4, col = t & 15;
-    const int B = hb.B, A = hb.A, tq = hb.tq;
+    const int B = hb.B, A = hb.A;
     const int m = m0 + row;
-    const bool rok = m < B, jok = col < A, ok = rok && jok;
+    const bool rok = m < B + hb.ne, jok = col < A, ok = rok && jok;
+    const bool pol = m < B;                     // policy row (else an expert row, SAC-EO)
     const int ci = m * A + col;
     const float ct = bload(rs(hb.c_t), boff(ok, ci));
     const float sd = bload(rs(hb.c_std), boff(ok, ci));
@@ -686,32 +688,42 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
     const float mk = bload(rs(hb.c_mask), boff(ok, ci));
     const float ad = bload(rs(hb.a_den), boff(jok, col));
     const __amdgpu_buffer_rsrc_t rg = rs(hb.gpol);
-    const float g0 = bload(rg, boff(rok, m));
-    const float g1 = bload(rg, boff(rok, B + m));
+    const float g0 = bload(rg, boff(rok && pol, m));
+    const float g1 = bload(rg, boff(rok && pol, B + m));
     const float alpha = bload(rs(hb.alpha), 0u);
-    // partials [critic][row][action][tq] (host: tq <= 16, tq % 4 == 0): 4 float4 per critic
-    const __amdgpu_buffer_rsrc_t rp = rs(hb.part);
-    float4 v0[4], v1[4];
+    const float eps = hb.ctl != nullptr ? bload(rs(reinterpret_cast<const float*>(hb.ctl)),
+                                               (uint32_t)offsetof(Ctl, epsilon)) : 0.f;
+    // partials [critic][row][action][tq] (policy rows, tq <= 16) or [expert row][action][tqm]
+    // (expert rows, tqm <= 32), both multiples of 4: float4 loads, all issued together
+    const __amdgpu_buffer_rsrc_t rp = rs(hb.part), rm = rs(hb.mpart);
+    const int tq = hb.tq, tqm = hb.tqm, e = m - B;
+    float4 v0[4], v1[4], vm[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const bool iok = ok && 4 * i < tq;
+        const bool iok = ok && pol && 4 * i < tq;
         v0[i] = bload4(rp, boff(iok, (m * A + col) * tq + 4 * i));
         v1[i] = bload4(rp, boff(iok, ((B + m) * A + col) * tq + 4 * i));
     }
-    float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vm[i] = bload4(rm, boff(ok && !pol && 4 * i < tqm, (e * A + col) * tqm + 4 * i));
+    float p0 = 0.f, p1 = 0.f, pm = 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         p0 = p0 + v0[i].x; p0 = p0 + v0[i].y; p0 = p0 + v0[i].z; p0 = p0 + v0[i].w;
         p1 = p1 + v1[i].x; p1 = p1 + v1[i].y; p1 = p1 + v1[i].z; p1 = p1 + v1[i].w;
     }
-    const float c = -alpha * (1.f / (float)B);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        pm = pm + vm[i].x; pm = pm + vm[i].y; pm = pm + vm[i].z; pm = pm + vm[i].w;
+    }
+    const float c = -(1.f - eps) * alpha * (1.f / (float)B);
     float gx = 0.f, dl = 0.f;
     if (jok) {
-        const float ga = (g0 * p0 + g1 * p1) / ad;
+        const float ga = (pol ? g0 * p0 + g1 * p1 : pm) / ad;
         gx = ga * hb.lim * (1.f - ct * ct);
-        gx = gx - (2.f * c) * ct;
+        if (pol) gx = gx - (2.f * c) * ct;
         dl = (gx * sd) * u;
-        dl = dl + c;
+        if (pol) dl = dl + c;
         dl = dl * mk;
     }
     // per_state_std: the logstd rows' gradients follow the mean rows (column A + j <- lane j)

@@ -303,6 +303,7 @@ void build_layout(sacx_handle* h) {
     h->add("ws.lp", 1, B, F, 0);
     h->add("ws.gp", 2, B, F, 0);                 // policy-row output gradients of q0, q1
     h->add("ws.apart", 2 * B, ((H0 + 15) / 16) * A, F, 0);   // their action-gradient partials (folded head bwd)
+    h->add("ws.mpart", ne1, ((Hm0 + 15) / 16) * A, F, 0);       // the expert rows' ones (SAC-EO, model.bwd1)
     h->add("ws.ones", 1, std::max(std::max(Rb, B), std::max(1, h->mb)) + 4, F, SACX_ROLE_STATE);
     h->add("ws.Hm1", ne1, Hm0, F, 0);
     h->add("ws.Hm2", ne1, Hm1, F, 0);
@@ -669,7 +670,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // by default: there the launches are bound by workgroup residency, not by their number, and
     // the folds' extra work loses (HC 8 seeds, A/B x2: both on 42.3k, hbw fold only 43.4k, head
     // partials only 43.1k, both off 43.9k updates/s; tools/pk_ab.sh).
-    const bool fold_hbw = !eo && Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
+    const bool fold_hbw = Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
+                          (!eo || (Hm0 <= 512 && Hm0 % 64 == 0)) &&
                           (fhb ? std::atoi(fhb) != 0 : h->tile32 == 0);
     // ---- actor head
     if (fuse_head) {
@@ -911,7 +913,20 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 pd.push_back(prob_dx(Dm2 + (size_t)k * half * Hm1, mrows, Hm1, W(n + ".l1"), Hm0,
                                      Hm1b + (size_t)k * half * Hm0, Dm1 + (size_t)k * half * Hm0, m0));
             }
+            if (fold_hbw) {                  // partial action gradients of the expert rows instead of Dm1
+                const int tqm = (Hm0 + 15) / 16;
+                for (int k = 0; k < nm; ++k) {
+                    GemmProb& p = pd[k];
+                    p.pw = W("m" + std::to_string(k) + ".l0") + (size_t)S * Hm0;   // action rows of W_ext
+                    p.pw_ld = Hm0;
+                    p.pw_cs = 1;
+                    p.pw_n = A;
+                    p.ppart = W("ws.mpart") + (size_t)k * half * A * tqm;
+                    p.C = nullptr;
+                }
+            }
             add_gemm(h, plan, "model.bwd1", pd, record_probs);
+            if (fold_hbw) plan.back().gemm.rowk = 2;   // DX with the partial epilogue (no q-head rows)
         }
     }
     // ---- actor backward
@@ -933,6 +948,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.alpha = W("alpha");
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
         b.Da3 = Da3; b.E = E; b.Da2 = Da2;
+        b.ne = ne; b.tqm = (Hm0 + 15) / 16; b.mpart = eo ? W("ws.mpart") : nullptr; b.ctl = eo ? h->ctl() : nullptr;
         L.flops += 2.0 * B * 2 * H0 * A + 2.0 * Rb * H1 * Aout;
         L.bytes += 4.0 * (2.0 * B * tq * A + 2.0 * Rb * H1);
     }

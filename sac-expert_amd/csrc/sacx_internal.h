@@ -118,8 +118,15 @@ struct HeadBwdArgs {
     const float* gpol;      // [2, B] output gradients of q0, q1 (the partials are unscaled)
     const float* a_den;
     const float* alpha;
-    const float *c_t, *c_std, *c_u, *c_mask;   // backward cache rows [0, B)
+    const float *c_t, *c_std, *c_u, *c_mask;   // backward cache rows [0, B + ne)
     float* Da3; float* E; float* Da2;
+    // SAC-EO: rows [B, B + ne) are the expert rows, whose action gradient comes through their
+    // world model's layer-0 action rows: partials [ne, A, tqm] written by model.bwd1 (unscaled
+    // by any output gradient: the model head's MSE gradient already carries epsilon); the
+    // policy rows' alpha term takes (1 - epsilon) (SAC_expert.py:305-338)
+    int32_t ne, tqm;
+    const float* mpart;
+    const Ctl* ctl;         // epsilon (use_expert)
 };
 
 struct FinalArgs {
