@@ -657,7 +657,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // Packed seeds (>= 4) keep the separate launch: the prologue recomputes each tile's 16 rows
     // once per column tile, which a full GPU of seeds pays for (measured 34.3k vs 31.6k updates/s
     // at 8 seeds); one seed gains the launch it saves.
-    const bool fuse_head = !eo && Aout <= 16 && S + A <= 64 && H1 % 16 == 0 && H1 <= 512 &&
+    // SAC-EO as well: the expert rows (sample -> the world models' inputs Xm) ride as row
+    // workgroups of q.fwd0, and the models' forward shifts one launch later (layer 0 in q.fwd1,
+    // layer 1 in pi.q.fwd0, the MSE head in pi.q.fwd1)
+    const bool fuse_head = Aout <= 16 && S + A <= 64 && H1 % 16 == 0 && H1 <= 512 &&
                            (fh ? std::atoi(fh) != 0 : h->seeds < 4);
     HeadArgs head_fused{};
     // actor.head.bwd folded into actor.bwd1 (plain SAC; the expert rows' model gradients keep
@@ -689,6 +692,12 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         a.total_rows = h->Ra;
         a.cache_row0 = 1 << 30;             // no backward cache from these rows (target, alpha)
         a.cache_row1 = 1 << 30;
+        if (eo) {                           // SAC-EO expert rows: sample() into Xm, cached
+            a.nseg = 2;
+            a.seg[1] = {2 * B, 2 * B + ne, 1, 0, noise_e, Xm, nullptr};
+            a.cache_row0 = B;
+            a.cache_row1 = h->Ra;
+        }
         a.c_t = W("ws.c_t"); a.c_std = W("ws.c_std"); a.c_u = W("ws.c_u"); a.c_mask = W("ws.c_mask");
         a.alpha_mode = 0;
     } else {
@@ -730,11 +739,19 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         Launch& L = plan.back();
         L.gemm.rowk = 3;
         L.gemm.head = head_fused;
-        L.gemm.head_block0 = ((h->Ra + 3) & ~3) / 4;
-        L.gemm.row_blocks = 0;              // + the alpha rows when merged_body folds them in
+        L.gemm.head_block0 = eo ? (2 * B) / 4 : ((h->Ra + 3) & ~3) / 4;
+        L.gemm.row_blocks = eo ? (h->Ra + 3) / 4 - (2 * B) / 4 : 0;   // + the alpha rows (merged_body)
+        L.grid += L.gemm.row_blocks;
         L.flops += 2.0 * B * H1 * Aout;
         L.bytes += 4.0 * B * (H1 + 6.0 * A);
         L.frees_slot = true;
+        if (eo) {                           // the models' layer 0 on Xm (written by the rows above)
+            for (int k = 0; k < nm; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                p1.push_back(prob_fwd(Xm + (size_t)k * half * ldQ, ldQ, mrows, S + A, W(n + ".l0"), Hm0,
+                                      Hm1b + (size_t)k * half * Hm0, m0));
+            }
+        }
         add_gemm(h, plan, "q.fwd1", p1, record_probs);
     } else {
         std::vector<GemmProb> p0, p1;
@@ -847,9 +864,17 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 pm.push_back(p);
             }
         }
+        if (eo && fuse_head) {               // the models' layer 1 on Hm1 (from q.fwd1)
+            for (int k = 0; k < nm; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                p0.push_back(prob_fwd(Hm1b + (size_t)k * half * Hm0, Hm0, mrows, Hm0, W(n + ".l1"), Hm1,
+                                      Hm2b + (size_t)k * half * Hm1, m1));
+            }
+        }
         fwd_pair("pi.q.fwd", p0, p1);
-        if (eo) {                            // plan.back() is pi.q.fwd1: fold into pi.q.fwd0
-            Launch& F0 = plan[plan.size() - 2];
+        if (eo) {                            // plan.back() is pi.q.fwd1: fold into pi.q.fwd0 (or, with
+                                             // the fused head, into pi.q.fwd1: Hm2 comes from pi.q.fwd0)
+            Launch& F0 = plan[plan.size() - (fuse_head ? 1 : 2)];
             std::vector<Launch> one;
             add_gemm(h, one, "model.head", pm, false);
             h->probs_cursor -= (int)pm.size();
