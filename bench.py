@@ -274,15 +274,16 @@ def drop_in_loop(eng, cfgd, n=300):
     reference's SAC_exp.train calls _update at SAC_expert.py:780): per iteration the
     behaviour action of one observation comes back to the host (actor.sample, B=1), one
     transition is appended to the device ring, and step(1) runs one update."""
-    import torch
     S, A = cfgd["S"], cfgd["A"]
-    obs = torch.randn(1, S, device=eng.device)
-    row = lambda k: torch.randn(1, k, device=eng.device)
+    rs = np.random.RandomState(0)
+    obs = [rs.normal(size=S).astype(np.float32) for _ in range(16)]   # a gym env's host arrays
+    r1, d1 = np.zeros(1, np.float32), np.zeros(1, np.float32)
     eng.prepare(1)
 
     def it(j):
-        a = eng.act(obs, deterministic=False).cpu()          # host env gets the action
-        eng.append(obs, a, torch.zeros(1), row(S), torch.zeros(1))
+        o, o2 = obs[j % 16], obs[(j + 1) % 16]
+        a = eng.act_host(o, deterministic=False)               # host env gets the action
+        eng.append(o[None], a[None], r1, o2[None], d1)         # the transition, from the host
         eng.step(1, num_timesteps=j, ts_increment=1)
     for j in range(10):
         it(j)
@@ -293,7 +294,7 @@ def drop_in_loop(eng, cfgd, n=300):
     eng.sync()
     el = time.perf_counter() - t0
     return {"updates_per_s": round(n / el, 1), "us_per_iteration": round(el / n * 1e6, 2), "iterations": n,
-            "iteration": "act(1 obs, stochastic) -> host, append(1 transition), step(1)"}
+            "iteration": "act(1 host obs, stochastic) -> host action, append(1 host transition), step(1)"}
 
 
 def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):

@@ -158,6 +158,9 @@ struct sacx_handle {
     std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;   // (G, with_rng, skipped kind)
     std::vector<std::pair<RollKey, hipGraphExec_t>> roll_graphs;     // sacx_rollout replays
     std::vector<hipEvent_t> events;
+    float* pin = nullptr;            // pinned host staging (STAGE_CAP floats), the _host entry points
+    hipEvent_t pin_ev = nullptr;     // the last host-to-device copy out of it
+    bool pin_pending = false;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
 
     uint64_t add(const std::string& name, int64_t rows, int64_t cols, int dtype, int role) {
@@ -196,6 +199,7 @@ int fail(sacx_handle* h, const std::string& msg) {
     } while (0)
 
 constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
+constexpr int STAGE_CAP = 1 << 16;   // floats in the host-transfer staging buffers (pinned + ws.stage)
 constexpr int ROLL_CAP = 4096;  // trajectories per sacx_rollout launch chain
 
 void build_layout(sacx_handle* h) {
@@ -319,6 +323,7 @@ void build_layout(sacx_handle* h) {
     h->alias("ws.Hl2", oHa2 + (uint64_t)Ra4 * H1 * 4, B, H1, F, 0);
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
+    h->add("ws.stage", 1, STAGE_CAP, F, 0);              // host-pointer entry points: device side
     h->add("act.H1", ACT_CAP, H0, F, 0);
     h->add("act.H2", ACT_CAP, H1, F, 0);
     h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
@@ -1620,6 +1625,8 @@ void sacx_destroy(sacx_handle* h) {
     if (h->mgraph) (void)hipGraphExecDestroy(h->mgraph);
     for (auto& kv : h->roll_graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : h->events) (void)hipEventDestroy(e);
+    if (h->pin) (void)hipHostFree(h->pin);
+    if (h->pin_ev) (void)hipEventDestroy(h->pin_ev);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
     if (h->comm) (void)ncclCommDestroy(h->comm);
@@ -1758,6 +1765,70 @@ int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const flo
     g.s = s; g.a = a; g.r = r; g.sp = sp; g.d = d; g.n = n; g.ctl = h->ctl();
     launch_append(g, h->stream);
     HIPCHK(h, hipGetLastError());
+    return 0;
+}
+
+// Host-pointer variants for the env loop (one transition / one observation per call): the
+// rows go through one pinned buffer and ONE asynchronous copy on the handle's stream.
+static int stage_begin(sacx_handle* h) {
+    if (!h->pin) {
+        HIPCHK(h, hipHostMalloc((void**)&h->pin, sizeof(float) * STAGE_CAP, hipHostMallocDefault));
+        HIPCHK(h, hipEventCreateWithFlags(&h->pin_ev, hipEventDisableTiming));
+    }
+    if (h->pin_pending) HIPCHK(h, hipEventSynchronize(h->pin_ev));   // the previous copy has left it
+    h->pin_pending = false;
+    return 0;
+}
+
+static int stage_push(sacx_handle* h, size_t nfloat) {
+    HIPCHK(h, hipMemcpyAsync(h->f("ws.stage"), h->pin, sizeof(float) * nfloat, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
+    h->pin_pending = true;
+    return 0;
+}
+
+int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, const float* r, const float* sp,
+                            const float* d, int64_t n) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n <= 0) return 0;
+    if (!s || !a || !r || !sp || !d) return fail(h, "null row pointer");
+    const int S = h->S, A = h->A;
+    const int64_t per = 2 * S + A + 2, chunk = STAGE_CAP / per;
+    for (int64_t done = 0; done < n; done += chunk) {
+        const int64_t m = std::min(chunk, n - done);
+        if (stage_begin(h)) return -1;
+        float* p = h->pin;
+        std::memcpy(p, s + done * S, sizeof(float) * m * S);
+        std::memcpy(p + m * S, a + done * A, sizeof(float) * m * A);
+        std::memcpy(p + m * (S + A), r + done, sizeof(float) * m);
+        std::memcpy(p + m * (S + A + 1), sp + done * S, sizeof(float) * m * S);
+        std::memcpy(p + m * (2 * S + A + 1), d + done, sizeof(float) * m);
+        if (stage_push(h, (size_t)(m * per))) return -1;
+        const float* g = h->f("ws.stage");
+        const int rc = sacx_buffer_append(h, g, g + m * S, g + m * (S + A), g + m * (S + A + 1), g + m * (2 * S + A + 1), m);
+        if (rc) return rc;
+    }
+    return 0;
+}
+
+int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
+    const int S = h->S, A = h->A;
+    const int64_t chunk = std::min<int64_t>(ACT_CAP, STAGE_CAP / (S + A));
+    for (int64_t done = 0; done < n; done += chunk) {
+        const int64_t m = std::min(chunk, n - done);
+        if (stage_begin(h)) return -1;
+        std::memcpy(h->pin, obs + done * S, sizeof(float) * m * S);
+        if (stage_push(h, (size_t)(m * S))) return -1;
+        float* g = h->f("ws.stage");
+        const int rc = sacx_actor_act(h, g, m, deterministic, g + m * S);
+        if (rc) return rc;
+        HIPCHK(h, hipMemcpyAsync(h->pin + m * S, g + m * S, sizeof(float) * m * A, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->pin_pending = false;
+        std::memcpy(act_out + done * A, h->pin + m * S, sizeof(float) * m * A);
+    }
     return 0;
 }
 

@@ -24,7 +24,7 @@ STAT_NAMES = ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss",
 # every symbol include/sacx.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "sacx_create", "sacx_destroy", "sacx_last_error", "sacx_arena_bytes", "sacx_layout", "sacx_bind",
-    "sacx_buffer_append", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
+    "sacx_buffer_append", "sacx_buffer_append_host", "sacx_actor_act_host", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
     "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
@@ -139,6 +139,8 @@ def lib():
         "sacx_profile": (ctypes.c_int, [vp, i64, P(f64), i32]),
         "sacx_time_graph": (ctypes.c_int, [vp, i64, ctypes.c_char_p, P(f64)]),
         "sacx_actor_act": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+        "sacx_buffer_append_host": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64]),
+        "sacx_actor_act_host": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sacx_actor_evaluate": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "sacx_critic_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, i32, vp]),
         "sacx_model_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, f32, f32, vp, vp, vp]),

@@ -305,10 +305,26 @@ class Engine:
         t = torch.as_tensor(x, dtype=torch.float32, device=self.device).reshape(shape).contiguous()
         return t
 
+    @staticmethod
+    def _is_host(x) -> bool:
+        return not (torch.is_tensor(x) and x.is_cuda)
+
+    @staticmethod
+    def _host_f32(x, shape) -> np.ndarray:
+        xv = x.detach().cpu().numpy() if torch.is_tensor(x) else x
+        return np.ascontiguousarray(np.asarray(xv, dtype=np.float32).reshape(shape))
+
     def append(self, s, a, r, sp, d):
         """TrajectoryBuffer.add (buffers.py:41-71) into the device ring."""
         n = int(np.shape(r)[0]) if not torch.is_tensor(r) else int(r.shape[0])
         S, A = self.cfg.s_dim, self.cfg.a_dim
+        if all(self._is_host(x) for x in (s, a, r, sp, d)):
+            # env-loop transitions: one pinned staging copy inside the library
+            hs = [self._host_f32(s, (n, S)), self._host_f32(a, (n, A)), self._host_f32(r, (n,)),
+                  self._host_f32(sp, (n, S)), self._host_f32(d, (n,))]
+            N.check(self.lib.sacx_buffer_append_host(self.h, *[x.ctypes.data for x in hs], n),
+                    self.h, "buffer_append_host")
+            return n
         ts = [self._dev(s, (n, S)), self._dev(a, (n, A)), self._dev(r, (n,)), self._dev(sp, (n, S)),
               self._dev(d, (n,))]
         N.check(self.lib.sacx_buffer_append(self.h, *[ctypes.c_void_p(t.data_ptr()) for t in ts], n),
@@ -339,6 +355,18 @@ class Engine:
         N.check(self.lib.sacx_actor_act(self.h, ctypes.c_void_p(o.data_ptr()), n, int(bool(deterministic)),
                                         ctypes.c_void_p(out.data_ptr())), self.h, "actor_act")
         self._keep_act = o
+        return out[0] if single else out
+
+    def act_host(self, obs, deterministic: bool = True) -> np.ndarray:
+        """SquashedGaussianActor.sample for the env loop: host obs [n, S] or [S] -> host actions
+        [n, A] ([A] for one row), as the reference hands env.step a NumPy action
+        (sac_eo/algs/SAC_expert.py:585-605).  One pinned copy each way inside the library."""
+        S, A = self.cfg.s_dim, self.cfg.a_dim
+        single = np.ndim(obs) == 1 if not torch.is_tensor(obs) else obs.dim() == 1
+        o = self._host_f32(obs, (-1, S))
+        out = np.empty((o.shape[0], A), dtype=np.float32)
+        N.check(self.lib.sacx_actor_act_host(self.h, o.ctypes.data, int(o.shape[0]), int(bool(deterministic)),
+                                             out.ctypes.data), self.h, "actor_act_host")
         return out[0] if single else out
 
     def evaluate(self, s):

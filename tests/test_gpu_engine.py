@@ -56,16 +56,23 @@ def test_rng_big_draws(gpu_available):
     eng.close()
 
 
-def test_replay_ring_fifo(gpu_available):
-    """TrajectoryBuffer.add truncation (buffers.py:60-66) on the device ring."""
+@pytest.mark.parametrize("host", [True, False])
+def test_replay_ring_fifo(gpu_available, host):
+    """TrajectoryBuffer.add truncation (buffers.py:60-66) on the device ring, from host rows
+    (sacx_buffer_append_host: pinned staging, chunked at 64 Ki floats -- the 7000-row add
+    spans two chunks) and from device rows (sacx_buffer_append)."""
+    import torch
     from sac_eo.engine import Engine, EngineConfig
     eng = Engine(EngineConfig(s_dim=3, a_dim=2, hidden=(16, 16), batch=4, buffer_capacity=10))
     rs = np.random.RandomState(0)
     ref = {k: np.zeros((0,) + sh, np.float32) for k, sh in (("s", (3,)), ("a", (2,)), ("r", ()), ("sp", (3,)), ("d", ()))}
-    for n in (4, 5, 3, 12, 1):
+    for n in (4, 5, 3, 12, 1, 7000, 2):
         rows = dict(s=rs.normal(size=(n, 3)), a=rs.normal(size=(n, 2)), r=rs.normal(size=n),
                     sp=rs.normal(size=(n, 3)), d=(rs.uniform(size=n) < .5).astype(np.float64))
-        eng.append(rows["s"], rows["a"], rows["r"], rows["sp"], rows["d"])
+        args = [rows[k] for k in ("s", "a", "r", "sp", "d")]
+        if not host:
+            args = [torch.as_tensor(x, dtype=torch.float32, device=eng.device) for x in args]
+        eng.append(*args)
         for k in ref:
             ref[k] = np.concatenate([ref[k], rows[k].astype(np.float32)])[-10:]
     c = eng.ctl()
@@ -271,9 +278,11 @@ def test_model_fit_matches_oracle(gpu_available, eager):
     eng.close()
 
 
-@pytest.mark.parametrize("deterministic,per_state_std,n", [(True, False, 37), (False, False, 37), (False, True, 5),
-                                                           (False, False, 1)])
-def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n):
+@pytest.mark.parametrize("deterministic,per_state_std,n,host", [(True, False, 37, False), (False, False, 37, False),
+                                                                (False, True, 5, False), (False, False, 1, False),
+                                                                (False, False, 1, True), (True, False, 37, True),
+                                                                (False, True, 3000, True)])
+def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n, host):
     """Behaviour-policy inference (sample(), continuous_actors.py:270-306) vs the oracle;
     the stochastic draw advances the device stream exactly as np.random.normal(size=(n, A))."""
     eng, ocfg, st, buf, nrm, _ = make_pair(act="tanh", B=64, seed=41, normalizers="random",
@@ -282,7 +291,10 @@ def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n
     obs = np.random.RandomState(3).normal(size=(n, S)) * 2.0
     eng.rng_set_state(np.random.RandomState(17).get_state())
     ref_rs = np.random.RandomState(17)
-    got = eng.act(obs[0] if n == 1 else obs, deterministic).cpu().numpy().reshape(n, A)
+    if host:    # sacx_actor_act_host: host rows in and out (3000 rows span 3 ACT_CAP chunks)
+        got = np.asarray(eng.act_host(obs[0] if n == 1 else obs, deterministic)).reshape(n, A)
+    else:
+        got = eng.act(obs[0] if n == 1 else obs, deterministic).cpu().numpy().reshape(n, A)
     x = (obs.astype(np.float32) - nrm.s_mean) / nrm.s_den
     out, _ = O.mlp_forward(st.actor, x.astype(np.float64), ocfg.act)
     mu, lraw = O.split_head(out, st.logstd, ocfg)
