@@ -194,13 +194,14 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
 
 /* --- host-pointer forms for the env loop (SAC_exp.train, sac_eo/algs/SAC_expert.py:585-605:
  * one host observation -> actor.sample -> env.step -> buffer.add per timestep) -------------- */
-/* sacx_buffer_append with HOST rows: packed into a library-owned pinned buffer and sent in one
- * asynchronous copy on the bound stream (chunked above 64 Ki floats).  Returns once the rows
- * are in the pinned buffer; the caller's arrays may be reused immediately. */
+/* sacx_buffer_append with HOST rows: packed into a library-owned pinned, device-mapped buffer
+ * that k_append reads in place (no DMA copy; chunked above 64 Ki floats).  Asynchronous: returns
+ * once the rows are packed, so the caller's arrays may be reused immediately. */
 int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, const float* r,
                             const float* sp, const float* d, int64_t n);
-/* sacx_actor_act with HOST obs[n,S] in and HOST act_out[n,A] out.  Synchronous: waits for the
- * bound stream (and so for any queued update) before returning the actions. */
+/* sacx_actor_act with HOST obs[n,S] in and HOST act_out[n,A] out, through the same mapped
+ * buffer (the normaliser reads obs and the head writes actions in place).  Synchronous: waits
+ * for the bound stream (and so for any queued update) before returning the actions. */
 int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
 
 /* --- the reference objects' standalone network calls (device rows in, device rows out) -- */

@@ -159,7 +159,8 @@ struct sacx_handle {
     std::vector<std::pair<RollKey, hipGraphExec_t>> roll_graphs;     // sacx_rollout replays
     std::vector<hipEvent_t> events;
     float* pin = nullptr;            // pinned host staging (STAGE_CAP floats), the _host entry points
-    hipEvent_t pin_ev = nullptr;     // the last host-to-device copy out of it
+    float* pin_dev = nullptr;        // its device-side address (kernels read / write it in place)
+    hipEvent_t pin_ev = nullptr;     // the last kernel that reads it
     bool pin_pending = false;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
 
@@ -199,7 +200,7 @@ int fail(sacx_handle* h, const std::string& msg) {
     } while (0)
 
 constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
-constexpr int STAGE_CAP = 1 << 16;   // floats in the host-transfer staging buffers (pinned + ws.stage)
+constexpr int STAGE_CAP = 1 << 16;   // floats in the pinned host staging buffer of the _host entry points
 constexpr int ROLL_CAP = 4096;  // trajectories per sacx_rollout launch chain
 
 void build_layout(sacx_handle* h) {
@@ -323,7 +324,6 @@ void build_layout(sacx_handle* h) {
     h->alias("ws.Hl2", oHa2 + (uint64_t)Ra4 * H1 * 4, B, H1, F, 0);
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
-    h->add("ws.stage", 1, STAGE_CAP, F, 0);              // host-pointer entry points: device side
     h->add("act.H1", ACT_CAP, H0, F, 0);
     h->add("act.H2", ACT_CAP, H1, F, 0);
     h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
@@ -1768,22 +1768,18 @@ int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const flo
     return 0;
 }
 
-// Host-pointer variants for the env loop (one transition / one observation per call): the
-// rows go through one pinned buffer and ONE asynchronous copy on the handle's stream.
+// Host-pointer variants for the env loop (one transition / one observation per call).  The
+// rows go into one pinned, device-mapped buffer that the kernels read (k_append, the obs
+// normaliser) and write (the action head) in place over PCIe: no DMA copy on either side,
+// whose fixed cost exceeds the whole transfer at these sizes.
 static int stage_begin(sacx_handle* h) {
     if (!h->pin) {
-        HIPCHK(h, hipHostMalloc((void**)&h->pin, sizeof(float) * STAGE_CAP, hipHostMallocDefault));
+        HIPCHK(h, hipHostMalloc((void**)&h->pin, sizeof(float) * STAGE_CAP, hipHostMallocMapped));
+        HIPCHK(h, hipHostGetDevicePointer((void**)&h->pin_dev, h->pin, 0));
         HIPCHK(h, hipEventCreateWithFlags(&h->pin_ev, hipEventDisableTiming));
     }
-    if (h->pin_pending) HIPCHK(h, hipEventSynchronize(h->pin_ev));   // the previous copy has left it
+    if (h->pin_pending) HIPCHK(h, hipEventSynchronize(h->pin_ev));   // its last reader has finished
     h->pin_pending = false;
-    return 0;
-}
-
-static int stage_push(sacx_handle* h, size_t nfloat) {
-    HIPCHK(h, hipMemcpyAsync(h->f("ws.stage"), h->pin, sizeof(float) * nfloat, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
-    h->pin_pending = true;
     return 0;
 }
 
@@ -1803,10 +1799,11 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
         std::memcpy(p + m * (S + A), r + done, sizeof(float) * m);
         std::memcpy(p + m * (S + A + 1), sp + done * S, sizeof(float) * m * S);
         std::memcpy(p + m * (2 * S + A + 1), d + done, sizeof(float) * m);
-        if (stage_push(h, (size_t)(m * per))) return -1;
-        const float* g = h->f("ws.stage");
+        const float* g = h->pin_dev;
         const int rc = sacx_buffer_append(h, g, g + m * S, g + m * (S + A), g + m * (S + A + 1), g + m * (2 * S + A + 1), m);
         if (rc) return rc;
+        HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
+        h->pin_pending = true;
     }
     return 0;
 }
@@ -1820,13 +1817,9 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
         const int64_t m = std::min(chunk, n - done);
         if (stage_begin(h)) return -1;
         std::memcpy(h->pin, obs + done * S, sizeof(float) * m * S);
-        if (stage_push(h, (size_t)(m * S))) return -1;
-        float* g = h->f("ws.stage");
-        const int rc = sacx_actor_act(h, g, m, deterministic, g + m * S);
+        const int rc = sacx_actor_act(h, h->pin_dev, m, deterministic, h->pin_dev + m * S);
         if (rc) return rc;
-        HIPCHK(h, hipMemcpyAsync(h->pin + m * S, g + m * S, sizeof(float) * m * A, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
-        h->pin_pending = false;
         std::memcpy(act_out + done * A, h->pin + m * S, sizeof(float) * m * A);
     }
     return 0;
