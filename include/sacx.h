@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 4
+#define SACX_ABI_VERSION 5
 
 typedef struct sacx_handle sacx_handle;
 
@@ -100,6 +100,9 @@ typedef struct sacx_config {
     int32_t act_layers[3][2];   /* [actor | critics | world models][hidden layer 0, 1]: a sacx_activation
                                    value; the --actor_activations / --critic_activations / --model_activations
                                    lists of nn_utils.py:5-22 */
+    /* --- ABI 5 --- */
+    float delta_clip_pred;      /* --delta_clip_pred: MSEModel.sample clips the normalised delta prediction
+                                   (base_world_model.py:80-82) in the SAC-EO expert term; <= 0: None */
 } sacx_config;
 
 typedef struct sacx_segment {

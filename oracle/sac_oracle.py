@@ -78,6 +78,7 @@ class Config:
     model_act: str = "relu"
     lr_model: float = 1e-3
     reward_loss_coef: float = 1.0
+    delta_clip_pred: float = 0.0  # --delta_clip_pred (base_world_model.py:80-82); 0: None
 
     @property
     def aacts(self):
@@ -518,9 +519,17 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
             ca, cache_e = head_sample(mu_e, ls_e, ne, lim, dt)
             xm = np.concatenate([se_n, _norm(ca, nrm.a_mean, nrm.a_den)], axis=1)
             om, hsm = mlp_forward(st.models[k], xm, cfg.model_act)
-            sp_hat = se + (om[:, :S] * nrm.d_den + nrm.d_mean)
+            dn = om[:, :S]
+            dpass = np.ones_like(dn)
+            if cfg.delta_clip_pred:
+                # MSEModel.sample -> _forward(clip=True): tf.clip_by_value, whose gradient is zero
+                # outside [-c, c] and passes at the bounds (TF _ClipByValueGrad)
+                c = F(cfg.delta_clip_pred)
+                dpass = ((dn >= -c) & (dn <= c)).astype(dt)
+                dn = np.minimum(np.maximum(dn, -c), c)
+            sp_hat = se + (dn * nrm.d_den + nrm.d_mean)
             diffs.append(spe - sp_hat)
-            caches.append((se_n, hs_e, cache_e, xm, hsm, spe, sp_hat))
+            caches.append((se_n, hs_e, cache_e, xm, hsm, spe, sp_hat, dpass))
         if len(diffs) == 2:
             dl_e = F(0.5) * ((diffs[0] ** 2).sum(-1) + (diffs[1] ** 2).sum(-1))
         else:
@@ -528,10 +537,12 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
         mse = np.mean(dl_e)
         p_loss = (F(1) - eps) * p_loss + eps * mse
         ne_half = diffs[0].shape[0]
-        for k, (se_n, hs_e, cache_e, xm, hsm, spe, sp_hat) in enumerate(caches):
+        for k, (se_n, hs_e, cache_e, xm, hsm, spe, sp_hat, dpass) in enumerate(caches):
             dsp = -eps * F(1.0 / ne_half) * diffs[k]
             dout = np.zeros((ne_half, S + 1), dt)
-            dout[:, :S] = dsp * nrm.d_den
+            dout[:, :S] = dsp * nrm.d_den * dpass
+            if keep is not None:
+                keep["clip_frac%d" % k] = float(1.0 - dpass.mean())
             _, dxm = mlp_backward(st.models[k], xm, hsm, dout, cfg.model_act,
                                   need_dx=True, need_dw=False)
             dca = dxm[:, S:] / nrm.a_den

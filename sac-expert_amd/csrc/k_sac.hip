@@ -901,7 +901,10 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         }
         if constexpr (MODE == GM_FWD) {
             if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
-                const float pred = v + e0[s];
+                float pred = v + e0[s];
+                // --delta_clip_pred (base_world_model.py:80-82): clip, no gradient outside [-c, c]
+                const bool pass = g.dclip <= 0.f || (pred >= -g.dclip && pred <= g.dclip);
+                if (g.dclip > 0.f) pred = fminf(fmaxf(pred, -g.dclip), g.dclip);
                 const float sp_hat = e1[s] + (pred * e4[s] + e3[s]);
                 const float diff = e2[s] - sp_hat;
                 const float gscale = -es.eps * g.grad_scale;
@@ -911,7 +914,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 sq += __shfl_xor(sq, 2, 16);
                 sq += __shfl_xor(sq, 1, 16);
                 if (out_ok) {
-                    st_out(&g.C[(size_t)mm * g.ldc + nn], (gscale * diff) * e4[s]);
+                    st_out(&g.C[(size_t)mm * g.ldc + nn], pass ? (gscale * diff) * e4[s] : 0.f);
                     if (col == 0) st_out(&g.part[(size_t)mm * ((g.N + 15) >> 4) + 2 * tn + (s & 1)], sq);
                 }
                 continue;
@@ -1006,7 +1009,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                      "s"(g.pw), "s"(g.ppart), "s"(g.pw_ld), "s"(g.pw_cs), "s"(g.pw_n));
     } else if constexpr (MODE == GM_FWD) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
-                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.dclip), "s"(g.se_raw), "s"(g.spe_raw),
                      "s"(g.dmean), "s"(g.dden), "s"(g.headp), "s"(g.vec));
     } else if constexpr (MODE == GM_DX && ROWK == 2) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
@@ -1236,7 +1239,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     v = v + red[3][R][L];
     if constexpr (MODE == GM_FWD && ROWK != 3 && ROWK != 5) {
         if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
-            const float pred = v + e0;
+            float pred = v + e0;
+            // --delta_clip_pred (base_world_model.py:80-82): clip, no gradient outside [-c, c]
+            const bool pass = g.dclip <= 0.f || (pred >= -g.dclip && pred <= g.dclip);
+            if (g.dclip > 0.f) pred = fminf(fmaxf(pred, -g.dclip), g.dclip);
             const float sp_hat = e1 + (pred * e4 + e3);
             const float diff = e2 - sp_hat;
             const float gscale = -es.eps * g.grad_scale;
@@ -1246,7 +1252,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             sq += __shfl_xor(sq, 2, 16);
             sq += __shfl_xor(sq, 1, 16);
             if (!out_ok) return;
-            st_out(&g.C[(size_t)mm * g.ldc + nn], (gscale * diff) * e4);
+            st_out(&g.C[(size_t)mm * g.ldc + nn], pass ? (gscale * diff) * e4 : 0.f);
             if (col == 0) st_out(&g.part[(size_t)mm * g.tiles_n + tn], sq);
             return;
         }

@@ -863,6 +863,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 p.C = W("ws.dout") + (size_t)k * half * S; p.ldc = S;
                 p.epi = EPI_FWD; p.act = ACT_NONE;
                 p.mse = 1; p.grad_scale = 1.f / (float)mrows;       // MSE_loss = mean over the rows
+                p.dclip = h->cfg.delta_clip_pred > 0.f ? h->cfg.delta_clip_pred : 0.f;
                 p.se_raw = se_raw + (size_t)k * half * S; p.spe_raw = spe_raw + (size_t)k * half * S;
                 p.dmean = W("norm.d_mean"); p.dden = W("norm.d_den");
                 p.part = W("ws.mse") + (size_t)k * half * mtn;

@@ -84,6 +84,7 @@ struct GemmProb {
     // diff = sp_e - (s_e + out * d_den + d_mean); part[row * tiles_n + tn] = sum of diff^2 over
     // the tile's columns (row stride of se_raw / spe_raw is N)
     int32_t mse;
+    float dclip;            // --delta_clip_pred on `out` (clipped, zero gradient outside); 0: off
     const float *se_raw, *spe_raw, *dmean, *dden;
     float* part;
     // GM_FWD: the A operand's last columns [K - A, K) are the actor's evaluate() actions of the

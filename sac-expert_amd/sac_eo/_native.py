@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 4
+SACX_ABI_VERSION = 5
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1
@@ -76,6 +76,7 @@ class Config(ctypes.Structure):
         ("reward_clip_loss", ctypes.c_float),
         ("act_per_layer", ctypes.c_int32),
         ("act_layers", (ctypes.c_int32 * 2) * 3),
+        ("delta_clip_pred", ctypes.c_float),
     ]
 
 

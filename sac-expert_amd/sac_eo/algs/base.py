@@ -107,10 +107,8 @@ class SACBase:
             num_models=len(self.models) if self.use_expert else 2, actor_layer_norm=self.actor.layer_norm,
             model_max_grad_norm=float(self.model_max_grad_norm or 0.0),
             delta_clip_loss=float(self.models[0].delta_clip_loss or 0.0) if self.use_expert else 0.0,
-            reward_clip_loss=float(self.models[0].reward_clip_loss or 0.0) if self.use_expert else 0.0)
-        if self.use_expert and self.models[0].delta_clip_pred:
-            raise NotImplementedError("delta_clip_pred inside the SAC-EO update's expert term is not built "
-                                      "(the rollout, diagnostics and MSEModel calls take it)")
+            reward_clip_loss=float(self.models[0].reward_clip_loss or 0.0) if self.use_expert else 0.0,
+            delta_clip_pred=float(self.models[0].delta_clip_pred or 0.0) if self.use_expert else 0.0)
         eng = Engine(cfg)
         self.actor._bind(eng, "actor")
         for i, q in enumerate(self.q_critics):

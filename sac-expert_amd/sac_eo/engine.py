@@ -65,6 +65,7 @@ class EngineConfig:
     model_max_grad_norm: float = 0.0    # <= 0: None
     delta_clip_loss: float = 0.0        # <= 0: None
     reward_clip_loss: float = 0.0       # <= 0: None
+    delta_clip_pred: float = 0.0        # the expert term's MSEModel.sample clip; <= 0: None
     # per-layer activations (the reference's --actor_activations / --critic_activations /
     # --model_activations lists); None: `activation` / `model_activation` for every layer
     actor_activations: Optional[Sequence[str]] = None
@@ -107,6 +108,7 @@ class EngineConfig:
         c.model_max_grad_norm = float(self.model_max_grad_norm or 0.0)
         c.delta_clip_loss = float(self.delta_clip_loss or 0.0)
         c.reward_clip_loss = float(self.reward_clip_loss or 0.0)
+        c.delta_clip_pred = float(self.delta_clip_pred or 0.0)
         lists = (self.actor_activations, self.critic_activations, self.model_activations)
         if any(x is not None for x in lists):
             c.act_per_layer = 1

@@ -29,8 +29,9 @@ def test_struct_layouts():
     from sac_eo import _native as N
     # offsets fixed by include/sacx.h (natural alignment)
     assert N.Config.buffer_capacity.offset == 32
-    assert ctypes.sizeof(N.Config) == 200          # gcc: sizeof(sacx_config)
+    assert ctypes.sizeof(N.Config) == 208          # gcc: sizeof(sacx_config)
     assert N.Config.act_per_layer.offset == 172 and N.Config.act_layers.offset == 176
+    assert N.Config.delta_clip_pred.offset == 200
     assert N.Config.reward_loss_coef.offset == 128
     assert N.Config.gemm_bf16.offset == 132
     assert N.Config.seeds.offset == 136
@@ -103,3 +104,24 @@ def test_no_kernel_uses_kilobytes_of_scratch():
     assert len(sizes) > 50
     bad = {k: v for k, v in sizes.items() if v > 256}
     assert not bad, bad
+
+
+def test_config_layout_matches_gcc(tmp_path):
+    """Every sacx_config field offset of the ctypes mirror equals gcc's offsetof on include/sacx.h."""
+    import os
+    import shutil
+    import subprocess
+    from sac_eo import _native as N
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not on PATH")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    names = [f[0] for f in N.Config._fields_]
+    src = tmp_path / "lay.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "sacx.h"\nint main(void) {\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(sacx_config, {n}));\n' for n in names)
+                   + '  printf("%zu\\n", sizeof(sacx_config));\n  return 0;\n}\n')
+    exe = tmp_path / "lay"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)], text=True).split()]
+    want = [getattr(N.Config, n).offset for n in names] + [ctypes.sizeof(N.Config)]
+    assert got == want, list(zip(names + ["sizeof"], got, want))

@@ -211,3 +211,38 @@ def test_layer_norm_inference_paths(gpu_available):
         if name != "d":
             assert relerr(g, r) < 1e-4, name
     eng.close()
+
+
+@pytest.mark.parametrize("nm,dcp", [(1, 0.2), (2, 0.1)])
+def test_delta_clip_pred_update(gpu_available, nm, dcp):
+    """--delta_clip_pred in the SAC-EO expert term (MSEModel.sample -> _forward(clip=True),
+    base_world_model.py:80-82): the clipped prediction enters the MSE and its gradient is zero
+    outside [-c, c] (tf.clip_by_value).  c is chosen so that a part of the predictions clip."""
+    B, ne = 128, 20
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=23, use_expert=True, ne=ne,
+                                                normalizers="random", num_models=nm, delta_clip_pred=dcp)
+    ocfg.delta_clip_pred = dcp
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(92)
+    eng.rng_set_state(rs.get_state())
+    R = O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=ne, n_models=nm, gen=np.random.default_rng(29))
+    if nm == 2:
+        eng.push_perms(R["perm"][None, :])
+    keep = {}
+    ref = oracle_step(st, ocfg, nrm, buf, R, expert, keep)
+    frac = np.mean([keep["clip_frac%d" % k] for k in range(nm)])
+    assert 0.05 < frac < 0.95, frac          # both branches of the clip are exercised
+    eng.step(1, eager=True)
+    eng.sync()
+    row = eng.stats(1)[0]
+    for i, k in enumerate(("q1_loss", "q2_loss", "p_loss", "alpha_loss")):
+        assert abs(row[i] - ref[k]) <= 2e-5 * abs(ref[k]) + 1e-7, (k, row[i], ref[k])
+    assert abs(row[5] - ref["mse_loss"]) <= 2e-5 * abs(ref["mse_loss"])
+    m = eng.v["adam_m"][0]
+    for i in range(3):
+        seg = eng.segments[f"actor.l{i}"]
+        o, n = seg["offset"] // 4, seg["rows"] * seg["cols"]
+        gd = m[o:o + n].cpu().numpy().reshape(seg["rows"], seg["cols"]) / (np.float32(1) - np.float32(0.9))
+        assert relerr(gd[:-1], keep["actor_grads"][2 * i]) < 2e-4
+        assert relerr(gd[-1], keep["actor_grads"][2 * i + 1]) < 2e-4
+    eng.close()
