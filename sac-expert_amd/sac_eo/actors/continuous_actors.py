@@ -37,8 +37,9 @@ class GaussianActor:
         self.activations = list(activations)          # one name for all layers, or one per layer
         self.activation = self.activations[0]
         self.layer_norm = bool(layer_norm)
-        if output_norm and self.squash:
-            raise NotImplementedError("actor_output_norm of the squashed actor is not built (off by default)")
+        # SquashedGaussianActor.sample / evaluate (continuous_actors.py:270-379) never call
+        # _output_normalization, so the flag changes nothing on the squashed actor's SAC path; it is
+        # kept as an attribute and acts only on GaussianActor (its _forward, :97-98)
         self.output_norm = bool(output_norm)
         self.gain, self.init_type = gain, init_type
         self.per_state_std = bool(per_state_std)

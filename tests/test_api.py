@@ -34,6 +34,11 @@ def test_actor_weight_layout_matches_reference():
     g = init_actor(env, **dict(ak, actor_weights=w, actor_squash=False))
     assert type(g) is GaussianActor and not g.squash and isinstance(actor, SquashedGaussianActor)
     assert all(np.array_equal(a, b) for a, b in zip(g.get_weights(), w))
+    # --actor_output_norm: the reference's squashed sample / evaluate never apply it
+    # (continuous_actors.py:270-379), so the squashed actor accepts and ignores it
+    # (an init_actor keyword, init_actor.py:10; the reference parser has no flag for it)
+    sq = init_actor(env, **dict(ak, actor_weights=w, actor_squash=True, actor_output_norm=True))
+    assert sq.output_norm and isinstance(sq, SquashedGaussianActor)
 
 
 def test_critics_and_models_construction():
