@@ -1009,7 +1009,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                      "s"(g.pw), "s"(g.ppart), "s"(g.pw_ld), "s"(g.pw_cs), "s"(g.pw_n));
     } else if constexpr (MODE == GM_FWD) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
-                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.dclip), "s"(g.se_raw), "s"(g.spe_raw),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.bias), "s"(g.mse), "s"(g.se_raw), "s"(g.spe_raw),
                      "s"(g.dmean), "s"(g.dden), "s"(g.headp), "s"(g.vec));
     } else if constexpr (MODE == GM_DX && ROWK == 2) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
