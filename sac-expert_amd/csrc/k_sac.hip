@@ -358,23 +358,35 @@ __device__ float mean_rows(const float* x, int n) {
     return wave_sum(s) / (float)n;
 }
 
-// Lane-strided partial sums of x[0, n) in increasing i -- the order of mean_rows, so the
-// results are bit-identical -- with the first 4 chunks of 64 (n <= 256) loaded up front by
-// the caller (v0) and the remainder, if any, in further chunks.
-__device__ __forceinline__ float strided_rest(const float* x, int n, const float (&v0)[4]) {
+// Lane-strided partial sums of four row arrays at once, each in increasing i -- the order of
+// mean_rows, so the results are bit-identical -- in rounds of 4 chunks of 64 rows per array:
+// 16 loads in flight per round, one round for B <= 256 and four for Humanoid's B = 1,024.
+// (One array after the other, the dependent chunk loads made the folded alpha.final the
+// longest workgroup of its Humanoid launch.)
+__device__ __forceinline__ void strided_sums4(const float* const (&x)[4], const int (&n)[4], float (&s)[4]) {
     const int lane = threadIdx.x & 63;
-    float s = 0.f;
+    __amdgpu_buffer_rsrc_t r[4];
+    int nmax = 0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) s += v0[u];
-    for (int i = 256 + lane; i < n; i += 64) s += x[i];
-    return s;
-}
-
-__device__ __forceinline__ void strided_head(const float* x, int n, float (&v)[4]) {
-    const int lane = threadIdx.x & 63;
-    const __amdgpu_buffer_rsrc_t r = rs(x);
+    for (int a = 0; a < 4; ++a) {
+        r[a] = rs(x[a]);
+        s[a] = 0.f;
+        nmax = max(nmax, n[a]);
+    }
+    for (int base = 0; base < nmax; base += 256) {
+        float v[4][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = bload(r, boff(lane + 64 * u < n, lane + 64 * u));
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = base + lane + 64 * u;
+                v[a][u] = bload(r[a], boff(i < n[a], i));
+            }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int u = 0; u < 4; ++u) s[a] += v[a][u];
+    }
 }
 
 __device__ void finalize_update(const FinalArgs& f, int nred) {
@@ -382,11 +394,12 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
     const int lane = threadIdx.x & 63;
     // every operand of the common case (B <= 256, nred <= 256) is requested before the first
     // use: one memory round trip instead of one per reduction
-    float vr[4], v1[4], v2[4], vp[4];
-    strided_head(f.red, nred, vr);
-    strided_head(f.lq, f.B, v1);
-    strided_head(f.lq + f.B, f.B, v2);
-    strided_head(f.lp, f.B, vp);
+    float ps[4];
+    {
+        const float* const xs[4] = {f.red, f.lq, f.lq + f.B, f.lp};
+        const int ns[4] = {nred, f.B, f.B, f.B};
+        strided_sums4(xs, ns, ps);
+    }
     float a_old = 0.f, a_m = 0.f, a_v = 0.f;
     int64_t t_sac = 0, seq0 = 0, nts = 0, tsi = 0;
     if (lane == 0) {
@@ -394,11 +407,11 @@ __device__ void finalize_update(const FinalArgs& f, int nred) {
         t_sac = f.ctl->t_sac; seq0 = f.ctl->step_seq;
         nts = f.ctl->num_timesteps; tsi = f.ctl->ts_increment;
     }
-    const float ent_sum = wave_sum(strided_rest(f.red, nred, vr));   // sum_i (-nlp_i + H)
+    const float ent_sum = wave_sum(ps[0]);   // sum_i (-nlp_i + H)
     const float m_ent = ent_sum / (float)f.B;   // reduce_mean
-    const float q1 = wave_sum(strided_rest(f.lq, f.B, v1)) / (float)f.B;
-    const float q2 = wave_sum(strided_rest(f.lq + f.B, f.B, v2)) / (float)f.B;
-    float pl = wave_sum(strided_rest(f.lp, f.B, vp)) / (float)f.B;
+    const float q1 = wave_sum(ps[1]) / (float)f.B;
+    const float q2 = wave_sum(ps[2]) / (float)f.B;
+    float pl = wave_sum(ps[3]) / (float)f.B;
     float mse = 0.f;
     if (f.use_expert && f.ne > 0 && f.nm == 1) {
         // one model (SAC_expert.py:293-295): mean over the n_e rows of 0.5 ||sp_e - sp_pred||^2
