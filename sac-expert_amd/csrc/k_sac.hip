@@ -1993,6 +1993,83 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s) {
     }
 }
 
+// ==================================================================== k_act_rows
+// Behaviour-policy inference on a few rows (SquashedGaussianActor.sample /
+// GaussianActor.sample, continuous_actors.py:270-306 / :74-123, on the env loop's one
+// observation): one 1,024-thread workgroup per row normalises the observation, runs both
+// hidden layers and the head with the vectors in LDS, and samples -- one launch where the
+// batched path takes four (obs_norm, two GEMM launches, the head), each of them a few
+// microseconds of launch and round trip for a single row.
+// Dense layer: the 16 waves split K four ways for 256 output columns at a time (thread
+// (q, j) sums k in quarter q of column j: each k reads 1 KB of W contiguously across the
+// threads), and the quarters add in order; fp32 FMAs, within the parity tolerance of the
+// batched MFMA path (a different summation order, not bit-identical to it).
+__device__ __forceinline__ void act_dense(const float* in, int K, const float* W, int N, int act, float* out,
+                                          float (&part)[4][ACT_ROWS_DIM]) {
+    const int t = threadIdx.x, q = t >> 8, j0 = t & 255;
+    const int kq = (K + 3) >> 2, k0 = q * kq, k1 = min(K, k0 + kq);
+    for (int j = j0; j < N; j += 256) {
+        float s = 0.f;
+        for (int k = k0; k < k1; ++k) s = fmaf(in[k], W[(size_t)k * N + j], s);
+        part[q][j] = s;
+    }
+    __syncthreads();
+    for (int j = t; j < N; j += 1024) {
+        float v = part[0][j] + part[1][j];
+        v = v + part[2][j];
+        v = v + part[3][j];
+        out[j] = act_f(v + W[(size_t)K * N + j], act);
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
+    __shared__ float xs[ACT_ROWS_DIM], h1s[ACT_ROWS_DIM], h2s[ACT_ROWS_DIM];
+    __shared__ float part[4][ACT_ROWS_DIM];
+    __shared__ float outs[64];
+    const int t = threadIdx.x, row = blockIdx.x, lane = t & 63, wave = t >> 6;
+    const int S = g.S, A = g.A, Aout = g.Aout;
+    for (int c = t; c < S; c += 1024) xs[c] = (g.obs[(size_t)row * S + c] - g.s_mean[c]) / g.s_den[c];
+    __syncthreads();
+    act_dense(xs, S, g.W0, g.H0, g.act0, h1s, part);
+    act_dense(h1s, g.H0, g.W1, g.H1, g.act1, h2s, part);
+    // head: output o on wave o mod 16, lanes over k, one wave sum
+    for (int o = wave; o < Aout; o += 16) {
+        float s = 0.f;
+        for (int k = lane; k < g.H1; k += 64) s = fmaf(h2s[k], g.W3[(size_t)k * Aout + o], s);
+        s = wave_sum(s);
+        if (lane == 0) outs[o] = s + g.W3[(size_t)g.H1 * Aout + o];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const bool jok = lane < A;
+    const float mu = jok ? outs[lane] : 0.f;
+    const float lraw = jok ? (g.per_state_std ? outs[A + lane] : g.logstd[lane]) : 0.f;
+    const float u = (jok && g.noise != nullptr) ? g.noise[(size_t)row * A + lane] : 0.f;
+    if (g.mode == 2) {              // as actor_head_body's GaussianActor.sample
+        float m = mu;
+        if (g.output_norm) {
+            const float s = wave_sum(jok ? fabsf(mu) : 0.f) / (float)A;
+            m = mu / fmaxf(s, 1.f);
+        }
+        if (jok) {
+            float l = g.per_state_std ? logf(softplus_f(lraw)) : lraw;
+            l = fmaxf(l + g.logstd_init, logf(1e-3f));
+            g.out[(size_t)row * A + lane] = m + expf(l) * u;
+        }
+        return;
+    }
+    if (jok) {                      // SquashedGaussianActor.sample: lim * tanh(mu + exp(clip(l)) u)
+        const float l = fminf(fmaxf(lraw, -5.f), 2.f);
+        const float x = mu + expf(l) * u;
+        g.out[(size_t)row * A + lane] = g.lim * tanhf(x);
+    }
+}
+
+void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s) {
+    hipLaunchKernelGGL(k_act_rows, dim3(m), dim3(1024), 0, s, a);
+}
+
 // ==================================================================== k_qhead
 template <int MODE, int NQ>
 __device__ __forceinline__ void qhead_block(const QHeadArgs& q_in, int block, int64_t so) {

@@ -2037,6 +2037,35 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
     auto W = [&](const std::string& nm) { return h->f(nm); };
+    if (n > 0 && n <= ACT_ROWS_MAX && !h->ln && S <= ACT_ROWS_DIM && h->H0 <= ACT_ROWS_DIM &&
+        H1 <= ACT_ROWS_DIM && h->Aout <= 64) {
+        // the env loop's few rows: the noise draw, then one workgroup per row (k_act_rows)
+        float* noise = deterministic ? nullptr : W("act.noise");
+        if (!deterministic) {          // u = np.random.normal(size=(n, A)) from the global stream
+            RngArgs r{};
+            r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
+            r.n_int = 0; r.n_norm = (int32_t)n * A; r.out_idx = nullptr; r.out_norm = noise;
+            r.slot = -1; r.reset_seq = 0; r.nupd = 1;
+            launch_rng(r, h->stream);
+        }
+        ActRowArgs a{};
+        a.obs = obs; a.s_mean = W("norm.s_mean"); a.s_den = W("norm.s_den");
+        a.W0 = W("actor.l0"); a.W1 = W("actor.l1"); a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.noise = noise; a.out = act_out;
+        a.S = S; a.A = A; a.Aout = h->Aout; a.H0 = h->H0; a.H1 = H1;
+        a.act0 = h->aact[0]; a.act1 = h->aact[1];
+        a.mode = h->cfg.actor_gaussian ? 2 : 1;
+        a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit;
+        if (h->cfg.actor_gaussian) {          // logstd_init (continuous_actors.py:39-44), f32
+            const double sm = h->cfg.actor_std_mult > 0.f ? h->cfg.actor_std_mult : 1.0;
+            a.logstd_init = (float)(std::log(sm) - (h->cfg.per_state_std ? std::log(std::log(2.0)) : 0.0));
+            a.output_norm = h->cfg.actor_output_norm;
+        }
+        launch_act_rows(a, (int)n, h->stream);
+        HIPCHK(h, hipGetLastError());
+        return 0;
+    }
     for (int64_t done = 0; done < n; done += ACT_CAP) {
         const int m = (int)std::min<int64_t>(ACT_CAP, n - done);
         float* noise = deterministic ? nullptr : W("act.noise");

@@ -465,7 +465,25 @@ struct DiagArgs {
     float* out;
 };
 
+// sacx_actor_act on a few rows (the env loop's one observation): one workgroup per row runs
+// the normaliser, both hidden layers and the sampling head (k_act_rows)
+#define ACT_ROWS_MAX 16       // rows per call that take k_act_rows
+#define ACT_ROWS_DIM 1024     // S, H0, H1 bound (LDS vectors)
+struct ActRowArgs {
+    const float* obs;          // [m, S]
+    const float *s_mean, *s_den;
+    const float *W0, *W1, *W3; // Keras (in, out) with the bias as the last row
+    const float* logstd;       // [A] (per_state_std == 0)
+    const float* noise;        // [m, A] or null (deterministic)
+    float* out;                // [m, A]
+    int32_t S, A, Aout, H0, H1, act0, act1;
+    int32_t mode;              // 1: SquashedGaussianActor.sample, 2: GaussianActor.sample
+    int32_t per_state_std, output_norm;
+    float lim, logstd_init;
+};
+
 // launchers (defined in k_sac.hip)
+void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s);
 void launch_gemm(const GemmArgs& a, hipStream_t s);
 void launch_rng(const RngArgs& a, hipStream_t s);
 void launch_gather(const GatherArgs& a, hipStream_t s);

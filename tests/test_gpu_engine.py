@@ -281,7 +281,8 @@ def test_model_fit_matches_oracle(gpu_available, eager):
 @pytest.mark.parametrize("deterministic,per_state_std,n,host", [(True, False, 37, False), (False, False, 37, False),
                                                                 (False, True, 5, False), (False, False, 1, False),
                                                                 (False, False, 1, True), (True, False, 37, True),
-                                                                (False, True, 3000, True)])
+                                                                (False, True, 3000, True), (True, True, 16, False),
+                                                                (False, False, 16, True), (False, True, 2, True)])
 def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n, host):
     """Behaviour-policy inference (sample(), continuous_actors.py:270-306) vs the oracle;
     the stochastic draw advances the device stream exactly as np.random.normal(size=(n, A))."""

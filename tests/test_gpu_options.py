@@ -93,11 +93,13 @@ def test_model_fit_options(gpu_available, nm, max_norm, dclip, rclip):
     eng.close()
 
 
-@pytest.mark.parametrize("per_state_std,output_norm,deterministic", [(False, False, True), (False, True, False),
-                                                                     (True, False, False), (True, True, True)])
-def test_gaussian_actor_sample(gpu_available, per_state_std, output_norm, deterministic):
+@pytest.mark.parametrize("per_state_std,output_norm,deterministic,n", [(False, False, True, 300), (False, True, False, 300),
+                                                                       (True, False, False, 300), (True, True, True, 300),
+                                                                       (True, True, False, 1), (False, True, True, 16)])
+def test_gaussian_actor_sample(gpu_available, per_state_std, output_norm, deterministic, n):
+    """n <= 16 rows take k_act_rows (one workgroup per row), n = 300 the batched launches."""
     from sac_eo.engine import Engine, EngineConfig
-    S, A, n = 11, 3, 300
+    S, A = 11, 3
     cfg = O.Config(S=S, A=A, hidden=(64, 64), act="tanh", per_state_std=per_state_std)
     st = O.init_state(cfg, seed=8, bias_scale=0.2, actor_gain=2.0)
     st.logstd = np.full((1, A), -0.7, np.float32)
