@@ -22,16 +22,20 @@ def kernel_resources(so_path):
         subprocess.check_call([f"{LLVM}/clang-offload-bundler", "--unbundle", "--type=o",
                                "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}", f"--output={dev}"])
         notes = subprocess.check_output([f"{LLVM}/llvm-readelf", "--notes", dev], text=True)
-    out, name = {}, None
+    # one YAML list item per kernel ("  - .agpr_count: ..."); keys before and after .name belong to it
+    out, cur = {}, None
     for line in notes.splitlines():
-        m = re.match(r"\s*\.name:\s+(\S+)", line)
+        if re.match(r"\s{2}- \.", line):
+            cur = {}
+        if cur is None:
+            continue
+        m = re.match(r"\s*-?\s*\.name:\s+(\S+)", line)
         if m:
-            name = m.group(1)
-            out.setdefault(name, {})
+            out[m.group(1)] = cur
         for key in ("vgpr_count", "agpr_count", "sgpr_count", "group_segment_fixed_size"):
-            m = re.match(r"\s*\.%s:\s+(\d+)" % key, line)
-            if m and name:
-                out[name][key] = int(m.group(1))
+            m = re.match(r"\s*-?\s*\.%s:\s+(\d+)" % key, line)
+            if m:
+                cur[key] = int(m.group(1))
     return out
 
 
