@@ -2008,9 +2008,18 @@ __device__ __forceinline__ void act_dense(const float* in, int K, const float* W
                                           float (&part)[4][ACT_ROWS_DIM]) {
     const int t = threadIdx.x, q = t >> 8, j0 = t & 255;
     const int kq = (K + 3) >> 2, k0 = q * kq, k1 = min(K, k0 + kq);
+    const __amdgpu_buffer_rsrc_t rW = make_rsrc(W, 0x7fffffffu);
     for (int j = j0; j < N; j += 256) {
         float s = 0.f;
-        for (int k = k0; k < k1; ++k) s = fmaf(in[k], W[(size_t)k * N + j], s);
+        // 32 weights requested per round trip (one unconditional buffer load each, zero past
+        // k1), then the FMAs in k order
+        for (int kb = k0; kb < k1; kb += 32) {
+            float w[32];
+#pragma unroll
+            for (int i = 0; i < 32; ++i) w[i] = bload(rW, boff(kb + i < k1, (kb + i) * N + j));
+#pragma unroll
+            for (int i = 0; i < 32; ++i) s = (kb + i < k1) ? fmaf(in[min(kb + i, K - 1)], w[i], s) : s;
+        }
         part[q][j] = s;
     }
     __syncthreads();
@@ -2023,29 +2032,13 @@ __device__ __forceinline__ void act_dense(const float* in, int K, const float* W
     __syncthreads();
 }
 
-__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
-    __shared__ float xs[ACT_ROWS_DIM], h1s[ACT_ROWS_DIM], h2s[ACT_ROWS_DIM];
-    __shared__ float part[4][ACT_ROWS_DIM];
-    __shared__ float outs[64];
-    const int t = threadIdx.x, row = blockIdx.x, lane = t & 63, wave = t >> 6;
-    const int S = g.S, A = g.A, Aout = g.Aout;
-    for (int c = t; c < S; c += 1024) xs[c] = (g.obs[(size_t)row * S + c] - g.s_mean[c]) / g.s_den[c];
-    __syncthreads();
-    act_dense(xs, S, g.W0, g.H0, g.act0, h1s, part);
-    act_dense(h1s, g.H0, g.W1, g.H1, g.act1, h2s, part);
-    // head: output o on wave o mod 16, lanes over k, one wave sum
-    for (int o = wave; o < Aout; o += 16) {
-        float s = 0.f;
-        for (int k = lane; k < g.H1; k += 64) s = fmaf(h2s[k], g.W3[(size_t)k * Aout + o], s);
-        s = wave_sum(s);
-        if (lane == 0) outs[o] = s + g.W3[(size_t)g.H1 * Aout + o];
-    }
-    __syncthreads();
-    if (wave != 0) return;
+// sampling tail on wave 0 (outs = mu [, raw logstd]); ls / u: this lane's logstd variable and
+// noise (already loaded)
+__device__ __forceinline__ void act_tail(const ActRowArgs& g, const float* outs, int row, int lane, float ls, float u) {
+    const int A = g.A;
     const bool jok = lane < A;
     const float mu = jok ? outs[lane] : 0.f;
-    const float lraw = jok ? (g.per_state_std ? outs[A + lane] : g.logstd[lane]) : 0.f;
-    const float u = (jok && g.noise != nullptr) ? g.noise[(size_t)row * A + lane] : 0.f;
+    const float lraw = jok ? (g.per_state_std ? outs[A + lane] : ls) : 0.f;
     if (g.mode == 2) {              // as actor_head_body's GaussianActor.sample
         float m = mu;
         if (g.output_norm) {
@@ -2066,8 +2059,103 @@ __global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
     }
 }
 
+// PF (S <= 128, H0, H1 <= 256, Aout <= 16): every operand of the row -- the observation and
+// its normaliser, all the weights this thread multiplies (<= 32 of W0, <= 64 of W1, <= 4 of W3),
+// the biases, logstd and the noise -- is requested before the first barrier, so the row costs
+// one memory round trip instead of one per layer.  Same FMA order as the generic path.
+template <bool PF>
+__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
+    __shared__ float xs[ACT_ROWS_DIM], h1s[ACT_ROWS_DIM], h2s[ACT_ROWS_DIM];
+    __shared__ float part[4][ACT_ROWS_DIM];
+    __shared__ float outs[64];
+    const int t = threadIdx.x, row = blockIdx.x, lane = t & 63, wave = t >> 6;
+    const int S = g.S, A = g.A, Aout = g.Aout;
+    const bool jok = wave == 0 && lane < A;
+    if constexpr (PF) {
+        const int H0 = g.H0, H1 = g.H1;
+        const int q = t >> 8, j = t & 255;
+        const int kq0 = (S + 3) >> 2, a0 = q * kq0, n0 = min(S, a0 + kq0) - a0;
+        const int kq1 = (H0 + 3) >> 2, a1 = q * kq1, n1 = min(H0, a1 + kq1) - a1;
+        const __amdgpu_buffer_rsrc_t rW0 = make_rsrc(g.W0, 0x7fffffffu), rW1 = make_rsrc(g.W1, 0x7fffffffu),
+                                     rW3 = make_rsrc(g.W3, 0x7fffffffu);
+        const float ob = bload(rs(g.obs), boff(t < S, row * S + t));
+        const float om = bload(rs(g.s_mean), boff(t < S, t)), od = bload(rs(g.s_den), boff(t < S, t));
+        float w0[32], w1[64], w3[4];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) w0[i] = bload(rW0, boff(i < n0 && j < H0, (a0 + i) * H0 + j));
+#pragma unroll
+        for (int i = 0; i < 64; ++i) w1[i] = bload(rW1, boff(i < n1 && j < H1, (a1 + i) * H1 + j));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w3[i] = bload(rW3, boff(wave < Aout && lane + 64 * i < H1, (lane + 64 * i) * Aout + wave));
+        const float b0 = bload(rW0, boff(t < H0, S * H0 + t)), b1 = bload(rW1, boff(t < H1, H0 * H1 + t));
+        const float b3 = bload(rW3, boff(wave < Aout, H1 * Aout + wave));
+        const float ls = bload(rs(g.logstd), boff(jok && !g.per_state_std, lane));
+        const float u = bload(rs(g.noise), boff(jok, row * A + lane));
+        if (t < S) xs[t] = (ob - om) / od;
+        __syncthreads();
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 32; ++i) s = i < n0 ? fmaf(xs[min(a0 + i, S - 1)], w0[i], s) : s;
+        part[q][j] = s;
+        __syncthreads();
+        if (t < H0) {
+            float v = part[0][t] + part[1][t];
+            v = v + part[2][t];
+            v = v + part[3][t];
+            h1s[t] = act_f(v + b0, g.act0);
+        }
+        __syncthreads();
+        s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 64; ++i) s = i < n1 ? fmaf(h1s[min(a1 + i, H0 - 1)], w1[i], s) : s;
+        part[q][j] = s;
+        __syncthreads();
+        if (t < H1) {
+            float v = part[0][t] + part[1][t];
+            v = v + part[2][t];
+            v = v + part[3][t];
+            h2s[t] = act_f(v + b1, g.act1);
+        }
+        __syncthreads();
+        if (wave < Aout) {
+            s = 0.f;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) s = lane + 64 * i < H1 ? fmaf(h2s[min(lane + 64 * i, H1 - 1)], w3[i], s) : s;
+            s = wave_sum(s);
+            if (lane == 0) outs[wave] = s + b3;
+        }
+        __syncthreads();
+        if (wave == 0) act_tail(g, outs, row, lane, ls, u);
+        return;
+    }
+    for (int c = t; c < S; c += 1024) xs[c] = (g.obs[(size_t)row * S + c] - g.s_mean[c]) / g.s_den[c];
+    __syncthreads();
+    act_dense(xs, S, g.W0, g.H0, g.act0, h1s, part);
+    act_dense(h1s, g.H0, g.W1, g.H1, g.act1, h2s, part);
+    // head: output o on wave o mod 16, lanes over k, one wave sum
+    const __amdgpu_buffer_rsrc_t rW3 = make_rsrc(g.W3, 0x7fffffffu);
+    for (int o = wave; o < Aout; o += 16) {
+        float w[ACT_ROWS_DIM / 64];
+#pragma unroll
+        for (int i = 0; i < ACT_ROWS_DIM / 64; ++i) w[i] = bload(rW3, boff(lane + 64 * i < g.H1, (lane + 64 * i) * Aout + o));
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < ACT_ROWS_DIM / 64; ++i)
+            s = (lane + 64 * i < g.H1) ? fmaf(h2s[min(lane + 64 * i, g.H1 - 1)], w[i], s) : s;
+        s = wave_sum(s);
+        if (lane == 0) outs[o] = s + g.W3[(size_t)g.H1 * Aout + o];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    const float ls = jok && !g.per_state_std ? g.logstd[lane] : 0.f;
+    const float u = (jok && g.noise != nullptr) ? g.noise[(size_t)row * A + lane] : 0.f;
+    act_tail(g, outs, row, lane, ls, u);
+}
+
 void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s) {
-    hipLaunchKernelGGL(k_act_rows, dim3(m), dim3(1024), 0, s, a);
+    const bool pf = a.S <= 128 && a.H0 <= 256 && a.H1 <= 256 && a.Aout <= 16;
+    if (pf) hipLaunchKernelGGL(k_act_rows<true>, dim3(m), dim3(1024), 0, s, a);
+    else hipLaunchKernelGGL(k_act_rows<false>, dim3(m), dim3(1024), 0, s, a);
 }
 
 // ==================================================================== k_qhead

@@ -307,6 +307,28 @@ def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n
     eng.close()
 
 
+@pytest.mark.parametrize("S,A,act,per_state_std,n", [(376, 17, "tanh", False, 3), (376, 17, "relu", True, 1),
+                                                      (17, 6, "elu", True, 16)])
+def test_actor_act_rows_shapes(gpu_available, S, A, act, per_state_std, n):
+    """k_act_rows on both of its paths: the prefetching one (S <= 128, H <= 256) and the generic
+    one (Humanoid S = 376), stochastic, vs the oracle; the device stream advances as NumPy's."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, act=act, B=64, N=500, seed=43, normalizers="random",
+                                           per_state_std=per_state_std)
+    obs = np.random.RandomState(5).normal(size=(n, S)) * 2.0
+    eng.rng_set_state(np.random.RandomState(19).get_state())
+    ref_rs = np.random.RandomState(19)
+    got = np.asarray(eng.act_host(obs[0] if n == 1 else obs, False)).reshape(n, A)
+    x = (obs.astype(np.float32) - nrm.s_mean) / nrm.s_den
+    out, _ = O.mlp_forward(st.actor, x.astype(np.float64), ocfg.act)
+    mu, lraw = O.split_head(out, st.logstd, ocfg)
+    u = O.f32_noise(ref_rs.normal(size=(n, A))).astype(np.float64)
+    pi, _ = O.head_sample(mu, lraw, u, ocfg.act_limit, np.float64)
+    assert relerr(got, pi) < 2e-5, relerr(got, pi)
+    dev, ref = eng.rng_get_state(), ref_rs.get_state()
+    assert np.array_equal(dev[1], ref[1]) and dev[2] == ref[2] and dev[3] == ref[3] and dev[4] == ref[4]
+    eng.close()
+
+
 @pytest.mark.parametrize("deterministic,n,horizon,clip", [(False, 37, 5, 0.0), (True, 8, 3, 0.0),
                                                          (False, 4100, 2, 0.05)])
 def test_rollout_matches_oracle(gpu_available, deterministic, n, horizon, clip):
