@@ -308,10 +308,12 @@ def test_actor_act_matches_oracle(gpu_available, deterministic, per_state_std, n
 
 
 @pytest.mark.parametrize("S,A,act,per_state_std,n", [(376, 17, "tanh", False, 3), (376, 17, "relu", True, 1),
-                                                      (17, 6, "elu", True, 16)])
+                                                      (17, 6, "elu", True, 16), (17, 6, "relu", False, 1),
+                                                      (17, 6, "tanh", True, 1)])
 def test_actor_act_rows_shapes(gpu_available, S, A, act, per_state_std, n):
-    """k_act_rows on both of its paths: the prefetching one (S <= 128, H <= 256) and the generic
-    one (Humanoid S = 376), stochastic, vs the oracle; the device stream advances as NumPy's."""
+    """k_act_rows on both of its paths (the prefetching one, S <= 128 and H <= 256; the generic
+    one, Humanoid S = 376), stochastic, vs the oracle; the device stream advances as NumPy's;
+    repeats from the same stream state give the same action."""
     eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, act=act, B=64, N=500, seed=43, normalizers="random",
                                            per_state_std=per_state_std)
     obs = np.random.RandomState(5).normal(size=(n, S)) * 2.0
@@ -326,6 +328,10 @@ def test_actor_act_rows_shapes(gpu_available, S, A, act, per_state_std, n):
     assert relerr(got, pi) < 2e-5, relerr(got, pi)
     dev, ref = eng.rng_get_state(), ref_rs.get_state()
     assert np.array_equal(dev[1], ref[1]) and dev[2] == ref[2] and dev[3] == ref[3] and dev[4] == ref[4]
+    for _ in range(3):
+        eng.rng_set_state(np.random.RandomState(19).get_state())
+        again = np.asarray(eng.act_host(obs[0] if n == 1 else obs, False)).reshape(n, A)
+        assert np.array_equal(again, got)
     eng.close()
 
 
