@@ -429,17 +429,20 @@ def _norm(x, mean, den):
 
 def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, noise_pi, noise_alpha,
                expert: Optional[Expert] = None, do_polyak: bool = True, keep: Optional[dict] = None,
-               grad_hook=None):
+               grad_hook=None, mnrm: Optional[Normalizers] = None):
     """One ``_update`` (SAC_expert.py:463-477 / SAC.py:236-250), in place on
     ``st``.  ``batch`` = (s, a, sp, r, d) raw rows; noises are (n, A) arrays.
     Returns the step statistics.  ``keep`` (optional dict) receives the
     intermediates used by the stage-level GPU parity tests.  ``grad_hook(name, grads)``
     (optional) maps each optimiser's gradient list before its Adam ("q0", "q1", "actor",
-    "alpha"): the data-parallel mode's all-reduce / ranks (include/sacx.h sacx_dp_init)."""
+    "alpha"): the data-parallel mode's all-reduce / ranks (include/sacx.h sacx_dp_init).
+    ``mnrm``: the world models' normaliser (SAC_expert.py:139-144, --only_model_normalizer);
+    None: the shared ``nrm`` (the reference's default)."""
     hook = grad_hook if grad_hook is not None else (lambda name, g: g)
     dt = st.alpha.dtype.type
     F = lambda x: _F(dt, x)
     nrm = nrm.cast(dt)
+    mnrm = nrm if mnrm is None else mnrm.cast(dt)
     s, a, sp, r, d = [np.asarray(x, dt) for x in batch]
     n1, n2, n3 = [np.asarray(x, dt) for x in (noise_t, noise_pi, noise_alpha)]
     B, S = s.shape
@@ -517,7 +520,8 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
             out_e, hs_e = actor_forward(actor_all, se_n, cfg)
             mu_e, ls_e = split_head(out_e, st.logstd, cfg)
             ca, cache_e = head_sample(mu_e, ls_e, ne, lim, dt)
-            xm = np.concatenate([se_n, _norm(ca, nrm.a_mean, nrm.a_den)], axis=1)
+            # the model normalises its own inputs (MSEModel.sample -> _forward, base_world_model.py:67-69)
+            xm = np.concatenate([_norm(se, mnrm.s_mean, mnrm.s_den), _norm(ca, mnrm.a_mean, mnrm.a_den)], axis=1)
             om, hsm = mlp_forward(st.models[k], xm, cfg.model_act)
             dn = om[:, :S]
             dpass = np.ones_like(dn)
@@ -527,7 +531,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
                 c = F(cfg.delta_clip_pred)
                 dpass = ((dn >= -c) & (dn <= c)).astype(dt)
                 dn = np.minimum(np.maximum(dn, -c), c)
-            sp_hat = se + (dn * nrm.d_den + nrm.d_mean)
+            sp_hat = se + (dn * mnrm.d_den + mnrm.d_mean)
             diffs.append(spe - sp_hat)
             caches.append((se_n, hs_e, cache_e, xm, hsm, spe, sp_hat, dpass))
         if len(diffs) == 2:
@@ -540,12 +544,12 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
         for k, (se_n, hs_e, cache_e, xm, hsm, spe, sp_hat, dpass) in enumerate(caches):
             dsp = -eps * F(1.0 / ne_half) * diffs[k]
             dout = np.zeros((ne_half, S + 1), dt)
-            dout[:, :S] = dsp * nrm.d_den * dpass
+            dout[:, :S] = dsp * mnrm.d_den * dpass
             if keep is not None:
                 keep["clip_frac%d" % k] = float(1.0 - dpass.mean())
             _, dxm = mlp_backward(st.models[k], xm, hsm, dout, cfg.model_act,
                                   need_dx=True, need_dw=False)
-            dca = dxm[:, S:] / nrm.a_den
+            dca = dxm[:, S:] / mnrm.a_den
             dmu_e, dl_ee = head_backward(dca, None, cache_e, lim, dt)
             rows_x.append(se_n)
             rows_h.append(hs_e)
@@ -645,7 +649,8 @@ def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches, max_gra
 # MSEModel as the environment (continuous_models.py:225-258)
 # ---------------------------------------------------------------------------
 def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k: int, rs=None,
-            deterministic: bool = False, delta_clip: float = 0.0, reward_clip: float = 0.0):
+            deterministic: bool = False, delta_clip: float = 0.0, reward_clip: float = 0.0,
+            mnrm: Optional[Normalizers] = None):
     """Returns (s, a, r, sp, d) of shapes [n,H,S], [n,H,A], [n,H], [n,H,S], [n,H].
 
     Per step (samplers.py:89-116): a = actor.sample(s) (continuous_actors.py:270-306,
@@ -653,10 +658,11 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
     = MSEModel.step: (delta_n, r_n) = _forward(s, clip(a)) with the optional prediction clips
     (base_world_model.py:65-87), s <- s + delta_rms.denormalize(delta_n), r =
     r_rms.denormalize(r_n), d = (ones_like(r) == 0) = False; the last step stores
-    d = terminated (all False)."""
+    d = terminated (all False).  ``mnrm``: the model's normaliser (None: ``nrm``)."""
     dt = st.alpha.dtype.type
     F = lambda x: _F(dt, x)
     nrm = nrm.cast(dt)
+    mnrm = nrm if mnrm is None else mnrm.cast(dt)
     S, A = cfg.S, cfg.A
     s = np.asarray(s_init, dt).reshape(-1, S)
     n = s.shape[0]
@@ -669,15 +675,15 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
         u = np.zeros_like(mu) if deterministic else f32_noise(rs.normal(size=mu.shape)).astype(dt)
         a, _ = head_sample(mu, lraw, u, cfg.act_limit, dt)
         ac = np.clip(a, -lim, lim)                                # actor.clip (continuous_actors.py:125)
-        xm = np.concatenate([x, _norm(ac, nrm.a_mean, nrm.a_den)], 1)
+        xm = np.concatenate([_norm(s, mnrm.s_mean, mnrm.s_den), _norm(ac, mnrm.a_mean, mnrm.a_den)], 1)
         pred, _ = mlp_forward(st.models[k], xm, cfg.model_act)
         dn, rn = pred[:, :S], pred[:, S]
         if delta_clip:
             dn = np.clip(dn, -F(delta_clip), F(delta_clip))
         if reward_clip:
             rn = np.clip(rn, -F(reward_clip), F(reward_clip))
-        sp = s + (dn * nrm.d_den + nrm.d_mean)
-        r = rn * nrm.r_den + nrm.r_mean
+        sp = s + (dn * mnrm.d_den + mnrm.d_mean)
+        r = rn * mnrm.r_den + mnrm.r_mean
         for key, v in (("s", s), ("a", a), ("r", r), ("sp", sp), ("d", np.zeros(n, bool))):
             out[key].append(v)
         s = sp
@@ -706,18 +712,20 @@ def _actor_sample(st, cfg, nrm, s, rs):
     return head_sample(mu, lraw, u, cfg.act_limit, dt)[0]
 
 
-def expert_mse_diag(st, cfg, nrm, s_e, a_e, sp_e, rs=None, use_expert_actions=False, delta_clip=0.0):
+def expert_mse_diag(st, cfg, nrm, s_e, a_e, sp_e, rs=None, use_expert_actions=False, delta_clip=0.0, mnrm=None):
     """(model_MSE_on_expert_data, model_MSE_on_expert_counterfactual_action): per model
     mean_i 0.5 ||model.sample(s_e, a) - sp_e||^2, averaged over the models; a = a_e, then
     a = actor.sample(s_e, deterministic=False) (one normal(size=(n, A)) draw) unless
-    use_expert_actions."""
+    use_expert_actions.  ``mnrm``: the models' normaliser (None: ``nrm``, the actor's)."""
     dt = st.alpha.dtype.type
     nrm = nrm.cast(dt)
+    mnrm = nrm if mnrm is None else mnrm.cast(dt)
     s_e, a_e, sp_e = [np.asarray(x, dt) for x in (s_e, a_e, sp_e)]
+    nmod = len(st.models)
 
     def mse(a):
-        per = [np.mean(_F(dt, 0.5) * ((_model_sample(st, cfg, nrm, k, s_e, a, delta_clip) - sp_e) ** 2).sum(-1))
-               for k in range(2)]
+        per = [np.mean(_F(dt, 0.5) * ((_model_sample(st, cfg, mnrm, k, s_e, a, delta_clip) - sp_e) ** 2).sum(-1))
+               for k in range(nmod)]
         return float(np.mean(per)), per
     m_data, per_data = mse(a_e)
     if use_expert_actions:
@@ -726,14 +734,15 @@ def expert_mse_diag(st, cfg, nrm, s_e, a_e, sp_e, rs=None, use_expert_actions=Fa
     return m_data, m_cf, per_data, per_cf
 
 
-def calc_disc(st, cfg, nrm, s_e, a_e, rs=None, use_expert_actions=False, delta_clip=0.0):
+def calc_disc(st, cfg, nrm, s_e, a_e, rs=None, use_expert_actions=False, delta_clip=0.0, mnrm=None):
     """_calc_disc: (disc_ratio, max_disc, median_disc, s_disc_total) of the two models'
     predictions on (s_e, a) with a = a_e or a fresh actor.sample(s_e) (tf_clip: a no-op)."""
     dt = st.alpha.dtype.type
     nrm = nrm.cast(dt)
+    mnrm = nrm if mnrm is None else mnrm.cast(dt)
     s_e = np.asarray(s_e, dt)
     a = np.asarray(a_e, dt) if use_expert_actions else _actor_sample(st, cfg, nrm, s_e, rs)
-    diff = _model_sample(st, cfg, nrm, 0, s_e, a, delta_clip) - _model_sample(st, cfg, nrm, 1, s_e, a, delta_clip)
+    diff = _model_sample(st, cfg, mnrm, 0, s_e, a, delta_clip) - _model_sample(st, cfg, mnrm, 1, s_e, a, delta_clip)
     s_disc = np.sqrt((diff * diff).sum(axis=1))
     tot = np.sum(s_disc)
     return s_disc / tot, float(np.max(s_disc)), float(np.median(s_disc)), float(tot)

@@ -232,7 +232,7 @@ __device__ __forceinline__ void reloc(HeadBwdArgs& b, int64_t so) {
     b.part = sr(b.part, so); b.gpol = sr(b.gpol, so); b.a_den = sr(b.a_den, so); b.alpha = sr(b.alpha, so);
     b.c_t = sr(b.c_t, so); b.c_std = sr(b.c_std, so); b.c_u = sr(b.c_u, so); b.c_mask = sr(b.c_mask, so);
     b.Da3 = sr(b.Da3, so); b.E = sr(b.E, so); b.Da2 = sr(b.Da2, so);
-    b.mpart = sr(b.mpart, so); b.ctl = sr(b.ctl, so);
+    b.mpart = sr(b.mpart, so); b.ctl = sr(b.ctl, so); b.ma_den = sr(b.ma_den, so);
 }
 __device__ __forceinline__ void reloc(FinalArgs& f, int64_t so) {
     f.alpha = sr(f.alpha, so); f.alpha_m = sr(f.alpha_m, so); f.alpha_v = sr(f.alpha_v, so); f.ctl = sr(f.ctl, so);
@@ -261,7 +261,8 @@ __device__ __forceinline__ void reloc(ActorBwdArgs& b, int64_t so) {
         b.Wq1[k] = sr(b.Wq1[k], so);
         b.Wm1[k] = sr(b.Wm1[k], so);
     }
-    b.Dm1 = sr(b.Dm1, so); b.a_den = sr(b.a_den, so); b.alpha = sr(b.alpha, so); b.ctl = sr(b.ctl, so);
+    b.Dm1 = sr(b.Dm1, so); b.a_den = sr(b.a_den, so); b.ma_den = sr(b.ma_den, so); b.alpha = sr(b.alpha, so);
+    b.ctl = sr(b.ctl, so);
     b.c_t = sr(b.c_t, so); b.c_std = sr(b.c_std, so); b.c_u = sr(b.c_u, so); b.c_mask = sr(b.c_mask, so);
     b.W3a = sr(b.W3a, so); b.Ha2 = sr(b.Ha2, so); b.Da3 = sr(b.Da3, so); b.Da2 = sr(b.Da2, so); b.E = sr(b.E, so);
     b.gpol = sr(b.gpol, so);
@@ -699,7 +700,8 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
     const float sd = bload(rs(hb.c_std), boff(ok, ci));
     const float u = bload(rs(hb.c_u), boff(ok, ci));
     const float mk = bload(rs(hb.c_mask), boff(ok, ci));
-    const float ad = bload(rs(hb.a_den), boff(jok, col));
+    // the action column's normaliser: the critics' for policy rows, the world models' for expert rows
+    const float ad = bload(rs(pol ? hb.a_den : hb.ma_den), boff(jok, col));
     const __amdgpu_buffer_rsrc_t rg = rs(hb.gpol);
     const float g0 = bload(rg, boff(rok && pol, m));
     const float g1 = bload(rg, boff(rok && pol, B + m));
@@ -1738,6 +1740,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
         g.slot = ga.slot + (int)blockIdx.y;
         g.replay = sr(ga.replay, so); g.ctl = sr(ga.ctl, so);
         g.s_mean = sr(ga.s_mean, so); g.s_den = sr(ga.s_den, so); g.a_mean = sr(ga.a_mean, so); g.a_den = sr(ga.a_den, so);
+        g.ms_mean = sr(ga.ms_mean, so); g.ms_den = sr(ga.ms_den, so);
         g.exp_s = sr(ga.exp_s, so); g.exp_sp = sr(ga.exp_sp, so); g.perm_ring = sr(ga.perm_ring, so);
     }
     const int S = g.S, A = g.A;
@@ -1779,17 +1782,22 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
         const int64_t slot = g.ctl->pseq[g.slot] % g.perm_cap;
         const int src = g.perm_ring != nullptr ? g.perm_ring[slot * g.ne + e] : e;
         const __amdgpu_buffer_rsrc_t rse = rs(g.exp_s + (size_t)src * S), rspe = rs(g.exp_sp + (size_t)src * S);
+        // the actor row takes the actor's normaliser, the world-model row the models' (the same
+        // values unless --only_model_normalizer, SAC_expert.py:139-144)
+        const __amdgpu_buffer_rsrc_t rmm = rs(g.ms_mean), rmd = rs(g.ms_den);
         for (int c = lane; c < g.ldQ; c += 64) {
             const bool cs = c < S;
             const float xs = bload(rse, boff(cs, c)), xsp = bload(rspe, boff(cs, c));
             const float ms = bload(rsm, boff(cs, c)), ds = bload(rsd, boff(cs, c));
+            const float mms = bload(rmm, boff(cs, c)), mds = bload(rmd, boff(cs, c));
             const float sn = cs ? (xs - ms) / ds : 0.f;
+            const float smn = cs ? (xs - mms) / mds : 0.f;
             if (cs) {
                 g.se_raw[(size_t)e * S + c] = xs;
                 g.spe_raw[(size_t)e * S + c] = xsp;
             }
             if (c < g.ldS) g.Xa[(size_t)(2 * g.B + e) * g.ldS + c] = sn;
-            if (c < S || c >= S + A) g.Xm[(size_t)e * g.ldQ + c] = sn;
+            if (c < S || c >= S + A) g.Xm[(size_t)e * g.ldQ + c] = smn;
         }
     }
 }
@@ -1857,8 +1865,10 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         const __amdgpu_buffer_rsrc_t rW = rs(sr(h.W3, so));
         const float u_pf = bload(rs(sg.noise), boff(jok, (row - sg.r0) * A + lane));
         const float ls_pf = bload(rs(sr(h.logstd, so)), boff(jok && !h.per_state_std, lane));
-        const float am_pf = bload(rs(sr(h.a_mean, so)), boff(jok, lane));
-        const float ad_pf = bload(rs(sr(h.a_den, so)), boff(jok, lane));
+        // sample segments (mode 1) feed the world models: their normaliser for the action columns
+        const bool msg = sg.mode == 1 && h.ma_mean != nullptr;
+        const float am_pf = bload(rs(sr(msg ? h.ma_mean : h.a_mean, so)), boff(jok, lane));
+        const float ad_pf = bload(rs(sr(msg ? h.ma_den : h.a_den, so)), boff(jok, lane));
         const float bmu = bload(rW, boff(jok, h.H1 * Aout + lane));
         const float bls = bload(rW, boff(jok && h.per_state_std, h.H1 * Aout + A + lane));
         float mu = 0.f, lraw = 0.f;
@@ -2325,7 +2335,7 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     // every argument in one batch of kernarg loads (else one dependent batch per branch)
     asm volatile("" ::"s"(b.B), "s"(b.ne), "s"(b.S), "s"(b.A), "s"(b.Aout), "s"(b.H0), "s"(b.H1), "s"(b.Hm0),
                  "s"(b.per_state_std), "s"(b.lim), "s"(b.Dp1), "s"(b.Wq1[0]), "s"(b.Wq1[1]), "s"(b.Dm1),
-                 "s"(b.Wm1[0]), "s"(b.Wm1[1]), "s"(b.a_den), "s"(b.alpha), "s"(b.ctl), "s"(b.use_expert),
+                 "s"(b.Wm1[0]), "s"(b.Wm1[1]), "s"(b.a_den), "s"(b.ma_den), "s"(b.alpha), "s"(b.ctl), "s"(b.use_expert),
                  "s"(b.c_t), "s"(b.c_std), "s"(b.c_u), "s"(b.c_mask), "s"(b.W3a), "s"(b.Ha2), "s"(b.act),
                  "s"(b.gpol));
     if constexpr (PK) reloc(b, seed_off(b_in.sstride));
@@ -2357,7 +2367,7 @@ __device__ __forceinline__ void actor_bwd_body(const ActorBwdArgs& b_in) {
     const float sd_pf = bload(rs(b.c_std), boff(jok, ci));
     const float u_pf = bload(rs(b.c_u), boff(jok, ci));
     const float mk_pf = bload(rs(b.c_mask), boff(jok, ci));
-    const float ad_pf = bload(rs(b.a_den), boff(jok, lane));
+    const float ad_pf = bload(rs(pol ? b.a_den : b.ma_den), boff(jok, lane));   // expert rows: the models' normaliser
     float h2v[NQ];
     load_row(rs(b.Ha2), row * b.H1, b.H1, h2v);
     // W3's first 8 output columns (all of them when Aout <= 8) load with the phase-1 operands,
@@ -2613,9 +2623,9 @@ __global__ __launch_bounds__(256) void k_diag_prep(DiagArgs g) {
     const int i = blockIdx.x * 4 + wave;
     if (i >= g.n) return;
     for (int j = lane; j < g.S; j += 64) {
-        const float xn = (g.s_e[(int64_t)i * g.S + j] - g.s_mean[j]) / g.s_den[j];
-        g.X[(int64_t)i * g.ldS + j] = xn;
-        g.Xm[(int64_t)i * g.ldQ + j] = xn;
+        const float x = g.s_e[(int64_t)i * g.S + j];
+        g.X[(int64_t)i * g.ldS + j] = (x - g.s_mean[j]) / g.s_den[j];
+        g.Xm[(int64_t)i * g.ldQ + j] = (x - g.ms_mean[j]) / g.ms_den[j];
     }
     if (g.a_e)
         for (int j = lane; j < g.A; j += 64)
@@ -2767,9 +2777,8 @@ __global__ __launch_bounds__(256) void k_roll(RollArgs g) {
         for (int j = lane; j < S; j += 64) {
             const float v = src[j];
             if (g.t == 0 && g.s_init) g.s_out[o * S + j] = v;
-            const float xn = (v - g.s_mean[j]) / g.s_den[j];
-            g.X[(int64_t)i * g.ldS + j] = xn;
-            g.Xm[(int64_t)i * g.ldQ + j] = xn;
+            g.X[(int64_t)i * g.ldS + j] = (v - g.s_mean[j]) / g.s_den[j];
+            g.Xm[(int64_t)i * g.ldQ + j] = (v - g.ms_mean[j]) / g.ms_den[j];
         }
         return;
     }

@@ -188,6 +188,12 @@ struct sacx_handle {
 
 namespace {
 
+// a segment of the normaliser set the world models use: mnorm.* (SAC-EO) -- or norm.* on a handle
+// without models, where only the update's own normaliser exists
+std::string mnorm(const sacx_handle* h, const char* x) {
+    return std::string(h->cfg.use_expert ? "mnorm." : "norm.") + x;
+}
+
 int fail(sacx_handle* h, const std::string& msg) {
     if (h) h->err = msg;
     return -1;
@@ -242,6 +248,17 @@ void build_layout(sacx_handle* h) {
     h->add("norm.d_den", 1, S, F, SACX_ROLE_STATE);
     h->add("norm.r", 1, 2, F, SACX_ROLE_STATE);  // r_mean, r_den
     h->add("norm.ret_den", 1, 1, F, SACX_ROLE_STATE);
+    // the world models' own normaliser set (SAC_expert.py:53-54, :139-144): a copy of norm.*
+    // unless --only_model_normalizer gives the models a RunningNormalizers of their own
+    if (h->cfg.use_expert) {
+        h->add("mnorm.s_mean", 1, S, F, SACX_ROLE_STATE);
+        h->add("mnorm.s_den", 1, S, F, SACX_ROLE_STATE);
+        h->add("mnorm.a_mean", 1, A, F, SACX_ROLE_STATE);
+        h->add("mnorm.a_den", 1, A, F, SACX_ROLE_STATE);
+        h->add("mnorm.d_mean", 1, S, F, SACX_ROLE_STATE);
+        h->add("mnorm.d_den", 1, S, F, SACX_ROLE_STATE);
+        h->add("mnorm.r", 1, 2, F, SACX_ROLE_STATE);
+    }
     // ---------------- control + RNG
     h->add("ctl", 1, 32, SACX_I64, SACX_ROLE_STATE);
     const uint64_t roff = h->add("rng", 1, sizeof(RngState) / 4, SACX_U32, SACX_ROLE_STATE);
@@ -597,6 +614,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         g.S = S; g.A = A; g.B = B; g.ne = ne; g.idx = idx; g.ctl = h->ctl();
         g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den");
         g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
+        g.ms_mean = W(mnorm(h, "s_mean")); g.ms_den = W(mnorm(h, "s_den"));
         g.Xa = Xa; g.ldS = ldS; g.Xq = Xq; g.Xt = Xt; g.Xp = Xp; g.Xm = Xm; g.ldQ = ldQ;
         g.r = r_in; g.d = d_in; g.slot = slot; g.nupd = 1; g.slot_bytes = h->slot_bytes;
         g.exp_s = W("expert.s"); g.exp_sp = W("expert.sp");
@@ -688,6 +706,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         a.part = head_part ? hpart : nullptr; a.tq = tqh;
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.ma_mean = W(mnorm(h, "a_mean")); a.ma_den = W(mnorm(h, "a_den"));
         // q.fwd0 carries the target rows (tile prologues) and, folded, the previous update's
         // alpha rows; the policy rows ride as extra workgroups of critic.adam (policy_head)
         a.nseg = 1;
@@ -715,6 +734,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         a.part = head_part ? hpart : nullptr; a.tq = tqh;
         a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.ma_mean = W(mnorm(h, "a_mean")); a.ma_den = W(mnorm(h, "a_den"));
         a.nseg = eo ? 3 : 2;
         a.seg[0] = {0, B, 0, 0, noise_t, Xt, W("ws.nlp_t")};
         a.seg[1] = {B, 2 * B, 0, 0, noise_pi, Xp, W("ws.nlp_p")};
@@ -865,7 +885,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 p.mse = 1; p.grad_scale = 1.f / (float)mrows;       // MSE_loss = mean over the rows
                 p.dclip = h->cfg.delta_clip_pred > 0.f ? h->cfg.delta_clip_pred : 0.f;
                 p.se_raw = se_raw + (size_t)k * half * S; p.spe_raw = spe_raw + (size_t)k * half * S;
-                p.dmean = W("norm.d_mean"); p.dden = W("norm.d_den");
+                p.dmean = W("mnorm.d_mean"); p.dden = W("mnorm.d_den");
                 p.part = W("ws.mse") + (size_t)k * half * mtn;
                 pm.push_back(p);
             }
@@ -976,7 +996,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         HeadBwdArgs& b = L.gemm.hbw;
         b.B = B; b.A = A; b.Aout = Aout; b.per_state_std = h->cfg.per_state_std; b.tq = tq;
         b.lim = h->cfg.act_limit; b.part = W("ws.apart"); b.gpol = W("ws.gp"); b.a_den = W("norm.a_den");
-        b.alpha = W("alpha");
+        b.ma_den = W(mnorm(h, "a_den")); b.alpha = W("alpha");
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
         b.Da3 = Da3; b.E = E; b.Da2 = Da2;
         b.ne = ne; b.tqm = (Hm0 + 15) / 16; b.mpart = eo ? W("ws.mpart") : nullptr; b.ctl = eo ? h->ctl() : nullptr;
@@ -992,7 +1012,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.per_state_std = h->cfg.per_state_std; b.lim = h->cfg.act_limit;
         b.Dp1 = Dp1; b.Wq1[0] = W("q0.l0"); b.Wq1[1] = W("q1.l0");
         b.Dm1 = Dm1; b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W(nm > 1 ? "m1.l0" : "m0.l0") : nullptr;
-        b.a_den = W("norm.a_den"); b.alpha = W("alpha"); b.ctl = h->ctl(); b.use_expert = eo;
+        b.a_den = W("norm.a_den"); b.ma_den = W(mnorm(h, "a_den")); b.alpha = W("alpha"); b.ctl = h->ctl();
+        b.use_expert = eo;
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
         b.W3a = W("actor.l2"); b.Ha2 = Ha2 + (size_t)B * H1; b.act = a1;
         b.Da3 = Da3; b.Da2 = Da2; b.E = E;
@@ -1141,8 +1162,8 @@ void build_model_plan(sacx_handle* h) {
         MGatherArgs& g = L.mg;
         g.replay = W("replay"); g.cap = h->cap; g.stride = h->stride; g.S = S; g.A = A; g.mb = mb;
         g.idx_ring = h->ptr<int32_t>("mfit.idx"); g.idx_cap = h->mfit_cap; g.ctl = h->ctl();
-        g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den"); g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
-        g.d_mean = W("norm.d_mean"); g.d_den = W("norm.d_den"); g.r_norm = W("norm.r");
+        g.s_mean = W("mnorm.s_mean"); g.s_den = W("mnorm.s_den"); g.a_mean = W("mnorm.a_mean");
+        g.a_den = W("mnorm.a_den"); g.d_mean = W("mnorm.d_mean"); g.d_den = W("mnorm.d_den"); g.r_norm = W("mnorm.r");
         g.X = Xf; g.ldQ = ldQ; g.T = Tf; g.nm = nm;
         g.clip_d = h->cfg.delta_clip_loss; g.clip_r = h->cfg.reward_clip_loss;
         L.grid = (nm * mb + 3) / 4;
@@ -1791,6 +1812,7 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
     if (!s || !a || !r || !sp || !d) return fail(h, "null row pointer");
     const int S = h->S, A = h->A;
     const int64_t per = 2 * S + A + 2, chunk = STAGE_CAP / per;
+    if (chunk <= 0) return fail(h, "a transition is larger than the pinned staging buffer (use sacx_buffer_append)");
     for (int64_t done = 0; done < n; done += chunk) {
         const int64_t m = std::min(chunk, n - done);
         if (stage_begin(h)) return -1;
@@ -1814,6 +1836,7 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A;
     const int64_t chunk = std::min<int64_t>(ACT_CAP, STAGE_CAP / (S + A));
+    if (chunk <= 0) return fail(h, "an observation row is larger than the pinned staging buffer (use sacx_actor_act)");
     for (int64_t done = 0; done < n; done += chunk) {
         const int64_t m = std::min(chunk, n - done);
         if (stage_begin(h)) return -1;
@@ -2101,12 +2124,14 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
 }
 
 // ---------------------------------------------------------------- reference object methods
-static NetIOArgs netio_base(sacx_handle* h) {
+// model = true: the world models' normaliser set (MSEModel calls), else the update's (QCritic)
+static NetIOArgs netio_base(sacx_handle* h, bool model = false) {
     auto W = [&](const std::string& nm) { return h->f(nm); };
+    auto N = [&](const char* x) { return model ? W(mnorm(h, x)) : W(std::string("norm.") + x); };
     NetIOArgs g{};
     g.S = h->S; g.A = h->A;
-    g.s_mean = W("norm.s_mean"); g.s_den = W("norm.s_den"); g.a_mean = W("norm.a_mean"); g.a_den = W("norm.a_den");
-    g.d_mean = W("norm.d_mean"); g.d_den = W("norm.d_den"); g.r_norm = W("norm.r"); g.ret_den = W("norm.ret_den");
+    g.s_mean = N("s_mean"); g.s_den = N("s_den"); g.a_mean = N("a_mean"); g.a_den = N("a_den");
+    g.d_mean = N("d_mean"); g.d_den = N("d_den"); g.r_norm = N("r"); g.ret_den = W("norm.ret_den");
     g.reward_coef = h->cfg.reward_loss_coef;
     return g;
 }
@@ -2175,7 +2200,7 @@ static void model_net_chunk(sacx_handle* h, int32_t model, const float* s, const
     const int S = h->S, A = h->A, ldQ = h->ldQ, Hm0 = h->Hm0, Hm1 = h->Hm1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     const std::string mn = "m" + std::to_string(model);
-    NetIOArgs g = netio_base(h);
+    NetIOArgs g = netio_base(h, true);
     g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s; g.a = a; g.X = W("roll.Xm");
     launch_net_io(g, h->stream);
     std::vector<Launch> pl;
@@ -2198,7 +2223,7 @@ int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const floa
     for (int64_t done = 0; done < n; done += ROLL_CAP) {
         const int m = (int)std::min<int64_t>(ROLL_CAP, n - done);
         model_net_chunk(h, model, s + done * S, a + done * h->A, m);
-        NetIOArgs g = netio_base(h);
+        NetIOArgs g = netio_base(h, true);
         g.mode = 2; g.n = m; g.s = s + done * S; g.O = h->f("roll.O"); g.ldO = S + 1;
         g.clip_d = delta_clip; g.clip_r = reward_clip;
         g.out0 = pred_out ? pred_out + done * (S + 1) : nullptr;
@@ -2220,7 +2245,7 @@ int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* 
     for (int64_t done = 0; done < n; done += ROLL_CAP) {
         const int m = (int)std::min<int64_t>(ROLL_CAP, n - done);
         model_net_chunk(h, model, s + done * S, a + done * A, m);      // _forward(s, a, clip=False)
-        NetIOArgs g = netio_base(h);
+        NetIOArgs g = netio_base(h, true);
         g.mode = 3; g.n = m; g.s = s + done * S; g.sp = sp + done * S; g.r = r + done;
         g.O = h->f("roll.O"); g.ldO = S + 1;
         g.clip_d = delta_clip_loss; g.clip_r = reward_clip_loss;
@@ -2252,8 +2277,9 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
             ra.s_out = s_out + c0 * horizon * S; ra.a_out = a_out + c0 * horizon * A;
             ra.r_out = r_out + c0 * horizon; ra.sp_out = sp_out + c0 * horizon * S; ra.d_out = d_out + c0 * horizon;
             ra.O = W("roll.O"); ra.a_raw = W("roll.A"); ra.X = W("roll.X"); ra.Xm = W("roll.Xm");
-            ra.s_mean = W("norm.s_mean"); ra.s_den = W("norm.s_den");
-            ra.d_mean = W("norm.d_mean"); ra.d_den = W("norm.d_den"); ra.r_norm = W("norm.r");
+            ra.s_mean = W("norm.s_mean"); ra.s_den = W("norm.s_den");          // the actor's
+            ra.ms_mean = W("mnorm.s_mean"); ra.ms_den = W("mnorm.s_den");      // the model's
+            ra.d_mean = W("mnorm.d_mean"); ra.d_den = W("mnorm.d_den"); ra.r_norm = W("mnorm.r");
             ra.clip_d = delta_clip; ra.clip_r = reward_clip;
             ra.mode = 0;
             launch_roll(ra, st);
@@ -2271,6 +2297,7 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
             a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
             a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
             a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+            a.ma_mean = W("mnorm.a_mean"); a.ma_den = W("mnorm.a_den");
             a.nseg = 1;
             // sample(): raw action to roll.A, normalised clip(a) (= a: |lim tanh| <= lim) into
             // the action columns of the model input
@@ -2348,8 +2375,10 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     DiagArgs d{};
     d.n = n; d.S = S; d.A = A; d.ldS = ldS; d.ldQ = ldQ;
     d.s_e = s_e; d.a_e = a_e; d.sp_e = sp_e; d.O = W("roll.O"); d.X = W("roll.X"); d.Xm = W("roll.Xm");
-    d.s_mean = W("norm.s_mean"); d.s_den = W("norm.s_den"); d.a_mean = W("norm.a_mean"); d.a_den = W("norm.a_den");
-    d.d_mean = W("norm.d_mean"); d.d_den = W("norm.d_den"); d.clip_d = delta_clip; d.out = out;
+    d.s_mean = W("norm.s_mean"); d.s_den = W("norm.s_den");                 // the actor's
+    d.ms_mean = W("mnorm.s_mean"); d.ms_den = W("mnorm.s_den");             // the models'
+    d.a_mean = W("mnorm.a_mean"); d.a_den = W("mnorm.a_den");
+    d.d_mean = W("mnorm.d_mean"); d.d_den = W("mnorm.d_den"); d.clip_d = delta_clip; d.out = out;
     // both models on the same n input rows: model k's rows land at [k n, (k+1) n)
     auto models = [&]() {
         std::vector<Launch> pl;
@@ -2380,6 +2409,7 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
         a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.ma_mean = W("mnorm.a_mean"); a.ma_den = W("mnorm.a_den");
         a.nseg = 1;
         a.seg[0] = {0, n, 1, 0, W("roll.noise"), W("roll.Xm"), nullptr, W("roll.A")};
         a.total_rows = n;

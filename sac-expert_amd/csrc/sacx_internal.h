@@ -128,6 +128,7 @@ struct HeadBwdArgs {
     int32_t ne, tqm;
     const float* mpart;
     const Ctl* ctl;         // epsilon (use_expert)
+    const float* ma_den;    // the world models' action normaliser (expert rows; --only_model_normalizer)
 };
 
 struct FinalArgs {
@@ -205,6 +206,9 @@ struct HeadArgs {
     int32_t H1, A, Aout, S, ldQ, per_state_std;
     float lim;
     const float *a_mean, *a_den;
+    // mode-1 (sample) segments write world-model inputs: their actions take the models'
+    // normaliser (SAC_expert.py:139-144 --only_model_normalizer; the same values otherwise)
+    const float *ma_mean, *ma_den;
     float logstd_init;     // mode 2: GaussianActor.logstd_init (continuous_actors.py:39-44)
     int32_t output_norm;   // mode 2: --actor_output_norm (continuous_actors.py:68-72)
     // nullable: the head's Ha2 . W3 as per-column-tile partials written by actor.fwd1 (rowk 5),
@@ -293,6 +297,7 @@ struct GatherArgs {
     int32_t nupd;          // consecutive slots gathered by this launch (blockIdx.y)
     int64_t slot_bytes;    // distance between consecutive slots' buffers
     const float *s_mean, *s_den, *a_mean, *a_den;
+    const float *ms_mean, *ms_den;   // the world models' state normaliser: Xm's state columns
     float* Xa;  int32_t ldS;   // actor rows [sp(B) ; s(B) ; s_e(ne)]
     float* Xq;  float* Xt; float* Xp; float* Xm; int32_t ldQ;
     float* r; float* d;
@@ -318,6 +323,7 @@ struct ActorBwdArgs {
     const float* Dm1;       // [ne, Hm0]
     const float* Wm1[2];    // W1_ext of the models [(S+A+1), Hm0]
     const float *a_den;
+    const float* ma_den;    // the world models' action normaliser (expert rows)
     const float* alpha;
     const Ctl* ctl;         // epsilon
     int32_t use_expert;
@@ -446,7 +452,8 @@ struct RollArgs {
     const float* O;             // model output [n, S+1] = [delta_n | r_n]
     const float* a_raw;         // actor sample [n, A]
     float* X; float* Xm;        // actor input [n, ldS], model input [n, ldQ] (columns < S)
-    const float *s_mean, *s_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den)
+    const float *s_mean, *s_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den); d / r: the model's
+    const float *ms_mean, *ms_den;   // the model's state normaliser (Xm); s_*: the actor's (X)
     float clip_d, clip_r;       // > 0: clip_by_value(-clip, clip) (delta_clip_pred / reward_clip_pred)
 };
 
@@ -460,7 +467,8 @@ struct DiagArgs {
     const float *s_e, *a_e, *sp_e;
     const float* O;             // [2n, S+1]
     float* X; float* Xm;        // actor input [n, ldS]; model input [n, ldQ]
-    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den;
+    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den;   // s: the actor's; a, d: the models'
+    const float *ms_mean, *ms_den;   // the models' state normaliser (Xm)
     float clip_d;
     float* out;
 };

@@ -128,9 +128,6 @@ class SAC_exp(SACBase):
         n = len(self._eps_log)
         if n == 0:
             return
-        cap = self.engine.cfg.stats_capacity
-        if n > cap:
-            raise RuntimeError("more updates than the statistics ring holds between flushes")
         st = self.engine.stats(n)
         for i in range(n):
             self.logger.log_train({"alpha_loss": np.float32(st[i, 3]), "p_loss": np.float32(st[i, 2]),
@@ -150,10 +147,15 @@ class SAC_exp(SACBase):
             self.engine.push_perms(idx[None, :])
         self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
         self._eps_log.append(self._eps_cur)
+        if len(self._eps_log) >= self.engine.cfg.stats_capacity:
+            self._flush_update_logs()        # the device ring is full (epsilon is constant within an episode)
 
     def _update_models(self):
         t0 = time.time()
         n_model = min(self.steps_total, self.model_buffer_size)   # model_data = last rows of the env data
+        if n_model > int(self.engine.ctl()["cur_size"]):
+            # model_data would hold rows the (smaller) replay ring already dropped
+            raise NotImplementedError("--model_buffer_size larger than --env_buffer_size")
         if n_model < self.model_batch_size:
             return
         base = int(self.engine.ctl()["cur_size"]) - n_model
@@ -197,34 +199,45 @@ class SAC_exp(SACBase):
 
     # ------------------------------------------------------------------ loop
     def train(self, total_timesteps, params):
+        """SAC_expert.py:685-824."""
         self._set_rms()
         self._collect_expert_data()
         checkpoints = self._checkpoints(total_timesteps)
-        ck = 0
+        eval_points = self._eval_points(total_timesteps)
+        ck = ev = 0
         num_timesteps = 0
+        if eval_points is not None:
+            self._evaluate(num_timesteps)
         num_timesteps += self._collect_env_data(num_timesteps, update_normalizers=self.update_normalizers,
                                                 only_model_normalizer=self.only_model_normalizer)
         episode_step, episode, episode_reward, done = 0, 0, 0.0, True
+        t_episode = time.time()
         obs, expert_reg = None, None
         while num_timesteps < total_timesteps:
             if done:
                 self._flush_update_logs()            # before epsilon can change
+                self._episode_normalizer_update(episode)      # :740-746
                 if episode > 0:
-                    self.logger.log_train({"J_tot": episode_reward, "steps": episode_step, "traj": 1})
+                    self.logger.log_train({"J_tot": episode_reward, "steps": episode_step, "traj": 1,
+                                           "time_env_data": time.time() - t_episode})
                 obs = self.env.reset()
                 done, episode_reward, episode_step = False, 0.0, 0
                 episode += 1
                 self._update_models()
                 expert_reg = self._expert_preprocess()
+                t_episode = time.time()
             a = self.actor.sample(obs, deterministic=not self.random_act).numpy()
             self._update(num_timesteps, expert_reg)
             next_obs, r, done, _ = self.env.step(self.actor.clip(a))
             done_no_max = False if episode_step + 1 == self._max_episode_steps else done
             episode_reward += r
-            self._add(obs[None], a[None], [r], next_obs[None], [float(done_no_max)])
+            self._add(obs[None], a[None], [r], next_obs[None], [float(done_no_max)], track_episode=True)
             obs = next_obs
             episode_step += 1
             num_timesteps += 1
+            if eval_points is not None and num_timesteps >= eval_points[ev]:
+                self._evaluate(num_timesteps)
+                ev = min(ev + 1, len(eval_points) - 1)
             if num_timesteps >= checkpoints[ck]:
                 self._dump_and_save(params)
                 ck = min(ck + 1, len(checkpoints) - 1)

@@ -33,6 +33,11 @@ class SACBase:
         self.logger = Logger()
         self.rng = np.random.default_rng(self.alg_seed)            # base_onpolicy_alg.py:108-109
         self.normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, self.init_rms_stats)
+        # the world models' own normaliser (SAC.py:51-52, SAC_expert.py:53-54): used by the models
+        # only with --only_model_normalizer (:139-144), updated by the collection and episode hooks
+        self.model_normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, self.init_rms_stats)
+        self._new_traj = []                 # the episode's transitions (new_traj, SAC_expert.py:49-51)
+        self.last_eval = 0
         self.engine = self._build_engine(alg_kwargs)
         self.steps_total = 0
         self.traj_total = 0
@@ -118,7 +123,7 @@ class SACBase:
         if self.use_expert:
             for i, m in enumerate(self.models):
                 m._bind(eng, f"m{i}")
-        self.normalizer.push_to(eng)
+        self._push_normalizers(eng)
         eng.rng_set_state(np.random.get_state())       # adopt the global stream
         return eng
 
@@ -131,16 +136,56 @@ class SACBase:
         finally:
             self.engine.rng_set_state(np.random.get_state())
 
-    # ------------------------------------------------------------------ data
-    def _set_rms(self):
-        for obj in [self.actor] + list(self.q_critics) + list(self.q_targets) + list(self.models or []):
-            obj.set_rms(self.normalizer)
-        self.normalizer.push_to(self.engine)
+    # ------------------------------------------------------------------ normalisers
+    def _models_normalizer(self):
+        """The normaliser the world models use (SAC_expert.py:139-144)."""
+        return self.model_normalizer if self.only_model_normalizer else self.normalizer
 
-    def _add(self, s, a, r, sp, d):
-        n = self.engine.append(np.asarray(s, np.float32), np.asarray(a, np.float32), np.asarray(r, np.float32),
-                               np.asarray(sp, np.float32), np.asarray(d, np.float32))
+    def _push_normalizers(self, eng=None):
+        """The device copies: norm.* from the shared normaliser, mnorm.* from the models' one."""
+        eng = eng if eng is not None else self.engine
+        self.normalizer.push_to(eng, which="main")
+        if self.use_expert:
+            self._models_normalizer().push_to(eng, which="model")
+
+    def _set_rms(self):
+        for obj in [self.actor] + list(self.q_critics) + list(self.q_targets):
+            obj.set_rms(self.normalizer)
+        for m in (self.models or []) if self.use_expert else []:
+            m.set_rms(self._models_normalizer())
+        self._push_normalizers()
+
+    def _update_rms_traj(self, s, a, r, sp, episode_hook=False):
+        """RunningNormalizers.update_rms on a trajectory: _collect_env_data (SAC_expert.py:646-650)
+        updates one normaliser; the per-episode hook (:740-746, SAC.py:309-315) updates the
+        shared normaliser and the models' (or only the models' with --only_model_normalizer)."""
+        if self.only_model_normalizer:
+            self.model_normalizer.update_rms(s, a, r, sp)
+        else:
+            self.normalizer.update_rms(s, a, r, sp)
+            if episode_hook:
+                self.model_normalizer.update_rms(s, a, r, sp)
+        self._push_normalizers()
+
+    def _episode_normalizer_update(self, episode):
+        """At an episode boundary (done, episode > 0): the episode's transitions into the
+        normalisers (new_traj.get_model_info(): s, a, r, sp in add order), then new_traj.reset()."""
+        if self.update_normalizers and episode > 0 and self._new_traj:
+            s, a, r, sp = (np.concatenate([t[i] for t in self._new_traj]) for i in range(4))
+            self._update_rms_traj(s, a, r, sp, episode_hook=True)
+        self._new_traj = []
+
+    # ------------------------------------------------------------------ data
+
+    def _add(self, s, a, r, sp, d, track_episode=False):
+        r64 = np.asarray(r, np.float64)
+        s, a, r, sp = (np.asarray(x, np.float32) for x in (s, a, r, sp))
+        n = self.engine.append(s, a, r, sp, np.asarray(d, np.float32))
         self.steps_total += n
+        if track_episode and self.update_normalizers:
+            # new_traj.add (SAC_expert.py:799-801): np.array([r]) keeps the env's float64 reward,
+            # which r_rms.update then merges in float64
+            self._new_traj.append((s, a, r64, sp))
 
     def _collect_env_data(self, num_timesteps, update_normalizers=True, only_model_normalizer=False):
         """SAC_expert.py:625-684: rollouts of the stochastic actor until the batch is full."""
@@ -151,8 +196,11 @@ class SACBase:
             horizon = min(batch_size - cur, self.env_horizon) if self.env_batch_type == "steps" else self.env_horizon
             s, a, r, sp, d, J = trajectory_sampler(self.env, self.actor, horizon, eval=True)
             if update_normalizers:
-                self.normalizer.update_rms(s, a, r, sp)
-                self.normalizer.push_to(self.engine)
+                if only_model_normalizer:
+                    self.model_normalizer.update_rms(s, a, r, sp)
+                else:
+                    self.normalizer.update_rms(s, a, r, sp)
+                self._push_normalizers()
             self._add(s, a, r, sp, d)
             self.traj_total += 1
             if horizon == self.env_horizon:
@@ -165,11 +213,21 @@ class SACBase:
         return steps_new
 
     def _evaluate(self, num_timesteps):
+        """base_onpolicy_alg.py:174-197: eval_num_traj deterministic rollouts in env_eval."""
+        t0 = time.time()
         J = []
         for _ in range(self.eval_num_traj):
             *_, Jt = trajectory_sampler(self.env_eval, self.actor, self.env_horizon, eval=True, deterministic=True)
             J.append(Jt)
-        self.logger.log_eval({"J_tot": float(np.mean(J)), "steps": num_timesteps})
+        self.logger.log_train({"J_tot_eval": float(np.mean(J)), "steps_eval": num_timesteps - self.last_eval,
+                               "time_eval": time.time() - t0})
+        self.last_eval = num_timesteps
+
+    def _eval_points(self, total_timesteps):
+        """SAC_expert.py:707-714: None without --eval_freq."""
+        if self.eval_freq is None:
+            return None
+        return np.concatenate((np.arange(0, total_timesteps, self.eval_freq)[1:], [total_timesteps]))
 
     # ------------------------------------------------------------------ update
     def _update(self, num_timesteps, expert_reg=None, ts_increment=1):

@@ -12,9 +12,13 @@ import pickle
 import numpy as np
 
 # (module, name) globals a log may reference: NumPy's array / scalar reconstruction
-# (numpy 1.x pickles name numpy.core, numpy 2.x numpy._core)
+# (numpy 1.x pickles name numpy.core, numpy 2.x numpy._core); protocol 5 pickles contiguous
+# arrays through numeric._frombuffer, which only builds an array from bytes
 _ALLOWED = {(m, n) for m in ("numpy.core.multiarray", "numpy._core.multiarray")
-            for n in ("_reconstruct", "scalar")} | {("numpy", "ndarray"), ("numpy", "dtype")}
+            for n in ("_reconstruct", "scalar")} | {("numpy", "ndarray"), ("numpy", "dtype")} | \
+           {(m, "_frombuffer") for m in ("numpy.core.numeric", "numpy._core.numeric")}
+# written with protocol 4 so the file does not depend on the interpreter's default protocol
+PICKLE_PROTOCOL = 4
 
 
 class _LogUnpickler(pickle.Unpickler):
@@ -50,10 +54,6 @@ class Logger:
                 ens.setdefault(k, []).append(v)
         self.log_train({k: np.array(v) for k, v in ens.items()})
 
-    def log_eval(self, kv):
-        """_evaluate's record (base_onpolicy_alg.py:190-195: J_tot_eval / steps_eval / time_eval)."""
-        self.log_train({f"{k}_eval": v for k, v in kv.items()})
-
     def log_params(self, kv):
         for k, v in kv.items():
             self.param_dict[k] = v
@@ -67,16 +67,22 @@ class Logger:
                 "final": self.final_dict}
 
     def dump_and_save(self, log_path, log_name):
-        """Writes ``{'param', 'train', 'final'}``; train arrays already in the file come first."""
+        """Writes ``{'param', 'train', 'final'}``; train arrays already in the file come first.
+        An existing file that cannot be read (or merged) is overwritten, as the reference's
+        bare ``except: pass`` does (``logger.py:71-83``)."""
         out = self.dump()
         os.makedirs(log_path, exist_ok=True)
         filename = os.path.join(log_path, log_name)
-        if os.path.exists(filename):
+        try:
             old = load_log(filename)
+            merged = dict(out["train"])
             for k, v in old["train"].items():
-                out["train"][k] = np.concatenate((v, out["train"][k]), axis=0) if k in out["train"] else v
+                merged[k] = np.concatenate((v, out["train"][k]), axis=0) if k in out["train"] else v
+            out["train"] = merged
+        except (OSError, EOFError, pickle.UnpicklingError, KeyError, TypeError, ValueError, AttributeError):
+            pass
         with open(filename, "wb") as fh:
-            pickle.dump(out, fh)
+            pickle.dump(out, fh, protocol=PICKLE_PROTOCOL)
         return filename
 
     def reset(self):

@@ -7,14 +7,17 @@ import numpy as np
 
 
 def discounted_sum(x, rate):
-    """buffer_utils.discounted_sum: y_t = x_t + rate * y_{t+1}."""
+    """buffer_utils.discounted_sum (buffer_utils.py:8-9): y_t = x_t + rate * y_{t+1}, in
+    float64 as scipy.signal.lfilter returns it (its direct form computes the same products and
+    sums), so ret_rms merges the float64 returns the reference's does."""
     x = np.asarray(x, dtype=np.float64)
     y = np.zeros_like(x)
     acc = 0.0
+    rate = float(rate)
     for t in range(len(x) - 1, -1, -1):
         acc = x[t] + rate * acc
         y[t] = acc
-    return y.astype(np.float32)
+    return y
 
 
 class RunningNormalizer:
@@ -99,12 +102,13 @@ class RunningNormalizers:
     def get_rms_stats(self):
         return {k: getattr(self, k).get_stats() for k in ("s_rms", "a_rms", "r_rms", "delta_rms", "ret_rms")}
 
-    def push_to(self, engine):
-        """Writes the derived vectors the kernels use into the engine."""
+    def push_to(self, engine, which: str = "all"):
+        """Writes the derived vectors the kernels use into the engine (which: "all", "main" =
+        the actor's / critics' set, "model" = the world models' set; Engine.set_normalizers)."""
         f = lambda x, n: np.broadcast_to(np.asarray(x, np.float32), (n,))
         S, A = engine.cfg.s_dim, engine.cfg.a_dim
         engine.set_normalizers(f(self.s_rms.mean, S), f(self.s_rms.den(), S), f(self.a_rms.mean, A),
                                f(self.a_rms.den(), A), f(self.delta_rms.mean, S), f(self.delta_rms.den(), S),
                                float(np.asarray(self.r_rms.mean).reshape(-1)[0]),
                                float(np.asarray(self.r_rms.den()).reshape(-1)[0]),
-                               float(np.asarray(self.ret_rms.den()).reshape(-1)[0]))
+                               float(np.asarray(self.ret_rms.den()).reshape(-1)[0]), which=which)

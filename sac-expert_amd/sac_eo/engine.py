@@ -221,6 +221,10 @@ class Engine:
         for k in ("norm.s_den", "norm.a_den", "norm.d_den", "norm.ret_den"):
             v[k].fill_(1.0)
         v["norm.r"][0, 1] = 1.0
+        if "mnorm.r" in v:                       # the world models' normaliser set (SAC-EO)
+            for k in ("mnorm.s_den", "mnorm.a_den", "mnorm.d_den"):
+                v[k].fill_(1.0)
+            v["mnorm.r"][0, 1] = 1.0
         v["alpha"].fill_(float(np.float32(np.log(cfg.init_temperature))))   # SAC_expert.py:106
         if cfg.actor_layer_norm:
             v["actor.ln"][0].fill_(1.0)                                      # gamma = 1, beta = 0
@@ -265,19 +269,28 @@ class Engine:
         return float(self.v["alpha"].item())
 
     def set_normalizers(self, s_mean, s_den, a_mean, a_den, d_mean=None, d_den=None,
-                        r_mean=0.0, r_den=1.0, ret_den=1.0):
-        """Values of RunningNormalizer.normalize: mean and max(std, 1e-8) (normalizer.py:26-41)."""
+                        r_mean=0.0, r_den=1.0, ret_den=1.0, which: str = "all"):
+        """Values of RunningNormalizer.normalize: mean and max(std, 1e-8) (normalizer.py:26-41).
+
+        which = "main": the set the actor and critics use (norm.*); "model": the world models'
+        set (mnorm.*, SAC-EO; SAC_expert.py:139-144 gives the models their own normaliser with
+        --only_model_normalizer); "all": both (the reference's shared normaliser)."""
+        if which not in ("all", "main", "model"):
+            raise ValueError("which must be 'all', 'main' or 'model'")
         v = self.v
         S, A = self.cfg.s_dim, self.cfg.a_dim
         put = lambda k, x, n: v[k].copy_(torch.as_tensor(np.array(x, np.float32).reshape(1, n)))
-        put("norm.s_mean", s_mean, S)
-        put("norm.s_den", s_den, S)
-        put("norm.a_mean", a_mean, A)
-        put("norm.a_den", a_den, A)
-        put("norm.d_mean", np.zeros(S) if d_mean is None else d_mean, S)
-        put("norm.d_den", np.ones(S) if d_den is None else d_den, S)
-        v["norm.r"].copy_(torch.tensor([[np.float32(r_mean), np.float32(r_den)]]))
-        v["norm.ret_den"].fill_(float(np.float32(ret_den)))
+        pres = (["norm."] if which != "model" else []) + (["mnorm."] if which != "main" and "mnorm.r" in v else [])
+        for p in pres:
+            put(p + "s_mean", s_mean, S)
+            put(p + "s_den", s_den, S)
+            put(p + "a_mean", a_mean, A)
+            put(p + "a_den", a_den, A)
+            put(p + "d_mean", np.zeros(S) if d_mean is None else d_mean, S)
+            put(p + "d_den", np.ones(S) if d_den is None else d_den, S)
+            v[p + "r"].copy_(torch.tensor([[np.float32(r_mean), np.float32(r_den)]]))
+        if which != "model":
+            v["norm.ret_den"].fill_(float(np.float32(ret_den)))
 
     def reset_optimizers(self):
         self.v["adam_m"].zero_()
@@ -573,7 +586,8 @@ class Engine:
 
     def reset_model_optimizer(self):
         """--reset_model_optimizer (SAC_expert.py:553-555): fresh Adam state for the models."""
-        for net in ("m0", "m1"):
+        for k in range(int(self.cfg.num_models or 2)):
+            net = f"m{k}"
             for i in range(3):
                 seg = self.segments[f"{net}.l{i}"]
                 o, n = seg["offset"] // 4, seg["rows"] * seg["cols"]

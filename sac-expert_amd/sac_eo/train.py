@@ -102,7 +102,7 @@ def main(argv=None):
         ([args.save_file] if args.save_file is not None else []) + [date]
     save_filefull = os.path.join(args.save_path, "_".join(parts))
     with open(save_filefull, "wb") as fh:
-        pickle.dump(outputs, fh)
+        pickle.dump(outputs, fh, protocol=4)
     for r in sorted(names):
         os.remove(os.path.join(args.save_path, names[r]))
     print(f"done: {save_filefull} in {(datetime.now() - start).total_seconds():.1f}s", flush=True)

@@ -1,0 +1,153 @@
+"""The drop-in TRAINING LOOP against an oracle-driven restatement of it.
+
+``SAC_exp.train`` (sac_eo/algs/SAC_expert.py:685-824) and ``SAC.train`` (sac_eo/algs/SAC.py:254-385)
+run on the device (``sac_eo.algs``: behaviour actions, replay appends, gradient steps, model
+fits and expert diagnostics through libsacx) and on the CPU (``oracle/sac_loop.py``: the same
+loop over ``sac_oracle`` in fp64), on the same synthetic environments, initial weights, global
+NumPy stream and expert-permutation Generator.  Compared:
+
+* every update's Q1 / Q2 / policy / alpha loss (relative to the trajectory's scale),
+* the global NumPy stream (MT19937 key, position, cached gauss) at every episode boundary,
+  bit for bit -- it carries the sampler, the actor noise, the model-fit shuffles, the expert
+  batch draw and the counterfactual actions of the diagnostics in the reference's order,
+* SAC-EO's per-episode expert MSE diagnostics and last model-fit loss,
+* with ``--update_normalizers`` (per-trajectory merge during the initial collection, per-episode
+  merge of new_traj, :740-746) and ``--only_model_normalizer`` (the world models on their own
+  normaliser, :53-54 / :139-144 / :646-650), whose normaliser statistics must also agree.
+"""
+import numpy as np
+import pytest
+
+import sac_oracle as O
+from sac_loop import LoopOracle
+
+pytestmark = pytest.mark.gpu
+
+EP_LEN = 40          # synthetic episodes end (done) after EP_LEN steps
+INIT = 200           # --env_batch_size_init
+LOSS_TOL = 1e-4      # north_star: Q-loss trajectory within 1e-4 relative
+
+
+def _build(alg, flags, seed=7):
+    """The construction sequence of sac_eo/train.py:28-59 with short synthetic episodes."""
+    from sac_eo.actors import init_actor
+    from sac_eo.algs import init_alg
+    from sac_eo.common.seeding import derive_seeds, init_seeds
+    from sac_eo.common.train_parser import create_train_parser, gather_inputs
+    from sac_eo.critics import init_critics
+    from sac_eo.envs.synthetic import SyntheticEnv
+    from sac_eo.models import init_world_models
+    total = INIT + 3 * EP_LEN
+    argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", "64", "64",
+            "--critic_layers", "64", "64", "--actor_activations", "relu", "--critic_activations", "relu",
+            "--model_layers", "64", "64", "--total_timesteps", str(total), "--env_batch_size_init", str(INIT),
+            "--env_horizon", "100", "--sac_batch_size", "64", "--model_batch_size", "50", "--model_num_epochs", "2",
+            "--seed", str(seed)] + flags
+    d = gather_inputs(create_train_parser().parse_args(argv))
+    d["actor_kwargs"]["actor_squash"] = True
+    sd = derive_seeds(seed, 1, 0)
+    ak = dict(d["alg_kwargs"], alg_seed=int(sd["algorithm"][0]), save_path="/tmp/sacx_loop_test")
+    init_seeds(int(sd["setup"][0]))
+    envs = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=EP_LEN) for _ in range(3)]
+    actor = init_actor(envs[0], **dict(d["actor_kwargs"], actor_weights=None))
+    expert = init_actor(envs[0], **dict(d["actor_kwargs"], actor_weights=None))
+    critics, q_targets, q_critics = init_critics(envs[0], **dict(d["critic_kwargs"], critic_weights=None))
+    models = init_world_models(envs[0], **dict(d["model_kwargs"], model_weights=None, reward_weights=None),
+                               model_setup_kwargs=d["model_setup_kwargs"])
+    init_seeds(int(sd["eval"][0]), envs[1])
+    init_seeds(int(sd["sim"][0]), envs[0])
+    init_seeds(int(sd["expert"][0]), envs[2])
+    alg_obj = init_alg(0, envs[0], envs[1], envs[2], actor, critics, q_targets, q_critics, models, ak,
+                       d["mf_update_kwargs"], expert, None)
+    # what the oracle starts from: the bound weights, the global stream, fresh env copies
+    oenvs = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=EP_LEN) for _ in range(3)]
+    oenvs[0].seed(int(sd["sim"][0]))
+    oenvs[2].seed(int(sd["expert"][0]))
+    return alg_obj, d, ak, total, oenvs, np.random.get_state()
+
+
+def _oracle_state(alg_obj, ocfg):
+    aw = alg_obj.actor.get_weights()
+    q = [c.get_weights() for c in alg_obj.q_critics]
+    qt = [t.get_weights() for t in alg_obj.q_targets]
+    alpha = np.asarray(np.float32(np.log(ocfg.init_temperature)), np.float32)     # SAC_expert.py:106
+    st = O.SACState(aw[:-1], aw[-1], q, qt, alpha, O.AdamState.zeros_like(aw),
+                    [O.AdamState.zeros_like(n) for n in q], O.AdamState.zeros_like([alpha]))
+    if alg_obj.use_expert:
+        st.models = [m.get_weights() for m in alg_obj.models]
+        st.opt_model = O.AdamState.zeros_like([w for m in st.models for w in m])
+    return st.astype(np.float64)
+
+
+def _series_err(dev, ref):
+    return float(np.max(np.abs(dev - ref)) / max(np.max(np.abs(ref)), 1e-30))
+
+
+def _same_stream(a, b):
+    return np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
+
+
+@pytest.mark.parametrize("alg,flags", [
+    ("sac_imit", []),
+    ("sac_imit", ["--update_normalizers"]),
+    ("sac_imit", ["--update_normalizers", "--only_model_normalizer"]),
+    ("sac", []),
+    ("sac", ["--update_normalizers"]),
+])
+def test_train_loop_matches_oracle(gpu_available, alg, flags):
+    alg_obj, d, ak, total, oenvs, rs_state = _build(alg, flags)
+    S, A = alg_obj.s_dim, alg_obj.a_dim
+    ocfg = O.Config(S=S, A=A, hidden=(64, 64), act="relu", B=64, gamma=ak["gamma"], tau=ak["soft_tau"],
+                    lr_q=ak["q_crit_lr"], lr_pi=ak["mbpo_actor_lr"], lr_alpha=ak["mbpo_alpha_lr"],
+                    init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(64, 64),
+                    model_act="relu", lr_model=ak["model_lr"])
+    st = _oracle_state(alg_obj, ocfg)
+    ex = alg_obj.expert.get_weights()
+    expert = ([np.asarray(w, np.float64) for w in ex[:-1]], np.asarray(ex[-1], np.float64))
+    # the device loop, with the global stream recorded at every episode boundary
+    dev_rng = []
+    hook = alg_obj._episode_normalizer_update
+
+    def rec(episode):
+        dev_rng.append(alg_obj.engine.rng_get_state())
+        return hook(episode)
+    alg_obj._episode_normalizer_update = rec
+    name = alg_obj.train(total, d)
+    dev_rng.append(alg_obj.engine.rng_get_state())
+    n_upd = alg_obj.engine.ctl()["step_seq"]
+    dev = alg_obj.engine.stats(n_upd)
+    ok = dict(ak, num_models=d["model_kwargs"]["num_models"])
+    orc = LoopOracle(alg, ocfg, st, oenvs[0], oenvs[2], expert, ok, rs_state, ak["alg_seed"],
+                     max_episode_steps=1000).train(total)
+    ref = np.array([[u["q1_loss"], u["q2_loss"], u["p_loss"], u["alpha_loss"]] for u in orc.update_stats])
+    assert dev.shape[0] == ref.shape[0], (dev.shape, ref.shape)
+    errs = [_series_err(dev[:, c], ref[:, c]) for c in range(4)]
+    print(f"{alg} {flags}: {n_upd} updates, errors q1 {errs[0]:.2e} q2 {errs[1]:.2e} p {errs[2]:.2e} "
+          f"alpha {errs[3]:.2e}")
+    assert len(dev_rng) == len(orc.episode_rng)
+    for i, (a, b) in enumerate(zip(dev_rng, orc.episode_rng)):
+        assert _same_stream(a, b), f"global stream differs at episode boundary {i}"
+    assert max(errs[:3]) < LOSS_TOL, errs
+    assert errs[3] < 10 * LOSS_TOL, errs
+    if "--update_normalizers" in flags:
+        for which in ("normalizer", "model_normalizer"):
+            mine, theirs = getattr(alg_obj, which), getattr(orc, which)
+            for kk in ("s_rms", "a_rms", "r_rms", "delta_rms", "ret_rms"):
+                a, b = getattr(mine, kk), getattr(theirs, kk)
+                assert a.t_last == b.t_last, (which, kk)
+                np.testing.assert_allclose(np.asarray(a.mean, np.float64), np.asarray(b.mean, np.float64),
+                                           rtol=1e-5, atol=1e-6, err_msg=f"{which}.{kk}")
+                np.testing.assert_allclose(np.asarray(a.var, np.float64), np.asarray(b.var, np.float64),
+                                           rtol=1e-4, atol=1e-6, err_msg=f"{which}.{kk}")
+    if alg == "sac_imit":
+        from sac_eo.common.logger import load_log
+        import os
+        log = load_log(os.path.join(ak["save_path"], name))
+        dd = np.asarray(log["train"]["model_MSE_on_expert_data"], np.float64)
+        dc = np.asarray(log["train"]["model_MSE_on_expert_counterfactual_action"], np.float64)
+        od = np.array(orc.diag)
+        assert len(dd) == len(od)
+        np.testing.assert_allclose(dd, od[:, 0], rtol=1e-4)
+        np.testing.assert_allclose(dc, od[:, 1], rtol=1e-4)
+        os.remove(os.path.join(ak["save_path"], name))
+    alg_obj.engine.close()

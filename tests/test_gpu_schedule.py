@@ -5,10 +5,13 @@ the graph_steps = 8 tests.
 
 * 300 updates (two 128-update graphs + one 44-update remainder graph) vs the fp64 oracle:
   Q1/Q2 losses and the policy loss (which carries SAC-EO's expert MSE, relative to the
-  trajectory's scale) within 1e-4 over the first 100 updates (north_star) and TRAJ_TOL_300
-  over all 300, weights / targets after 100 and 300 updates within PARAM_TOL_100 /
-  PARAM_TOL_300 (norm-relative per tensor), the update sequence numbers and the RNG stream
-  exact.
+  trajectory's scale) within 1e-4 over the first 100 updates (north_star).  Beyond, the bar
+  is set by the drift a faithful fp32 execution has: the same oracle run in fp32 (op-by-op
+  TF fp32 emulation) on the same inputs, whose distance from the fp64 run grows along the
+  trajectory (Adam's m / sqrt(v) turns rounding-level gradient differences into lr-sized
+  steps).  Device error <= DRIFT_FACTOR x that fp32 drift + 1e-5, for the losses over all
+  300 updates and for every weight / target tensor after 100 and 300 updates; the update
+  sequence numbers and the RNG stream exact.
 * graph replay == eager launches, bit for bit, at SACX_NBATCH 2 / 4 / 8 (± expert).
 * 8 packed seeds at graph_steps = 128 == 8 one-seed engines, bit for bit.
 Reference: SAC_exp._update (sac_eo/algs/SAC_expert.py:463-477), SAC._update (SAC.py:236-250).
@@ -21,18 +24,20 @@ from helpers import load_learner, make_learner, make_pair, oracle_step
 
 pytestmark = pytest.mark.gpu
 
-PARAM_TOL_100 = 1e-4    # ||w_dev - w_oracle|| / ||w_oracle|| per tensor after 100 updates
-PARAM_TOL_300 = 1e-2    # ... after 300 (fp32 vs fp64 rounding compounded through Adam)
-TRAJ_TOL_300 = 3e-3     # Q / policy loss over all 300 updates (fp32 device vs fp64 oracle)
+DRIFT_FACTOR = 2.0      # device error <= DRIFT_FACTOR x (fp32 oracle - fp64 oracle) + 1e-5
 
 
-def _params_close(eng, st, use_expert):
-    nets = [("actor", st.actor)] + [(f"q{k}", st.q[k]) for k in range(2)] + [(f"t{k}", st.q_targ[k]) for k in range(2)]
-    worst = 0.0
-    for name, ref in nets:
-        for a, b in zip(eng.get_net(name), ref):
-            worst = max(worst, float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)))
-    return worst
+def _net_lists(st):
+    return [st.actor] + [st.q[k] for k in range(2)] + [st.q_targ[k] for k in range(2)]
+
+
+def _params_err(got_lists, st):
+    """per tensor ||w - w_fp64|| / ||w_fp64|| for the actor, critics and targets"""
+    out = []
+    for got, ref in zip(got_lists, _net_lists(st)):
+        for a, b in zip(got, ref):
+            out.append(float(np.linalg.norm(np.asarray(a, np.float64) - b) / max(np.linalg.norm(b), 1e-30)))
+    return np.array(out)
 
 
 @pytest.mark.parametrize("use_expert", [False, True])
@@ -41,6 +46,7 @@ def test_production_schedule_trajectory_300(gpu_available, use_expert):
     B, steps = 256, 300
     eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=13, use_expert=use_expert, done_p=0.01,
                                                 graph_steps=128)
+    st32 = st.astype(np.float32)                        # the fp32 execution the bar is set by
     N = buf["r"].shape[0]
     rs = np.random.RandomState(321)
     gen = np.random.default_rng(78)
@@ -48,7 +54,7 @@ def test_production_schedule_trajectory_300(gpu_available, use_expert):
     Rs = [O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=20 if use_expert else 0, gen=gen) for _ in range(steps)]
     if use_expert:
         eng.push_perms(np.stack([R["perm"] for R in Rs]))
-    ref = []
+    ref, ref32 = [], []
     for part in (100, 200):
         eng.prepare(part)
         eng.step(part, num_timesteps=len(ref), ts_increment=1)
@@ -56,27 +62,30 @@ def test_production_schedule_trajectory_300(gpu_available, use_expert):
         for R in Rs[len(ref):len(ref) + part]:
             o = oracle_step(st, ocfg, nrm, buf, R, expert)
             ref.append([o["q1_loss"], o["q2_loss"], o["p_loss"], o["alpha_loss"]])
-        worst = _params_close(eng, st, use_expert)
-        print(f"weights after {len(ref)} updates: worst ||dev - oracle|| / ||oracle|| per tensor {worst:.2e}")
-        assert worst < (PARAM_TOL_100 if len(ref) == 100 else PARAM_TOL_300), (len(ref), worst)
+            o32 = oracle_step(st32, ocfg, nrm, buf, R, expert)
+            ref32.append([o32["q1_loss"], o32["q2_loss"], o32["p_loss"], o32["alpha_loss"]])
+        e_dev = _params_err([eng.get_net(n) for n in ("actor", "q0", "q1", "t0", "t1")], st)
+        e_32 = _params_err(_net_lists(st32), st)
+        print(f"weights after {len(ref)} updates: worst per-tensor error device {e_dev.max():.2e}, "
+              f"fp32 oracle {e_32.max():.2e}")
+        assert np.all(e_dev <= DRIFT_FACTOR * e_32 + 1e-5), (len(ref), e_dev.max(), e_32.max())
     dev = eng.stats(steps)
-    ref = np.array(ref)
-    rel_q = np.abs(dev[:, :2] - ref[:, :2]) / np.abs(ref[:, :2])
-    rel_p = np.abs(dev[:, 2] - ref[:, 2]) / np.max(np.abs(ref[:, 2]))
-    # alpha loss relative to the trajectory's scale: once alpha sits at its 1e-5 clamp the loss
-    # is ~1e-5 and its pointwise relative error says nothing
-    rel_a = np.abs(dev[:, 3] - ref[:, 3]) / np.max(np.abs(ref[:, 3]))
+    ref, ref32 = np.array(ref), np.array(ref32)
+    # losses relative to each series' scale (alpha's loss sits near 1e-5 once alpha reaches its
+    # clamp, so a pointwise relative error says nothing there)
+    scale = np.max(np.abs(ref), axis=0)
+    err = np.abs(dev[:, :4] - ref) / scale
+    err32 = np.abs(ref32 - ref) / scale
     for lo in range(0, steps, 50):
-        print(f"updates {lo}-{lo + 49}: q {rel_q[lo:lo + 50].max():.2e} p {rel_p[lo:lo + 50].max():.2e} "
-              f"alpha {rel_a[lo:lo + 50].max():.2e}")
-    # the north_star bar over the first 100 updates; beyond, fp32-vs-fp64 rounding compounds
-    # through the Adam steps and alpha's clamp (a schedule fault -- a stale or overwritten
+        print(f"updates {lo}-{lo + 49}: device q {err[lo:lo + 50, :2].max():.2e} p {err[lo:lo + 50, 2].max():.2e} "
+              f"alpha {err[lo:lo + 50, 3].max():.2e} | fp32 oracle q {err32[lo:lo + 50, :2].max():.2e} "
+              f"p {err32[lo:lo + 50, 2].max():.2e} alpha {err32[lo:lo + 50, 3].max():.2e}")
+    # the north_star bar over the first 100 updates (a schedule fault -- a stale or overwritten
     # slot -- shows as 1e-2 to 1e-1 from the update it hits, see the slot-ring fix)
-    assert rel_q[:100].max() < 1e-4, rel_q[:100].max()
-    assert rel_p[:100].max() < 1e-4, rel_p[:100].max()
-    assert rel_q.max() < TRAJ_TOL_300, rel_q.max()
-    assert rel_p.max() < TRAJ_TOL_300, rel_p.max()
-    assert rel_a.max() < 1e-3, rel_a.max()
+    assert err[:100, :3].max() < 1e-4, err[:100, :3].max()
+    # then the fp32 execution's own drift, per loss series, as the bound
+    for c in range(4):
+        assert err[:, c].max() <= DRIFT_FACTOR * err32[:, c].max() + 1e-5, (c, err[:, c].max(), err32[:, c].max())
     assert np.array_equal(dev[:, 7], np.arange(steps, dtype=np.float32))      # update sequence numbers
     got, exp = eng.rng_get_state(), rs.get_state()
     assert np.array_equal(got[1], exp[1]) and got[2] == exp[2] and got[3] == exp[3] and got[4] == exp[4]

@@ -113,3 +113,28 @@ def test_expert_import_per_state_std_and_ignore_key(tmp_path):
     for k in ("a", "r", "delta", "ret"):
         flat.update({f"{k}_t": 1, f"{k}_mean": np.zeros(1), f"{k}_var": np.ones(1)})
     assert set(organize_rms_inputs(flat)) == {"s_rms", "a_rms", "r_rms", "delta_rms", "ret_rms"}
+
+
+def test_protocol5_log_round_trip_and_unreadable_file(tmp_path):
+    """A log pickled with protocol 5 (numpy arrays through numeric._frombuffer) loads through
+    the allow-list; our own writer uses protocol 4; an unreadable existing file is overwritten
+    (the reference's ``except: pass``, logger.py:71-83)."""
+    p = os.path.join(tmp_path, "p5")
+    arr = np.arange(12, dtype=np.float32).reshape(3, 4)
+    with open(p, "wb") as fh:
+        pickle.dump({"param": {}, "train": {"x": arr}, "final": {"w": [arr.T.copy()]}}, fh, protocol=5)
+    log = load_log(p)
+    assert np.array_equal(log["train"]["x"], arr) and np.array_equal(log["final"]["w"][0], arr.T)
+    lg = Logger()
+    lg.log_train({"x": np.ones(4, np.float32)})
+    lg.dump_and_save(str(tmp_path), "p5")                 # appends to the protocol-5 file
+    assert load_log(p)["train"]["x"].shape == (4, 4)
+    with open(p, "rb") as fh:
+        assert fh.read(2) == b"\x80\x04"                  # protocol 4 header
+    bad = os.path.join(tmp_path, "bad")
+    with open(bad, "wb") as fh:
+        fh.write(b"not a pickle")
+    lg = Logger()
+    lg.log_train({"y": 1.0})
+    lg.dump_and_save(str(tmp_path), "bad")
+    assert list(load_log(bad)["train"]["y"]) == [1.0]
