@@ -257,13 +257,32 @@ def softplus(x):
 # ---------------------------------------------------------------------------
 # MLP (Keras Dense: y = act(x @ W + b))
 # ---------------------------------------------------------------------------
+# Summation order of the fp32 forward products.  Every order is a faithful fp32 execution of
+# the reference's Dense layers (TF's kernels fix none of them); tests/test_gpu_schedule.py runs
+# the fp32 oracle under each to get the envelope of the drift a faithful fp32 run has from fp64.
+MATMUL_ORDERS = ("default", "reversed", "split4")
+MATMUL_ORDER = "default"
+
+
+def matmul(h, w):
+    if h.dtype != np.float32 or MATMUL_ORDER == "default":
+        return h @ w
+    if MATMUL_ORDER == "reversed":                   # k accumulated from the last row of w
+        return np.ascontiguousarray(h[:, ::-1]) @ np.ascontiguousarray(w[::-1])
+    if MATMUL_ORDER == "split4":                     # four k slabs, summed pairwise (k_gemm's 4 waves)
+        c = (w.shape[0] + 3) // 4
+        p = [h[:, i * c:(i + 1) * c] @ w[i * c:(i + 1) * c] for i in range(4)]
+        return (p[0] + p[1]) + (p[2] + p[3])
+    raise ValueError(MATMUL_ORDER)
+
+
 def mlp_forward(params, x, act):
     hs = []
     h = x
     nl = len(params) // 2
     out = None
     for l in range(nl):
-        z = h @ params[2 * l] + params[2 * l + 1]
+        z = matmul(h, params[2 * l]) + params[2 * l + 1]
         if l < nl - 1:
             h = act_fwd(z, act[l] if isinstance(act, (list, tuple)) else act)
             hs.append(h)
@@ -580,9 +599,10 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
     m_ent = np.mean(-nlp_3 + F(cfg.target_entropy))
     stats["alpha_loss"] = float(-alpha * m_ent)
     g_alpha = np.asarray(-m_ent, dt)
-    al = [st.alpha]
+    # a 0-d ARRAY, updated in place by adam_step (a NumPy scalar would be rebound, not updated)
+    al = [np.array(st.alpha, dtype=dt)]
     adam_step(al, hook("alpha", [g_alpha]), st.opt_alpha, cfg.lr_alpha, dt)
-    st.alpha = np.maximum(st.alpha, F(1e-5)).astype(dt)
+    st.alpha = np.array(np.maximum(al[0], F(1e-5)), dtype=dt)
     stats["alpha"] = float(st.alpha)
     if keep is not None:
         keep.update(nlp_3=nlp_3, g_alpha=g_alpha)

@@ -102,8 +102,10 @@ def test_train_loop_matches_oracle(gpu_available, alg, flags):
                     init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(64, 64),
                     model_act="relu", lr_model=ak["model_lr"])
     st = _oracle_state(alg_obj, ocfg)
-    ex = alg_obj.expert.get_weights()
-    expert = ([np.asarray(w, np.float64) for w in ex[:-1]], np.asarray(ex[-1], np.float64))
+    expert = None
+    if alg == "sac_imit":
+        ex = alg_obj.expert.get_weights()
+        expert = ([np.asarray(w, np.float64) for w in ex[:-1]], np.asarray(ex[-1], np.float64))
     # the device loop, with the global stream recorded at every episode boundary
     dev_rng = []
     hook = alg_obj._episode_normalizer_update
