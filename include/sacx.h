@@ -23,9 +23,9 @@
  * sacx_seed_stride() bytes apart, each laid out as sacx_layout() describes.
  * sacx_sac_step advances all K in the same kernel launches (grid z = seed).
  * The data-path and RNG calls (append, expert rows, permutations, RNG state,
- * actor_act, rollout, expert_diag, resync) address the seed chosen with
- * sacx_seed_select (default 0).  sacx_model_fit and the data-parallel mode
- * need K = 1.
+ * actor_act, rollout, expert_diag, model_fit, resync) address the seed chosen with
+ * sacx_seed_select (default 0); the *_seeds forms address every seed at once.
+ * The data-parallel mode needs K = 1.
  */
 #ifndef SACX_H
 #define SACX_H
@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 5
+#define SACX_ABI_VERSION 6
 
 typedef struct sacx_handle sacx_handle;
 
@@ -103,6 +103,11 @@ typedef struct sacx_config {
     /* --- ABI 5 --- */
     float delta_clip_pred;      /* --delta_clip_pred: MSEModel.sample clips the normalised delta prediction
                                    (base_world_model.py:80-82) in the SAC-EO expert term; <= 0: None */
+    /* --- ABI 6 --- */
+    int32_t single_seed_plan;   /* packed seeds: 1 = every seed runs the launch plan of a one-seed handle
+                                   (tile shapes, folds, fused heads), so each is bit-identical to its
+                                   one-seed run (sac_eo.train --runs in lock-step); 0 = the packed plan
+                                   (32x32 tiles from 1,024 rows, separate heads at >= 4 seeds: faster) */
 } sacx_config;
 
 typedef struct sacx_segment {
@@ -206,6 +211,14 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
  * buffer (the normaliser reads obs and the head writes actions in place).  Synchronous: waits
  * for the bound stream (and so for any queued update) before returning the actions. */
 int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
+/* Both for EVERY seed of a packed handle in one launch chain: K runs of the reference's
+ * --runs (sac_eo/train.py:118-152) stepping their env loops in lock-step hand over n rows each.
+ * Arrays are [seeds, n, ...] in seed order; each seed appends to its own ring / acts with its
+ * own actor, normaliser and RNG stream (as sacx_seed_select + the calls above would, seed by
+ * seed).  act: n <= 16 rows per seed, no --actor_layer_norm. */
+int sacx_buffer_append_host_seeds(sacx_handle* h, const float* s, const float* a, const float* r,
+                                  const float* sp, const float* d, int64_t n);
+int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
 
 /* --- the reference objects' standalone network calls (device rows in, device rows out) -- */
 /* SquashedGaussianActor.evaluate (sac_eo/actors/continuous_actors.py:327-379) on s[n,S]:
@@ -275,6 +288,15 @@ int sacx_resync(sacx_handle* h);
  * Plain SAC only (use_expert = 0). */
 int sacx_dp_unique_id(void* id_out, int32_t cap);
 int sacx_dp_init(sacx_handle* h, const void* id, int32_t nranks, int32_t rank);
+/* The same protocol with the ranks as handles of ONE process (<= 8, no RCCL): sacx_dp_init_local
+ * on each (before sacx_bind; all bound to one stream), then sacx_dp_local_step(handles in rank
+ * order, ...) runs n_steps updates of every rank eagerly, interleaved at the all-reduce points,
+ * where one kernel sums the ranks' gradient ranges in rank order and writes the sum back to each
+ * (ncclAllReduce(sum)'s result; with two ranks bit for bit).  The reduce is the only difference
+ * from the RCCL mode: the plans, local-gradient stores and Adam apply launches are the same. */
+int sacx_dp_init_local(sacx_handle* h, int32_t nranks, int32_t rank);
+int sacx_dp_local_step(sacx_handle* const* handles, int32_t nranks, int64_t n_steps, int64_t num_timesteps,
+                       int32_t ts_increment);
 
 /* --- measurement ----------------------------------------------------------- */
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);

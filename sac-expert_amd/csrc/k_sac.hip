@@ -2074,10 +2074,18 @@ __device__ __forceinline__ void act_tail(const ActRowArgs& g, const float* outs,
 // the biases, logstd and the noise -- is requested before the first barrier, so the row costs
 // one memory round trip instead of one per layer.  Same FMA order as the generic path.
 template <bool PF>
-__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
+__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g_in) {
     __shared__ float xs[ACT_ROWS_DIM], h1s[ACT_ROWS_DIM], h2s[ACT_ROWS_DIM];
     __shared__ float part[4][ACT_ROWS_DIM];
     __shared__ float outs[64];
+    ActRowArgs g = g_in;
+    if (g_in.nseeds > 1) {          // packed seeds: seed z's weights, normaliser and noise; its rows
+        const int64_t so = seed_off(g_in.sstride);
+        g.s_mean = sr(g.s_mean, so); g.s_den = sr(g.s_den, so); g.W0 = sr(g.W0, so); g.W1 = sr(g.W1, so);
+        g.W3 = sr(g.W3, so); g.logstd = sr(g.logstd, so); g.noise = sr(g.noise, so);
+        g.obs = g.obs + (size_t)blockIdx.z * g.m * g.S;
+        g.out = g.out + (size_t)blockIdx.z * g.m * g.A;
+    }
     const int t = threadIdx.x, row = blockIdx.x, lane = t & 63, wave = t >> 6;
     const int S = g.S, A = g.A, Aout = g.Aout;
     const bool jok = wave == 0 && lane < A;
@@ -2164,8 +2172,9 @@ __global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
 
 void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s) {
     const bool pf = a.S <= 128 && a.H0 <= 256 && a.H1 <= 256 && a.Aout <= 16;
-    if (pf) hipLaunchKernelGGL(k_act_rows<true>, dim3(m), dim3(1024), 0, s, a);
-    else hipLaunchKernelGGL(k_act_rows<false>, dim3(m), dim3(1024), 0, s, a);
+    const dim3 grid(m, 1, seeds_z(a.nseeds));
+    if (pf) hipLaunchKernelGGL(k_act_rows<true>, grid, dim3(1024), 0, s, a);
+    else hipLaunchKernelGGL(k_act_rows<false>, grid, dim3(1024), 0, s, a);
 }
 
 // ==================================================================== k_qhead
@@ -2526,8 +2535,15 @@ void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {
 // ==================================================================== k_append
 // TrajectoryBuffer.add (buffers.py:41-71) as a device ring: one workgroup so the
 // control-block update is ordered after every row write.
-__global__ __launch_bounds__(256) void k_append(AppendArgs a) {
+__global__ __launch_bounds__(256) void k_append(AppendArgs a_in) {
     __shared__ int64_t cur_s, start_s;
+    AppendArgs a = a_in;
+    if (a_in.nseeds > 1) {          // packed seeds: seed z's ring and counters, its n source rows
+        const int64_t so = seed_off(a_in.sstride), z = blockIdx.z;
+        a.replay = sr(a.replay, so); a.ctl = sr(a.ctl, so);
+        a.s = a.s + z * a.n * a.S; a.a = a.a + z * a.n * a.A; a.sp = a.sp + z * a.n * a.S;
+        a.r = a.r + z * a.n; a.d = a.d + z * a.n;
+    }
     if (threadIdx.x == 0) {
         cur_s = a.ctl->cur_size;
         start_s = a.ctl->start;
@@ -2558,7 +2574,7 @@ __global__ __launch_bounds__(256) void k_append(AppendArgs a) {
 }
 
 void launch_append(const AppendArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_append, dim3(1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_append, dim3(1, 1, seeds_z(a.nseeds)), dim3(256), 0, s, a);
 }
 
 }  // namespace sacx
@@ -2738,6 +2754,20 @@ __global__ __launch_bounds__(256) void k_adam_apply(AdamApplyArgs a) {
 
 void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_adam_apply, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
+}
+
+// sacx_dp_local_step's reduce: the ranks' gradient ranges summed in rank order, the sum written
+// back to every rank (ncclAllReduce(sum)'s result; with two ranks a + b, exactly RCCL's)
+__global__ __launch_bounds__(256) void k_dp_sum(DpSumArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    float v = a.buf[0][i];
+    for (int r = 1; r < a.nranks; ++r) v = v + a.buf[r][i];
+    for (int r = 0; r < a.nranks; ++r) a.buf[r][i] = v;
+}
+
+void launch_dp_sum(const DpSumArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_dp_sum, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a);
 }
 
 // the alpha half of finalize_update that follows the all-reduce of the alpha gradient

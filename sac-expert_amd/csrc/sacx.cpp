@@ -133,6 +133,7 @@ struct sacx_handle {
     // packed seeds: K learners in K arena blocks seed_bytes apart; `arena` is the block of the
     // selected seed (the per-seed calls), arena0 seed 0's (the plans: grid z covers the rest)
     int seeds = 1, sel = 0;
+    int plan_seeds = 1;       // the seed count the plan's shape decisions see (1 with single_seed_plan)
     uint64_t seed_bytes = 0;
     char* arena0 = nullptr;
     // binding
@@ -148,11 +149,13 @@ struct sacx_handle {
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
     // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
     int dp_ranks = 0, dp_rank = 0;
+    bool dp_local = false;    // sacx_dp_init_local: the ranks are handles of this process (no RCCL)
     ncclComm_t comm = nullptr;
     bool nccl_failed = false;
-    std::vector<Launch> mplan;
-    hipGraphExec_t mgraph = nullptr;
-    int64_t mfit_host = 0;  // model steps issued (mirrors ctl->mfit_seq)
+    // world-model fitting, per seed (packed seeds fit one seed at a time: its arena block's plan)
+    std::vector<std::vector<Launch>> mplans;
+    std::vector<hipGraphExec_t> mgraphs;
+    std::vector<int64_t> mfit_hosts;   // model steps issued per seed (mirror ctl->mfit_seq)
     std::vector<GemmProb> probs;
     int probs_cursor = 0;
     std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;   // (G, with_rng, skipped kind)
@@ -181,6 +184,8 @@ struct sacx_handle {
     template <class T>
     T* ptr(const std::string& n) const { return reinterpret_cast<T*>(arena + seg(n).off); }
     float* f(const std::string& n) const { return ptr<float>(n); }
+    // seed 0's segment (the packed launches relocate it by blockIdx.z * seed_bytes)
+    float* f0(const std::string& n) const { return reinterpret_cast<float*>(arena0 + seg(n).off); }
     Ctl* ctl() const { return ptr<Ctl>("ctl"); }
     Ctl* ctl0() const { return reinterpret_cast<Ctl*>(arena0 + seg("ctl").off); }
     uint64_t total_bytes() const { return seeds > 1 ? (uint64_t)seeds * seed_bytes : arena_bytes; }
@@ -684,7 +689,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // workgroups of q.fwd0, and the models' forward shifts one launch later (layer 0 in q.fwd1,
     // layer 1 in pi.q.fwd0, the MSE head in pi.q.fwd1)
     const bool fuse_head = Aout <= 16 && S + A <= 64 && H1 % 16 == 0 && H1 <= 512 &&
-                           (fh ? std::atoi(fh) != 0 : h->seeds < 4);
+                           (fh ? std::atoi(fh) != 0 : h->plan_seeds < 4);
     HeadArgs head_fused{};
     // actor.head.bwd folded into actor.bwd1 (plain SAC; the expert rows' model gradients keep
     // the row kernel): pi.q.bwd1 writes per-tile partial action gradients, actor.bwd1's tiles
@@ -1145,8 +1150,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
 }
 
 // one world-model fitting step: gather -> 3 fwd GEMMs -> loss grads -> 2 dX GEMMs -> dW + Adam -> finalize
+// the fitting plan of the selected seed (its arena block's pointers)
 void build_model_plan(sacx_handle* h) {
-    std::vector<Launch>& plan = h->mplan;
+    std::vector<Launch>& plan = h->mplans[h->sel];
     plan.clear();
     if (!h->cfg.use_expert) return;
     const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ;
@@ -1255,6 +1261,7 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::MLOSS: launch_mloss(L.ml, s); break;
         case Launch::MFINAL: launch_mfinal(L.mf, s); break;
         case Launch::ALLREDUCE:
+            if (h->dp_local) break;            // sacx_dp_local_step reduces over the ranks' handles
             if (ncclAllReduce(L.ar_buf, L.ar_buf, (size_t)L.ar_count, ncclFloat32, ncclSum, h->comm, s) != ncclSuccess)
                 h->nccl_failed = true;
             break;
@@ -1637,6 +1644,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     build_layout(h);
     h->seeds = cfg->seeds > 1 ? cfg->seeds : 1;
     h->seed_bytes = h->seeds > 1 ? (h->arena_bytes + 65535) & ~uint64_t(65535) : h->arena_bytes;
+    h->plan_seeds = cfg->single_seed_plan ? 1 : h->seeds;
     *out = h;
     return 0;
 }
@@ -1644,7 +1652,8 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
 void sacx_destroy(sacx_handle* h) {
     if (!h) return;
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-    if (h->mgraph) (void)hipGraphExecDestroy(h->mgraph);
+    for (auto g : h->mgraphs)
+        if (g) (void)hipGraphExecDestroy(g);
     for (auto& kv : h->roll_graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->pin) (void)hipHostFree(h->pin);
@@ -1710,7 +1719,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // the launches merged_body folds together always agree.  From 4,096 rows the dW + Adam
     // launches take 32x32 tiles too (tools/t32_dw.sh: Humanoid 4 seeds +3.5 %, 8 seeds +5 %,
     // bf16 4 seeds +8 %, HC 32 seeds +1.9 %; HC 8 / 16 seeds and one Humanoid seed even or worse)
-    const int64_t rows = (int64_t)h->seeds * h->B;
+    const int64_t rows = (int64_t)h->plan_seeds * h->B;
     h->tile32 = rows >= 4096 ? 1 : rows >= 1024 ? 2 : 0;
     if (const char* e = std::getenv("SACX_T32")) h->tile32 = std::atoi(e);
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
@@ -1736,7 +1745,14 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
                  h->plan[0][i].gemm_first + h->plan[0][i].gemm.nprob > (int)h->probs.size()))
                 return fail(h, "internal: GEMM problem table mismatch");
     }
-    build_model_plan(h);
+    h->mplans.assign(h->seeds, {});
+    h->mgraphs.assign(h->seeds, nullptr);
+    h->mfit_hosts.assign(h->seeds, 0);
+    {
+        const int cur = h->probs_cursor;
+        build_model_plan(h);                  // seed 0's; the others' on their first model_fit
+        h->probs_cursor = cur;
+    }
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
     h->bound = true;
@@ -1749,7 +1765,7 @@ int sacx_resync(sacx_handle* h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(&c, h->ctl(), sizeof(Ctl), hipMemcpyDeviceToHost));
     h->seq_host = c.step_seq;
-    h->mfit_host = c.mfit_seq;
+    h->mfit_hosts[h->sel] = c.mfit_seq;
     return 0;
 }
 
@@ -1774,6 +1790,63 @@ int sacx_dp_init(sacx_handle* h, const void* id, int32_t nranks, int32_t rank) {
     if (r != ncclSuccess) return fail(h, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     h->dp_ranks = nranks;
     h->dp_rank = rank;
+    return 0;
+}
+
+int sacx_dp_init_local(sacx_handle* h, int32_t nranks, int32_t rank) {
+    if (!h) return -1;
+    if (h->bound) return fail(h, "sacx_dp_init_local must precede sacx_bind");
+    if (h->comm || h->dp_ranks) return fail(h, "data-parallel mode already set");
+    if (h->seeds > 1) return fail(h, "data-parallel mode needs seeds = 1");
+    if (nranks < 1 || nranks > DP_LOCAL_MAX || rank < 0 || rank >= nranks) return fail(h, "bad data-parallel arguments");
+    if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
+    h->dp_ranks = nranks;
+    h->dp_rank = rank;
+    h->dp_local = true;
+    return 0;
+}
+
+int sacx_dp_local_step(sacx_handle* const* hs, int32_t nranks, int64_t n_steps, int64_t num_timesteps,
+                       int32_t ts_increment) {
+    if (!hs || nranks < 1 || nranks > DP_LOCAL_MAX) return -1;
+    sacx_handle* h0 = hs[0];
+    for (int r = 0; r < nranks; ++r) {
+        sacx_handle* h = hs[r];
+        if (!h || !h->bound) return fail(h0, "rank handle not bound");
+        if (!h->dp_local || h->dp_ranks != nranks || h->dp_rank != r)
+            return fail(h0, "handles must be ranks 0..n-1 of one sacx_dp_init_local group, in rank order");
+        if (h->stream != h0->stream) return fail(h0, "the ranks' handles must be bound to one stream");
+    }
+    if (n_steps <= 0) return 0;
+    hipStream_t s = h0->stream;
+    for (int r = 0; r < nranks; ++r)
+        launch_set_ctl(hs[r]->ctl0(), num_timesteps, ts_increment, 0, 1, s);
+    for (int64_t j = 0; j < n_steps; ++j) {
+        std::vector<size_t> pos(nranks, 0);
+        for (;;) {
+            // every rank up to its next all-reduce (or its end), in rank order, on the one stream
+            int at_ar = 0;
+            for (int r = 0; r < nranks; ++r) {
+                const std::vector<Launch>& pl = hs[r]->plan[0];
+                while (pos[r] < pl.size() && pl[pos[r]].kind != Launch::ALLREDUCE) enqueue(pl[pos[r]++], hs[r], s);
+                at_ar += pos[r] < pl.size();
+            }
+            if (at_ar == 0) break;
+            if (at_ar != nranks) return fail(h0, "internal: the ranks' plans do not line up");
+            DpSumArgs a{};
+            a.nranks = nranks;
+            a.n = hs[0]->plan[0][pos[0]].ar_count;
+            for (int r = 0; r < nranks; ++r) {
+                const Launch& L = hs[r]->plan[0][pos[r]];
+                if (L.ar_count != a.n) return fail(h0, "internal: all-reduce sizes differ");
+                a.buf[r] = L.ar_buf;
+                ++pos[r];
+            }
+            launch_dp_sum(a, s);
+        }
+    }
+    HIPCHK(h0, hipGetLastError());
+    for (int r = 0; r < nranks; ++r) hs[r]->seq_host += n_steps;
     return 0;
 }
 
@@ -1849,6 +1922,76 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
     return 0;
 }
 
+// Every seed of a packed handle at once (one launch chain for all): the env loop of K lock-step
+// runs (sac_eo.train --runs K) hands over one row per run.  Arrays are [seeds, n, ...].
+int sacx_buffer_append_host_seeds(sacx_handle* h, const float* s, const float* a, const float* r, const float* sp,
+                                  const float* d, int64_t n) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n <= 0) return 0;
+    if (!s || !a || !r || !sp || !d) return fail(h, "null row pointer");
+    const int S = h->S, A = h->A, K = h->seeds;
+    const int64_t tot = (int64_t)K * n;
+    if (tot * (2 * S + A + 2) > STAGE_CAP) return fail(h, "rows exceed the pinned staging buffer (append per seed)");
+    if (stage_begin(h)) return -1;
+    float* p = h->pin;
+    std::memcpy(p, s, sizeof(float) * tot * S);
+    std::memcpy(p + tot * S, a, sizeof(float) * tot * A);
+    std::memcpy(p + tot * (S + A), r, sizeof(float) * tot);
+    std::memcpy(p + tot * (S + A + 1), sp, sizeof(float) * tot * S);
+    std::memcpy(p + tot * (2 * S + A + 1), d, sizeof(float) * tot);
+    const float* g = h->pin_dev;
+    AppendArgs ag{};
+    ag.replay = h->f0("replay"); ag.cap = h->cap; ag.stride = h->stride; ag.S = S; ag.A = A;
+    ag.s = g; ag.a = g + tot * S; ag.r = g + tot * (S + A); ag.sp = g + tot * (S + A + 1); ag.d = g + tot * (2 * S + A + 1);
+    ag.n = n; ag.ctl = h->ctl0(); ag.sstride = (int64_t)h->seed_bytes; ag.nseeds = K;
+    launch_append(ag, h->stream);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
+    h->pin_pending = true;
+    return 0;
+}
+
+int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    if (n <= 0 || !obs || !act_out) return fail(h, "bad arguments");
+    const int S = h->S, A = h->A, K = h->seeds;
+    if (n > ACT_ROWS_MAX || h->ln || S > ACT_ROWS_DIM || h->H0 > ACT_ROWS_DIM || h->H1 > ACT_ROWS_DIM || h->Aout > 64)
+        return fail(h, "sacx_actor_act_host_seeds: n <= 16 rows per seed, no layer norm (use per-seed calls)");
+    const int64_t tot = (int64_t)K * n;
+    if (tot * (S + A) > STAGE_CAP) return fail(h, "rows exceed the pinned staging buffer (act per seed)");
+    if (stage_begin(h)) return -1;
+    std::memcpy(h->pin, obs, sizeof(float) * tot * S);
+    float* noise = deterministic ? nullptr : h->f0("act.noise");
+    if (!deterministic) {            // each seed's u = np.random.normal(size=(n, A)) from its own stream
+        RngArgs r{};
+        r.st = reinterpret_cast<RngState*>(h->f0("rng")); r.ctl = h->ctl0();
+        r.n_int = 0; r.n_norm = (int32_t)n * A; r.out_idx = nullptr; r.out_norm = noise;
+        r.slot = -1; r.reset_seq = 0; r.nupd = 1;
+        r.sstride = (int64_t)h->seed_bytes; r.nseeds = K;
+        launch_rng(r, h->stream);
+    }
+    ActRowArgs a{};
+    a.obs = h->pin_dev; a.s_mean = h->f0("norm.s_mean"); a.s_den = h->f0("norm.s_den");
+    a.W0 = h->f0("actor.l0"); a.W1 = h->f0("actor.l1"); a.W3 = h->f0("actor.l2"); a.logstd = h->f0("actor.logstd");
+    a.noise = noise; a.out = h->pin_dev + tot * S;
+    a.S = S; a.A = A; a.Aout = h->Aout; a.H0 = h->H0; a.H1 = h->H1;
+    a.act0 = h->aact[0]; a.act1 = h->aact[1];
+    a.mode = h->cfg.actor_gaussian ? 2 : 1;
+    a.per_state_std = h->cfg.per_state_std;
+    a.lim = h->cfg.act_limit;
+    if (h->cfg.actor_gaussian) {
+        const double sm = h->cfg.actor_std_mult > 0.f ? h->cfg.actor_std_mult : 1.0;
+        a.logstd_init = (float)(std::log(sm) - (h->cfg.per_state_std ? std::log(std::log(2.0)) : 0.0));
+        a.output_norm = h->cfg.actor_output_norm;
+    }
+    a.sstride = (int64_t)h->seed_bytes; a.nseeds = K; a.m = (int32_t)n;
+    launch_act_rows(a, (int)n, h->stream);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    std::memcpy(act_out, h->pin + tot * S, sizeof(float) * tot * A);
+    return 0;
+}
+
 int sacx_expert_set(sacx_handle* h, const float* s_e, const float* sp_e, int32_t n, float epsilon) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert");
@@ -1919,6 +2062,7 @@ int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t*
 
 int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_t ts_increment, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (h->dp_local) return fail(h, "in-process data-parallel ranks step together (sacx_dp_local_step)");
     if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n_steps <= 0) return 0;
     launch_set_ctl(h->ctl0(), num_timesteps, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
@@ -1949,36 +2093,42 @@ int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags) {
 int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert (no world models)");
-    if (h->seeds > 1) return fail(h, "model_fit needs seeds = 1");
     if (n_steps <= 0) return 0;
     if (!idx) return fail(h, "null index array");
+    const int k = h->sel;                 // packed seeds: the selected seed's models and ring
+    if (h->mplans[k].empty()) {
+        const int cur = h->probs_cursor;
+        build_model_plan(h);
+        h->probs_cursor = cur;
+    }
+    const std::vector<Launch>& mplan = h->mplans[k];
     const int R2 = h->nm * h->mb;
     int32_t* ring = h->ptr<int32_t>("mfit.idx");
     for (int64_t done = 0; done < n_steps;) {
         const int64_t chunk = std::min<int64_t>(n_steps - done, h->mfit_cap);
         HIPCHK(h, hipStreamSynchronize(h->stream));   // ring slots of earlier chunks are consumed
         for (int64_t j = 0; j < chunk; ++j) {
-            const int64_t slot = (h->mfit_host + done + j) % h->mfit_cap;
+            const int64_t slot = (h->mfit_hosts[k] + done + j) % h->mfit_cap;
             HIPCHK(h, hipMemcpy(ring + slot * R2, idx + (done + j) * R2, sizeof(int32_t) * R2, hipMemcpyHostToDevice));
         }
         if (flags & SACX_STEP_EAGER) {
             for (int64_t j = 0; j < chunk; ++j)
-                for (const Launch& L : h->mplan) enqueue(L, h, h->stream);
+                for (const Launch& L : mplan) enqueue(L, h, h->stream);
             HIPCHK(h, hipGetLastError());
         } else {
-            if (!h->mgraph) {
+            if (!h->mgraphs[k]) {
                 HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-                for (const Launch& L : h->mplan) enqueue(L, h, h->cap_stream);
+                for (const Launch& L : mplan) enqueue(L, h, h->cap_stream);
                 hipGraph_t graph;
                 HIPCHK(h, hipStreamEndCapture(h->cap_stream, &graph));
-                HIPCHK(h, hipGraphInstantiateWithFlags(&h->mgraph, graph, 0));
+                HIPCHK(h, hipGraphInstantiateWithFlags(&h->mgraphs[k], graph, 0));
                 HIPCHK(h, hipGraphDestroy(graph));
             }
-            for (int64_t j = 0; j < chunk; ++j) HIPCHK(h, hipGraphLaunch(h->mgraph, h->stream));
+            for (int64_t j = 0; j < chunk; ++j) HIPCHK(h, hipGraphLaunch(h->mgraphs[k], h->stream));
         }
         done += chunk;
     }
-    h->mfit_host += n_steps;
+    h->mfit_hosts[k] += n_steps;
     return 0;
 }
 

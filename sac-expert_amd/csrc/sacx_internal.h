@@ -348,6 +348,10 @@ struct AppendArgs {
     const float *s, *a, *r, *sp, *d;
     int64_t n;
     Ctl* ctl;
+    // packed seeds (sacx_buffer_append_host_seeds): grid z = seed; replay / ctl move by z * sstride,
+    // the source rows by z * n rows (arrays [seeds, n, ...])
+    int64_t sstride;
+    int32_t nseeds;
 };
 
 // ---------------------------------------------------------------- world-model fitting
@@ -409,6 +413,15 @@ struct AdamApplyArgs {
     const float* scale_dev;     // nullable: gradients also times *scale_dev (clip_by_global_norm)
     const Ctl* ctl;
     AdamConsts adam;
+};
+
+// In-process data-parallel reduce (sacx_dp_local_step): buf[r][i] = sum over r' of buf[r'][i], in
+// rank order, for every rank r -- what ncclAllReduce(sum) leaves on each rank.
+#define DP_LOCAL_MAX 8
+struct DpSumArgs {
+    float* buf[DP_LOCAL_MAX];
+    int32_t nranks;
+    int64_t n;
 };
 
 // ---------------------------------------------------------------- actor layer norm (A3)
@@ -488,6 +501,10 @@ struct ActRowArgs {
     int32_t mode;              // 1: SquashedGaussianActor.sample, 2: GaussianActor.sample
     int32_t per_state_std, output_norm;
     float lim, logstd_init;
+    // packed seeds (sacx_actor_act_host_seeds): grid z = seed; the arena pointers (normaliser,
+    // weights, noise) move by z * sstride, obs / out by z * m rows (arrays [seeds, m, S / A])
+    int64_t sstride;
+    int32_t nseeds, m;
 };
 
 // launchers (defined in k_sac.hip)
@@ -515,5 +532,6 @@ void launch_ln(const LNArgs& a, hipStream_t s);
 void launch_diag(const DiagArgs& a, hipStream_t s);
 void launch_adam_apply(const AdamApplyArgs& a, hipStream_t s);
 void launch_alpha_apply(const FinalArgs& f, hipStream_t s);
+void launch_dp_sum(const DpSumArgs& a, hipStream_t s);
 
 }  // namespace sacx

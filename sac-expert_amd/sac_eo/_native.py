@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 5
+SACX_ABI_VERSION = 6
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1
@@ -24,10 +24,11 @@ STAT_NAMES = ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss",
 # every symbol include/sacx.h declares (checked by tests/test_abi.py)
 EXPORTS = [
     "sacx_create", "sacx_destroy", "sacx_last_error", "sacx_arena_bytes", "sacx_layout", "sacx_bind",
-    "sacx_buffer_append", "sacx_buffer_append_host", "sacx_actor_act_host", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
+    "sacx_buffer_append", "sacx_buffer_append_host", "sacx_actor_act_host",
+    "sacx_buffer_append_host_seeds", "sacx_actor_act_host_seeds", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
     "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
-    "sacx_dp_unique_id", "sacx_dp_init", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
+    "sacx_dp_unique_id", "sacx_dp_init", "sacx_dp_init_local", "sacx_dp_local_step", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
     "sacx_seed_select", "sacx_prepare", "sacx_actor_evaluate", "sacx_critic_forward", "sacx_model_forward",
     "sacx_model_loss",
 ]
@@ -77,6 +78,7 @@ class Config(ctypes.Structure):
         ("act_per_layer", ctypes.c_int32),
         ("act_layers", (ctypes.c_int32 * 2) * 3),
         ("delta_clip_pred", ctypes.c_float),
+        ("single_seed_plan", ctypes.c_int32),
     ]
 
 
@@ -142,6 +144,8 @@ def lib():
         "sacx_actor_act": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sacx_buffer_append_host": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64]),
         "sacx_actor_act_host": (ctypes.c_int, [vp, vp, i64, i32, vp]),
+        "sacx_buffer_append_host_seeds": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, i64]),
+        "sacx_actor_act_host_seeds": (ctypes.c_int, [vp, vp, i64, i32, vp]),
         "sacx_actor_evaluate": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "sacx_critic_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, i32, vp]),
         "sacx_model_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, f32, f32, vp, vp, vp]),
@@ -151,6 +155,8 @@ def lib():
         "sacx_resync": (ctypes.c_int, [vp]),
         "sacx_expert_diag": (ctypes.c_int, [vp, vp, vp, vp, i32, i32, f32, vp]),
         "sacx_dp_init": (ctypes.c_int, [vp, vp, i32, i32]),
+        "sacx_dp_init_local": (ctypes.c_int, [vp, i32, i32]),
+        "sacx_dp_local_step": (ctypes.c_int, [vp, i32, i64, i64, i32]),
         "sacx_rollout": (ctypes.c_int, [vp, i32, vp, i64, i32, i32, f32, f32, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():

@@ -10,8 +10,8 @@ from .base import SACBase
 class SAC(SACBase):
     use_expert = False
 
-    def train(self, total_timesteps, params):
-        """SAC.py:254-385."""
+    def _train_loop(self, total_timesteps, params):
+        """SAC.py:254-385 (a generator of env-loop requests, see SACBase.train)."""
         self._set_rms()
         checkpoints = self._checkpoints(total_timesteps)
         eval_points = self._eval_points(total_timesteps)
@@ -34,14 +34,17 @@ class SAC(SACBase):
                 done, episode_reward, episode_step = False, 0.0, 0
                 episode += 1
                 t_episode = time.time()
-            a = self.actor.sample(obs, deterministic=not self.random_act).numpy()
+            a = yield ("act", obs, not self.random_act)
             if episode_step % int(self.repeat_after_real_steps) == 0:
-                for _ in range(self.G):          # G updates at one env step: num_timesteps unchanged
-                    self._update(num_timesteps, ts_increment=0)
+                # G updates at one env step: num_timesteps unchanged (ts_increment 0)
+                self._pre_update(self.G)
+                yield ("update", int(self.G), num_timesteps, 0)
+                self._post_update(self.G)
             next_obs, r, done, _ = self.env.step(self.actor.clip(a))
             done_no_max = False if episode_step + 1 == self._max_episode_steps else done
             episode_reward += r
-            self._add(obs[None], a[None], [r], next_obs[None], [float(done_no_max)], track_episode=True)
+            rows = self._add_rows(obs[None], a[None], [r], next_obs[None], [float(done_no_max)])
+            self._added(rows, (yield ("add", rows)), True)
             obs = next_obs
             episode_step += 1
             num_timesteps += 1

@@ -46,6 +46,7 @@ class SAC_exp(SACBase):
         self.delta_clip_pred = (mf_update_kwargs or {}).get("delta_clip_pred") or alg_kwargs.get("delta_clip_pred")
         self.model_MSE_on_expert_data = []
         self._eps_log, self._eps_cur = [], float(self.epsilon)
+        self._perm_queue = None        # expert permutations drawn ahead and pushed, not yet used
         self.model_MSE_on_expert_counterfactual_action = []
         self._expert_engine = None
         self.s_expert = self.a_expert = self.sp_expert = None
@@ -140,15 +141,30 @@ class SAC_exp(SACBase):
         super()._dump_and_save(params)
 
     # ------------------------------------------------------------------ update
-    def _update(self, num_timesteps, expert_reg=None, ts_increment=1):
-        if len(self.models) > 1:                 # SAC_expert.py:301-303 (one model: no shuffle)
-            idx = np.arange(self.engine.cfg.expert_batch)
-            self.rng.shuffle(idx)
-            self.engine.push_perms(idx[None, :])
-        self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
-        self._eps_log.append(self._eps_cur)
-        if len(self._eps_log) >= self.engine.cfg.stats_capacity:
-            self._flush_update_logs()        # the device ring is full (epsilon is constant within an episode)
+    _PERM_AHEAD = 256
+
+    def _pre_update(self, n):
+        """The self.rng.shuffle permutation of each update (SAC_expert.py:301-303; one model: no
+        shuffle).  self.rng is used for nothing else, so they are drawn ahead in the same order,
+        _PERM_AHEAD at a time, and pushed into the device ring in one copy."""
+        if len(self.models) < 2:
+            return
+        q = self._perm_queue
+        have = 0 if q is None else q.shape[0]
+        if have < n:
+            m = max(n - have, min(self._PERM_AHEAD, self.engine.cfg.perm_capacity - have))
+            new = np.tile(np.arange(self.engine.cfg.expert_batch), (m, 1))
+            for row in new:
+                self.rng.shuffle(row)
+            q = new if q is None else np.concatenate([q, new])
+            self.engine.push_perms(q)           # the ring slots of the next len(q) updates
+        self._perm_queue = q[n:]
+
+    def _post_update(self, n):
+        for _ in range(n):
+            self._eps_log.append(self._eps_cur)
+            if len(self._eps_log) >= self.engine.cfg.stats_capacity:
+                self._flush_update_logs()        # the device ring is full (epsilon is constant within an episode)
 
     def _update_models(self):
         t0 = time.time()
@@ -198,8 +214,8 @@ class SAC_exp(SACBase):
                                "model_loss_last": float(self.engine.model_stats(1)[0].sum())})
 
     # ------------------------------------------------------------------ loop
-    def train(self, total_timesteps, params):
-        """SAC_expert.py:685-824."""
+    def _train_loop(self, total_timesteps, params):
+        """SAC_expert.py:685-824 (a generator of env-loop requests, see SACBase.train)."""
         self._set_rms()
         self._collect_expert_data()
         checkpoints = self._checkpoints(total_timesteps)
@@ -226,12 +242,15 @@ class SAC_exp(SACBase):
                 self._update_models()
                 expert_reg = self._expert_preprocess()
                 t_episode = time.time()
-            a = self.actor.sample(obs, deterministic=not self.random_act).numpy()
-            self._update(num_timesteps, expert_reg)
+            a = yield ("act", obs, not self.random_act)
+            self._pre_update(1)                      # _update(num_timesteps, expert_reg), :780
+            yield ("update", 1, num_timesteps, 1)
+            self._post_update(1)
             next_obs, r, done, _ = self.env.step(self.actor.clip(a))
             done_no_max = False if episode_step + 1 == self._max_episode_steps else done
             episode_reward += r
-            self._add(obs[None], a[None], [r], next_obs[None], [float(done_no_max)], track_episode=True)
+            rows = self._add_rows(obs[None], a[None], [r], next_obs[None], [float(done_no_max)])
+            self._added(rows, (yield ("add", rows)), True)
             obs = next_obs
             episode_step += 1
             num_timesteps += 1

@@ -8,6 +8,7 @@ device keeps the live copy (updates, stochastic actions); host code that draws f
 pulls the device state into NumPy and pushes it back afterwards, so draws happen in
 the reference's order."""
 import contextlib
+import dataclasses
 import time
 
 import numpy as np
@@ -27,6 +28,9 @@ class SACBase:
         self.env, self.env_eval = env, env_eval
         self.actor, self.critics, self.q_targets, self.q_critics = actor, critics, q_targets, q_critics
         self.models = models
+        # packed runs (sac_eo.train --runs K, lock-step): (shared packed Engine or None, seed, K);
+        # popped so it never reaches the logged params
+        self._pack = alg_kwargs.pop("_pack", None)
         self.s_dim = int(np.prod(env.observation_space.shape))
         self.a_dim = int(np.prod(env.action_space.shape))
         self._setup(alg_kwargs)
@@ -89,6 +93,31 @@ class SACBase:
         return max(1, self.total_timesteps + self.env_batch_size_init + self.env_horizon)
 
     def _build_engine(self, k):
+        cfg = self._engine_config(k)
+        if self._pack is None:
+            eng = Engine(cfg)
+        else:                                  # one seed of a packed handle (sac_eo.algs.lockstep)
+            shared, seed, n = self._pack
+            # every seed on the one-seed plan: each run bit-identical to its serial run
+            pcfg = dataclasses.replace(cfg, seeds=int(n), single_seed_plan=True)
+            if shared is None:
+                shared = Engine(pcfg)
+            elif shared.cfg != pcfg:
+                raise ValueError("packed runs need one configuration (shapes and hyper-parameters)")
+            eng = shared.seed_view(seed)
+        self.actor._bind(eng, "actor")
+        for i, q in enumerate(self.q_critics):
+            q._bind(eng, f"q{i}")
+        for i, t in enumerate(self.q_targets):
+            t._bind(eng, f"t{i}")
+        if self.use_expert:
+            for i, m in enumerate(self.models):
+                m._bind(eng, f"m{i}")
+        self._push_normalizers(eng)
+        eng.rng_set_state(np.random.get_state())       # adopt the global stream
+        return eng
+
+    def _engine_config(self, k):
         if not getattr(self.actor, "squash", False):
             raise ValueError("SAC trains the squashed Gaussian actor (--actor_squash)")
         hidden = self.actor.layers
@@ -114,18 +143,7 @@ class SACBase:
             delta_clip_loss=float(self.models[0].delta_clip_loss or 0.0) if self.use_expert else 0.0,
             reward_clip_loss=float(self.models[0].reward_clip_loss or 0.0) if self.use_expert else 0.0,
             delta_clip_pred=float(self.models[0].delta_clip_pred or 0.0) if self.use_expert else 0.0)
-        eng = Engine(cfg)
-        self.actor._bind(eng, "actor")
-        for i, q in enumerate(self.q_critics):
-            q._bind(eng, f"q{i}")
-        for i, t in enumerate(self.q_targets):
-            t._bind(eng, f"t{i}")
-        if self.use_expert:
-            for i, m in enumerate(self.models):
-                m._bind(eng, f"m{i}")
-        self._push_normalizers(eng)
-        eng.rng_set_state(np.random.get_state())       # adopt the global stream
-        return eng
+        return cfg
 
     # ------------------------------------------------------------------ RNG sharing
     @contextlib.contextmanager
@@ -178,14 +196,52 @@ class SACBase:
     # ------------------------------------------------------------------ data
 
     def _add(self, s, a, r, sp, d, track_episode=False):
-        r64 = np.asarray(r, np.float64)
-        s, a, r, sp = (np.asarray(x, np.float32) for x in (s, a, r, sp))
-        n = self.engine.append(s, a, r, sp, np.asarray(d, np.float32))
+        rows = self._add_rows(s, a, r, sp, d)
+        self._added(rows, self.engine.append(*rows), track_episode)
+
+    @staticmethod
+    def _add_rows(s, a, r, sp, d):
+        return tuple(np.asarray(x, np.float32) for x in (s, a, r, sp, d)) + (np.asarray(r, np.float64),)
+
+    def _added(self, rows, n, track_episode):
         self.steps_total += n
         if track_episode and self.update_normalizers:
             # new_traj.add (SAC_expert.py:799-801): np.array([r]) keeps the env's float64 reward,
             # which r_rms.update then merges in float64
+            s, a, _, sp, _, r64 = rows
             self._new_traj.append((s, a, r64, sp))
+
+    # ------------------------------------------------------------------ the env loop as requests
+    # The train loops are generators that yield the three requests of a timestep -- ("act", obs,
+    # deterministic), ("update", n, num_timesteps, ts_increment), ("add", rows) -- and do everything
+    # else (episode hooks, model fits, logging, checkpoints) themselves.  train() serves them one by
+    # one on this learner's engine; sac_eo.algs.lockstep serves K learners of one packed handle with
+    # one launch chain per request (the reference's --runs, sac_eo/train.py:118-152).
+    def train(self, total_timesteps, params):
+        loop = self._train_loop(total_timesteps, params)
+        try:
+            req = next(loop)
+            while True:
+                req = loop.send(self._serve(req))
+        except StopIteration as stop:
+            return stop.value
+
+    def _serve(self, req):
+        kind = req[0]
+        if kind == "act":
+            return self.engine.act_host(np.asarray(req[1], np.float32), deterministic=req[2])
+        if kind == "update":
+            self.engine.step(req[1], num_timesteps=req[2], ts_increment=req[3])
+            return None
+        if kind == "add":
+            return self.engine.append(*req[1][:5])
+        raise ValueError(kind)
+
+    def _pre_update(self, n):
+        """Host work ahead of n updates (SAC_exp: the expert permutations)."""
+
+    def _post_update(self, n):
+        """Host bookkeeping after n updates (SAC_exp: the per-update log)."""
 
     def _collect_env_data(self, num_timesteps, update_normalizers=True, only_model_normalizer=False):
         """SAC_expert.py:625-684: rollouts of the stochastic actor until the batch is full."""
@@ -231,7 +287,10 @@ class SACBase:
 
     # ------------------------------------------------------------------ update
     def _update(self, num_timesteps, expert_reg=None, ts_increment=1):
+        """One gradient step (SAC_expert.py:463-477 / SAC.py:236-250) on this learner's engine."""
+        self._pre_update(1)
         self.engine.step(1, num_timesteps=num_timesteps, ts_increment=ts_increment)
+        self._post_update(1)
 
     def _dump_stats(self):
         """The reference's final dict (base_onpolicy_alg.py:351-364, mbrl_onpolicy_alg.py:321-329):

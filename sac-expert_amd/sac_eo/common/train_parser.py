@@ -4,7 +4,8 @@ Same flag names, types, defaults and kwargs groups as the reference parser
 (sac_eo/common/train_parser.py:8-439) so existing command lines and logged
 ``param`` dicts carry over.  Flags the reference accepts but never reads
 ("Dead flags") are accepted and ignored here too.  One addition
-in the setup group: ``--gpus`` (learners are placed one per GPU).
+in the setup group: ``--gpus`` (learners are placed one per GPU) and ``--serial_runs`` (run the
+``--runs`` of one process one after another instead of as lock-step packed seeds).
 """
 import argparse
 
@@ -21,7 +22,7 @@ _FLAGS = [
     ("setup", "import_path", S, "./logs", {}), ("setup", "import_file", S, None, {}),
     ("setup", "import_idx", I, None, {}), ("setup", "import_all", T, False, {}),
     ("setup", "expert_file", S, None, {}), ("setup", "expert_path", S, "./experts", {}),
-    ("setup", "gpus", I, None, {}),
+    ("setup", "gpus", I, None, {}), ("setup", "serial_runs", T, False, {}),
     # environment
     ("env", "env_type", S, "gym", {}), ("env", "env_name", S, "Pendulum-v1", {}), ("env", "task_name", S, None, {}),
     # actor
@@ -102,8 +103,8 @@ _GROUP_NAMES = {"setup": "setup_kwargs", "env": "env_kwargs", "actor": "actor_kw
 
 all_kwargs = {v: [] for v in _GROUP_NAMES.values()}
 for grp, name, _t, _d, extra in _FLAGS:
-    if name == "gpus":
-        continue   # local addition, not a reference kwarg
+    if name in ("gpus", "serial_runs"):
+        continue   # local additions, not reference kwargs
     all_kwargs[_GROUP_NAMES[grp]].append(name)
     if extra.get("group2"):
         all_kwargs[_GROUP_NAMES[extra["group2"]]].append(name)

@@ -57,6 +57,7 @@ class EngineConfig:
     reward_loss_coef: float = 1.0
     gemm_bf16: bool = False     # config C5: bf16 MFMA operands, fp32 accumulate / master weights
     seeds: int = 1              # independent learners packed in one handle (one launch chain for all)
+    single_seed_plan: bool = False  # packed seeds run the one-seed plan: each seed bit-identical to its own run
     actor_gaussian: bool = False    # GaussianActor (no squash): inference only (an imported expert)
     actor_std_mult: float = 1.0
     actor_output_norm: bool = False
@@ -100,6 +101,7 @@ class EngineConfig:
         c.reward_loss_coef = self.reward_loss_coef
         c.gemm_bf16 = int(bool(self.gemm_bf16))
         c.seeds = int(self.seeds)
+        c.single_seed_plan = int(bool(self.single_seed_plan))
         c.actor_gaussian = int(bool(self.actor_gaussian))
         c.actor_std_mult = float(self.actor_std_mult)
         c.actor_output_norm = int(bool(self.actor_output_norm))
@@ -130,9 +132,12 @@ class Engine:
 
     NETS = ("actor", "q0", "q1", "t0", "t1", "m0", "m1")
 
-    def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None, stream=None, dp=None):
+    def __init__(self, cfg: EngineConfig, device: Optional[torch.device] = None, stream=None, dp=None,
+                 dp_local=None):
         """dp = (unique_id bytes, nranks, rank): data-parallel mode (sacx_dp_init), the
-        gradients of the local batch ``cfg.batch`` are summed over the ranks by RCCL."""
+        gradients of the local batch ``cfg.batch`` are summed over the ranks by RCCL.
+        dp_local = (nranks, rank): the same protocol over handles of this process
+        (sacx_dp_init_local; the ranks step together through Engine.dp_local_step)."""
         if not torch.cuda.is_available():
             raise RuntimeError("sac_eo.engine needs a ROCm GPU (no CPU fallback)")
         self.cfg = cfg
@@ -176,7 +181,10 @@ class Engine:
                 uid, nranks, rank = dp
                 buf = ctypes.create_string_buffer(bytes(uid), len(uid))
                 N.check(self.lib.sacx_dp_init(h, buf, int(nranks), int(rank)), h, "sacx_dp_init")
+            if dp_local is not None:
+                N.check(self.lib.sacx_dp_init_local(h, int(dp_local[0]), int(dp_local[1])), h, "sacx_dp_init_local")
         self.dp = dp
+        self.dp_local = dp_local
         N.check(self.lib.sacx_bind(h, ctypes.c_void_p(self.arena_all.data_ptr()), total,
                                    ctypes.c_void_p(self.stream.cuda_stream)), h, "sacx_bind")
         for k in range(self.seeds):
@@ -191,6 +199,15 @@ class Engine:
         self.seed_index = k
         self.arena = self._arenas[k]
         self.v = self._views[k]
+
+    @staticmethod
+    def dp_local_step(engines: Sequence["Engine"], n: int = 1, num_timesteps: int = 0, ts_increment: int = 1):
+        """n updates of every in-process data-parallel rank (sacx_dp_local_step); ``engines`` in
+        rank order, all on one stream."""
+        lib = N.lib()
+        hs = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
+        N.check(lib.sacx_dp_local_step(hs, len(engines), int(n), int(num_timesteps), int(ts_increment)),
+                engines[0].h, "dp_local_step")
 
     @staticmethod
     def dp_unique_id() -> bytes:
@@ -383,6 +400,31 @@ class Engine:
         N.check(self.lib.sacx_actor_act_host(self.h, o.ctypes.data, int(o.shape[0]), int(bool(deterministic)),
                                              out.ctypes.data), self.h, "actor_act_host")
         return out[0] if single else out
+
+    def act_host_seeds(self, obs, deterministic: bool = True) -> np.ndarray:
+        """act_host for EVERY seed of a packed handle in one launch chain: obs [seeds, n, S]
+        (or [seeds, S]) -> actions [seeds, n, A] (or [seeds, A]); each seed draws from its own
+        stream (sacx_actor_act_host_seeds)."""
+        S, A, K = self.cfg.s_dim, self.cfg.a_dim, self.seeds
+        o = np.ascontiguousarray(np.asarray(obs, np.float32))
+        one = o.ndim == 2
+        o = o.reshape(K, -1, S)
+        out = np.empty((K, o.shape[1], A), dtype=np.float32)
+        N.check(self.lib.sacx_actor_act_host_seeds(self.h, o.ctypes.data, int(o.shape[1]), int(bool(deterministic)),
+                                                   out.ctypes.data), self.h, "actor_act_host_seeds")
+        return out[:, 0] if one else out
+
+    def append_host_seeds(self, s, a, r, sp, d) -> int:
+        """append for EVERY seed of a packed handle (sacx_buffer_append_host_seeds): arrays
+        [seeds, n, ...]; returns n."""
+        S, A, K = self.cfg.s_dim, self.cfg.a_dim, self.seeds
+        r = np.asarray(r, np.float32).reshape(K, -1)
+        n = r.shape[1]
+        hs = [self._host_f32(s, (K, n, S)), self._host_f32(a, (K, n, A)), np.ascontiguousarray(r),
+              self._host_f32(sp, (K, n, S)), self._host_f32(d, (K, n))]
+        N.check(self.lib.sacx_buffer_append_host_seeds(self.h, *[x.ctypes.data for x in hs], n),
+                self.h, "buffer_append_host_seeds")
+        return n
 
     def evaluate(self, s):
         """SquashedGaussianActor.evaluate (continuous_actors.py:327-379) on the device:
@@ -598,6 +640,10 @@ class Engine:
     def sync(self):
         N.check(self.lib.sacx_sync(self.h), self.h, "sync")
 
+    def seed_view(self, k: int) -> "SeedView":
+        """The per-seed face of a packed handle for one learner's host code (SeedView)."""
+        return SeedView(self, k)
+
     def ctl(self) -> Dict[str, int]:
         c = self.v["ctl"][0].cpu().numpy()
         return {k: int(c[i]) for k, i in CTL.items()}
@@ -640,3 +686,34 @@ class Engine:
         out = (ctypes.c_double * k)()
         N.check(self.lib.sacx_profile(self.h, int(n_steps), out, k), self.h, "profile")
         return np.array(list(out)) / n_steps
+
+
+class SeedView:
+    """One seed of a packed Engine, seen as an Engine of its own by a learner's host code
+    (an algorithm, its actor / critic / model objects): every per-seed method selects the
+    seed first and ``v`` is the seed's views.  ``step`` / ``prepare`` advance every seed of
+    the handle, so they belong to the lock-step driver (sac_eo.algs.lockstep), not to a view."""
+
+    _SHARED = ("step", "prepare", "close", "time_graph", "time_kernels", "profile", "plan_info")
+
+    def __init__(self, engine: Engine, k: int):
+        self._eng, self._k = engine, int(k)
+
+    @property
+    def v(self):
+        return self._eng._views[self._k]
+
+    @property
+    def seed_index(self):
+        return self._k
+
+    def __getattr__(self, name):
+        if name in SeedView._SHARED:
+            raise AttributeError(f"SeedView.{name}: advances every seed of the packed handle (use the lock-step driver)")
+        attr = getattr(self._eng, name)
+        if callable(attr):
+            def call(*a, **kw):
+                self._eng.select_seed(self._k)
+                return attr(*a, **kw)
+            return call
+        return attr

@@ -2,10 +2,13 @@
 construction sequence, one learner per process, the same log files.
 
 Runs are spread over processes: under ``torch.distributed.run`` rank r trains runs
-``r, r + world, ...`` on its local GPU; otherwise the runs execute one after another on
-the current GPU.  No data moves between learners (replicas).  As in the
-reference (``:159-191``), the runs' checkpoint logs are gathered into one pickled list
-``<env_type>_<env>_<alg_type>_<mf_algo>[_<save_file>]_<date>`` and removed."""
+``r, r + world, ...`` on its local GPU.  The runs of one process train as K packed seeds of
+ONE device handle in lock-step (sac_eo.algs.lockstep: one launch chain per timestep for all
+of them, each run's log identical to its serial run's), or -- with ``--serial_runs``, or where
+lock-step cannot hold (SAC with early-terminating episodes, ``--env_batch_type traj``,
+``--actor_layer_norm``) -- one after another.  No data moves between learners (SURVEY §8e:
+replicas).  As in the reference (``:159-191``), the runs' checkpoint logs are gathered into one
+pickled list ``<env_type>_<env>_<alg_type>_<mf_algo>[_<save_file>]_<date>`` and removed."""
 import copy
 import os
 import pickle
@@ -25,8 +28,9 @@ from .envs import init_env
 from .models import init_world_models
 
 
-def train(inputs_dict):
-    """Training on one seed (reference train.py:33-100)."""
+def build_alg(inputs_dict, pack=None):
+    """The construction sequence of one run (reference train.py:33-103); pack = (shared packed
+    Engine or None, seed, K) makes the learner one seed of a packed handle."""
     sk = inputs_dict["setup_kwargs"]
     idx = sk["idx"]
     inputs_dict["alg_kwargs"]["alg_seed"] = sk["algorithm_seed"]
@@ -54,9 +58,39 @@ def train(inputs_dict):
     init_seeds(sk["eval_seed"], env_eval)
     init_seeds(sk["sim_seed"], env)
     init_seeds(sk["expert_seed"], env_expert)
-    alg = init_alg(idx, env, env_eval, env_expert, actor, critics, q_targets, q_critics, models,
-                   inputs_dict["alg_kwargs"], inputs_dict["mf_update_kwargs"], expert, init_expert_rms_stats)
+    if pack is not None:
+        inputs_dict["alg_kwargs"]["_pack"] = pack
+    return init_alg(idx, env, env_eval, env_expert, actor, critics, q_targets, q_critics, models,
+                    inputs_dict["alg_kwargs"], inputs_dict["mf_update_kwargs"], expert, init_expert_rms_stats)
+
+
+def train(inputs_dict):
+    """Training on one seed (reference train.py:33-107)."""
+    alg = build_alg(inputs_dict)
     return alg.train(inputs_dict["alg_kwargs"]["total_timesteps"], inputs_dict)
+
+
+def lockstep_ok(args, env_kwargs) -> bool:
+    """Whether the runs of a process can train as packed seeds in lock-step (sac_eo.algs.lockstep)."""
+    if args.serial_runs or args.alg_type not in ("sac", "sac_imit") or args.env_batch_type != "steps":
+        return False
+    if args.actor_layer_norm:
+        return False
+    if args.alg_type == "sac":            # G updates every real_step_mod steps of an EPISODE
+        env = init_env(**env_kwargs)
+        return getattr(env, "terminate", True) is False
+    return True
+
+
+def train_packed(inputs_list):
+    """The runs of ``inputs_list`` as seeds of one packed handle, in lock-step."""
+    from .algs.lockstep import run_lockstep
+    algs, shared = [], None
+    for i, d in enumerate(inputs_list):
+        alg = build_alg(d, pack=(shared, i, len(inputs_list)))
+        shared = shared if shared is not None else alg.engine._eng
+        algs.append(alg)
+    return run_lockstep(algs, shared, inputs_list[0]["alg_kwargs"]["total_timesteps"], inputs_list)
 
 
 def main(argv=None):
@@ -73,18 +107,24 @@ def main(argv=None):
         rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
         torch.cuda.set_device(local)
         runs = runs[rank::ws]
-    names = {}
+    names, run_inputs = {}, []
     for r in runs:
         d = copy.deepcopy(inputs_dict)
         d["setup_kwargs"].update(idx=args.runs_start + r, setup_seed=int(seeds["setup"][r]),
                                  sim_seed=int(seeds["sim"][r]), eval_seed=int(seeds["eval"][r]),
                                  expert_seed=int(seeds["expert"][r]), algorithm_seed=int(seeds["algorithm"][r]))
-        d = import_inputs(d)                         # train_utils.py:20-92 (no-op without --import_file)
-        names[r] = train(d)
+        run_inputs.append(import_inputs(d))          # train_utils.py:20-92 (no-op without --import_file)
+    if len(runs) > 1 and lockstep_ok(args, inputs_dict["env_kwargs"]):
+        names = dict(zip(runs, train_packed(run_inputs)))
+    else:
+        for r, d in zip(runs, run_inputs):
+            names[r] = train(d)
     if ws > 1:                                       # every rank's runs are on disk before gathering
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=ws)
+        import datetime
+        # ranks may finish their runs far apart: no collective timeout in the gathering group
+        dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=datetime.timedelta(days=7))
         dist.barrier()
         allnames = [None] * ws
         dist.all_gather_object(allnames, names)

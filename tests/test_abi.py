@@ -31,7 +31,7 @@ def test_struct_layouts():
     assert N.Config.buffer_capacity.offset == 32
     assert ctypes.sizeof(N.Config) == 208          # gcc: sizeof(sacx_config)
     assert N.Config.act_per_layer.offset == 172 and N.Config.act_layers.offset == 176
-    assert N.Config.delta_clip_pred.offset == 200
+    assert N.Config.delta_clip_pred.offset == 200 and N.Config.single_seed_plan.offset == 204
     assert N.Config.reward_loss_coef.offset == 128
     assert N.Config.gemm_bf16.offset == 132
     assert N.Config.seeds.offset == 136

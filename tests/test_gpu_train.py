@@ -61,3 +61,47 @@ def test_train_one_model_and_imported_expert(gpu_available, tmp_path):
     assert len(log["final"]["model_weights"]) == 1
     assert np.all(np.isfinite(log["train"]["p_loss"])) and len(log["train"]["p_loss"]) == 1600 - 300
     assert log["train"]["expert_steps"][-1] == 20           # the imported expert collected the expert rows
+
+
+def _logs_equal(a, b):
+    """Two runs' checkpoint logs, bit for bit except wall-clock fields."""
+    assert set(a["train"]) == set(b["train"])
+    for k in a["train"]:
+        if "time" in k:
+            continue
+        assert np.array_equal(np.asarray(a["train"][k]), np.asarray(b["train"][k]), equal_nan=True), k
+    fa, fb = a["final"], b["final"]
+    assert set(fa) == set(fb)
+    for k in fa:
+        if k == "rms_stats":
+            continue
+        xa, xb = fa[k], fb[k]
+        flat_a = [np.asarray(x) for x in (xa if isinstance(xa, list) else [xa])]
+        flat_b = [np.asarray(x) for x in (xb if isinstance(xb, list) else [xb])]
+        for u, v in zip(flat_a, flat_b):
+            if isinstance(u, np.ndarray) and u.dtype == object:
+                for p, q in zip(u, v):
+                    assert np.array_equal(np.asarray(p), np.asarray(q)), k
+            else:
+                assert np.array_equal(u, v), k
+
+
+@pytest.mark.parametrize("alg,extra", [("sac_imit", []), ("sac", []),
+                                       ("sac_imit", ["--update_normalizers", "--only_model_normalizer"])])
+def test_packed_runs_equal_serial_runs(gpu_available, tmp_path, alg, extra):
+    """--runs 3 as three lock-step seeds of one packed handle (sac_eo.algs.lockstep) vs the same
+    three runs one after another: every run's log identical, bit for bit."""
+    from sac_eo.train import main
+    from sac_eo.common.logger import load_log
+    argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", "64", "64",
+            "--critic_layers", "64", "64", "--actor_activations", "relu", "--critic_activations", "relu",
+            "--model_layers", "64", "64", "--total_timesteps", "1400", "--env_batch_size_init", "300",
+            "--env_horizon", "200", "--sac_batch_size", "64", "--model_batch_size", "50",
+            "--model_num_epochs", "1", "--seed", "11", "--runs", "3"] + extra
+    packed = load_log(main(argv + ["--save_path", str(tmp_path / "packed")]))
+    serial = load_log(main(argv + ["--serial_runs", "--save_path", str(tmp_path / "serial")]))
+    assert len(packed) == len(serial) == 3
+    for a, b in zip(packed, serial):
+        _logs_equal(a, b)
+    # the runs are different learners (different seeds)
+    assert not np.array_equal(packed[0]["final"]["actor_weights"][0], packed[1]["final"]["actor_weights"][0])

@@ -1,0 +1,26 @@
+"""Wall time of ``python -m sac_eo.train --runs K`` as K lock-step packed seeds vs the same K runs
+one after another (--serial_runs), on one GPU.  Usage: packed_runs_time.py [K] [alg]."""
+import os
+import sys
+import tempfile
+import time
+
+sys.path[:0] = ["sac-expert_amd"]
+
+from sac_eo.train import main   # noqa: E402
+
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+alg = sys.argv[2] if len(sys.argv) > 2 else "sac_imit"
+argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", "256", "256",
+        "--critic_layers", "256", "256", "--actor_activations", "relu", "--critic_activations", "relu",
+        "--total_timesteps", "3000", "--env_batch_size_init", "1000", "--model_num_epochs", "1",
+        "--seed", "0", "--runs", str(K)]
+out = {}
+for mode in ("packed", "serial"):
+    d = tempfile.mkdtemp()
+    t0 = time.perf_counter()
+    main(argv + ["--save_path", d] + (["--serial_runs"] if mode == "serial" else []))
+    out[mode] = time.perf_counter() - t0
+    print(f"{mode}: {K} runs of {alg} (256x2, 3000 steps: 1000 collected, 2000 loop steps with updates) "
+          f"in {out[mode]:.1f} s", flush=True)
+print(f"packed / serial speed-up: {out['serial'] / out['packed']:.2f}x")
