@@ -197,7 +197,7 @@ class SACBase:
 
     def _add(self, s, a, r, sp, d, track_episode=False):
         rows = self._add_rows(s, a, r, sp, d)
-        self._added(rows, self.engine.append(*rows), track_episode)
+        self._added(rows, self.engine.append(*rows[:5]), track_episode)
 
     @staticmethod
     def _add_rows(s, a, r, sp, d):

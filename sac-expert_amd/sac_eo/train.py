@@ -122,9 +122,9 @@ def main(argv=None):
     if ws > 1:                                       # every rank's runs are on disk before gathering
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        import datetime
+        from datetime import timedelta
         # ranks may finish their runs far apart: no collective timeout in the gathering group
-        dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=datetime.timedelta(days=7))
+        dist.init_process_group("gloo", rank=rank, world_size=ws, timeout=timedelta(days=7))
         dist.barrier()
         allnames = [None] * ws
         dist.all_gather_object(allnames, names)
