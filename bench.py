@@ -273,7 +273,9 @@ def drop_in_loop(eng, cfgd, n=300):
     """The drop-in train loop's rate (algs/base.py: one update per env step, as the
     reference's SAC_exp.train calls _update at SAC_expert.py:780): per iteration the
     behaviour action of one observation comes back to the host (actor.sample, B=1), one
-    transition is appended to the device ring, and step(1) runs one update."""
+    transition is appended to the device ring, and step(1) runs one update.  The action is
+    deterministic, the reference's default behaviour policy (SAC_expert.py:779, --random_act off):
+    it draws nothing, so step(1)'s speculative draw of the next update's randoms stands."""
     S, A = cfgd["S"], cfgd["A"]
     rs = np.random.RandomState(0)
     obs = [rs.normal(size=S).astype(np.float32) for _ in range(16)]   # a gym env's host arrays
@@ -282,7 +284,7 @@ def drop_in_loop(eng, cfgd, n=300):
 
     def it(j):
         o, o2 = obs[j % 16], obs[(j + 1) % 16]
-        a = eng.act_host(o, deterministic=False)               # host env gets the action
+        a = eng.act_host(o, deterministic=True)                # host env gets the action
         eng.append(o[None], a[None], r1, o2[None], d1)         # the transition, from the host
         eng.step(1, num_timesteps=j, ts_increment=1)
     for j in range(10):
@@ -294,7 +296,8 @@ def drop_in_loop(eng, cfgd, n=300):
     eng.sync()
     el = time.perf_counter() - t0
     return {"updates_per_s": round(n / el, 1), "us_per_iteration": round(el / n * 1e6, 2), "iterations": n,
-            "iteration": "act(1 host obs, stochastic) -> host action, append(1 host transition), step(1)"}
+            "iteration": "act(1 host obs, deterministic: the default behaviour policy) -> host action, "
+                         "append(1 host transition), step(1)"}
 
 
 def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):

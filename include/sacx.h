@@ -104,10 +104,11 @@ typedef struct sacx_config {
     float delta_clip_pred;      /* --delta_clip_pred: MSEModel.sample clips the normalised delta prediction
                                    (base_world_model.py:80-82) in the SAC-EO expert term; <= 0: None */
     /* --- ABI 6 --- */
-    int32_t single_seed_plan;   /* packed seeds: 1 = every seed runs the launch plan of a one-seed handle
-                                   (tile shapes, folds, fused heads), so each is bit-identical to its
-                                   one-seed run (sac_eo.train --runs in lock-step); 0 = the packed plan
-                                   (32x32 tiles from 1,024 rows, separate heads at >= 4 seeds: faster) */
+    int32_t single_seed_plan;   /* packed seeds: 1 = every seed sums as a one-seed handle does (the
+                                   one-seed plan's head folds and fused heads; 32x32 workgroup tiles, which
+                                   accumulate exactly as 16x16 ones, still by the packed row count), so
+                                   each is bit-identical to its one-seed run (sac_eo.train --runs in
+                                   lock-step); 0 = the packed plan (separate heads from 4 seeds: faster) */
 } sacx_config;
 
 typedef struct sacx_segment {

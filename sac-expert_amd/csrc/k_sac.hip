@@ -1574,8 +1574,16 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         S.has = a.st->has_gauss;
         S.gauss = a.st->gauss;
     }
+    if (a.backup != nullptr) {          // the state before this draw (undo of a speculative draw)
+        for (int i = t; i < 624; i += RNG_THREADS) a.backup->key[i] = a.st->key[i];
+        if (t == 0) {
+            a.backup->pos = pos0;
+            a.backup->has_gauss = a.st->has_gauss;
+            a.backup->gauss = a.st->gauss;
+        }
+    }
     // randint(high): masked rejection on 32-bit words (legacy bounded uint64 path, rng < 2^32)
-    const uint64_t high = (uint64_t)a.ctl->cur_size;
+    const uint64_t high = a.size_fixed > 0 ? (uint64_t)a.size_fixed : (uint64_t)a.ctl->cur_size;
     const uint64_t rng = high > 0 ? high - 1 : 0;
     uint64_t mask = rng;
     mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;

@@ -145,6 +145,8 @@ struct sacx_handle {
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
     int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
+    int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
+                              // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
     // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
@@ -166,6 +168,15 @@ struct sacx_handle {
     hipEvent_t pin_ev = nullptr;     // the last kernel that reads it
     bool pin_pending = false;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
+    // Speculative sampler of the drop-in loop: after sacx_sac_step(1) the next update's randoms are
+    // drawn on rng_stream, for the ring size one append later, while the host steps its env; the
+    // next sacx_sac_step(1) replays a graph without the sampler when the ring did reach that size.
+    // Every other consumer of the RNG stream first undoes the draw (spec_cancel).
+    bool spec_enabled = true;  // SACX_SPEC=0: off
+    bool spec_live = false;    // a speculative draw is (being) made
+    int64_t spec_size = 0;     // the ring size it assumed
+    int64_t cur_size_host = 0; // mirrors ctl->cur_size (appends, resync)
+    hipEvent_t spec_ev = nullptr, spec_go = nullptr;
 
     uint64_t add(const std::string& name, int64_t rows, int64_t cols, int dtype, int role) {
         const int esz = (dtype == SACX_I64 || dtype == SACX_F64) ? 8 : 4;
@@ -202,6 +213,19 @@ std::string mnorm(const sacx_handle* h, const char* x) {
 int fail(sacx_handle* h, const std::string& msg) {
     if (h) h->err = msg;
     return -1;
+}
+
+// Undoes a live speculative draw (sacx_sac_step(1)): waits for it, then restores the RNG state it
+// started from.  keep_state: only wait (the caller overwrites the state anyway).
+int spec_cancel(sacx_handle* h, bool keep_state = false) {
+    if (!h->spec_live) return 0;
+    h->spec_live = false;
+    if (hipStreamWaitEvent(h->stream, h->spec_ev, 0) != hipSuccess) return fail(h, "spec wait");
+    if (!keep_state &&
+        hipMemcpyAsync(h->ptr<RngState>("rng"), h->ptr<RngState>("rng.spec"), sizeof(RngState),
+                       hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
+        return fail(h, "spec restore");
+    return 0;
 }
 
 #define HIPCHK(h, x)                                                                    \
@@ -270,6 +294,7 @@ void build_layout(sacx_handle* h) {
     h->alias("rng.key", roff, 1, 624, SACX_U32, SACX_ROLE_STATE);
     h->alias("rng.pos", roff + offsetof(RngState, pos), 1, 2, SACX_I32, SACX_ROLE_STATE);
     h->alias("rng.gauss", roff + offsetof(RngState, gauss), 1, 1, SACX_F64, SACX_ROLE_STATE);
+    h->add("rng.spec", 1, sizeof(RngState) / 4, SACX_U32, SACX_ROLE_WORK);   // state before a speculative draw
     // per-slot update inputs: the sampler + gather of update j+2 run while update j+1
     // executes, so everything they write is double buffered
     const int ne1 = std::max(1, h->ne);
@@ -657,7 +682,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     const char* hpe = std::getenv("SACX_HEAD_PART");
     const int tqh = (H1 + 15) / 16;
     const bool head_part = Aout <= 8 && H1 <= 256 && H1 % 64 == 0 &&
-                           (hpe ? std::atoi(hpe) != 0 : h->tile32 == 0);
+                           (hpe ? std::atoi(hpe) != 0 : h->tile32_plan == 0);
     float* hpart = W("ws.hpart");
     // layer 1 of the actor on `rows` rows from row r0 of Ha1 / Ha2 (+ the head partials)
     auto actor_fwd1 = [&](int r0, int rows) {
@@ -703,7 +728,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // partials only 43.1k, both off 43.9k updates/s; tools/pk_ab.sh).
     const bool fold_hbw = Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
                           (!eo || (Hm0 <= 512 && Hm0 % 64 == 0)) &&
-                          (fhb ? std::atoi(fhb) != 0 : h->tile32 == 0);
+                          (fhb ? std::atoi(fhb) != 0 : h->tile32_plan == 0);
     // ---- actor head
     if (fuse_head) {
         HeadArgs& a = head_fused;
@@ -1651,6 +1676,9 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
 
 void sacx_destroy(sacx_handle* h) {
     if (!h) return;
+    if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);   // a speculative draw in flight
+    if (h->spec_ev) (void)hipEventDestroy(h->spec_ev);
+    if (h->spec_go) (void)hipEventDestroy(h->spec_go);
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto g : h->mgraphs)
         if (g) (void)hipGraphExecDestroy(g);
@@ -1719,9 +1747,10 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // the launches merged_body folds together always agree.  From 4,096 rows the dW + Adam
     // launches take 32x32 tiles too (tools/t32_dw.sh: Humanoid 4 seeds +3.5 %, 8 seeds +5 %,
     // bf16 4 seeds +8 %, HC 32 seeds +1.9 %; HC 8 / 16 seeds and one Humanoid seed even or worse)
-    const int64_t rows = (int64_t)h->plan_seeds * h->B;
-    h->tile32 = rows >= 4096 ? 1 : rows >= 1024 ? 2 : 0;
-    if (const char* e = std::getenv("SACX_T32")) h->tile32 = std::atoi(e);
+    auto t32_of = [](int64_t rows) { return rows >= 4096 ? 1 : rows >= 1024 ? 2 : 0; };
+    h->tile32 = t32_of((int64_t)h->seeds * h->B);
+    h->tile32_plan = t32_of((int64_t)h->plan_seeds * h->B);
+    if (const char* e = std::getenv("SACX_T32")) h->tile32 = h->tile32_plan = std::atoi(e);
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
     // an expensive one (Humanoid: 52k normals, 146 us per update) keeps 4, where the graph's
@@ -1755,16 +1784,22 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     }
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
+    HIPCHK(h, hipEventCreateWithFlags(&h->spec_ev, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->spec_go, hipEventDisableTiming));
+    if (const char* e = std::getenv("SACX_SPEC")) h->spec_enabled = std::atoi(e) != 0;
+    h->cur_size_host = 0;
     h->bound = true;
     return 0;
 }
 
 int sacx_resync(sacx_handle* h) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (spec_cancel(h, true)) return -1;     // the restored state is authoritative
     Ctl c{};
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(&c, h->ctl(), sizeof(Ctl), hipMemcpyDeviceToHost));
     h->seq_host = c.step_seq;
+    h->cur_size_host = c.cur_size;
     h->mfit_hosts[h->sel] = c.mfit_seq;
     return 0;
 }
@@ -1860,6 +1895,7 @@ int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const flo
     g.s = s; g.a = a; g.r = r; g.sp = sp; g.d = d; g.n = n; g.ctl = h->ctl();
     launch_append(g, h->stream);
     HIPCHK(h, hipGetLastError());
+    h->cur_size_host = std::min<int64_t>(h->cur_size_host + n, h->cap);
     return 0;
 }
 
@@ -2022,6 +2058,7 @@ int sacx_perm_push(sacx_handle* h, const int32_t* perms, int64_t n_steps) {
 
 int sacx_rng_seed(sacx_handle* h, uint32_t seed) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (spec_cancel(h, true)) return -1;
     RngState st{};
     for (int pos = 0; pos < 624; ++pos) {       // init_genrand (seeding.py:12 -> np.random.seed)
         st.key[pos] = seed;
@@ -2037,6 +2074,7 @@ int sacx_rng_seed(sacx_handle* h, uint32_t seed) {
 
 int sacx_rng_set_state(sacx_handle* h, const uint32_t key[624], int32_t pos, int32_t has_gauss, double gauss) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (spec_cancel(h, true)) return -1;
     if (pos < 0 || pos > 624) return fail(h, "pos out of range");
     RngState st{};
     std::memcpy(st.key, key, sizeof(st.key));
@@ -2050,6 +2088,7 @@ int sacx_rng_set_state(sacx_handle* h, const uint32_t key[624], int32_t pos, int
 
 int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t* has_gauss, double* gauss) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (spec_cancel(h)) return -1;
     RngState st{};
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(&st, h->ptr<RngState>("rng"), sizeof(st), hipMemcpyDeviceToHost));
@@ -2065,9 +2104,21 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     if (h->dp_local) return fail(h, "in-process data-parallel ranks step together (sacx_dp_local_step)");
     if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n_steps <= 0) return 0;
+    // the drop-in loop's one-update steps: the randoms drawn speculatively after the previous
+    // step are valid when the ring now holds the size they assumed (nothing else drew meanwhile:
+    // every other consumer of the stream undid the draw)
+    const bool spec_ok = h->spec_enabled && n_steps == 1 && flags == 0 && h->seeds == 1 && h->dp_ranks == 0;
+    const bool use_spec = spec_ok && h->spec_live && h->spec_size == h->cur_size_host;
+    if (!use_spec && spec_cancel(h)) return -1;
     launch_set_ctl(h->ctl0(), num_timesteps, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
-    if (flags & SACX_STEP_EAGER) {
+    if (use_spec) {
+        h->spec_live = false;
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->spec_ev, 0));
+        hipGraphExec_t g;                 // gather + update, the randoms already in slot 0
+        if (get_graph(h, 1, false, &g)) return -1;
+        HIPCHK(h, hipGraphLaunch(g, h->stream));
+    } else if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
         HIPCHK(h, hipGetLastError());
     } else {
@@ -2078,6 +2129,26 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     }
     h->seq_host += n_steps;
     if (h->nccl_failed) return fail(h, "ncclAllReduce failed");
+    if (spec_ok) {
+        // the next update's randint + normals into slot 0 on the side stream, for the ring one
+        // append larger, while the caller acts and steps its environment
+        const Launch* R = nullptr;
+        for (const Launch& L : h->plan[0])
+            if (L.kind == Launch::RNG) { R = &L; break; }
+        if (!R) return fail(h, "internal: no sampler launch");
+        RngArgs r = R->rng;
+        r.reset_seq = 1;
+        r.nupd = 1;
+        r.size_fixed = std::min<int64_t>(h->cur_size_host + 1, h->cap);
+        r.backup = h->ptr<RngState>("rng.spec");
+        HIPCHK(h, hipEventRecord(h->spec_go, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(h->rng_stream, h->spec_go, 0));
+        launch_rng(r, h->rng_stream);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipEventRecord(h->spec_ev, h->rng_stream));
+        h->spec_live = true;
+        h->spec_size = r.size_fixed;
+    }
     return 0;
 }
 
@@ -2134,6 +2205,7 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
 
 int sacx_sync(sacx_handle* h) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (spec_cancel(h)) return -1;           // an observation point: the arena holds no speculative draw
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -2161,6 +2233,7 @@ int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int
 }
 
 int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t cap) {
+    if (h && h->bound && spec_cancel(h)) return -1;
     if (!h || !h->bound) return fail(h, "not bound");
     const auto& plan = h->plan[0];
     const int n = (int)plan.size();
@@ -2207,6 +2280,7 @@ static void actor_hidden(sacx_handle* h, const float* X, int ldX, int m, float* 
 
 int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (!deterministic && spec_cancel(h)) return -1;   // a draw from the stream: undo the speculative one
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
     auto W = [&](const std::string& nm) { return h->f(nm); };
@@ -2288,6 +2362,7 @@ static NetIOArgs netio_base(sacx_handle* h, bool model = false) {
 
 int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out, float* nlp_out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (spec_cancel(h)) return -1;
     if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n < 0 || (n > 0 && (!s || !pi_out || !nlp_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
@@ -2479,6 +2554,7 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
     if (n < 0 || horizon < 0) return fail(h, "bad arguments");
     if (n == 0 || horizon == 0) return 0;
     if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
+    if (!deterministic && spec_cancel(h)) return -1;
     // one captured graph per (model, shape, clips, pointers): the Python host keeps its
     // staging / output buffers per shape, so repeated calls replay (SACX_ROLL_GRAPH=0: eager)
     const char* rg = std::getenv("SACX_ROLL_GRAPH");
@@ -2519,6 +2595,7 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     const bool disc = (flags & SACX_DIAG_DISC) != 0, ea = (flags & SACX_DIAG_EXPERT_ACTIONS) != 0;
     if (disc && h->nm < 2) return fail(h, "_calc_disc compares two world models (num_models = 2)");
     if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
+    if (!ea && spec_cancel(h)) return -1;
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
@@ -2594,6 +2671,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
                       int64_t* n_launches) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!kernel || std::strcmp(kernel, "k_gemm") != 0) return fail(h, "only k_gemm carries timestamps");
+    if (spec_cancel(h)) return -1;
     if (!avg_us || n_replays <= 0) return fail(h, "bad arguments");
     const int G = h->graph_steps;
     KTimeMap kt;
@@ -2664,6 +2742,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
 int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, double* ms_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!ms_out || n_replays <= 0) return fail(h, "bad arguments");
+    if (spec_cancel(h)) return -1;
     int skip = -1;
     if (skip_kernel && skip_kernel[0]) {
         for (int k = Launch::RNG; k <= Launch::MFINAL; ++k)

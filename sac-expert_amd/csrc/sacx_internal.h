@@ -280,6 +280,11 @@ struct RngArgs {
     int32_t reset_seq;     // first sampler launch of a chain: rng_seq = step_seq
     int32_t nupd;          // consecutive updates drawn by this launch (slots slot .. slot+nupd-1)
     int64_t slot_bytes;    // distance between consecutive slots' buffers
+    // the speculative draw of the drop-in loop (sacx_sac_step(1)): randint's bound given by the
+    // host (the ring size after the append to come) instead of ctl->cur_size, and the state
+    // before the draw saved to `backup` so the draw can be undone
+    int64_t size_fixed;    // > 0: randint(size_fixed)
+    RngState* backup;      // nullable
     // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
     int64_t sstride;

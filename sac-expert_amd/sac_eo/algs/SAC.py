@@ -19,8 +19,8 @@ class SAC(SACBase):
         num_timesteps = 0
         if eval_points is not None:
             self._evaluate(num_timesteps)
-        num_timesteps += self._collect_env_data(num_timesteps, update_normalizers=self.update_normalizers,
-                                                only_model_normalizer=self.only_model_normalizer)
+        num_timesteps += yield from self._collect_env_data_steps(num_timesteps, self.update_normalizers,
+                                                                 self.only_model_normalizer)
         episode_step, episode, episode_reward, done = 0, 0, 0.0, True
         t_episode = time.time()
         obs = None

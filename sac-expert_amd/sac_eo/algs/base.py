@@ -218,7 +218,10 @@ class SACBase:
     # one on this learner's engine; sac_eo.algs.lockstep serves K learners of one packed handle with
     # one launch chain per request (the reference's --runs, sac_eo/train.py:118-152).
     def train(self, total_timesteps, params):
-        loop = self._train_loop(total_timesteps, params)
+        return self._drive(self._train_loop(total_timesteps, params))
+
+    def _drive(self, loop):
+        """Serves a request generator on this learner's engine; returns its value."""
         try:
             req = next(loop)
             while True:
@@ -245,12 +248,33 @@ class SACBase:
 
     def _collect_env_data(self, num_timesteps, update_normalizers=True, only_model_normalizer=False):
         """SAC_expert.py:625-684: rollouts of the stochastic actor until the batch is full."""
+        return self._drive(self._collect_env_data_steps(num_timesteps, update_normalizers, only_model_normalizer))
+
+    def _trajectory_steps(self, env, horizon, deterministic=False):
+        """trajectory_sampler(env, actor, horizon, eval=True) (samplers.py:3-70) with the actor's
+        sample() as an "act" request per step."""
+        s_t, a_t, r_t, sp_t, d_t, J = [], [], [], [], [], 0.0
+        s = env.reset()
+        for t in range(horizon):
+            a = yield ("act", s, deterministic)
+            sp, r, d, _ = env.step(self.actor.clip(a))
+            J += r
+            if t == horizon - 1:
+                d = False
+            s_t.append(s); a_t.append(a); r_t.append(r); sp_t.append(sp); d_t.append(d)
+            s = sp
+            if d:
+                break
+        return (np.array(s_t, np.float32), np.array(a_t, np.float32), np.array(r_t, np.float32),
+                np.array(sp_t, np.float32), np.array(d_t), J)
+
+    def _collect_env_data_steps(self, num_timesteps, update_normalizers=True, only_model_normalizer=False):
         t0 = time.time()
         batch_size = self.env_batch_size_init if num_timesteps == 0 else self.env_batch_size
         steps_start, J_all, cur = self.steps_total, [], 0
         while cur < batch_size:
             horizon = min(batch_size - cur, self.env_horizon) if self.env_batch_type == "steps" else self.env_horizon
-            s, a, r, sp, d, J = trajectory_sampler(self.env, self.actor, horizon, eval=True)
+            s, a, r, sp, d, J = yield from self._trajectory_steps(self.env, horizon)
             if update_normalizers:
                 if only_model_normalizer:
                     self.model_normalizer.update_rms(s, a, r, sp)

@@ -63,27 +63,29 @@ def test_train_one_model_and_imported_expert(gpu_available, tmp_path):
     assert log["train"]["expert_steps"][-1] == 20           # the imported expert collected the expert rows
 
 
+def _same(x, y, what):
+    """Nested lists / dicts of arrays and scalars, bit for bit."""
+    if isinstance(x, dict):
+        assert set(x) == set(y), what
+        for k in x:
+            _same(x[k], y[k], f"{what}.{k}")
+    elif isinstance(x, (list, tuple)):
+        assert len(x) == len(y), what
+        for i, (u, v) in enumerate(zip(x, y)):
+            _same(u, v, f"{what}[{i}]")
+    elif x is None:
+        assert y is None, what
+    else:
+        assert np.array_equal(np.asarray(x), np.asarray(y), equal_nan=True), what
+
+
 def _logs_equal(a, b):
     """Two runs' checkpoint logs, bit for bit except wall-clock fields."""
     assert set(a["train"]) == set(b["train"])
     for k in a["train"]:
-        if "time" in k:
-            continue
-        assert np.array_equal(np.asarray(a["train"][k]), np.asarray(b["train"][k]), equal_nan=True), k
-    fa, fb = a["final"], b["final"]
-    assert set(fa) == set(fb)
-    for k in fa:
-        if k == "rms_stats":
-            continue
-        xa, xb = fa[k], fb[k]
-        flat_a = [np.asarray(x) for x in (xa if isinstance(xa, list) else [xa])]
-        flat_b = [np.asarray(x) for x in (xb if isinstance(xb, list) else [xb])]
-        for u, v in zip(flat_a, flat_b):
-            if isinstance(u, np.ndarray) and u.dtype == object:
-                for p, q in zip(u, v):
-                    assert np.array_equal(np.asarray(p), np.asarray(q)), k
-            else:
-                assert np.array_equal(u, v), k
+        if "time" not in k:
+            _same(a["train"][k], b["train"][k], k)
+    _same(a["final"], b["final"], "final")
 
 
 @pytest.mark.parametrize("alg,extra", [("sac_imit", []), ("sac", []),

@@ -54,7 +54,7 @@ def test_packed_runs_host(monkeypatch, tmp_path, alg):
     big = [e for e in engines if e.seeds == 3]
     assert len(big) == 1 and big[0].cfg.single_seed_plan
     steps = [c for c in big[0].calls if isinstance(c, tuple)]
-    assert big[0].calls.count("act_seeds") == 2300 and big[0].calls.count("append_seeds") == 2300
+    assert big[0].calls.count("act_seeds") == 300 + 2300 and big[0].calls.count("append_seeds") == 2300
     assert len(steps) == (2300 if alg == "sac_imit" else 2 * 334 + 1 * 100)
     serial = load_log(main(_argv(alg, tmp_path / "s", ["--runs", "3", "--serial_runs"])))
     for a, b in zip(packed, serial):

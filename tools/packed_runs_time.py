@@ -8,6 +8,8 @@ import time
 sys.path[:0] = ["sac-expert_amd"]
 
 from sac_eo.train import main   # noqa: E402
+from sac_eo.common.logger import load_log   # noqa: E402
+import numpy as np   # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 alg = sys.argv[2] if len(sys.argv) > 2 else "sac_imit"
@@ -19,8 +21,12 @@ out = {}
 for mode in ("packed", "serial"):
     d = tempfile.mkdtemp()
     t0 = time.perf_counter()
-    main(argv + ["--save_path", d] + (["--serial_runs"] if mode == "serial" else []))
+    path = main(argv + ["--save_path", d] + (["--serial_runs"] if mode == "serial" else []))
     out[mode] = time.perf_counter() - t0
+    logs = load_log(path)
+    parts = {k: sum(float(np.sum(lg["train"].get(k, 0.0))) for lg in logs)
+             for k in ("time_env_data", "time_model_fit", "expert_time")}
+    print(f"  {mode} parts summed over runs (s): " + ", ".join(f"{k} {v:.2f}" for k, v in parts.items()))
     print(f"{mode}: {K} runs of {alg} (256x2, 3000 steps: 1000 collected, 2000 loop steps with updates) "
           f"in {out[mode]:.1f} s", flush=True)
 print(f"packed / serial speed-up: {out['serial'] / out['packed']:.2f}x")
