@@ -270,12 +270,13 @@ def _cpu_port_rate(cfgd, seconds, threads):
 
 
 def drop_in_loop(eng, cfgd, n=300):
-    """The drop-in train loop's rate (algs/base.py: one update per env step, as the
-    reference's SAC_exp.train calls _update at SAC_expert.py:780): per iteration the
-    behaviour action of one observation comes back to the host (actor.sample, B=1), one
-    transition is appended to the device ring, and step(1) runs one update.  The action is
-    deterministic, the reference's default behaviour policy (SAC_expert.py:779, --random_act off):
-    it draws nothing, so step(1)'s speculative draw of the next update's randoms stands."""
+    """The drop-in train loop's rate (algs/SAC_expert.py: one update per env step in the
+    reference's order, SAC_expert.py:779-797: a = actor.sample(obs); _update; env.step(a);
+    env_data.add): per iteration the behaviour action of one observation comes back to the host
+    (B=1), step(1) runs one update, and the transition is appended to the device ring.  The
+    action is deterministic, the reference's default behaviour policy (:779, --random_act off).
+    act_host queues the next update's sampler draw behind the action kernel, so step(1) replays
+    the sampler-less graph (spec_hits counts it)."""
     S, A = cfgd["S"], cfgd["A"]
     rs = np.random.RandomState(0)
     obs = [rs.normal(size=S).astype(np.float32) for _ in range(16)]   # a gym env's host arrays
@@ -285,19 +286,21 @@ def drop_in_loop(eng, cfgd, n=300):
     def it(j):
         o, o2 = obs[j % 16], obs[(j + 1) % 16]
         a = eng.act_host(o, deterministic=True)                # host env gets the action
-        eng.append(o[None], a[None], r1, o2[None], d1)         # the transition, from the host
         eng.step(1, num_timesteps=j, ts_increment=1)
+        eng.append(o[None], a[None], r1, o2[None], d1)         # the transition, from the host
     for j in range(10):
         it(j)
     eng.sync()
+    h0 = eng.spec_hits()
     t0 = time.perf_counter()
     for j in range(n):
         it(j)
     eng.sync()
     el = time.perf_counter() - t0
     return {"updates_per_s": round(n / el, 1), "us_per_iteration": round(el / n * 1e6, 2), "iterations": n,
+            "speculative_steps": eng.spec_hits() - h0,
             "iteration": "act(1 host obs, deterministic: the default behaviour policy) -> host action, "
-                         "append(1 host transition), step(1)"}
+                         "step(1), append(1 host transition)"}
 
 
 def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):

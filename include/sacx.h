@@ -300,6 +300,10 @@ int sacx_dp_local_step(sacx_handle* const* handles, int32_t nranks, int64_t n_st
                        int32_t ts_increment);
 
 /* --- measurement ----------------------------------------------------------- */
+/* One-update sacx_sac_step calls that replayed the sampler-less graph on randoms drawn
+ * speculatively by the preceding sacx_actor_act_host (the drop-in loop's cadence act -> step ->
+ * append of SAC_expert.py:779-797); the other steps drew their own.  -1 for a NULL handle. */
+int64_t sacx_spec_hits(const sacx_handle* h);
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);
 /* Runs n_steps updates eagerly with a HIP event around every launch on the
  * bound stream and returns the summed device milliseconds per launch index

@@ -28,10 +28,22 @@
 namespace sacx {
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef short shortx4 __attribute__((ext_vector_type(4)));
 
-// fp32 -> bf16 bits, round to nearest even (v_cvt_pk_bf16_f32 on gfx950)
-__device__ __forceinline__ short bf16_bits(float x) { return __builtin_bit_cast(short, (__bf16)x); }
+// fp32 -> bf16 (__bf16 conversion): round to nearest even (v_cvt_pk_bf16_f32 on gfx950)
+
+// One gfx950 v_mfma_f32_16x16x32_bf16 over TWO 16-wide k slabs held the f32 way: lane (r, grp)
+// has k = 4 grp + 0..3 of slab 0 in a0 / b0 and of slab 1 in a1 / b1.  The instruction wants k =
+// 8 grp + j in element j; A and B carry the same k permutation (element j <-> slab j >> 2, k
+// 4 grp + (j & 3)), and a permutation of k common to both operands leaves the sum over k as is.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ floatx4 mfma_bf16_2slab(const float (&a0)[4], const float (&a1)[4], const float (&b0)[4],
+                                                   const float (&b1)[4], floatx4 c) {
+    const bf16x8_t av = {(__bf16)a0[0], (__bf16)a0[1], (__bf16)a0[2], (__bf16)a0[3],
+                         (__bf16)a1[0], (__bf16)a1[1], (__bf16)a1[2], (__bf16)a1[3]};
+    const bf16x8_t bv = {(__bf16)b0[0], (__bf16)b0[1], (__bf16)b0[2], (__bf16)b0[3],
+                         (__bf16)b1[0], (__bf16)b1[1], (__bf16)b1[2], (__bf16)b1[3]};
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, c, 0, 0, 0);
+}
 
 #define LOG2PI_F 0x1.d67f1ep+0f     // f32 log(f32(2*pi))  (continuous_actors.py:360)
 #define LN2_F 0x1.62e430p-1f        // f32(np.log(2.))     (continuous_actors.py:366)
@@ -813,12 +825,14 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         acc0[s] = floatx4{0.f, 0.f, 0.f, 0.f};
         acc1[s] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
+    // bf16: two k slabs per load group, one 16x16x32 MFMA per sub-tile and slab pair
+    constexpr int NS = BF ? 2 : SACX_T32_NS;
     auto main_loop = [&](auto vt) {   // unswitched on the problem's float4 flag, as gemm_core
     constexpr bool V = decltype(vt)::value;
-    for (int it = it0; it < it1; it += SACX_T32_NS) {
-        float a[SACX_T32_NS][2][4], b[SACX_T32_NS][2][4];
+    for (int it = it0; it < it1; it += NS) {
+        float a[NS][2][4], b[NS][2][4];
 #pragma unroll
-        for (int u = 0; u < SACX_T32_NS; ++u) {
+        for (int u = 0; u < NS; ++u) {
             const int k0 = (it + u) * 16 + grp * 4;
             const int k0e = (it + u < it1) ? k0 : (1 << 30);
             load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, ma, maok, k0e, a[u][0], rw);
@@ -827,22 +841,19 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, nb, nbok, k0e, b[u][1]);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (BF) {
+            // slab pairs (it0 + 2i, it0 + 2i + 1), alternately into acc0 / acc1 -- the pairs and
+            // accumulators of gemm_core's 16x16 path (groups of 4 from it0), so both tile shapes
+            // sum alike
 #pragma unroll
-        for (int u = 0; u < SACX_T32_NS; ++u) {
-            if constexpr (BF) {
-#pragma unroll
-                for (int s = 0; s < 4; ++s) {
-                    const float (&av)[4] = a[u][s >> 1];
-                    const float (&bv)[4] = b[u][s & 1];
-                    const shortx4 as = {bf16_bits(av[0]), bf16_bits(av[1]), bf16_bits(av[2]), bf16_bits(av[3])};
-                    const shortx4 bs = {bf16_bits(bv[0]), bf16_bits(bv[1]), bf16_bits(bv[2]), bf16_bits(bv[3])};
-                    // slab parity relative to it0, as gemm_core's 16x16 path (its groups of 4
-                    // start at it0): the same slabs land in acc0 / acc1 for any SACX_T32_NS
-                    if ((it + u - it0) & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc1[s], 0, 0, 0);
-                    else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(as, bs, acc0[s], 0, 0, 0);
-                }
-                continue;
+            for (int s = 0; s < 4; ++s) {
+                if (((it - it0) >> 1) & 1) acc1[s] = mfma_bf16_2slab(a[0][s >> 1], a[1][s >> 1], b[0][s & 1], b[1][s & 1], acc1[s]);
+                else acc0[s] = mfma_bf16_2slab(a[0][s >> 1], a[1][s >> 1], b[0][s & 1], b[1][s & 1], acc0[s]);
             }
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < NS; ++u) {
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -1122,9 +1133,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) a[j] = (k0 + j < g.K) ? As[r][k0 + j] : 0.f;
                 if constexpr (BF) {
-                    const shortx4 av = {bf16_bits(a[0]), bf16_bits(a[1]), bf16_bits(a[2]), bf16_bits(a[3])};
-                    const shortx4 bv = {bf16_bits(bp[0]), bf16_bits(bp[1]), bf16_bits(bp[2]), bf16_bits(bp[3])};
-                    acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc0, 0, 0, 0);
+                    const float z[4] = {0.f, 0.f, 0.f, 0.f};      // one slab: the pair's second is zero
+                    acc0 = mfma_bf16_2slab(a, z, bp, z, acc0);
                 } else {
                     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], bp[0], acc0, 0, 0, 0);
                     acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], bp[1], acc1, 0, 0, 0);
@@ -1178,15 +1188,13 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                 if (store && it0 + u < it1)
                     *reinterpret_cast<float4*>(&Da2[(size_t)m * g.K + k0]) = float4{a[u][0], a[u][1], a[u][2], a[u][3]};
             }
+            if constexpr (BF) {
+                acc0 = mfma_bf16_2slab(a[0], a[1], b[0], b[1], acc0);
+                acc1 = mfma_bf16_2slab(a[2], a[3], b[2], b[3], acc1);
+                return;
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                if constexpr (BF) {
-                    const shortx4 av = {bf16_bits(a[u][0]), bf16_bits(a[u][1]), bf16_bits(a[u][2]), bf16_bits(a[u][3])};
-                    const shortx4 bv = {bf16_bits(b[u][0]), bf16_bits(b[u][1]), bf16_bits(b[u][2]), bf16_bits(b[u][3])};
-                    if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc1, 0, 0, 0);
-                    else acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc0, 0, 0, 0);
-                    continue;
-                }
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
                 acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1], b[u][1], acc1, 0, 0, 0);
                 acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);
@@ -1216,17 +1224,14 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, n, nok, k0e, b[u]);
         }
         __builtin_amdgcn_sched_barrier(0);
+        if constexpr (BF) {
+            // slabs (0, 1) and (2, 3) of the group, one v_mfma_f32_16x16x32_bf16 each
+            acc0 = mfma_bf16_2slab(a[0], a[1], b[0], b[1], acc0);
+            acc1 = mfma_bf16_2slab(a[2], a[3], b[2], b[3], acc1);
+            continue;
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            if constexpr (BF) {
-                // lane (r, grp) holds k = 4 grp + 0..3 of this 16-wide k slab: exactly the
-                // A / B operand of one v_mfma_f32_16x16x16_bf16
-                const shortx4 av = {bf16_bits(a[u][0]), bf16_bits(a[u][1]), bf16_bits(a[u][2]), bf16_bits(a[u][3])};
-                const shortx4 bv = {bf16_bits(b[u][0]), bf16_bits(b[u][1]), bf16_bits(b[u][2]), bf16_bits(b[u][3])};
-                if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc1, 0, 0, 0);
-                else acc0 = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(av, bv, acc0, 0, 0, 0);
-                continue;
-            }
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1], b[u][1], acc1, 0, 0, 0);
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);

@@ -163,20 +163,25 @@ struct sacx_handle {
     std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;   // (G, with_rng, skipped kind)
     std::vector<std::pair<RollKey, hipGraphExec_t>> roll_graphs;     // sacx_rollout replays
     std::vector<hipEvent_t> events;
-    float* pin = nullptr;            // pinned host staging (STAGE_CAP floats), the _host entry points
-    float* pin_dev = nullptr;        // its device-side address (kernels read / write it in place)
+    float* pin = nullptr;            // pinned host staging (2 x STAGE_CAP floats), the _host entry points:
+    float* pin_dev = nullptr;        // [0, STAGE_CAP) appends, [STAGE_CAP, 2 STAGE_CAP) acts; pin_dev is its
+                                     // device-side address (kernels read / write it in place)
     hipEvent_t pin_ev = nullptr;     // the last kernel that reads it
     bool pin_pending = false;
     int64_t seq_host = 0;  // updates issued (mirrors ctl->step_seq)
-    // Speculative sampler of the drop-in loop: after sacx_sac_step(1) the next update's randoms are
-    // drawn on rng_stream, for the ring size one append later, while the host steps its env; the
-    // next sacx_sac_step(1) replays a graph without the sampler when the ring did reach that size.
-    // Every other consumer of the RNG stream first undoes the draw (spec_cancel).
+    // Speculative sampler of the drop-in loop (the reference's cadence act -> _update -> env.step ->
+    // add, SAC_expert.py:779-797): when the caller steps one update at a time, sacx_actor_act_host
+    // queues the next update's randint + normals right behind the action kernel and returns once
+    // the action is back, so the draw runs while the host has the action; the next
+    // sacx_sac_step(1) then replays a graph without the sampler if the ring still holds the size
+    // the draw assumed.  Every other consumer of the RNG stream first undoes the draw (spec_cancel).
     bool spec_enabled = true;  // SACX_SPEC=0: off
-    bool spec_live = false;    // a speculative draw is (being) made
+    bool spec_live = false;    // a speculative draw is queued
+    bool last_step_one = false;  // the last sacx_sac_step was a plain one-update step
     int64_t spec_size = 0;     // the ring size it assumed
+    int64_t spec_hits = 0;     // one-update steps that used a speculative draw (sacx_spec_hits)
     int64_t cur_size_host = 0; // mirrors ctl->cur_size (appends, resync)
-    hipEvent_t spec_ev = nullptr, spec_go = nullptr;
+    hipEvent_t act_ev = nullptr;   // end of the last act_host kernel chain (its actions are on the host)
 
     uint64_t add(const std::string& name, int64_t rows, int64_t cols, int dtype, int role) {
         const int esz = (dtype == SACX_I64 || dtype == SACX_F64) ? 8 : 4;
@@ -215,18 +220,21 @@ int fail(sacx_handle* h, const std::string& msg) {
     return -1;
 }
 
-// Undoes a live speculative draw (sacx_sac_step(1)): waits for it, then restores the RNG state it
-// started from.  keep_state: only wait (the caller overwrites the state anyway).
+// Undoes a queued speculative draw (drawn on the bound stream, so stream order alone puts the
+// restore after it): restores the RNG state it started from.  keep_state: nothing to restore
+// (the caller overwrites the state anyway).
 int spec_cancel(sacx_handle* h, bool keep_state = false) {
     if (!h->spec_live) return 0;
     h->spec_live = false;
-    if (hipStreamWaitEvent(h->stream, h->spec_ev, 0) != hipSuccess) return fail(h, "spec wait");
     if (!keep_state &&
         hipMemcpyAsync(h->ptr<RngState>("rng"), h->ptr<RngState>("rng.spec"), sizeof(RngState),
                        hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
         return fail(h, "spec restore");
     return 0;
 }
+
+// the handles the speculative draw applies to: one learner, its own RNG stream
+bool spec_mode(const sacx_handle* h) { return h->spec_enabled && h->seeds == 1 && h->dp_ranks == 0 && !h->dp_local; }
 
 #define HIPCHK(h, x)                                                                    \
     do {                                                                                \
@@ -1553,6 +1561,33 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     return 0;
 }
 
+// The one-update graph of the drop-in loop's speculative path: gather + update reading the
+// randoms the speculative k_rng drew into slot kSpecSlot (not slot 0, so that slot 0 keeps the
+// randoms of the last update a caller observed: a cancelled draw leaves no trace in it).
+constexpr int kSpecSlot = 1;
+
+int get_spec_graph(sacx_handle* h, hipGraphExec_t* out) {
+    const auto key = std::make_tuple(1, 2, -1);
+    auto it = h->graphs.find(key);
+    if (it != h->graphs.end()) {
+        *out = it->second;
+        return 0;
+    }
+    if (2 * h->nbatch <= kSpecSlot || h->plan[kSpecSlot].empty()) return fail(h, "internal: no spare slot for the speculative draw");
+    HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+    for (const Launch& L : h->plan[kSpecSlot])   // the draw stamped pseq[kSpecSlot] itself
+        if (L.kind != Launch::RNG) enqueue(L, h, h->cap_stream);
+    hipGraph_t graph;
+    HIPCHK(h, hipStreamEndCapture(h->cap_stream, &graph));
+    hipGraphExec_t exec;
+    HIPCHK(h, hipGraphInstantiateWithFlags(&exec, graph, 0));
+    HIPCHK(h, hipGraphDestroy(graph));
+    HIPCHK(h, hipGraphUpload(exec, h->stream));
+    h->graphs[key] = exec;
+    *out = exec;
+    return 0;
+}
+
 // The graphs sacx_sac_step(n_steps) replays: n_steps / G full graphs of G updates, then the
 // remainder as ONE graph of exactly r updates (each graph pays its own sampler start-up and
 // alpha tail, so one remainder graph beats a chain of power-of-two pieces).  Up to
@@ -1676,9 +1711,8 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
 
 void sacx_destroy(sacx_handle* h) {
     if (!h) return;
-    if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);   // a speculative draw in flight
-    if (h->spec_ev) (void)hipEventDestroy(h->spec_ev);
-    if (h->spec_go) (void)hipEventDestroy(h->spec_go);
+    if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
+    if (h->act_ev) (void)hipEventDestroy(h->act_ev);
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto g : h->mgraphs)
         if (g) (void)hipGraphExecDestroy(g);
@@ -1784,8 +1818,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     }
     HIPCHK(h, hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking));
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
-    HIPCHK(h, hipEventCreateWithFlags(&h->spec_ev, hipEventDisableTiming));
-    HIPCHK(h, hipEventCreateWithFlags(&h->spec_go, hipEventDisableTiming));
+    HIPCHK(h, hipEventCreateWithFlags(&h->act_ev, hipEventDisableTiming));
     if (const char* e = std::getenv("SACX_SPEC")) h->spec_enabled = std::atoi(e) != 0;
     h->cur_size_host = 0;
     h->bound = true;
@@ -1903,12 +1936,17 @@ int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const flo
 // rows go into one pinned, device-mapped buffer that the kernels read (k_append, the obs
 // normaliser) and write (the action head) in place over PCIe: no DMA copy on either side,
 // whose fixed cost exceeds the whole transfer at these sizes.
-static int stage_begin(sacx_handle* h) {
+static int stage_alloc(sacx_handle* h) {
     if (!h->pin) {
-        HIPCHK(h, hipHostMalloc((void**)&h->pin, sizeof(float) * STAGE_CAP, hipHostMallocMapped));
+        HIPCHK(h, hipHostMalloc((void**)&h->pin, sizeof(float) * 2 * STAGE_CAP, hipHostMallocMapped));
         HIPCHK(h, hipHostGetDevicePointer((void**)&h->pin_dev, h->pin, 0));
         HIPCHK(h, hipEventCreateWithFlags(&h->pin_ev, hipEventDisableTiming));
     }
+    return 0;
+}
+// the append half: waits until its last reader (a k_append) has finished
+static int stage_begin(sacx_handle* h) {
+    if (stage_alloc(h)) return -1;
     if (h->pin_pending) HIPCHK(h, hipEventSynchronize(h->pin_ev));   // its last reader has finished
     h->pin_pending = false;
     return 0;
@@ -1940,6 +1978,26 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
     return 0;
 }
 
+// The speculative draw (see sacx_handle::spec_live): the sampler launch of slot kSpecSlot for one
+// update at the ring's current size, queued on the bound stream; it saves the state it starts
+// from into "rng.spec" for spec_cancel.
+static int spec_draw(sacx_handle* h) {
+    const Launch* R = nullptr;
+    for (const Launch& L : h->plan[kSpecSlot])
+        if (L.kind == Launch::RNG) { R = &L; break; }
+    if (!R) return fail(h, "internal: no sampler launch");
+    RngArgs r = R->rng;
+    r.reset_seq = 1;            // stamps pseq[kSpecSlot] = step_seq: the update that follows
+    r.nupd = 1;
+    r.size_fixed = h->cur_size_host;
+    r.backup = h->ptr<RngState>("rng.spec");
+    launch_rng(r, h->stream);
+    HIPCHK(h, hipGetLastError());
+    h->spec_live = true;
+    h->spec_size = h->cur_size_host;
+    return 0;
+}
+
 int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
@@ -1948,12 +2006,19 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
     if (chunk <= 0) return fail(h, "an observation row is larger than the pinned staging buffer (use sacx_actor_act)");
     for (int64_t done = 0; done < n; done += chunk) {
         const int64_t m = std::min(chunk, n - done);
-        if (stage_begin(h)) return -1;
-        std::memcpy(h->pin, obs + done * S, sizeof(float) * m * S);
-        const int rc = sacx_actor_act(h, h->pin_dev, m, deterministic, h->pin_dev + m * S);
+        if (stage_alloc(h)) return -1;
+        float* p = h->pin + STAGE_CAP;          // the act half: its last reader was a synchronous act
+        const float* g = h->pin_dev + STAGE_CAP;
+        std::memcpy(p, obs + done * S, sizeof(float) * m * S);
+        const int rc = sacx_actor_act(h, g, m, deterministic, (float*)g + m * S);
         if (rc) return rc;
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        std::memcpy(act_out + done * A, h->pin + m * S, sizeof(float) * m * A);
+        HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+        // the drop-in loop steps next: its randoms are drawn while the host has the action
+        if (done + m >= n && h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0 &&
+            spec_draw(h))
+            return -1;
+        HIPCHK(h, hipEventSynchronize(h->act_ev));
+        std::memcpy(act_out + done * A, p + m * S, sizeof(float) * m * A);
     }
     return 0;
 }
@@ -1995,8 +2060,10 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         return fail(h, "sacx_actor_act_host_seeds: n <= 16 rows per seed, no layer norm (use per-seed calls)");
     const int64_t tot = (int64_t)K * n;
     if (tot * (S + A) > STAGE_CAP) return fail(h, "rows exceed the pinned staging buffer (act per seed)");
-    if (stage_begin(h)) return -1;
-    std::memcpy(h->pin, obs, sizeof(float) * tot * S);
+    if (stage_alloc(h)) return -1;
+    float* const pa = h->pin + STAGE_CAP;          // the act half (acts are synchronous)
+    float* const ga = h->pin_dev + STAGE_CAP;
+    std::memcpy(pa, obs, sizeof(float) * tot * S);
     float* noise = deterministic ? nullptr : h->f0("act.noise");
     if (!deterministic) {            // each seed's u = np.random.normal(size=(n, A)) from its own stream
         RngArgs r{};
@@ -2007,9 +2074,9 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         launch_rng(r, h->stream);
     }
     ActRowArgs a{};
-    a.obs = h->pin_dev; a.s_mean = h->f0("norm.s_mean"); a.s_den = h->f0("norm.s_den");
+    a.obs = ga; a.s_mean = h->f0("norm.s_mean"); a.s_den = h->f0("norm.s_den");
     a.W0 = h->f0("actor.l0"); a.W1 = h->f0("actor.l1"); a.W3 = h->f0("actor.l2"); a.logstd = h->f0("actor.logstd");
-    a.noise = noise; a.out = h->pin_dev + tot * S;
+    a.noise = noise; a.out = ga + tot * S;
     a.S = S; a.A = A; a.Aout = h->Aout; a.H0 = h->H0; a.H1 = h->H1;
     a.act0 = h->aact[0]; a.act1 = h->aact[1];
     a.mode = h->cfg.actor_gaussian ? 2 : 1;
@@ -2024,7 +2091,7 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
     launch_act_rows(a, (int)n, h->stream);
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    std::memcpy(act_out, h->pin + tot * S, sizeof(float) * tot * A);
+    std::memcpy(act_out, pa + tot * S, sizeof(float) * tot * A);
     return 0;
 }
 
@@ -2107,16 +2174,17 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // the drop-in loop's one-update steps: the randoms drawn speculatively after the previous
     // step are valid when the ring now holds the size they assumed (nothing else drew meanwhile:
     // every other consumer of the stream undid the draw)
-    const bool spec_ok = h->spec_enabled && n_steps == 1 && flags == 0 && h->seeds == 1 && h->dp_ranks == 0;
+    const bool spec_ok = spec_mode(h) && n_steps == 1 && flags == 0;
     const bool use_spec = spec_ok && h->spec_live && h->spec_size == h->cur_size_host;
     if (!use_spec && spec_cancel(h)) return -1;
+    h->last_step_one = spec_ok;
     launch_set_ctl(h->ctl0(), num_timesteps, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
     if (use_spec) {
         h->spec_live = false;
-        HIPCHK(h, hipStreamWaitEvent(h->stream, h->spec_ev, 0));
-        hipGraphExec_t g;                 // gather + update, the randoms already in slot 0
-        if (get_graph(h, 1, false, &g)) return -1;
+        ++h->spec_hits;
+        hipGraphExec_t g;                 // gather + update, the randoms already in kSpecSlot
+        if (get_spec_graph(h, &g)) return -1;
         HIPCHK(h, hipGraphLaunch(g, h->stream));
     } else if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
@@ -2129,26 +2197,6 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     }
     h->seq_host += n_steps;
     if (h->nccl_failed) return fail(h, "ncclAllReduce failed");
-    if (spec_ok) {
-        // the next update's randint + normals into slot 0 on the side stream, for the ring one
-        // append larger, while the caller acts and steps its environment
-        const Launch* R = nullptr;
-        for (const Launch& L : h->plan[0])
-            if (L.kind == Launch::RNG) { R = &L; break; }
-        if (!R) return fail(h, "internal: no sampler launch");
-        RngArgs r = R->rng;
-        r.reset_seq = 1;
-        r.nupd = 1;
-        r.size_fixed = std::min<int64_t>(h->cur_size_host + 1, h->cap);
-        r.backup = h->ptr<RngState>("rng.spec");
-        HIPCHK(h, hipEventRecord(h->spec_go, h->stream));
-        HIPCHK(h, hipStreamWaitEvent(h->rng_stream, h->spec_go, 0));
-        launch_rng(r, h->rng_stream);
-        HIPCHK(h, hipGetLastError());
-        HIPCHK(h, hipEventRecord(h->spec_ev, h->rng_stream));
-        h->spec_live = true;
-        h->spec_size = r.size_fixed;
-    }
     return 0;
 }
 
@@ -2157,6 +2205,10 @@ int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags) {
     if (n_steps <= 0 || (flags & SACX_STEP_EAGER)) return 0;
     std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
     if (step_graph_list(h, n_steps, (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0, &gl)) return -1;
+    if (h->spec_enabled && n_steps == 1 && flags == 0 && h->seeds == 1 && h->dp_ranks == 0) {
+        hipGraphExec_t g;                 // the drop-in loop's speculative path replays this one
+        if (get_spec_graph(h, &g)) return -1;
+    }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
 }
@@ -2210,6 +2262,8 @@ int sacx_sync(sacx_handle* h) {
     HIPCHK(h, hipGetLastError());
     return 0;
 }
+
+int64_t sacx_spec_hits(const sacx_handle* h) { return h ? h->spec_hits : -1; }
 
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out) {
     if (!h || !n_out) return -1;

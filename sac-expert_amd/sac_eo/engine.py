@@ -640,6 +640,10 @@ class Engine:
     def sync(self):
         N.check(self.lib.sacx_sync(self.h), self.h, "sync")
 
+    def spec_hits(self) -> int:
+        """One-update steps that ran on randoms drawn speculatively by the preceding act_host."""
+        return int(self.lib.sacx_spec_hits(self.h))
+
     def seed_view(self, k: int) -> "SeedView":
         """The per-seed face of a packed handle for one learner's host code (SeedView)."""
         return SeedView(self, k)

@@ -1,9 +1,10 @@
-"""The drop-in loop's speculative sampler (sacx_sac_step(1)): after each one-update step the
-next update's randint + normals are drawn on a side stream for the ring size one append later,
-and used by the next step(1) when the ring did reach that size; any other draw from the global
-stream (a stochastic action, get_state) first undoes it.  Whatever the interleaving, the run must
-equal the same calls with the speculation off (SACX_SPEC=0), bit for bit: losses, weights, Adam
-state, ring and the RNG stream."""
+"""The drop-in loop's speculative sampler.  In the reference's cadence (act -> _update -> env.step
+-> add, /root/reference/sac_eo/algs/SAC_expert.py:779-797) act_host queues the next update's
+randint + normals right behind the action kernel, for the ring as it is then, and the following
+step(1) replays the sampler-less graph on them when the ring still has that size; any other
+draw from the global stream (a stochastic action, get_state) or an append in between first
+undoes it.  Whatever the interleaving, the run must equal the same calls with the speculation
+off (SACX_SPEC=0), bit for bit: losses, weights, Adam state, ring and the RNG stream."""
 import numpy as np
 import pytest
 
@@ -16,7 +17,7 @@ pytestmark = pytest.mark.gpu
 def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full):
     from sac_eo.engine import Engine, EngineConfig
     B, N, n = 64, 600, 48
-    outs = []
+    outs, hits = [], []
     for spec in ("1", "0"):
         monkeypatch.setenv("SACX_SPEC", spec)
         ocfg, st, buf, nrm, _ = make_learner(act="relu", B=B, N=N, seed=5, done_p=0.05)
@@ -28,16 +29,23 @@ def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full):
         for j in range(n):
             o, o2 = rs.normal(size=17).astype(np.float32), rs.normal(size=17).astype(np.float32)
             a = eng.act_host(o, deterministic=(j % 11 != 7))     # now and then a stochastic action
-            if j % 13 == 5:
-                eng.append(np.stack([o, o2]), np.stack([a, a]), np.zeros(2), np.stack([o2, o]), np.zeros(2))  # 2 rows
-            else:
+            late = j % 9 == 4                                     # now and then the add before the update
+            if late:
                 eng.append(o[None], a[None], np.array([0.5], np.float32), o2[None], np.zeros(1, np.float32))
             eng.step(1, num_timesteps=j, ts_increment=1)
+            if j % 13 == 5:
+                eng.append(np.stack([o, o2]), np.stack([a, a]), np.zeros(2), np.stack([o2, o]), np.zeros(2))  # 2 rows
+            elif not late:
+                eng.append(o[None], a[None], np.array([0.5], np.float32), o2[None], np.zeros(1, np.float32))
             if j == 30:
                 eng.rng_get_state()                               # an observation point mid-run
+            if j == 40:
+                assert np.isfinite(eng.stats(1)).all()            # another one
         eng.sync()
+        hits.append(eng.spec_hits())
         outs.append((eng.stats(n).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy(),
                      eng.v["replay"].cpu().numpy().copy(), eng.rng_get_state()[1].copy(), eng.ctl()["cur_size"]))
         eng.close()
+    assert hits[1] == 0 and hits[0] >= n // 2, hits          # the speculative path did run
     for i, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), i
