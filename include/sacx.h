@@ -210,7 +210,11 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
                             const float* sp, const float* d, int64_t n);
 /* sacx_actor_act with HOST obs[n,S] in and HOST act_out[n,A] out, through the same mapped
  * buffer (the normaliser reads obs and the head writes actions in place).  Synchronous: waits
- * for the bound stream (and so for any queued update) before returning the actions. */
+ * for the action kernel (and so for any update queued before it) before returning the actions.
+ * Drop-in cadence (SAC_expert.py:779-797: sample, _update, env.step, add): after a one-update
+ * sacx_sac_step it also queues the next update's sampler draw behind the action kernel (for the
+ * ring as it is now), which the next sacx_sac_step(h, 1, ...) uses when the ring still has that
+ * size; that step then also runs the previous update's alpha branch, folded into its launches. */
 int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out);
 /* Both for EVERY seed of a packed handle in one launch chain: K runs of the reference's
  * --runs (sac_eo/train.py:118-152) stepping their env loops in lock-step hand over n rows each.
@@ -271,6 +275,12 @@ enum { SACX_DIAG_DISC = 1, SACX_DIAG_EXPERT_ACTIONS = 2 };
 int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const float* sp_e, int32_t n,
                      int32_t flags, float delta_clip, float* out);
 int sacx_sync(sacx_handle* h);
+/* Brings the arena to the state the calls so far define, without waiting: runs an alpha branch
+ * the drop-in loop's one-update steps deferred (its alpha Adam, stats row and counters; see
+ * sacx_actor_act_host) and undoes a speculative sampler draw.  Every entry point but act, append
+ * and the speculative step does this itself; a caller that reads or writes the arena directly
+ * (segment views) calls it first.  sacx_sync = sacx_settle + a wait for the bound stream. */
+int sacx_settle(sacx_handle* h);
 
 /* After the caller restored the arena's PARAM / TARGET / STATE segments (a resume
  * snapshot, sac_eo Engine.load_state): re-reads the host mirrors of the device counters

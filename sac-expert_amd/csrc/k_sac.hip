@@ -1571,6 +1571,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         const int64_t so = seed_off(a_in.sstride);
         a.st = sr(a_in.st, so); a.ctl = sr(a_in.ctl, so);
         a.out_idx = sr(a_in.out_idx, so); a.out_norm = sr(a_in.out_norm, so);
+        a.pairs = sr(a_in.pairs, so); a.pairs_oi = sr(a_in.pairs_oi, so);
     }
     const int t = threadIdx.x;
     for (int i = t; i < 624; i += RNG_THREADS) S.ring[i] = a.st->key[i];
@@ -1669,6 +1670,8 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
             oi = 1;
         }
         const int need_pairs = (a.n_norm - oi + 1) >> 1;
+        uint32_t* const pairs_u = a.pairs ? a.pairs + (size_t)u * a.pcap * 4 : nullptr;
+        if (a.pairs && t == 0) a.pairs_oi[u] = oi;
         int got = 0;
         while (got < need_pairs) {
             ensure(q + 4 * RNG_THREADS);
@@ -1682,19 +1685,28 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
             const double x2 = 2.0 * u2 - 1.0;
             const double r2 = x1 * x1 + x2 * x2;
             const bool acc = (r2 < 1.0) && (r2 != 0.0);
-            double f = 0.0;
-            if (acc) f = sqrt(-2.0 * log(r2) / r2);
             int total;
             const int rank = block_rank(acc, S.wtot, total);
             const int np = need_pairs - got;
             if (acc && rank < np) {
                 const int o = oi + 2 * (got + rank);
-                out_norm[o] = (float)(f * x2);
-                if (o + 1 < a.n_norm) {
-                    out_norm[o + 1] = (float)(f * x1);
+                if (pairs_u) {
+                    // k_polar computes this pair's normals; the cached second value of an odd
+                    // count is state, so that one pair's transform also runs here (same code)
+                    *reinterpret_cast<uint4*>(pairs_u + 4 * (got + rank)) = make_uint4(w0, w1, w2, w3);
+                    if (o + 1 >= a.n_norm) {
+                        S.gauss = sqrt(-2.0 * log(r2) / r2) * x1;
+                        S.has = 1;
+                    }
                 } else {
-                    S.gauss = f * x1;
-                    S.has = 1;
+                    const double f = sqrt(-2.0 * log(r2) / r2);
+                    out_norm[o] = (float)(f * x2);
+                    if (o + 1 < a.n_norm) {
+                        out_norm[o + 1] = (float)(f * x1);
+                    } else {
+                        S.gauss = f * x1;
+                        S.has = 1;
+                    }
                 }
             }
             if (acc && rank == np - 1) S.last = t;
@@ -1726,15 +1738,39 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         a.st->has_gauss = S.has;
         a.st->gauss = S.gauss;
         if (a.slot >= 0) {
-            const int64_t seq = a.reset_seq ? a.ctl->step_seq : a.ctl->rng_seq;
+            // reset_seq = 1 + k: the update after the next k (a deferred alpha.final, sacx.cpp)
+            const int64_t seq = a.reset_seq ? a.ctl->step_seq + (a.reset_seq - 1) : a.ctl->rng_seq;
             for (int u = 0; u < a.nupd; ++u) a.ctl->pseq[a.slot + u] = seq + u;
             a.ctl->rng_seq = seq + a.nupd;
         }
     }
 }
 
+// The polar transform of the pairs k_rng accepted (legacy_gauss, mtrand): one thread per pair of
+// every update of the batch, the same fp64 arithmetic as k_rng's own path (bit-identical output)
+__global__ __launch_bounds__(256) void k_polar(RngArgs a) {
+    const int64_t so = seed_off(a.sstride);
+    const int u = blockIdx.y;
+    const int j = blockIdx.x * 256 + threadIdx.x;
+    const int oi = sr(a.pairs_oi, so)[u];
+    if (j >= ((a.n_norm - oi + 1) >> 1)) return;
+    const uint4 w = *reinterpret_cast<const uint4*>(sr(a.pairs, so) + ((size_t)u * a.pcap + j) * 4);
+    const double u1 = ((double)(int32_t)(w.x >> 5) * 67108864.0 + (double)(int32_t)(w.y >> 6)) / 9007199254740992.0;
+    const double u2 = ((double)(int32_t)(w.z >> 5) * 67108864.0 + (double)(int32_t)(w.w >> 6)) / 9007199254740992.0;
+    const double x1 = 2.0 * u1 - 1.0;
+    const double x2 = 2.0 * u2 - 1.0;
+    const double r2 = x1 * x1 + x2 * x2;
+    const double f = sqrt(-2.0 * log(r2) / r2);
+    float* out = (float*)((char*)sr(a.out_norm, so) + (int64_t)u * a.slot_bytes);
+    const int o = oi + 2 * j;
+    out[o] = (float)(f * x2);
+    if (o + 1 < a.n_norm) out[o + 1] = (float)(f * x1);
+}
+
 void launch_rng(const RngArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_rng, dim3(1, 1, seeds_z(a.nseeds)), dim3(RNG_THREADS), 0, s, a);
+    if (a.pairs != nullptr && a.n_norm > 0)
+        hipLaunchKernelGGL(k_polar, dim3((a.pcap + 255) / 256, a.nupd, seeds_z(a.nseeds)), dim3(256), 0, s, a);
 }
 
 // ==================================================================== k_gather

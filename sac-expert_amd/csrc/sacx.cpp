@@ -144,6 +144,8 @@ struct sacx_handle {
     std::vector<Launch> plan[NSLOT];
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
     int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
+    bool rng_split = false;   // k_rng + k_polar (rng.pairs): the polar transform spread over the GPU
+    int pcap = 0;             // polar pairs per update (rng.pairs rows per update)
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
     int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
@@ -180,6 +182,12 @@ struct sacx_handle {
     bool last_step_one = false;  // the last sacx_sac_step was a plain one-update step
     int64_t spec_size = 0;     // the ring size it assumed
     int64_t spec_hits = 0;     // one-update steps that used a speculative draw (sacx_spec_hits)
+    int spec_slot = 1;         // the slot the queued draw fills (1 or 2: never the pending alpha's)
+    // The alpha branch (alpha.fwd, alpha.head, alpha.final) of the last speculative one-update
+    // step is deferred into the next one (merged_body, as inside a captured multi-update graph):
+    // the next act needs the updated actor, not alpha.  alpha_pending = that update's slot, or -1;
+    // every entry point that could observe or disturb it runs it first (settle).
+    int alpha_pending = -1;
     int64_t cur_size_host = 0; // mirrors ctl->cur_size (appends, resync)
     hipEvent_t act_ev = nullptr;   // end of the last act_host kernel chain (its actions are on the host)
 
@@ -234,7 +242,9 @@ int spec_cancel(sacx_handle* h, bool keep_state = false) {
 }
 
 // the handles the speculative draw applies to: one learner, its own RNG stream
-bool spec_mode(const sacx_handle* h) { return h->spec_enabled && h->seeds == 1 && h->dp_ranks == 0 && !h->dp_local; }
+bool spec_mode(const sacx_handle* h) {
+    return h->spec_enabled && h->seeds == 1 && h->dp_ranks == 0 && !h->dp_local && 2 * h->nbatch >= 3;
+}
 
 #define HIPCHK(h, x)                                                                    \
     do {                                                                                \
@@ -303,6 +313,15 @@ void build_layout(sacx_handle* h) {
     h->alias("rng.pos", roff + offsetof(RngState, pos), 1, 2, SACX_I32, SACX_ROLE_STATE);
     h->alias("rng.gauss", roff + offsetof(RngState, gauss), 1, 1, SACX_F64, SACX_ROLE_STATE);
     h->add("rng.spec", 1, sizeof(RngState) / 4, SACX_U32, SACX_ROLE_WORK);   // state before a speculative draw
+    // Split sampler (many normals per update, Humanoid): k_rng ranks the accepted polar pairs and
+    // stores their four words; k_polar turns them into normals over the whole GPU
+    h->rng_split = h->n_norm > 16384;
+    if (const char* e = std::getenv("SACX_RNG_SPLIT")) h->rng_split = std::atoi(e) != 0;
+    if (h->rng_split) {
+        h->pcap = (h->n_norm + 1) / 2;
+        h->add("rng.pairs", (int64_t)NBATCH_MAX * h->pcap, 4, SACX_U32, SACX_ROLE_WORK);
+        h->add("rng.pairs_oi", 1, NBATCH_MAX, SACX_I32, SACX_ROLE_WORK);
+    }
     // per-slot update inputs: the sampler + gather of update j+2 run while update j+1
     // executes, so everything they write is double buffered
     const int ne1 = std::max(1, h->ne);
@@ -637,6 +656,11 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.rng.reset_seq = 1;   // cleared for the chained launches of a captured graph
         L.rng.nupd = 1;
         L.rng.slot_bytes = h->slot_bytes;
+        if (h->rng_split) {
+            L.rng.pairs = h->ptr<uint32_t>("rng.pairs");
+            L.rng.pairs_oi = h->ptr<int32_t>("rng.pairs_oi");
+            L.rng.pcap = h->pcap;
+        }
         L.grid = 1;
         L.block = 1024;
         L.bytes = 4.0 * (B + h->n_norm) + 2.0 * sizeof(RngState);
@@ -1561,22 +1585,32 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
     return 0;
 }
 
-// The one-update graph of the drop-in loop's speculative path: gather + update reading the
-// randoms the speculative k_rng drew into slot kSpecSlot (not slot 0, so that slot 0 keeps the
-// randoms of the last update a caller observed: a cancelled draw leaves no trace in it).
-constexpr int kSpecSlot = 1;
-
-int get_spec_graph(sacx_handle* h, hipGraphExec_t* out) {
-    const auto key = std::make_tuple(1, 2, -1);
+// The one-update graphs of the drop-in loop's speculative path: gather + update of slot `slot`
+// (1 or 2), reading the randoms the speculative k_rng drew there -- not slot 0, so that slot 0
+// keeps the randoms of the last update a caller observed: a cancelled draw leaves no trace in it
+// -- with the alpha branch of the previous speculative update (slot `prev`, -1: none) folded in
+// and the update's own alpha branch left out (deferred to the next one, or to settle()).
+int get_spec_graph(sacx_handle* h, int slot, int prev, hipGraphExec_t* out) {
+    const auto key = std::make_tuple(1, 16 + 64 * slot + (prev + 1), -1);
     auto it = h->graphs.find(key);
     if (it != h->graphs.end()) {
         *out = it->second;
         return 0;
     }
-    if (2 * h->nbatch <= kSpecSlot || h->plan[kSpecSlot].empty()) return fail(h, "internal: no spare slot for the speculative draw");
+    if (2 * h->nbatch <= slot || h->plan[slot].empty()) return fail(h, "internal: no spare slot for the speculative draw");
+    std::vector<Launch> body;
+    if (!merged_body(h, slot, prev, body)) {   // plans that do not fold: the branch, then the body
+        std::vector<Launch> own;
+        if (!merged_body(h, slot, -1, own)) return fail(h, "internal: speculative update body");
+        body.clear();
+        for (const Launch& L : h->plan[prev])
+            if (L.alpha_branch) body.push_back(L);
+        body.insert(body.end(), own.begin(), own.end());
+    }
     HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-    for (const Launch& L : h->plan[kSpecSlot])   // the draw stamped pseq[kSpecSlot] itself
-        if (L.kind != Launch::RNG) enqueue(L, h, h->cap_stream);
+    for (const Launch& L : h->plan[slot])      // the draw stamped pseq[slot] itself
+        if (L.kind == Launch::GATHER) enqueue(L, h, h->cap_stream);
+    for (const Launch& L : body) enqueue(L, h, h->cap_stream);
     hipGraph_t graph;
     HIPCHK(h, hipStreamEndCapture(h->cap_stream, &graph));
     hipGraphExec_t exec;
@@ -1586,6 +1620,20 @@ int get_spec_graph(sacx_handle* h, hipGraphExec_t* out) {
     h->graphs[key] = exec;
     *out = exec;
     return 0;
+}
+
+// Runs a deferred alpha branch (the tail a one-update graph would have ended with), then undoes
+// a queued speculative draw: the state every entry point but act / append / the speculative
+// step(1) starts from.
+int settle(sacx_handle* h, bool keep_rng_state = false) {
+    if (h->alpha_pending >= 0) {
+        const int slot = h->alpha_pending;
+        h->alpha_pending = -1;
+        for (const Launch& L : h->plan[slot])
+            if (L.alpha_branch) enqueue(L, h, h->stream);
+        HIPCHK(h, hipGetLastError());
+    }
+    return spec_cancel(h, keep_rng_state);
 }
 
 // The graphs sacx_sac_step(n_steps) replays: n_steps / G full graphs of G updates, then the
@@ -1827,7 +1875,8 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
 
 int sacx_resync(sacx_handle* h) {
     if (!h || !h->bound) return fail(h, "not bound");
-    if (spec_cancel(h, true)) return -1;     // the restored state is authoritative
+    h->alpha_pending = -1;                   // the restored state is authoritative
+    if (spec_cancel(h, true)) return -1;
     Ctl c{};
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(&c, h->ctl(), sizeof(Ctl), hipMemcpyDeviceToHost));
@@ -1978,16 +2027,20 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
     return 0;
 }
 
-// The speculative draw (see sacx_handle::spec_live): the sampler launch of slot kSpecSlot for one
+// The speculative draw (see sacx_handle::spec_live): the sampler launch of slot 1 or 2 for one
 // update at the ring's current size, queued on the bound stream; it saves the state it starts
 // from into "rng.spec" for spec_cancel.
 static int spec_draw(sacx_handle* h) {
+    const int slot = h->alpha_pending == 1 ? 2 : 1;    // not the slot a deferred alpha branch reads
     const Launch* R = nullptr;
-    for (const Launch& L : h->plan[kSpecSlot])
+    for (const Launch& L : h->plan[slot])
         if (L.kind == Launch::RNG) { R = &L; break; }
     if (!R) return fail(h, "internal: no sampler launch");
     RngArgs r = R->rng;
-    r.reset_seq = 1;            // stamps pseq[kSpecSlot] = step_seq: the update that follows
+    // stamps pseq[slot] with the update that follows: step_seq, + 1 while a deferred
+    // alpha.final has not counted the previous update yet
+    r.reset_seq = h->alpha_pending >= 0 ? 2 : 1;
+    h->spec_slot = slot;
     r.nupd = 1;
     r.size_fixed = h->cur_size_host;
     r.backup = h->ptr<RngState>("rng.spec");
@@ -2097,6 +2150,7 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
 
 int sacx_expert_set(sacx_handle* h, const float* s_e, const float* sp_e, int32_t n, float epsilon) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (settle(h)) return -1;             // alpha.final reads the epsilon this sets
     if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert");
     if (n != h->ne) return fail(h, "expert rows must equal expert_batch");
     const size_t bytes = sizeof(float) * (size_t)n * h->S;
@@ -2125,7 +2179,7 @@ int sacx_perm_push(sacx_handle* h, const int32_t* perms, int64_t n_steps) {
 
 int sacx_rng_seed(sacx_handle* h, uint32_t seed) {
     if (!h || !h->bound) return fail(h, "not bound");
-    if (spec_cancel(h, true)) return -1;
+    if (settle(h, true)) return -1;
     RngState st{};
     for (int pos = 0; pos < 624; ++pos) {       // init_genrand (seeding.py:12 -> np.random.seed)
         st.key[pos] = seed;
@@ -2141,7 +2195,7 @@ int sacx_rng_seed(sacx_handle* h, uint32_t seed) {
 
 int sacx_rng_set_state(sacx_handle* h, const uint32_t key[624], int32_t pos, int32_t has_gauss, double gauss) {
     if (!h || !h->bound) return fail(h, "not bound");
-    if (spec_cancel(h, true)) return -1;
+    if (settle(h, true)) return -1;
     if (pos < 0 || pos > 624) return fail(h, "pos out of range");
     RngState st{};
     std::memcpy(st.key, key, sizeof(st.key));
@@ -2155,7 +2209,7 @@ int sacx_rng_set_state(sacx_handle* h, const uint32_t key[624], int32_t pos, int
 
 int sacx_rng_get_state(sacx_handle* h, uint32_t key[624], int32_t* pos, int32_t* has_gauss, double* gauss) {
     if (!h || !h->bound) return fail(h, "not bound");
-    if (spec_cancel(h)) return -1;
+    if (settle(h)) return -1;
     RngState st{};
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(&st, h->ptr<RngState>("rng"), sizeof(st), hipMemcpyDeviceToHost));
@@ -2176,16 +2230,21 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // every other consumer of the stream undid the draw)
     const bool spec_ok = spec_mode(h) && n_steps == 1 && flags == 0;
     const bool use_spec = spec_ok && h->spec_live && h->spec_size == h->cur_size_host;
-    if (!use_spec && spec_cancel(h)) return -1;
+    if (!use_spec && settle(h)) return -1;
     h->last_step_one = spec_ok;
-    launch_set_ctl(h->ctl0(), num_timesteps, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
+    // a deferred alpha.final (folded into this update) adds ts_increment to num_timesteps before
+    // this update reads it
+    const int prev = use_spec ? h->alpha_pending : -1;
+    launch_set_ctl(h->ctl0(), num_timesteps - (prev >= 0 ? ts_increment : 0), ts_increment,
+                   (int64_t)h->seed_bytes, h->seeds, h->stream);
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
     if (use_spec) {
         h->spec_live = false;
         ++h->spec_hits;
-        hipGraphExec_t g;                 // gather + update, the randoms already in kSpecSlot
-        if (get_spec_graph(h, &g)) return -1;
+        hipGraphExec_t g;                 // gather + update, the randoms already in spec_slot
+        if (get_spec_graph(h, h->spec_slot, prev, &g)) return -1;
         HIPCHK(h, hipGraphLaunch(g, h->stream));
+        h->alpha_pending = h->spec_slot;
     } else if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
         HIPCHK(h, hipGetLastError());
@@ -2202,12 +2261,15 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
 
 int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (settle(h)) return -1;
     if (n_steps <= 0 || (flags & SACX_STEP_EAGER)) return 0;
     std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
     if (step_graph_list(h, n_steps, (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0, &gl)) return -1;
-    if (h->spec_enabled && n_steps == 1 && flags == 0 && h->seeds == 1 && h->dp_ranks == 0) {
-        hipGraphExec_t g;                 // the drop-in loop's speculative path replays this one
-        if (get_spec_graph(h, &g)) return -1;
+    if (spec_mode(h) && n_steps == 1 && flags == 0) {
+        hipGraphExec_t g;                 // the drop-in loop's speculative path replays these
+        for (int slot = 1; slot <= 2; ++slot)
+            for (int prev : {-1, 3 - slot})
+                if (get_spec_graph(h, slot, prev, &g)) return -1;
     }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     return 0;
@@ -2215,6 +2277,7 @@ int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags) {
 
 int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (settle(h)) return -1;
     if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert (no world models)");
     if (n_steps <= 0) return 0;
     if (!idx) return fail(h, "null index array");
@@ -2255,9 +2318,14 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
     return 0;
 }
 
+int sacx_settle(sacx_handle* h) {
+    if (!h || !h->bound) return fail(h, "not bound");
+    return settle(h);
+}
+
 int sacx_sync(sacx_handle* h) {
     if (!h || !h->bound) return fail(h, "not bound");
-    if (spec_cancel(h)) return -1;           // an observation point: the arena holds no speculative draw
+    if (settle(h)) return -1;           // an observation point: the arena holds no speculative draw
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipGetLastError());
     return 0;
@@ -2287,7 +2355,7 @@ int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int
 }
 
 int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t cap) {
-    if (h && h->bound && spec_cancel(h)) return -1;
+    if (h && h->bound && settle(h)) return -1;
     if (!h || !h->bound) return fail(h, "not bound");
     const auto& plan = h->plan[0];
     const int n = (int)plan.size();
@@ -2416,7 +2484,7 @@ static NetIOArgs netio_base(sacx_handle* h, bool model = false) {
 
 int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out, float* nlp_out) {
     if (!h || !h->bound) return fail(h, "not bound");
-    if (spec_cancel(h)) return -1;
+    if (settle(h)) return -1;
     if (h->cfg.actor_gaussian) return fail(h, "GaussianActor handle: inference only (sacx_actor_act)");
     if (n < 0 || (n > 0 && (!s || !pi_out || !nlp_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
@@ -2448,6 +2516,7 @@ int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out
 int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float* a, int64_t n, int32_t value,
                         float* out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (settle(h)) return -1;
     if (net < 0 || net > 3) return fail(h, "net must be 0..3 (q0, q1, t0, t1)");
     if (n < 0 || (n > 0 && (!s || !a || !out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldQ = h->ldQ;
@@ -2495,6 +2564,7 @@ static void model_net_chunk(sacx_handle* h, int32_t model, const float* s, const
 int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n, float delta_clip,
                        float reward_clip, float* pred_out, float* sp_out, float* r_out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (settle(h)) return -1;
     if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
     if (model < 0 || model >= h->nm) return fail(h, "model index out of range (num_models)");
     if (n < 0 || (n > 0 && (!s || !a))) return fail(h, "bad arguments");
@@ -2517,6 +2587,7 @@ int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const floa
 int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* sp, const float* a, const float* r,
                     int64_t n, float delta_clip_loss, float reward_clip_loss, float* loss_out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (settle(h)) return -1;
     if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
     if (model < 0 || model >= h->nm) return fail(h, "model index out of range (num_models)");
     if (n <= 0 || !s || !sp || !a || !r || !loss_out) return fail(h, "bad arguments");
@@ -2608,7 +2679,7 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
     if (n < 0 || horizon < 0) return fail(h, "bad arguments");
     if (n == 0 || horizon == 0) return 0;
     if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
-    if (!deterministic && spec_cancel(h)) return -1;
+    if (settle(h)) return -1;
     // one captured graph per (model, shape, clips, pointers): the Python host keeps its
     // staging / output buffers per shape, so repeated calls replay (SACX_ROLL_GRAPH=0: eager)
     const char* rg = std::getenv("SACX_ROLL_GRAPH");
@@ -2649,7 +2720,7 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     const bool disc = (flags & SACX_DIAG_DISC) != 0, ea = (flags & SACX_DIAG_EXPERT_ACTIONS) != 0;
     if (disc && h->nm < 2) return fail(h, "_calc_disc compares two world models (num_models = 2)");
     if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
-    if (!ea && spec_cancel(h)) return -1;
+    if (settle(h)) return -1;
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
@@ -2725,7 +2796,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
                       int64_t* n_launches) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!kernel || std::strcmp(kernel, "k_gemm") != 0) return fail(h, "only k_gemm carries timestamps");
-    if (spec_cancel(h)) return -1;
+    if (settle(h)) return -1;
     if (!avg_us || n_replays <= 0) return fail(h, "bad arguments");
     const int G = h->graph_steps;
     KTimeMap kt;
@@ -2796,7 +2867,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
 int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, double* ms_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!ms_out || n_replays <= 0) return fail(h, "bad arguments");
-    if (spec_cancel(h)) return -1;
+    if (settle(h)) return -1;
     int skip = -1;
     if (skip_kernel && skip_kernel[0]) {
         for (int k = Launch::RNG; k <= Launch::MFINAL; ++k)

@@ -289,6 +289,12 @@ struct RngArgs {
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
     int64_t sstride;
     int32_t nseeds;
+    // split sampler: k_rng stores each accepted polar pair's four tempered words at
+    // pairs[(u * pcap + j) * 4] and update u's leading cached normal (0 / 1) at pairs_oi[u];
+    // k_polar (launched by launch_rng after it) computes the normals.  nullptr: k_rng does both
+    uint32_t* pairs;
+    int32_t* pairs_oi;
+    int32_t pcap;
 };
 
 struct GatherArgs {

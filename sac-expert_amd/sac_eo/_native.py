@@ -30,7 +30,7 @@ EXPORTS = [
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
     "sacx_dp_unique_id", "sacx_dp_init", "sacx_dp_init_local", "sacx_dp_local_step", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
     "sacx_seed_select", "sacx_prepare", "sacx_actor_evaluate", "sacx_critic_forward", "sacx_model_forward",
-    "sacx_model_loss", "sacx_spec_hits",
+    "sacx_model_loss", "sacx_spec_hits", "sacx_settle",
 ]
 
 
@@ -138,6 +138,7 @@ def lib():
         "sacx_prepare": (ctypes.c_int, [vp, i64, i32]),
         "sacx_model_fit": (ctypes.c_int, [vp, vp, i64, i32]),
         "sacx_sync": (ctypes.c_int, [vp]),
+        "sacx_settle": (ctypes.c_int, [vp]),
         "sacx_plan_info": (ctypes.c_int, [vp, P(LaunchInfo), i32, P(i32)]),
         "sacx_spec_hits": (i64, [vp]),
         "sacx_profile": (ctypes.c_int, [vp, i64, P(f64), i32]),

@@ -174,7 +174,8 @@ class Engine:
             self._views.append(views)
         self.seed_index = 0
         self.arena = self._arenas[0]
-        self.v: Dict[str, torch.Tensor] = self._views[0]
+        self._v: Dict[str, torch.Tensor] = self._views[0]
+        self._bound = False
         with torch.cuda.device(self.device):
             self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
             if dp is not None:
@@ -187,6 +188,7 @@ class Engine:
         self.dp_local = dp_local
         N.check(self.lib.sacx_bind(h, ctypes.c_void_p(self.arena_all.data_ptr()), total,
                                    ctypes.c_void_p(self.stream.cuda_stream)), h, "sacx_bind")
+        self._bound = True
         for k in range(self.seeds):
             self.select_seed(k)
             self._init_state()
@@ -198,7 +200,16 @@ class Engine:
         N.check(self.lib.sacx_seed_select(self.h, k), self.h, "seed_select")
         self.seed_index = k
         self.arena = self._arenas[k]
-        self.v = self._views[k]
+        self._v = self._views[k]
+
+    @property
+    def v(self) -> Dict[str, torch.Tensor]:
+        """The segment views of the selected seed.  Reading or writing them is an observation
+        point: a deferred alpha branch runs and a speculative draw is undone first (sacx_settle;
+        a no-op unless the drop-in loop's one-update steps left one)."""
+        if getattr(self, "h", None) is not None and getattr(self, "_bound", False):
+            N.check(self.lib.sacx_settle(self.h), self.h, "settle")
+        return self._v
 
     @staticmethod
     def dp_local_step(engines: Sequence["Engine"], n: int = 1, num_timesteps: int = 0, ts_increment: int = 1):

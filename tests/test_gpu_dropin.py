@@ -49,3 +49,45 @@ def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full):
     assert hits[1] == 0 and hits[0] >= n // 2, hits          # the speculative path did run
     for i, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), i
+
+
+def test_speculative_sac_eo_with_deferred_alpha(gpu_available, monkeypatch):
+    """SAC-EO (two world models, expert permutations) through the same cadence, with the
+    things that must run a deferred alpha branch first: a new expert set / epsilon mid-run
+    (alpha.final mixes the expert MSE with it), a multi-update step, a stats read."""
+    from helpers import make_pair
+    n, outs, hits = 40, [], []
+    for spec in ("1", "0"):
+        monkeypatch.setenv("SACX_SPEC", spec)
+        eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=64, N=800, seed=8, use_expert=True,
+                                                    graph_steps=1, done_p=0.05)
+        eng.rng_set_state(np.random.RandomState(21).get_state())
+        rp = np.random.RandomState(4)
+        eng.push_perms(np.stack([rp.permutation(eng.cfg.expert_batch) for _ in range(n + 8)]))
+        rs = np.random.RandomState(5)
+        t = 0
+        for j in range(n):
+            o, o2 = rs.normal(size=17).astype(np.float32), rs.normal(size=17).astype(np.float32)
+            a = eng.act_host(o, deterministic=(j % 7 != 3))
+            eng.step(1, num_timesteps=t, ts_increment=1)
+            t += 1
+            eng.append(o[None], a[None], np.array([0.25], np.float32), o2[None], np.zeros(1, np.float32))
+            if j == 15:
+                eng.set_expert(expert["s"], expert["sp"], 0.3)
+            if j == 25:
+                eng.step(3, num_timesteps=t, ts_increment=1)
+                t += 3
+            if j == 33:
+                assert np.isfinite(eng.stats(1)).all()
+        eng.sync()
+        hits.append(eng.spec_hits())
+        outs.append((eng.stats(n + 3).copy(), eng.v["params"].cpu().numpy().copy(),
+                     eng.v["adam_m"].cpu().numpy().copy(), eng.rng_get_state()[1].copy(),
+                     {k: v for k, v in eng.ctl().items() if k in ("t_sac", "num_timesteps", "cur_size", "start", "step_seq")}))
+        eng.close()
+    assert hits[1] == 0 and hits[0] >= n // 2, hits
+    for i, (a, b) in enumerate(zip(*outs)):
+        if isinstance(a, dict):
+            assert a == b, (a, b)
+        else:
+            assert np.array_equal(a, b), i

@@ -5,6 +5,8 @@
 #include "../sac-expert_amd/csrc/k_sac.hip"
 #include <chrono>
 #include <cstdio>
+#include <cstring>
+#include <vector>
 using namespace sacx;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("err %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
 
@@ -20,11 +22,38 @@ int main() {
     CK(hipMemcpy(st, &h, sizeof(h), hipMemcpyHostToDevice));
     Ctl c{}; c.cur_size = 1000000;
     CK(hipMemcpy(ctl, &c, sizeof(c), hipMemcpyHostToDevice));
-    struct Cfg { const char* name; int B, A, nupd; } cfgs[] = {{"hc B=256 A=6", 256, 6, 4}, {"humanoid B=1024 A=17", 1024, 17, 4}};
+    uint32_t* pairs; int32_t* poi; float* nz2; int32_t* idx2;
+    CK(hipMalloc(&pairs, 8 << 20)); CK(hipMalloc(&poi, 64)); CK(hipMalloc(&nz2, 32 << 20)); CK(hipMalloc(&idx2, 32 << 20));
+    struct Cfg { const char* name; int B, A, nupd; bool split; } cfgs[] = {
+        {"hc B=256 A=6", 256, 6, 4, false}, {"hc B=256 A=6 split", 256, 6, 4, true},
+        {"humanoid B=1024 A=17", 1024, 17, 4, false}, {"humanoid split", 1024, 17, 4, true}};
     for (auto& cf : cfgs) {
         RngArgs a{};
         a.st = st; a.ctl = ctl; a.n_int = cf.B; a.n_norm = 3 * cf.B * cf.A; a.out_idx = idx; a.out_norm = nz;
         a.slot = -1; a.nupd = cf.nupd; a.slot_bytes = (int64_t)4 << 20;
+        if (cf.split) { a.pairs = pairs; a.pairs_oi = poi; a.pcap = (a.n_norm + 1) / 2; }
+        {   // bit-identity of the two paths from the same state (one odd-count draw first: cached gauss)
+            RngArgs b = a;
+            b.pairs = nullptr; b.out_idx = idx2; b.out_norm = nz2;
+            RngArgs o = a; o.n_int = 0; o.n_norm = 7; o.nupd = 1; o.pairs = nullptr;
+            CK(hipMemcpy(st, &h, sizeof(h), hipMemcpyHostToDevice));
+            launch_rng(o, s); launch_rng(a, s);
+            CK(hipMemcpy(st, &h, sizeof(h), hipMemcpyHostToDevice));
+            launch_rng(o, s); launch_rng(b, s);
+            CK(hipStreamSynchronize(s));
+            size_t bad = 0;
+            std::vector<float> x(a.n_norm), y(a.n_norm);
+            std::vector<int32_t> ix(a.n_int), iy(a.n_int);
+            for (int u = 0; u < a.nupd; ++u) {
+                CK(hipMemcpy(x.data(), (char*)nz + u * a.slot_bytes, 4 * a.n_norm, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(y.data(), (char*)nz2 + u * a.slot_bytes, 4 * a.n_norm, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(ix.data(), (char*)idx + u * a.slot_bytes, 4 * a.n_int, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(iy.data(), (char*)idx2 + u * a.slot_bytes, 4 * a.n_int, hipMemcpyDeviceToHost));
+                for (int i = 0; i < a.n_norm; ++i) bad += memcmp(&x[i], &y[i], 4) != 0;
+                for (int i = 0; i < a.n_int; ++i) bad += ix[i] != iy[i];
+            }
+            printf("%-22s split == one-kernel: %s (%zu mismatches)\n", cf.name, bad ? "NO" : "yes", bad);
+        }
         for (int w = 0; w < 3; ++w) launch_rng(a, s);
         CK(hipStreamSynchronize(s));
         unsigned long long z[8] = {0};
