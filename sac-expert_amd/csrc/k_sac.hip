@@ -1502,6 +1502,32 @@ __device__ __forceinline__ int block_rank(bool flag, int* wtot, int& total) {
     return off + below;
 }
 
+// two flags per thread, candidate sets A (thread order) then B (thread order): the exclusive
+// ranks of this thread's A and B candidates among all flagged ones, and the total
+__device__ __forceinline__ void block_rank2(bool fa, bool fb, int* wtot, int& ra, int& rb, int& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long ba = __ballot(fa), bb = __ballot(fb);
+    const unsigned long long lo = (1ULL << lane) - 1ULL;
+    if (lane == 0) {
+        wtot[w] = __popcll(ba);
+        wtot[RNG_THREADS / 64 + w] = __popcll(bb);
+    }
+    __syncthreads();
+    int offa = 0, tota = 0, offb = 0, totb = 0;
+#pragma unroll
+    for (int i = 0; i < RNG_THREADS / 64; ++i) {
+        const int ca = wtot[i], cb = wtot[RNG_THREADS / 64 + i];
+        offa += (i < w) ? ca : 0;
+        tota += ca;
+        offb += (i < w) ? cb : 0;
+        totb += cb;
+    }
+    __syncthreads();
+    ra = offa + __popcll(ba & lo);
+    rb = tota + offb + __popcll(bb & lo);
+    total = tota + totb;
+}
+
 // The stream lives in an LDS ring of raw (untempered) MT words: stream word q (words 0..623 =
 // the state's key) sits at ring[q % RNG_RW].  MT19937 as a word recurrence is
 //   x[n] = x[n-227] ^ g(n-624),   g(m) = twist(x[m], x[m+1])      (n >= 624)
@@ -1513,11 +1539,15 @@ __device__ __forceinline__ int block_rank(bool flag, int* wtot, int& total) {
 // per thread (a word for randint, 4 words for a polar pair), accepted ones ranked by a
 // block-wide ballot prefix.  The state written back is (block holding the last consumed word,
 // position); the ring keeps that block resident and it is generated to its end first.
+// The ring's first RNG_MIR words are mirrored past its end, so the 1079-word operand window of
+// any word is contiguous from one base address and every read is that base plus an immediate
+// offset.
 #define RNG_RW 32768          // ring words (a power of two: the index wraps with a mask)
+#define RNG_MIR 1080          // mirrored head (>= the 1078-word reach of the recurrence, even)
 
 struct RngShared {
-    uint32_t ring[RNG_RW];
-    int wtot[RNG_THREADS / 64];
+    uint32_t ring[RNG_RW + RNG_MIR];
+    int wtot[2 * RNG_THREADS / 64];
     int last;
     int has;
     double gauss;
@@ -1529,21 +1559,53 @@ __device__ __forceinline__ uint32_t rng_g(RngShared& S, int m) {
     return (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
 }
 
-// all threads: stream words [w0, w1), w0 >= 624
+// stores stream word q (and its mirror copy)
+__device__ __forceinline__ void rng_put(RngShared& S, int q, uint32_t v) {
+    const unsigned p = (unsigned)q & (RNG_RW - 1u);
+    S.ring[p] = v;
+    if (p < RNG_MIR) S.ring[RNG_RW + p] = v;
+}
+__device__ __forceinline__ uint32_t mt_g(uint32_t a, uint32_t b) {
+    const uint32_t y = (a & 0x80000000U) | (b & 0x7fffffffU);
+    return (y >> 1) ^ ((0U - (y & 1U)) & 0x9908b0dfU);
+}
+
+// all threads: stream words [w0, w1), w0 >= 624.  Steps of RNG_RUN * 207 <= 623 words, RNG_RUN
+// consecutive words per thread (operands shared between them; reads at odd lane strides are
+// free of bank conflicts)
+#ifndef RNG_RUN
+#define RNG_RUN 1
+#endif
 __device__ void rng_twist(RngShared& S, int w0, int w1) {
     const int t = threadIdx.x;
     int n0 = w0;
     while (n0 < w1 && n0 < 1078) {               // 227-wide steps (history from the key only)
         const int n1 = min(min(w1, 1078), n0 + 227);
         const int n = n0 + t;
-        if (n < n1) rng_at(S, n) = rng_at(S, n - 227) ^ rng_g(S, n - 624);
+        if (n < n1) rng_put(S, n, rng_at(S, n - 227) ^ rng_g(S, n - 624));
         __syncthreads();
         n0 = n1;
     }
-    while (n0 < w1) {                             // 623-wide steps
-        const int n1 = min(w1, n0 + 623);
-        const int n = n0 + t;
-        if (n < n1) rng_at(S, n) = rng_at(S, n - 681) ^ rng_g(S, n - 624) ^ rng_g(S, n - 851) ^ rng_g(S, n - 1078);
+    constexpr int STEP = RNG_RUN == 1 ? 623 : RNG_RUN * (623 / RNG_RUN);
+    while (n0 < w1) {
+        const int n1 = min(w1, n0 + STEP);
+        const int n = n0 + RNG_RUN * t;
+        if (n < n1) {
+            const unsigned p = (unsigned)n & (RNG_RW - 1u);
+            const uint32_t* b = S.ring + (p >= 1078u ? p : p + RNG_RW) - 1078u;   // b[i] = word n - 1078 + i
+            uint32_t a[RNG_RUN + 1], c[RNG_RUN + 1], e[RNG_RUN], f[RNG_RUN + 1];
+#pragma unroll
+            for (int i = 0; i <= RNG_RUN; ++i) {
+                a[i] = b[i];            // n-1078 ..
+                c[i] = b[227 + i];      // n-851 ..
+                f[i] = b[454 + i];      // n-624 ..
+                if (i < RNG_RUN) e[i] = b[397 + i];   // n-681 ..
+            }
+#pragma unroll
+            for (int i = 0; i < RNG_RUN; ++i)
+                if (RNG_RUN == 1 || n + i < n1)
+                    rng_put(S, n + i, e[i] ^ mt_g(f[i], f[i + 1]) ^ mt_g(c[i], c[i + 1]) ^ mt_g(a[i], a[i + 1]));
+        }
         __syncthreads();
         n0 = n1;
     }
@@ -1574,7 +1636,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         a.pairs = sr(a_in.pairs, so); a.pairs_oi = sr(a_in.pairs_oi, so);
     }
     const int t = threadIdx.x;
-    for (int i = t; i < 624; i += RNG_THREADS) S.ring[i] = a.st->key[i];
+    for (int i = t; i < 624; i += RNG_THREADS) rng_put(S, i, a.st->key[i]);
     const int pos0 = a.st->pos;
     if (t == 0) {
         S.has = a.st->has_gauss;
@@ -1673,49 +1735,59 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         uint32_t* const pairs_u = a.pairs ? a.pairs + (size_t)u * a.pcap * 4 : nullptr;
         if (a.pairs && t == 0) a.pairs_oi[u] = oi;
         int got = 0;
+        // two candidates per thread and round: words [q, q + 4096) (set A) and [q + 4096, q + 8192)
+        // (set B), ranked in stream order -- half the barrier rounds of one candidate per thread
         while (got < need_pairs) {
-            ensure(q + 4 * RNG_THREADS);
+            ensure(q + 8 * RNG_THREADS);
             RNG_PROF_T(c0);
-            const int c = q + 4 * t;
-            const uint32_t w0 = mt_temper(rng_word(S, c)), w1 = mt_temper(rng_word(S, c + 1));
-            const uint32_t w2 = mt_temper(rng_word(S, c + 2)), w3 = mt_temper(rng_word(S, c + 3));
-            const double u1 = ((double)(int32_t)(w0 >> 5) * 67108864.0 + (double)(int32_t)(w1 >> 6)) / 9007199254740992.0;
-            const double u2 = ((double)(int32_t)(w2 >> 5) * 67108864.0 + (double)(int32_t)(w3 >> 6)) / 9007199254740992.0;
-            const double x1 = 2.0 * u1 - 1.0;
-            const double x2 = 2.0 * u2 - 1.0;
-            const double r2 = x1 * x1 + x2 * x2;
-            const bool acc = (r2 < 1.0) && (r2 != 0.0);
-            int total;
-            const int rank = block_rank(acc, S.wtot, total);
+            uint32_t w[2][4];
+            double x1[2], x2[2], r2[2];
+            bool acc[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int c = q + 4 * (t + k * RNG_THREADS);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) w[k][i] = mt_temper(rng_word(S, c + i));
+                const double u1 = ((double)(int32_t)(w[k][0] >> 5) * 67108864.0 + (double)(int32_t)(w[k][1] >> 6)) / 9007199254740992.0;
+                const double u2 = ((double)(int32_t)(w[k][2] >> 5) * 67108864.0 + (double)(int32_t)(w[k][3] >> 6)) / 9007199254740992.0;
+                x1[k] = 2.0 * u1 - 1.0;
+                x2[k] = 2.0 * u2 - 1.0;
+                r2[k] = x1[k] * x1[k] + x2[k] * x2[k];
+                acc[k] = (r2[k] < 1.0) && (r2[k] != 0.0);
+            }
+            int rk[2], total;
+            block_rank2(acc[0], acc[1], S.wtot, rk[0], rk[1], total);
             const int np = need_pairs - got;
-            if (acc && rank < np) {
-                const int o = oi + 2 * (got + rank);
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                if (!(acc[k] && rk[k] < np)) continue;
+                const int o = oi + 2 * (got + rk[k]);
                 if (pairs_u) {
                     // k_polar computes this pair's normals; the cached second value of an odd
                     // count is state, so that one pair's transform also runs here (same code)
-                    *reinterpret_cast<uint4*>(pairs_u + 4 * (got + rank)) = make_uint4(w0, w1, w2, w3);
+                    *reinterpret_cast<uint4*>(pairs_u + 4 * (got + rk[k])) = make_uint4(w[k][0], w[k][1], w[k][2], w[k][3]);
                     if (o + 1 >= a.n_norm) {
-                        S.gauss = sqrt(-2.0 * log(r2) / r2) * x1;
+                        S.gauss = sqrt(-2.0 * log(r2[k]) / r2[k]) * x1[k];
                         S.has = 1;
                     }
                 } else {
-                    const double f = sqrt(-2.0 * log(r2) / r2);
-                    out_norm[o] = (float)(f * x2);
+                    const double f = sqrt(-2.0 * log(r2[k]) / r2[k]);
+                    out_norm[o] = (float)(f * x2[k]);
                     if (o + 1 < a.n_norm) {
-                        out_norm[o + 1] = (float)(f * x1);
+                        out_norm[o + 1] = (float)(f * x1[k]);
                     } else {
-                        S.gauss = f * x1;
+                        S.gauss = f * x1[k];
                         S.has = 1;
                     }
                 }
+                if (rk[k] == np - 1) S.last = t + k * RNG_THREADS;   // the candidate that completes the draw
             }
-            if (acc && rank == np - 1) S.last = t;
             __syncthreads();
             if (total >= np) {
                 q += 4 * (S.last + 1);
                 got = need_pairs;
             } else {
-                q += 4 * RNG_THREADS;
+                q += 8 * RNG_THREADS;
                 got += total;
             }
             RNG_PROF_T(c1);

@@ -189,6 +189,8 @@ struct sacx_handle {
     // every entry point that could observe or disturb it runs it first (settle).
     int alpha_pending = -1;
     int64_t cur_size_host = 0; // mirrors ctl->cur_size (appends, resync)
+    int64_t n_appends = 0;     // sacx_buffer_append calls (a full ring changes content, not size)
+    int64_t spec_appends = 0;  // n_appends when the speculative draw was queued
     hipEvent_t act_ev = nullptr;   // end of the last act_host kernel chain (its actions are on the host)
 
     uint64_t add(const std::string& name, int64_t rows, int64_t cols, int dtype, int role) {
@@ -1608,8 +1610,9 @@ int get_spec_graph(sacx_handle* h, int slot, int prev, hipGraphExec_t* out) {
         body.insert(body.end(), own.begin(), own.end());
     }
     HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-    for (const Launch& L : h->plan[slot])      // the draw stamped pseq[slot] itself
-        if (L.kind == Launch::GATHER) enqueue(L, h, h->cap_stream);
+    if (h->cfg.use_expert)                     // plain SAC: the speculative draw gathered too
+        for (const Launch& L : h->plan[slot])  // (the draw stamped pseq[slot] itself)
+            if (L.kind == Launch::GATHER) enqueue(L, h, h->cap_stream);
     for (const Launch& L : body) enqueue(L, h, h->cap_stream);
     hipGraph_t graph;
     HIPCHK(h, hipStreamEndCapture(h->cap_stream, &graph));
@@ -1978,6 +1981,7 @@ int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const flo
     launch_append(g, h->stream);
     HIPCHK(h, hipGetLastError());
     h->cur_size_host = std::min<int64_t>(h->cur_size_host + n, h->cap);
+    ++h->n_appends;
     return 0;
 }
 
@@ -2045,9 +2049,13 @@ static int spec_draw(sacx_handle* h) {
     r.size_fixed = h->cur_size_host;
     r.backup = h->ptr<RngState>("rng.spec");
     launch_rng(r, h->stream);
+    if (!h->cfg.use_expert)      // plain SAC: the gather too (SAC-EO's reads the permutation the
+        for (const Launch& L : h->plan[slot])   // caller pushes before the update)
+            if (L.kind == Launch::GATHER) enqueue(L, h, h->stream);
     HIPCHK(h, hipGetLastError());
     h->spec_live = true;
     h->spec_size = h->cur_size_host;
+    h->spec_appends = h->n_appends;
     return 0;
 }
 
@@ -2229,7 +2237,8 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // step are valid when the ring now holds the size they assumed (nothing else drew meanwhile:
     // every other consumer of the stream undid the draw)
     const bool spec_ok = spec_mode(h) && n_steps == 1 && flags == 0;
-    const bool use_spec = spec_ok && h->spec_live && h->spec_size == h->cur_size_host;
+    const bool use_spec = spec_ok && h->spec_live && h->spec_size == h->cur_size_host &&
+                          h->spec_appends == h->n_appends;
     if (!use_spec && settle(h)) return -1;
     h->last_step_one = spec_ok;
     // a deferred alpha.final (folded into this update) adds ts_increment to num_timesteps before

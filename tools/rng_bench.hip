@@ -36,8 +36,10 @@ int main() {
             RngArgs b = a;
             b.pairs = nullptr; b.out_idx = idx2; b.out_norm = nz2;
             RngArgs o = a; o.n_int = 0; o.n_norm = 7; o.nupd = 1; o.pairs = nullptr;
+            CK(hipStreamSynchronize(s));
             CK(hipMemcpy(st, &h, sizeof(h), hipMemcpyHostToDevice));
             launch_rng(o, s); launch_rng(a, s);
+            CK(hipStreamSynchronize(s));
             CK(hipMemcpy(st, &h, sizeof(h), hipMemcpyHostToDevice));
             launch_rng(o, s); launch_rng(b, s);
             CK(hipStreamSynchronize(s));
