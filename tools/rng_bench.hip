@@ -36,6 +36,7 @@ int main() {
             RngArgs b = a;
             b.pairs = nullptr; b.out_idx = idx2; b.out_norm = nz2;
             RngArgs o = a; o.n_int = 0; o.n_norm = 7; o.nupd = 1; o.pairs = nullptr;
+            o.out_norm = nz + (24 << 20) / 4;   // away from the compared slots
             CK(hipStreamSynchronize(s));
             CK(hipMemcpy(st, &h, sizeof(h), hipMemcpyHostToDevice));
             launch_rng(o, s); launch_rng(a, s);
