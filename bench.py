@@ -126,6 +126,26 @@ def pmc_traffic(kernel, config):
         return None, None
 
 
+def rocprof_family_avg(kernel, config, flops_per_launch):
+    """Calls-weighted average duration of `kernel`'s instances in the newest committed
+    profiles/r*_<config>_kernel_stats_*.csv and the roofline fraction it gives."""
+    import csv
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_kernel_stats_*.csv")))
+    if not paths:
+        return {}
+    tot, n = 0.0, 0
+    with open(paths[-1]) as fh:
+        for r in csv.DictReader(fh):
+            if f"::{kernel}<" in r["Name"] or f"::{kernel}(" in r["Name"] or f"{kernel}_head<" in r["Name"]:
+                tot += float(r["TotalDurationNs"])
+                n += int(r["Calls"])
+    if n == 0:
+        return {}
+    avg_us = tot / n / 1e3
+    return {"rocprof_stats": os.path.relpath(paths[-1], ROOT), "rocprof_avg_launch_us": round(avg_us, 3),
+            "rocprof_frac": round(flops_per_launch / (avg_us * 1e-6) / (FP32_PEAK_TFLOPS * 1e12), 5)}
+
+
 def pmc_counter(kernel, config, counter):
     """Mean per-dispatch value of a PMC counter of `kernel` from profiles/pmc_<config>.json."""
     try:
@@ -182,6 +202,9 @@ def roofline(eng, config, n_prof=20, n_replays=20):
             glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_kernel_table_*.md")))[-1:]), None),
         "flops_per_launch": flops_per_launch,
         "algorithmic_bytes_per_launch": f["bytes"] / launches,
+        # the committed rocprofv3 --kernel-trace --stats summary of this command (calls-weighted
+        # over every k_gemm instance): its dispatch window includes the end-of-kernel release
+        **rocprof_family_avg(dom, config, flops_per_launch),
         "timing": "per-workgroup device timestamps in a replay of the update graph (sacx_time_kernels)",
         "family_us_per_update": round(us_per_update, 3),
         "graph_us_per_update": round(t_full * 1e3, 3),
