@@ -1634,6 +1634,7 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
         a.st = sr(a_in.st, so); a.ctl = sr(a_in.ctl, so);
         a.out_idx = sr(a_in.out_idx, so); a.out_norm = sr(a_in.out_norm, so);
         a.pairs = sr(a_in.pairs, so); a.pairs_oi = sr(a_in.pairs_oi, so);
+        a.backup = sr(a_in.backup, so);
     }
     const int t = threadIdx.x;
     for (int i = t; i < 624; i += RNG_THREADS) rng_put(S, i, a.st->key[i]);

@@ -236,16 +236,18 @@ int fail(sacx_handle* h, const std::string& msg) {
 int spec_cancel(sacx_handle* h, bool keep_state = false) {
     if (!h->spec_live) return 0;
     h->spec_live = false;
+    // every seed's state (packed seeds: one block per seed, seed_bytes apart)
+    const size_t pitch = h->seeds > 1 ? (size_t)h->seed_bytes : sizeof(RngState);
     if (!keep_state &&
-        hipMemcpyAsync(h->ptr<RngState>("rng"), h->ptr<RngState>("rng.spec"), sizeof(RngState),
-                       hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
+        hipMemcpy2DAsync(h->arena0 + h->off_of("rng"), pitch, h->arena0 + h->off_of("rng.spec"), pitch,
+                         sizeof(RngState), (size_t)h->seeds, hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
         return fail(h, "spec restore");
     return 0;
 }
 
 // the handles the speculative draw applies to: one learner, its own RNG stream
 bool spec_mode(const sacx_handle* h) {
-    return h->spec_enabled && h->seeds == 1 && h->dp_ranks == 0 && !h->dp_local && 2 * h->nbatch >= 3;
+    return h->spec_enabled && h->dp_ranks == 0 && !h->dp_local && 2 * h->nbatch >= 3;
 }
 
 #define HIPCHK(h, x)                                                                    \
@@ -2046,8 +2048,8 @@ static int spec_draw(sacx_handle* h) {
     r.reset_seq = h->alpha_pending >= 0 ? 2 : 1;
     h->spec_slot = slot;
     r.nupd = 1;
-    r.size_fixed = h->cur_size_host;
-    r.backup = h->ptr<RngState>("rng.spec");
+    r.size_fixed = 0;           // each seed's ring size, read on the device (final until the update)
+    r.backup = reinterpret_cast<RngState*>(h->arena0 + h->off_of("rng.spec"));   // seed 0's (relocated per seed)
     launch_rng(r, h->stream);
     if (!h->cfg.use_expert)      // plain SAC: the gather too (SAC-EO's reads the permutation the
         for (const Launch& L : h->plan[slot])   // caller pushes before the update)
@@ -2107,6 +2109,8 @@ int sacx_buffer_append_host_seeds(sacx_handle* h, const float* s, const float* a
     ag.s = g; ag.a = g + tot * S; ag.r = g + tot * (S + A); ag.sp = g + tot * (S + A + 1); ag.d = g + tot * (2 * S + A + 1);
     ag.n = n; ag.ctl = h->ctl0(); ag.sstride = (int64_t)h->seed_bytes; ag.nseeds = K;
     launch_append(ag, h->stream);
+    h->cur_size_host = std::min<int64_t>(h->cur_size_host + n, h->cap);   // every seed grows alike
+    ++h->n_appends;
     HIPCHK(h, hipGetLastError());
     HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
     h->pin_pending = true;
@@ -2126,6 +2130,7 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
     float* const ga = h->pin_dev + STAGE_CAP;
     std::memcpy(pa, obs, sizeof(float) * tot * S);
     float* noise = deterministic ? nullptr : h->f0("act.noise");
+    if (!deterministic && spec_cancel(h)) return -1;   // a draw from the streams: undo the speculative one
     if (!deterministic) {            // each seed's u = np.random.normal(size=(n, A)) from its own stream
         RngArgs r{};
         r.st = reinterpret_cast<RngState*>(h->f0("rng")); r.ctl = h->ctl0();
@@ -2151,7 +2156,10 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
     a.sstride = (int64_t)h->seed_bytes; a.nseeds = K; a.m = (int32_t)n;
     launch_act_rows(a, (int)n, h->stream);
     HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+    // lock-step drop-in cadence: every seed's next sampler draw queued behind the actions
+    if (h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0 && spec_draw(h)) return -1;
+    HIPCHK(h, hipEventSynchronize(h->act_ev));
     std::memcpy(act_out, pa + tot * S, sizeof(float) * tot * A);
     return 0;
 }
@@ -2237,8 +2245,7 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // step are valid when the ring now holds the size they assumed (nothing else drew meanwhile:
     // every other consumer of the stream undid the draw)
     const bool spec_ok = spec_mode(h) && n_steps == 1 && flags == 0;
-    const bool use_spec = spec_ok && h->spec_live && h->spec_size == h->cur_size_host &&
-                          h->spec_appends == h->n_appends;
+    const bool use_spec = spec_ok && h->spec_live && h->spec_appends == h->n_appends;
     if (!use_spec && settle(h)) return -1;
     h->last_step_one = spec_ok;
     // a deferred alpha.final (folded into this update) adds ts_increment to num_timesteps before

@@ -100,7 +100,9 @@ class GaussianActor:
         return _as_out(out.cpu().numpy())
 
     def clip(self, a):
-        return np.clip(a, self.act_low, self.act_high)
+        # np.clip (continuous_actors.py's tf.clip_by_value on host arrays); minimum / maximum
+        # give the same values without np.clip's per-call dispatch cost in the env loop
+        return np.minimum(np.maximum(a, self.act_low), self.act_high)
 
     def tf_clip(self, a):
         return self.clip(a)

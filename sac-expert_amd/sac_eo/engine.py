@@ -716,7 +716,10 @@ class SeedView:
 
     @property
     def v(self):
-        return self._eng._views[self._k]
+        eng = self._eng
+        if getattr(eng, "h", None) is not None and getattr(eng, "_bound", False):   # an observation point
+            N.check(eng.lib.sacx_settle(eng.h), eng.h, "settle")
+        return eng._views[self._k]
 
     @property
     def seed_index(self):

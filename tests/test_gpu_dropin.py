@@ -91,3 +91,50 @@ def test_speculative_sac_eo_with_deferred_alpha(gpu_available, monkeypatch):
             assert a == b, (a, b)
         else:
             assert np.array_equal(a, b), i
+
+
+@pytest.mark.parametrize("use_expert", [False, True])
+def test_speculative_packed_lockstep(gpu_available, monkeypatch, use_expert):
+    """The lock-step --runs cadence on a packed handle (act_host_seeds -> step(1) ->
+    append_host_seeds; single_seed_plan): every seed's speculative draw and deferred alpha branch
+    == the same calls with SACX_SPEC=0, bit for bit, incl. a stochastic round and a per-seed
+    observation (SeedView stats) mid-run."""
+    from sac_eo.engine import Engine, EngineConfig
+    K, B, N, n = 3, 64, 700, 30
+    outs, hits = [], []
+    for spec in ("1", "0"):
+        monkeypatch.setenv("SACX_SPEC", spec)
+        learners = [make_learner(act="relu", B=B, N=N, seed=40 + 3 * k, use_expert=use_expert, done_p=0.05)
+                    for k in range(K)]
+        eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=N + 100,
+                                  graph_steps=1, seeds=K, single_seed_plan=True, use_expert=use_expert,
+                                  expert_capacity=20, expert_batch=20, epsilon=0.1))
+        for k, (ocfg, st, buf, nrm, expert) in enumerate(learners):
+            eng.select_seed(k)
+            load_learner(eng, st, buf, nrm, expert, 0.1)
+            eng.rng_set_state(np.random.RandomState(50 + k).get_state())
+            if use_expert:
+                rp = np.random.RandomState(60 + k)
+                eng.push_perms(np.stack([rp.permutation(20) for _ in range(n + 4)]))
+        eng.select_seed(0)
+        rs = np.random.RandomState(9)
+        for j in range(n):
+            o = rs.normal(size=(K, 17)).astype(np.float32)
+            o2 = rs.normal(size=(K, 17)).astype(np.float32)
+            a = eng.act_host_seeds(o, deterministic=(j % 9 != 4))
+            eng.step(1, num_timesteps=j, ts_increment=1)
+            eng.append_host_seeds(o[:, None], a[:, None], np.full((K, 1), 0.5, np.float32), o2[:, None],
+                                  np.zeros((K, 1), np.float32))
+            if j == 17:
+                assert np.isfinite(eng.seed_view(1).stats(1)).all()
+        eng.sync()
+        hits.append(eng.spec_hits())
+        res = []
+        for k in range(K):
+            eng.select_seed(k)
+            res += [eng.stats(n).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state()[1].copy()]
+        outs.append(res)
+        eng.close()
+    assert hits[1] == 0 and hits[0] >= n // 2, hits
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert np.array_equal(a, b), i
