@@ -1821,29 +1821,37 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
 
 // The polar transform of the pairs k_rng accepted (legacy_gauss, mtrand): one thread per pair of
 // every update of the batch, the same fp64 arithmetic as k_rng's own path (bit-identical output)
+// A few workgroups per update, striding over its pairs: off the update chain, so it need not be
+// fast, but a wide grid would take CUs from the chain's launches running beside it.
+#ifndef SACX_POLAR_WGS
+#define SACX_POLAR_WGS 8
+#endif
 __global__ __launch_bounds__(256) void k_polar(RngArgs a) {
     const int64_t so = seed_off(a.sstride);
     const int u = blockIdx.y;
-    const int j = blockIdx.x * 256 + threadIdx.x;
     const int oi = sr(a.pairs_oi, so)[u];
-    if (j >= ((a.n_norm - oi + 1) >> 1)) return;
-    const uint4 w = *reinterpret_cast<const uint4*>(sr(a.pairs, so) + ((size_t)u * a.pcap + j) * 4);
-    const double u1 = ((double)(int32_t)(w.x >> 5) * 67108864.0 + (double)(int32_t)(w.y >> 6)) / 9007199254740992.0;
-    const double u2 = ((double)(int32_t)(w.z >> 5) * 67108864.0 + (double)(int32_t)(w.w >> 6)) / 9007199254740992.0;
-    const double x1 = 2.0 * u1 - 1.0;
-    const double x2 = 2.0 * u2 - 1.0;
-    const double r2 = x1 * x1 + x2 * x2;
-    const double f = sqrt(-2.0 * log(r2) / r2);
-    float* out = (float*)((char*)sr(a.out_norm, so) + (int64_t)u * a.slot_bytes);
-    const int o = oi + 2 * j;
-    out[o] = (float)(f * x2);
-    if (o + 1 < a.n_norm) out[o + 1] = (float)(f * x1);
+    const int np = (a.n_norm - oi + 1) >> 1;
+    const uint32_t* const pairs = sr(a.pairs, so) + (size_t)u * a.pcap * 4;
+    float* const out = (float*)((char*)sr(a.out_norm, so) + (int64_t)u * a.slot_bytes);
+    for (int j = blockIdx.x * 256 + threadIdx.x; j < np; j += gridDim.x * 256) {
+        const uint4 w = *reinterpret_cast<const uint4*>(pairs + (size_t)j * 4);
+        const double u1 = ((double)(int32_t)(w.x >> 5) * 67108864.0 + (double)(int32_t)(w.y >> 6)) / 9007199254740992.0;
+        const double u2 = ((double)(int32_t)(w.z >> 5) * 67108864.0 + (double)(int32_t)(w.w >> 6)) / 9007199254740992.0;
+        const double x1 = 2.0 * u1 - 1.0;
+        const double x2 = 2.0 * u2 - 1.0;
+        const double r2 = x1 * x1 + x2 * x2;
+        const double f = sqrt(-2.0 * log(r2) / r2);
+        const int o = oi + 2 * j;
+        out[o] = (float)(f * x2);
+        if (o + 1 < a.n_norm) out[o + 1] = (float)(f * x1);
+    }
 }
 
 void launch_rng(const RngArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_rng, dim3(1, 1, seeds_z(a.nseeds)), dim3(RNG_THREADS), 0, s, a);
     if (a.pairs != nullptr && a.n_norm > 0)
-        hipLaunchKernelGGL(k_polar, dim3((a.pcap + 255) / 256, a.nupd, seeds_z(a.nseeds)), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_polar, dim3(std::min((a.pcap + 255) / 256, SACX_POLAR_WGS), a.nupd, seeds_z(a.nseeds)),
+                           dim3(256), 0, s, a);
 }
 
 // ==================================================================== k_gather
