@@ -1370,6 +1370,307 @@ __global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
     }
 }
 
+// ==================================================================== k_dwl
+// dW + Keras Adam for long reductions (K = batch rows >= 512: Humanoid's B = 1,024): 32x32
+// output tiles whose operand rows stream into LDS by LDS-DMA (global_load_lds), several 16-row
+// slabs ahead of the MFMAs.  The 16x16 dW tile reads each of its K rows as 64-B column pieces
+// straight into the MFMA operand layout (fragment-shaped loads: half cache lines, 12 dependent
+// dword loads per lane and slab) and runs L2-bound; here each row piece is a whole 128-B line,
+// and the loads of slab i + NST - 1 are in flight while slab i is multiplied.
+// Summation order is gemm_core's 16x16 path, sub-tile by sub-tile: wave w owns the same quarter
+// of K, each MFMA the same four k (16 it + 4 grp + j), the same acc0 / acc1 split and the same
+// 4-wave reduction order, so all three dW tilings give bit-identical results.
+#ifndef SACX_DWL_NST
+#define SACX_DWL_NST 4    // slabs in flight per wave (LDS 4 waves x NST x 4.25 KB: 2 workgroups per CU)
+#endif
+#define DWL_STG 1088      // floats per slab stage: X [16][32], D [16][32], bscale [64] (16 used)
+
+typedef __attribute__((address_space(3))) void* lds_vp;
+__device__ __forceinline__ uint32_t lds_addr(const float* p) { return (uint32_t)(uintptr_t)(lds_vp)(p); }
+// One LDS-DMA wave-instruction: lane l's 16 (V4) or 4 bytes from g land at LDS byte address
+// l0 + l * size.  Inline asm rather than __builtin_amdgcn_global_load_lds: knowing of the DMA,
+// hipcc waits vmcnt(0) before every LDS read of the slab loop, which drains the pipeline; the
+// loop orders its reads by explicit counted waits instead.  m0 is saved and restored.
+template <bool V4>
+__device__ __forceinline__ void glds(const float* g, uint32_t l0) {
+    uint32_t keep;
+    if constexpr (V4)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(l0) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(keep) : "v"(g), "s"(l0) : "memory");
+}
+
+// LDS column c of slab row `row` holds operand column c ^ dwl_sw(row): rows 4-7 and 12-15 swap
+// their 16-column halves, so the two row groups of one ds_read_b32 lane group (grp 0 / 1, 2 / 3)
+// fall into different banks
+__device__ __forceinline__ int dwl_sw(int row) { return ((row >> 2) & 1) << 4; }
+
+// one slab (rows k0 .. k0 + 15, columns c0 .. c0 + 31) of a row-major [K][ld] operand into the
+// LDS image [16][32] at byte address l0: V4 by 16-B pieces (ld % 4 == 0, 16-B aligned base: 2
+// instructions), else by dwords (8 instructions).  Rows past K and columns past the row repeat
+// valid elements; the reader masks them exactly where load_a / load_b read zeros.
+template <bool V4>
+__device__ __forceinline__ void dwl_issue(const float* base, int ld, int k0, int K, int c0, uint32_t l0, int lane) {
+    if constexpr (V4) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int row = 8 * q + (lane >> 3);
+            const int col = min(c0 + (((lane & 7) << 2) ^ dwl_sw(row)), ld - 4);
+            const int k = min(k0 + row, K - 1);
+            glds<true>(base + (size_t)k * ld + col, l0 + q * 1024);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int row = 2 * q + (lane >> 5);
+            const int col = min(c0 + ((lane & 31) ^ dwl_sw(row)), ld - 1);
+            const int k = min(k0 + row, K - 1);
+            glds<false>(base + (size_t)k * ld + col, l0 + q * 256);
+        }
+    }
+}
+
+template <bool BF, bool PK>
+__global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#ifdef SACX_GEMM_PHASES
+    if (threadIdx.x == 0) g_gemm_ph[blockIdx.x][0] = t0;
+#endif
+    __shared__ float lds[4 * SACX_DWL_NST * DWL_STG];    // the one LDS object (staging, then reduction)
+    const int64_t so = PK ? seed_off(ga.sstride) : 0;
+    const int total_tiles = ga.total_tiles, xcd_map = ga.xcd_map, nprob = ga.nprob;
+    int tb[GEMM_MAXP];
+#pragma unroll
+    for (int i = 0; i < GEMM_MAXP; ++i) tb[i] = ga.probs[i].tile_begin;
+    asm volatile("" ::"s"(total_tiles), "s"(xcd_map), "s"(nprob), "s"(tb[1]), "s"(tb[2]), "s"(tb[3]), "s"(tb[4]),
+                 "s"(tb[5]), "s"(tb[6]), "s"(tb[7]));
+    int tile = (int)blockIdx.x;
+    if (xcd_map) tile = xcd_tile(tile, total_tiles);
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < GEMM_MAXP; ++i)
+        if (i < nprob && tile >= tb[i]) p = i;
+    GemmProb g = ga.probs[p];
+    asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                 "s"(g.tile_begin), "s"(g.bscale), "s"(g.P), "s"(g.T), "s"(g.ldp), "s"(g.ones_row), "s"(g.group),
+                 "s"(g.epi), "s"(g.grad_scale), "s"(g.vec), "s"(ga.adam.lr[0]), "s"(ga.adam.lr[1]), "s"(ga.adam.lr[2]),
+                 "s"(ga.adam.lr[3]), "s"(ga.adam.tau_keep), "s"(ga.adam.tau_take), "s"(ga.adam.target_update_int));
+    reloc(g, so);
+    const int lt = tile - g.tile_begin;
+    const int tm = lt / g.tiles_n, tn = lt - tm * g.tiles_n;
+    const int m0 = tm * 32, n0 = tn * 32;
+    const int wave = wave_id(), lane = threadIdx.x & 63;     // wave uniform: the slab loop is scalar
+    const int r = lane & 15, grp = lane >> 4;
+    const int t = threadIdx.x, row = t >> 4, col = t & 15;
+
+    // ---- epilogue operands of this thread's four outputs first (sub-tile s = 2 i + j: rows
+    // +16 i, cols +16 j), as gemm_tile32
+    float e0[4], e1[4], e2[4], e3[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int mm = m0 + 16 * (s >> 1) + row, nn = n0 + 16 * (s & 1) + col;
+        const size_t pidx = (size_t)min(mm, g.M - 1) * g.ldp + min(nn, g.N - 1);
+#ifdef SACX_DWL_NOEPI       // diagnostic builds: no epilogue operand loads
+        e0[s] = e1[s] = e2[s] = e3[s] = (float)pidx;
+        continue;
+#endif
+        e0[s] = g.P[pidx];
+        e1[s] = g.P[pidx + ga.p_stride];
+        e2[s] = g.P[pidx + 2 * ga.p_stride];
+        e3[s] = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
+    }
+    const EpiScalars es = epi_scalars(sr(ga.ctl, so), g.group);
+
+    const int nIt = (g.K + 15) >> 4;
+    const int per = (nIt + 3) >> 2;
+    const int it0 = wave * per;
+    const int n = max(0, min(nIt, it0 + per) - it0);      // this wave's slabs (uniform per wave)
+    float* wl = lds + wave * (SACX_DWL_NST * DWL_STG);
+    const uint32_t wl_addr = __builtin_amdgcn_readfirstlane(lds_addr(wl));
+    // Operand values.  Rows past M and columns past N of a tile only feed outputs that are never
+    // stored, so they need no masking; the bias-gradient row (m == ones_row) takes 1.0 for X, and
+    // reduction rows past K (their DMA repeats row K - 1) take a zero scale, as load_a / load_b
+    // read zeros there (a zero of either sign contributes nothing to a sum that starts at +0).
+    bool isone[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) isone[h] = m0 + 16 * h + r == g.ones_row;
+    // lane (r, grp) reads rows 4 grp + j: its swizzle is dwl_sw(4 grp + j) = 16 (grp & 1)
+    const int sx = 16 * (grp & 1);
+    floatx4 acc0[4], acc1[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        acc0[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+        acc1[s] = floatx4{0.f, 0.f, 0.f, 0.f};
+    }
+    // the raw LDS values of one slab in this lane's MFMA layout (X, D, bscale)
+    struct Slab { float x[2][4], d[2][4], bs[4]; };
+    auto read_slab = [&](int i, Slab& v) {
+        const float* st = wl + (i % SACX_DWL_NST) * DWL_STG;
+        const float4 b4 = *reinterpret_cast<const float4*>(st + 1024 + 4 * grp);
+        v.bs[0] = b4.x; v.bs[1] = b4.y; v.bs[2] = b4.z; v.bs[3] = b4.w;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int o = (4 * grp + j) * 32 + ((16 * h) ^ sx) + r;
+                v.x[h][j] = st[o];
+                v.d[h][j] = st[512 + o];
+            }
+    };
+    auto body = [&](auto xv, auto dv) {
+        constexpr bool XV = decltype(xv)::value, DV = decltype(dv)::value;
+        constexpr int G = (XV ? 2 : 8) + (DV ? 2 : 8) + 1;      // LDS-DMA instructions per slab
+        constexpr int NST = SACX_DWL_NST;
+        auto issue = [&](int i) {
+#ifdef SACX_DWL_NOLOAD      // diagnostic builds (tools/dw_bench.hip): the loop without its loads
+            return;
+#endif
+            const uint32_t st = wl_addr + (uint32_t)((i % NST) * DWL_STG * 4);
+            const int k0 = (it0 + i) * 16;
+            dwl_issue<XV>(g.A, g.lda, k0, g.K, m0, st, lane);
+            dwl_issue<DV>(g.B, g.ldb, k0, g.K, n0, st + 2048, lane);
+            glds<false>(g.bscale + min(k0 + (lane & 15), g.K - 1), st + 4096);
+        };
+        if (n == 0) return;
+#pragma unroll
+        for (int i = 0; i < NST - 1; ++i)
+            if (i < n) issue(i);
+        if (n >= NST - 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * G) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        GEMM_PH(1);
+        Slab cur, nxt;
+        read_slab(0, cur);
+        // retire slab 0's reads here, in hipcc's own wait bookkeeping: left pending into the loop
+        // they make it wait (on every iteration) for the reads of the next slab as well
+        asm volatile("" ::"v"(cur.x[0][0]), "v"(cur.x[0][1]), "v"(cur.x[0][2]), "v"(cur.x[0][3]), "v"(cur.x[1][0]),
+                     "v"(cur.x[1][1]), "v"(cur.x[1][2]), "v"(cur.x[1][3]), "v"(cur.bs[0]), "v"(cur.bs[1]),
+                     "v"(cur.bs[2]), "v"(cur.bs[3]));
+        asm volatile("" ::"v"(cur.d[0][0]), "v"(cur.d[0][1]), "v"(cur.d[0][2]), "v"(cur.d[0][3]), "v"(cur.d[1][0]),
+                     "v"(cur.d[1][1]), "v"(cur.d[1][2]), "v"(cur.d[1][3]));
+        float pa[2][4], pb[2][4];      // bf16: the even slab of the pair
+        for (int i = 0; i < n; ++i) {
+            // Slab i's values are in registers.  Refill the stage slab i - 1 left (its reads
+            // retired), wait for slab i + 1 and request its values, then multiply slab i: the
+            // LDS round trip of slab i + 1 runs under the MFMAs of slab i.
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (i + NST - 1 < n) {
+                issue(i + NST - 1);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * G) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            if (i + 1 < n) read_slab(i + 1, nxt);
+            const int kb = (it0 + i) * 16 + 4 * grp;
+            float a[2][4], b[2][4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float sc = kb + j < g.K ? cur.bs[j] : 0.f;
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    a[h][j] = isone[h] ? 1.f : cur.x[h][j];
+                    b[h][j] = cur.d[h][j] * sc;
+                }
+            }
+            if constexpr (BF) {
+                // slab pairs (it0 + 2q, it0 + 2q + 1), alternately into acc0 / acc1 (gemm_core's
+                // groups of four from it0); an odd last slab pairs with zeros
+                const bool last = i == n - 1;
+                if ((i & 1) == 0 && !last) {
+#pragma unroll
+                    for (int h = 0; h < 2; ++h)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) { pa[h][j] = a[h][j]; pb[h][j] = b[h][j]; }
+                } else {
+                    const bool odd = (i & 1) != 0;
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        float a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            a0[j] = odd ? pa[s >> 1][j] : a[s >> 1][j];
+                            a1[j] = odd ? a[s >> 1][j] : 0.f;
+                            b0[j] = odd ? pb[s & 1][j] : b[s & 1][j];
+                            b1[j] = odd ? b[s & 1][j] : 0.f;
+                        }
+                        if ((i >> 1) & 1) acc1[s] = mfma_bf16_2slab(a0, a1, b0, b1, acc1[s]);
+                        else acc0[s] = mfma_bf16_2slab(a0, a1, b0, b1, acc0[s]);
+                    }
+                }
+            } else {
+#ifdef SACX_DWL_NOMFMA      // diagnostic builds: the loop without its MFMAs
+                acc0[0][0] += a[0][0] + b[0][0] + a[1][3] + b[1][3];
+#else
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int s = 0; s < 4; ++s) {
+                        if (j & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s >> 1][j], b[s & 1][j], acc1[s], 0, 0, 0);
+                        else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s >> 1][j], b[s & 1][j], acc0[s], 0, 0, 0);
+                    }
+#endif
+            }
+            cur = nxt;
+        }
+    };
+    if (g.vec & 1) {
+        if (g.vec & 2) body(std::true_type{}, std::true_type{});
+        else body(std::true_type{}, std::false_type{});
+    } else {
+        if (g.vec & 2) body(std::false_type{}, std::true_type{});
+        else body(std::false_type{}, std::false_type{});
+    }
+    GEMM_PH(2);
+    // reduction through the wave's own (retired) staging: sub-tile s of wave w at wl + s * 256
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const floatx4 acc = acc0[s] + acc1[s];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) wl[s * 256 + q * 64 + lane] = acc[q];
+    }
+    __syncthreads();
+    GEMM_PH(3);
+    const int L = ((row >> 2) << 4) | col, R = row & 3;
+    const int64_t nts = (int64_t)__builtin_amdgcn_readfirstlane((int)(es.nts >> 32)) << 32 |
+                        (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
+    const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
+    const bool polyak = nts % tui == 0;
+    constexpr int WS = SACX_DWL_NST * DWL_STG;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int o = s * 256 + R * 64 + L;
+        float v = lds[o] + lds[WS + o];
+        v = v + lds[2 * WS + o];
+        v = v + lds[3 * WS + o];
+        const int mm = m0 + 16 * (s >> 1) + row, nn = n0 + 16 * (s & 1) + col;
+        if (mm >= g.M || nn >= g.N) continue;
+        const size_t pidx = (size_t)mm * g.ldp + nn;
+        if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
+            st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
+            continue;
+        }
+        const float lr_t = adam_lr(ga.adam, g.group, es.t + 1);
+        const float gr = v * g.grad_scale;
+        const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+        const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
+        const float vv1 = e2[s] + (gr * gr - e2[s]) * (1.f - b2);
+        const float pn = e0[s] - (mm1 * lr_t) / (sqrtf(vv1) + eps);
+        st_out(&g.P[pidx], pn);
+        st_out(&g.P[pidx + ga.p_stride], mm1);
+        st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+        if (g.T != nullptr && polyak) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
+    }
+    GEMM_PH(4);
+    if (ga.ktime != nullptr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            ga.ktime[2 * ktime_wg()] = t0;
+            ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
 template <bool PK, bool T32>
 static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     const unsigned z = seeds_z(a.nseeds);
@@ -1452,6 +1753,17 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
+    if (a.dwl) {   // dW + Adam with LDS-staged rows: plain problems only (no fused rows, no alpha.final)
+        const dim3 grid(a.total_tiles, 1, seeds_z(a.nseeds)), block(256);
+        if (a.nseeds > 1) {
+            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, true>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_dwl<false, true>), grid, block, 0, s, a);
+        } else {
+            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, false>), grid, block, 0, s, a);
+            else hipLaunchKernelGGL((k_dwl<false, false>), grid, block, 0, s, a);
+        }
+        return;
+    }
     // 32x32 tiles: plain FWD / DX / DW launches only (the host never sets t32 elsewhere)
     const bool t32 = a.t32 && !(a.mode == GM_FWD && a.rowk == 3);
     if (a.nseeds > 1) {

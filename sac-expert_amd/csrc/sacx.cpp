@@ -148,6 +148,8 @@ struct sacx_handle {
     int pcap = 0;             // polar pairs per update (rng.pairs rows per update)
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
     int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
+    int dwl = 0;              // dW + Adam launches on k_dwl: 0 never, 1 when K >= 512, 2 always (SACX_DWL)
+    int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
@@ -486,7 +488,7 @@ double gemm_bytes(const GemmProb& p) {
 }
 
 void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name, std::vector<GemmProb> ps,
-              bool record_probs) {
+              bool record_probs, bool allow_dwl = true) {
     Launch L{};
     L.kind = Launch::GEMM;
     L.name = name;
@@ -494,9 +496,26 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     // (packed seeds: many tiles per launch); head-prologue and fused two-layer launches stay 16x16
     // (tile32 = 2: forward / dX launches only -- the dW + Adam epilogue's registers cost occupancy)
     bool t32 = h->tile32 > 0;
+    // tile32 = 2 keeps dW + Adam on 16x16 tiles (their registers cost occupancy), except a launch
+    // whose 16x16 tiles exceed what is resident at once (5 workgroups on each of 256 CUs): there
+    // the last tiles start a whole workgroup time late (Humanoid critic.adam: 1,378 tiles, 11 us
+    // of skew in a 23 us launch), and 32x32 tiles -- bit-identical sums -- run in one round
+    // (tools/dw_bench.hip: Humanoid critic.adam 23.7 -> 21.0 us fp32, 21.1 -> 14.3 us bf16)
+    int tiles16 = 0;
+    for (auto& p : ps) tiles16 += ((p.M + 15) / 16) * ((p.N + 15) / 16);
+    const bool dw_wide = tiles16 > h->dw_round_tiles;
     for (auto& p : ps)
-        t32 = t32 && p.headp == 0 && !(h->tile32 == 2 && p.epi == EPI_ADAM) && p.hbw == 0;
-    const int ts = t32 ? 32 : 16;
+        t32 = t32 && p.headp == 0 && !(h->tile32 == 2 && p.epi == EPI_ADAM && !dw_wide) && p.hbw == 0;
+    // dW + Adam launches with long reductions take k_dwl (32x32 tiles, LDS-DMA staged rows)
+    bool dwl = h->dwl > 0 && allow_dwl;   // not where rows ride along (the policy head rows)
+    int kmax = 0;
+    for (auto& p : ps) {
+        dwl = dwl && p.epi == EPI_ADAM;
+        kmax = std::max(kmax, (int)p.K);
+    }
+    dwl = dwl && (h->dwl == 2 || kmax >= 512);
+    if (dwl) t32 = false;
+    const int ts = (t32 || dwl) ? 32 : 16;
     int tiles = 0;
     for (auto& p : ps) {
         p.tiles_n = (p.N + ts - 1) / ts;
@@ -536,7 +555,17 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         p.vec = (mode != GM_DW && v_a && v_b && p.K >= 4) ? 1 : 0;
         vec = vec || p.vec;
     }
+    if (dwl) {
+        // 16-B row pieces need 16-B aligned rows in every seed's arena block
+        const bool sa = h->seeds <= 1 || h->seed_bytes % 16 == 0;
+        for (auto& p : ps) {
+            const bool a4 = sa && p.lda >= 4 && p.lda % 4 == 0 && (((uintptr_t)p.A) & 15) == 0;
+            const bool b4 = sa && p.ldb >= 4 && p.ldb % 4 == 0 && (((uintptr_t)p.B) & 15) == 0;
+            p.vec = (a4 ? 1 : 0) | (b4 ? 2 : 0);
+        }
+    }
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
+    L.gemm.dwl = dwl ? 1 : 0;
     L.gemm.mode = mode;
     L.gemm.vec = vec ? 1 : 0;
     for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
@@ -559,7 +588,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
 
 // Appends the problems of GEMM launch `b` to launch `a` (same mode; tile ranges follow a's).
 bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
-    if (a.mode != b.mode || a.t32 != b.t32 || a.nprob + b.nprob > GEMM_MAXP) return false;
+    if (a.mode != b.mode || a.t32 != b.t32 || a.dwl != b.dwl || a.nprob + b.nprob > GEMM_MAXP) return false;
     for (int i = 0; i < b.nprob; ++i) {
         GemmProb p = b.probs[i];
         p.tile_begin += a.total_tiles;
@@ -904,7 +933,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             pw.push_back(prob_dw(Hq2 + (size_t)(2 + k) * B * H1, H1, H1, B, W("ws.gq") + (size_t)k * B, 1,
                                  W(n + ".l2"), W(t + ".l2"), GRP_Q));
         }
-        add_gemm(h, plan, "critic.adam", pw, record_probs);
+        add_gemm(h, plan, "critic.adam", pw, record_probs, !fuse_head);
         if (fuse_head) {                    // the policy rows of actor.head (read from pi.q.fwd0 on)
             Launch& L = plan.back();
             HeadArgs a = head_fused;
@@ -1838,6 +1867,10 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->tile32 = t32_of((int64_t)h->seeds * h->B);
     h->tile32_plan = t32_of((int64_t)h->plan_seeds * h->B);
     if (const char* e = std::getenv("SACX_T32")) h->tile32 = h->tile32_plan = std::atoi(e);
+    // dW + Adam over >= 512 batch rows (Humanoid B = 1,024) on k_dwl: LDS-DMA staged 128-B row
+    // pieces instead of the fragment-shaped column loads, bit-identical results
+    if (const char* e = std::getenv("SACX_DWL")) h->dwl = std::atoi(e);
+    if (const char* e = std::getenv("SACX_DW_ROUND")) h->dw_round_tiles = std::atoi(e);
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
     // an expensive one (Humanoid: 52k normals, 146 us per update) keeps 4, where the graph's

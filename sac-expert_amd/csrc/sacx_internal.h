@@ -242,6 +242,8 @@ struct GemmArgs {
     int32_t xcd_map;       // 1: each XCD takes a contiguous tile range (see xcd_tile)
     int32_t bf16;          // 1: bf16 MFMA operands (rounded on load), fp32 accumulate (config C5)
     int32_t t32;           // 1: 32x32 output tiles per workgroup (tile_begin / tiles_n count those)
+    int32_t dwl;           // GM_DW: k_dwl (32x32 tiles, LDS-DMA staged rows; probs[].vec bit 0 / 1:
+                           // A / B rows by 16-B pieces)
     int64_t p_stride;      // floats between params / adam_m / adam_v blocks
     const Ctl* ctl;
     AdamConsts adam;
