@@ -1383,7 +1383,9 @@ __global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
 #ifndef SACX_DWL_NST
 #define SACX_DWL_NST 4    // slabs in flight per wave (LDS 4 waves x NST x 4.25 KB: 2 workgroups per CU)
 #endif
-#define DWL_STG 1088      // floats per slab stage: X [16][32], D [16][32], bscale [64] (16 used)
+// floats per slab stage: X [16][32], D [16][16 NH], bscale [64] (16 used)
+template <int NH>
+constexpr int dwl_stg() { return 512 + 256 * NH + 64; }
 
 typedef __attribute__((address_space(3))) void* lds_vp;
 __device__ __forceinline__ uint32_t lds_addr(const float* p) { return (uint32_t)(uintptr_t)(lds_vp)(p); }
@@ -1407,38 +1409,61 @@ __device__ __forceinline__ void glds(const float* g, uint32_t l0) {
 // fall into different banks
 __device__ __forceinline__ int dwl_sw(int row) { return ((row >> 2) & 1) << 4; }
 
-// one slab (rows k0 .. k0 + 15, columns c0 .. c0 + 31) of a row-major [K][ld] operand into the
-// LDS image [16][32] at byte address l0: V4 by 16-B pieces (ld % 4 == 0, 16-B aligned base: 2
-// instructions), else by dwords (8 instructions).  Rows past K and columns past the row repeat
-// valid elements; the reader masks them exactly where load_a / load_b read zeros.
-template <bool V4>
+// one slab (rows k0 .. k0 + 15, columns c0 .. c0 + NC - 1) of a row-major [K][ld] operand into
+// the LDS image at byte address l0: V4 by 16-B pieces (ld % 4 == 0, 16-B aligned base), else by
+// dwords.  NC = 32: image [16][32], columns swizzled by dwl_sw.  NC = 16: image [16][16] whose
+// row slot q holds row q ^ ((q >> 2) & 1) (rows 4-7, 12-15 swapped in pairs), the same bank split
+// for 64-B rows.  Rows past K and columns past the row repeat valid elements; the reader masks
+// them exactly where load_a / load_b read zeros.
+__device__ __forceinline__ int dwl_slot(int row) { return row ^ ((row >> 2) & 1); }
+template <bool V4, int NC>
 __device__ __forceinline__ void dwl_issue(const float* base, int ld, int k0, int K, int c0, uint32_t l0, int lane) {
-    if constexpr (V4) {
+    if constexpr (NC == 32) {
+        if constexpr (V4) {
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const int row = 8 * q + (lane >> 3);
-            const int col = min(c0 + (((lane & 7) << 2) ^ dwl_sw(row)), ld - 4);
-            const int k = min(k0 + row, K - 1);
-            glds<true>(base + (size_t)k * ld + col, l0 + q * 1024);
+            for (int q = 0; q < 2; ++q) {
+                const int row = 8 * q + (lane >> 3);
+                const int col = min(c0 + (((lane & 7) << 2) ^ dwl_sw(row)), ld - 4);
+                const int k = min(k0 + row, K - 1);
+                glds<true>(base + (size_t)k * ld + col, l0 + q * 1024);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int row = 2 * q + (lane >> 5);
+                const int col = min(c0 + ((lane & 31) ^ dwl_sw(row)), ld - 1);
+                const int k = min(k0 + row, K - 1);
+                glds<false>(base + (size_t)k * ld + col, l0 + q * 256);
+            }
         }
     } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            const int row = 2 * q + (lane >> 5);
-            const int col = min(c0 + ((lane & 31) ^ dwl_sw(row)), ld - 1);
+        if constexpr (V4) {
+            const int row = dwl_slot(lane >> 2);
+            const int col = min(c0 + ((lane & 3) << 2), ld - 4);
             const int k = min(k0 + row, K - 1);
-            glds<false>(base + (size_t)k * ld + col, l0 + q * 256);
+            glds<true>(base + (size_t)k * ld + col, l0);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = dwl_slot(4 * q + (lane >> 4));
+                const int col = min(c0 + (lane & 15), ld - 1);
+                const int k = min(k0 + row, K - 1);
+                glds<false>(base + (size_t)k * ld + col, l0 + q * 256);
+            }
         }
     }
 }
 
-template <bool BF, bool PK>
+// NH: 16-column halves per tile -- 2: 32x32 tiles, 1: 32x16 (twice the workgroups, two or three
+// per CU: more waves per SIMD to hide each slab's non-MFMA instructions)
+template <bool BF, bool PK, int NH>
 __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
+    constexpr int STG = dwl_stg<NH>(), NS = 2 * NH;     // stage floats; sub-tiles per thread
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SACX_GEMM_PHASES
     if (threadIdx.x == 0) g_gemm_ph[blockIdx.x][0] = t0;
 #endif
-    __shared__ float lds[4 * SACX_DWL_NST * DWL_STG];    // the one LDS object (staging, then reduction)
+    __shared__ float lds[4 * SACX_DWL_NST * STG];    // the one LDS object (staging, then reduction)
     const int64_t so = PK ? seed_off(ga.sstride) : 0;
     const int total_tiles = ga.total_tiles, xcd_map = ga.xcd_map, nprob = ga.nprob;
     int tb[GEMM_MAXP];
@@ -1460,17 +1485,17 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
     reloc(g, so);
     const int lt = tile - g.tile_begin;
     const int tm = lt / g.tiles_n, tn = lt - tm * g.tiles_n;
-    const int m0 = tm * 32, n0 = tn * 32;
+    const int m0 = tm * 32, n0 = tn * 16 * NH;
     const int wave = wave_id(), lane = threadIdx.x & 63;     // wave uniform: the slab loop is scalar
     const int r = lane & 15, grp = lane >> 4;
     const int t = threadIdx.x, row = t >> 4, col = t & 15;
 
-    // ---- epilogue operands of this thread's four outputs first (sub-tile s = 2 i + j: rows
-    // +16 i, cols +16 j), as gemm_tile32
-    float e0[4], e1[4], e2[4], e3[4];
+    // ---- epilogue operands of this thread's outputs first (sub-tile s = NH i + j: rows +16 i,
+    // cols +16 j), as gemm_tile32
+    float e0[NS], e1[NS], e2[NS], e3[NS];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int mm = m0 + 16 * (s >> 1) + row, nn = n0 + 16 * (s & 1) + col;
+    for (int s = 0; s < NS; ++s) {
+        const int mm = m0 + 16 * (s / NH) + row, nn = n0 + 16 * (s % NH) + col;
         const size_t pidx = (size_t)min(mm, g.M - 1) * g.ldp + min(nn, g.N - 1);
 #ifdef SACX_DWL_NOEPI       // diagnostic builds: no epilogue operand loads
         e0[s] = e1[s] = e2[s] = e3[s] = (float)pidx;
@@ -1487,7 +1512,7 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
     const int per = (nIt + 3) >> 2;
     const int it0 = wave * per;
     const int n = max(0, min(nIt, it0 + per) - it0);      // this wave's slabs (uniform per wave)
-    float* wl = lds + wave * (SACX_DWL_NST * DWL_STG);
+    float* wl = lds + wave * (SACX_DWL_NST * STG);
     const uint32_t wl_addr = __builtin_amdgcn_readfirstlane(lds_addr(wl));
     // Operand values.  Rows past M and columns past N of a tile only feed outputs that are never
     // stored, so they need no masking; the bias-gradient row (m == ones_row) takes 1.0 for X, and
@@ -1498,17 +1523,17 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
     for (int h = 0; h < 2; ++h) isone[h] = m0 + 16 * h + r == g.ones_row;
     // lane (r, grp) reads rows 4 grp + j: its swizzle is dwl_sw(4 grp + j) = 16 (grp & 1)
     const int sx = 16 * (grp & 1);
-    floatx4 acc0[4], acc1[4];
+    floatx4 acc0[NS], acc1[NS];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NS; ++s) {
         acc0[s] = floatx4{0.f, 0.f, 0.f, 0.f};
         acc1[s] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     // the raw LDS values of one slab in this lane's MFMA layout (X, D, bscale)
-    struct Slab { float x[2][4], d[2][4], bs[4]; };
+    struct Slab { float x[2][4], d[NH][4], bs[4]; };
     auto read_slab = [&](int i, Slab& v) {
-        const float* st = wl + (i % SACX_DWL_NST) * DWL_STG;
-        const float4 b4 = *reinterpret_cast<const float4*>(st + 1024 + 4 * grp);
+        const float* st = wl + (i % SACX_DWL_NST) * STG;
+        const float4 b4 = *reinterpret_cast<const float4*>(st + 512 + 256 * NH + 4 * grp);
         v.bs[0] = b4.x; v.bs[1] = b4.y; v.bs[2] = b4.z; v.bs[3] = b4.w;
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -1516,22 +1541,23 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
             for (int h = 0; h < 2; ++h) {
                 const int o = (4 * grp + j) * 32 + ((16 * h) ^ sx) + r;
                 v.x[h][j] = st[o];
-                v.d[h][j] = st[512 + o];
+                if constexpr (NH == 2) v.d[h][j] = st[512 + o];
+                else if (h == 0) v.d[0][j] = st[512 + dwl_slot(4 * grp + j) * 16 + r];
             }
     };
     auto body = [&](auto xv, auto dv) {
         constexpr bool XV = decltype(xv)::value, DV = decltype(dv)::value;
-        constexpr int G = (XV ? 2 : 8) + (DV ? 2 : 8) + 1;      // LDS-DMA instructions per slab
+        constexpr int G = (XV ? 2 : 8) + (DV ? NH : 4 * NH) + 1;      // LDS-DMA instructions per slab
         constexpr int NST = SACX_DWL_NST;
         auto issue = [&](int i) {
 #ifdef SACX_DWL_NOLOAD      // diagnostic builds (tools/dw_bench.hip): the loop without its loads
             return;
 #endif
-            const uint32_t st = wl_addr + (uint32_t)((i % NST) * DWL_STG * 4);
+            const uint32_t st = wl_addr + (uint32_t)((i % NST) * STG * 4);
             const int k0 = (it0 + i) * 16;
-            dwl_issue<XV>(g.A, g.lda, k0, g.K, m0, st, lane);
-            dwl_issue<DV>(g.B, g.ldb, k0, g.K, n0, st + 2048, lane);
-            glds<false>(g.bscale + min(k0 + (lane & 15), g.K - 1), st + 4096);
+            dwl_issue<XV, 32>(g.A, g.lda, k0, g.K, m0, st, lane);
+            dwl_issue<DV, 16 * NH>(g.B, g.ldb, k0, g.K, n0, st + 2048, lane);
+            glds<false>(g.bscale + min(k0 + (lane & 15), g.K - 1), st + 2048 + 1024 * NH);
         };
         if (n == 0) return;
 #pragma unroll
@@ -1547,9 +1573,10 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
         asm volatile("" ::"v"(cur.x[0][0]), "v"(cur.x[0][1]), "v"(cur.x[0][2]), "v"(cur.x[0][3]), "v"(cur.x[1][0]),
                      "v"(cur.x[1][1]), "v"(cur.x[1][2]), "v"(cur.x[1][3]), "v"(cur.bs[0]), "v"(cur.bs[1]),
                      "v"(cur.bs[2]), "v"(cur.bs[3]));
-        asm volatile("" ::"v"(cur.d[0][0]), "v"(cur.d[0][1]), "v"(cur.d[0][2]), "v"(cur.d[0][3]), "v"(cur.d[1][0]),
-                     "v"(cur.d[1][1]), "v"(cur.d[1][2]), "v"(cur.d[1][3]));
-        float pa[2][4], pb[2][4];      // bf16: the even slab of the pair
+#pragma unroll
+        for (int h = 0; h < NH; ++h)
+            asm volatile("" ::"v"(cur.d[h][0]), "v"(cur.d[h][1]), "v"(cur.d[h][2]), "v"(cur.d[h][3]));
+        float pa[2][4], pb[NH][4];     // bf16: the even slab of the pair
         for (int i = 0; i < n; ++i) {
             // Slab i's values are in registers.  Refill the stage slab i - 1 left (its reads
             // retired), wait for slab i + 1 and request its values, then multiply slab i: the
@@ -1563,15 +1590,14 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
             }
             if (i + 1 < n) read_slab(i + 1, nxt);
             const int kb = (it0 + i) * 16 + 4 * grp;
-            float a[2][4], b[2][4];
+            float a[2][4], b[NH][4];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float sc = kb + j < g.K ? cur.bs[j] : 0.f;
 #pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    a[h][j] = isone[h] ? 1.f : cur.x[h][j];
-                    b[h][j] = cur.d[h][j] * sc;
-                }
+                for (int h = 0; h < 2; ++h) a[h][j] = isone[h] ? 1.f : cur.x[h][j];
+#pragma unroll
+                for (int h = 0; h < NH; ++h) b[h][j] = cur.d[h][j] * sc;
             }
             if constexpr (BF) {
                 // slab pairs (it0 + 2q, it0 + 2q + 1), alternately into acc0 / acc1 (gemm_core's
@@ -1579,20 +1605,23 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
                 const bool last = i == n - 1;
                 if ((i & 1) == 0 && !last) {
 #pragma unroll
-                    for (int h = 0; h < 2; ++h)
+                    for (int j = 0; j < 4; ++j) {
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) { pa[h][j] = a[h][j]; pb[h][j] = b[h][j]; }
+                        for (int h = 0; h < 2; ++h) pa[h][j] = a[h][j];
+#pragma unroll
+                        for (int h = 0; h < NH; ++h) pb[h][j] = b[h][j];
+                    }
                 } else {
                     const bool odd = (i & 1) != 0;
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) {
+                    for (int s = 0; s < NS; ++s) {
                         float a0[4], a1[4], b0[4], b1[4];
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
-                            a0[j] = odd ? pa[s >> 1][j] : a[s >> 1][j];
-                            a1[j] = odd ? a[s >> 1][j] : 0.f;
-                            b0[j] = odd ? pb[s & 1][j] : b[s & 1][j];
-                            b1[j] = odd ? b[s & 1][j] : 0.f;
+                            a0[j] = odd ? pa[s / NH][j] : a[s / NH][j];
+                            a1[j] = odd ? a[s / NH][j] : 0.f;
+                            b0[j] = odd ? pb[s % NH][j] : b[s % NH][j];
+                            b1[j] = odd ? b[s % NH][j] : 0.f;
                         }
                         if ((i >> 1) & 1) acc1[s] = mfma_bf16_2slab(a0, a1, b0, b1, acc1[s]);
                         else acc0[s] = mfma_bf16_2slab(a0, a1, b0, b1, acc0[s]);
@@ -1605,9 +1634,9 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int s = 0; s < 4; ++s) {
-                        if (j & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s >> 1][j], b[s & 1][j], acc1[s], 0, 0, 0);
-                        else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s >> 1][j], b[s & 1][j], acc0[s], 0, 0, 0);
+                    for (int s = 0; s < NS; ++s) {
+                        if (j & 1) acc1[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s / NH][j], b[s % NH][j], acc1[s], 0, 0, 0);
+                        else acc0[s] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s / NH][j], b[s % NH][j], acc0[s], 0, 0, 0);
                     }
 #endif
             }
@@ -1624,7 +1653,7 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
     GEMM_PH(2);
     // reduction through the wave's own (retired) staging: sub-tile s of wave w at wl + s * 256
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NS; ++s) {
         const floatx4 acc = acc0[s] + acc1[s];
 #pragma unroll
         for (int q = 0; q < 4; ++q) wl[s * 256 + q * 64 + lane] = acc[q];
@@ -1636,14 +1665,14 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
                         (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
     const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
     const bool polyak = nts % tui == 0;
-    constexpr int WS = SACX_DWL_NST * DWL_STG;
+    constexpr int WS = SACX_DWL_NST * STG;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < NS; ++s) {
         const int o = s * 256 + R * 64 + L;
         float v = lds[o] + lds[WS + o];
         v = v + lds[2 * WS + o];
         v = v + lds[3 * WS + o];
-        const int mm = m0 + 16 * (s >> 1) + row, nn = n0 + 16 * (s & 1) + col;
+        const int mm = m0 + 16 * (s / NH) + row, nn = n0 + 16 * (s % NH) + col;
         if (mm >= g.M || nn >= g.N) continue;
         const size_t pidx = (size_t)mm * g.ldp + nn;
         if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
@@ -1755,13 +1784,19 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
     if (a.dwl) {   // dW + Adam with LDS-staged rows: plain problems only (no fused rows, no alpha.final)
         const dim3 grid(a.total_tiles, 1, seeds_z(a.nseeds)), block(256);
-        if (a.nseeds > 1) {
-            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, true>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_dwl<false, true>), grid, block, 0, s, a);
-        } else {
-            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, false>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_dwl<false, false>), grid, block, 0, s, a);
-        }
+#define SACX_DWLL(NH)                                                                                  \
+    do {                                                                                              \
+        if (a.nseeds > 1) {                                                                           \
+            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, true, NH>), grid, block, 0, s, a);            \
+            else hipLaunchKernelGGL((k_dwl<false, true, NH>), grid, block, 0, s, a);                  \
+        } else {                                                                                      \
+            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, false, NH>), grid, block, 0, s, a);           \
+            else hipLaunchKernelGGL((k_dwl<false, false, NH>), grid, block, 0, s, a);                 \
+        }                                                                                             \
+    } while (0)
+        if (a.dwl == 2) SACX_DWLL(1);      // 32x16 tiles
+        else SACX_DWLL(2);                 // 32x32 tiles
+#undef SACX_DWLL
         return;
     }
     // 32x32 tiles: plain FWD / DX / DW launches only (the host never sets t32 elsewhere)

@@ -149,6 +149,7 @@ struct sacx_handle {
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
     int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
     int dwl = 0;              // dW + Adam launches on k_dwl: 0 never, 1 when K >= 512, 2 always (SACX_DWL)
+    int dwl_nh = 1;           // k_dwl tile width in 16-column halves (SACX_DWL_NH: 1 -> 32x16, 2 -> 32x32)
     int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
@@ -516,9 +517,10 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     dwl = dwl && (h->dwl == 2 || kmax >= 512);
     if (dwl) t32 = false;
     const int ts = (t32 || dwl) ? 32 : 16;
+    const int tsn = dwl ? 16 * h->dwl_nh : ts;    // k_dwl: 32 x 16 NH tiles
     int tiles = 0;
     for (auto& p : ps) {
-        p.tiles_n = (p.N + ts - 1) / ts;
+        p.tiles_n = (p.N + tsn - 1) / tsn;
         p.tile_begin = tiles;
         tiles += ((p.M + ts - 1) / ts) * p.tiles_n;
         L.flops += gemm_flops(p);
@@ -565,7 +567,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         }
     }
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
-    L.gemm.dwl = dwl ? 1 : 0;
+    L.gemm.dwl = dwl ? (h->dwl_nh == 1 ? 2 : 1) : 0;    // 2: 32x16 tiles, 1: 32x32
     L.gemm.mode = mode;
     L.gemm.vec = vec ? 1 : 0;
     for (size_t i = 0; i < ps.size(); ++i) L.gemm.probs[i] = ps[i];
@@ -1871,6 +1873,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // pieces instead of the fragment-shaped column loads, bit-identical results
     if (const char* e = std::getenv("SACX_DWL")) h->dwl = std::atoi(e);
     if (const char* e = std::getenv("SACX_DW_ROUND")) h->dw_round_tiles = std::atoi(e);
+    if (const char* e = std::getenv("SACX_DWL_NH")) h->dwl_nh = std::atoi(e) == 2 ? 2 : 1;
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
     // an expensive one (Humanoid: 52k normals, 146 us per update) keeps 4, where the graph's

@@ -1,5 +1,6 @@
 """dW + Adam tilings: the 16x16 k_gemm tiles, 32x32 tiles for launches past one round of
-residency (SACX_DW_ROUND) and k_dwl (LDS-DMA staged rows, SACX_DWL) keep gemm_core's
+residency (SACX_DW_ROUND) and k_dwl (LDS-DMA staged rows, SACX_DWL; 32x16 or 32x32 tiles,
+SACX_DWL_NH) keep gemm_core's
 summation order, so a learner ends bit-identical whichever the plan takes (stats, every
 parameter / Adam / target value).  B = 128 runs k_dwl's short path (2 slabs per wave, fewer
 than its stages); B = 1024 its steady-state pipeline."""
@@ -11,7 +12,7 @@ from helpers import load_learner, make_learner
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("variant", ["dwl", "round"])
+@pytest.mark.parametrize("variant", ["dwl32x16", "dwl32x32", "round"])
 @pytest.mark.parametrize("B", [128, 1024])
 @pytest.mark.parametrize("bf16", [False, True])
 @pytest.mark.parametrize("use_expert", [False, True])
@@ -42,7 +43,10 @@ def test_dw_tilings_bit_identical(monkeypatch, variant, B, bf16, use_expert):
         return out
 
     ref = run({"SACX_DWL": "0", "SACX_DW_ROUND": "100000000"})
-    got = run({"SACX_DWL": "2"} if variant == "dwl" else {"SACX_DWL": "0", "SACX_DW_ROUND": "1"})
+    if variant.startswith("dwl"):
+        got = run({"SACX_DWL": "2", "SACX_DWL_NH": "1" if variant == "dwl32x16" else "2"})
+    else:
+        got = run({"SACX_DWL": "0", "SACX_DW_ROUND": "1"})
     assert np.all(np.isfinite(ref[0]))
     for i, (a, b) in enumerate(zip(got, ref)):
         assert np.array_equal(a, b), (variant, i, int(np.sum(a != b)))

@@ -88,15 +88,15 @@ int main(int argc, char** argv) {
     actor.push_back({Ha1, 256, 256, Da2, 256, 256, ones, po, 256}); po += 257 * 256;
     actor.push_back({Ha2, 256, 256, Da3, 34, 34, ones, po, 256}); po += 257 * 34;
     actor.push_back({E, 1, 0, E, 17, 17, ones, po, 0}); po += 17;
-    auto args = [&](const std::vector<Op>& ops, int variant, bool bf) {   // 0: 16x16, 1: T32, 2: dwl
+    auto args = [&](const std::vector<Op>& ops, int variant, bool bf) {   // 0: 16x16, 1: T32, 2: dwl 32x32, 3: dwl 32x16
         GemmArgs ga{};
-        const int ts = variant ? 32 : 16;
+        const int ts = variant ? 32 : 16, tsn = variant == 3 ? 16 : ts;
         int tiles = 0;
         for (size_t i = 0; i < ops.size(); ++i) {
             GemmProb p = prob(ops[i]);
-            p.tiles_n = (p.N + ts - 1) / ts; p.tile_begin = tiles;
+            p.tiles_n = (p.N + tsn - 1) / tsn; p.tile_begin = tiles;
             tiles += ((p.M + ts - 1) / ts) * p.tiles_n;
-            if (variant == 2) {
+            if (variant >= 2) {
                 const bool a4 = p.lda >= 4 && p.lda % 4 == 0 && (((uintptr_t)p.A) & 15) == 0;
                 const bool b4 = p.ldb >= 4 && p.ldb % 4 == 0 && (((uintptr_t)p.B) & 15) == 0;
                 p.vec = (a4 ? 1 : 0) | (b4 ? 2 : 0);
@@ -104,28 +104,29 @@ int main(int argc, char** argv) {
             ga.probs[i] = p;
         }
         ga.nprob = (int)ops.size(); ga.mode = GM_DW; ga.total_tiles = tiles; ga.xcd_map = 1;
-        ga.t32 = variant == 1; ga.dwl = variant == 2; ga.bf16 = bf; ga.p_stride = PS; ga.ctl = ctl;
+        ga.t32 = variant == 1; ga.dwl = variant == 2 ? 1 : variant == 3 ? 2 : 0; ga.bf16 = bf; ga.p_stride = PS; ga.ctl = ctl;
         ga.adam.lr[0] = 3e-4f; ga.adam.tau_keep = 0.995f; ga.adam.tau_take = 0.005f; ga.adam.target_update_int = 1;
         return ga;
     };
-    const char* vn[3] = {"16x16", "t32  ", "dwl  "};
+    const char* vn[4] = {"16x16", "t32  ", "dwl  ", "dwl16"};
     for (int bf = 0; bf < 2; ++bf)
         for (int set = 0; set < 2; ++set) {
             const auto& ops = set ? actor : critic;
-            std::vector<float> out[5];
-            for (int v = 0; v < 5; ++v) {      // 3: 16x16 again, 4: 16x16 without the XCD map
+            std::vector<float> out[6];
+            for (int v = 0; v < 6; ++v) {      // 3: 16x16 again, 4: 16x16 without the XCD map, 5: dwl 32x16
                 CK(hipMemcpy(P, P0, 4 * PS * 4, hipMemcpyDeviceToDevice));
                 CK(hipDeviceSynchronize());
-                GemmArgs ga = args(ops, v < 3 ? v : 0, bf);
+                GemmArgs ga = args(ops, v < 3 ? v : v == 5 ? 3 : 0, bf);
                 if (v == 4) ga.xcd_map = 0;
                 launch_gemm(ga, s);
                 CK(hipStreamSynchronize(s));
                 out[v].resize(4 * PS);
                 CK(hipMemcpy(out[v].data(), P, 4 * PS * 4, hipMemcpyDeviceToHost));
             }
-            const int pairs[5][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}, {0, 4}};
-            const char* pn[5] = {"16x16 vs t32", "16x16 vs dwl", "t32 vs dwl", "16x16 vs 16x16 again", "16x16 vs 16x16 no xcd"};
-            for (int q = 0; q < 5; ++q) {
+            const int pairs[6][2] = {{0, 1}, {0, 2}, {1, 2}, {0, 3}, {0, 4}, {0, 5}};
+            const char* pn[6] = {"16x16 vs t32", "16x16 vs dwl", "t32 vs dwl", "16x16 vs 16x16 again", "16x16 vs 16x16 no xcd",
+                                 "16x16 vs dwl 32x16"};
+            for (int q = 0; q < 6; ++q) {
                 const auto& x = out[pairs[q][0]];
                 const auto& y = out[pairs[q][1]];
                 size_t diff = 0, first = 0;
@@ -135,7 +136,7 @@ int main(int argc, char** argv) {
                        diff ? "" : " (bit-identical)\n");
                 if (diff) printf(" first at %zu: %a vs %a (P0 %s)\n", first, x[first], y[first], "");
             }
-            for (int v = 0; v < 3; ++v) {
+            for (int v = 0; v < 4; ++v) {
                 GemmArgs ga = args(ops, v, bf);
                 {   // per-workgroup start / end stamps (100 MHz) of one launch
                     static uint64_t* kt = nullptr;
@@ -153,7 +154,7 @@ int main(int argc, char** argv) {
                         smax = std::max(smax, h[2 * b]);
                     }
 #ifdef SACX_GEMM_PHASES
-                    if (v == 2) {
+                    if (v >= 2) {
                         static unsigned long long ph[8192][5];
                         CK(hipMemcpyFromSymbol(ph, HIP_SYMBOL(g_gemm_ph), sizeof(ph)));
                         double d[4] = {0, 0, 0, 0};

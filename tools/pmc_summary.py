@@ -1,8 +1,13 @@
 """Summarise rocprofv3 PMC passes (tools/gpu_pmc.sh) into profiles/pmc_<config>.json.
 
 Per kernel family: mean over dispatches of FETCH_SIZE and WRITE_SIZE (KB), and
-traffic_bytes_per_launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 -- on gfx950
-FETCH_SIZE counts 128-B requests at 64 B (MI355X_MICROARCH.md, section HBM).
+traffic_bytes_per_launch = (f * FETCH_SIZE + WRITE_SIZE) * 1024.  The factor f depends on the
+access shape (tools/fetch_calib.hip, profiles/r03_fetch_calib_v1.txt: each shape reading a fresh
+64 MiB once): FETCH_SIZE reports 0.50x the bytes of coalesced streaming reads (16 B or 4 B per
+lane, 1 KiB / 256 B per wave-instruction; MI355X_MICROARCH.md, section HBM) but 1.00x for
+k_gemm's MFMA-fragment loads (16 lanes x 4 B = one 64-B piece of a row, 4 rows per
+instruction).  So f = 1 for k_gemm (its operand and epilogue loads are all 64-B row pieces),
+f = 2 for the row-streaming kernels.
 Families follow sacx kernel names (template arguments folded: k_gemm<1, 1> -> k_gemm;
 k_gemm_head -> k_gemm).
 usage: python tools/pmc_summary.py gpurun_out/pmc hc [source-tag] [extra-copy-path]
@@ -53,7 +58,9 @@ def main():
         k = {c: sum(v) / len(v) for c, v in cs.items()}
         k["dispatches"] = max(len(v) for v in cs.values())
         if "FETCH_SIZE" in k and "WRITE_SIZE" in k:
-            k["traffic_bytes_per_launch"] = (2.0 * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0
+            f = 1.0 if fam.startswith("k_gemm") else 2.0
+            k["fetch_factor"] = f
+            k["traffic_bytes_per_launch"] = (f * k["FETCH_SIZE"] + k["WRITE_SIZE"]) * 1024.0
         out["kernels"][fam] = k
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     path = os.path.join(root, "profiles", f"pmc_{config}.json")
