@@ -1973,8 +1973,7 @@ __device__ __forceinline__ uint32_t rng_word(const RngShared& S, int q) {
     return S.ring[(unsigned)q & (RNG_RW - 1u)];
 }
 
-__global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
-    __shared__ RngShared S;
+__device__ __forceinline__ void rng_body(const RngArgs& a_in, RngShared& S) {
     RngArgs a = a_in;
     {
         const int64_t so = seed_off(a_in.sstride);
@@ -2164,6 +2163,11 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a_in) {
             a.ctl->rng_seq = seq + a.nupd;
         }
     }
+}
+
+__global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
+    __shared__ RngShared S;
+    rng_body(a, S);
 }
 
 // The polar transform of the pairs k_rng accepted (legacy_gauss, mtrand): one thread per pair of
@@ -2550,11 +2554,18 @@ __device__ __forceinline__ void act_tail(const ActRowArgs& g, const float* outs,
 // its normaliser, all the weights this thread multiplies (<= 32 of W0, <= 64 of W1, <= 4 of W3),
 // the biases, logstd and the noise -- is requested before the first barrier, so the row costs
 // one memory round trip instead of one per layer.  Same FMA order as the generic path.
+struct ActShared {
+    float xs[ACT_ROWS_DIM], h1s[ACT_ROWS_DIM], h2s[ACT_ROWS_DIM];
+    float part[4][ACT_ROWS_DIM];
+    float outs[64];
+};
 template <bool PF>
-__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g_in) {
-    __shared__ float xs[ACT_ROWS_DIM], h1s[ACT_ROWS_DIM], h2s[ACT_ROWS_DIM];
-    __shared__ float part[4][ACT_ROWS_DIM];
-    __shared__ float outs[64];
+__device__ __forceinline__ void act_rows_body(const ActRowArgs& g_in, const int row, ActShared& L) {
+    float(&xs)[ACT_ROWS_DIM] = L.xs;
+    float(&h1s)[ACT_ROWS_DIM] = L.h1s;
+    float(&h2s)[ACT_ROWS_DIM] = L.h2s;
+    float(&part)[4][ACT_ROWS_DIM] = L.part;
+    float(&outs)[64] = L.outs;
     ActRowArgs g = g_in;
     if (g_in.nseeds > 1) {          // packed seeds: seed z's weights, normaliser and noise; its rows
         const int64_t so = seed_off(g_in.sstride);
@@ -2563,7 +2574,7 @@ __global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g_in) {
         g.obs = g.obs + (size_t)blockIdx.z * g.m * g.S;
         g.out = g.out + (size_t)blockIdx.z * g.m * g.A;
     }
-    const int t = threadIdx.x, row = blockIdx.x, lane = t & 63, wave = t >> 6;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
     const int S = g.S, A = g.A, Aout = g.Aout;
     const bool jok = wave == 0 && lane < A;
     if constexpr (PF) {
@@ -2647,11 +2658,43 @@ __global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g_in) {
     act_tail(g, outs, row, lane, ls, u);
 }
 
+template <bool PF>
+__global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
+    __shared__ ActShared L;
+    act_rows_body<PF>(g, blockIdx.x, L);
+}
+
+// The drop-in loop's deterministic act with the next update's sampler draw beside it: the
+// action rows are workgroups 0 .. m - 1 and k_rng's draw is workgroup m, so the draw (one CU,
+// ~13 us at HC shapes) runs while the rows run instead of after them.  One LDS image, either
+// role's.  (A deterministic act reads no randoms: the two are independent.)
+union ActRngShared {
+    RngShared r;
+    ActShared a;
+};
+template <bool PF>
+__global__ __launch_bounds__(1024) void k_act_rng(ActRowArgs g, RngArgs r) {
+    __shared__ ActRngShared U;
+    if (blockIdx.x + 1 < gridDim.x) act_rows_body<PF>(g, blockIdx.x, U.a);
+    else rng_body(r, U.r);
+}
+
+
 void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s) {
     const bool pf = a.S <= 128 && a.H0 <= 256 && a.H1 <= 256 && a.Aout <= 16;
     const dim3 grid(m, 1, seeds_z(a.nseeds));
     if (pf) hipLaunchKernelGGL(k_act_rows<true>, grid, dim3(1024), 0, s, a);
     else hipLaunchKernelGGL(k_act_rows<false>, grid, dim3(1024), 0, s, a);
+}
+
+void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s) {
+    const bool pf = a.S <= 128 && a.H0 <= 256 && a.H1 <= 256 && a.Aout <= 16;
+    const dim3 grid(m + 1, 1, seeds_z(a.nseeds));
+    if (pf) hipLaunchKernelGGL(k_act_rng<true>, grid, dim3(1024), 0, s, a, r);
+    else hipLaunchKernelGGL(k_act_rng<false>, grid, dim3(1024), 0, s, a, r);
+    if (r.pairs != nullptr && r.n_norm > 0)     // the split sampler's polar transform, as launch_rng
+        hipLaunchKernelGGL(k_polar, dim3(std::min((r.pcap + 255) / 256, SACX_POLAR_WGS), r.nupd, seeds_z(r.nseeds)),
+                           dim3(256), 0, s, r);
 }
 
 // ==================================================================== k_qhead

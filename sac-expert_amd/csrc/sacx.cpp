@@ -194,6 +194,7 @@ struct sacx_handle {
     int64_t cur_size_host = 0; // mirrors ctl->cur_size (appends, resync)
     int64_t n_appends = 0;     // sacx_buffer_append calls (a full ring changes content, not size)
     int64_t spec_appends = 0;  // n_appends when the speculative draw was queued
+    bool act_rng = true;       // deterministic act + speculative draw in one launch (k_act_rng; SACX_ACT_RNG=0: two)
     hipEvent_t act_ev = nullptr;   // end of the last act_host kernel chain (its actions are on the host)
 
     uint64_t add(const std::string& name, int64_t rows, int64_t cols, int dtype, int role) {
@@ -1909,6 +1910,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     HIPCHK(h, hipStreamCreateWithFlags(&h->rng_stream, hipStreamNonBlocking));
     HIPCHK(h, hipEventCreateWithFlags(&h->act_ev, hipEventDisableTiming));
     if (const char* e = std::getenv("SACX_SPEC")) h->spec_enabled = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SACX_ACT_RNG")) h->act_rng = std::atoi(e) != 0;
     h->cur_size_host = 0;
     h->bound = true;
     return 0;
@@ -2072,7 +2074,7 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
 // The speculative draw (see sacx_handle::spec_live): the sampler launch of slot 1 or 2 for one
 // update at the ring's current size, queued on the bound stream; it saves the state it starts
 // from into "rng.spec" for spec_cancel.
-static int spec_draw(sacx_handle* h) {
+static int spec_rng_args(sacx_handle* h, RngArgs* out) {
     const int slot = h->alpha_pending == 1 ? 2 : 1;    // not the slot a deferred alpha branch reads
     const Launch* R = nullptr;
     for (const Launch& L : h->plan[slot])
@@ -2086,9 +2088,15 @@ static int spec_draw(sacx_handle* h) {
     r.nupd = 1;
     r.size_fixed = 0;           // each seed's ring size, read on the device (final until the update)
     r.backup = reinterpret_cast<RngState*>(h->arena0 + h->off_of("rng.spec"));   // seed 0's (relocated per seed)
-    launch_rng(r, h->stream);
-    if (!h->cfg.use_expert)      // plain SAC: the gather too (SAC-EO's reads the permutation the
-        for (const Launch& L : h->plan[slot])   // caller pushes before the update)
+    *out = r;
+    return 0;
+}
+
+// after the speculative sampler launch: plain SAC's gather too (SAC-EO's reads the permutation the
+// caller pushes before the update), and the draw's bookkeeping
+static int spec_after_rng(sacx_handle* h) {
+    if (!h->cfg.use_expert)
+        for (const Launch& L : h->plan[h->spec_slot])
             if (L.kind == Launch::GATHER) enqueue(L, h, h->stream);
     HIPCHK(h, hipGetLastError());
     h->spec_live = true;
@@ -2097,25 +2105,65 @@ static int spec_draw(sacx_handle* h) {
     return 0;
 }
 
+static int spec_draw(sacx_handle* h) {
+    RngArgs r;
+    if (spec_rng_args(h, &r)) return -1;
+    launch_rng(r, h->stream);
+    return spec_after_rng(h);
+}
+
+// k_act_rows' arguments for n <= ACT_ROWS_MAX observation rows of the selected seed
+static ActRowArgs act_rows_args(sacx_handle* h, const float* obs, float* noise, float* act_out) {
+    ActRowArgs a{};
+    a.obs = obs; a.s_mean = h->f("norm.s_mean"); a.s_den = h->f("norm.s_den");
+    a.W0 = h->f("actor.l0"); a.W1 = h->f("actor.l1"); a.W3 = h->f("actor.l2"); a.logstd = h->f("actor.logstd");
+    a.noise = noise; a.out = act_out;
+    a.S = h->S; a.A = h->A; a.Aout = h->Aout; a.H0 = h->H0; a.H1 = h->H1;
+    a.act0 = h->aact[0]; a.act1 = h->aact[1];
+    a.mode = h->cfg.actor_gaussian ? 2 : 1;
+    a.per_state_std = h->cfg.per_state_std;
+    a.lim = h->cfg.act_limit;
+    if (h->cfg.actor_gaussian) {          // logstd_init (continuous_actors.py:39-44), f32
+        const double sm = h->cfg.actor_std_mult > 0.f ? h->cfg.actor_std_mult : 1.0;
+        a.logstd_init = (float)(std::log(sm) - (h->cfg.per_state_std ? std::log(std::log(2.0)) : 0.0));
+        a.output_norm = h->cfg.actor_output_norm;
+    }
+    return a;
+}
+static bool act_rows_ok(const sacx_handle* h, int64_t n) {
+    return n > 0 && n <= ACT_ROWS_MAX && !h->ln && h->S <= ACT_ROWS_DIM && h->H0 <= ACT_ROWS_DIM &&
+           h->H1 <= ACT_ROWS_DIM && h->Aout <= 64;
+}
+
 int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A;
     const int64_t chunk = std::min<int64_t>(ACT_CAP, STAGE_CAP / (S + A));
     if (chunk <= 0) return fail(h, "an observation row is larger than the pinned staging buffer (use sacx_actor_act)");
+    const bool spec = h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0;
     for (int64_t done = 0; done < n; done += chunk) {
         const int64_t m = std::min(chunk, n - done);
         if (stage_alloc(h)) return -1;
         float* p = h->pin + STAGE_CAP;          // the act half: its last reader was a synchronous act
         const float* g = h->pin_dev + STAGE_CAP;
         std::memcpy(p, obs + done * S, sizeof(float) * m * S);
+        if (spec && deterministic && h->act_rng && done + m >= n && act_rows_ok(h, m)) {
+            // the drop-in loop's act with the next update's draw beside the rows (k_act_rng)
+            RngArgs r;
+            if (spec_rng_args(h, &r)) return -1;
+            launch_act_rng(act_rows_args(h, g, nullptr, (float*)g + m * S), (int)m, r, h->stream);
+            HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+            if (spec_after_rng(h)) return -1;
+            HIPCHK(h, hipEventSynchronize(h->act_ev));
+            std::memcpy(act_out + done * A, p + m * S, sizeof(float) * m * A);
+            continue;
+        }
         const int rc = sacx_actor_act(h, g, m, deterministic, (float*)g + m * S);
         if (rc) return rc;
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         // the drop-in loop steps next: its randoms are drawn while the host has the action
-        if (done + m >= n && h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0 &&
-            spec_draw(h))
-            return -1;
+        if (done + m >= n && spec && spec_draw(h)) return -1;
         HIPCHK(h, hipEventSynchronize(h->act_ev));
         std::memcpy(act_out + done * A, p + m * S, sizeof(float) * m * A);
     }
@@ -2190,11 +2238,21 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         a.output_norm = h->cfg.actor_output_norm;
     }
     a.sstride = (int64_t)h->seed_bytes; a.nseeds = K; a.m = (int32_t)n;
-    launch_act_rows(a, (int)n, h->stream);
-    HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
-    // lock-step drop-in cadence: every seed's next sampler draw queued behind the actions
-    if (h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0 && spec_draw(h)) return -1;
+    // lock-step drop-in cadence: every seed's next sampler draw, beside the action rows
+    // (deterministic: k_act_rng) or queued behind them
+    const bool spec = h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0;
+    if (spec && deterministic && h->act_rng) {
+        RngArgs r;
+        if (spec_rng_args(h, &r)) return -1;
+        launch_act_rng(a, (int)n, r, h->stream);
+        HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+        if (spec_after_rng(h)) return -1;
+    } else {
+        launch_act_rows(a, (int)n, h->stream);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+        if (spec && spec_draw(h)) return -1;
+    }
     HIPCHK(h, hipEventSynchronize(h->act_ev));
     std::memcpy(act_out, pa + tot * S, sizeof(float) * tot * A);
     return 0;
@@ -2458,8 +2516,7 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS;
     auto W = [&](const std::string& nm) { return h->f(nm); };
-    if (n > 0 && n <= ACT_ROWS_MAX && !h->ln && S <= ACT_ROWS_DIM && h->H0 <= ACT_ROWS_DIM &&
-        H1 <= ACT_ROWS_DIM && h->Aout <= 64) {
+    if (act_rows_ok(h, n)) {
         // the env loop's few rows: the noise draw, then one workgroup per row (k_act_rows)
         float* noise = deterministic ? nullptr : W("act.noise");
         if (!deterministic) {          // u = np.random.normal(size=(n, A)) from the global stream
@@ -2469,21 +2526,7 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
             r.slot = -1; r.reset_seq = 0; r.nupd = 1;
             launch_rng(r, h->stream);
         }
-        ActRowArgs a{};
-        a.obs = obs; a.s_mean = W("norm.s_mean"); a.s_den = W("norm.s_den");
-        a.W0 = W("actor.l0"); a.W1 = W("actor.l1"); a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
-        a.noise = noise; a.out = act_out;
-        a.S = S; a.A = A; a.Aout = h->Aout; a.H0 = h->H0; a.H1 = H1;
-        a.act0 = h->aact[0]; a.act1 = h->aact[1];
-        a.mode = h->cfg.actor_gaussian ? 2 : 1;
-        a.per_state_std = h->cfg.per_state_std;
-        a.lim = h->cfg.act_limit;
-        if (h->cfg.actor_gaussian) {          // logstd_init (continuous_actors.py:39-44), f32
-            const double sm = h->cfg.actor_std_mult > 0.f ? h->cfg.actor_std_mult : 1.0;
-            a.logstd_init = (float)(std::log(sm) - (h->cfg.per_state_std ? std::log(std::log(2.0)) : 0.0));
-            a.output_norm = h->cfg.actor_output_norm;
-        }
-        launch_act_rows(a, (int)n, h->stream);
+        launch_act_rows(act_rows_args(h, obs, noise, act_out), (int)n, h->stream);
         HIPCHK(h, hipGetLastError());
         return 0;
     }
