@@ -2658,10 +2658,19 @@ __device__ __forceinline__ void act_rows_body(const ActRowArgs& g_in, const int 
     act_tail(g, outs, row, lane, ls, u);
 }
 
+// after a row's outputs: publish them to a polling host (ActRowArgs::done)
+__device__ __forceinline__ void act_rows_done(uint32_t* done) {
+    if (done == nullptr) return;
+    __threadfence_system();            // every thread's output stores, before the count
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 template <bool PF>
 __global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
     __shared__ ActShared L;
     act_rows_body<PF>(g, blockIdx.x, L);
+    act_rows_done(g.done);
 }
 
 // The drop-in loop's deterministic act with the next update's sampler draw beside it: the
@@ -2675,8 +2684,12 @@ union ActRngShared {
 template <bool PF>
 __global__ __launch_bounds__(1024) void k_act_rng(ActRowArgs g, RngArgs r) {
     __shared__ ActRngShared U;
-    if (blockIdx.x + 1 < gridDim.x) act_rows_body<PF>(g, blockIdx.x, U.a);
-    else rng_body(r, U.r);
+    if (blockIdx.x + 1 < gridDim.x) {
+        act_rows_body<PF>(g, blockIdx.x, U.a);
+        act_rows_done(g.done);
+    } else {
+        rng_body(r, U.r);
+    }
 }
 
 

@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstddef>
+#include <chrono>
 #include <cstring>
 #include <map>
 #include <string>
@@ -168,6 +169,10 @@ struct sacx_handle {
     std::map<std::tuple<int, int, int>, hipGraphExec_t> graphs;   // (G, with_rng, skipped kind)
     std::vector<std::pair<RollKey, hipGraphExec_t>> roll_graphs;     // sacx_rollout replays
     std::vector<hipEvent_t> events;
+    uint32_t* done_host = nullptr;   // pinned completion counter of act_host's rows (ActRowArgs::done)
+    uint32_t* done_dev = nullptr;
+    uint32_t done_seq = 0;           // its value once every row launched so far has finished
+    bool act_poll = true;            // act_host waits on the counter, not on the stream (SACX_ACT_POLL=0: event)
     float* pin = nullptr;            // pinned host staging (2 x STAGE_CAP floats), the _host entry points:
     float* pin_dev = nullptr;        // [0, STAGE_CAP) appends, [STAGE_CAP, 2 STAGE_CAP) acts; pin_dev is its
                                      // device-side address (kernels read / write it in place)
@@ -1804,6 +1809,7 @@ void sacx_destroy(sacx_handle* h) {
     for (auto& kv : h->roll_graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->pin) (void)hipHostFree(h->pin);
+    if (h->done_host) (void)hipHostFree(h->done_host);
     if (h->pin_ev) (void)hipEventDestroy(h->pin_ev);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->rng_stream) (void)hipStreamDestroy(h->rng_stream);
@@ -1911,6 +1917,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     HIPCHK(h, hipEventCreateWithFlags(&h->act_ev, hipEventDisableTiming));
     if (const char* e = std::getenv("SACX_SPEC")) h->spec_enabled = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_ACT_RNG")) h->act_rng = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SACX_ACT_POLL")) h->act_poll = std::atoi(e) != 0;
     h->cur_size_host = 0;
     h->bound = true;
     return 0;
@@ -2034,6 +2041,29 @@ static int stage_alloc(sacx_handle* h) {
         HIPCHK(h, hipHostMalloc((void**)&h->pin, sizeof(float) * 2 * STAGE_CAP, hipHostMallocMapped));
         HIPCHK(h, hipHostGetDevicePointer((void**)&h->pin_dev, h->pin, 0));
         HIPCHK(h, hipEventCreateWithFlags(&h->pin_ev, hipEventDisableTiming));
+        HIPCHK(h, hipHostMalloc((void**)&h->done_host, 64, hipHostMallocMapped));
+        HIPCHK(h, hipHostGetDevicePointer((void**)&h->done_dev, h->done_host, 0));
+        __atomic_store_n(h->done_host, 0u, __ATOMIC_RELEASE);
+        h->done_seq = 0;
+    }
+    return 0;
+}
+
+// The act_host rows' outputs are on the host once the counter reaches done_seq: spin on it (a
+// few us) instead of waiting for the whole stream position (k_act_rng's sampler workgroup, the
+// event's own latency).  Past 1 s the stream is waited for, and a counter still short is an error.
+static int act_rows_wait(sacx_handle* h) {
+    if (!h->act_poll) return hipEventSynchronize(h->act_ev) == hipSuccess ? 0 : fail(h, "act event");
+    const uint32_t target = h->done_seq;
+    auto reached = [&]() { return (int32_t)(__atomic_load_n(h->done_host, __ATOMIC_ACQUIRE) - target) >= 0; };
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t it = 1; !reached(); ++it) {
+        __builtin_ia32_pause();
+        if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+            HIPCHK(h, hipEventSynchronize(h->act_ev));
+            if (!reached()) return fail(h, "act rows finished without their completion count");
+            break;
+        }
     }
     return 0;
 }
@@ -2130,6 +2160,8 @@ static ActRowArgs act_rows_args(sacx_handle* h, const float* obs, float* noise, 
     }
     return a;
 }
+static int actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out,
+                     uint32_t* done);
 static bool act_rows_ok(const sacx_handle* h, int64_t n) {
     return n > 0 && n <= ACT_ROWS_MAX && !h->ln && h->S <= ACT_ROWS_DIM && h->H0 <= ACT_ROWS_DIM &&
            h->H1 <= ACT_ROWS_DIM && h->Aout <= 64;
@@ -2152,19 +2184,28 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
             // the drop-in loop's act with the next update's draw beside the rows (k_act_rng)
             RngArgs r;
             if (spec_rng_args(h, &r)) return -1;
-            launch_act_rng(act_rows_args(h, g, nullptr, (float*)g + m * S), (int)m, r, h->stream);
+            ActRowArgs a = act_rows_args(h, g, nullptr, (float*)g + m * S);
+            a.done = h->done_dev;
+            h->done_seq += (uint32_t)m;
+            launch_act_rng(a, (int)m, r, h->stream);
             HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
             if (spec_after_rng(h)) return -1;
-            HIPCHK(h, hipEventSynchronize(h->act_ev));
+            if (act_rows_wait(h)) return -1;
             std::memcpy(act_out + done * A, p + m * S, sizeof(float) * m * A);
             continue;
         }
-        const int rc = sacx_actor_act(h, g, m, deterministic, (float*)g + m * S);
+        const bool rows = act_rows_ok(h, m);     // k_act_rows: the host polls the rows' count
+        if (rows) h->done_seq += (uint32_t)m;
+        const int rc = actor_act(h, g, m, deterministic, (float*)g + m * S, rows ? h->done_dev : nullptr);
         if (rc) return rc;
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         // the drop-in loop steps next: its randoms are drawn while the host has the action
         if (done + m >= n && spec && spec_draw(h)) return -1;
-        HIPCHK(h, hipEventSynchronize(h->act_ev));
+        if (rows) {
+            if (act_rows_wait(h)) return -1;
+        } else {
+            HIPCHK(h, hipEventSynchronize(h->act_ev));
+        }
         std::memcpy(act_out + done * A, p + m * S, sizeof(float) * m * A);
     }
     return 0;
@@ -2238,6 +2279,8 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         a.output_norm = h->cfg.actor_output_norm;
     }
     a.sstride = (int64_t)h->seed_bytes; a.nseeds = K; a.m = (int32_t)n;
+    a.done = h->done_dev;                   // every seed's rows count
+    h->done_seq += (uint32_t)(n * K);
     // lock-step drop-in cadence: every seed's next sampler draw, beside the action rows
     // (deterministic: k_act_rng) or queued behind them
     const bool spec = h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0;
@@ -2253,7 +2296,7 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         if (spec && spec_draw(h)) return -1;
     }
-    HIPCHK(h, hipEventSynchronize(h->act_ev));
+    if (act_rows_wait(h)) return -1;
     std::memcpy(act_out, pa + tot * S, sizeof(float) * tot * A);
     return 0;
 }
@@ -2510,7 +2553,14 @@ static void actor_hidden(sacx_handle* h, const float* X, int ldX, int m, float* 
     launch_gemm(pl[1].gemm, st);
 }
 
+static int actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out,
+                     uint32_t* done);
 int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
+    return actor_act(h, obs, n, deterministic, act_out, nullptr);
+}
+// done: the rows' completion counter (act_host; k_act_rows path only)
+static int actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out,
+                     uint32_t* done) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!deterministic && spec_cancel(h)) return -1;   // a draw from the stream: undo the speculative one
     if (n < 0 || (n > 0 && (!obs || !act_out))) return fail(h, "bad arguments");
@@ -2526,7 +2576,9 @@ int sacx_actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determin
             r.slot = -1; r.reset_seq = 0; r.nupd = 1;
             launch_rng(r, h->stream);
         }
-        launch_act_rows(act_rows_args(h, obs, noise, act_out), (int)n, h->stream);
+        ActRowArgs a = act_rows_args(h, obs, noise, act_out);
+        a.done = done;
+        launch_act_rows(a, (int)n, h->stream);
         HIPCHK(h, hipGetLastError());
         return 0;
     }

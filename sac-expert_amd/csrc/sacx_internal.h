@@ -518,6 +518,10 @@ struct ActRowArgs {
     // weights, noise) move by z * sstride, obs / out by z * m rows (arrays [seeds, m, S / A])
     int64_t sstride;
     int32_t nseeds, m;
+    // host-mapped completion counter (nullable): each row's workgroup adds 1 (system-scope
+    // release) once its outputs are written, so a synchronous host caller can take the actions
+    // without waiting for the rest of the launch (k_act_rng's sampler workgroup)
+    uint32_t* done;
 };
 
 // launchers (defined in k_sac.hip)
