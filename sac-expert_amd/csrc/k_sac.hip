@@ -1337,7 +1337,21 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 #ifndef SACX_T32_DW_WGS
 #define SACX_T32_DW_WGS 1
 #endif
-#define SACX_T32_OCC (T32 ? (MODE != GM_DW ? SACX_T32_WGS : SACX_T32_DW_WGS) : 1)
+// bf16 operands (config C5) need ~110 VGPRs in the 32x32 forward / dX tiles: at 6 workgroups per
+// CU (80 VGPRs) they spilled 12-80 registers to scratch (36-136 B per lane); 4 fit without
+// (Humanoid bf16 6.08k -> 7.1k updates/s, tools/ab_ns.sh)
+#ifndef SACX_T32_BF_WGS
+#define SACX_T32_BF_WGS 4
+#endif
+// fp32 32x32 dX tiles with the Q-head rows (rowk 1) spill 17-18 VGPRs at 6 per CU; 5 per CU
+// (no spill) measured neutral (Humanoid +0.2 %, HC 8 seeds -0.7 %, tools/ab_qh.sh), so 6 stays
+#ifndef SACX_T32_QH_WGS
+#define SACX_T32_QH_WGS SACX_T32_WGS
+#endif
+#define SACX_T32_OCC                                                                                         \
+    (T32 ? (MODE != GM_DW ? (BF ? SACX_T32_BF_WGS : (MODE == GM_DX && ROWK == 1 ? SACX_T32_QH_WGS : SACX_T32_WGS)) \
+                          : SACX_T32_DW_WGS)                                                                 \
+         : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
 __global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
