@@ -773,6 +773,9 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
 #ifndef SACX_T32_NS
 #define SACX_T32_NS 1   // k slabs per load group of a 32x32 tile (1: 6 workgroups per CU fit)
 #endif
+#ifndef SACX_T32_DW_NS
+#define SACX_T32_DW_NS 1   // the same for the dW + Adam tiles (uncapped registers)
+#endif
 template <int MODE, int VEC, bool BF, bool PART = false>
 __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
                                             float (&red)[16][4][64]) {
@@ -826,7 +829,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         acc1[s] = floatx4{0.f, 0.f, 0.f, 0.f};
     }
     // bf16: two k slabs per load group, one 16x16x32 MFMA per sub-tile and slab pair
-    constexpr int NS = BF ? 2 : SACX_T32_NS;
+    constexpr int NS = BF ? 2 : (MODE == GM_DW ? SACX_T32_DW_NS : SACX_T32_NS);
     auto main_loop = [&](auto vt) {   // unswitched on the problem's float4 flag, as gemm_core
     constexpr bool V = decltype(vt)::value;
     for (int it = it0; it < it1; it += NS) {
