@@ -47,6 +47,9 @@ enum sacx_role { SACX_ROLE_WORK = 0, SACX_ROLE_PARAM = 1, SACX_ROLE_TARGET = 2, 
 /* Flags for sacx_sac_step. */
 #define SACX_STEP_EXTERNAL_RANDOMS 1  /* skip the device sampler: caller filled slot0.idx / slot0.noise */
 #define SACX_STEP_EAGER 2             /* launch kernels directly instead of replaying a hipGraph */
+/* floats in the pinned staging buffer of each half (append / act) of the *_host entry points:
+   one append_host_seeds call takes seeds*n*(2S+A+2) <= this, act_host_seeds seeds*n*(S+A) */
+#define SACX_STAGE_FLOATS 65536
 
 /* Hyper-parameters; names follow sac_eo/common/train_parser.py. */
 typedef struct sacx_config {

@@ -180,8 +180,13 @@ class LoopOracle:
         self.episode_rng: List[tuple] = []      # the global stream at each episode start (before the hooks)
         self.diag: List[tuple] = []             # (MSE on expert data, on counterfactual actions) per episode
         self.model_losses: List[float] = []
+        self.fit_last: List[float] = []          # the last model-fit step's loss of each episode's fit
         self.eps = float(k.get("epsilon", 1e-3))
         self.s_expert = self.sp_expert = self.a_expert = None
+        # TrajectoryCorruptor (corruptor.py:3-30, base_onpolicy_alg.py:52): its own default_rng(0)
+        self.s_noise_std = float(k.get("s_noise_std") or 0.0)
+        self.s_noise_type = k.get("s_noise_type", "all")
+        self.s_noise_rng = np.random.default_rng(0)
 
     # ---------------------------------------------------------------- pieces
     def _nrm(self):
@@ -208,12 +213,16 @@ class LoopOracle:
         s = env.reset()
         for t in range(horizon):
             a = self._sample(params, logstd, s, deterministic, nrm)
-            sp, r, d, _ = env.step(np.clip(a, -self.cfg.act_limit, self.cfg.act_limit))
+            s_true, r, d, _ = env.step(np.clip(a, -self.cfg.act_limit, self.cfg.act_limit))
+            sp = s_true
+            if self.s_noise_std > 0.0:                         # corrupt_samples (corruptor.py:23-30)
+                u = self.s_noise_rng.normal(size=np.shape(s_true)).astype("float32")
+                sp = s_true + u * np.sqrt(self.normalizer.delta_rms.var) * self.s_noise_std
             J += r
             if t == horizon - 1:
                 d = False
             s_t.append(s); a_t.append(a); r_t.append(r); sp_t.append(sp); d_t.append(d)
-            s = sp
+            s = sp if self.s_noise_type == "all" else s_true   # samplers.py:35-43
             if d:
                 break
         return (np.array(s_t, np.float32), np.array(a_t, np.float32), np.array(r_t, np.float32),
@@ -285,6 +294,14 @@ class LoopOracle:
         k, rs = self.k, self.rs
         md = self.model_data
         n = md.current_size
+        ms, ma, msp, mr = md.s, md.a, md.sp, md.r
+        ratio = float(k.get("model_holdout_ratio") or 0.0)
+        if ratio > 0.0:                                         # :492-513: fit the shuffled head
+            n = int(md.current_size * (1 - ratio))
+            rows = np.arange(md.current_size)
+            rs.shuffle(rows)
+            rows = rows[:n]
+            ms, ma, msp, mr = ms[rows], ma[rows], msp[rows], mr[rows]
         mb = int(k.get("model_batch_size", 200))
         nm = int(k.get("num_models", 2))
         max_upd = k.get("model_max_updates", 1e5)
@@ -304,7 +321,7 @@ class LoopOracle:
             if n % mb != 0:
                 batches = batches[:-1]
             for bi in batches:
-                parts = [(md.s[bi[j]], md.a[bi[j]], md.sp[bi[j]], md.r[bi[j]]) for j in range(nm)]
+                parts = [(ms[bi[j]], ma[bi[j]], msp[bi[j]], mr[bi[j]]) for j in range(nm)]
                 self.model_losses.append(O.model_fit_step(
                     self.st, self.cfg, mnrm, parts, max_grad_norm=k.get("model_max_grad_norm"),
                     delta_clip_loss=k.get("delta_clip_loss") or 0.0, reward_clip_loss=k.get("reward_clip_loss") or 0.0))
@@ -313,6 +330,7 @@ class LoopOracle:
                     break
             if num_updates >= max_upd:
                 break
+        self.fit_last.append(self.model_losses[-1] if self.model_losses else float("nan"))
         if k.get("reset_model_optimizer"):
             self.st.opt_model = O.AdamState.zeros_like(self.st.opt_model.m)
         dc = k.get("delta_clip_pred") or 0.0

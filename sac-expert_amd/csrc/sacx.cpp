@@ -266,7 +266,7 @@ bool spec_mode(const sacx_handle* h) {
     } while (0)
 
 constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
-constexpr int STAGE_CAP = 1 << 16;   // floats in the pinned host staging buffer of the _host entry points
+constexpr int STAGE_CAP = SACX_STAGE_FLOATS;   // floats in the pinned host staging buffer of the _host entry points
 constexpr int ROLL_CAP = 4096;  // trajectories per sacx_rollout launch chain
 
 void build_layout(sacx_handle* h) {
@@ -2049,19 +2049,31 @@ static int stage_alloc(sacx_handle* h) {
     return 0;
 }
 
+static inline void cpu_relax() {
+#if defined(__x86_64__)
+    __builtin_ia32_pause();
+#endif
+}
+
 // The act_host rows' outputs are on the host once the counter reaches done_seq: spin on it (a
 // few us) instead of waiting for the whole stream position (k_act_rng's sampler workgroup, the
-// event's own latency).  Past 1 s the stream is waited for, and a counter still short is an error.
+// event's own latency).  An act queued behind a long stream prefix (step(G), a model fit) would
+// keep spinning, so past ACT_SPIN the stream is waited for instead; a counter still short then
+// is an error, and done_seq is resynchronised from the counter so later acts do not wait on it.
+static constexpr auto ACT_SPIN = std::chrono::microseconds(2000);   // > one update graph (the drop-in cadence)
 static int act_rows_wait(sacx_handle* h) {
     if (!h->act_poll) return hipEventSynchronize(h->act_ev) == hipSuccess ? 0 : fail(h, "act event");
     const uint32_t target = h->done_seq;
     auto reached = [&]() { return (int32_t)(__atomic_load_n(h->done_host, __ATOMIC_ACQUIRE) - target) >= 0; };
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t it = 1; !reached(); ++it) {
-        __builtin_ia32_pause();
-        if ((it & 4095) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
-            HIPCHK(h, hipEventSynchronize(h->act_ev));
-            if (!reached()) return fail(h, "act rows finished without their completion count");
+        cpu_relax();
+        if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > ACT_SPIN) {
+            const hipError_t e = hipEventSynchronize(h->act_ev);
+            if (e != hipSuccess || !reached()) {
+                h->done_seq = __atomic_load_n(h->done_host, __ATOMIC_ACQUIRE);
+                return fail(h, e != hipSuccess ? "act event" : "act rows finished without their completion count");
+            }
             break;
         }
     }
@@ -2180,14 +2192,17 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
         float* p = h->pin + STAGE_CAP;          // the act half: its last reader was a synchronous act
         const float* g = h->pin_dev + STAGE_CAP;
         std::memcpy(p, obs + done * S, sizeof(float) * m * S);
-        if (spec && deterministic && h->act_rng && done + m >= n && act_rows_ok(h, m)) {
+        // (one seed's handle only: on a packed handle the act is the selected seed's rows while the
+        // draw is every seed's, which spec_draw's own sampler launch covers)
+        if (spec && deterministic && h->act_rng && h->seeds == 1 && done + m >= n && act_rows_ok(h, m)) {
             // the drop-in loop's act with the next update's draw beside the rows (k_act_rng)
             RngArgs r;
             if (spec_rng_args(h, &r)) return -1;
             ActRowArgs a = act_rows_args(h, g, nullptr, (float*)g + m * S);
             a.done = h->done_dev;
-            h->done_seq += (uint32_t)m;
             launch_act_rng(a, (int)m, r, h->stream);
+            HIPCHK(h, hipGetLastError());
+            h->done_seq += (uint32_t)m;
             HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
             if (spec_after_rng(h)) return -1;
             if (act_rows_wait(h)) return -1;
@@ -2195,9 +2210,9 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
             continue;
         }
         const bool rows = act_rows_ok(h, m);     // k_act_rows: the host polls the rows' count
-        if (rows) h->done_seq += (uint32_t)m;
         const int rc = actor_act(h, g, m, deterministic, (float*)g + m * S, rows ? h->done_dev : nullptr);
         if (rc) return rc;
+        if (rows) h->done_seq += (uint32_t)m;    // only once the launch that counts them is queued
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         // the drop-in loop steps next: its randoms are drawn while the host has the action
         if (done + m >= n && spec && spec_draw(h)) return -1;
@@ -2280,7 +2295,6 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
     }
     a.sstride = (int64_t)h->seed_bytes; a.nseeds = K; a.m = (int32_t)n;
     a.done = h->done_dev;                   // every seed's rows count
-    h->done_seq += (uint32_t)(n * K);
     // lock-step drop-in cadence: every seed's next sampler draw, beside the action rows
     // (deterministic: k_act_rng) or queued behind them
     const bool spec = h->last_step_one && spec_mode(h) && !h->spec_live && h->cur_size_host > 0;
@@ -2288,11 +2302,14 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         RngArgs r;
         if (spec_rng_args(h, &r)) return -1;
         launch_act_rng(a, (int)n, r, h->stream);
+        HIPCHK(h, hipGetLastError());
+        h->done_seq += (uint32_t)(n * K);
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         if (spec_after_rng(h)) return -1;
     } else {
         launch_act_rows(a, (int)n, h->stream);
         HIPCHK(h, hipGetLastError());
+        h->done_seq += (uint32_t)(n * K);
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         if (spec && spec_draw(h)) return -1;
     }

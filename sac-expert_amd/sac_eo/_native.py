@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
 SACX_ABI_VERSION = 6
+STAGE_FLOATS = 65536            # SACX_STAGE_FLOATS (include/sacx.h)
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
 STEP_EXTERNAL_RANDOMS = 1

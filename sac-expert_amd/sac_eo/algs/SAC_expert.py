@@ -32,6 +32,14 @@ class SAC_exp(SACBase):
             raise ValueError("SAC-EO uses one or two world models (SAC_expert.py:271-336)")
         super().__init__(idx, env, env_eval, actor, v_critic, q_targets, q_critics, models, alg_kwargs,
                          mf_update_kwargs)
+        if self.env_buffer_size:
+            # the world models fit the last model_buffer_size rows of the replay ring; a smaller ring
+            # would have dropped some of them by the time the run holds that many rows
+            most = max(self.total_timesteps, self.env_batch_size_init)
+            if int(self.env_buffer_size) < min(self.model_buffer_size, most):
+                raise NotImplementedError(
+                    f"--model_buffer_size {self.model_buffer_size} larger than --env_buffer_size "
+                    f"{int(self.env_buffer_size)} for a run of {most} steps (the model data is the replay ring's tail)")
         self.env_expert = env_expert
         self.expert = expert
         self.expert_normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, init_expert_rms_stats)
@@ -77,7 +85,7 @@ class SAC_exp(SACBase):
         while cur < self.expert_buffer_size:
             horizon = min(self.expert_buffer_size - cur, self.env_horizon)
             s, a, r, sp, d, J = trajectory_sampler(self.env_expert, self.expert, horizon, eval=True,
-                                                   deterministic=True)
+                                                   deterministic=True, corruptor=self.corruptor)
             s_all.append(s)
             a_all.append(a)
             sp_all.append(sp)
@@ -167,19 +175,29 @@ class SAC_exp(SACBase):
                 self._flush_update_logs()        # the device ring is full (epsilon is constant within an episode)
 
     def _update_models(self):
+        """:480-552: optional holdout split (a global-stream shuffle of the model rows, the fit on
+        the first int(n·(1−ratio)) of them, :492-513), then the epoch / minibatch index draws
+        (:519-550), fitted on the device."""
         t0 = time.time()
         n_model = min(self.steps_total, self.model_buffer_size)   # model_data = last rows of the env data
         if n_model > int(self.engine.ctl()["cur_size"]):
-            # model_data would hold rows the (smaller) replay ring already dropped
+            # model_data would hold rows the (smaller) replay ring already dropped (checked at setup)
             raise NotImplementedError("--model_buffer_size larger than --env_buffer_size")
-        if n_model < self.model_batch_size:
+        if n_model == 0:
             return
         base = int(self.engine.ctl()["cur_size"]) - n_model
         batches = []
         num_updates = 0
         with self._host_rng():
+            rows = None                                # model-data row of each training index
+            n_train = n_model
+            if self.model_holdout_ratio > 0.0:
+                n_train = int(n_model * (1 - self.model_holdout_ratio))
+                rows = np.arange(n_model)
+                np.random.shuffle(rows)
+                rows = rows[:n_train]
             for ep in range(self.model_num_epochs):
-                idx = np.arange(n_model)
+                idx = np.arange(n_train)
                 nm = len(self.models)                 # self.B (SAC_expert.py:61)
                 if self.model_batch_shuffle:
                     idx = np.tile(idx, (nm, 1))
@@ -188,12 +206,12 @@ class SAC_exp(SACBase):
                 else:
                     np.random.shuffle(idx)
                     idx = np.tile(idx, (nm, 1))
-                sections = np.arange(0, n_model, self.model_batch_size)[1:]
+                sections = np.arange(0, n_train, self.model_batch_size)[1:]
                 parts = np.array_split(idx, sections, axis=1)
-                if n_model % self.model_batch_size != 0:
+                if n_train % self.model_batch_size != 0:
                     parts = parts[:-1]
                 for p in parts:
-                    batches.append(p)
+                    batches.append(p if rows is None else rows[p])
                     num_updates += 1
                     if num_updates >= self.model_max_updates:
                         break

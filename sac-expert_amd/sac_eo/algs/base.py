@@ -13,6 +13,7 @@ import time
 
 import numpy as np
 
+from ..common.corruptor import TrajectoryCorruptor
 from ..common.logger import Logger
 from ..common.normalizer import RunningNormalizers
 from ..common.samplers import trajectory_sampler
@@ -41,6 +42,10 @@ class SACBase:
         # only with --only_model_normalizer (:139-144), updated by the collection and episode hooks
         self.model_normalizer = RunningNormalizers(self.s_dim, self.a_dim, self.gamma, self.init_rms_stats)
         self._new_traj = []                 # the episode's transitions (new_traj, SAC_expert.py:49-51)
+        # --s_noise_std / --s_noise_type (base_onpolicy_alg.py:52): applied to every collected
+        # trajectory (samplers.py:35-43), its variance read from self.normalizer (set in _set_rms)
+        self.corruptor = TrajectoryCorruptor(self.s_noise_std, self.s_noise_type)
+        self.corruptor.set_rms(self.normalizer)
         self.last_eval = 0
         self.engine = self._build_engine(alg_kwargs)
         self.steps_total = 0
@@ -79,9 +84,11 @@ class SACBase:
         self.model_max_updates = k.get("model_max_updates", 1e5)
         self.model_max_grad_norm = k.get("model_max_grad_norm")
         self.model_batch_shuffle = k.get("model_batch_shuffle", True)
-        self.model_holdout_ratio = k.get("model_holdout_ratio", 0.0)
         self.reset_model_optimizer = k.get("reset_model_optimizer", False)
         self.epsilon = k.get("epsilon", 1e-3)
+        self.s_noise_std = float(k.get("s_noise_std") or 0.0)
+        self.s_noise_type = k.get("s_noise_type", "all")
+        self.model_holdout_ratio = float(k.get("model_holdout_ratio") or 0.0)
         self.expert_buffer_size = int(k.get("expert_buffer_size") or 20)
         self.expert_batch_size = k.get("expert_batch_size")
         self._max_episode_steps = 1000
@@ -169,6 +176,7 @@ class SACBase:
     def _set_rms(self):
         for obj in [self.actor] + list(self.q_critics) + list(self.q_targets):
             obj.set_rms(self.normalizer)
+        self.corruptor.set_rms(self.normalizer)          # base_onpolicy_alg.py:204
         for m in (self.models or []) if self.use_expert else []:
             m.set_rms(self._models_normalizer())
         self._push_normalizers()
@@ -251,18 +259,19 @@ class SACBase:
         return self._drive(self._collect_env_data_steps(num_timesteps, update_normalizers, only_model_normalizer))
 
     def _trajectory_steps(self, env, horizon, deterministic=False):
-        """trajectory_sampler(env, actor, horizon, eval=True) (samplers.py:3-70) with the actor's
-        sample() as an "act" request per step."""
+        """trajectory_sampler(env, actor, horizon, eval=True, corruptor=self.corruptor)
+        (samplers.py:3-70) with the actor's sample() as an "act" request per step."""
         s_t, a_t, r_t, sp_t, d_t, J = [], [], [], [], [], 0.0
         s = env.reset()
         for t in range(horizon):
             a = yield ("act", s, deterministic)
-            sp, r, d, _ = env.step(self.actor.clip(a))
+            s_true, r, d, _ = env.step(self.actor.clip(a))
+            sp, s_next = self.corruptor.store_and_next(s_true)
             J += r
             if t == horizon - 1:
                 d = False
             s_t.append(s); a_t.append(a); r_t.append(r); sp_t.append(sp); d_t.append(d)
-            s = sp
+            s = s_next
             if d:
                 break
         return (np.array(s_t, np.float32), np.array(a_t, np.float32), np.array(r_t, np.float32),

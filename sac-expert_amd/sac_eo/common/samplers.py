@@ -10,11 +10,7 @@ def trajectory_sampler(env, actor, horizon, s_init=None, eval=False, determinist
         s_old = s
         a = actor.sample(s_old, deterministic=deterministic).numpy()
         s_true, r, d, _ = env.step(actor.clip(a))
-        if corruptor is not None:
-            s_store = corruptor.corrupt_samples(s_true)
-            s = s_store if corruptor.s_noise_type == "all" else s_true
-        else:
-            s_store = s = s_true
+        s_store, s = corruptor.store_and_next(s_true) if corruptor is not None else (s_true, s_true)
         if eval:
             J_tot += r
         if t == horizon - 1:

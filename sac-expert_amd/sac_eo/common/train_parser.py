@@ -11,13 +11,16 @@ import argparse
 
 F, I, S = float, int, str
 T = "store_true"
+SAME = "same"   # a second kwargs group for a flag defined earlier (no new parser argument)
 
-# (group, flag, type_or_action, default, extra)
+# (group, flag, type_or_action, default, extra).  The rows are in the reference's order within each
+# kwargs group (all_kwargs is the logged ``param`` layout, pinned by tests/golden/ref_fixtures.json);
+# group None = a parser flag in no kwargs group (--alg_seed)
 _FLAGS = [
     # setup
     ("setup", "runs", I, 1, {}), ("setup", "runs_start", I, 0, {}), ("setup", "cores", I, None, {}),
     ("setup", "seed", I, 0, {}), ("setup", "setup_seed", I, None, {}), ("setup", "sim_seed", I, None, {}),
-    ("setup", "eval_seed", I, None, {}), ("setup", "expert_seed", I, None, {}), ("setup", "alg_seed", I, None, {}),
+    ("setup", "eval_seed", I, None, {}), ("setup", "expert_seed", I, None, {}), (None, "alg_seed", I, None, {}),
     ("setup", "save_path", S, "./logs", {}), ("setup", "save_file", S, None, {}),
     ("setup", "import_path", S, "./logs", {}), ("setup", "import_file", S, None, {}),
     ("setup", "import_idx", I, None, {}), ("setup", "import_all", T, False, {}),
@@ -33,10 +36,10 @@ _FLAGS = [
     # critic
     ("critic", "critic_layers", I, [64, 64], {"nargs": "+"}), ("critic", "critic_activations", S, ["tanh"], {"nargs": "+"}),
     ("critic", "critic_gain", F, 1.0, {}), ("critic", "critic_ensemble", T, False, {}),
-    ("critic", "num_models", I, 2, {"group2": "model"}), ("critic", "critic_init_type", S, "orthogonal", {}),
+    ("critic", "num_models", I, 2, {}), ("critic", "critic_init_type", S, "orthogonal", {}),
     ("critic", "critic_layer_norm", T, False, {}),
     # model
-    ("model", "gaussian_model", T, False, {}),
+    ("model", "gaussian_model", T, False, {}), ("model", "num_models", SAME, None, {}),
     ("model", "model_layers", I, [512, 512], {"nargs": "+"}), ("model", "model_activations", S, ["relu"], {"nargs": "+"}),
     ("model", "model_gain", F, 0.01, {}), ("model", "model_std_mult", F, 1.0, {}),
     ("model", "reward_layers", I, [512, 512], {"nargs": "+"}), ("model", "reward_activations", S, ["relu"], {"nargs": "+"}),
@@ -51,7 +54,7 @@ _FLAGS = [
     ("alg", "sim_buffer_size", F, None, {}), ("alg", "model_buffer_size", F, 1e5, {}),
     ("alg", "expert_buffer_size", F, 20, {}),
     # training
-    ("alg", "checkpoint_file", S, "TEMPLOG", {}), ("alg", "save_freq", F, None, {}),
+    ("alg", "save_path", SAME, None, {}), ("alg", "checkpoint_file", S, "TEMPLOG", {}), ("alg", "save_freq", F, None, {}),
     ("alg", "eval_freq", F, None, {}), ("alg", "eval_num_traj", I, 5, {}),
     ("alg", "alg_type", S, "sac_imit", {}), ("alg", "mf_algo", S, "trpo", {}),
     ("alg", "total_timesteps", F, 5e5, {}), ("alg", "env_horizon", I, 1000, {}),
@@ -62,6 +65,8 @@ _FLAGS = [
     ("alg", "sim_batch_size", I, 10000, {}), ("alg", "exp_batch_type", S, "steps", {"choices": ["steps", "traj"]}),
     # model update
     ("alg", "model_lr", F, 1e-3, {}), ("alg", "model_num_epochs", I, 10, {}), ("alg", "model_batch_size", I, 200, {}),
+    # model-update batch shuffling is a negative flag in the reference (--no_model_batch_shuffle)
+    ("alg", "model_batch_shuffle", "store_false_alias:no_model_batch_shuffle", True, {}),
     ("alg", "model_max_updates", F, 1e5, {}), ("alg", "model_max_grad_norm", F, None, {}),
     ("alg", "model_holdout_ratio", F, 0.0, {}), ("alg", "model_holdout_epochs", I, 5, {}),
     ("alg", "reset_model_optimizer", T, False, {}),
@@ -94,8 +99,6 @@ _FLAGS = [
     ("mf", "adaptlr", "store_false_alias:no_adaptlr", True, {}), ("mf", "adapt_factor", F, 0.03, {}),
     ("mf", "adapt_minthresh", F, 0.0, {}), ("mf", "adapt_maxthresh", F, 1.0, {}),
 ]
-# model-update batch shuffling is a negative flag in the reference (--no_model_batch_shuffle)
-_FLAGS.append(("alg", "model_batch_shuffle", "store_false_alias:no_model_batch_shuffle", True, {}))
 
 _GROUP_NAMES = {"setup": "setup_kwargs", "env": "env_kwargs", "actor": "actor_kwargs", "critic": "critic_kwargs",
                 "model": "model_kwargs", "model_setup": "model_setup_kwargs", "alg": "alg_kwargs",
@@ -103,17 +106,17 @@ _GROUP_NAMES = {"setup": "setup_kwargs", "env": "env_kwargs", "actor": "actor_kw
 
 all_kwargs = {v: [] for v in _GROUP_NAMES.values()}
 for grp, name, _t, _d, extra in _FLAGS:
-    if name in ("gpus", "serial_runs"):
-        continue   # local additions, not reference kwargs
+    if grp is None or name in ("gpus", "serial_runs"):
+        continue   # parser-only flags, and the local additions
     all_kwargs[_GROUP_NAMES[grp]].append(name)
-    if extra.get("group2"):
-        all_kwargs[_GROUP_NAMES[extra["group2"]]].append(name)
 
 
 def create_train_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description="MI355X SAC / SAC-EO training (noc-lab/sac-expert compatible flags)")
     for _grp, name, typ, default, extra in _FLAGS:
         kw = {k: v for k, v in extra.items() if k in ("nargs", "choices")}
+        if typ == SAME:
+            continue
         if typ == T:
             p.add_argument("--" + name, action="store_true")
         elif isinstance(typ, str) and typ.startswith("store_false_alias:"):

@@ -39,7 +39,7 @@ def import_inputs(inputs_dict: dict) -> dict:
         if idx is None:
             idx = run if len(logs) > run else 0
         elif idx >= len(logs):
-            raise ValueError("import_idx too large")
+            raise AssertionError("import_idx too large")            # train_utils.py:43
         param, final = logs[idx]["param"], logs[idx]["final"]
         if sk.get("import_all"):
             setup = sk

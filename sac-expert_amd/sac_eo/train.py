@@ -70,14 +70,19 @@ def train(inputs_dict):
     return alg.train(inputs_dict["alg_kwargs"]["total_timesteps"], inputs_dict)
 
 
-def lockstep_ok(args, env_kwargs) -> bool:
-    """Whether the runs of a process can train as packed seeds in lock-step (sac_eo.algs.lockstep)."""
+def lockstep_ok(args, env_kwargs, k: int) -> bool:
+    """Whether k runs of a process can train as packed seeds in lock-step (sac_eo.algs.lockstep):
+    one row per run and request must fit the library's pinned staging (SACX_STAGE_FLOATS)."""
     if args.serial_runs or args.alg_type not in ("sac", "sac_imit") or args.env_batch_type != "steps":
         return False
     if args.actor_layer_norm:
         return False
+    env = init_env(**env_kwargs)
+    S, A = int(np.prod(env.observation_space.shape)), int(np.prod(env.action_space.shape))
+    from ._native import STAGE_FLOATS
+    if k * (2 * S + A + 2) > STAGE_FLOATS or k * (S + A) > STAGE_FLOATS:
+        return False
     if args.alg_type == "sac":            # G updates every real_step_mod steps of an EPISODE
-        env = init_env(**env_kwargs)
         return getattr(env, "terminate", True) is False
     return True
 
@@ -110,11 +115,17 @@ def main(argv=None):
     names, run_inputs = {}, []
     for r in runs:
         d = copy.deepcopy(inputs_dict)
-        d["setup_kwargs"].update(idx=args.runs_start + r, setup_seed=int(seeds["setup"][r]),
-                                 sim_seed=int(seeds["sim"][r]), eval_seed=int(seeds["eval"][r]),
-                                 expert_seed=int(seeds["expert"][r]), algorithm_seed=int(seeds["algorithm"][r]))
+        # train.py:132-142: a seed given on the command line is kept, the others derived per run
+        # (--alg_seed, which the reference never stores and then fails on, is used as given)
+        sk = d["setup_kwargs"]
+        sk["idx"] = args.runs_start + r
+        for kind, key in (("setup", "setup_seed"), ("sim", "sim_seed"), ("eval", "eval_seed"),
+                          ("expert", "expert_seed")):
+            if sk.get(key) is None:
+                sk[key] = int(seeds[kind][r])
+        sk["algorithm_seed"] = int(seeds["algorithm"][r]) if args.alg_seed is None else int(args.alg_seed)
         run_inputs.append(import_inputs(d))          # train_utils.py:20-92 (no-op without --import_file)
-    if len(runs) > 1 and lockstep_ok(args, inputs_dict["env_kwargs"]):
+    if len(runs) > 1 and lockstep_ok(args, inputs_dict["env_kwargs"], len(runs)):
         names = dict(zip(runs, train_packed(run_inputs)))
     else:
         for r, d in zip(runs, run_inputs):

@@ -138,3 +138,38 @@ def test_speculative_packed_lockstep(gpu_available, monkeypatch, use_expert):
     assert hits[1] == 0 and hits[0] >= n // 2, hits
     for i, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), i
+
+
+def test_speculative_packed_per_seed_act(gpu_available, monkeypatch):
+    """A per-seed act_host on a packed handle (select_seed(k), act_host(det)) followed by a packed
+    step(1): the speculative draw it queues must cover EVERY seed's stream (not only the selected
+    seed's), so the run equals the same calls with SACX_SPEC=0 bit for bit, seeds 1..K-1 included."""
+    from sac_eo.engine import Engine, EngineConfig
+    K, B, N, n = 3, 64, 700, 24
+    outs, hits = [], []
+    for spec in ("1", "0"):
+        monkeypatch.setenv("SACX_SPEC", spec)
+        learners = [make_learner(act="relu", B=B, N=N, seed=70 + 3 * k, done_p=0.05) for k in range(K)]
+        eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=N + 100,
+                                  graph_steps=1, seeds=K, single_seed_plan=True))
+        for k, (ocfg, st, buf, nrm, expert) in enumerate(learners):
+            eng.select_seed(k)
+            load_learner(eng, st, buf, nrm, expert, 0.1)
+            eng.rng_set_state(np.random.RandomState(80 + k).get_state())
+        rs = np.random.RandomState(11)
+        for j in range(n):
+            eng.select_seed(j % K)
+            o = rs.normal(size=17).astype(np.float32)
+            eng.act_host(o, deterministic=(j % 7 != 3))
+            eng.step(1, num_timesteps=j, ts_increment=1)
+        eng.sync()
+        hits.append(eng.spec_hits())
+        res = []
+        for k in range(K):
+            eng.select_seed(k)
+            res += [eng.stats(n).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state()[1].copy()]
+        outs.append(res)
+        eng.close()
+    assert hits[1] == 0 and hits[0] >= n // 2, hits
+    for i, (a, b) in enumerate(zip(*outs)):
+        assert np.array_equal(a, b), i

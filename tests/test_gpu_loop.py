@@ -23,12 +23,14 @@ from sac_loop import LoopOracle
 
 pytestmark = pytest.mark.gpu
 
-EP_LEN = 40          # synthetic episodes end (done) after EP_LEN steps
-INIT = 200           # --env_batch_size_init
 LOSS_TOL = 1e-4      # north_star: Q-loss trajectory within 1e-4 relative
+# the loop shapes: SMALL runs every flag variant fast; BENCH is the metric's configuration
+# (256x2 nets, B = 256, 512x2 world models, model minibatch 200, 100-step episodes)
+SMALL = dict(hidden=64, B=64, model_hidden=64, model_batch=50, epochs=2, ep_len=40, init=200, episodes=3)
+BENCH = dict(hidden=256, B=256, model_hidden=512, model_batch=200, epochs=3, ep_len=100, init=400, episodes=3)
 
 
-def _build(alg, flags, seed=7):
+def _build(alg, flags, seed=7, shape=SMALL, act="relu"):
     """The construction sequence of sac_eo/train.py:28-59 with short synthetic episodes."""
     from sac_eo.actors import init_actor
     from sac_eo.algs import init_alg
@@ -37,18 +39,20 @@ def _build(alg, flags, seed=7):
     from sac_eo.critics import init_critics
     from sac_eo.envs.synthetic import SyntheticEnv
     from sac_eo.models import init_world_models
-    total = INIT + 3 * EP_LEN
-    argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", "64", "64",
-            "--critic_layers", "64", "64", "--actor_activations", "relu", "--critic_activations", "relu",
-            "--model_layers", "64", "64", "--total_timesteps", str(total), "--env_batch_size_init", str(INIT),
-            "--env_horizon", "100", "--sac_batch_size", "64", "--model_batch_size", "50", "--model_num_epochs", "2",
-            "--seed", str(seed)] + flags
+    ep_len = shape["ep_len"]
+    total = shape["init"] + shape["episodes"] * ep_len
+    h, mh = str(shape["hidden"]), str(shape["model_hidden"])
+    argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", h, h,
+            "--critic_layers", h, h, "--actor_activations", act, "--critic_activations", act,
+            "--model_layers", mh, mh, "--total_timesteps", str(total), "--env_batch_size_init", str(shape["init"]),
+            "--env_horizon", "1000", "--sac_batch_size", str(shape["B"]), "--model_batch_size",
+            str(shape["model_batch"]), "--model_num_epochs", str(shape["epochs"]), "--seed", str(seed)] + flags
     d = gather_inputs(create_train_parser().parse_args(argv))
     d["actor_kwargs"]["actor_squash"] = True
     sd = derive_seeds(seed, 1, 0)
     ak = dict(d["alg_kwargs"], alg_seed=int(sd["algorithm"][0]), save_path="/tmp/sacx_loop_test")
     init_seeds(int(sd["setup"][0]))
-    envs = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=EP_LEN) for _ in range(3)]
+    envs = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=ep_len) for _ in range(3)]
     actor = init_actor(envs[0], **dict(d["actor_kwargs"], actor_weights=None))
     expert = init_actor(envs[0], **dict(d["actor_kwargs"], actor_weights=None))
     critics, q_targets, q_critics = init_critics(envs[0], **dict(d["critic_kwargs"], critic_weights=None))
@@ -60,7 +64,7 @@ def _build(alg, flags, seed=7):
     alg_obj = init_alg(0, envs[0], envs[1], envs[2], actor, critics, q_targets, q_critics, models, ak,
                        d["mf_update_kwargs"], expert, None)
     # what the oracle starts from: the bound weights, the global stream, fresh env copies
-    oenvs = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=EP_LEN) for _ in range(3)]
+    oenvs = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=ep_len) for _ in range(3)]
     oenvs[0].seed(int(sd["sim"][0]))
     oenvs[2].seed(int(sd["expert"][0]))
     return alg_obj, d, ak, total, oenvs, np.random.get_state()
@@ -87,19 +91,24 @@ def _same_stream(a, b):
     return np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
 
 
-@pytest.mark.parametrize("alg,flags", [
-    ("sac_imit", []),
-    ("sac_imit", ["--update_normalizers"]),
-    ("sac_imit", ["--update_normalizers", "--only_model_normalizer"]),
-    ("sac", []),
-    ("sac", ["--update_normalizers"]),
-])
-def test_train_loop_matches_oracle(gpu_available, alg, flags):
-    alg_obj, d, ak, total, oenvs, rs_state = _build(alg, flags)
+def _fresh_envs(shape):
+    from sac_eo.common.seeding import derive_seeds
+    from sac_eo.envs.synthetic import SyntheticEnv
+    sd = derive_seeds(7, 1, 0)
+    e = [SyntheticEnv("HalfCheetah-v3", max_episode_steps=shape["ep_len"]) for _ in range(3)]
+    e[0].seed(int(sd["sim"][0]))
+    e[2].seed(int(sd["expert"][0]))
+    return e
+
+
+def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
+    """The device loop and the fp64 oracle loop from the same start; returns everything compared."""
+    alg_obj, d, ak, total, oenvs, rs_state = _build(alg, flags, shape=shape, act=act)
     S, A = alg_obj.s_dim, alg_obj.a_dim
-    ocfg = O.Config(S=S, A=A, hidden=(64, 64), act="relu", B=64, gamma=ak["gamma"], tau=ak["soft_tau"],
+    H, MH = shape["hidden"], shape["model_hidden"]
+    ocfg = O.Config(S=S, A=A, hidden=(H, H), act=act, B=shape["B"], gamma=ak["gamma"], tau=ak["soft_tau"],
                     lr_q=ak["q_crit_lr"], lr_pi=ak["mbpo_actor_lr"], lr_alpha=ak["mbpo_alpha_lr"],
-                    init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(64, 64),
+                    init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(MH, MH),
                     model_act="relu", lr_model=ak["model_lr"])
     st = _oracle_state(alg_obj, ocfg)
     expert = None
@@ -122,15 +131,22 @@ def test_train_loop_matches_oracle(gpu_available, alg, flags):
     orc = LoopOracle(alg, ocfg, st, oenvs[0], oenvs[2], expert, ok, rs_state, ak["alg_seed"],
                      max_episode_steps=1000).train(total)
     ref = np.array([[u["q1_loss"], u["q2_loss"], u["p_loss"], u["alpha_loss"]] for u in orc.update_stats])
-    assert dev.shape[0] == ref.shape[0], (dev.shape, ref.shape)
-    errs = [_series_err(dev[:, c], ref[:, c]) for c in range(4)]
-    print(f"{alg} {flags}: {n_upd} updates, errors q1 {errs[0]:.2e} q2 {errs[1]:.2e} p {errs[2]:.2e} "
-          f"alpha {errs[3]:.2e}")
+    env32 = None
+    if fp32_envelope:
+        # the drift a faithful fp32 execution has: the same loop in fp32 against the fp64 one
+        e32 = _fresh_envs(shape)
+        ex32 = None if expert is None else ([w.astype(np.float32) for w in expert[0]], expert[1].astype(np.float32))
+        o32 = LoopOracle(alg, ocfg, st.astype(np.float32), e32[0], e32[2], ex32, ok, rs_state, ak["alg_seed"],
+                         max_episode_steps=1000).train(total)
+        r32 = np.array([[u["q1_loss"], u["q2_loss"], u["p_loss"], u["alpha_loss"]] for u in o32.update_stats])
+        env32 = [_series_err(r32[:, c], ref[:, c]) for c in range(4)]
+    return alg_obj, ak, name, dev, dev_rng, orc, ref, env32
+
+
+def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc):
     assert len(dev_rng) == len(orc.episode_rng)
     for i, (a, b) in enumerate(zip(dev_rng, orc.episode_rng)):
         assert _same_stream(a, b), f"global stream differs at episode boundary {i}"
-    assert max(errs[:3]) < LOSS_TOL, errs
-    assert errs[3] < 10 * LOSS_TOL, errs
     if "--update_normalizers" in flags:
         for which in ("normalizer", "model_normalizer"):
             mine, theirs = getattr(alg_obj, which), getattr(orc, which)
@@ -151,5 +167,56 @@ def test_train_loop_matches_oracle(gpu_available, alg, flags):
         assert len(dd) == len(od)
         np.testing.assert_allclose(dd, od[:, 0], rtol=1e-4)
         np.testing.assert_allclose(dc, od[:, 1], rtol=1e-4)
+        ml = np.asarray(log["train"]["model_loss_last"], np.float64)
+        assert len(ml) == len(orc.fit_last)
+        np.testing.assert_allclose(ml, np.array(orc.fit_last), rtol=1e-4)   # sum over the models, last fit step
         os.remove(os.path.join(ak["save_path"], name))
+
+
+@pytest.mark.parametrize("alg,flags", [
+    ("sac_imit", []),
+    ("sac_imit", ["--update_normalizers"]),
+    ("sac_imit", ["--update_normalizers", "--only_model_normalizer"]),
+    ("sac_imit", ["--model_holdout_ratio", "0.2"]),
+    ("sac_imit", ["--update_normalizers", "--s_noise_std", "0.3"]),
+    ("sac_imit", ["--update_normalizers", "--s_noise_std", "0.3", "--s_noise_type", "next"]),
+    ("sac", []),
+    ("sac", ["--update_normalizers"]),
+    ("sac", ["--update_normalizers", "--s_noise_std", "0.5"]),
+])
+def test_train_loop_matches_oracle(gpu_available, alg, flags):
+    alg_obj, ak, name, dev, dev_rng, orc, ref, _ = _run(alg, flags)
+    assert dev.shape[0] == ref.shape[0], (dev.shape, ref.shape)
+    errs = [_series_err(dev[:, c], ref[:, c]) for c in range(4)]
+    print(f"{alg} {flags}: {dev.shape[0]} updates, errors q1 {errs[0]:.2e} q2 {errs[1]:.2e} p {errs[2]:.2e} "
+          f"alpha {errs[3]:.2e}")
+    _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc)
+    assert max(errs[:3]) < LOSS_TOL, errs
+    assert errs[3] < 10 * LOSS_TOL, errs
+    alg_obj.engine.close()
+
+
+@pytest.mark.parametrize("alg,act,flags", [
+    ("sac_imit", "tanh", []),                       # the parser's default activation, 2 world models
+    ("sac_imit", "relu", ["--num_models", "1"]),
+    ("sac", "tanh", []),
+    ("sac", "relu", []),
+])
+def test_train_loop_bench_config(gpu_available, alg, act, flags):
+    """The loops at the metric's shapes (256x2, B = 256, 512x2 models, minibatch 200, three
+    100-step episodes after a 400-step collection): the global stream bit for bit at every episode
+    boundary; every update's losses within 1e-4 relative over the first 100 updates and, over the
+    whole run, within the drift a faithful fp32 execution has (2x the fp32-vs-fp64 oracle error
+    + 1e-5 per series)."""
+    alg_obj, ak, name, dev, dev_rng, orc, ref, env32 = _run(alg, flags, shape=BENCH, act=act, fp32_envelope=True)
+    assert dev.shape[0] == ref.shape[0] >= 200, (dev.shape, ref.shape)
+    head = [_series_err(dev[:100, c], ref[:100, c]) for c in range(4)]
+    full = [_series_err(dev[:, c], ref[:, c]) for c in range(4)]
+    print(f"{alg} {act} {flags}: {dev.shape[0]} updates; first 100: {['%.2e' % e for e in head]}; "
+          f"all: {['%.2e' % e for e in full]}; fp32 oracle drift {['%.2e' % e for e in env32]}")
+    _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc)
+    assert max(head[:3]) < LOSS_TOL, head
+    assert head[3] < 10 * LOSS_TOL, head
+    for c in range(4):
+        assert full[c] <= 2 * env32[c] + 1e-5 or full[c] < LOSS_TOL, (c, full, env32)
     alg_obj.engine.close()
