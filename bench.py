@@ -243,20 +243,53 @@ def host_cpu_info():
 
 
 def cpu_baseline(cfgd, seconds=10.0):
-    """The CPU oracle (numpy fp32 port of the reference update, oracle/sac_oracle.py) on the
-    host cores: timed at 1 BLAS thread and at every usable core; ``value`` is the faster."""
+    """The reference-equivalent CPU path on the host cores (TensorFlow is not installable, so the
+    reference itself cannot run): ``oracle/sac_eager_torch.py``, an eager op-by-op PyTorch-CPU
+    restatement of ``_update`` with the reference's per-op dispatch structure and Keras Adam
+    (SURVEY.md §8d), timed at 1 thread and at every usable core; ``value`` is the faster.  Beside
+    it: the vectorised NumPy fp32 oracle (no per-op dispatch: an upper bound on a CPU port), and
+    config C1 (SAC-EO: the expert term through two 512x2 world models, plus the per-episode model
+    fit amortised at the reference defaults: 5 fit steps per update)."""
     total, usable, model = host_cpu_info()
-    runs = {}
-    for th in sorted({1, usable}):
-        runs[th] = _cpu_port_rate(cfgd, seconds / (2 if usable > 1 else 1), th)
-    best = max(runs, key=lambda t: runs[t][0])
-    v, n, el = runs[best]
+    q = seconds / 4.0
+    eager = {th: _eager_rate(cfgd, q / (2 if usable > 1 else 1), th) for th in sorted({1, usable})}
+    best = max(eager, key=lambda t: eager[t][0])
+    v, n, el = eager[best][:3]
+    npy = {th: _cpu_port_rate(cfgd, q / (2 if usable > 1 else 1), th) for th in sorted({1, usable})}
+    nb = max(npy, key=lambda t: npy[t][0])
+    c1 = _eager_c1(cfgd, q, best)
     return {"value": round(v, 3), "unit": "gradient-steps/s", "cores": best, "kind": "port",
-            "value_1thread": round(runs[1][0], 3), "value_all_cores": round(runs[usable][0], 3),
+            "path": "reference-equivalent: eager op-by-op PyTorch-CPU restatement of _update "
+                    "(oracle/sac_eager_torch.py; TensorFlow reference not installable)",
+            "value_1thread": round(eager[1][0], 3), "value_all_cores": round(eager[usable][0], 3),
             "cores_usable": usable, "os_cpu_count": total, "cpu_model": model,
-            "sample": f"{n} updates of the numpy fp32 oracle (oracle/sac_oracle.py) at the bench shapes in "
-                      f"{el:.1f}s at {best} BLAS thread(s) (also timed at 1 and {usable} threads); "
-                      "TensorFlow reference not installable"}
+            "sample": f"{n} eager updates at the bench shapes in {el:.1f}s at {best} thread(s) "
+                      f"(also timed at 1 and {usable} threads)",
+            "numpy_oracle": {"value": round(npy[nb][0], 3), "cores": nb, "value_1thread": round(npy[1][0], 3),
+                             "value_all_cores": round(npy[usable][0], 3),
+                             "path": "vectorised NumPy fp32 oracle (oracle/sac_oracle.py), no per-op dispatch"},
+            "c1_sac_eo": c1}
+
+
+def _eager_rate(cfgd, seconds, threads, use_expert=False):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sac_oracle as O
+    import sac_eager_torch as E
+    ocfg = O.Config(S=cfgd["S"], A=cfgd["A"], B=cfgd["B"], hidden=cfgd["hidden"], act="relu")
+    st = O.init_state(ocfg, seed=1, with_models=use_expert)
+    return E.time_updates(st, ocfg, seconds, threads, use_expert=use_expert)
+
+
+def _eager_c1(cfgd, seconds, threads):
+    """Config C1 on the CPU: SAC-EO updates (expert term, 2 world models 512x2, 20 expert rows) and
+    model-fit steps (2 x minibatch 200) of the eager restatement; per update the reference also
+    runs 5 fit steps at its defaults (1e5 model rows x 10 epochs / 200 per episode of 1,000 steps)."""
+    import sac_eager_torch as E
+    r, n, el, eng, buf = _eager_rate(cfgd, seconds / 2, threads, use_expert=True)
+    f, nf, elf = E.time_model_fit(eng, buf, eng.cfg, seconds / 2)
+    return {"updates_per_s": round(r, 3), "fit_steps_per_s": round(f, 3),
+            "value": round(1.0 / (1.0 / r + 5.0 / f), 3), "unit": "gradient-steps/s incl. amortised model fit",
+            "cores": threads, "sample": f"{n} SAC-EO updates and {nf} model-fit steps (eager PyTorch-CPU)"}
 
 
 def _cpu_port_rate(cfgd, seconds, threads):
@@ -447,7 +480,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--config", default="hc", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--mode", default="replicas", choices=["replicas", "dp"],

@@ -162,7 +162,7 @@ struct sacx_handle {
     bool nccl_failed = false;
     // world-model fitting, per seed (packed seeds fit one seed at a time: its arena block's plan)
     std::vector<std::vector<Launch>> mplans;
-    std::vector<hipGraphExec_t> mgraphs;
+    std::vector<std::map<int, hipGraphExec_t>> mgraphs;   // per seed: fit steps per graph -> graph
     std::vector<int64_t> mfit_hosts;   // model steps issued per seed (mirror ctl->mfit_seq)
     std::vector<GemmProb> probs;
     int probs_cursor = 0;
@@ -266,6 +266,7 @@ bool spec_mode(const sacx_handle* h) {
     } while (0)
 
 constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
+constexpr int MFIT_GRAPH = 64;      // model-fit steps per captured graph (then 8, then 1)
 constexpr int STAGE_CAP = SACX_STAGE_FLOATS;   // floats in the pinned host staging buffer of the _host entry points
 constexpr int ROLL_CAP = 4096;  // trajectories per sacx_rollout launch chain
 
@@ -1804,8 +1805,8 @@ void sacx_destroy(sacx_handle* h) {
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     if (h->act_ev) (void)hipEventDestroy(h->act_ev);
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
-    for (auto g : h->mgraphs)
-        if (g) (void)hipGraphExecDestroy(g);
+    for (auto& m : h->mgraphs)
+        for (auto& kv : m) (void)hipGraphExecDestroy(kv.second);
     for (auto& kv : h->roll_graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto e : h->events) (void)hipEventDestroy(e);
     if (h->pin) (void)hipHostFree(h->pin);
@@ -1905,7 +1906,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
                 return fail(h, "internal: GEMM problem table mismatch");
     }
     h->mplans.assign(h->seeds, {});
-    h->mgraphs.assign(h->seeds, nullptr);
+    h->mgraphs.assign(h->seeds, {});
     h->mfit_hosts.assign(h->seeds, 0);
     {
         const int cur = h->probs_cursor;
@@ -2460,27 +2461,45 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
     const std::vector<Launch>& mplan = h->mplans[k];
     const int R2 = h->nm * h->mb;
     int32_t* ring = h->ptr<int32_t>("mfit.idx");
+    // every step's launches read their minibatch rows from the index ring at ctl->mfit_seq, so a
+    // graph of several steps replays them back to back (one graph launch per MFIT_GRAPH steps)
+    auto graph_of = [&](int n) -> hipGraphExec_t {
+        auto it = h->mgraphs[k].find(n);
+        if (it != h->mgraphs[k].end()) return it->second;
+        hipGraphExec_t ex = nullptr;
+        if (hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return nullptr;
+        for (int j = 0; j < n; ++j)
+            for (const Launch& L : mplan) enqueue(L, h, h->cap_stream);
+        hipGraph_t graph;
+        if (hipStreamEndCapture(h->cap_stream, &graph) != hipSuccess) return nullptr;
+        const hipError_t e = hipGraphInstantiateWithFlags(&ex, graph, 0);
+        (void)hipGraphDestroy(graph);
+        if (e != hipSuccess) return nullptr;
+        h->mgraphs[k][n] = ex;
+        return ex;
+    };
     for (int64_t done = 0; done < n_steps;) {
         const int64_t chunk = std::min<int64_t>(n_steps - done, h->mfit_cap);
         HIPCHK(h, hipStreamSynchronize(h->stream));   // ring slots of earlier chunks are consumed
-        for (int64_t j = 0; j < chunk; ++j) {
-            const int64_t slot = (h->mfit_hosts[k] + done + j) % h->mfit_cap;
-            HIPCHK(h, hipMemcpy(ring + slot * R2, idx + (done + j) * R2, sizeof(int32_t) * R2, hipMemcpyHostToDevice));
-        }
+        // the chunk's slots are contiguous modulo the ring: at most two copies
+        const int64_t s0 = (h->mfit_hosts[k] + done) % h->mfit_cap;
+        const int64_t first = std::min<int64_t>(chunk, h->mfit_cap - s0);
+        HIPCHK(h, hipMemcpy(ring + s0 * R2, idx + done * R2, sizeof(int32_t) * R2 * first, hipMemcpyHostToDevice));
+        if (chunk > first)
+            HIPCHK(h, hipMemcpy(ring, idx + (done + first) * R2, sizeof(int32_t) * R2 * (chunk - first),
+                                hipMemcpyHostToDevice));
         if (flags & SACX_STEP_EAGER) {
             for (int64_t j = 0; j < chunk; ++j)
                 for (const Launch& L : mplan) enqueue(L, h, h->stream);
             HIPCHK(h, hipGetLastError());
         } else {
-            if (!h->mgraphs[k]) {
-                HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
-                for (const Launch& L : mplan) enqueue(L, h, h->cap_stream);
-                hipGraph_t graph;
-                HIPCHK(h, hipStreamEndCapture(h->cap_stream, &graph));
-                HIPCHK(h, hipGraphInstantiateWithFlags(&h->mgraphs[k], graph, 0));
-                HIPCHK(h, hipGraphDestroy(graph));
+            for (int64_t j = 0; j < chunk;) {
+                const int n = chunk - j >= MFIT_GRAPH ? MFIT_GRAPH : chunk - j >= 8 ? 8 : 1;
+                hipGraphExec_t ex = graph_of(n);
+                if (!ex) return fail(h, "model-fit graph capture");
+                HIPCHK(h, hipGraphLaunch(ex, h->stream));
+                j += n;
             }
-            for (int64_t j = 0; j < chunk; ++j) HIPCHK(h, hipGraphLaunch(h->mgraphs[k], h->stream));
         }
         done += chunk;
     }
