@@ -98,6 +98,34 @@ def train_packed(inputs_list):
     return run_lockstep(algs, shared, inputs_list[0]["alg_kwargs"]["total_timesteps"], inputs_list)
 
 
+def _train_runs(runs, run_inputs, args, local_rank=None):
+    """One process's share of the runs: lock-step packed seeds of one handle where that holds,
+    else one after another.  Returns {run: checkpoint name}."""
+    if local_rank is not None:
+        import torch
+        torch.cuda.set_device(local_rank)
+    if len(runs) > 1 and lockstep_ok(args, run_inputs[0]["env_kwargs"], len(runs)):
+        return dict(zip(runs, train_packed(run_inputs)))
+    return {r: train(d) for r, d in zip(runs, run_inputs)}
+
+
+def _pool_worker(job):
+    runs, run_inputs, args, local_rank = job
+    return _train_runs(runs, run_inputs, args, local_rank)
+
+
+def pool_size(args, n_runs: int) -> int:
+    """Processes per GPU for the runs of one rank: the reference's Pool(--cores) (train.py:148-152;
+    default one per run), capped by the usable host cores and by MAX_PROCS_PER_GPU (each process
+    holds its own device context and arena); each process trains its runs as packed seeds."""
+    want = args.cores if args.cores is not None else n_runs
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    return max(1, min(want, n_runs, usable, MAX_PROCS_PER_GPU))
+
+
+MAX_PROCS_PER_GPU = int(os.environ.get("SACX_MAX_PROCS_PER_GPU", "4"))
+
+
 def main(argv=None):
     start = datetime.now()
     args = create_train_parser().parse_args(argv)
@@ -107,10 +135,9 @@ def main(argv=None):
     seeds = derive_seeds(args.seed, args.runs, args.runs_start)
     runs = list(range(args.runs))
     ws = int(os.environ.get("WORLD_SIZE", "1"))
+    local = None
     if ws > 1:
-        import torch
         rank, local = int(os.environ.get("RANK", "0")), int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(local)
         runs = runs[rank::ws]
     names, run_inputs = {}, []
     for r in runs:
@@ -125,11 +152,17 @@ def main(argv=None):
                 sk[key] = int(seeds[kind][r])
         sk["algorithm_seed"] = int(seeds["algorithm"][r]) if args.alg_seed is None else int(args.alg_seed)
         run_inputs.append(import_inputs(d))          # train_utils.py:20-92 (no-op without --import_file)
-    if len(runs) > 1 and lockstep_ok(args, inputs_dict["env_kwargs"], len(runs)):
-        names = dict(zip(runs, train_packed(run_inputs)))
+    P = pool_size(args, len(runs))
+    if P > 1:
+        # the reference's process pool (train.py:151-152): P spawned processes share this GPU, each
+        # with runs r, r + P, ... as lock-step packed seeds; this process never touches the GPU
+        import multiprocessing as mp
+        jobs = [(runs[i::P], run_inputs[i::P], args, local) for i in range(P)]
+        with mp.get_context("spawn").Pool(P) as pool:
+            for part in pool.map(_pool_worker, jobs):
+                names.update(part)
     else:
-        for r, d in zip(runs, run_inputs):
-            names[r] = train(d)
+        names = _train_runs(runs, run_inputs, args, local)
     if ws > 1:                                       # every rank's runs are on disk before gathering
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -88,11 +88,14 @@ def _logs_equal(a, b):
     _same(a["final"], b["final"], "final")
 
 
-@pytest.mark.parametrize("alg,extra", [("sac_imit", []), ("sac", []),
-                                       ("sac_imit", ["--update_normalizers", "--only_model_normalizer"])])
+@pytest.mark.parametrize("alg,extra", [("sac_imit", ["--cores", "1"]), ("sac", ["--cores", "1"]),
+                                       ("sac_imit", ["--cores", "1", "--update_normalizers", "--only_model_normalizer"]),
+                                       ("sac_imit", ["--cores", "2"])])
 def test_packed_runs_equal_serial_runs(gpu_available, tmp_path, alg, extra):
-    """--runs 3 as three lock-step seeds of one packed handle (sac_eo.algs.lockstep) vs the same
-    three runs one after another: every run's log identical, bit for bit."""
+    """--runs 3 as three lock-step seeds of one packed handle (sac_eo.algs.lockstep) -- or, with
+    --cores 2, as two spawned processes on the GPU with runs {0, 2} packed and {1} alone (the
+    reference's process pool) -- vs the same three runs one after another: every run's log
+    identical, bit for bit."""
     from sac_eo.train import main
     from sac_eo.common.logger import load_log
     argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", "64", "64",
@@ -101,7 +104,7 @@ def test_packed_runs_equal_serial_runs(gpu_available, tmp_path, alg, extra):
             "--env_horizon", "200", "--sac_batch_size", "64", "--model_batch_size", "50",
             "--model_num_epochs", "1", "--seed", "11", "--runs", "3"] + extra
     packed = load_log(main(argv + ["--save_path", str(tmp_path / "packed")]))
-    serial = load_log(main(argv + ["--serial_runs", "--save_path", str(tmp_path / "serial")]))
+    serial = load_log(main(argv + ["--serial_runs", "--cores", "1", "--save_path", str(tmp_path / "serial")]))
     assert len(packed) == len(serial) == 3
     for a, b in zip(packed, serial):
         _logs_equal(a, b)

@@ -50,14 +50,27 @@ def test_packed_runs_host(monkeypatch, tmp_path, alg):
         orig(self, cfg, *a, **k)
         engines.append(self)
     monkeypatch.setattr(fake_engine.FakeEngine, "__init__", track)
-    packed = load_log(main(_argv(alg, tmp_path / "p", ["--runs", "3"])))
+    packed = load_log(main(_argv(alg, tmp_path / "p", ["--runs", "3", "--cores", "1"])))
     big = [e for e in engines if e.seeds == 3]
     assert len(big) == 1 and big[0].cfg.single_seed_plan
     steps = [c for c in big[0].calls if isinstance(c, tuple)]
     assert big[0].calls.count("act_seeds") == 300 + 2300 and big[0].calls.count("append_seeds") == 2300
     assert len(steps) == (2300 if alg == "sac_imit" else 2 * 334 + 1 * 100)
-    serial = load_log(main(_argv(alg, tmp_path / "s", ["--runs", "3", "--serial_runs"])))
+    serial = load_log(main(_argv(alg, tmp_path / "s", ["--runs", "3", "--serial_runs", "--cores", "1"])))
     for a, b in zip(packed, serial):
         for k in a["train"]:
             if "time" not in k:
                 assert np.array_equal(np.asarray(a["train"][k]), np.asarray(b["train"][k]), equal_nan=True), k
+
+
+def test_pool_size_and_split():
+    """--cores as the reference's Pool size (train.py:148-152): default one process per run, capped
+    by the usable cores and MAX_PROCS_PER_GPU; runs dealt round-robin over the processes."""
+    import argparse
+    from sac_eo import train as T
+    ns = lambda cores: argparse.Namespace(cores=cores)
+    usable = len(__import__("os").sched_getaffinity(0))
+    assert T.pool_size(ns(None), 1) == 1
+    assert T.pool_size(ns(1), 8) == 1
+    assert T.pool_size(ns(None), 8) == min(8, usable, T.MAX_PROCS_PER_GPU)
+    assert T.pool_size(ns(3), 2) == min(2, usable)

@@ -1,5 +1,7 @@
-"""Wall time of ``python -m sac_eo.train --runs K`` as K lock-step packed seeds vs the same K runs
-one after another (--serial_runs), on one GPU.  Usage: packed_runs_time.py [K] [alg] [steps]."""
+"""Wall time of ``python -m sac_eo.train --runs K`` on one GPU: the K runs one after another
+(--serial_runs --cores 1), as K lock-step packed seeds of one handle (--cores 1), and as P spawned
+processes (--cores P) each packing K/P seeds -- the reference's process pool.
+Usage: packed_runs_time.py [K] [alg] [steps] [P,P,...]."""
 import os
 import sys
 import tempfile
@@ -14,20 +16,24 @@ import numpy as np   # noqa: E402
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 alg = sys.argv[2] if len(sys.argv) > 2 else "sac_imit"
 steps = int(sys.argv[3]) if len(sys.argv) > 3 else 3000
+pools = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else [2, 4]
 argv = ["--alg_type", alg, "--env_name", "HalfCheetah-v3", "--actor_layers", "256", "256",
         "--critic_layers", "256", "256", "--actor_activations", "relu", "--critic_activations", "relu",
         "--total_timesteps", str(steps), "--env_batch_size_init", "1000", "--model_num_epochs", "1",
         "--seed", "0", "--runs", str(K)]
-out = {}
-for mode in ("packed", "serial"):
+modes = [("serial", ["--serial_runs", "--cores", "1"]), ("packed", ["--cores", "1"])] + \
+        [(f"pool{p}", ["--cores", str(p)]) for p in pools]
+out, ref = {}, None
+for mode, extra in modes:
     d = tempfile.mkdtemp()
     t0 = time.perf_counter()
-    path = main(argv + ["--save_path", d] + (["--serial_runs"] if mode == "serial" else []))
+    path = main(argv + ["--save_path", d] + extra)
     out[mode] = time.perf_counter() - t0
     logs = load_log(path)
-    parts = {k: sum(float(np.sum(lg["train"].get(k, 0.0))) for lg in logs)
-             for k in ("time_env_data", "time_model_fit", "expert_time")}
-    print(f"  {mode} parts summed over runs (s): " + ", ".join(f"{k} {v:.2f}" for k, v in parts.items()))
-    print(f"{mode}: {K} runs of {alg} (256x2, {steps} steps: 1000 collected, {steps - 1000} loop steps with updates) "
-          f"in {out[mode]:.1f} s", flush=True)
-print(f"packed / serial speed-up: {out['serial'] / out['packed']:.2f}x")
+    if ref is None:
+        ref = logs
+    same = all(np.array_equal(np.asarray(a["train"][k]), np.asarray(b["train"][k]), equal_nan=True)
+               for a, b in zip(logs, ref) for k in a["train"] if "time" not in k)
+    print(f"{mode}: {K} runs of {alg} (256x2, {steps} steps: 1000 collected, {steps - 1000} loop steps with "
+          f"updates) in {out[mode]:.1f} s = {out['serial'] / out[mode]:.2f}x serial; logs equal serial: {same}",
+          flush=True)
