@@ -1,0 +1,56 @@
+#!/bin/bash
+# One gpurun call = a list of named steps, run in order; stops at the first failing step (a test
+# failure too: nothing after it is trusted).  Logs under gpurun_out/${TAG:-run}/.
+#   bash tools/gpu_run.sh tests [pytest selectors, comma-separated] | smoke | bench[=<bench args>]
+#                         | driver | mfit | humanoid | prof=<config> | pmc=<config> | ktime=<config> ...
+# e.g. bash tools/gpu_run.sh tests smoke bench "bench=--config hc_eo --no-cpu-baseline" prof=hc
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/${TAG:-run}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+n=0
+value() { grep -o '"value": [0-9.]*' "$1" | head -1; }
+for step in "$@"; do
+  n=$((n + 1))
+  name=${step%%=*}; arg=""; [ "$name" != "$step" ] && arg=${step#*=}
+  log=$OUT/$n-$name.log
+  case $name in
+    tests)
+      sel=${arg:-tests}
+      timeout -k 10 1100 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+          ${sel//,/ } > "$log" 2>&1
+      rc=$?; echo "[$n tests] rc=$rc $(tail -n 1 "$log")" ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1
+      rc=$?; echo "[$n smoke] rc=$rc $(tail -n 1 "$log")" ;;
+    bench)
+      timeout -k 10 500 python bench.py $arg > "$log" 2>&1
+      rc=$?; echo "[$n bench $arg] rc=$rc $(value "$log")" ;;
+    driver)     # the driver's own command
+      timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > "$log" 2>&1
+      rc=$?; echo "[$n driver] rc=$rc $(value "$log")" ;;
+    mfit)       # world-model fit (A16) at HC and Humanoid shapes
+      { timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
+        timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
+      rc=$?; echo "[$n mfit] rc=$rc"; cat "$log" ;;
+    humanoid)
+      rc=0
+      for c in humanoid_sac humanoid_bf16 humanoid_eo; do
+        timeout -k 10 300 python bench.py --config $c --steps 1000 --warmup 100 --no-cpu-baseline > "$OUT/$n-$c.log" 2>&1
+        rc=$?; echo "[$n $c] rc=$rc $(value "$OUT/$n-$c.log")"; [ $rc -eq 0 ] || break
+      done ;;
+    prof)       # rocprofv3 kernel-trace stats of the one-seed bench of config $arg
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof_${arg:-hc}" -o s \
+          -- python bench.py --config "${arg:-hc}" --steps 2000 --warmup 200 --no-cpu-baseline --packed-leg 0 > "$log" 2>&1
+      rc=$?; echo "[$n prof ${arg:-hc}] rc=$rc $(value "$log")" ;;
+    pmc)
+      CONFIG=${arg:-hc} bash tools/gpu_pmc.sh > "$log" 2>&1
+      rc=$?; echo "[$n pmc ${arg:-hc}] rc=$rc"; tail -n 3 "$log" ;;
+    ktime)
+      timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
+      rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+  [ $rc -eq 0 ] || { tail -n 30 "$log"; exit $rc; }
+done
