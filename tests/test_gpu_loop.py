@@ -87,6 +87,11 @@ def _series_err(dev, ref):
     return float(np.max(np.abs(dev - ref)) / max(np.max(np.abs(ref)), 1e-30))
 
 
+def _rel_drift(a, b):
+    """Largest elementwise relative difference (per episode: the diagnostics are not a series)."""
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-30))) if b.size else 0.0
+
+
 def _same_stream(a, b):
     return np.array_equal(a[1], b[1]) and a[2] == b[2] and a[3] == b[3] and a[4] == b[4]
 
@@ -140,10 +145,16 @@ def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
                          max_episode_steps=1000).train(total)
         r32 = np.array([[u["q1_loss"], u["q2_loss"], u["p_loss"], u["alpha_loss"]] for u in o32.update_stats])
         env32 = [_series_err(r32[:, c], ref[:, c]) for c in range(4)]
+        if alg == "sac_imit":
+            # the same drift for the per-episode diagnostics (model MSEs) and last fit losses
+            env32.append(_rel_drift(np.array(o32.diag), np.array(orc.diag)))
+            env32.append(_rel_drift(np.array(o32.fit_last), np.array(orc.fit_last)))
     return alg_obj, ak, name, dev, dev_rng, orc, ref, env32
 
 
-def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc):
+def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, env32=None):
+    """env32 (bench shapes): the diagnostics and fit losses may differ from the fp64 loop by what a
+    faithful fp32 execution of the same loop does (2x its drift), at least 1e-4 relative."""
     assert len(dev_rng) == len(orc.episode_rng)
     for i, (a, b) in enumerate(zip(dev_rng, orc.episode_rng)):
         assert _same_stream(a, b), f"global stream differs at episode boundary {i}"
@@ -165,11 +176,16 @@ def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc):
         dc = np.asarray(log["train"]["model_MSE_on_expert_counterfactual_action"], np.float64)
         od = np.array(orc.diag)
         assert len(dd) == len(od)
-        np.testing.assert_allclose(dd, od[:, 0], rtol=1e-4)
-        np.testing.assert_allclose(dc, od[:, 1], rtol=1e-4)
+        tol_d = 1e-4 if env32 is None else max(1e-4, 2 * env32[4])
+        tol_f = 1e-4 if env32 is None else max(1e-4, 2 * env32[5])
+        print(f"diagnostics: rel err {_rel_drift(np.stack([dd, dc], 1), od[:, :2]):.2e} (tol {tol_d:.2e}), "
+              f"fit loss {_rel_drift(np.asarray(log['train']['model_loss_last'], np.float64), np.array(orc.fit_last)):.2e} "
+              f"(tol {tol_f:.2e})")
+        np.testing.assert_allclose(dd, od[:, 0], rtol=tol_d)
+        np.testing.assert_allclose(dc, od[:, 1], rtol=tol_d)
         ml = np.asarray(log["train"]["model_loss_last"], np.float64)
         assert len(ml) == len(orc.fit_last)
-        np.testing.assert_allclose(ml, np.array(orc.fit_last), rtol=1e-4)   # sum over the models, last fit step
+        np.testing.assert_allclose(ml, np.array(orc.fit_last), rtol=tol_f)   # sum over the models, last fit step
         os.remove(os.path.join(ak["save_path"], name))
 
 
@@ -214,7 +230,7 @@ def test_train_loop_bench_config(gpu_available, alg, act, flags):
     full = [_series_err(dev[:, c], ref[:, c]) for c in range(4)]
     print(f"{alg} {act} {flags}: {dev.shape[0]} updates; first 100: {['%.2e' % e for e in head]}; "
           f"all: {['%.2e' % e for e in full]}; fp32 oracle drift {['%.2e' % e for e in env32]}")
-    _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc)
+    _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, env32)
     assert max(head[:3]) < LOSS_TOL, head
     assert head[3] < 10 * LOSS_TOL, head
     for c in range(4):
