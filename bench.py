@@ -391,6 +391,39 @@ def world_model_legs(eng, cfgd, n_fit=200, n_roll=20):
              "transitions_per_s": round(5000 / roll_s, 1), "launches_per_step": 9, "graph": True})
 
 
+def model_fit_leg(rep, n_fit=512):
+    """SAC-EO's world-model fit (A16) at the HalfCheetah shapes of config C1 (the reference's default
+    algorithm: 2 world models 512x2, minibatch 200, SAC_expert.py:480-552 / mbrl_onpolicy_alg.py:301-319),
+    graph replay of the folded fit chain, timed after the main region on rank 0.  At the reference
+    defaults an episode runs ~5,000 fit steps beside its 1,000 updates."""
+    cfgd = dict(CONFIGS["hc_eo"], buffer=200_000)
+    eng = build_engine(cfgd, rep.seeds(0), device=rep.device)
+    mb = eng.cfg.model_batch
+    idx = np.random.RandomState(3).randint(cfgd["buffer"], size=(n_fit + 64, 2, mb))
+    eng.model_fit(idx[:64])
+    eng.sync()
+    t0 = time.perf_counter()
+    eng.model_fit(idx[64:])
+    eng.sync()
+    us = (time.perf_counter() - t0) / n_fit * 1e6
+    S, A, Hm = cfgd["S"], cfgd["A"], 512
+    macs = 3 * ((S + A) * Hm + Hm * Hm + Hm * (S + 1)) - (S + A) * Hm      # SURVEY.md section 8d model-fit row
+    flops = 2.0 * macs * 2 * mb
+    launches = eng.model_plan_info()
+    eng.close()
+    out = {"config": "HalfCheetah-shaped SAC-EO world-model fit: 2 models 512x2, minibatch 200 (config C1 shapes)",
+           "steps": n_fit, "us_per_step": round(us, 2), "steps_per_s": round(1e6 / us, 1),
+           "flops_per_step": flops, "achieved_tflops": round(flops / us / 1e6, 3),
+           "frac_fp32_peak": round(flops / us / 1e6 / FP32_PEAK_TFLOPS, 5), "graph": True}
+    gemms = [L for L in launches if L["kernel"] == "k_gemm"]
+    out["launches_per_step"] = len(launches)
+    out["launches"] = [L["name"] for L in launches]
+    out["us_per_launch"] = round(us / max(1, len(launches)), 3)
+    # the committed rocprofv3 --kernel-trace --stats summary of the fit (tools/gpu_run.sh mprof)
+    out.update(rocprof_family_avg("k_gemm", "mfit_hc", sum(L["flops"] for L in gemms) / max(1, len(gemms))))
+    return out
+
+
 def replica_seeds(rep, k):
     """The reference-style seeds of this replica's k learners: run indices rank*k .. rank*k+k-1
     of derive_seeds (sac_eo/train.py:108-118), one dict per learner."""
@@ -550,6 +583,9 @@ def main():
     fit = roll = None
     if rank == 0 and cfgd["use_expert"] and K == 1:
         fit, roll = world_model_legs(eng, cfgd)
+    mfit = None
+    if rank == 0 and not args.no_roofline and not dp and K == 1 and args.config == "hc":
+        mfit = model_fit_leg(rep)
     roof = None
     if rank == 0 and not args.no_roofline and not dp:
         roof, _ = roofline(eng, args.config)
@@ -588,6 +624,8 @@ def main():
         }
         if fit is not None:
             line["model_fit"], line["rollout"] = fit, roll
+        if mfit is not None:
+            line["model_fit_c1"] = mfit
         if loop is not None:
             line["drop_in_loop"] = loop
         if packed is not None:

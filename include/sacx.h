@@ -318,6 +318,9 @@ int sacx_dp_local_step(sacx_handle* const* handles, int32_t nranks, int64_t n_st
  * append of SAC_expert.py:779-797); the other steps drew their own.  -1 for a NULL handle. */
 int64_t sacx_spec_hits(const sacx_handle* h);
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);
+/* The launches of one world-model fitting step (sacx_model_fit) of the selected seed, as
+ * sacx_plan_info (use_expert handles; *n_out = 0 before the first sacx_model_fit builds them). */
+int sacx_model_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out);
 /* Runs n_steps updates eagerly with a HIP event around every launch on the
  * bound stream and returns the summed device milliseconds per launch index
  * (array of length n_launches from sacx_plan_info).  Each step is queued

@@ -572,6 +572,45 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
     }
 }
 
+// The end of a world-model fitting step (mbrl_onpolicy_alg.py:305-319): each model's loss
+// (reduce_mean over its minibatch) into the stats ring, loss_all = their sum, and the optimiser
+// step / fit sequence advanced.  k_mfinal (one wave, per-row losses of k_mloss) or one extra
+// workgroup of a later launch of the step (256 threads, the fit-loss epilogue's tile partials).
+__device__ void mfit_final(const MFinalArgs& f) {
+    __shared__ float mred[2][4];
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
+    const int n = f.nt > 0 ? f.mb * f.nt : f.mb;
+    float s0 = 0.f, s1 = 0.f;
+    for (int i = t; i < n; i += blockDim.x) {
+        s0 += f.loss_rows[i];
+        if (f.nm > 1) s1 += f.loss_rows[n + i];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (lane == 0) {
+        mred[0][wave] = s0;
+        mred[1][wave] = s1;
+    }
+    __syncthreads();
+    if (t == 0) {
+        float a0 = mred[0][0], a1 = mred[1][0];
+        for (int w = 1; w < nw; ++w) {
+            a0 += mred[0][w];
+            a1 += mred[1][w];
+        }
+        if (f.nt > 0) {        // partials of e^2: get_loss's 0.5 factor
+            a0 = 0.5f * a0;
+            a1 = 0.5f * a1;
+        }
+        const float l0 = a0 / (float)f.mb, l1 = a1 / (float)f.mb;
+        const int64_t seq = f.ctl->mfit_seq;
+        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = f.nm > 1 ? l0 + l1 : l0;     // loss_all (:305-312)
+        f.mstats[(size_t)(seq % f.mstats_cap) * 2 + 1] = (float)seq;
+        f.ctl->t_model += 1;
+        f.ctl->mfit_seq = seq + 1;
+    }
+}
+
 // MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
@@ -929,21 +968,24 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             }
         }
         if constexpr (MODE == GM_FWD) {
-            if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
+            if (g.mse) {          // uniform: the expert MSE / fit-loss epilogue (all 256 threads take part)
+                const bool fit = g.mse == 2;
                 float pred = v + e0[s];
                 // --delta_clip_pred (base_world_model.py:80-82): clip, no gradient outside [-c, c]
                 const bool pass = g.dclip <= 0.f || (pred >= -g.dclip && pred <= g.dclip);
                 if (g.dclip > 0.f) pred = fminf(fmaxf(pred, -g.dclip), g.dclip);
                 const float sp_hat = e1[s] + (pred * e4[s] + e3[s]);
-                const float diff = e2[s] - sp_hat;
+                const float diff = fit ? e1[s] - pred : e2[s] - sp_hat;
                 const float gscale = -es.eps * g.grad_scale;
-                float sq = out_ok ? diff * diff : 0.f;
+                const float cf = (fit && nn == g.N - 1) ? g.fcoef : 1.f;     // the reward column
+                float sq = out_ok ? diff * diff * cf : 0.f;
                 sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's sub-tile row
                 sq += __shfl_xor(sq, 4, 16);
                 sq += __shfl_xor(sq, 2, 16);
                 sq += __shfl_xor(sq, 1, 16);
                 if (out_ok) {
-                    st_out(&g.C[(size_t)mm * g.ldc + nn], pass ? (gscale * diff) * e4[s] : 0.f);
+                    st_out(&g.C[(size_t)mm * g.ldc + nn],
+                           fit ? -diff * (cf * g.grad_scale) : (pass ? (gscale * diff) * e4[s] : 0.f));
                     if (col == 0) st_out(&g.part[(size_t)mm * ((g.N + 15) >> 4) + 2 * tn + (s & 1)], sq);
                 }
                 continue;
@@ -957,7 +999,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
                 continue;
             }
-            const float lr_t = adam_lr(ga.adam, g.group, es.t + 1);
+            const float lr_t = adam_lr(ga.adam, g.group, es.t + 1 - ga.t_adv);
             const float gr = v * g.grad_scale;
             const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
             const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
@@ -1011,6 +1053,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     if (tile >= total_tiles) {
         if constexpr (ROWK > 0 && ROWK < 3) {   // horizontally fused Q-head rows
             qhead_block<ROWK - 1, NQ>(ga.qh, tile - total_tiles, so);
+        } else if constexpr (ROWK == 0 || ROWK == 7) {
+            if (ga.has_mfinal) mfit_final(ga.mfin);   // the world-model fit step's k_mfinal
         }
         return;
     }
@@ -1044,6 +1088,10 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec),
                      "s"(g.pw), "s"(g.ppart), "s"(g.pw_ld), "s"(g.pw_cs), "s"(g.pw_n), "s"(g.C));
+    } else if constexpr (MODE == GM_DX && ROWK == 7) {
+        asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
+                     "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec),
+                     "s"(g.gd), "s"(g.gst), "s"(g.gd_ld), "s"(g.g_o), "s"(g.gst_ld));
     } else if constexpr (MODE == GM_DX) {
         asm volatile("" ::"s"(g.A), "s"(g.B), "s"(g.lda), "s"(g.ldb), "s"(g.M), "s"(g.N), "s"(g.K), "s"(g.tiles_n),
                      "s"(g.tile_begin), "s"(g.act), "s"(g.wgen), "s"(g.gen_act), "s"(g.H), "s"(g.ldh), "s"(g.vec));
@@ -1080,7 +1128,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float e4 = 0.f;
     if constexpr (MODE == GM_FWD) {
         e0 = g.bias[nnc];
-        if constexpr (ROWK != 3 && ROWK != 5) {   // head-fused / actor launches: no mse problems
+        if constexpr (ROWK != 3 && ROWK != 5 && ROWK != 6) {   // head-fused / actor / fit launches: no mse problems
             // world-model head rows (mse): zero-sized resources when not an mse problem
             e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
             e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
@@ -1097,7 +1145,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         e3 = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
     }
     EpiScalars es{};
-    if constexpr (MODE == GM_DW || (MODE == GM_FWD && ROWK != 3 && ROWK != 5))
+    if constexpr (MODE == GM_DW || (MODE == GM_FWD && ROWK != 3 && ROWK != 5 && ROWK != 6))
         es = epi_scalars(sr(ga.ctl, so), g.group);
     // partial-dot weights of this thread's output column (zero-sized resource: no partials)
     constexpr bool PART = (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5);
@@ -1212,6 +1260,151 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         }
         a_lds = true;
     }
+    // rowk 6 (model.fwd0 of the fit): this lane's A row is replay record phys(idx[m]) and its
+    // tile row's (t >> 4) the one whose target columns the tile stores; every address is valid
+    // (clamped row, in-record columns) and out-of-range values are masked after the arithmetic
+    const float* grow = nullptr;
+    float traw0 = 0.f, traw1 = 0.f, tmu = 0.f, tden = 1.f;
+    int tcol = 0;
+    bool tstore = false;
+    if constexpr (MODE == GM_FWD && ROWK == 6) {
+        const MGatherArgs& mg = ga.mg;
+        const int64_t seq = mg.ctl->mfit_seq, start = mg.ctl->start;
+        const int32_t* ir = mg.idx_ring + (seq % mg.idx_cap) * (int64_t)(mg.nm * mg.mb) + (int64_t)p * mg.mb;
+        auto rec_of = [&](int row) {
+            int64_t phys = start + ir[min(row, g.M - 1)];
+            phys = phys >= mg.cap ? phys - mg.cap : phys;
+            return mg.replay + phys * (int64_t)mg.stride;
+        };
+        grow = rec_of(m);
+        // targets T[row][c] (get_loss :286-296): c < S the normalised delta sp - s, c == S the reward
+        const int S = mg.S, A = mg.A;
+        const float* trec = rec_of(mm);
+        tcol = tn * 16 + col;
+        tstore = mm < g.M && tcol <= S;
+        const int c = min(tcol, S);
+        traw0 = c < S ? trec[S + A + c] : trec[2 * S + A];
+        traw1 = c < S ? trec[c] : 0.f;
+        tmu = c < S ? mg.d_mean[c] : mg.r_norm[0];
+        tden = c < S ? mg.d_den[c] : mg.r_norm[1];
+    }
+    auto gather_a = [&](int k0, float (&a)[4], auto vt) {
+        constexpr bool V = decltype(vt)::value;
+        const MGatherArgs& mg = ga.mg;
+        const bool live = mok && k0 < g.K;
+        const int kb = k0 < g.K ? k0 : 0;
+        float raw[4];
+        if constexpr (V) {      // 16-B aligned: record stride and k0 are multiples of 4, r4(K) <= stride
+            const float4 q = *reinterpret_cast<const float4*>(grow + kb);
+            raw[0] = q.x; raw[1] = q.y; raw[2] = q.z; raw[3] = q.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) raw[j] = grow[min(kb + j, g.K - 1)];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int kc = min(kb + j, g.K - 1);
+            const float* mu = kc < mg.S ? mg.s_mean + kc : mg.a_mean + (kc - mg.S);
+            const float* den = kc < mg.S ? mg.s_den + kc : mg.a_den + (kc - mg.S);
+            float x = (raw[j] - *mu) / *den;          // k_mgather's normalisation
+            asm("" : "+v"(x));
+            a[j] = (live && kb + j < g.K) ? x : 0.f;
+        }
+        if (tn == 0 && mok && k0 < g.lda)        // X for model.adam's layer-0 dW (zero pad columns)
+            *reinterpret_cast<float4*>(const_cast<float*>(g.A) + (size_t)m * g.lda + k0) = float4{a[0], a[1], a[2], a[3]};
+    };
+    if constexpr (MODE == GM_DX && ROWK == 7) {
+        // model.bwd1 with model.bwd2 folded in (host: g_o <= 32, every problem a generated one).
+        // D3 operand of the generation, per output slab t and pair member j: lane (r, grp) holds
+        // D3[m0 + r][16 t + 4 grp + j] (zero past g_o / M), as model.bwd2's A operand
+        float d3[2][4];
+        const __amdgpu_buffer_rsrc_t rd = rs(g.gd);
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int o = 16 * t2 + 4 * grp + j;
+                d3[t2][j] = bload(rd, boff(mok && o < g.g_o, m * g.gd_ld + o));
+            }
+        const bool store = tn == 0 && mok;
+        auto gen_loop = [&](auto vt) {
+            constexpr bool V = decltype(vt)::value;
+            for (int it = it0; it < it1; it += 4) {
+                float a[4][4], b[4][4], w[4][2][4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int k0 = (it + u) * 16 + grp * 4;
+                    const int k0e = (it + u < it1) ? k0 : (1 << 30);
+                    load_a<true, V, false>(ra, g, m, mok, k0e, a[u], rw);      // H2
+                    load_b<true, V>(rb, g, n, nok, k0e, b[u]);
+                    // generation A operand: lane (r, grp) holds W2[16 (it + u) + r][16 t + 4 grp + j],
+                    // one 16-B load per slab t at a 4-B aligned offset (the host requires unaligned
+                    // dX loads); elements past g_o (the next row's) are zeroed
+                    const int kr = (it + u) * 16 + r;
+                    const bool kok = it + u < it1 && kr < g.K;
+#pragma unroll
+                    for (int t2 = 0; t2 < 2; ++t2) {
+                        const int o0 = 16 * t2 + 4 * grp;
+                        const float4 q = bload4(rw, boff(kok && o0 < g.g_o, kr * g.g_o + o0));
+                        w[u][t2][0] = q.x;
+                        w[u][t2][1] = o0 + 1 < g.g_o ? q.y : 0.f;
+                        w[u][t2][2] = o0 + 2 < g.g_o ? q.z : 0.f;
+                        w[u][t2][3] = o0 + 3 < g.g_o ? q.w : 0.f;
+                    }
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    // D2^T slab = W2 rows x D3^T: lane (r, grp) gets rows k = 16 (it+u) + 4 grp + q of
+                    // column m0 + r, exactly its A elements a[u][q]; per output slab the pairs
+                    // (j 0, 2) and (1, 3) accumulate apart, then the slabs add in wave order
+                    floatx4 pt[2];
+                    // an MFMA whose operands are zero in every lane (output columns 16 t + j past
+                    // g_o for all grp) is left out: it would add +0, which the +0 of the wave sum
+                    // below makes indistinguishable
+#pragma unroll
+                    for (int t2 = 0; t2 < 2; ++t2) {
+                        floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = {0.f, 0.f, 0.f, 0.f};
+                        const int live = g.g_o - 16 * t2;      // uniform
+                        if (live > 0) x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u][t2][0], d3[t2][0], x0, 0, 0, 0);
+                        if (live > 1) x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u][t2][1], d3[t2][1], x1, 0, 0, 0);
+                        if (live > 2) x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u][t2][2], d3[t2][2], x0, 0, 0, 0);
+                        if (live > 3) x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w[u][t2][3], d3[t2][3], x1, 0, 0, 0);
+                        pt[t2] = x0 + x1;
+                    }
+                    const int k0 = (it + u) * 16 + grp * 4;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        float v = pt[0][q] + pt[1][q];
+                        v = v + 0.f;          // model.bwd2's idle waves 2 and 3
+                        v = v + 0.f;
+                        a[u][q] = v * dact_f(a[u][q], g.gen_act);
+                    }
+                    if (store && it + u < it1)
+                        *reinterpret_cast<float4*>(&g.gst[(size_t)m * g.gst_ld + k0]) = float4{a[u][0], a[u][1], a[u][2], a[u][3]};
+                }
+                if constexpr (BF) {
+                    acc0 = mfma_bf16_2slab(a[0], a[1], b[0], b[1], acc0);
+                    acc1 = mfma_bf16_2slab(a[2], a[3], b[2], b[3], acc1);
+                    continue;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][0], b[u][0], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][1], b[u][1], acc1, 0, 0, 0);
+                    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][2], b[u][2], acc0, 0, 0, 0);
+                    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u][3], b[u][3], acc1, 0, 0, 0);
+                }
+            }
+        };
+        if constexpr (VEC == 1) {
+            if (g.vec) gen_loop(std::true_type{});
+            else gen_loop(std::false_type{});
+        } else {
+            gen_loop(std::false_type{});
+        }
+        a_lds = true;
+    }
     // float4 operand loads per problem (g.vec): a launch can mix problems with and without
     // them, and the loop is unswitched on the flag
     auto main_loop = [&](auto vt) {
@@ -1223,7 +1416,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             // iterations past it1 read a clamped (valid) slab and are zeroed
             const int k0 = (it + u) * 16 + grp * 4;
             const int k0e = (it + u < it1) ? k0 : (1 << 30);
-            load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, m, mok, k0e, a[u], rw);
+            if constexpr (MODE == GM_FWD && ROWK == 6) gather_a(k0e, a[u], vt);
+            else load_a<AKC, V && AKC, MODE == GM_DX>(ra, g, m, mok, k0e, a[u], rw);
             load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, n, nok, k0e, b[u]);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -1249,6 +1443,15 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         main_loop(std::false_type{});
     }
     GEMM_PH(2);
+    if constexpr (MODE == GM_FWD && ROWK == 6) {
+        const MGatherArgs& mg = ga.mg;
+        if (tstore) {
+            float y = tcol < mg.S ? ((traw0 - traw1) - tmu) / tden : (traw0 - tmu) / tden;
+            const float cl = tcol < mg.S ? mg.clip_d : mg.clip_r;
+            if (cl > 0.f) y = fminf(fmaxf(y, -cl), cl);
+            mg.T[(size_t)(p * mg.mb + mm) * (mg.S + 1) + tcol] = y;
+        }
+    }
     const floatx4 acc = acc0 + acc1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) red[wave][q][lane] = acc[q];
@@ -1260,22 +1463,25 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
-    if constexpr (MODE == GM_FWD && ROWK != 3 && ROWK != 5) {
-        if (g.mse) {          // uniform: the expert MSE epilogue (all 256 threads take part)
+    if constexpr (MODE == GM_FWD && ROWK != 3 && ROWK != 5 && ROWK != 6) {
+        if (g.mse) {          // uniform: the expert MSE / fit-loss epilogue (all 256 threads take part)
+            const bool fit = g.mse == 2;
             float pred = v + e0;
             // --delta_clip_pred (base_world_model.py:80-82): clip, no gradient outside [-c, c]
             const bool pass = g.dclip <= 0.f || (pred >= -g.dclip && pred <= g.dclip);
             if (g.dclip > 0.f) pred = fminf(fmaxf(pred, -g.dclip), g.dclip);
             const float sp_hat = e1 + (pred * e4 + e3);
-            const float diff = e2 - sp_hat;
+            const float diff = fit ? e1 - pred : e2 - sp_hat;
             const float gscale = -es.eps * g.grad_scale;
-            float sq = out_ok ? diff * diff : 0.f;
+            const float cf = (fit && nn == g.N - 1) ? g.fcoef : 1.f;     // the reward column
+            float sq = out_ok ? diff * diff * cf : 0.f;
             sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's tile row
             sq += __shfl_xor(sq, 4, 16);
             sq += __shfl_xor(sq, 2, 16);
             sq += __shfl_xor(sq, 1, 16);
             if (!out_ok) return;
-            st_out(&g.C[(size_t)mm * g.ldc + nn], pass ? (gscale * diff) * e4 : 0.f);
+            st_out(&g.C[(size_t)mm * g.ldc + nn],
+                   fit ? -diff * (cf * g.grad_scale) : (pass ? (gscale * diff) * e4 : 0.f));
             if (col == 0) st_out(&g.part[(size_t)mm * g.tiles_n + tn], sq);
             return;
         }
@@ -1314,7 +1520,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             return;
         }
-        const float lr_t = adam_lr(ga.adam, g.group, es.t + 1);
+        const float lr_t = adam_lr(ga.adam, g.group, es.t + 1 - ga.t_adv);
         const float gr = v * g.grad_scale;
         const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
         const float mm1 = e1 + (gr - e1) * (1.f - b1);
@@ -1696,7 +1902,7 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
             st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             continue;
         }
-        const float lr_t = adam_lr(ga.adam, g.group, es.t + 1);
+        const float lr_t = adam_lr(ga.adam, g.group, es.t + 1 - ga.t_adv);
         const float gr = v * g.grad_scale;
         const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
         const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
@@ -1720,7 +1926,7 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
 template <bool PK, bool T32>
 static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     const unsigned z = seeds_z(a.nseeds);
-    const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0), 1, z), block(256);
+    const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0) + (a.has_mfinal ? 1 : 0), 1, z), block(256);
     switch (a.mode) {
     case GM_FWD:
         if (a.rowk == 3) {                 // q.fwd0 with the actor head folded in
@@ -1742,6 +1948,16 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
                 if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, false, PK, T32>), grid, block, 0, s, a);
                 else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, false, PK, T32>), grid, block, 0, s, a);
             }
+        } else if (a.rowk == 6) {          // model.fwd0 of the fit, gathering its rows (one seed, 16x16)
+            if constexpr (!PK && !T32) {
+                if (a.bf16) {
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, true, false, false>), grid, block, 0, s, a);
+                    else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, true, false, false>), grid, block, 0, s, a);
+                } else {
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, false, false, false>), grid, block, 0, s, a);
+                    else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, false, false, false>), grid, block, 0, s, a);
+                }
+            }
         } else if (a.bf16) {
             if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, a);
             else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK, T32>), grid, block, 0, s, a);
@@ -1751,14 +1967,24 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
         }
         break;
     case GM_DX: {
-        const dim3 gx(a.total_tiles + (a.rowk && a.rowk < 3 ? a.row_blocks : 0), 1, z);
+        const dim3 gx(a.total_tiles + (a.rowk && a.rowk < 3 ? a.row_blocks : 0) + (a.has_mfinal ? 1 : 0), 1, z);
         const bool q8 = a.rowk && a.qh.H1 > 256;
 #define SACX_DX(V, R, Q)                                                                            \
     do {                                                                                           \
         if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK, T32>), gx, block, 0, s, a);          \
         else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK, T32>), gx, block, 0, s, a);                      \
     } while (0)
-        if (a.rowk == 4) {                 // actor.bwd1 with actor.head.bwd folded in (16x16 only)
+        if (a.rowk == 7) {                 // model.bwd1 with model.bwd2 folded in (one seed, 16x16)
+            if constexpr (!PK && !T32) {
+                if (a.bf16) {
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 7, 4, true, false, false>), gx, block, 0, s, a);
+                    else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 7, 4, true, false, false>), gx, block, 0, s, a);
+                } else {
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 7, 4, false, false, false>), gx, block, 0, s, a);
+                    else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 7, 4, false, false, false>), gx, block, 0, s, a);
+                }
+            }
+        } else if (a.rowk == 4) {                 // actor.bwd1 with actor.head.bwd folded in (16x16 only)
             if (a.bf16) {
                 if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, true, PK, false>), gx, block, 0, s, a);
                 else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, true, PK, false>), gx, block, 0, s, a);
@@ -3283,7 +3509,7 @@ __global__ __launch_bounds__(256) void k_adam_apply(AdamApplyArgs a) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const Ctl* ctl = a.ctl;
-    const int64_t tstep = (a.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1;
+    const int64_t tstep = (a.group == GRP_MODEL ? ctl->t_model : ctl->t_sac) + 1 - a.t_adv;
     const float lr_t = adam_lr(a.adam, a.group, tstep);
     float* P = a.P + i;
     float gr = P[3 * a.p_stride] * a.grad_scale;
@@ -3537,10 +3763,10 @@ __global__ __launch_bounds__(256) void k_mloss(MLossArgs g) {
         const float e = g.T[(size_t)row * O + c] - g.O[(size_t)row * O + c];
         if (c < S) {
             sq = sq + e * e;
-            g.D3[(size_t)row * O + c] = -e * inv;
+            g.D3[(size_t)row * g.ldD + c] = -e * inv;
         } else {
             er = e;
-            g.D3[(size_t)row * O + c] = -e * (g.reward_coef * inv);
+            g.D3[(size_t)row * g.ldD + c] = -e * (g.reward_coef * inv);
         }
     }
     const float tot = wave_sum(sq);
@@ -3548,22 +3774,7 @@ __global__ __launch_bounds__(256) void k_mloss(MLossArgs g) {
     if (lane == 0) g.loss_rows[row] = 0.5f * tot + g.reward_coef * (0.5f * (e_r * e_r));
 }
 
-__global__ __launch_bounds__(64) void k_mfinal(MFinalArgs f) {
-    const int lane = threadIdx.x & 63;
-    float s0 = 0.f, s1 = 0.f;
-    for (int i = lane; i < f.mb; i += 64) {
-        s0 += f.loss_rows[i];
-        if (f.nm > 1) s1 += f.loss_rows[f.mb + i];
-    }
-    const float l0 = wave_sum(s0) / (float)f.mb, l1 = wave_sum(s1) / (float)f.mb;
-    if (lane == 0) {
-        const int64_t seq = f.ctl->mfit_seq;
-        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = f.nm > 1 ? l0 + l1 : l0;     // loss_all (:305-312)
-        f.mstats[(size_t)(seq % f.mstats_cap) * 2 + 1] = (float)seq;
-        f.ctl->t_model += 1;
-        f.ctl->mfit_seq = seq + 1;
-    }
-}
+__global__ __launch_bounds__(64) void k_mfinal(MFinalArgs f) { mfit_final(f); }
 
 void launch_mgather(const MGatherArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_mgather, dim3((a.nm * a.mb + 3) / 4), dim3(256), 0, s, a);

@@ -151,6 +151,12 @@ struct sacx_handle {
     int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
     int dwl = 0;              // dW + Adam launches on k_dwl: 0 never, 1 when K >= 512, 2 always (SACX_DWL)
     int dwl_nh = 1;           // k_dwl tile width in 16-column halves (SACX_DWL_NH: 1 -> 32x16, 2 -> 32x32)
+    int mfuse = 2;            // model fit folds (SACX_MFUSE): 1 the loss into model.fwd2's epilogue and k_mfinal
+                              // into model.bwd2, 2 also k_mgather into model.fwd0's operand loads (default);
+                              // 3 also model.bwd2 into model.bwd1 (generated operand, heads of <= 32
+                              // outputs; bit-identical, measured slower: HC 49.7 vs 46.9 us per step)
+    int unaligned_b = 1;      // dX launches: float4 loads of W_ext rows at any 4-B offset (SACX_UNALIGNED)
+    int mtile = 1;            // model fit tiles: 0 16x16, 1 16x16 + wide dW on 32x32, 2 the handle's (SACX_MTILE)
     int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
@@ -433,10 +439,10 @@ void build_layout(sacx_handle* h) {
         h->add("ws.Hf1", R2, Hm0, F, 0);
         h->add("ws.Hf2", R2, Hm1, F, 0);
         h->add("ws.Of", R2, O, F, 0);
-        h->add("ws.Df3", R2, O, F, 0);
+        h->add("ws.Df3", R2, r4(O), F, 0);    // float4 rows: model.bwd2's A operand
         h->add("ws.Df2", R2, Hm1, F, 0);
         h->add("ws.Df1", R2, Hm0, F, 0);
-        h->add("ws.lf", 1, R2, F, 0);
+        h->add("ws.lf", 1, (int64_t)R2 * ((O + 15) / 16), F, 0);   // fit-loss partials (per row: k_mloss)
         // model rollout (sacx_rollout), up to ROLL_CAP trajectories per launch chain
         h->add("roll.X", ROLL_CAP, h->ldS, F, 0);
         h->add("roll.H1", ROLL_CAP, H0, F, 0);
@@ -560,7 +566,11 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         const int64_t k4 = r4(p.K);
         const bool v_a = (p.lda % 4 == 0) && (k4 <= p.lda) && ((((uintptr_t)p.A) & 15) == 0) &&
                          ((((uintptr_t)p.wgen) & 15) == 0);
-        const bool v_b = mode == GM_DX ? ((p.ldb % 4 == 0) && (k4 <= p.ldb) && ((((uintptr_t)p.B) & 15) == 0)) : true;
+        // dX: B = W_ext rows (n < N = K_in, so a row's float4 over-read past K stays inside W_ext: the
+        // bias row follows the last); rows at any 4-B offset with h->unaligned_b (dword-aligned 16-B
+        // buffer loads), whose elements past K meet A's zero pad (A rows are 16-B aligned)
+        const bool b_al = (p.ldb % 4 == 0) && (k4 <= p.ldb) && ((((uintptr_t)p.B) & 15) == 0);
+        const bool v_b = mode == GM_DX ? (b_al || (h->unaligned_b && (((uintptr_t)p.B) & 3) == 0)) : true;
         p.vec = (mode != GM_DW && v_a && v_b && p.K >= 4) ? 1 : 0;
         vec = vec || p.vec;
     }
@@ -1249,7 +1259,10 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
 }
 
 // one world-model fitting step: gather -> 3 fwd GEMMs -> loss grads -> 2 dX GEMMs -> dW + Adam -> finalize
-// the fitting plan of the selected seed (its arena block's pointers)
+// the fitting plan of the selected seed (its arena block's pointers).  Folded (h->mfuse, the
+// default): the loss and its gradient are model.fwd2's epilogue (mse = 2) and the finalisation is
+// one extra workgroup of model.bwd2, so model.adam takes the already-advanced step counter (t_adv);
+// the weights are bit-identical to the unfolded chain, the loss statistic sums in another order.
 void build_model_plan(sacx_handle* h) {
     std::vector<Launch>& plan = h->mplans[h->sel];
     plan.clear();
@@ -1257,20 +1270,28 @@ void build_model_plan(sacx_handle* h) {
     const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ;
     const int m0 = h->macts[0], m1 = h->macts[1];
     const int nm = h->nm;
+    const bool fuse = h->mfuse != 0;
+    const int nt = (O + 15) / 16;     // fit-loss partials per row (16-column tiles of model.fwd2)
+    const int ldO = (int)r4(O);       // D3 row stride
+    // model.bwd2 generated on model.bwd1's operand loads (rowk 7) for narrow heads (S + 1 <= 32)
+    const bool bfold = fuse && h->mfuse >= 3 && O <= 32 && h->mtile != 2 && h->unaligned_b;
     auto W = [&](const std::string& n) { return h->f(n); };
     float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Hf1 = W("ws.Hf1"), *Hf2 = W("ws.Hf2"), *Of = W("ws.Of");
     float *Df3 = W("ws.Df3"), *Df2 = W("ws.Df2"), *Df1 = W("ws.Df1");
-    {
+    MGatherArgs mg{};
+    mg.replay = W("replay"); mg.cap = h->cap; mg.stride = h->stride; mg.S = S; mg.A = A; mg.mb = mb;
+    mg.idx_ring = h->ptr<int32_t>("mfit.idx"); mg.idx_cap = h->mfit_cap; mg.ctl = h->ctl();
+    mg.s_mean = W("mnorm.s_mean"); mg.s_den = W("mnorm.s_den"); mg.a_mean = W("mnorm.a_mean");
+    mg.a_den = W("mnorm.a_den"); mg.d_mean = W("mnorm.d_mean"); mg.d_den = W("mnorm.d_den"); mg.r_norm = W("mnorm.r");
+    mg.X = Xf; mg.ldQ = ldQ; mg.T = Tf; mg.nm = nm;
+    mg.clip_d = h->cfg.delta_clip_loss; mg.clip_r = h->cfg.reward_clip_loss;
+    // the gather on model.fwd0's operand loads (rowk 6: 16x16 tiles, whose rows are whole records)
+    const bool gfold = fuse && h->mfuse >= 2 && h->mtile != 2 && h->stride % 4 == 0 && ldQ % 4 == 0;
+    if (!gfold) {
         Launch L{};
         L.kind = Launch::MGATHER;
         L.name = "model.gather";
-        MGatherArgs& g = L.mg;
-        g.replay = W("replay"); g.cap = h->cap; g.stride = h->stride; g.S = S; g.A = A; g.mb = mb;
-        g.idx_ring = h->ptr<int32_t>("mfit.idx"); g.idx_cap = h->mfit_cap; g.ctl = h->ctl();
-        g.s_mean = W("mnorm.s_mean"); g.s_den = W("mnorm.s_den"); g.a_mean = W("mnorm.a_mean");
-        g.a_den = W("mnorm.a_den"); g.d_mean = W("mnorm.d_mean"); g.d_den = W("mnorm.d_den"); g.r_norm = W("mnorm.r");
-        g.X = Xf; g.ldQ = ldQ; g.T = Tf; g.nm = nm;
-        g.clip_d = h->cfg.delta_clip_loss; g.clip_r = h->cfg.reward_clip_loss;
+        L.mg = mg;
         L.grid = (nm * mb + 3) / 4;
         L.bytes = 4.0 * nm * mb * (2.0 * S + A + 1 + ldQ + O);
         plan.push_back(L);
@@ -1281,29 +1302,82 @@ void build_model_plan(sacx_handle* h) {
         const size_t r0 = (size_t)k * mb;
         f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, m0));
         f1.push_back(prob_fwd(Hf1 + r0 * Hm0, Hm0, mb, Hm0, W(n + ".l1"), Hm1, Hf2 + r0 * Hm1, m1));
-        f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), O, Of + r0 * O, ACT_NONE));
-        b2.push_back(prob_dx(Df3 + r0 * O, mb, O, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, m1));
+        f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), O, fuse ? Df3 + r0 * ldO : Of + r0 * O,
+                              ACT_NONE));
+        if (fuse) {   // MSEModel.get_loss as the head's epilogue: C = d loss / d out, per-tile partials
+            GemmProb& p = f2.back();
+            p.ldc = ldO;
+            p.mse = 2; p.se_raw = Tf + r0 * O; p.part = W("ws.lf") + r0 * nt;
+            p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;
+        }
+        b2.push_back(prob_dx(Df3 + r0 * ldO, mb, O, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, m1));
+        b2.back().lda = ldO;
         b1.push_back(prob_dx(Df2 + r0 * Hm1, mb, Hm1, W(n + ".l1"), Hm0, Hf1 + r0 * Hm0, Df1 + r0 * Hm0, m0));
+        if (bfold) {   // A = D2 generated from H2, D3 and W2 on load; column tile 0 stores it for model.adam
+            GemmProb& q = b1.back();
+            q.A = Hf2 + r0 * Hm1; q.wgen = W(n + ".l2"); q.gen_act = m1;
+            q.gd = Df3 + r0 * ldO; q.gd_ld = ldO; q.g_o = O; q.gst = Df2 + r0 * Hm1; q.gst_ld = Hm1;
+        }
         w.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Df1 + r0 * Hm0, Hm0, W(n + ".l0"), nullptr, GRP_MODEL));
         w.push_back(prob_dw(Hf1 + r0 * Hm0, Hm0, Hm0, mb, Df2 + r0 * Hm1, Hm1, W(n + ".l1"), nullptr, GRP_MODEL));
-        w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * O, O, W(n + ".l2"), nullptr, GRP_MODEL));
+        w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * ldO, O, W(n + ".l2"), nullptr, GRP_MODEL));
+        w.back().ldb = ldO;
     }
+    // the fit's own tile shapes (SACX_MTILE): its 2 x 200 rows want 16x16 forward / dX tiles
+    // (832 workgroups at 512 wide, against 224 as 32x32) whatever the update's batch made
+    // h->tile32; the dW + Adam launch takes 32x32 tiles when its 16x16 ones exceed one round of
+    // residency (HC 2,372 -> 610 tiles), the rule of add_gemm at tile32 = 2.  2: the handle's.
+    const int tile32_h = h->tile32;
+    if (h->mtile != 2) h->tile32 = 0;
     add_gemm(h, plan, "model.fwd0", f0, false);
+    if (gfold) {
+        Launch& F = plan.back();
+        if (F.gemm.t32 || F.gemm.dwl) { fprintf(stderr, "sacx: model.fwd0 gather needs 16x16 tiles\n"); abort(); }
+        F.gemm.rowk = 6;
+        F.gemm.mg = mg;
+        F.name = "model.gather+fwd0";
+        F.bytes += 4.0 * nm * mb * (2.0 * S + A + 1 + O);
+    }
     add_gemm(h, plan, "model.fwd1", f1, false);
     add_gemm(h, plan, "model.fwd2", f2, false);
-    {
+    if (fuse) plan.back().name = "model.fwd2+loss";
+    if (!fuse) {
         Launch L{};
         L.kind = Launch::MLOSS;
         L.name = "model.loss";
-        L.ml.S = S; L.ml.mb = mb; L.ml.nm = nm; L.ml.T = Tf; L.ml.O = Of; L.ml.D3 = Df3; L.ml.loss_rows = W("ws.lf");
+        L.ml.S = S; L.ml.mb = mb; L.ml.nm = nm; L.ml.T = Tf; L.ml.O = Of; L.ml.D3 = Df3; L.ml.ldD = ldO;
+        L.ml.loss_rows = W("ws.lf");
         L.ml.reward_coef = h->cfg.reward_loss_coef;
         L.grid = (nm * mb + 3) / 4;
         L.bytes = 4.0 * nm * mb * O * 3;
         plan.push_back(L);
     }
-    add_gemm(h, plan, "model.bwd2", b2, false);
+    MFinalArgs mf{};
+    mf.ctl = h->ctl(); mf.loss_rows = W("ws.lf"); mf.mb = mb; mf.nm = nm;
+    mf.mstats = W("mstats"); mf.mstats_cap = h->stats_cap; mf.nt = fuse ? nt : 0;
+    if (!bfold) {
+        add_gemm(h, plan, "model.bwd2", b2, false);
+        if (fuse) {
+            Launch& B2 = plan.back();
+            B2.name = "model.bwd2+final";
+            B2.gemm.has_mfinal = 1;
+            B2.gemm.mfin = mf;
+        }
+    }
     add_gemm(h, plan, "model.bwd1", b1, false);
+    if (bfold) {
+        Launch& B1 = plan.back();
+        if (B1.gemm.t32 || B1.gemm.dwl) { fprintf(stderr, "sacx: model.bwd1 generation needs 16x16 tiles\n"); abort(); }
+        B1.name = "model.bwd2+bwd1+final";
+        B1.gemm.rowk = 7;
+        B1.gemm.has_mfinal = 1;
+        B1.gemm.mfin = mf;
+        for (const GemmProb& q : b2) { B1.flops += gemm_flops(q); B1.bytes += gemm_bytes(q); }
+    }
+    if (h->mtile == 1) h->tile32 = 2;
     add_gemm(h, plan, "model.adam", w, false);
+    h->tile32 = tile32_h;
+    plan.back().gemm.t_adv = fuse ? 1 : 0;
     if (h->cfg.model_max_grad_norm > 0.f) {
         // --model_max_grad_norm (mbrl_onpolicy_alg.py:315-317): the dW launch stores the
         // gradients (+3 p_stride); their global norm gives one scale; Adam applies g * scale
@@ -1330,17 +1404,16 @@ void build_model_plan(sacx_handle* h) {
         AdamApplyArgs& a = U.ap;
         a.P = P; a.n = n; a.p_stride = h->p_stride; a.group = GRP_MODEL; a.t_off = 0;
         a.grad_scale = 1.f; a.scale_dev = N.gn.scale_out;
-        a.ctl = h->ctl(); a.adam = G.gemm.adam;
+        a.ctl = h->ctl(); a.adam = G.gemm.adam; a.t_adv = fuse ? 1 : 0;
         U.grid = (int)((n + 255) / 256);
         U.bytes = 4.0 * n * 7;
         plan.push_back(U);
     }
-    {
+    if (!fuse) {
         Launch L{};
         L.kind = Launch::MFINAL;
         L.name = "model.final";
-        L.mf.ctl = h->ctl(); L.mf.loss_rows = W("ws.lf"); L.mf.mb = mb; L.mf.nm = nm;
-        L.mf.mstats = W("mstats"); L.mf.mstats_cap = h->stats_cap;
+        L.mf = mf;
         L.grid = 1;
         L.block = 64;
         plan.push_back(L);
@@ -1881,6 +1954,9 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // pieces instead of the fragment-shaped column loads, bit-identical results
     if (const char* e = std::getenv("SACX_DWL")) h->dwl = std::atoi(e);
     if (const char* e = std::getenv("SACX_DW_ROUND")) h->dw_round_tiles = std::atoi(e);
+    if (const char* e = std::getenv("SACX_MFUSE")) h->mfuse = std::atoi(e);
+    if (const char* e = std::getenv("SACX_MTILE")) h->mtile = std::atoi(e);
+    if (const char* e = std::getenv("SACX_UNALIGNED")) h->unaligned_b = std::atoi(e);
     if (const char* e = std::getenv("SACX_DWL_NH")) h->dwl_nh = std::atoi(e) == 2 ? 2 : 1;
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
@@ -2522,13 +2598,27 @@ int sacx_sync(sacx_handle* h) {
 
 int64_t sacx_spec_hits(const sacx_handle* h) { return h ? h->spec_hits : -1; }
 
+static int launch_info(const std::vector<Launch>& plan, sacx_launch_info* out, int32_t cap, int32_t* n_out);
+
 int sacx_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out) {
     if (!h || !n_out) return -1;
     if (!h->bound) {
         *n_out = 0;
         return -1;
     }
-    const auto& plan = h->plan[0];
+    return launch_info(h->plan[0], out, cap, n_out);
+}
+
+int sacx_model_plan_info(const sacx_handle* h, sacx_launch_info* out, int32_t cap, int32_t* n_out) {
+    if (!h || !n_out) return -1;
+    if (!h->bound || h->mplans.empty()) {
+        *n_out = 0;
+        return h->bound ? 0 : -1;
+    }
+    return launch_info(h->mplans[h->sel], out, cap, n_out);
+}
+
+static int launch_info(const std::vector<Launch>& plan, sacx_launch_info* out, int32_t cap, int32_t* n_out) {
     *n_out = (int32_t)plan.size();
     if (!out) return 0;
     for (int i = 0; i < (int)plan.size() && i < cap; ++i) {

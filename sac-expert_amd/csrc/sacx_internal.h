@@ -83,7 +83,12 @@ struct GemmProb {
     // is the normalised delta; C receives d loss / d out = (-eps * grad_scale * diff) * d_den,
     // diff = sp_e - (s_e + out * d_den + d_mean); part[row * tiles_n + tn] = sum of diff^2 over
     // the tile's columns (row stride of se_raw / spe_raw is N)
+    // mse = 2: the world-model FIT loss (MSEModel.get_loss, continuous_models.py:280-302, in the
+    // model.fwd2 epilogue): se_raw = the normalised targets T [M, N]; C = d loss / d out =
+    // -(T - out) * (cf / mb) with cf = fcoef (reward_loss_coef) on column N - 1, else 1
+    // (grad_scale = 1 / mb); part[row * tiles + tn] = sum over the tile's columns of cf (T - out)^2
     int32_t mse;
+    float fcoef;
     float dclip;            // --delta_clip_pred on `out` (clipped, zero gradient outside); 0: off
     const float *se_raw, *spe_raw, *dmean, *dden;
     float* part;
@@ -105,6 +110,14 @@ struct GemmProb {
     int32_t pw_ld, pw_cs, pw_n;
     // GM_DX with rowk 4: the folded actor head backward problem (GemmArgs::hbw)
     int32_t hbw;
+    // GM_DX with rowk 7 (model.bwd1 of the fit with model.bwd2 folded in): the A operand, the
+    // layer-2 delta D2 = (D3 . W2^T) (.) act'(H2), is generated on load from A = H2 [M, K] and
+    // gd = D3 [M, g_o] (row stride gd_ld) through wgen = W2_ext [K (+1), g_o] (row stride g_o),
+    // with model.bwd2's exact MFMA sequence (16-wide output slabs t, j = 0 2 / 1 3 pairs, the
+    // slabs as waves summed in order; g_o <= 32); column tile 0 stores D2 to gst (ld gst_ld)
+    const float* gd;
+    float* gst;
+    int32_t gd_ld, g_o, gst_ld;
 };
 
 // rowk 4 (GM_DX, actor.bwd1): the actor head backward (k_actor_bwd's policy-row work) runs as
@@ -232,6 +245,30 @@ struct HeadArgs {
     int32_t nseeds;
 };
 
+// world-model fit inputs: the step's minibatch rows gathered from the replay ring (k_mgather, or
+// on load by model.fwd0's tiles: GemmArgs rowk 6)
+struct MGatherArgs {        // rows [0, 2*mb): model k = row / mb
+    const float* replay; int64_t cap; int32_t stride;
+    int32_t S, A, mb;
+    const int32_t* idx_ring; int32_t idx_cap;   // [idx_cap, 2*mb] replay-logical rows
+    const Ctl* ctl;
+    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den)
+    float* X; int32_t ldQ;      // [2mb, ldQ] = [s_n | a_n | 0]
+    float* T;                   // [2mb, S+1] = [norm(sp - s) | norm(r)]
+    int32_t nm;                 // world models fitted (rows [0, nm*mb))
+    float clip_d, clip_r;       // > 0: --delta_clip_loss / --reward_clip_loss on T (get_loss :286-296)
+};
+
+// end of a world-model fitting step (k_mfinal, or folded into a launch of the step)
+struct MFinalArgs {
+    Ctl* ctl;
+    const float* loss_rows; int32_t mb, nm;
+    float* mstats; int32_t mstats_cap;
+    // nt > 0: loss_rows holds nt partials per row (the fit-loss epilogue's, sums of cf e^2 over a
+    // column tile: the loss is 0.5 x their sum); 0: one loss per row (k_mloss)
+    int32_t nt;
+};
+
 #define GEMM_MAXP 8
 struct GemmArgs {
     GemmProb probs[GEMM_MAXP];   // by value: no dependent global load to find a tile's problem
@@ -267,6 +304,17 @@ struct GemmArgs {
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
     int64_t sstride;
     int32_t nseeds;
+    // world-model fit (ROWK 0 launches): one extra workgroup after the tiles finalises the fit step
+    // (k_mfinal's work: loss statistics, t_model and mfit_seq advance)
+    int32_t has_mfinal;
+    // GM_DW: the optimiser step counter was already advanced in this step (the folded model
+    // finalisation runs before model.adam): the Adam step is t + 1 - t_adv
+    int32_t t_adv;
+    MFinalArgs mfin;
+    // GM_FWD rowk 6 (model.fwd0 of the fit): problem p's A rows are replay records gathered by the
+    // step's indices (model p's minibatch) and normalised on load; column tile 0 stores them to
+    // the problem's A (X, read by model.adam) and each tile stores its 16 columns of the targets
+    MGatherArgs mg;
 };
 static_assert(sizeof(GemmArgs) <= 4096, "GemmArgs travels as kernel arguments");
 
@@ -368,17 +416,6 @@ struct AppendArgs {
 };
 
 // ---------------------------------------------------------------- world-model fitting
-struct MGatherArgs {        // rows [0, 2*mb): model k = row / mb
-    const float* replay; int64_t cap; int32_t stride;
-    int32_t S, A, mb;
-    const int32_t* idx_ring; int32_t idx_cap;   // [idx_cap, 2*mb] replay-logical rows
-    const Ctl* ctl;
-    const float *s_mean, *s_den, *a_mean, *a_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den)
-    float* X; int32_t ldQ;      // [2mb, ldQ] = [s_n | a_n | 0]
-    float* T;                   // [2mb, S+1] = [norm(sp - s) | norm(r)]
-    int32_t nm;                 // world models fitted (rows [0, nm*mb))
-    float clip_d, clip_r;       // > 0: --delta_clip_loss / --reward_clip_loss on T (get_loss :286-296)
-};
 // ---------------------------------------------------------------- reference object methods
 // The standalone network calls of the reference's actor / critic / model objects
 // (sacx_critic_forward, sacx_actor_evaluate, sacx_model_forward, sacx_model_loss): the
@@ -405,14 +442,10 @@ struct NetIOArgs {
 struct MLossArgs {
     int32_t S, mb, nm;
     const float* T; const float* O;   // [2mb, S+1]
-    float* D3;                        // dL/dout [2mb, S+1]
+    float* D3;                        // dL/dout [2mb, ldD]
+    int32_t ldD;                      // r4(S+1): float4 rows for model.bwd2's operand loads
     float* loss_rows;                 // [2mb]
     float reward_coef;
-};
-struct MFinalArgs {
-    Ctl* ctl;
-    const float* loss_rows; int32_t mb, nm;
-    float* mstats; int32_t mstats_cap;
 };
 
 // ---------------------------------------------------------------- data-parallel Adam (C4)
@@ -426,6 +459,7 @@ struct AdamApplyArgs {
     const float* scale_dev;     // nullable: gradients also times *scale_dev (clip_by_global_norm)
     const Ctl* ctl;
     AdamConsts adam;
+    int32_t t_adv;              // as GemmArgs::t_adv
 };
 
 // In-process data-parallel reduce (sacx_dp_local_step): buf[r][i] = sum over r' of buf[r'][i], in

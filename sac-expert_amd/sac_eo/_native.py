@@ -27,7 +27,7 @@ EXPORTS = [
     "sacx_create", "sacx_destroy", "sacx_last_error", "sacx_arena_bytes", "sacx_layout", "sacx_bind",
     "sacx_buffer_append", "sacx_buffer_append_host", "sacx_actor_act_host",
     "sacx_buffer_append_host_seeds", "sacx_actor_act_host_seeds", "sacx_expert_set", "sacx_perm_push", "sacx_rng_seed", "sacx_rng_set_state",
-    "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_profile",
+    "sacx_rng_get_state", "sacx_sac_step", "sacx_model_fit", "sacx_sync", "sacx_plan_info", "sacx_model_plan_info", "sacx_profile",
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
     "sacx_dp_unique_id", "sacx_dp_init", "sacx_dp_init_local", "sacx_dp_local_step", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
     "sacx_seed_select", "sacx_prepare", "sacx_actor_evaluate", "sacx_critic_forward", "sacx_model_forward",
@@ -141,6 +141,7 @@ def lib():
         "sacx_sync": (ctypes.c_int, [vp]),
         "sacx_settle": (ctypes.c_int, [vp]),
         "sacx_plan_info": (ctypes.c_int, [vp, P(LaunchInfo), i32, P(i32)]),
+        "sacx_model_plan_info": (ctypes.c_int, [vp, P(LaunchInfo), i32, P(i32)]),
         "sacx_spec_hits": (i64, [vp]),
         "sacx_profile": (ctypes.c_int, [vp, i64, P(f64), i32]),
         "sacx_time_graph": (ctypes.c_int, [vp, i64, ctypes.c_char_p, P(f64)]),

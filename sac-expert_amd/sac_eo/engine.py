@@ -680,6 +680,15 @@ class Engine:
         return [dict(name=a.name.decode(), kernel=a.kernel.decode(), grid=a.grid, block=a.block,
                      flops=a.flops, bytes=a.bytes) for a in arr]
 
+    def model_plan_info(self) -> List[dict]:
+        """The launches of one world-model fitting step of the selected seed (after a model_fit)."""
+        n = ctypes.c_int32()
+        self.lib.sacx_model_plan_info(self.h, None, 0, ctypes.byref(n))
+        arr = (N.LaunchInfo * n.value)()
+        N.check(self.lib.sacx_model_plan_info(self.h, arr, n.value, ctypes.byref(n)), self.h, "model_plan_info")
+        return [dict(name=a.name.decode(), kernel=a.kernel.decode(), grid=a.grid, block=a.block,
+                     flops=a.flops, bytes=a.bytes) for a in arr]
+
     def time_graph(self, n_replays: int, skip_kernel: str = None) -> float:
         """ms per update of graph replays (HIP events); skip_kernel leaves a kernel family
         out (the state is meaningless afterwards)."""

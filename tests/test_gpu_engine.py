@@ -278,6 +278,36 @@ def test_model_fit_matches_oracle(gpu_available, eager):
     eng.close()
 
 
+@pytest.mark.parametrize("S,A,B,clip", [(17, 6, 256, 0.0), (376, 17, 1024, 0.0), (17, 6, 64, 5.0)])
+def test_model_fit_folds_bit_identical(gpu_available, monkeypatch, S, A, B, clip):
+    """The folded world-model fit chain (the loss and its gradient in model.fwd2's epilogue,
+    k_mfinal as an extra workgroup of model.bwd2: SACX_MFUSE=1; the rows gathered on model.fwd0's
+    operand loads: 2; model.bwd2 generated on model.bwd1's operand loads for heads of <= 32
+    outputs: 3, the default; the fit's own tile shapes: SACX_MTILE=1, the default, or 16x16
+    everywhere: 0) leaves the weights and Adam state of the unfolded chain
+    (SACX_MFUSE=0, SACX_MTILE=2) bit for bit, eager and graph; the loss statistic sums the
+    same squares in another order (<= 1e-6 relative)."""
+    outs = []
+    steps = 12
+    for fuse, tile in (("0", "2"), ("1", "1"), ("2", "1"), ("3", "1"), ("3", "0")):
+        monkeypatch.setenv("SACX_MFUSE", fuse)
+        monkeypatch.setenv("SACX_MTILE", tile)
+        eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, B=B, act="tanh", N=3000, seed=33, use_expert=True,
+                                               normalizers="random", model_max_grad_norm=clip)
+        mb = eng.cfg.model_batch
+        idx = np.random.RandomState(4).randint(buf["r"].shape[0], size=(steps, 2, mb))
+        eng.model_fit(idx[:3], eager=True)
+        eng.model_fit(idx[3:])
+        eng.sync()
+        P = np.concatenate([eng.v[k].cpu().numpy().ravel() for k in ("params", "adam_m", "adam_v")])
+        outs.append((eng.model_stats(steps).copy(), P, eng.ctl()["t_model"]))
+        eng.close()
+    for o in outs[1:]:
+        assert o[2] == outs[0][2] == steps
+        assert np.array_equal(o[1], outs[0][1])
+        assert np.max(np.abs(o[0] - outs[0][0]) / np.abs(outs[0][0])) < 1e-6, (o[0], outs[0][0])
+
+
 @pytest.mark.parametrize("deterministic,per_state_std,n,host", [(True, False, 37, False), (False, False, 37, False),
                                                                 (False, True, 5, False), (False, False, 1, False),
                                                                 (False, False, 1, True), (True, False, 37, True),

@@ -34,6 +34,20 @@ for step in "$@"; do
       { timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
         timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
       rc=$?; echo "[$n mfit] rc=$rc"; cat "$log" ;;
+    mtrace)     # kernel trace of the model fit of config $arg: one step's launches, durations, gaps
+      cfg=${arg:-hc_eo}
+      timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$PWD/$OUT/mtrace_$cfg" -o m \
+          -- python tools/model_fit_time.py $cfg 128 > "$log" 2>&1
+      rc=$?
+      if [ $rc -eq 0 ]; then
+        f=$(find "$OUT/mtrace_$cfg" -name "*kernel_trace.csv" | head -1)
+        python tools/trace_view.py "$f" 24 "k_mgather,k_gemm<0, 1, 6,k_gemm<0, 0, 6" > "$OUT/$n-mtrace_$cfg.txt" 2>&1; cat "$OUT/$n-mtrace_$cfg.txt"
+      fi
+      echo "[$n mtrace $cfg] rc=$rc" ;;
+    mprof)      # rocprofv3 kernel-trace stats of the HC model fit (graph replay only) -> profiles r*_mfit_hc_kernel_stats
+      MFT_GRAPH_ONLY=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/mprof" -o m \
+          -- python tools/model_fit_time.py hc_eo 2048 > "$log" 2>&1
+      rc=$?; echo "[$n mprof] rc=$rc $(grep graph "$log")" ;;
     humanoid)
       rc=0
       for c in humanoid_sac humanoid_bf16 humanoid_eo; do

@@ -1,6 +1,7 @@
 """Print one update's worth of the kernel trace: queue, start, duration, gap to the previous
 kernel on the same queue.  usage: python tools/trace_view.py <kernel_trace.csv> [n] [first-kernel]
-(first-kernel: start the window at a dispatch of that kernel, e.g. k_mgather for a model-fit step)"""
+(first-kernel: start the window at a dispatch of that kernel, e.g. k_mgather for a model-fit step;
+ comma-separated: the first marker the trace holds)"""
 import csv
 import sys
 
@@ -10,9 +11,12 @@ for r in rows:
 rows.sort(key=lambda r: r["s"])
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 40
 mid = len(rows) * 2 // 3
-if len(sys.argv) > 3:
-    hits = [i for i, r in enumerate(rows) if sys.argv[3] in r["Kernel_Name"]]
-    mid = hits[len(hits) * 5 // 6]
+if len(sys.argv) > 3:       # comma-separated markers: the first one present in the trace
+    for mark in sys.argv[3].split(","):
+        hits = [i for i, r in enumerate(rows) if mark in r["Kernel_Name"]]
+        if hits:
+            mid = hits[len(hits) * 5 // 6]
+            break
 w = rows[mid: mid + n]
 t0 = w[0]["s"]
 last = {}
