@@ -115,10 +115,13 @@ def _pool_worker(job):
 
 
 def pool_size(args, n_runs: int) -> int:
-    """Processes per GPU for the runs of one rank: the reference's Pool(--cores) (train.py:148-152;
-    default one per run), capped by the usable host cores and by MAX_PROCS_PER_GPU (each process
-    holds its own device context and arena); each process trains its runs as packed seeds."""
-    want = args.cores if args.cores is not None else n_runs
+    """Processes per GPU for the runs of one rank: the reference's Pool(--cores) (train.py:148-152),
+    capped by the usable host cores and by MAX_PROCS_PER_GPU (each process holds its own device
+    context and arena); each process trains its runs as packed seeds.  Without --cores: ONE process
+    per GPU packing all of its runs -- not the reference's one process per run: processes sharing a
+    GPU time-slice it (8 HC runs of sac: packed 3.02x serial, 2 / 4 / 8 processes 1.46x / 0.72x /
+    0.73x; profiles/r04_packed_runs_sac_v1.log)."""
+    want = args.cores if args.cores is not None else 1
     usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
     return max(1, min(want, n_runs, usable, MAX_PROCS_PER_GPU))
 

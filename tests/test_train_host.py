@@ -64,13 +64,15 @@ def test_packed_runs_host(monkeypatch, tmp_path, alg):
 
 
 def test_pool_size_and_split():
-    """--cores as the reference's Pool size (train.py:148-152): default one process per run, capped
-    by the usable cores and MAX_PROCS_PER_GPU; runs dealt round-robin over the processes."""
+    """--cores as the reference's Pool size (train.py:148-152), capped by the usable cores and
+    MAX_PROCS_PER_GPU; without it one packed process per GPU (processes sharing a GPU time-slice
+    it); runs dealt round-robin over the processes."""
     import argparse
     from sac_eo import train as T
     ns = lambda cores: argparse.Namespace(cores=cores)
     usable = len(__import__("os").sched_getaffinity(0))
     assert T.pool_size(ns(None), 1) == 1
     assert T.pool_size(ns(1), 8) == 1
-    assert T.pool_size(ns(None), 8) == min(8, usable, T.MAX_PROCS_PER_GPU)
+    assert T.pool_size(ns(None), 8) == 1
+    assert T.pool_size(ns(8), 8) == min(8, usable, T.MAX_PROCS_PER_GPU)
     assert T.pool_size(ns(3), 2) == min(2, usable)
