@@ -815,7 +815,7 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
 #ifndef SACX_T32_DW_NS
 #define SACX_T32_DW_NS 1   // the same for the dW + Adam tiles (uncapped registers)
 #endif
-template <int MODE, int VEC, bool BF, bool PART = false>
+template <int MODE, int VEC, bool BF, bool PART = false, bool MSE = false>
 __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
                                             float (&red)[16][4][64]) {
     constexpr bool AKC = (MODE != GM_DW);
@@ -837,10 +837,12 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         e0[s] = e1[s] = e2[s] = e3[s] = e4[s] = 0.f;
         if constexpr (MODE == GM_FWD) {
             e0[s] = g.bias[nnc];
-            e1[s] = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
-            e2[s] = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
-            e3[s] = bload(rs(g.dmean), boff(g.mse != 0, nnc));
-            e4[s] = bload(rs(g.dden), boff(g.mse != 0, nnc));
+            if constexpr (MSE) {   // launches with world-model head rows only (the registers cost occupancy)
+                e1[s] = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
+                e2[s] = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
+                e3[s] = bload(rs(g.dmean), boff(g.mse != 0, nnc));
+                e4[s] = bload(rs(g.dden), boff(g.mse != 0, nnc));
+            }
         } else if constexpr (MODE == GM_DX) {
             e0[s] = g.H[(size_t)mmc * g.ldh + nnc];
         } else {
@@ -850,7 +852,8 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             e3[s] = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
         }
     }
-    const EpiScalars es = epi_scalars(sr(ga.ctl, so), g.group);
+    EpiScalars es{};
+    if constexpr (MODE == GM_DW || MSE) es = epi_scalars(sr(ga.ctl, so), g.group);
 
     const int nIt = (g.K + 15) >> 4;
     const int per = (nIt + 3) >> 2;
@@ -871,8 +874,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
     constexpr int NS = BF ? 2 : (MODE == GM_DW ? SACX_T32_DW_NS : SACX_T32_NS);
     auto main_loop = [&](auto vt) {   // unswitched on the problem's float4 flag, as gemm_core
     constexpr bool V = decltype(vt)::value;
-    for (int it = it0; it < it1; it += NS) {
-        float a[NS][2][4], b[NS][2][4];
+    auto load_group = [&](int it, float (&a)[NS][2][4], float (&b)[NS][2][4]) {
 #pragma unroll
         for (int u = 0; u < NS; ++u) {
             const int k0 = (it + u) * 16 + grp * 4;
@@ -882,6 +884,10 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, na, naok, k0e, b[u][0]);
             load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, nb, nbok, k0e, b[u][1]);
         }
+    };
+    for (int it = it0; it < it1; it += NS) {
+        float a[NS][2][4], b[NS][2][4];
+        load_group(it, a, b);
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (BF) {
             // slab pairs (it0 + 2i, it0 + 2i + 1), alternately into acc0 / acc1 -- the pairs and
@@ -967,7 +973,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 continue;
             }
         }
-        if constexpr (MODE == GM_FWD) {
+        if constexpr (MODE == GM_FWD && MSE) {
             if (g.mse) {          // uniform: the expert MSE / fit-loss epilogue (all 256 threads take part)
                 const bool fit = g.mse == 2;
                 float pred = v + e0[s];
@@ -990,6 +996,8 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 }
                 continue;
             }
+        }
+        if constexpr (MODE == GM_FWD) {
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], act_f(v + e0[s], g.act));
         } else if constexpr (MODE == GM_DX) {
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0[s], g.act));
@@ -1106,8 +1114,8 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     GEMM_PH(1);
     if constexpr (T32) {
         static_assert(!(MODE == GM_FWD && ROWK == 3), "T32: plain FWD / DX / DW tiles");
-        gemm_tile32<MODE, VEC, BF, (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5)>(
-            ga, g, tile - g.tile_begin, so, red);
+        gemm_tile32<MODE, VEC, BF, (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5),
+                    MODE == GM_FWD && ROWK == 8>(ga, g, tile - g.tile_begin, so, red);
         return;
     }
     const int lt = tile - g.tile_begin;
@@ -1128,7 +1136,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float e4 = 0.f;
     if constexpr (MODE == GM_FWD) {
         e0 = g.bias[nnc];
-        if constexpr (ROWK != 3 && ROWK != 5 && ROWK != 6) {   // head-fused / actor / fit launches: no mse problems
+        if constexpr (ROWK == 8) {   // launches with world-model head rows (mse problems) only
             // world-model head rows (mse): zero-sized resources when not an mse problem
             e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
             e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
@@ -1145,7 +1153,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         e3 = bload(make_rsrc(g.T, g.T != nullptr ? 0x7fffffffu : 0u), (uint32_t)pidx * 4u);
     }
     EpiScalars es{};
-    if constexpr (MODE == GM_DW || (MODE == GM_FWD && ROWK != 3 && ROWK != 5 && ROWK != 6))
+    if constexpr (MODE == GM_DW || (MODE == GM_FWD && ROWK == 8))
         es = epi_scalars(sr(ga.ctl, so), g.group);
     // partial-dot weights of this thread's output column (zero-sized resource: no partials)
     constexpr bool PART = (MODE == GM_DX && ROWK == 2) || (MODE == GM_FWD && ROWK == 5);
@@ -1463,7 +1471,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     float v = red[0][R][L] + red[1][R][L];
     v = v + red[2][R][L];
     v = v + red[3][R][L];
-    if constexpr (MODE == GM_FWD && ROWK != 3 && ROWK != 5 && ROWK != 6) {
+    if constexpr (MODE == GM_FWD && ROWK == 8) {
         if (g.mse) {          // uniform: the expert MSE / fit-loss epilogue (all 256 threads take part)
             const bool fit = g.mse == 2;
             float pred = v + e0;
@@ -1557,8 +1565,15 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
 #ifndef SACX_T32_QH_WGS
 #define SACX_T32_QH_WGS SACX_T32_WGS
 #endif
+// bf16 forward tiles without world-model head rows (rowk != 8: no mse epilogue operands held over the
+// main loop) fit 5 per CU: a 1,024-tile Humanoid q.fwd launch then runs in one round even with the
+// side stream's sampler holding a CU
+#ifndef SACX_T32_BF_FWD_WGS
+#define SACX_T32_BF_FWD_WGS 5
+#endif
 #define SACX_T32_OCC                                                                                         \
-    (T32 ? (MODE != GM_DW ? (BF ? SACX_T32_BF_WGS : (MODE == GM_DX && ROWK == 1 ? SACX_T32_QH_WGS : SACX_T32_WGS)) \
+    (T32 ? (MODE != GM_DW ? (BF ? (MODE == GM_FWD && ROWK != 8 ? SACX_T32_BF_FWD_WGS : SACX_T32_BF_WGS)          \
+                                : (MODE == GM_DX && ROWK == 1 ? SACX_T32_QH_WGS : SACX_T32_WGS))              \
                           : SACX_T32_DW_WGS)                                                                 \
          : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
@@ -1957,6 +1972,14 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
                     if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, false, false, false>), grid, block, 0, s, a);
                     else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, false, false, false>), grid, block, 0, s, a);
                 }
+            }
+        } else if (a.rowk == 8) {          // with world-model head rows (mse problems)
+            if (a.bf16) {
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 8, 4, true, PK, T32>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 8, 4, true, PK, T32>), grid, block, 0, s, a);
+            } else {
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 8, 4, false, PK, T32>), grid, block, 0, s, a);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 8, 4, false, PK, T32>), grid, block, 0, s, a);
             }
         } else if (a.bf16) {
             if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, a);

@@ -583,6 +583,10 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
             p.vec = (a4 ? 1 : 0) | (b4 ? 2 : 0);
         }
     }
+    // forward launches with world-model head rows (mse epilogues) take their own variant (rowk 8),
+    // so the others do not hold the mse operands in registers
+    for (auto& p : ps)
+        if (mode == GM_FWD && p.mse) L.gemm.rowk = 8;
     if (record_probs) h->probs.insert(h->probs.end(), ps.begin(), ps.end());
     L.gemm.dwl = dwl ? (h->dwl_nh == 1 ? 2 : 1) : 0;    // 2: 32x16 tiles, 1: 32x32
     L.gemm.mode = mode;
@@ -616,6 +620,10 @@ bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
     a.nprob += b.nprob;
     a.total_tiles += b.total_tiles;
     a.vec = a.vec || b.vec;
+    if (b.rowk == 8) {             // world-model head rows: the forward variant with mse operands
+        if (a.rowk != 0 && a.rowk != 8) return false;
+        a.rowk = 8;
+    }
     return true;
 }
 
