@@ -2047,7 +2047,190 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
     }
 }
 
+// ==================================================================== k_fwd2
+#ifndef SACX_FWD2_NW
+#define SACX_FWD2_NW 16   // waves per k_fwd2 workgroup (8 or 16)
+#endif
+// Two forward layers of a small-input net in ONE launch (GM_FWD2; one seed, fp32, 16x16 MFMA
+// tiles): a workgroup owns 16 rows x 64 columns of layer 1.  Its four waves first compute the 16
+// rows' whole layer 0 (wave w: the column tiles w, w + 4, ... of H0 <= 256; K0 <= 32) into LDS --
+// each 16-wide k slab's partial in k_gemm's acc0 / acc1 pattern, the slab partials added in the
+// order k_gemm's LDS reduction adds its waves', then bias and activation -- and column group 0's
+// workgroups store layer 0 for the backward.  Then layer 1: K = H0 split over the four waves as in
+// k_gemm (one group of <= 4 slabs each), A read from LDS, the partials reduced through LDS in wave
+// order, bias, activation, and (actor.fwd1, rowk 5) the head's per-tile partial dots.  Every output
+// is bit-identical to the two k_gemm launches; the launch boundary between them and layer 1's cold
+// operand round trip are gone.
+template <int VEC, int NW>
+__global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
+    // NW waves: layer 0 by column tiles (wave w: tiles w, w + NW, ... of H0 <= 256), layer 1 as
+    // k_gemm's four-way K split (wave w: quarter w & 3) for CTW of the group's four column tiles
+    constexpr int L0T = 16 / NW, CTW = 16 / NW;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    __shared__ float hs[16][256 + 4];
+    __shared__ float red2[4][4][4][64];    // [K quarter][column tile][q][lane]
+    const int nnet = ga.nprob >> 1;
+    const int tile = (int)blockIdx.x;
+    int p = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+        if (i < nnet && tile >= ga.probs[nnet + i].tile_begin) p = i;
+    const GemmProb g0 = ga.probs[p], g1 = ga.probs[nnet + p];
+    const int lt = tile - g1.tile_begin;
+    const int tm = lt / g1.tiles_n, cg = lt - tm * g1.tiles_n;
+    const int m0 = tm * 16;
+    const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 15, grp = lane >> 4;
+    const int kq = wave & 3, ch = wave >> 2;     // K quarter, column-tile group
+    const int m = m0 + r;
+    const bool mok = m < g0.M;
+    const int H0 = g0.N, N1 = g1.N;
+    const int nIt0 = (g0.K + 15) >> 4;       // <= 2 (host)
+    const int per1 = (H0 + 63) >> 6;         // layer-1 slabs per K quarter (H0 = 64 per1)
+
+    // ---- every operand requested up front
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(g0.A, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rw0 = make_rsrc(g0.B, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rw1 = make_rsrc(g1.B, 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rnull = rs(nullptr);
+    float xa[2][4];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) load_a<true, VEC == 1, false>(rx, g0, m, mok, s2 < nIt0 ? s2 * 16 + grp * 4 : (1 << 30), xa[s2], rnull);
+    float w0[L0T][2][4], b0[L0T];
+#pragma unroll
+    for (int i = 0; i < L0T; ++i) {
+        const int c = wave + NW * i;          // layer-0 column tile
+        const int nc = 16 * c + r;
+        const bool cok = nc < H0;
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) load_b<false, false>(rw0, g0, nc, cok, s2 < nIt0 && cok ? s2 * 16 + grp * 4 : (1 << 30), w0[i][s2]);
+        b0[i] = bload(rs(g0.bias), boff(cok, nc));
+    }
+    float w1[CTW][4][4];
+#pragma unroll
+    for (int j2 = 0; j2 < CTW; ++j2) {
+        const int ct = CTW * ch + j2;
+        const int n1 = 64 * cg + 16 * ct + r;
+        const bool nok = n1 < N1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int it = kq * per1 + u;
+            load_b<false, false>(rw1, g1, n1, nok, u < per1 ? it * 16 + grp * 4 : (1 << 30), w1[j2][u]);
+        }
+    }
+    // epilogue: thread t owns (row, col) of the column tiles CTW (t >> 8) + j2
+    const int te = threadIdx.x & 255, eh = threadIdx.x >> 8;
+    const int row = te >> 4, col = te & 15;
+    float b1[CTW];
+    float pwv[CTW][8];                          // head partial-dot weights of this thread's columns (rowk 5)
+#pragma unroll
+    for (int j2 = 0; j2 < CTW; ++j2) {
+        const int nn = 64 * cg + 16 * (CTW * eh + j2) + col;
+        b1[j2] = bload(rs(g1.bias), boff(nn < N1, nn));
+        const __amdgpu_buffer_rsrc_t rpw = rs(ga.rowk == 5 ? g1.pw : nullptr);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pwv[j2][j] = bload(rpw, boff(j < g1.pw_n && nn < N1, j * g1.pw_ld + min(nn, N1 - 1) * g1.pw_cs));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+
+    // ---- layer 0: per column tile, slab s2 is k_gemm's wave s2 (K0 <= 32: one slab per wave)
+#pragma unroll
+    for (int i = 0; i < L0T; ++i) {
+        const int c = wave + NW * i;
+        if (16 * c >= H0) break;              // uniform
+        floatx4 ps[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+            floatx4 x0 = {0.f, 0.f, 0.f, 0.f}, x1 = {0.f, 0.f, 0.f, 0.f};
+            x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s2][0], w0[i][s2][0], x0, 0, 0, 0);
+            x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s2][1], w0[i][s2][1], x1, 0, 0, 0);
+            x0 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s2][2], w0[i][s2][2], x0, 0, 0, 0);
+            x1 = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s2][3], w0[i][s2][3], x1, 0, 0, 0);
+            ps[s2] = x0 + x1;
+        }
+        const floatx4 v4 = ((ps[0] + ps[1]) + floatx4{0.f, 0.f, 0.f, 0.f}) + floatx4{0.f, 0.f, 0.f, 0.f};
+        // lane (r, grp) holds rows 4 grp + q of column 16 c + r
+        const int nc = 16 * c + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const float h = act_f(v4[q] + b0[i], g0.act);
+            hs[4 * grp + q][nc] = h;
+            const int mm = m0 + 4 * grp + q;
+            if (cg == 0 && mm < g0.M && nc < H0) st_out(&g0.C[(size_t)mm * g0.ldc + nc], h);
+        }
+    }
+    __syncthreads();
+
+    // ---- layer 1: K quarter kq (slabs kq * per1 + u), A from LDS, CTW column tiles
+    float a1[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int k0 = (kq * per1 + u) * 16 + grp * 4;
+        const float4 q4 = u < per1 ? *reinterpret_cast<const float4*>(&hs[r][k0]) : float4{0.f, 0.f, 0.f, 0.f};
+        a1[u][0] = q4.x; a1[u][1] = q4.y; a1[u][2] = q4.z; a1[u][3] = q4.w;
+    }
+#pragma unroll
+    for (int j2 = 0; j2 < CTW; ++j2) {
+        floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (u >= per1) break;             // uniform (k_gemm's zero slabs add +0)
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][0], w1[j2][u][0], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][1], w1[j2][u][1], acc1, 0, 0, 0);
+            acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][2], w1[j2][u][2], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][3], w1[j2][u][3], acc1, 0, 0, 0);
+        }
+        const floatx4 acc = acc0 + acc1;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red2[kq][CTW * ch + j2][q][lane] = acc[q];
+    }
+    __syncthreads();
+    // (row, col) lives in lane (row >> 2) * 16 + col, register row & 3 of each quarter's tile
+    const int L = ((row >> 2) << 4) | col, R = row & 3;
+    const int mm = m0 + row;
+    const int tiles16 = (N1 + 15) >> 4;
+#pragma unroll
+    for (int j2 = 0; j2 < CTW; ++j2) {
+        const int ct = CTW * eh + j2;
+        const int nn = 64 * cg + 16 * ct + col;
+        if (64 * cg + 16 * ct >= N1) break;   // uniform per wave
+        float v = red2[0][ct][R][L] + red2[1][ct][R][L];
+        v = v + red2[2][ct][R][L];
+        v = v + red2[3][ct][R][L];
+        const float x = nn < N1 ? act_f(v + b1[j2], g1.act) : 0.f;
+        if (ga.rowk == 5 && g1.ppart != nullptr) {
+            // the actor head's partial dots (k_gemm rowk 5), per 16-column tile
+            if (mm < g1.M) {
+                float mine = 0.f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float sdot = x * pwv[j2][j];
+                    sdot = sdot + dpp<0xB1>(sdot);
+                    sdot = sdot + dpp<0x4E>(sdot);
+                    sdot = sdot + dpp<0x124>(sdot);
+                    sdot = sdot + dpp<0x128>(sdot);
+                    mine = col == j ? sdot : mine;
+                }
+                if (col < g1.pw_n)
+                    st_out(&g1.ppart[((size_t)mm * g1.pw_n + col) * tiles16 + 4 * cg + ct], mine);
+            }
+        }
+        if (mm < g1.M && nn < N1 && g1.C != nullptr) st_out(&g1.C[(size_t)mm * g1.ldc + nn], x);
+    }
+    if (ga.ktime != nullptr) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            ga.ktime[2 * ktime_wg()] = t0;
+            ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
+    if (a.mode == GM_FWD2) {       // two forward layers in one launch (host: one seed, fp32, 16x16)
+        if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW>), dim3(a.total_tiles), dim3(SACX_FWD2_NW * 64), 0, s, a);
+        else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW>), dim3(a.total_tiles), dim3(SACX_FWD2_NW * 64), 0, s, a);
+        return;
+    }
     if (a.dwl) {   // dW + Adam with LDS-staged rows: plain problems only (no fused rows, no alpha.final)
         const dim3 grid(a.total_tiles, 1, seeds_z(a.nseeds)), block(256);
 #define SACX_DWLL(NH)                                                                                  \

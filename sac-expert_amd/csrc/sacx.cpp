@@ -156,6 +156,7 @@ struct sacx_handle {
                               // 3 also model.bwd2 into model.bwd1 (generated operand, heads of <= 32
                               // outputs; bit-identical, measured slower: HC 49.7 vs 46.9 us per step)
     int unaligned_b = 1;      // dX launches: float4 loads of W_ext rows at any 4-B offset (SACX_UNALIGNED)
+    int fwd2 = 1;             // two-layer forward pairs as one k_fwd2 launch where they qualify (SACX_FWD2)
     int mtile = 1;            // model fit tiles: 0 16x16, 1 16x16 + wide dW on 32x32, 2 the handle's (SACX_MTILE)
     int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
@@ -610,7 +611,75 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
 }
 
 // Appends the problems of GEMM launch `b` to launch `a` (same mode; tile ranges follow a's).
+// Replaces the plan's last two launches -- the layers 0 and 1 of the same nets, as add_gemm built
+// them -- by one k_fwd2 launch (GM_FWD2) when the pair qualifies: fp32, one seed, 16x16 tiles, plain
+// forward problems (layer 1 optionally with the actor head's partial dots, rowk 5), at most 4 nets,
+// K0 <= 32, H0 a multiple of 64 up to 256, layer 1 reading exactly layer 0's output.  Returns
+// whether it fused.
+bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& name) {
+    if (plan.size() < 2) return false;
+    Launch& L0 = plan[plan.size() - 2];
+    Launch& L1 = plan[plan.size() - 1];
+    const GemmArgs &a0 = L0.gemm, &a1 = L1.gemm;
+    if (L0.kind != Launch::GEMM || L1.kind != Launch::GEMM || a0.mode != GM_FWD || a1.mode != GM_FWD) return false;
+    if (a0.t32 || a1.t32 || a0.dwl || a1.dwl || a0.bf16 || a0.nseeds > 1 || h->seeds > 1) return false;
+    if (a0.rowk != 0 || (a1.rowk != 0 && a1.rowk != 5) || a0.has_final || a1.has_final || a0.nprob != a1.nprob ||
+        a0.nprob > 4)
+        return false;
+    bool vec = true;
+    for (int i = 0; i < a0.nprob; ++i) {
+        const GemmProb &p0 = a0.probs[i], &p1 = a1.probs[i];
+        if (p0.mse || p1.mse || p0.headp || p1.headp || p0.K > 32 || p0.N % 64 != 0 || p0.N > 256 ||
+            p1.K != p0.N || p1.A != p0.C || p1.lda != p0.ldc || p1.M != p0.M || p1.N % 16 != 0)
+            return false;
+        vec = vec && p0.vec;
+    }
+    Launch F = L1;
+    F.name = name;
+    GemmArgs& g = F.gemm;
+    const int n = a0.nprob;
+    int tiles = 0;
+    for (int i = 0; i < n; ++i) {
+        g.probs[i] = a0.probs[i];
+        GemmProb q = a1.probs[i];
+        q.tiles_n = (q.N + 63) / 64;
+        q.tile_begin = tiles;
+        tiles += ((q.M + 15) / 16) * q.tiles_n;
+        g.probs[n + i] = q;
+    }
+    g.nprob = 2 * n;
+    g.mode = GM_FWD2;
+    g.vec = vec ? 1 : 0;
+    g.total_tiles = tiles;
+    F.grid = tiles;
+    F.block = 1024;     // k_fwd2's SACX_FWD2_NW waves
+    F.flops = L0.flops + L1.flops;
+    F.bytes = L0.bytes + L1.bytes;
+    F.gemm_first = L0.gemm_first;
+    plan.pop_back();
+    plan.pop_back();
+    plan.push_back(F);
+    return true;
+}
+
 bool merge_gemm(GemmArgs& a, const GemmArgs& b) {
+    if (a.mode == GM_FWD2 || b.mode == GM_FWD2) {
+        // two k_fwd2 launches: layer-0 problems, then layer-1 problems, each launch's in order
+        const int na = a.nprob / 2, nb = b.nprob / 2;
+        if (a.mode != b.mode || na + nb > 4 || a.vec != b.vec) return false;
+        GemmProb l0[4], l1[4];
+        for (int i = 0; i < na; ++i) { l0[i] = a.probs[i]; l1[i] = a.probs[na + i]; }
+        for (int i = 0; i < nb; ++i) {
+            l0[na + i] = b.probs[i];
+            l1[na + i] = b.probs[nb + i];
+            l1[na + i].tile_begin += a.total_tiles;
+        }
+        for (int i = 0; i < na + nb; ++i) { a.probs[i] = l0[i]; a.probs[na + nb + i] = l1[i]; }
+        a.nprob = 2 * (na + nb);
+        a.total_tiles += b.total_tiles;
+        if (b.rowk == 5) a.rowk = 5;           // head partials: per problem (ppart null or not)
+        return true;
+    }
     if (a.mode != b.mode || a.t32 != b.t32 || a.dwl != b.dwl || a.nprob + b.nprob > GEMM_MAXP) return false;
     for (int i = 0; i < b.nprob; ++i) {
         GemmProb p = b.probs[i];
@@ -754,6 +823,11 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         add_gemm(h, plan, name + "0", p0, record_probs);
         add_gemm(h, plan, name + "1", p1, record_probs);
     };
+    // the same pair as ONE k_fwd2 launch where it qualifies (fuse_fwd2), else the two launches
+    auto fwd_pair2 = [&](const std::string& name, const std::vector<GemmProb>& p0, const std::vector<GemmProb>& p1) {
+        fwd_pair(name, p0, p1);
+        if (h->fwd2) fuse_fwd2(h, plan, name + "01");
+    };
     const int Ra4 = (h->Ra + 3) & ~3;       // first row of the alpha rows (ws.Hl1 / ws.Hl2 alias Ha1 / Ha2)
     // --actor_layer_norm: layer 0 writes the pre-norm Z, k_ln turns it into tanh(LN(Z)) in place
     auto ln_fwd = [&](const std::string& name, int r0, int r1) {
@@ -794,6 +868,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     } else {
         fwd_pair("actor.fwd", {prob_fwd(Xa, ldS, h->Ra, S, W("actor.l0"), H0, Ha1, a0)}, {actor_fwd1(0, h->Ra)});
         mark_part();
+        if (h->fwd2) fuse_fwd2(h, plan, "actor.fwd01");
     }
     // actor.head folded into q.fwd0 (plain SAC): the target tiles compute their rows' actions
     // in a prologue, the policy rows (and the previous update's alpha rows) run as extra
@@ -1019,7 +1094,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                                       Hm2b + (size_t)k * half * Hm1, m1));
             }
         }
-        fwd_pair("pi.q.fwd", p0, p1);
+        if (eo) fwd_pair("pi.q.fwd", p0, p1);
+        else fwd_pair2("pi.q.fwd", p0, p1);
         if (eo) {                            // plan.back() is pi.q.fwd1: fold into pi.q.fwd0 (or, with
                                              // the fused head, into pi.q.fwd1: Hm2 comes from pi.q.fwd0)
             Launch& F0 = plan[plan.size() - (fuse_head ? 1 : 2)];
@@ -1196,6 +1272,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         fwd_pair("alpha.fwd", {prob_fwd(Xa + (size_t)B * ldS, ldS, B, S, W("actor.l0"), H0, Hl1, a0)},
                  {actor_fwd1(Ra4, B)});
         mark_part();
+        // fused as the actor pair is, so merged_body folds one k_fwd2 launch into the other
+        if (h->fwd2) fuse_fwd2(h, plan, "alpha.fwd01");
     }
     {
         Launch L{};
@@ -1965,6 +2043,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (const char* e = std::getenv("SACX_MFUSE")) h->mfuse = std::atoi(e);
     if (const char* e = std::getenv("SACX_MTILE")) h->mtile = std::atoi(e);
     if (const char* e = std::getenv("SACX_UNALIGNED")) h->unaligned_b = std::atoi(e);
+    if (const char* e = std::getenv("SACX_FWD2")) h->fwd2 = std::atoi(e);
     if (const char* e = std::getenv("SACX_DWL_NH")) h->dwl_nh = std::atoi(e) == 2 ? 2 : 1;
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);

@@ -55,7 +55,10 @@ struct AdamConsts {
 // K split over the 4 waves of a 256-thread workgroup and reduced through LDS.
 enum Epi { EPI_FWD = 0, EPI_DACT = 1, EPI_ADAM = 2, EPI_STORE = 3 };
 // launch-uniform operand/epilogue mode of k_gemm (template parameter)
-enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2 };
+// GM_FWD2: two forward layers of small-input nets in one launch (k_fwd2): probs[0, n) are layer 0,
+// probs[n, 2n) layer 1 of the same nets (layer 1 reads layer 0's output); the layer-1 problems'
+// tile_begin / tiles_n count (16-row block, 64-column group) workgroups
+enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2, GM_FWD2 = 3 };
 
 struct GemmProb {
     const float* A;        // a_kc: A[m*lda + k]   else A[k*lda + m] (row ones_row = 1.0)

@@ -278,6 +278,28 @@ def test_model_fit_matches_oracle(gpu_available, eager):
     eng.close()
 
 
+@pytest.mark.parametrize("act,B,eager", [("relu", 256, False), ("tanh", 256, True), ("elu", 100, False)])
+def test_fused_forward_pair_bit_identical(gpu_available, monkeypatch, act, B, eager):
+    """The two-layer forward pairs as ONE k_fwd2 launch each (both layers per workgroup, layer 0 in
+    LDS, SACX_FWD2=1, the default): the policy-loss critics' pair, the actor pair (with the head's
+    partial dots) and the alpha branch's pair folded into the next update's actor launch -- the
+    updates equal the two-launch k_gemm chain's bit for bit, eager and graph."""
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("SACX_FWD2", fused)
+        eng, ocfg, st, buf, nrm, _ = make_pair(act=act, B=B, seed=41, normalizers="random", graph_steps=8)
+        names = [L["name"] for L in eng.plan_info()]
+        for pair in ("pi.q.fwd01", "actor.fwd01", "alpha.fwd01"):
+            assert (pair in names) == (fused == "1"), names
+        eng.rng_set_state(np.random.RandomState(6).get_state())
+        eng.step(19, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy()))
+        eng.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)
+
+
 @pytest.mark.parametrize("S,A,B,clip", [(17, 6, 256, 0.0), (376, 17, 1024, 0.0), (17, 6, 64, 5.0)])
 def test_model_fit_folds_bit_identical(gpu_available, monkeypatch, S, A, B, clip):
     """The folded world-model fit chain (the loss and its gradient in model.fwd2's epilogue,
