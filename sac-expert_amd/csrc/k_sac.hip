@@ -615,8 +615,13 @@ __device__ void mfit_final(const MFinalArgs& f) {
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
 __device__ __forceinline__ void qhead_block(const QHeadArgs& q, int block, int64_t so);
+template <int NQ, int OW = 0, bool TICKET = false>
+__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so,
+                                                const FinalArgs& ffin);
 template <int NQ, int OW = 0>
-__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so);
+__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
+    actor_head_body<NQ, OW, false>(h, f, block, so, f);
+}
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
 // so blocks b and b+8 share an L2.  xcd_tile gives the blocks of one XCD a contiguous range of
@@ -633,6 +638,7 @@ __device__ __forceinline__ int xcd_tile(int b, int T) {
 // over the 4 waves) -- and the A tile [state columns of A | normalised actions] is staged in
 // LDS for the main loop.  Column tile 0 stores the rows' neglogp for q.head.  The same
 // arithmetic as k_actor_head, with the 16-lane row sums of the MFMA layout.
+template <bool SYNC = true>
 __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb& g, int m0, int tn,
                                               float (&As)[16][68], float (&red)[4][4][64], int64_t so) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 15, grp = lane >> 4;
@@ -730,7 +736,7 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
     for (int q = 0; q < 4; ++q)
         if (col + 16 * q < S) As[row][col + 16 * q] = xs[q];
     if (jok) As[row][S + col] = pin;
-    __syncthreads();
+    if constexpr (SYNC) __syncthreads();   // else the caller's (k_fwd2: threads >= 256 skip the body)
 }
 
 // actor.head.bwd folded into actor.bwd1 (rowk 4): the policy-row work of k_actor_bwd for the
@@ -2051,6 +2057,7 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 #ifndef SACX_FWD2_NW
 #define SACX_FWD2_NW 16   // waves per k_fwd2 workgroup (8 or 16)
 #endif
+
 // Two forward layers of a small-input net in ONE launch (GM_FWD2; one seed, fp32, 16x16 MFMA
 // tiles): a workgroup owns 16 rows x 64 columns of layer 1.  Its four waves first compute the 16
 // rows' whole layer 0 (wave w: the column tiles w, w + 4, ... of H0 <= 256; K0 <= 32) into LDS --
@@ -2061,8 +2068,12 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 // order, bias, activation, and (actor.fwd1, rowk 5) the head's per-tile partial dots.  Every output
 // is bit-identical to the two k_gemm launches; the launch boundary between them and layer 1's cold
 // operand round trip are gone.
-template <int VEC, int NW>
-__global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
+// HEAD (the target / critic pair of plain SAC, rowk 3): the first row_blocks workgroups are actor-head
+// rows (4 waves each: the previous update's alpha rows, whose last block then finalises that update's
+// alpha, k_alpha_final's work, when has_final), and the target nets' tiles (headp) compute their 16
+// rows' evaluate() actions in a prologue (head_prologue, actor.fwd1's partial dots) into the LDS A tile
+template <int VEC, int NW, bool HEAD>
+__global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArgs ga) {   // (min waves per SIMD)
     // NW waves: layer 0 by column tiles (wave w: tiles w, w + NW, ... of H0 <= 256), layer 1 as
     // k_gemm's four-way K split (wave w: quarter w & 3) for CTW of the group's four column tiles
     constexpr int L0T = 16 / NW, CTW = 16 / NW;
@@ -2070,7 +2081,23 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
     __shared__ float hs[16][256 + 4];
     __shared__ float red2[4][4][4][64];    // [K quarter][column tile][q][lane]
     const int nnet = ga.nprob >> 1;
-    const int tile = (int)blockIdx.x;
+    int tile = (int)blockIdx.x;
+    if constexpr (HEAD) {
+        if (tile < ga.row_blocks) {           // actor-head rows, dispatched first: NW / 4 blocks of 4
+            const int blk = ga.head_block0 + (NW / 4) * tile;
+            if (ga.has_final) actor_head_body<4, 0, true>(ga.head, ga.hfin, blk, 0, ga.fin);
+            else actor_head_body<4, 0, false>(ga.head, ga.hfin, blk, 0, ga.fin);
+            if (ga.ktime != nullptr) {
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    ga.ktime[2 * ktime_wg()] = t0;
+                    ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
+                }
+            }
+            return;
+        }
+        tile -= ga.row_blocks;
+    }
     int p = 0;
 #pragma unroll
     for (int i = 1; i < 4; ++i)
@@ -2081,6 +2108,7 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
     const int m0 = tm * 16;
     const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 15, grp = lane >> 4;
     const int kq = wave & 3, ch = wave >> 2;     // K quarter, column-tile group
+    const bool headp = HEAD && g0.headp;
     const int m = m0 + r;
     const bool mok = m < g0.M;
     const int H0 = g0.N, N1 = g1.N;
@@ -2094,7 +2122,8 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
     const __amdgpu_buffer_rsrc_t rnull = rs(nullptr);
     float xa[2][4];
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) load_a<true, VEC == 1, false>(rx, g0, m, mok, s2 < nIt0 ? s2 * 16 + grp * 4 : (1 << 30), xa[s2], rnull);
+    for (int s2 = 0; s2 < 2; ++s2)
+        load_a<true, VEC == 1, false>(rx, g0, m, mok && !headp, s2 < nIt0 ? s2 * 16 + grp * 4 : (1 << 30), xa[s2], rnull);
     float w0[L0T][2][4], b0[L0T];
 #pragma unroll
     for (int i = 0; i < L0T; ++i) {
@@ -2121,16 +2150,38 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
     const int te = threadIdx.x & 255, eh = threadIdx.x >> 8;
     const int row = te >> 4, col = te & 15;
     float b1[CTW];
-    float pwv[CTW][8];                          // head partial-dot weights of this thread's columns (rowk 5)
+    constexpr int NPW = HEAD ? 1 : 8;         // (the head pair never writes the head's partial dots)
+    float pwv[CTW][NPW];                      // head partial-dot weights of this thread's columns (rowk 5)
 #pragma unroll
     for (int j2 = 0; j2 < CTW; ++j2) {
         const int nn = 64 * cg + 16 * (CTW * eh + j2) + col;
         b1[j2] = bload(rs(g1.bias), boff(nn < N1, nn));
-        const __amdgpu_buffer_rsrc_t rpw = rs(ga.rowk == 5 ? g1.pw : nullptr);
+        if constexpr (!HEAD) {
+            const __amdgpu_buffer_rsrc_t rpw = rs(ga.rowk == 5 ? g1.pw : nullptr);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) pwv[j2][j] = bload(rpw, boff(j < g1.pw_n && nn < N1, j * g1.pw_ld + min(nn, N1 - 1) * g1.pw_cs));
+            for (int j = 0; j < NPW; ++j)
+                pwv[j2][j] = bload(rpw, boff(j < g1.pw_n && nn < N1, j * g1.pw_ld + min(nn, N1 - 1) * g1.pw_cs));
+        }
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (HEAD) {
+        // the target rows' A tile [sp_n | evaluate() actions], as k_gemm_head's tile prologue; column
+        // group 0 stores the rows' neglogp for q.head (host: the head's partial dots exist, so the
+        // prologue has no barrier of its own)
+        __shared__ float As[16][68];
+        __shared__ float hred[4][4][64];
+        if (headp) {                          // uniform
+            if (threadIdx.x < 256) head_prologue<false>(ga.head, g0, m0, cg, As, hred, 0);
+            __syncthreads();
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int k = s2 * 16 + grp * 4 + j;
+                    xa[s2][j] = (s2 < nIt0 && k < g0.K) ? As[r][k] : 0.f;
+                }
+        }
+    }
 
     // ---- layer 0: per column tile, slab s2 is k_gemm's wave s2 (K0 <= 32: one slab per wave)
 #pragma unroll
@@ -2197,12 +2248,12 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
         v = v + red2[2][ct][R][L];
         v = v + red2[3][ct][R][L];
         const float x = nn < N1 ? act_f(v + b1[j2], g1.act) : 0.f;
-        if (ga.rowk == 5 && g1.ppart != nullptr) {
+        if (!HEAD && ga.rowk == 5 && g1.ppart != nullptr) {
             // the actor head's partial dots (k_gemm rowk 5), per 16-column tile
             if (mm < g1.M) {
                 float mine = 0.f;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
+                for (int j = 0; j < NPW; ++j) {
                     float sdot = x * pwv[j2][j];
                     sdot = sdot + dpp<0xB1>(sdot);
                     sdot = sdot + dpp<0x4E>(sdot);
@@ -2227,8 +2278,15 @@ __global__ __launch_bounds__(NW * 64, 1) void k_fwd2(GemmArgs ga) {
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
     if (a.mode == GM_FWD2) {       // two forward layers in one launch (host: one seed, fp32, 16x16)
-        if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW>), dim3(a.total_tiles), dim3(SACX_FWD2_NW * 64), 0, s, a);
-        else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW>), dim3(a.total_tiles), dim3(SACX_FWD2_NW * 64), 0, s, a);
+        const dim3 block(SACX_FWD2_NW * 64);
+        if (a.rowk == 3) {          // the target / critic pair with the actor-head rows
+            const dim3 grid(a.total_tiles + a.row_blocks), hblock(SACX_FWD2_HEAD_NW * 64);
+            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_HEAD_NW, true>), grid, hblock, 0, s, a);
+            else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_HEAD_NW, true>), grid, hblock, 0, s, a);
+        } else {
+            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW, false>), dim3(a.total_tiles), block, 0, s, a);
+            else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW, false>), dim3(a.total_tiles), block, 0, s, a);
+        }
         return;
     }
     if (a.dwl) {   // dW + Adam with LDS-staged rows: plain problems only (no fused rows, no alpha.final)
@@ -2751,9 +2809,14 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // ==================================================================== k_actor_head
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
-template <int NQ, int OW>
-__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
-    __shared__ float red_s[4];
+// TICKET (k_fwd2's fused q launch): the alpha blocks take a ticket after storing their partial, and
+// the last of them runs the previous update's alpha finalisation (ffin) in the same launch
+template <int NQ, int OW, bool TICKET>
+__device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so,
+                                                const FinalArgs& ffin) {
+    // a workgroup of 4 G waves runs G blocks of 4 rows (block + wave >> 2): per block the same partial
+    __shared__ float red_s[16];
+    __shared__ int last_s[4];
     __shared__ float w3s[OW > 0 ? 256 * OW : 1];
     if constexpr (OW > 0) {
         // W3 (H1 x Aout, row-major) copied whole into LDS by the workgroup: contiguous loads,
@@ -2769,7 +2832,8 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
             if ((int)threadIdx.x + 256 * c < n) w3s[threadIdx.x + 256 * c] = wv[c];
         __syncthreads();
     }
-    const int wave = wave_id(), lane = threadIdx.x & 63;
+    const int wave = wave_id() & 3, lane = threadIdx.x & 63, g4 = wave_id() >> 2;
+    block += g4;
     const int row = block * 4 + wave;
     float row_ent = 0.f;
     int sidx = 0;
@@ -2880,15 +2944,35 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
             row_ent = -nlp + f.target_entropy;
         }
     }
-    if (!h.alpha_mode || block * 4 < h.alpha_row0) return;
+    // (a group whose block is past the rows -- the last workgroup of k_fwd2's rows -- ends here too)
+    if (!h.alpha_mode || block * 4 < h.alpha_row0 || block * 4 >= h.total_rows) return;
     // ---- alpha: block partial of sum(-nlp + H); k_alpha_final reduces them
-    if (lane == 0) red_s[wave] = row_ent;
+    if (lane == 0) red_s[4 * g4 + wave] = row_ent;
+    if constexpr (TICKET) {
+        if (threadIdx.x < 4) last_s[threadIdx.x] = 0;
+    }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        float part = red_s[0] + red_s[1];
-        part = part + red_s[2];
-        part = part + red_s[3];
+    if ((threadIdx.x & 255) == 0) {
+        float part = red_s[4 * g4] + red_s[4 * g4 + 1];
+        part = part + red_s[4 * g4 + 2];
+        part = part + red_s[4 * g4 + 3];
         sr(f.red, so)[block - h.alpha_row0 / 4] = part;
+        if constexpr (TICKET) {
+            // release this partial, count it; the block that brings the count to nred acquires the
+            // others' (vector atomics on the control block; self-resetting)
+            const int old = __hip_atomic_fetch_add(&ffin.ctl->red_counter[0], 1, __ATOMIC_ACQ_REL,
+                                                   __HIP_MEMORY_SCOPE_AGENT);
+            last_s[g4] = old == ffin.nred - 1;
+        }
+    }
+    if constexpr (TICKET) {
+        __syncthreads();
+        if (last_s[0] | last_s[1] | last_s[2] | last_s[3]) {
+            // wave 0 finalises; the acquire of the other blocks' partials is its own
+            if (threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            finalize_update(ffin, ffin.nred);
+            if (threadIdx.x == 0) __hip_atomic_store(&ffin.ctl->red_counter[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
 }
 

@@ -623,13 +623,17 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     const GemmArgs &a0 = L0.gemm, &a1 = L1.gemm;
     if (L0.kind != Launch::GEMM || L1.kind != Launch::GEMM || a0.mode != GM_FWD || a1.mode != GM_FWD) return false;
     if (a0.t32 || a1.t32 || a0.dwl || a1.dwl || a0.bf16 || a0.nseeds > 1 || h->seeds > 1) return false;
-    if (a0.rowk != 0 || (a1.rowk != 0 && a1.rowk != 5) || a0.has_final || a1.has_final || a0.nprob != a1.nprob ||
-        a0.nprob > 4)
+    // layer 0 may carry the actor head (rowk 3: target tile prologues from the head's partial dots,
+    // which keep the prologue free of barriers, and head rows as extra workgroups)
+    const bool head = a0.rowk == 3;
+    if ((a0.rowk != 0 && !head) || (a1.rowk != 0 && a1.rowk != 5) || (head && a1.rowk != 0) || a0.has_final ||
+        a1.has_final || a0.nprob != a1.nprob || a0.nprob > 4)
         return false;
+    if (head && (a0.head.part == nullptr || a0.head.H1 > 256 || a0.head.A > 16)) return false;
     bool vec = true;
     for (int i = 0; i < a0.nprob; ++i) {
         const GemmProb &p0 = a0.probs[i], &p1 = a1.probs[i];
-        if (p0.mse || p1.mse || p0.headp || p1.headp || p0.K > 32 || p0.N % 64 != 0 || p0.N > 256 ||
+        if (p0.mse || p1.mse || (p0.headp && !head) || p1.headp || p0.K > 32 || p0.N % 64 != 0 || p0.N > 256 ||
             p1.K != p0.N || p1.A != p0.C || p1.lda != p0.ldc || p1.M != p0.M || p1.N % 16 != 0)
             return false;
         vec = vec && p0.vec;
@@ -651,8 +655,17 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     g.mode = GM_FWD2;
     g.vec = vec ? 1 : 0;
     g.total_tiles = tiles;
+    g.rowk = head ? 3 : a1.rowk;
+    if (head) {
+        g.head = a0.head;
+        g.hfin = a0.hfin;
+        g.head_block0 = a0.head_block0;
+    }
+    if (head && a0.row_blocks != 0) return false;   // plain SAC: the head rows come with merged_body only
+    g.row_blocks = 0;
     F.grid = tiles;
-    F.block = 1024;     // k_fwd2's SACX_FWD2_NW waves
+    F.frees_slot = L0.frees_slot || L1.frees_slot;
+    F.block = head ? SACX_FWD2_HEAD_NW * 64 : 1024;     // k_fwd2 waves
     F.flops = L0.flops + L1.flops;
     F.bytes = L0.bytes + L1.bytes;
     F.gemm_first = L0.gemm_first;
@@ -975,6 +988,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             }
         }
         add_gemm(h, plan, "q.fwd1", p1, record_probs);
+        if (h->fwd2 && !eo) fuse_fwd2(h, plan, "q.fwd01+actor.head");
     } else {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 4; ++k) {
@@ -1597,12 +1611,20 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                     C.fin = ph->fin;
                 } else {
                     C.gemm.hfin = ph->fin;
-                    const int rb = (a.total_rows + 3) / 4 - C.gemm.head_block0;
+                    int rb = (a.total_rows + 3) / 4 - C.gemm.head_block0;
+                    if (C.gemm.mode == GM_FWD2) rb = (rb + SACX_FWD2_HEAD_NW / 4 - 1) / (SACX_FWD2_HEAD_NW / 4);
                     C.grid += rb - C.gemm.row_blocks;
                     C.gemm.row_blocks = rb;
                 }
                 C.name += "+alpha";
                 head_done = true;
+                if (C.kind == Launch::GEMM && C.gemm.mode == GM_FWD2 && pf) {
+                    // k_fwd2 has no later forward launch to take it: the last alpha block finalises
+                    C.gemm.has_final = 1;
+                    C.gemm.fin = pf->fin;
+                    C.name += ".final";
+                    final_done = true;
+                }
             } else if (C.kind == Launch::GEMM && head_done && !final_done && pf &&
                        C.gemm.mode == GM_FWD) {
                 C.gemm.has_final = 1;
@@ -1646,8 +1668,10 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         const bool timed = kt && (L.kind == Launch::GEMM || (kt->rows && (L.kind == Launch::AHEAD || L.kind == Launch::ABWD)));
         if (timed) {
             Launch C = L;
+            // (a k_fwd2 launch finalises alpha in its last alpha block, not in a workgroup of its own)
+            const int fin_wg = C.gemm.has_final && C.gemm.mode != GM_FWD2 ? 1 : 0;
             const int nwg1 = L.kind == Launch::GEMM
-                                 ? C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0) + (C.gemm.rowk ? C.gemm.row_blocks : 0)
+                                 ? C.gemm.total_tiles + fin_wg + (C.gemm.rowk ? C.gemm.row_blocks : 0)
                                  : (L.kind == Launch::AHEAD ? (C.head.total_rows + 3) / 4 : C.grid);
             const int nwg = nwg1 * h->seeds;   // slots of every seed (seed-major)
             if (kt->used + 2 * nwg <= kt->cap) {
@@ -1659,8 +1683,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 kt->names.push_back(C.name);
                 kt->is_gemm.push_back(L.kind == Launch::GEMM);
                 if (L.kind != Launch::GEMM) kt->rowspan.push_back({0, 0});
-                else if (C.gemm.rowk == 3) kt->rowspan.push_back({C.gemm.has_final ? 1 : 0, (C.gemm.has_final ? 1 : 0) + C.gemm.row_blocks});
-                else kt->rowspan.push_back({C.gemm.total_tiles + (C.gemm.has_final ? 1 : 0), nwg1});
+                else if (C.gemm.rowk == 3) kt->rowspan.push_back({fin_wg, fin_wg + C.gemm.row_blocks});
+                else kt->rowspan.push_back({C.gemm.total_tiles + fin_wg, nwg1});
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);

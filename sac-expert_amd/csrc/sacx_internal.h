@@ -59,6 +59,9 @@ enum Epi { EPI_FWD = 0, EPI_DACT = 1, EPI_ADAM = 2, EPI_STORE = 3 };
 // probs[n, 2n) layer 1 of the same nets (layer 1 reads layer 0's output); the layer-1 problems'
 // tile_begin / tiles_n count (16-row block, 64-column group) workgroups
 enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2, GM_FWD2 = 3 };
+// waves per k_fwd2 workgroup of the pair that carries actor-head rows (rowk 3): two workgroups per CU,
+// so the 256 tiles and the head rows run in one round; its head rows take NW / 4 blocks of 4 rows each
+#define SACX_FWD2_HEAD_NW 8
 
 struct GemmProb {
     const float* A;        // a_kc: A[m*lda + k]   else A[k*lda + m] (row ones_row = 1.0)

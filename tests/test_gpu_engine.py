@@ -282,14 +282,16 @@ def test_model_fit_matches_oracle(gpu_available, eager):
 def test_fused_forward_pair_bit_identical(gpu_available, monkeypatch, act, B, eager):
     """The two-layer forward pairs as ONE k_fwd2 launch each (both layers per workgroup, layer 0 in
     LDS, SACX_FWD2=1, the default): the policy-loss critics' pair, the actor pair (with the head's
-    partial dots) and the alpha branch's pair folded into the next update's actor launch -- the
-    updates equal the two-launch k_gemm chain's bit for bit, eager and graph."""
+    partial dots), the alpha branch's pair folded into the next update's actor launch, and the
+    target / critic pair with the actor-head prologue, the previous update's alpha rows and their
+    finalisation by the last alpha block -- the updates equal the k_gemm chain's bit for bit, eager
+    and graph."""
     outs = []
     for fused in ("0", "1"):
         monkeypatch.setenv("SACX_FWD2", fused)
         eng, ocfg, st, buf, nrm, _ = make_pair(act=act, B=B, seed=41, normalizers="random", graph_steps=8)
         names = [L["name"] for L in eng.plan_info()]
-        for pair in ("pi.q.fwd01", "actor.fwd01", "alpha.fwd01"):
+        for pair in ("pi.q.fwd01", "actor.fwd01", "alpha.fwd01", "q.fwd01+actor.head"):
             assert (pair in names) == (fused == "1"), names
         eng.rng_set_state(np.random.RandomState(6).get_state())
         eng.step(19, eager=eager)
