@@ -136,7 +136,9 @@ def rocprof_family_avg(kernel, config, flops_per_launch):
     tot, n = 0.0, 0
     with open(paths[-1]) as fh:
         for r in csv.DictReader(fh):
-            if f"::{kernel}<" in r["Name"] or f"::{kernel}(" in r["Name"] or f"{kernel}_head<" in r["Name"]:
+            # the plan's GEMM launches: k_gemm, k_gemm_head and k_fwd2 (two forward layers per launch)
+            if (f"::{kernel}<" in r["Name"] or f"::{kernel}(" in r["Name"] or f"{kernel}_head<" in r["Name"]
+                    or (kernel == "k_gemm" and "::k_fwd2<" in r["Name"])):
                 tot += float(r["TotalDurationNs"])
                 n += int(r["Calls"])
     if n == 0:

@@ -9,7 +9,7 @@ k_gemm's MFMA-fragment loads (16 lanes x 4 B = one 64-B piece of a row, 4 rows p
 instruction).  So f = 1 for k_gemm (its operand and epilogue loads are all 64-B row pieces),
 f = 2 for the row-streaming kernels.
 Families follow sacx kernel names (template arguments folded: k_gemm<1, 1> -> k_gemm;
-k_gemm_head -> k_gemm).
+k_gemm_head, k_fwd2 -> k_gemm).
 usage: python tools/pmc_summary.py gpurun_out/pmc hc [source-tag] [extra-copy-path]
 """
 import csv
@@ -26,14 +26,17 @@ def family(name):
     m = re.search(r"sacx::(k_[a-z_]+)", n)
     if not m:
         return None
-    # k_gemm_head is k_gemm with the actor-head prologue (one launch of the k_gemm family)
-    return "k_gemm" if m.group(1).startswith("k_gemm") else m.group(1)
+    # k_gemm_head is k_gemm with the actor-head prologue, k_fwd2 two forward layers in one launch:
+    # launches of the k_gemm family (the plan's GEMM launches)
+    return "k_gemm" if m.group(1).startswith("k_gemm") or m.group(1) == "k_fwd2" else m.group(1)
 
 
 def subfamily(name):
     """k_gemm launches split by operand mode (template argument 0): fwd / dx / dw (+ Adam) / fwd2."""
     if "k_gemm_head" in name:              # the forward launch with the actor-head prologue
         return "k_gemm.fwd_head"
+    if "k_fwd2" in name:                   # two forward layers in one launch
+        return "k_gemm.fwd2"
     m = re.search(r"sacx::k_gemm<(\d+)", name)
     if not m:
         return None
