@@ -2960,7 +2960,8 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         if constexpr (TICKET) {
             // release this partial, count it; the block that brings the count to nred acquires the
             // others' (vector atomics on the control block; self-resetting)
-            const int old = __hip_atomic_fetch_add(&ffin.ctl->red_counter[0], 1, __ATOMIC_ACQ_REL,
+            // (release only: the cache invalidation of an acquire is the last block's alone, below)
+            const int old = __hip_atomic_fetch_add(&ffin.ctl->red_counter[0], 1, __ATOMIC_RELEASE,
                                                    __HIP_MEMORY_SCOPE_AGENT);
             last_s[g4] = old == ffin.nred - 1;
         }
@@ -2968,7 +2969,8 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
     if constexpr (TICKET) {
         __syncthreads();
         if (last_s[0] | last_s[1] | last_s[2] | last_s[3]) {
-            // wave 0 finalises; the acquire of the other blocks' partials is its own
+            // wave 0 finalises; the acquire of the other blocks' partials is its own (the counter
+            // reached nred: every partial was released before its block's increment)
             if (threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             finalize_update(ffin, ffin.nred);
             if (threadIdx.x == 0) __hip_atomic_store(&ffin.ctl->red_counter[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
