@@ -61,6 +61,9 @@ for step in "$@"; do
     pmc)
       CONFIG=${arg:-hc} bash tools/gpu_pmc.sh > "$log" 2>&1
       rc=$?; echo "[$n pmc ${arg:-hc}] rc=$rc"; tail -n 3 "$log" ;;
+    overhead)   # fixed cost of one step(n) call (sampler start-up, alpha tail, launch + wake-up)
+      timeout -k 10 200 python tools/step_overhead.py $arg > "$log" 2>&1
+      rc=$?; echo "[$n overhead] rc=$rc"; cat "$log" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
