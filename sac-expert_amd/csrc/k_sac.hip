@@ -197,6 +197,22 @@ __device__ __forceinline__ uint32_t boff(bool ok, int elem) {
     asm("" : "+v"(o));
     return o;
 }
+
+// a converted slab pair as one bf16x8 operand (k = s0 + 4 grp + j, then s1 + 4 grp + j)
+__device__ __forceinline__ bf16x8_t pack_bf16(const float (&x0)[4], const float (&x1)[4]) {
+    return bf16x8_t{(__bf16)x0[0], (__bf16)x0[1], (__bf16)x0[2], (__bf16)x0[3],
+                    (__bf16)x1[0], (__bf16)x1[1], (__bf16)x1[2], (__bf16)x1[3]};
+}
+__device__ __forceinline__ bf16x8_t wbf_load(__amdgpu_buffer_rsrc_t r, bool ok, int elem) {
+    uint32_t o = ok ? (uint32_t)elem * 2u : SACX_BUF_OOB;
+    asm("" : "+v"(o));
+    return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
+}
+// a weight's bf16 shadow element (round to nearest even, as the converting loads)
+__device__ __forceinline__ void wbf_store(uint16_t* S, const GemmProb& g, int k, int n, float v) {
+    if (S != nullptr && k < g.wbf_k)
+        S[(size_t)n * g.wbf_ld + wbf_pos(k, g.wbf_per)] = __builtin_bit_cast(uint16_t, (__bf16)v);
+}
 // The control-block scalars a GEMM epilogue needs (the optimiser step, the Polyak gate, the
 // expert weight), requested with the epilogue operands before the main loop: read after the
 // tile reduction they were two more dependent memory round trips (the kernarg ctl pointer,
@@ -239,6 +255,7 @@ __device__ __forceinline__ void reloc(GemmProb& g, int64_t so) {
     g.bscale = sr(g.bscale, so); g.se_raw = sr(g.se_raw, so); g.spe_raw = sr(g.spe_raw, so);
     g.dmean = sr(g.dmean, so); g.dden = sr(g.dden, so); g.part = sr(g.part, so);
     g.pw = sr(g.pw, so); g.ppart = sr(g.ppart, so);
+    g.wbf = sr(g.wbf, so); g.obf = sr(g.obf, so); g.abf = sr(g.abf, so);
 }
 __device__ __forceinline__ void reloc(HeadBwdArgs& b, int64_t so) {
     b.part = sr(b.part, so); b.gpol = sr(b.gpol, so); b.a_den = sr(b.a_den, so); b.alpha = sr(b.alpha, so);
@@ -376,49 +393,86 @@ __device__ float mean_rows(const float* x, int n) {
 // 16 loads in flight per round, one round for B <= 256 and four for Humanoid's B = 1,024.
 // (One array after the other, the dependent chunk loads made the folded alpha.final the
 // longest workgroup of its Humanoid launch.)
-__device__ __forceinline__ void strided_sums4(const float* const (&x)[4], const int (&n)[4], float (&s)[4]) {
+template <int NA>
+__device__ __forceinline__ void strided_sums(const float* const (&x)[NA], const int (&n)[NA], float (&s)[NA]) {
     const int lane = threadIdx.x & 63;
-    __amdgpu_buffer_rsrc_t r[4];
+    __amdgpu_buffer_rsrc_t r[NA];
     int nmax = 0;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
+    for (int a = 0; a < NA; ++a) {
         r[a] = rs(x[a]);
         s[a] = 0.f;
         nmax = max(nmax, n[a]);
     }
     for (int base = 0; base < nmax; base += 256) {
-        float v[4][4];
+        float v[NA][4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int i = base + lane + 64 * u;
                 v[a][u] = bload(r[a], boff(i < n[a], i));
             }
 #pragma unroll
-        for (int a = 0; a < 4; ++a)
+        for (int a = 0; a < NA; ++a)
 #pragma unroll
             for (int u = 0; u < 4; ++u) s[a] += v[a][u];
     }
 }
 
-__device__ void finalize_update(const FinalArgs& f, int nred) {
+// The finalisation's operands that are final before the alpha rows run (the critic and policy
+// loss rows of the update, alpha and its moments, the counters): the ticketed path (k_fwd2's
+// fused q launch) loads them before its blocks take their tickets, so the last block's critical
+// path after the ticket is the alpha partials' load alone.  Same sums, same order.
+#ifndef SACX_FIN_PRE
+#define SACX_FIN_PRE 1
+#endif
+struct FinPre {
+    float ps[3];
+    float a_old, a_m, a_v;
+    int64_t t_sac, seq0, nts, tsi;
+};
+
+__device__ __forceinline__ void fin_prefetch(const FinalArgs& f, FinPre& p) {
+    const float* const xs[3] = {f.lq, f.lq + f.B, f.lp};
+    const int ns[3] = {f.B, f.B, f.B};
+    p.a_old = p.a_m = p.a_v = 0.f;
+    p.t_sac = p.seq0 = p.nts = p.tsi = 0;
+    if ((threadIdx.x & 63) == 0) {
+        p.a_old = *f.alpha; p.a_m = *f.alpha_m; p.a_v = *f.alpha_v;
+        p.t_sac = f.ctl->t_sac; p.seq0 = f.ctl->step_seq;
+        p.nts = f.ctl->num_timesteps; p.tsi = f.ctl->ts_increment;
+    }
+    strided_sums<3>(xs, ns, p.ps);
+}
+
+template <bool PRE = false>
+__device__ void finalize_update(const FinalArgs& f, int nred, const FinPre* pre = nullptr) {
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x & 63;
     // every operand of the common case (B <= 256, nred <= 256) is requested before the first
-    // use: one memory round trip instead of one per reduction
+    // use: one memory round trip instead of one per reduction (PRE: all but the alpha partials
+    // were loaded before the ticket, by fin_prefetch)
     float ps[4];
-    {
-        const float* const xs[4] = {f.red, f.lq, f.lq + f.B, f.lp};
-        const int ns[4] = {nred, f.B, f.B, f.B};
-        strided_sums4(xs, ns, ps);
-    }
     float a_old = 0.f, a_m = 0.f, a_v = 0.f;
     int64_t t_sac = 0, seq0 = 0, nts = 0, tsi = 0;
-    if (lane == 0) {
-        a_old = *f.alpha; a_m = *f.alpha_m; a_v = *f.alpha_v;
-        t_sac = f.ctl->t_sac; seq0 = f.ctl->step_seq;
-        nts = f.ctl->num_timesteps; tsi = f.ctl->ts_increment;
+    if constexpr (PRE) {
+        const float* const xs[1] = {f.red};
+        const int ns[1] = {nred};
+        float p0[1];
+        strided_sums<1>(xs, ns, p0);
+        ps[0] = p0[0]; ps[1] = pre->ps[0]; ps[2] = pre->ps[1]; ps[3] = pre->ps[2];
+        a_old = pre->a_old; a_m = pre->a_m; a_v = pre->a_v;
+        t_sac = pre->t_sac; seq0 = pre->seq0; nts = pre->nts; tsi = pre->tsi;
+    } else {
+        const float* const xs[4] = {f.red, f.lq, f.lq + f.B, f.lp};
+        const int ns[4] = {nred, f.B, f.B, f.B};
+        strided_sums<4>(xs, ns, ps);
+        if (lane == 0) {
+            a_old = *f.alpha; a_m = *f.alpha_m; a_v = *f.alpha_v;
+            t_sac = f.ctl->t_sac; seq0 = f.ctl->step_seq;
+            nts = f.ctl->num_timesteps; tsi = f.ctl->ts_increment;
+        }
     }
     const float ent_sum = wave_sum(ps[0]);   // sum_i (-nlp_i + H)
     const float m_ent = ent_sum / (float)f.B;   // reduce_mean
@@ -918,7 +972,72 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         }
     }
     };
-    if constexpr (VEC == 1) {
+    // bf16 forward with operand shadows: B from the weight's (wbf) and / or A from the layer-0
+    // activations' (abf), one bf16x8 per lane, sub-tile row / column and slab pair -- the values and
+    // order the converting path packs, so the sums are bit-identical
+    auto shadow_loop = [&](auto vt, auto at, auto bt) {
+    constexpr bool V = decltype(vt)::value, SA = decltype(at)::value, SB = decltype(bt)::value;
+    const __amdgpu_buffer_rsrc_t rwb = make_rsrc(reinterpret_cast<const float*>(g.wbf), 0x7fffffffu);
+    const __amdgpu_buffer_rsrc_t rab = make_rsrc(reinterpret_cast<const float*>(g.abf), 0x7fffffffu);
+    const int pb = wave * ((per + 1) >> 1);     // this wave's first slab pair in a shadow row
+    for (int it = it0; it < it1; it += 2) {
+        float a[2][2][4], b[2][2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k0 = (it + u) * 16 + grp * 4;
+            const int k0e = (it + u < it1) ? k0 : (1 << 30);
+            if constexpr (!SA) {
+                load_a<true, V, false>(ra, g, ma, maok, k0e, a[u][0], rw);
+                load_a<true, V, false>(ra, g, mb, mbok, k0e, a[u][1], rw);
+            }
+            if constexpr (!SB) {
+                load_b<false, false, false>(rb, g, na, naok, k0e, b[u][0]);
+                load_b<false, false, false>(rb, g, nb, nbok, k0e, b[u][1]);
+            }
+        }
+        const int po = (pb + ((it - it0) >> 1)) * 32 + grp * 8;
+        bf16x8_t aw[2], bw[2];
+        if constexpr (SA) {
+            aw[0] = wbf_load(rab, maok, ma * g.K + po);
+            aw[1] = wbf_load(rab, mbok, mb * g.K + po);
+        } else {
+            aw[0] = pack_bf16(a[0][0], a[1][0]);
+            aw[1] = pack_bf16(a[0][1], a[1][1]);
+        }
+        if constexpr (SB) {
+            bw[0] = wbf_load(rwb, naok, na * g.wbf_ld + po);
+            bw[1] = wbf_load(rwb, nbok, nb * g.wbf_ld + po);
+        } else {
+            bw[0] = pack_bf16(b[0][0], b[1][0]);
+            bw[1] = pack_bf16(b[0][1], b[1][1]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (((it - it0) >> 1) & 1)
+                acc1[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s >> 1], bw[s & 1], acc1[s], 0, 0, 0);
+            else
+                acc0[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s >> 1], bw[s & 1], acc0[s], 0, 0, 0);
+        }
+    }
+    };
+    bool shadow = false;
+    if constexpr (MODE == GM_FWD && BF) shadow = g.wbf != nullptr || g.abf != nullptr;
+    if (shadow) {
+        if constexpr (MODE == GM_FWD && BF) {
+            using T_ = std::true_type;
+            using F_ = std::false_type;
+            if (g.abf != nullptr) {
+                if (g.wbf != nullptr) shadow_loop(F_{}, T_{}, T_{});
+                else shadow_loop(F_{}, T_{}, F_{});
+            } else if constexpr (VEC == 1) {
+                if (g.vec) shadow_loop(T_{}, F_{}, T_{});
+                else shadow_loop(F_{}, F_{}, T_{});
+            } else {
+                shadow_loop(F_{}, F_{}, T_{});
+            }
+        }
+    } else if constexpr (VEC == 1) {
         if (g.vec) main_loop(std::true_type{});
         else main_loop(std::false_type{});
     } else {
@@ -1004,7 +1123,12 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             }
         }
         if constexpr (MODE == GM_FWD) {
-            if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], act_f(v + e0[s], g.act));
+            const float o = act_f(v + e0[s], g.act);
+            if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], o);
+            if constexpr (BF) {     // the next layer's bf16 A operand (its K = this N)
+                if (g.obf != nullptr && out_ok)
+                    g.obf[(size_t)mm * g.N + wbf_pos(nn, wbf_per_of(g.N))] = __builtin_bit_cast(uint16_t, (__bf16)o);
+            }
         } else if constexpr (MODE == GM_DX) {
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0[s], g.act));
         } else {
@@ -1022,7 +1146,12 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             st_out(&g.P[pidx], pn);
             st_out(&g.P[pidx + ga.p_stride], mm1);
             st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-            if (g.T != nullptr && polyak) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
+            wbf_store(g.wbf, g, mm, nn, pn);
+            if (g.T != nullptr && polyak) {
+                const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
+                st_out(&g.T[pidx], tv);
+                wbf_store(g.obf, g, mm, nn, tv);
+            }
         }
     }
 }
@@ -1543,11 +1672,16 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         st_out(&g.P[pidx], pn);
         st_out(&g.P[pidx + ga.p_stride], mm1);
         st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+        wbf_store(g.wbf, g, mm, nn, pn);
         if (g.T != nullptr) {
             const int64_t nts = (int64_t)__builtin_amdgcn_readfirstlane((int)(es.nts >> 32)) << 32 |
                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
-            if (nts % tui == 0) st_out(&g.T[pidx], e3 * ga.adam.tau_keep + pn * ga.adam.tau_take);
+            if (nts % tui == 0) {
+                const float tv = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
+                st_out(&g.T[pidx], tv);
+                wbf_store(g.obf, g, mm, nn, tv);
+            }
         }
     }
 }
@@ -1932,7 +2066,12 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
         st_out(&g.P[pidx], pn);
         st_out(&g.P[pidx + ga.p_stride], mm1);
         st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-        if (g.T != nullptr && polyak) st_out(&g.T[pidx], e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take);
+        wbf_store(g.wbf, g, mm, nn, pn);
+        if (g.T != nullptr && polyak) {
+            const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
+            st_out(&g.T[pidx], tv);
+            wbf_store(g.obf, g, mm, nn, tv);
+        }
     }
     GEMM_PH(4);
     if (ga.ktime != nullptr) {
@@ -2833,6 +2972,14 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         __syncthreads();
     }
     const int wave = wave_id() & 3, lane = threadIdx.x & 63, g4 = wave_id() >> 2;
+    FinPre fpre;
+    if constexpr (TICKET && SACX_FIN_PRE) {
+        // wave 0 of a workgroup holding alpha blocks (the one that may finalise) requests the
+        // finalisation's other operands now, under the rows' own loads
+        const int last_blk = block + (int)(blockDim.x >> 8) - 1;
+        if (threadIdx.x < 64 && h.alpha_mode && last_blk * 4 >= h.alpha_row0 && block * 4 < h.total_rows)
+            fin_prefetch(ffin, fpre);
+    }
     block += g4;
     const int row = block * 4 + wave;
     float row_ent = 0.f;
@@ -2972,7 +3119,7 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
             // wave 0 finalises; the acquire of the other blocks' partials is its own (the counter
             // reached nred: every partial was released before its block's increment)
             if (threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            finalize_update(ffin, ffin.nred);
+            finalize_update<SACX_FIN_PRE != 0>(ffin, ffin.nred, &fpre);
             if (threadIdx.x == 0) __hip_atomic_store(&ffin.ctl->red_counter[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
@@ -3990,6 +4137,49 @@ void launch_net_io(const NetIOArgs& a, hipStream_t s) {
     } else {
         hipLaunchKernelGGL(k_net_io_rows, dim3(1), dim3(256), 0, s, a);
     }
+}
+
+// k_wbf_refresh: thread (n, 8 shadow positions) of matrix blockIdx.y; the 8 positions are one lane
+// group's operand values of a slab pair (k = s0 + 4 grp + j, then s1 + 4 grp + j), read down
+// column n of W (coalesced across the threads' n) and stored as one 16-B row piece; positions
+// past K or of an unpaired slab get zeros
+__global__ __launch_bounds__(256) void k_wbf_refresh(WbfArgs a) {
+    const int mi = blockIdx.y;
+    if (mi >= a.nmat) return;
+    const int64_t so = a.nseeds > 1 ? (int64_t)blockIdx.z * a.sstride : 0;
+    const float* W = sr(a.W[mi], so);
+    uint16_t* S = sr(a.S[mi], so);
+    const int K = a.K[mi], N = a.N[mi], per = wbf_per_of(K), ld = wbf_ld_of(K), ppw = (per + 1) >> 1;
+    const int nIt = (K + 15) >> 4;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int n = (int)(idx % N);
+    const int64_t q = idx / N;                 // 8-position group of row n
+    if (q >= ld / 8) return;
+    const int pair = (int)(q >> 2), grp = (int)(q & 3);
+    const int w = pair / ppw, i0 = (pair - w * ppw) * 2;
+    uint16_t v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int i = i0 + h, sl = w * per + i;
+        const bool sok = i < per && sl < nIt;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int k = sl * 16 + grp * 4 + j;
+            const float x = (sok && k < K) ? W[(size_t)k * N + n] : 0.f;
+            v[h * 4 + j] = __builtin_bit_cast(uint16_t, (__bf16)x);
+        }
+    }
+    uint4 o;
+    o.x = v[0] | ((uint32_t)v[1] << 16); o.y = v[2] | ((uint32_t)v[3] << 16);
+    o.z = v[4] | ((uint32_t)v[5] << 16); o.w = v[6] | ((uint32_t)v[7] << 16);
+    *reinterpret_cast<uint4*>(S + (size_t)n * ld + q * 8) = o;
+}
+
+void launch_wbf_refresh(const WbfArgs& a, hipStream_t s) {
+    int64_t most = 0;
+    for (int i = 0; i < a.nmat; ++i) most = std::max<int64_t>(most, (int64_t)a.N[i] * (wbf_ld_of(a.K[i]) / 8));
+    const dim3 grid((unsigned)((most + 255) / 256), (unsigned)a.nmat, (unsigned)seeds_z(a.nseeds));
+    hipLaunchKernelGGL(k_wbf_refresh, grid, dim3(256), 0, s, a);
 }
 
 __global__ void k_set_pseq(Ctl* ctl, int slot, int64_t sstride) {

@@ -144,7 +144,17 @@ struct sacx_handle {
     bool bound = false;
     std::vector<Launch> plan[NSLOT];
     int64_t slot_bytes = 0;   // distance between consecutive update-input slots
-    int nbatch = 4;           // sampler batch (updates per k_rng launch); slots rotate over 2*nbatch
+    int nbatch = 4;           // sampler batch (updates per k_rng launch)
+    int nslot = 8;            // update-input slots the ring rotates over (a multiple of nbatch, >= 2 nbatch)
+    // bf16 weight shadows (SACX_WBF, default on): the matrices (segment "wbf.<name>") and whether
+    // add_gemm wires them into the problems it builds (the update plans only)
+    struct WbfMat { std::string name; int K, N; };
+    std::vector<WbfMat> wbf_mats;
+    int wbf_enabled = 1;      // SACX_WBF: 0 off, 1 weights + layer-0 activations, 2 weights only
+    bool wbf_attach = false;
+    bool wbf_live = false;    // the update plans read / maintain the shadows (refreshed per step call)
+    std::vector<std::string> abf_segs;          // activation segments with a bf16 shadow ("abf.<name>")
+    std::vector<std::pair<const float*, const float*>> abf_written;   // plan build: ranges a wired producer stores
     bool rng_split = false;   // k_rng + k_polar (rng.pairs): the polar transform spread over the GPU
     int pcap = 0;             // polar pairs per update (rng.pairs rows per update)
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
@@ -263,7 +273,7 @@ int spec_cancel(sacx_handle* h, bool keep_state = false) {
 
 // the handles the speculative draw applies to: one learner, its own RNG stream
 bool spec_mode(const sacx_handle* h) {
-    return h->spec_enabled && h->dp_ranks == 0 && !h->dp_local && 2 * h->nbatch >= 3;
+    return h->spec_enabled && h->dp_ranks == 0 && !h->dp_local && h->nslot >= 3;
 }
 
 #define HIPCHK(h, x)                                                                    \
@@ -316,6 +326,21 @@ void build_layout(sacx_handle* h) {
     h->add("norm.d_den", 1, S, F, SACX_ROLE_STATE);
     h->add("norm.r", 1, 2, F, SACX_ROLE_STATE);  // r_mean, r_den
     h->add("norm.ret_den", 1, 1, F, SACX_ROLE_STATE);
+    // bf16 shadows of the SAC nets' hidden-layer weights (config C5, 32x32 forward tiles): the
+    // forward launches read B from them (wbf_pos layout), the Adam epilogues keep them current
+    h->wbf_mats.clear();
+    if (h->cfg.gemm_bf16 && h->wbf_enabled) {
+        const char* nets[] = {"actor", "q0", "q1", "t0", "t1"};
+        for (const char* n : nets) {
+            const int in = std::string(n) == "actor" ? S : S + A;
+            for (int l = 0; l < 2; ++l) {
+                const int K = l == 0 ? in : H0, N = l == 0 ? H0 : H1;
+                const std::string w = std::string(n) + ".l" + std::to_string(l);
+                h->add("wbf." + w, N, wbf_ld_of(K) / 2, SACX_U32, SACX_ROLE_WORK);
+                h->wbf_mats.push_back({w, K, N});
+            }
+        }
+    }
     // the world models' own normaliser set (SAC_expert.py:53-54, :139-144): a copy of norm.*
     // unless --only_model_normalizer gives the models a RunningNormalizers of their own
     if (h->cfg.use_expert) {
@@ -328,7 +353,7 @@ void build_layout(sacx_handle* h) {
         h->add("mnorm.r", 1, 2, F, SACX_ROLE_STATE);
     }
     // ---------------- control + RNG
-    h->add("ctl", 1, 32, SACX_I64, SACX_ROLE_STATE);
+    h->add("ctl", 1, CTL_WORDS, SACX_I64, SACX_ROLE_STATE);
     const uint64_t roff = h->add("rng", 1, sizeof(RngState) / 4, SACX_U32, SACX_ROLE_STATE);
     h->alias("rng.key", roff, 1, 624, SACX_U32, SACX_ROLE_STATE);
     h->alias("rng.pos", roff + offsetof(RngState, pos), 1, 2, SACX_I32, SACX_ROLE_STATE);
@@ -343,10 +368,17 @@ void build_layout(sacx_handle* h) {
         h->add("rng.pairs", (int64_t)NBATCH_MAX * h->pcap, 4, SACX_U32, SACX_ROLE_WORK);
         h->add("rng.pairs_oi", 1, NBATCH_MAX, SACX_I32, SACX_ROLE_WORK);
     }
-    // per-slot update inputs: the sampler + gather of update j+2 run while update j+1
-    // executes, so everything they write is double buffered
+    // per-slot update inputs: the sampler + gather run ahead of the updates on a side stream,
+    // so everything they write rotates over a ring of slots.  A cheap sampler (HC: 1,536 normals
+    // per update) gets 32 slots: a graph of up to 32 updates draws every input at its start,
+    // with no sampler launch waiting on the update chain (a 20-update graph otherwise waits
+    // ~0.1 ms at update 8 for a sampler batch the runtime releases only when the chain reaches
+    // it); an expensive one (Humanoid: 10 MB of slot rows per update) keeps 8, the footprint
+    // the caches hold
+    h->nslot = h->n_norm <= 16384 ? NSLOT : 8;
+    if (const char* e = std::getenv("SACX_NSLOT")) h->nslot = std::max(2, std::min(NSLOT, std::atoi(e)));
     const int ne1 = std::max(1, h->ne);
-    for (int s = 0; s < NSLOT; ++s) {
+    for (int s = 0; s < h->nslot; ++s) {
         const std::string sl = "slot" + std::to_string(s);
         h->add(sl + ".idx", 1, B, SACX_I32, SACX_ROLE_WORK);
         h->add(sl + ".noise", 1, h->n_norm, F, SACX_ROLE_WORK);
@@ -361,7 +393,7 @@ void build_layout(sacx_handle* h) {
         h->add(sl + ".spe_raw", ne1, S, F, 0);
     }
     h->slot_bytes = (int64_t)(h->off_of("slot1.idx") - h->off_of("slot0.idx"));
-    for (int k = 1; k < NSLOT; ++k)      // the batched sampler / gather address slot k as slot 0 + k * slot_bytes
+    for (int k = 1; k < h->nslot; ++k)   // the batched sampler / gather address slot k as slot 0 + k * slot_bytes
         for (const char* nm : {".idx", ".noise", ".Xa", ".Xq", ".Xt", ".Xp", ".Xm", ".r", ".d", ".se_raw", ".spe_raw"})
             if (h->off_of("slot" + std::to_string(k) + nm) != h->off_of(std::string("slot0") + nm) + k * (uint64_t)h->slot_bytes) {
                 fprintf(stderr, "sacx: slot layout is not uniform\n");
@@ -417,6 +449,16 @@ void build_layout(sacx_handle* h) {
     h->add("ws.E", Rb, A, F, 0);
     h->alias("ws.Hl1", oHa1 + (uint64_t)Ra4 * H0 * 4, B, H0, F, 0);
     h->alias("ws.Hl2", oHa2 + (uint64_t)Ra4 * H1 * 4, B, H1, F, 0);
+    // bf16 shadows of the layer-0 outputs the 32x32 bf16 forward tiles of layer 1 read as A
+    // (H0 a multiple of 128: every shadow position holds a k < H0; not under the layer norm,
+    // which rewrites the actor's layer-0 output after the GEMM)
+    h->abf_segs.clear();
+    if (h->cfg.gemm_bf16 && h->wbf_enabled == 1 && H0 % 128 == 0 && !h->ln)
+        for (const char* n : {"ws.Ha1", "ws.Hq1", "ws.Hp1"}) {
+            const auto& sg = h->seg(n);
+            h->add(std::string("abf.") + n, sg.rows, H0 / 2, SACX_U32, SACX_ROLE_WORK);
+            h->abf_segs.push_back(n);
+        }
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
     h->add("act.H1", ACT_CAP, H0, F, 0);
@@ -502,6 +544,51 @@ double gemm_bytes(const GemmProb& p) {
     return b;
 }
 
+// The bf16 weight shadows of a problem (SACX_WBF): a forward problem on 32x32 tiles reads the
+// shadow of its B; a dW + Adam problem stores the shadows of the P and T it updates
+void wbf_wire(sacx_handle* h, GemmProb& p, int mode, bool t32) {
+    auto find = [&](const float* w) -> const sacx_handle::WbfMat* {
+        for (const auto& m : h->wbf_mats)
+            if (w != nullptr && w == h->f(m.name)) return &m;
+        return nullptr;
+    };
+    if (mode == GM_FWD && t32) {
+        const auto* m = find(p.B);
+        if (m && m->K == p.K && m->N == p.N && p.ldb == p.N) {
+            p.wbf = h->ptr<uint16_t>("wbf." + m->name);
+            p.wbf_ld = wbf_ld_of(m->K);
+            p.wbf_per = wbf_per_of(m->K);
+        }
+        // activations: a plain forward problem whose output lies in a shadowed segment stores its
+        // shadow; a layer-1 problem reads A from the shadow when a wired producer of this plan
+        // stores every row it reads (ranges recorded in build order: producers come first)
+        for (const auto& n : h->abf_segs) {
+            const auto& sg = h->seg(n);
+            const float* base = h->f(n);
+            const float* end = base + (size_t)sg.rows * sg.cols;
+            if (p.C && p.C >= base && p.C < end && p.ldc == sg.cols && p.N == sg.cols && p.mse == 0 &&
+                p.C + (size_t)p.M * p.ldc <= end) {
+                p.obf = h->ptr<uint16_t>("abf." + n) + (p.C - base);
+                h->abf_written.push_back({p.C, p.C + (size_t)p.M * p.ldc});
+            }
+            if (p.A >= base && p.A < end && p.lda == sg.cols && p.K == sg.cols && p.headp == 0) {
+                const float* a1 = p.A + (size_t)p.M * p.lda;
+                bool covered = false;
+                for (const auto& w : h->abf_written) covered = covered || (p.A >= w.first && a1 <= w.second);
+                if (covered) p.abf = h->ptr<uint16_t>("abf." + n) + (p.A - base);
+            }
+        }
+    } else if (mode == GM_DW && p.epi == EPI_ADAM) {
+        const auto* m = find(p.P);
+        if (!m || m->K != p.M - 1 || m->N != p.N || p.ldp != p.N) return;
+        p.wbf = h->ptr<uint16_t>("wbf." + m->name);
+        p.wbf_ld = wbf_ld_of(m->K);
+        p.wbf_per = wbf_per_of(m->K);
+        p.wbf_k = m->K;
+        if (const auto* t = find(p.T)) p.obf = h->ptr<uint16_t>("wbf." + t->name);
+    }
+}
+
 void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name, std::vector<GemmProb> ps,
               bool record_probs, bool allow_dwl = true) {
     Launch L{};
@@ -575,6 +662,8 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
         p.vec = (mode != GM_DW && v_a && v_b && p.K >= 4) ? 1 : 0;
         vec = vec || p.vec;
     }
+    if (h->wbf_attach && h->cfg.gemm_bf16)
+        for (auto& p : ps) wbf_wire(h, p, mode, t32);
     if (dwl) {
         // 16-B row pieces need 16-B aligned rows in every seed's arena block
         const bool sa = h->seeds <= 1 || h->seed_bytes % 16 == 0;
@@ -1544,6 +1633,24 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
     }
 }
 
+// Rebuilds every bf16 weight shadow from the fp32 weights (all seeds): at each entry point that
+// runs the update plans, so that parameter writes from the host reach the bf16 forward tiles
+void wbf_refresh(sacx_handle* h, hipStream_t s) {
+    if (!h->wbf_live) return;
+    WbfArgs a{};
+    for (const auto& m : h->wbf_mats) {
+        if (a.nmat == WBF_MAXM) break;
+        a.W[a.nmat] = reinterpret_cast<const float*>(h->arena0 + h->off_of(m.name));
+        a.S[a.nmat] = reinterpret_cast<uint16_t*>(h->arena0 + h->off_of("wbf." + m.name));
+        a.K[a.nmat] = m.K;
+        a.N[a.nmat] = m.N;
+        ++a.nmat;
+    }
+    a.sstride = (int64_t)h->seed_bytes;
+    a.nseeds = h->seeds;
+    launch_wbf_refresh(a, s);
+}
+
 // the sampler + gather launches of a slot (the update's inputs)
 bool is_prologue(const Launch& L) { return L.kind == Launch::RNG || L.kind == Launch::GATHER; }
 
@@ -1714,14 +1821,15 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         HIPCHK(h, hipStreamWaitEvent(rs, evFork, 0));
         // Sampler batches [s, e): one k_rng launch draws updates s..e-1 in stream order and one
         // gather fills their slots s % nslot .. s % nslot + (e - s) - 1 -- consecutive slots (the
-        // kernels address slot + u), so a batch never crosses a multiple of nbatch (nslot =
-        // 2 nbatch is one).  Sizes ramp 1, 2, 4, ... up to nbatch so the first update of the
-        // graph waits for one update's draws only.  Slot u%nslot is last read through update u's
-        // folded alpha rows in update u+1's actor.head, so batch [s, e) is drawn after the
-        // actor.head of update e-nslot (at graph start when e <= nslot) and must be done before
-        // update s.
+        // kernels address slot + u), so a batch never crosses a multiple of nbatch (nslot is
+        // one).  Sizes ramp 1, 2, 4, ... up to nbatch so the first update of the graph waits
+        // for one update's draws only.  Slot u%nslot is last read through update u's folded
+        // alpha rows in update u+1's actor.head, so batch [s, e) is drawn after the actor.head
+        // of update e-nslot, and must be done before update s.  When e <= nslot its slots are
+        // fresh at graph start: their last reader is update e-1-nslot < 0 of an earlier graph
+        // (update 0 folds no alpha rows), complete before this graph starts.
         std::vector<std::pair<int, int>> batches;
-        const int nbatch = h->nbatch, nslot = 2 * h->nbatch;
+        const int nbatch = h->nbatch, nslot = h->nslot;
         for (int s0 = 0, ramp = 1; s0 < G; ramp = std::min(nbatch, 2 * ramp)) {
             const int sz = std::min({ramp, nbatch - s0 % nbatch, G - s0});
             batches.push_back({s0, s0 + sz});
@@ -1752,10 +1860,10 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         std::vector<int> batch_of(G, -1), emit_after(batches.size(), -1);
         for (int b = 0; b < (int)batches.size(); ++b) {
             batch_of[batches[b].first] = b;
-            emit_after[b] = batches[b].second - nslot;          // < 0: slots fresh at graph start
+            emit_after[b] = batches[b].second - nslot;          // <= 0: slots fresh at graph start
         }
         for (int b = 0; b < (int)batches.size(); ++b)
-            if (emit_after[b] < 0) HIPCHK(h, prologue(b));
+            if (emit_after[b] <= 0) HIPCHK(h, prologue(b));
         std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
             if (batch_of[j] >= 0) HIPCHK(h, hipStreamWaitEvent(cs, evR[batch_of[j]], 0));
@@ -1822,7 +1930,7 @@ int get_spec_graph(sacx_handle* h, int slot, int prev, hipGraphExec_t* out) {
         *out = it->second;
         return 0;
     }
-    if (2 * h->nbatch <= slot || h->plan[slot].empty()) return fail(h, "internal: no spare slot for the speculative draw");
+    if (h->nslot <= slot || h->plan[slot].empty()) return fail(h, "internal: no spare slot for the speculative draw");
     std::vector<Launch> body;
     if (!merged_body(h, slot, prev, body)) {   // plans that do not fold: the branch, then the body
         std::vector<Launch> own;
@@ -1975,6 +2083,7 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
         delete h;
         return bad("action output > 64 unsupported");
     }
+    if (const char* e = std::getenv("SACX_WBF")) h->wbf_enabled = std::atoi(e);
     build_layout(h);
     h->seeds = cfg->seeds > 1 ? cfg->seeds : 1;
     h->seed_bytes = h->seeds > 1 ? (h->arena_bytes + 65535) & ~uint64_t(65535) : h->arena_bytes;
@@ -2075,6 +2184,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // ramp and the sampler's lead over the chain favour smaller batches (5.80k vs 5.62k at 8)
     h->nbatch = h->n_norm <= 16384 ? 8 : 4;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
+    while (h->nslot % h->nbatch || h->nslot < 2 * h->nbatch) --h->nbatch;   // the ring holds whole batches
     if (h->dp_ranks > 0) {
         if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
         const int64_t d = (int64_t)(h->off_of("t0.l0") - h->off_of("q0.l0"));
@@ -2083,8 +2193,17 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
                 if ((int64_t)(h->off_of("t" + std::to_string(k) + l) - h->off_of("q" + std::to_string(k) + l)) != d)
                     return fail(h, "internal: target layout is not a fixed shift of the critics");
     }
-    for (int sl = 0; sl < NSLOT; ++sl) build_plan(h, sl, sl == 0);
-    for (int sl = 1; sl < NSLOT; ++sl) {
+    // the weight shadows feed the update plans' 32x32 bf16 forward tiles; the Adam epilogues
+    // keep them current (not the data-parallel modes, whose Adam runs in k_adam_apply)
+    h->wbf_attach = !h->wbf_mats.empty() && h->tile32 > 0 && h->dp_ranks == 0;
+    h->wbf_live = h->wbf_attach;
+    for (int sl = 0; sl < h->nslot; ++sl) {
+        h->abf_written.clear();
+        build_plan(h, sl, sl == 0);
+    }
+    h->abf_written.clear();
+    h->wbf_attach = false;
+    for (int sl = 1; sl < h->nslot; ++sl) {
         if (h->plan[0].size() != h->plan[sl].size()) return fail(h, "internal: slot plans differ");
         for (size_t i = 0; i < h->plan[0].size(); ++i)
             if (h->plan[0][i].kind == Launch::GEMM &&
@@ -2593,6 +2712,7 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // a deferred alpha.final (folded into this update) adds ts_increment to num_timesteps before
     // this update reads it
     const int prev = use_spec ? h->alpha_pending : -1;
+    wbf_refresh(h, h->stream);
     launch_set_ctl(h->ctl0(), num_timesteps - (prev >= 0 ? ts_increment : 0), ts_increment,
                    (int64_t)h->seed_bytes, h->seeds, h->stream);
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
@@ -2747,6 +2867,7 @@ static int launch_info(const std::vector<Launch>& plan, sacx_launch_info* out, i
 int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t cap) {
     if (h && h->bound && settle(h)) return -1;
     if (!h || !h->bound) return fail(h, "not bound");
+    wbf_refresh(h, h->stream);
     const auto& plan = h->plan[0];
     const int n = (int)plan.size();
     std::vector<hipEvent_t> ev(n + 1);
@@ -3181,6 +3302,7 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
     if (!h || !h->bound) return fail(h, "not bound");
     if (!kernel || std::strcmp(kernel, "k_gemm") != 0) return fail(h, "only k_gemm carries timestamps");
     if (settle(h)) return -1;
+    wbf_refresh(h, h->stream);
     if (!avg_us || n_replays <= 0) return fail(h, "bad arguments");
     const int G = h->graph_steps;
     KTimeMap kt;
@@ -3252,6 +3374,7 @@ int sacx_time_graph(sacx_handle* h, int64_t n_replays, const char* skip_kernel, 
     if (!h || !h->bound) return fail(h, "not bound");
     if (!ms_out || n_replays <= 0) return fail(h, "bad arguments");
     if (settle(h)) return -1;
+    wbf_refresh(h, h->stream);
     int skip = -1;
     if (skip_kernel && skip_kernel[0]) {
         for (int k = Launch::RNG; k <= Launch::MFINAL; ++k)

@@ -8,12 +8,13 @@ namespace sacx {
 
 enum Act { ACT_RELU = 0, ACT_TANH = 1, ACT_ELU = 2, ACT_NONE = 3 };
 
-// Device control block (lives in the arena, segment "ctl", int64 x 32).
+// Device control block (lives in the arena, segment "ctl", int64 x CTL_WORDS).
 // update-input slots: the sampler + gather fill them a batch of NBATCH updates at a time,
-// one batch ahead of the updates that consume them (and an update's alpha rows are read
-// one update later by the folded launches), so two batches of slots rotate
+// ahead of the updates that consume them (and an update's alpha rows are read one update
+// later by the folded launches); the ring holds at least two batches (sacx_handle::nslot)
 #define NBATCH_MAX 8
-#define NSLOT (2 * NBATCH_MAX)
+#define NSLOT 32
+#define CTL_WORDS 48
 
 struct Ctl {
     int64_t t_sac;          // completed updates (Adam iterations of q / pi / alpha optimisers)
@@ -31,7 +32,7 @@ struct Ctl {
     int64_t rng_seq;        // update number the next sampler launch draws for
     int64_t pseq[NSLOT];    // update number whose randoms slot k holds (expert perm ring index)
 };
-static_assert(sizeof(Ctl) <= 32 * 8, "ctl segment is 32 int64");
+static_assert(sizeof(Ctl) <= CTL_WORDS * 8, "ctl segment is CTL_WORDS int64");
 
 struct RngState {          // NumPy legacy RandomState (MT19937) state
     uint32_t key[624];
@@ -124,6 +125,41 @@ struct GemmProb {
     const float* gd;
     float* gst;
     int32_t gd_ld, g_o, gst_ld;
+    // config C5 (bf16 GEMMs) with 32x32 forward tiles: bf16 shadows of operands in the MFMA pair
+    // layout of wbf_pos, read as one bf16x8 per lane and k-slab pair (null: the fp32 operand,
+    // converted on load).  Weights: each row n of W^T; GM_FWD reads B from wbf, GM_DW + Adam stores
+    // the updated rows k < wbf_k of P into wbf and the Polyak target into obf.  Activations (the
+    // hidden layer-0 outputs, K = H0 a multiple of 128: rows of K positions): GM_FWD reads A from
+    // abf (row stride K) and stores its own output into obf (row stride N) beside C.
+    uint16_t* wbf;
+    uint16_t* obf;
+    const uint16_t* abf;
+    int32_t wbf_ld, wbf_per, wbf_k;
+};
+
+// Shadow row layout: the consumer's K is split over 4 waves of `per` 16-wide slabs (gemm_core's
+// split: per = ceil(ceil(K / 16) / 4)); a wave's slabs pair up from its first, (it0, it0 + 1),
+// (it0 + 2, it0 + 3), ..., and each pair takes 32 consecutive bf16: lane group grp's 8 operand
+// values, k = s0 + 4 grp + j then s1 + 4 grp + j (j < 4) -- the order in which the bf16 MFMA
+// path packs a converted pair, so a 16-B load yields the same operand bit for bit.  Positions
+// of k >= K and of a wave's unpaired last slab stay zero.
+__host__ __device__ inline int wbf_per_of(int K) { return (((K + 15) >> 4) + 3) >> 2; }
+__host__ __device__ inline int wbf_ld_of(int K) { return 4 * ((wbf_per_of(K) + 1) >> 1) * 32; }
+__host__ __device__ inline int wbf_pos(int k, int per) {
+    const int s = k >> 4, w = s / per, i = s - w * per;
+    return (w * ((per + 1) >> 1) + (i >> 1)) * 32 + ((k >> 2) & 3) * 8 + (i & 1) * 4 + (k & 3);
+}
+
+// k_wbf_refresh: every shadow rebuilt from its fp32 weights (at each sacx_sac_step entry, so host
+// writes of the parameters reach it; the Adam epilogues keep it current inside a step)
+#define WBF_MAXM 12
+struct WbfArgs {
+    const float* W[WBF_MAXM];    // [K x N] row-major (the first K rows of W_ext)
+    uint16_t* S[WBF_MAXM];       // [N x ld]
+    int32_t K[WBF_MAXM], N[WBF_MAXM];
+    int32_t nmat;
+    int64_t sstride;             // packed seeds: grid z = seed
+    int32_t nseeds;
 };
 
 // rowk 4 (GM_DX, actor.bwd1): the actor head backward (k_actor_bwd's policy-row work) runs as
@@ -579,6 +615,7 @@ void launch_mloss(const MLossArgs& a, hipStream_t s);
 void launch_mfinal(const MFinalArgs& a, hipStream_t s);
 void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, int64_t sstride, int nseeds, hipStream_t s);
 void launch_set_pseq(Ctl* ctl, int slot, int64_t sstride, int nseeds, hipStream_t s);
+void launch_wbf_refresh(const WbfArgs& a, hipStream_t s);
 void launch_spin(double us, hipStream_t s);
 void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, const float* den, float* X, int ldX,
                      hipStream_t s);

@@ -1,6 +1,6 @@
 """Parity of the PRODUCTION schedule (graph_steps = 128, the bench's and EngineConfig's
-default): the sampler runs ahead on a side stream and its slot ring (2 x SACX_NBATCH slots)
-wraps many times inside one captured graph, so a slot-reuse race would show here and not in
+default): the sampler runs ahead on a side stream and its slot ring (SACX_NSLOT slots, whole
+batches of SACX_NBATCH) wraps many times inside one captured graph, so a slot-reuse race would show here and not in
 the graph_steps = 8 tests.
 
 * 300 updates (two 128-update graphs + one 44-update remainder graph) vs the fp64 oracle:
@@ -14,7 +14,8 @@ the graph_steps = 8 tests.
   to 2x); device error <= DRIFT_FACTOR x the largest of them + 1e-5, for each loss series
   over all 300 updates and for the weights / targets after 100 and 300 updates; the update
   sequence numbers and the RNG stream exact.
-* graph replay == eager launches, bit for bit, at SACX_NBATCH 2 / 4 / 8 (± expert).
+* graph replay == eager launches, bit for bit, at SACX_NBATCH 2 / 4 / 8 over rings of 2 batches
+  (the tightest reuse distance) and of 32 slots (the default at these shapes), ± expert.
 * 8 packed seeds at graph_steps = 128 == 8 one-seed engines, bit for bit.
 Reference: SAC_exp._update (sac_eo/algs/SAC_expert.py:463-477), SAC._update (SAC.py:236-250).
 """
@@ -97,11 +98,13 @@ def test_production_schedule_trajectory_300(gpu_available, use_expert):
     eng.close()
 
 
-@pytest.mark.parametrize("nbatch,use_expert", [(2, False), (4, False), (8, False), (4, True), (8, True)])
-def test_production_graph_equals_eager(gpu_available, monkeypatch, nbatch, use_expert):
+@pytest.mark.parametrize("nbatch,nslot,use_expert", [(2, 4, False), (4, 8, False), (8, 16, False), (8, 32, False),
+                                                     (4, 8, True), (8, 32, True)])
+def test_production_graph_equals_eager(gpu_available, monkeypatch, nbatch, nslot, use_expert):
     """graph_steps = 128, 300 updates: 2 full graphs + a 44-update remainder graph; the slot
-    ring (2 * nbatch slots) wraps 16-64 times inside each graph."""
+    ring (nslot slots) wraps 4-32 times inside each graph."""
     monkeypatch.setenv("SACX_NBATCH", str(nbatch))
+    monkeypatch.setenv("SACX_NSLOT", str(nslot))
     n = 300
     outs = []
     for eager in (True, False):

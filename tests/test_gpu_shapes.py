@@ -106,3 +106,61 @@ def test_sampler_on_4e6_ring(gpu_available):
         assert torch.equal(xq[:, :S], rows[:, :S]) and torch.equal(xq[:, S:S + A], rows[:, S:S + A])
         assert torch.equal(eng.v["slot0.r"][0], rows[:, 2 * S + A])
     eng.close()
+
+
+def _wbf_expected(W):
+    """The bf16 shadow of W [K x N] in the kernels' pair layout (sacx_internal.h wbf_pos), as uint16."""
+    import torch
+    K, N = W.shape
+    per = (((K + 15) >> 4) + 3) >> 2
+    ld = 4 * ((per + 1) >> 1) * 32
+    bits = torch.from_numpy(np.ascontiguousarray(W, np.float32)).to(torch.bfloat16).view(torch.int16).numpy()
+    out = np.zeros((N, ld), np.uint16)
+    k = np.arange(K)
+    s = k >> 4
+    w = s // per
+    i = s - w * per
+    pos = (w * ((per + 1) >> 1) + (i >> 1)) * 32 + ((k >> 2) & 3) * 8 + (i & 1) * 4 + (k & 3)
+    out[:, pos] = bits.view(np.uint16).T
+    return out
+
+
+@pytest.mark.parametrize("eager", [False, True])
+def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
+    """C5's forward tiles reading B from the bf16 weight shadows and layer 1's A from the layer-0
+    outputs' shadows (SACX_WBF=1, default; 2: weights only) equal the converting loads
+    (SACX_WBF=0) bit for bit over 2 x 24 Humanoid updates at B = 1,024, with a host write of the
+    parameters in between (the weight shadows are rebuilt at the next step call); after each run
+    every weight shadow equals the bf16 image of its fp32 weights in the wbf_pos layout, and the
+    critics' layer-0 output shadow that of the last update's activations."""
+    B, n = 1024, 24
+    outs = []
+    for wbf in ("0", "2", "1"):
+        monkeypatch.setenv("SACX_WBF", wbf)
+        eng, *_ = make_pair(act="relu", B=B, N=6000, seed=41, done_p=0.01, gemm_bf16=True, graph_steps=8, **HUM)
+        eng.rng_set_state(np.random.RandomState(8).get_state())
+        eng.step(n, eager=eager)
+        eng.sync()
+        p = eng.v["params"]
+        p.mul_(0.999)                      # a host-side write between step calls
+        eng.step(n, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(2 * n).copy(), eng.v["params"].cpu().numpy().copy(),
+                     eng.v["adam_v"].cpu().numpy().copy()))
+        if wbf != "0":
+            names = [f"{net}.l{l}" for net in ("actor", "q0", "q1", "t0", "t1") for l in (0, 1)]
+            for nm in names:
+                assert "wbf." + nm in eng.v, nm
+                Wx = eng.v[nm].cpu().numpy()
+                exp = _wbf_expected(Wx[:-1])             # W_ext without the bias row
+                got = eng.v["wbf." + nm].cpu().numpy().view(np.uint16).reshape(exp.shape[0], -1)
+                assert np.array_equal(got, exp), nm
+        if wbf == "1":
+            hq = eng.v["ws.Hq1"].cpu().numpy()
+            exp = _wbf_expected(hq.T)
+            got = eng.v["abf.ws.Hq1"].cpu().numpy().view(np.uint16).reshape(exp.shape[0], -1)
+            assert np.array_equal(got, exp)
+        eng.close()
+    for o in outs[1:]:
+        for i, (a, b) in enumerate(zip(outs[0], o)):
+            assert np.array_equal(a, b), i
