@@ -164,3 +164,41 @@ def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
     for o in outs[1:]:
         for i, (a, b) in enumerate(zip(outs[0], o)):
             assert np.array_equal(a, b), i
+
+
+def test_bf16_shadows_packed_seeds(gpu_available, monkeypatch):
+    """The shadows of packed seeds (one arena block per seed, relocated by grid z): 4 HC-shaped
+    bf16 seeds (4 x 256 rows: 32x32 forward tiles) over a 16-update graph, a host write, and 16
+    more, SACX_WBF=1 equal to SACX_WBF=0 bit for bit for every seed."""
+    from helpers import load_learner, make_learner
+    from sac_eo.engine import Engine, EngineConfig
+    K, n, B, N = 4, 16, 256, 3000
+    learners = [make_learner(act="relu", B=B, N=N, seed=90 + 3 * k) for k in range(K)]
+    outs = []
+    for wbf in ("0", "1"):
+        monkeypatch.setenv("SACX_WBF", wbf)
+        eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=N, graph_steps=16,
+                                  seeds=K, gemm_bf16=True))
+        for k in range(K):
+            eng.select_seed(k)
+            _, st, buf, nrm, ex = learners[k]
+            load_learner(eng, st, buf, nrm, ex, 0.1)
+            eng.rng_set_state(np.random.RandomState(300 + k).get_state())
+        eng.select_seed(0)
+        eng.step(n)
+        eng.sync()
+        eng.select_seed(2)
+        eng.v["params"].mul_(0.999)
+        eng.select_seed(0)
+        eng.step(n)
+        eng.sync()
+        got = []
+        for k in range(K):
+            eng.select_seed(k)
+            got.append((eng.stats(2 * n).copy(), eng.v["params"].cpu().numpy().copy(),
+                        eng.v["adam_v"].cpu().numpy().copy()))
+        outs.append(got)
+        eng.close()
+    for k in range(K):
+        for i, (a, b) in enumerate(zip(outs[0][k], outs[1][k])):
+            assert np.array_equal(a, b), (k, i)
