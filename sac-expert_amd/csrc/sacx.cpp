@@ -1863,7 +1863,10 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             emit_after[b] = batches[b].second - nslot;          // <= 0: slots fresh at graph start
         }
         for (int b = 0; b < (int)batches.size(); ++b)
-            if (emit_after[b] <= 0) HIPCHK(h, prologue(b));
+            if (emit_after[b] <= 0) {
+                HIPCHK(h, prologue(b));
+                emit_after[b] = -1;                             // drawn once: not again after update 0
+            }
         std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
             if (batch_of[j] >= 0) HIPCHK(h, hipStreamWaitEvent(cs, evR[batch_of[j]], 0));
