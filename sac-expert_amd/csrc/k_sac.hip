@@ -208,10 +208,37 @@ __device__ __forceinline__ bf16x8_t wbf_load(__amdgpu_buffer_rsrc_t r, bool ok, 
     asm("" : "+v"(o));
     return __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(r, o, 0, 0));
 }
-// a weight's bf16 shadow element (round to nearest even, as the converting loads)
-__device__ __forceinline__ void wbf_store(uint16_t* S, const GemmProb& g, int k, int n, float v) {
-    if (S != nullptr && k < g.wbf_k)
-        S[(size_t)n * g.wbf_ld + wbf_pos(k, g.wbf_per)] = __builtin_bit_cast(uint16_t, (__bf16)v);
+// bf16 image of a float as raw bits (round to nearest even, as the converting loads)
+__device__ __forceinline__ uint32_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, (__bf16)v); }
+// A weight shadow's 4 consecutive k of column n: in the GEMM epilogues' thread map (row = t >> 4,
+// col = t & 15) they are the rows of lanes l, l + 16, l + 32, l + 48 of one wave, so lane l < 16
+// (whose k is a multiple of 4) gathers them and stores one 8-B piece (4 consecutive shadow
+// positions); at the end of K only the positions of k < wbf_k.  Every lane of the wave calls it.
+__device__ __forceinline__ void wbf_store4(uint16_t* S, const GemmProb& g, int k, int n, bool nok, float v) {
+    const int lane = threadIdx.x & 63;
+    const float v1 = __shfl_down(v, 16, 64), v2 = __shfl_down(v, 32, 64), v3 = __shfl_down(v, 48, 64);
+    if (S == nullptr || lane >= 16 || !nok || k >= g.wbf_k) return;
+    uint16_t* p = S + (size_t)n * g.wbf_ld + wbf_pos(k, g.wbf_per);
+    if (k + 3 < g.wbf_k) {
+        uint2 o;
+        o.x = bf16_bits(v) | (bf16_bits(v1) << 16);
+        o.y = bf16_bits(v2) | (bf16_bits(v3) << 16);
+        *reinterpret_cast<uint2*>(p) = o;
+    } else {
+        const float vs[4] = {v, v1, v2, v3};
+        for (int i = 0; i < 4 && k + i < g.wbf_k; ++i) p[i] = (uint16_t)bf16_bits(vs[i]);
+    }
+}
+// An activation shadow's 4 consecutive columns n of row m (lanes l .. l + 3 of a row's 16):
+// lane l % 4 == 0 stores them as one 8-B piece (N % 128 == 0: no partial group).  Every lane calls it.
+__device__ __forceinline__ void abf_store4(uint16_t* S, int N, int m, bool mok, int n, float v) {
+    const int lane = threadIdx.x & 63;
+    const float v1 = __shfl_down(v, 1, 64), v2 = __shfl_down(v, 2, 64), v3 = __shfl_down(v, 3, 64);
+    if ((lane & 3) != 0 || !mok || n >= N) return;
+    uint2 o;
+    o.x = bf16_bits(v) | (bf16_bits(v1) << 16);
+    o.y = bf16_bits(v2) | (bf16_bits(v3) << 16);
+    *reinterpret_cast<uint2*>(S + (size_t)m * N + wbf_pos(n, wbf_per_of(N))) = o;
 }
 // The control-block scalars a GEMM epilogue needs (the optimiser step, the Polyak gate, the
 // expert weight), requested with the epilogue operands before the main loop: read after the
@@ -1126,32 +1153,31 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             const float o = act_f(v + e0[s], g.act);
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], o);
             if constexpr (BF) {     // the next layer's bf16 A operand (its K = this N)
-                if (g.obf != nullptr && out_ok)
-                    g.obf[(size_t)mm * g.N + wbf_pos(nn, wbf_per_of(g.N))] = __builtin_bit_cast(uint16_t, (__bf16)o);
+                if (g.obf != nullptr) abf_store4(g.obf, g.N, mm, mm < g.M, nn, o);
             }
         } else if constexpr (MODE == GM_DX) {
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0[s], g.act));
         } else {
-            if (!out_ok) continue;
             if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
-                st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
+                if (out_ok) st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
                 continue;
             }
+            // every lane computes (clamped operands) so the shadow stores can gather across lanes
             const float lr_t = adam_lr(ga.adam, g.group, es.t + 1 - ga.t_adv);
             const float gr = v * g.grad_scale;
             const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
             const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
             const float vv1 = e2[s] + (gr * gr - e2[s]) * (1.f - b2);
             const float pn = e0[s] - (mm1 * lr_t) / (sqrtf(vv1) + eps);
-            st_out(&g.P[pidx], pn);
-            st_out(&g.P[pidx + ga.p_stride], mm1);
-            st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-            wbf_store(g.wbf, g, mm, nn, pn);
-            if (g.T != nullptr && polyak) {
-                const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
-                st_out(&g.T[pidx], tv);
-                wbf_store(g.obf, g, mm, nn, tv);
+            const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
+            if (out_ok) {
+                st_out(&g.P[pidx], pn);
+                st_out(&g.P[pidx + ga.p_stride], mm1);
+                st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+                if (g.T != nullptr && polyak) st_out(&g.T[pidx], tv);
             }
+            wbf_store4(g.wbf, g, mm, nn, nn < g.N, pn);
+            if (g.T != nullptr && polyak) wbf_store4(g.obf, g, mm, nn, nn < g.N, tv);
         }
     }
 }
@@ -1653,34 +1679,38 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             return;
         }
     }
-    if (!out_ok) return;
     if constexpr (MODE == GM_FWD) {
+        if (!out_ok) return;
         st_out(&g.C[(size_t)mm * g.ldc + nn], act_f(v + e0, g.act));
     } else if constexpr (MODE == GM_DX) {
+        if (!out_ok) return;
         st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0, g.act));
     } else {
         if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
-            st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
+            if (out_ok) st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             return;
         }
+        // every lane computes (clamped operands) so the shadow stores can gather across lanes
         const float lr_t = adam_lr(ga.adam, g.group, es.t + 1 - ga.t_adv);
         const float gr = v * g.grad_scale;
         const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
         const float mm1 = e1 + (gr - e1) * (1.f - b1);
         const float vv1 = e2 + (gr * gr - e2) * (1.f - b2);
         const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
-        st_out(&g.P[pidx], pn);
-        st_out(&g.P[pidx + ga.p_stride], mm1);
-        st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-        wbf_store(g.wbf, g, mm, nn, pn);
+        if (out_ok) {
+            st_out(&g.P[pidx], pn);
+            st_out(&g.P[pidx + ga.p_stride], mm1);
+            st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+        }
+        wbf_store4(g.wbf, g, mm, nn, nn < g.N, pn);
         if (g.T != nullptr) {
             const int64_t nts = (int64_t)__builtin_amdgcn_readfirstlane((int)(es.nts >> 32)) << 32 |
                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
             if (nts % tui == 0) {
                 const float tv = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
-                st_out(&g.T[pidx], tv);
-                wbf_store(g.obf, g, mm, nn, tv);
+                if (out_ok) st_out(&g.T[pidx], tv);
+                wbf_store4(g.obf, g, mm, nn, nn < g.N, tv);
             }
         }
     }
@@ -2051,27 +2081,28 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
         v = v + lds[2 * WS + o];
         v = v + lds[3 * WS + o];
         const int mm = m0 + 16 * (s / NH) + row, nn = n0 + 16 * (s % NH) + col;
-        if (mm >= g.M || nn >= g.N) continue;
+        const bool ok = mm < g.M && nn < g.N;
         const size_t pidx = (size_t)mm * g.ldp + nn;
         if (g.epi == EPI_STORE) {    // data-parallel: the local gradient, Adam after the all-reduce
-            st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
+            if (ok) st_out(&g.P[pidx + 3 * ga.p_stride], v * g.grad_scale);
             continue;
         }
+        // every lane computes (clamped operands) so the shadow stores can gather across lanes
         const float lr_t = adam_lr(ga.adam, g.group, es.t + 1 - ga.t_adv);
         const float gr = v * g.grad_scale;
         const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
         const float mm1 = e1[s] + (gr - e1[s]) * (1.f - b1);
         const float vv1 = e2[s] + (gr * gr - e2[s]) * (1.f - b2);
         const float pn = e0[s] - (mm1 * lr_t) / (sqrtf(vv1) + eps);
-        st_out(&g.P[pidx], pn);
-        st_out(&g.P[pidx + ga.p_stride], mm1);
-        st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-        wbf_store(g.wbf, g, mm, nn, pn);
-        if (g.T != nullptr && polyak) {
-            const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
-            st_out(&g.T[pidx], tv);
-            wbf_store(g.obf, g, mm, nn, tv);
+        const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
+        if (ok) {
+            st_out(&g.P[pidx], pn);
+            st_out(&g.P[pidx + ga.p_stride], mm1);
+            st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+            if (g.T != nullptr && polyak) st_out(&g.T[pidx], tv);
         }
+        wbf_store4(g.wbf, g, mm, nn, nn < g.N, pn);
+        if (g.T != nullptr && polyak) wbf_store4(g.obf, g, mm, nn, nn < g.N, tv);
     }
     GEMM_PH(4);
     if (ga.ktime != nullptr) {

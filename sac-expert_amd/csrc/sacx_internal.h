@@ -146,7 +146,10 @@ struct GemmProb {
 __host__ __device__ inline int wbf_per_of(int K) { return (((K + 15) >> 4) + 3) >> 2; }
 __host__ __device__ inline int wbf_ld_of(int K) { return 4 * ((wbf_per_of(K) + 1) >> 1) * 32; }
 __host__ __device__ inline int wbf_pos(int k, int per) {
-    const int s = k >> 4, w = s / per, i = s - w * per;
+    const int s = k >> 4;
+    if ((per & 1) == 0)        // every wave starts on an even slab: pair s / 2, half s % 2
+        return (s >> 1) * 32 + ((k >> 2) & 3) * 8 + (s & 1) * 4 + (k & 3);
+    const int w = s / per, i = s - w * per;
     return (w * ((per + 1) >> 1) + (i >> 1)) * 32 + ((k >> 2) & 3) * 8 + (i & 1) * 4 + (k & 3);
 }
 

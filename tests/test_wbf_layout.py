@@ -75,3 +75,15 @@ def test_activation_shadows_are_dense_at_multiples_of_128():
     for K in (128, 256, 384, 512):
         assert ld_of(K) == K
         assert sorted(pos(k, per_of(K)) for k in range(K)) == list(range(K))
+
+
+def test_even_per_fast_path():
+    """wbf_pos's branch for an even `per` (every wave starts on an even slab) equals the general form."""
+    for K in range(1, 1100, 7):
+        per = per_of(K)
+        if per % 2:
+            continue
+        for k in range(K):
+            s = k >> 4
+            fast = (s >> 1) * 32 + ((k >> 2) & 3) * 8 + (s & 1) * 4 + (k & 3)
+            assert fast == pos(k, per), (K, k)
