@@ -210,24 +210,11 @@ __device__ __forceinline__ bf16x8_t wbf_load(__amdgpu_buffer_rsrc_t r, bool ok, 
 }
 // bf16 image of a float as raw bits (round to nearest even, as the converting loads)
 __device__ __forceinline__ uint32_t bf16_bits(float v) { return __builtin_bit_cast(uint16_t, (__bf16)v); }
-// A weight shadow's 4 consecutive k of column n: in the GEMM epilogues' thread map (row = t >> 4,
-// col = t & 15) they are the rows of lanes l, l + 16, l + 32, l + 48 of one wave, so lane l < 16
-// (whose k is a multiple of 4) gathers them and stores one 8-B piece (4 consecutive shadow
-// positions); at the end of K only the positions of k < wbf_k.  Every lane of the wave calls it.
-__device__ __forceinline__ void wbf_store4(uint16_t* S, const GemmProb& g, int k, int n, bool nok, float v) {
-    const int lane = threadIdx.x & 63;
-    const float v1 = __shfl_down(v, 16, 64), v2 = __shfl_down(v, 32, 64), v3 = __shfl_down(v, 48, 64);
-    if (S == nullptr || lane >= 16 || !nok || k >= g.wbf_k) return;
-    uint16_t* p = S + (size_t)n * g.wbf_ld + wbf_pos(k, g.wbf_per);
-    if (k + 3 < g.wbf_k) {
-        uint2 o;
-        o.x = bf16_bits(v) | (bf16_bits(v1) << 16);
-        o.y = bf16_bits(v2) | (bf16_bits(v3) << 16);
-        *reinterpret_cast<uint2*>(p) = o;
-    } else {
-        const float vs[4] = {v, v1, v2, v3};
-        for (int i = 0; i < 4 && k + i < g.wbf_k; ++i) p[i] = (uint16_t)bf16_bits(vs[i]);
-    }
+// a weight's bf16 shadow element (the Adam epilogues: one 2-B store per updated weight; the
+// lane-gathered 8-B form measured slower there -- 3 cross-lane reads per piece, 22.1 vs 17.9 us
+// for Humanoid's critic.adam)
+__device__ __forceinline__ void wbf_store(uint16_t* S, const GemmProb& g, int k, int n, float v) {
+    if (S != nullptr && k < g.wbf_k) S[(size_t)n * g.wbf_ld + wbf_pos(k, g.wbf_per)] = (uint16_t)bf16_bits(v);
 }
 // An activation shadow's 4 consecutive columns n of row m (lanes l .. l + 3 of a row's 16):
 // lane l % 4 == 0 stores them as one 8-B piece (N % 128 == 0: no partial group).  Every lane calls it.
@@ -1174,10 +1161,12 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 st_out(&g.P[pidx], pn);
                 st_out(&g.P[pidx + ga.p_stride], mm1);
                 st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-                if (g.T != nullptr && polyak) st_out(&g.T[pidx], tv);
+                wbf_store(g.wbf, g, mm, nn, pn);
+                if (g.T != nullptr && polyak) {
+                    st_out(&g.T[pidx], tv);
+                    wbf_store(g.obf, g, mm, nn, tv);
+                }
             }
-            wbf_store4(g.wbf, g, mm, nn, nn < g.N, pn);
-            if (g.T != nullptr && polyak) wbf_store4(g.obf, g, mm, nn, nn < g.N, tv);
         }
     }
 }
@@ -1701,16 +1690,18 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             st_out(&g.P[pidx], pn);
             st_out(&g.P[pidx + ga.p_stride], mm1);
             st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+            wbf_store(g.wbf, g, mm, nn, pn);
         }
-        wbf_store4(g.wbf, g, mm, nn, nn < g.N, pn);
         if (g.T != nullptr) {
             const int64_t nts = (int64_t)__builtin_amdgcn_readfirstlane((int)(es.nts >> 32)) << 32 |
                                 (uint32_t)__builtin_amdgcn_readfirstlane((int)es.nts);
             const int64_t tui = ga.adam.target_update_int > 0 ? ga.adam.target_update_int : 1;
             if (nts % tui == 0) {
                 const float tv = e3 * ga.adam.tau_keep + pn * ga.adam.tau_take;
-                if (out_ok) st_out(&g.T[pidx], tv);
-                wbf_store4(g.obf, g, mm, nn, nn < g.N, tv);
+                if (out_ok) {
+                    st_out(&g.T[pidx], tv);
+                    wbf_store(g.obf, g, mm, nn, tv);
+                }
             }
         }
     }
@@ -2099,10 +2090,12 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
             st_out(&g.P[pidx], pn);
             st_out(&g.P[pidx + ga.p_stride], mm1);
             st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
-            if (g.T != nullptr && polyak) st_out(&g.T[pidx], tv);
+            wbf_store(g.wbf, g, mm, nn, pn);
+            if (g.T != nullptr && polyak) {
+                st_out(&g.T[pidx], tv);
+                wbf_store(g.obf, g, mm, nn, tv);
+            }
         }
-        wbf_store4(g.wbf, g, mm, nn, nn < g.N, pn);
-        if (g.T != nullptr && polyak) wbf_store4(g.obf, g, mm, nn, nn < g.N, tv);
     }
     GEMM_PH(4);
     if (ga.ktime != nullptr) {

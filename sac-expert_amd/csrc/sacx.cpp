@@ -150,7 +150,7 @@ struct sacx_handle {
     // add_gemm wires them into the problems it builds (the update plans only)
     struct WbfMat { std::string name; int K, N; };
     std::vector<WbfMat> wbf_mats;
-    int wbf_enabled = 1;      // SACX_WBF: 0 off, 1 weights + layer-0 activations, 2 weights only
+    int wbf_enabled = 3;      // SACX_WBF: 0 off, 1 weights + layer-0 activations, 2 weights only, 3 activations only
     bool wbf_attach = false;
     bool wbf_live = false;    // the update plans read / maintain the shadows (refreshed per step call)
     std::vector<std::string> abf_segs;          // activation segments with a bf16 shadow ("abf.<name>")
@@ -329,7 +329,7 @@ void build_layout(sacx_handle* h) {
     // bf16 shadows of the SAC nets' hidden-layer weights (config C5, 32x32 forward tiles): the
     // forward launches read B from them (wbf_pos layout), the Adam epilogues keep them current
     h->wbf_mats.clear();
-    if (h->cfg.gemm_bf16 && h->wbf_enabled) {
+    if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 2)) {
         const char* nets[] = {"actor", "q0", "q1", "t0", "t1"};
         for (const char* n : nets) {
             const int in = std::string(n) == "actor" ? S : S + A;
@@ -453,7 +453,7 @@ void build_layout(sacx_handle* h) {
     // (H0 a multiple of 128: every shadow position holds a k < H0; not under the layer norm,
     // which rewrites the actor's layer-0 output after the GEMM)
     h->abf_segs.clear();
-    if (h->cfg.gemm_bf16 && h->wbf_enabled == 1 && H0 % 128 == 0 && !h->ln)
+    if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 3) && H0 % 128 == 0 && !h->ln)
         for (const char* n : {"ws.Ha1", "ws.Hq1", "ws.Hp1"}) {
             const auto& sg = h->seg(n);
             h->add(std::string("abf.") + n, sg.rows, H0 / 2, SACX_U32, SACX_ROLE_WORK);
@@ -1636,7 +1636,7 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
 // Rebuilds every bf16 weight shadow from the fp32 weights (all seeds): at each entry point that
 // runs the update plans, so that parameter writes from the host reach the bf16 forward tiles
 void wbf_refresh(sacx_handle* h, hipStream_t s) {
-    if (!h->wbf_live) return;
+    if (!h->wbf_live || h->wbf_mats.empty()) return;
     WbfArgs a{};
     for (const auto& m : h->wbf_mats) {
         if (a.nmat == WBF_MAXM) break;
@@ -2198,7 +2198,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     }
     // the weight shadows feed the update plans' 32x32 bf16 forward tiles; the Adam epilogues
     // keep them current (not the data-parallel modes, whose Adam runs in k_adam_apply)
-    h->wbf_attach = !h->wbf_mats.empty() && h->tile32 > 0 && h->dp_ranks == 0;
+    h->wbf_attach = (!h->wbf_mats.empty() || !h->abf_segs.empty()) && h->tile32 > 0 && h->dp_ranks == 0;
     h->wbf_live = h->wbf_attach;
     for (int sl = 0; sl < h->nslot; ++sl) {
         h->abf_written.clear();

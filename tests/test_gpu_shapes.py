@@ -127,15 +127,15 @@ def _wbf_expected(W):
 
 @pytest.mark.parametrize("eager", [False, True])
 def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
-    """C5's forward tiles reading B from the bf16 weight shadows and layer 1's A from the layer-0
-    outputs' shadows (SACX_WBF=1, default; 2: weights only) equal the converting loads
+    """C5's forward tiles reading layer 1's A from the layer-0 outputs' bf16 shadows (SACX_WBF=3,
+    the default), B from the weights' shadows (2), or both (1) equal the converting loads
     (SACX_WBF=0) bit for bit over 2 x 24 Humanoid updates at B = 1,024, with a host write of the
     parameters in between (the weight shadows are rebuilt at the next step call); after each run
     every weight shadow equals the bf16 image of its fp32 weights in the wbf_pos layout, and the
     critics' layer-0 output shadow that of the last update's activations."""
     B, n = 1024, 24
     outs = []
-    for wbf in ("0", "2", "1"):
+    for wbf in ("0", "3", "2", "1"):
         monkeypatch.setenv("SACX_WBF", wbf)
         eng, *_ = make_pair(act="relu", B=B, N=6000, seed=41, done_p=0.01, gemm_bf16=True, graph_steps=8, **HUM)
         eng.rng_set_state(np.random.RandomState(8).get_state())
@@ -147,7 +147,7 @@ def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
         eng.sync()
         outs.append((eng.stats(2 * n).copy(), eng.v["params"].cpu().numpy().copy(),
                      eng.v["adam_v"].cpu().numpy().copy()))
-        if wbf != "0":
+        if wbf in ("1", "2"):
             names = [f"{net}.l{l}" for net in ("actor", "q0", "q1", "t0", "t1") for l in (0, 1)]
             for nm in names:
                 assert "wbf." + nm in eng.v, nm
@@ -155,7 +155,7 @@ def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
                 exp = _wbf_expected(Wx[:-1])             # W_ext without the bias row
                 got = eng.v["wbf." + nm].cpu().numpy().view(np.uint16).reshape(exp.shape[0], -1)
                 assert np.array_equal(got, exp), nm
-        if wbf == "1":
+        if wbf in ("1", "3"):
             hq = eng.v["ws.Hq1"].cpu().numpy()
             exp = _wbf_expected(hq.T)
             got = eng.v["abf.ws.Hq1"].cpu().numpy().view(np.uint16).reshape(exp.shape[0], -1)
