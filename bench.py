@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import re
 import json
 import os
 import sys
@@ -130,7 +131,12 @@ def rocprof_family_avg(kernel, config, flops_per_launch):
     """Calls-weighted average duration of `kernel`'s instances in the newest committed
     profiles/r*_<config>_kernel_stats_*.csv and the roofline fraction it gives."""
     import csv
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_kernel_stats_*.csv")))
+    # r<round>_<config>_kernel_stats_v<n>.csv exactly (not another config's name ending in <config>),
+    # newest round, then highest version
+    pat = re.compile(rf"r(\d+)_{re.escape(config)}_kernel_stats_v(\d+)\.csv$")
+    found = [(int(m.group(1)), int(m.group(2)), p) for p in glob.glob(os.path.join(ROOT, "profiles", "*.csv"))
+             for m in [pat.match(os.path.basename(p))] if m]
+    paths = [p for _, _, p in sorted(found)]
     if not paths:
         return {}
     tot, n = 0.0, 0

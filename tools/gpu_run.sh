@@ -56,7 +56,7 @@ for step in "$@"; do
       done ;;
     prof)       # rocprofv3 kernel-trace stats of the one-seed bench of config $arg
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof_${arg:-hc}" -o s \
-          -- python bench.py --config "${arg:-hc}" --steps 2000 --warmup 200 --no-cpu-baseline --packed-leg 0 > "$log" 2>&1
+          -- python bench.py --config "${arg:-hc}" --steps 2000 --warmup 200 --no-cpu-baseline --no-roofline --packed-leg 0 > "$log" 2>&1
       rc=$?; echo "[$n prof ${arg:-hc}] rc=$rc $(value "$log")" ;;
     pmc)
       CONFIG=${arg:-hc} bash tools/gpu_pmc.sh > "$log" 2>&1
