@@ -27,6 +27,8 @@ def bench_order(order, steps=20, warmup=5):
     eng.step(warmup, num_timesteps=0, ts_increment=1)
     if order == "warmup-prepare":
         eng.prepare(steps)
+    if os.environ.get("PRE_STEPS"):           # experiment: more updates on warm graphs just before
+        eng.step(int(os.environ["PRE_STEPS"]), num_timesteps=0, ts_increment=1)
     eng.sync()
     if os.environ.get("SPIN_MS"):             # experiment: a non-learner GPU load before the region
         import torch
