@@ -184,3 +184,25 @@ def test_prepare_then_step_is_cached(gpu_available):
         outs.append((eng.stats(150).copy(), eng.v["params"].cpu().numpy().copy()))
         eng.close()
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+
+
+@pytest.mark.parametrize("n,nslot", [(20, 32), (33, 32), (20, 16), (8, 8)])
+def test_short_graphs_equal_eager(gpu_available, monkeypatch, n, nslot):
+    """Graphs no longer than the slot ring draw every sampler batch at their start (the driver's
+    step(20) on HC's 32-slot ring), or all but the last (33 > 32); a batch whose slots are fresh at
+    graph start is drawn exactly once (a batch due at update 0 was once drawn twice, shifting the
+    stream).  Two consecutive step(n) calls == eager launches, bit for bit, RNG state included."""
+    monkeypatch.setenv("SACX_NSLOT", str(nslot))
+    outs = []
+    for eager in (True, False):
+        eng, *_ = make_pair(act="relu", B=256, seed=31, graph_steps=128)
+        eng.rng_set_state(np.random.RandomState(12).get_state())
+        if not eager:
+            eng.prepare(n)
+        for _ in range(2):
+            eng.step(n, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(2 * n).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state()[1].copy()))
+        eng.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
