@@ -1761,6 +1761,19 @@ struct KTimeMap {
     bool rows = false;      // also stamp the row kernels (k_actor_head, k_actor_bwd): dump only
 };
 
+// Sampler batches [s, e) of a G-update call: sizes ramp 1, 2, 4, ... up to nbatch, never crossing
+// a multiple of nbatch (see get_graph)
+std::vector<std::pair<int, int>> sampler_batches(const sacx_handle* h, int G) {
+    std::vector<std::pair<int, int>> batches;
+    const int nbatch = h->nbatch;
+    for (int s0 = 0, ramp = 1; s0 < G; ramp = std::min(nbatch, 2 * ramp)) {
+        const int sz = std::min({ramp, nbatch - s0 % nbatch, G - s0});
+        batches.push_back({s0, s0 + sz});
+        s0 += sz;
+    }
+    return batches;
+}
+
 int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int skip_kind = -1,
               KTimeMap* kt = nullptr) {
     auto key = std::make_tuple(G, with_rng ? 1 : 0, skip_kind);
@@ -1828,13 +1841,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
         // of update e-nslot, and must be done before update s.  When e <= nslot its slots are
         // fresh at graph start: their last reader is update e-1-nslot < 0 of an earlier graph
         // (update 0 folds no alpha rows), complete before this graph starts.
-        std::vector<std::pair<int, int>> batches;
-        const int nbatch = h->nbatch, nslot = h->nslot;
-        for (int s0 = 0, ramp = 1; s0 < G; ramp = std::min(nbatch, 2 * ramp)) {
-            const int sz = std::min({ramp, nbatch - s0 % nbatch, G - s0});
-            batches.push_back({s0, s0 + sz});
-            s0 += sz;
-        }
+        const std::vector<std::pair<int, int>> batches = sampler_batches(h, G);
+        const int nslot = h->nslot;
         for (int b = 0; b < (int)batches.size(); ++b) {
             const int s0 = batches[b].first, n = batches[b].second - s0;
             if ((b + 1 < (int)batches.size() && batches[b + 1].first != batches[b].second) || n < 1 ||
@@ -1956,6 +1964,100 @@ int get_spec_graph(sacx_handle* h, int slot, int prev, hipGraphExec_t* out) {
     HIPCHK(h, hipGraphUpload(exec, h->stream));
     h->graphs[key] = exec;
     *out = exec;
+    return 0;
+}
+
+// Single-stream segments (round 4).  A graph that forks the sampler onto a second stream pays
+// two runtime costs the update chain does not: its host launch takes ~0.55 ms for 20 updates
+// (0.12-0.31 ms for a single-stream graph of the same chain), and its FIRST replay takes
+// ~0.17 ms longer on the device than later ones (a single-stream graph shows no such penalty;
+// r04_first_replay_v1.txt, r04_single_stream_v1.txt).  A call of n <= nslot updates draws every
+// input at its start anyway (all its slots are fresh), so it needs no dependency from the chain to
+// the sampler: the sampler batches run as plain launches on the side stream, and the chain as one
+// single-stream graph per batch segment [s, e), each behind its batch's event.  Segment graphs
+// carry exactly the fork / join graph's main-stream launches: the previous segment's last alpha
+// branch folded into their first update (merged_body), the call's last segment ending with the
+// tail; so the results are bit-identical.  Keyed by (first slot, length, folds a previous
+// branch, ends the call).
+int get_seg_graph(sacx_handle* h, int s0, int n, bool has_prev, bool is_last, hipGraphExec_t* out) {
+    const int nslot = h->nslot;
+    const auto key = std::make_tuple(4, (s0 % nslot) * 1024 + n, (has_prev ? 2 : 0) + (is_last ? 1 : 0));
+    auto it = h->graphs.find(key);
+    if (it != h->graphs.end()) {
+        *out = it->second;
+        return 0;
+    }
+    hipStream_t cs = h->cap_stream;
+    HIPCHK(h, hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
+    std::vector<Launch> body;
+    for (int j = s0; j < s0 + n; ++j) {
+        const int slot = j % nslot, prev = (j > s0 || has_prev) ? (j - 1 + nslot) % nslot : -1;
+        if (!merged_body(h, slot, prev, body)) {
+            hipGraph_t g;
+            (void)hipStreamEndCapture(cs, &g);
+            if (g) (void)hipGraphDestroy(g);
+            return fail(h, "internal: segment body");
+        }
+        for (const Launch& L : body) enqueue(L, h, cs);
+    }
+    if (is_last)
+        for (const Launch& L : h->plan[(s0 + n - 1) % nslot])
+            if (L.alpha_branch) enqueue(L, h, cs);
+    hipGraph_t graph;
+    HIPCHK(h, hipStreamEndCapture(cs, &graph));
+    hipGraphExec_t exec;
+    HIPCHK(h, hipGraphInstantiateWithFlags(&exec, graph, 0));
+    HIPCHK(h, hipGraphDestroy(graph));
+    HIPCHK(h, hipGraphUpload(exec, h->stream));
+    h->graphs[key] = exec;
+    *out = exec;
+    return 0;
+}
+
+// whether step(n) takes the single-stream segments (SACX_SEGMENTS, default on)
+bool use_segments(const sacx_handle* h, int64_t n, int32_t flags) {
+    static const int env = std::getenv("SACX_SEGMENTS") ? std::atoi(std::getenv("SACX_SEGMENTS")) : 1;
+    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 1 && n <= h->nslot;
+}
+
+// The segments of step(n): every segment graph instantiated (prepare), or also launched (run):
+// sampler batches as plain launches on the side stream, each segment behind its batch
+int run_segments(sacx_handle* h, int n, bool run) {
+    const auto batches = sampler_batches(h, n);
+    std::vector<hipGraphExec_t> gx(batches.size());
+    for (size_t b = 0; b < batches.size(); ++b)
+        if (get_seg_graph(h, batches[b].first, batches[b].second - batches[b].first, b > 0,
+                          b + 1 == batches.size(), &gx[b]))
+            return -1;
+    if (!run) return 0;
+    const int nev = (int)batches.size() + 1;
+    for (int i = (int)h->events.size(); i < nev; ++i) {
+        hipEvent_t e;
+        HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        h->events.push_back(e);
+    }
+    hipStream_t rs = h->rng_stream;
+    HIPCHK(h, hipEventRecord(h->events[batches.size()], h->stream));   // the call's start (set_ctl, earlier work)
+    HIPCHK(h, hipStreamWaitEvent(rs, h->events[batches.size()], 0));
+    for (size_t b = 0; b < batches.size(); ++b) {
+        const int j0 = batches[b].first, nb = batches[b].second - j0;
+        for (const Launch& L : h->plan[j0 % h->nslot]) {
+            if (!is_prologue(L)) continue;
+            Launch C = L;
+            if (C.kind == Launch::RNG) {
+                C.rng.reset_seq = (b == 0);
+                C.rng.nupd = nb;
+            } else {
+                C.gather.nupd = nb;
+            }
+            enqueue(C, h, rs);
+        }
+        HIPCHK(h, hipEventRecord(h->events[b], rs));
+    }
+    for (size_t b = 0; b < batches.size(); ++b) {
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->events[b], 0));
+        HIPCHK(h, hipGraphLaunch(gx[b], h->stream));
+    }
     return 0;
 }
 
@@ -2729,6 +2831,8 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     } else if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
         HIPCHK(h, hipGetLastError());
+    } else if (use_segments(h, n_steps, flags)) {
+        if (run_segments(h, (int)n_steps, true)) return -1;
     } else {
         std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
         if (step_graph_list(h, n_steps, ext, &gl)) return -1;
@@ -2744,8 +2848,12 @@ int sacx_prepare(sacx_handle* h, int64_t n_steps, int32_t flags) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (settle(h)) return -1;
     if (n_steps <= 0 || (flags & SACX_STEP_EAGER)) return 0;
-    std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
-    if (step_graph_list(h, n_steps, (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0, &gl)) return -1;
+    if (use_segments(h, n_steps, flags)) {
+        if (run_segments(h, (int)n_steps, false)) return -1;
+    } else {
+        std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
+        if (step_graph_list(h, n_steps, (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0, &gl)) return -1;
+    }
     if (spec_mode(h) && n_steps == 1 && flags == 0) {
         hipGraphExec_t g;                 // the drop-in loop's speculative path replays these
         for (int slot = 1; slot <= 2; ++slot)

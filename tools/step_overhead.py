@@ -21,6 +21,11 @@ def bench_order(order, steps=20, warmup=5):
     from sac_eo.common.replicas import init_replica
     rep = init_replica()
     eng = bench.build_engine(bench.CONFIGS["hc"], rep.seeds(0), device=rep.device)
+    if os.environ.get("EXTERNAL"):             # experiment: single-stream graphs (no sampler branch)
+        step0 = eng.step
+        eng.step = lambda n, **kw: step0(n, external=True, **kw)
+        prep0 = eng.prepare
+        eng.prepare = lambda n: prep0(n, external=True)
     if order == "prepare-warmup":
         eng.prepare(steps)
         eng.sync()
