@@ -2015,48 +2015,74 @@ int get_seg_graph(sacx_handle* h, int s0, int n, bool has_prev, bool is_last, hi
 }
 
 // whether step(n) takes the single-stream segments (SACX_SEGMENTS, default on)
+// (2: every call, the mid-call sampler batches behind the end of the segment holding the update
+// that frees their slots)
 bool use_segments(const sacx_handle* h, int64_t n, int32_t flags) {
     static const int env = std::getenv("SACX_SEGMENTS") ? std::atoi(std::getenv("SACX_SEGMENTS")) : 1;
-    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 1 && n <= h->nslot;
+    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 1 &&
+           (n <= h->nslot || (env == 2 && n <= (int64_t)1 << 24));
 }
 
 // The segments of step(n): every segment graph instantiated (prepare), or also launched (run):
 // sampler batches as plain launches on the side stream, each segment behind its batch
 int run_segments(sacx_handle* h, int n, bool run) {
     const auto batches = sampler_batches(h, n);
-    std::vector<hipGraphExec_t> gx(batches.size());
-    for (size_t b = 0; b < batches.size(); ++b)
-        if (get_seg_graph(h, batches[b].first, batches[b].second - batches[b].first, b > 0,
-                          b + 1 == batches.size(), &gx[b]))
+    const int nb = (int)batches.size(), nslot = h->nslot;
+    // segment k = batch k; batch b is drawn at the start when its slots are fresh (e <= nslot),
+    // else behind the end of the segment holding update e - nslot (the one that frees them)
+    std::vector<int> due_seg(nb, -1);
+    for (int b = 0, k = 0; b < nb; ++b) {
+        const int u = batches[b].second - nslot;
+        if (u <= 0) continue;
+        while (batches[k].second <= u) ++k;
+        due_seg[b] = k;
+    }
+    std::vector<hipGraphExec_t> gx(nb);
+    for (int b = 0; b < nb; ++b)
+        if (get_seg_graph(h, batches[b].first, batches[b].second - batches[b].first, b > 0, b + 1 == nb, &gx[b]))
             return -1;
     if (!run) return 0;
-    const int nev = (int)batches.size() + 1;
+    const int nev = 2 * nb + 1;
     for (int i = (int)h->events.size(); i < nev; ++i) {
         hipEvent_t e;
         HIPCHK(h, hipEventCreateWithFlags(&e, hipEventDisableTiming));
         h->events.push_back(e);
     }
+    hipEvent_t* evR = h->events.data();          // batch b drawn
+    hipEvent_t* evE = h->events.data() + nb;     // segment k done
     hipStream_t rs = h->rng_stream;
-    HIPCHK(h, hipEventRecord(h->events[batches.size()], h->stream));   // the call's start (set_ctl, earlier work)
-    HIPCHK(h, hipStreamWaitEvent(rs, h->events[batches.size()], 0));
-    for (size_t b = 0; b < batches.size(); ++b) {
-        const int j0 = batches[b].first, nb = batches[b].second - j0;
-        for (const Launch& L : h->plan[j0 % h->nslot]) {
+    auto draw = [&](int b) {
+        const int j0 = batches[b].first, n_b = batches[b].second - j0;
+        for (const Launch& L : h->plan[j0 % nslot]) {
             if (!is_prologue(L)) continue;
             Launch C = L;
             if (C.kind == Launch::RNG) {
                 C.rng.reset_seq = (b == 0);
-                C.rng.nupd = nb;
+                C.rng.nupd = n_b;
             } else {
-                C.gather.nupd = nb;
+                C.gather.nupd = n_b;
             }
             enqueue(C, h, rs);
         }
-        HIPCHK(h, hipEventRecord(h->events[b], rs));
-    }
-    for (size_t b = 0; b < batches.size(); ++b) {
-        HIPCHK(h, hipStreamWaitEvent(h->stream, h->events[b], 0));
-        HIPCHK(h, hipGraphLaunch(gx[b], h->stream));
+        return hipEventRecord(evR[b], rs);
+    };
+    HIPCHK(h, hipEventRecord(h->events[2 * nb], h->stream));   // the call's start (set_ctl, earlier work)
+    HIPCHK(h, hipStreamWaitEvent(rs, h->events[2 * nb], 0));
+    for (int b = 0; b < nb; ++b)
+        if (due_seg[b] < 0) HIPCHK(h, draw(b));
+    for (int k = 0; k < nb; ++k) {
+        HIPCHK(h, hipStreamWaitEvent(h->stream, evR[k], 0));
+        HIPCHK(h, hipGraphLaunch(gx[k], h->stream));
+        bool rec = false;
+        for (int b = 0; b < nb; ++b)
+            if (due_seg[b] == k) {
+                if (!rec) {
+                    HIPCHK(h, hipEventRecord(evE[k], h->stream));
+                    HIPCHK(h, hipStreamWaitEvent(rs, evE[k], 0));
+                    rec = true;
+                }
+                HIPCHK(h, draw(b));
+            }
     }
     return 0;
 }
