@@ -2018,7 +2018,8 @@ int get_seg_graph(sacx_handle* h, int s0, int n, bool has_prev, bool is_last, hi
 // (2: every call, the mid-call sampler batches behind the end of the segment holding the update
 // that frees their slots)
 bool use_segments(const sacx_handle* h, int64_t n, int32_t flags) {
-    static const int env = std::getenv("SACX_SEGMENTS") ? std::atoi(std::getenv("SACX_SEGMENTS")) : 1;
+    const char* e = std::getenv("SACX_SEGMENTS");
+    const int env = e ? std::atoi(e) : 1;
     return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 1 &&
            (n <= h->nslot || (env == 2 && n <= (int64_t)1 << 24));
 }
