@@ -153,6 +153,7 @@ struct sacx_handle {
     int wbf_enabled = 3;      // SACX_WBF: 0 off, 1 weights + layer-0 activations, 2 weights only, 3 activations only
     bool wbf_attach = false;
     bool wbf_live = false;    // the update plans read / maintain the shadows (refreshed per step call)
+    hipEvent_t seg_start = nullptr;   // run_segments: the call's start on the bound stream (before set_ctl)
     std::vector<std::string> abf_segs;          // activation segments with a bf16 shadow ("abf.<name>")
     std::vector<std::pair<const float*, const float*>> abf_written;   // plan build: ranges a wired producer stores
     bool rng_split = false;   // k_rng + k_polar (rng.pairs): the polar transform spread over the GPU
@@ -2020,7 +2021,9 @@ int get_seg_graph(sacx_handle* h, int s0, int n, bool has_prev, bool is_last, hi
 bool use_segments(const sacx_handle* h, int64_t n, int32_t flags) {
     const char* e = std::getenv("SACX_SEGMENTS");
     const int env = e ? std::atoi(e) : 1;
-    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 1 &&
+    // n = 1 keeps its fork / join graph: 115 vs 134 us per warm call (r04_segments_by_n_v1.txt;
+    // from n = 2 on the segments win, 202 vs 209 us, 1,316 vs 1,375 us at n = 20)
+    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 2 &&
            (n <= h->nslot || (env == 2 && n <= (int64_t)1 << 24));
 }
 
@@ -2067,8 +2070,10 @@ int run_segments(sacx_handle* h, int n, bool run) {
         }
         return hipEventRecord(evR[b], rs);
     };
-    HIPCHK(h, hipEventRecord(h->events[2 * nb], h->stream));   // the call's start (set_ctl, earlier work)
-    HIPCHK(h, hipStreamWaitEvent(rs, h->events[2 * nb], 0));
+    // the sampler follows the bound stream's earlier work but not this call's k_set_ctl (it writes
+    // num_timesteps / ts_increment, which the sampler does not read): sacx_sac_step recorded
+    // seg_start before launching it
+    HIPCHK(h, hipStreamWaitEvent(rs, h->seg_start, 0));
     for (int b = 0; b < nb; ++b)
         if (due_seg[b] < 0) HIPCHK(h, draw(b));
     for (int k = 0; k < nb; ++k) {
@@ -2228,6 +2233,7 @@ void sacx_destroy(sacx_handle* h) {
     if (!h) return;
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     if (h->act_ev) (void)hipEventDestroy(h->act_ev);
+    if (h->seg_start) (void)hipEventDestroy(h->seg_start);
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto& m : h->mgraphs)
         for (auto& kv : m) (void)hipGraphExecDestroy(kv.second);
@@ -2844,6 +2850,11 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // a deferred alpha.final (folded into this update) adds ts_increment to num_timesteps before
     // this update reads it
     const int prev = use_spec ? h->alpha_pending : -1;
+    const bool segs = !use_spec && !(flags & SACX_STEP_EAGER) && use_segments(h, n_steps, flags);
+    if (segs) {
+        if (!h->seg_start) HIPCHK(h, hipEventCreateWithFlags(&h->seg_start, hipEventDisableTiming));
+        HIPCHK(h, hipEventRecord(h->seg_start, h->stream));
+    }
     wbf_refresh(h, h->stream);
     launch_set_ctl(h->ctl0(), num_timesteps - (prev >= 0 ? ts_increment : 0), ts_increment,
                    (int64_t)h->seed_bytes, h->seeds, h->stream);
@@ -2858,7 +2869,7 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     } else if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
         HIPCHK(h, hipGetLastError());
-    } else if (use_segments(h, n_steps, flags)) {
+    } else if (segs) {
         if (run_segments(h, (int)n_steps, true)) return -1;
     } else {
         std::vector<std::pair<hipGraphExec_t, int64_t>> gl;
