@@ -2023,7 +2023,8 @@ bool use_segments(const sacx_handle* h, int64_t n, int32_t flags) {
     const int env = e ? std::atoi(e) : 1;
     // n = 1 keeps its fork / join graph: 115 vs 134 us per warm call (r04_segments_by_n_v1.txt;
     // from n = 2 on the segments win, 202 vs 209 us, 1,316 vs 1,375 us at n = 20)
-    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= 2 &&
+    const int nmin = std::getenv("SACX_SEG_NMIN") ? std::atoi(std::getenv("SACX_SEG_NMIN")) : 2;
+    return env != 0 && flags == 0 && h->dp_ranks == 0 && !h->dp_local && n >= nmin &&
            (n <= h->nslot || (env == 2 && n <= (int64_t)1 << 24));
 }
 
@@ -2055,7 +2056,7 @@ int run_segments(sacx_handle* h, int n, bool run) {
     hipEvent_t* evR = h->events.data();          // batch b drawn
     hipEvent_t* evE = h->events.data() + nb;     // segment k done
     hipStream_t rs = h->rng_stream;
-    auto draw = [&](int b) {
+    auto draw = [&](int b, hipStream_t st) {
         const int j0 = batches[b].first, n_b = batches[b].second - j0;
         for (const Launch& L : h->plan[j0 % nslot]) {
             if (!is_prologue(L)) continue;
@@ -2066,18 +2067,29 @@ int run_segments(sacx_handle* h, int n, bool run) {
             } else {
                 C.gather.nupd = n_b;
             }
-            enqueue(C, h, rs);
+            enqueue(C, h, st);
         }
-        return hipEventRecord(evR[b], rs);
+        return hipEventRecord(evR[b], st);
     };
     // the sampler follows the bound stream's earlier work but not this call's k_set_ctl (it writes
     // num_timesteps / ts_increment, which the sampler does not read): sacx_sac_step recorded
     // seg_start before launching it
-    HIPCHK(h, hipStreamWaitEvent(rs, h->seg_start, 0));
-    for (int b = 0; b < nb; ++b)
-        if (due_seg[b] < 0) HIPCHK(h, draw(b));
+    // SACX_SEG_INLINE0 (default 1): warm step(20) 1,296 vs 1,320 us, the driver's command +0.3 %
+    // (r04_seg_inline0_v1.txt)
+    const char* ie = std::getenv("SACX_SEG_INLINE0");
+    const int first_inline = ie ? std::atoi(ie) : 1;
+    if (first_inline) {
+        // batch 0 on the bound stream itself, right before segment 0: no cross-stream hop on the
+        // call's critical path; the side stream continues the draws after it
+        HIPCHK(h, draw(0, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(rs, evR[0], 0));
+    } else {
+        HIPCHK(h, hipStreamWaitEvent(rs, h->seg_start, 0));
+    }
+    for (int b = first_inline ? 1 : 0; b < nb; ++b)
+        if (due_seg[b] < 0) HIPCHK(h, draw(b, rs));
     for (int k = 0; k < nb; ++k) {
-        HIPCHK(h, hipStreamWaitEvent(h->stream, evR[k], 0));
+        if (k > 0 || !first_inline) HIPCHK(h, hipStreamWaitEvent(h->stream, evR[k], 0));
         HIPCHK(h, hipGraphLaunch(gx[k], h->stream));
         bool rec = false;
         for (int b = 0; b < nb; ++b)
@@ -2087,7 +2099,7 @@ int run_segments(sacx_handle* h, int n, bool run) {
                     HIPCHK(h, hipStreamWaitEvent(rs, evE[k], 0));
                     rec = true;
                 }
-                HIPCHK(h, draw(b));
+                HIPCHK(h, draw(b, rs));
             }
     }
     return 0;
