@@ -127,7 +127,7 @@ def pmc_traffic(kernel, config):
         return None, None
 
 
-def rocprof_family_avg(kernel, config, flops_per_launch):
+def rocprof_family_avg(kernel, config, flops_per_launch, peak=None):
     """Calls-weighted average duration of `kernel`'s instances in the newest committed
     profiles/r*_<config>_kernel_stats_*.csv and the roofline fraction it gives."""
     import csv
@@ -151,7 +151,8 @@ def rocprof_family_avg(kernel, config, flops_per_launch):
         return {}
     avg_us = tot / n / 1e3
     return {"rocprof_stats": os.path.relpath(paths[-1], ROOT), "rocprof_avg_launch_us": round(avg_us, 3),
-            "rocprof_frac": round(flops_per_launch / (avg_us * 1e-6) / (FP32_PEAK_TFLOPS * 1e12), 5)}
+            "rocprof_calls": n,
+            "rocprof_frac": round(flops_per_launch / (avg_us * 1e-6) / ((peak or FP32_PEAK_TFLOPS) * 1e12), 5)}
 
 
 def pmc_counter(kernel, config, counter):
@@ -197,14 +198,25 @@ def roofline(eng, config, n_prof=20, n_replays=20):
     mfma = pmc_counter(dom, config, "SQ_VALU_MFMA_BUSY_CYCLES")
     t_full = eng.time_graph(n_replays)
     t_wo = eng.time_graph(n_replays, dom)
+    rp = rocprof_family_avg(dom, config, flops_per_launch, peak)
+    # `achieved` / `frac` come from the committed rocprofv3 --kernel-trace --stats summary of this
+    # command (profiles/r<round>_<config>_kernel_stats_v<n>.csv: the family's calls-weighted average
+    # duration), so that frac x peak x avg_launch_us reproduces by hand from profiles/; the live
+    # per-workgroup stamps of this run are reported beside them as *_live
+    avg_rp = rp.get("rocprof_avg_launch_us")
+    achieved_rp = flops_per_launch / (avg_rp * 1e-6) / 1e12 if avg_rp else None
     out = {
-        "kernel": dom, "bound": "mfma", "achieved": round(achieved, 3), "peak": peak,
-        "unit": "TFLOP/s", "frac": round(achieved / peak, 5),
+        "kernel": dom, "bound": "mfma",
+        "achieved": round(achieved_rp if avg_rp else achieved, 3), "peak": peak,
+        "unit": "TFLOP/s", "frac": round((achieved_rp if avg_rp else achieved) / peak, 5),
+        "frac_source": rp.get("rocprof_stats") or "live stamps (no committed rocprof summary)",
+        "achieved_live": round(achieved, 3), "frac_live": round(achieved / peak, 5),
         "traffic": traffic, "traffic_source": src,
         # matrix-pipe busy cycles per launch (PMC, summed over the 1,024 SIMDs) over the launch's
         # SIMD-cycles at 2.4 GHz: the counter-side view of `frac`
-        "mfma_busy_frac": round(mfma / (avg_us * 1e-6 * 2.4e9 * 1024), 5) if mfma else None,
-        "avg_launch_us": round(avg_us, 3), "launches_per_update": round(launches, 3),
+        "mfma_busy_frac": round(mfma / ((avg_rp or avg_us) * 1e-6 * 2.4e9 * 1024), 5) if mfma else None,
+        "avg_launch_us": round(avg_rp if avg_rp else avg_us, 3), "avg_launch_us_live": round(avg_us, 3),
+        "launches_per_update": round(launches, 3),
         # per-kernel HBM GB/s and MFMA busy for every kernel (k_gather, k_rng, DW+Adam ...)
         "kernel_table": next((os.path.relpath(p, ROOT) for p in sorted(
             glob.glob(os.path.join(ROOT, "profiles", f"r*_{config}_kernel_table_*.md")))[-1:]), None),
@@ -212,8 +224,8 @@ def roofline(eng, config, n_prof=20, n_replays=20):
         "algorithmic_bytes_per_launch": f["bytes"] / launches,
         # the committed rocprofv3 --kernel-trace --stats summary of this command (calls-weighted
         # over every k_gemm instance): its dispatch window includes the end-of-kernel release
-        **rocprof_family_avg(dom, config, flops_per_launch),
-        "timing": "per-workgroup device timestamps in a replay of the update graph (sacx_time_kernels)",
+        **rp,
+        "timing_live": "per-workgroup device timestamps in a replay of the update graph (sacx_time_kernels)",
         "family_us_per_update": round(us_per_update, 3),
         "graph_us_per_update": round(t_full * 1e3, 3),
         "graph_us_per_update_without_family": round(t_wo * 1e3, 3),

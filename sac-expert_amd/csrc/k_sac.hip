@@ -3140,9 +3140,10 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
     if constexpr (TICKET) {
         __syncthreads();
         if (last_s[0] | last_s[1] | last_s[2] | last_s[3]) {
-            // wave 0 finalises; the acquire of the other blocks' partials is its own (the counter
-            // reached nred: every partial was released before its block's increment)
-            if (threadIdx.x < 64) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            // the winning group's RMW saw the count reach nred (every partial was released before its
+            // block's increment); after the barrier every wave of this workgroup acquires at agent
+            // scope itself, whichever wave's atomic observed the count
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
             finalize_update<SACX_FIN_PRE != 0>(ffin, ffin.nred, &fpre);
             if (threadIdx.x == 0) __hip_atomic_store(&ffin.ctl->red_counter[0], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }

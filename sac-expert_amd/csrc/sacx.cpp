@@ -1720,7 +1720,13 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                 } else {
                     C.gemm.hfin = ph->fin;
                     int rb = (a.total_rows + 3) / 4 - C.gemm.head_block0;
-                    if (C.gemm.mode == GM_FWD2) rb = (rb + SACX_FWD2_HEAD_NW / 4 - 1) / (SACX_FWD2_HEAD_NW / 4);
+                    if (C.gemm.mode == GM_FWD2) {
+                        // k_fwd2's head workgroups hold NW / 4 groups of 4 rows; the ticketed alpha
+                        // path needs the alpha rows to start a workgroup (its group 0 initialises the
+                        // ticket flags and no group of an alpha workgroup may take the early return)
+                        if ((r0 / 4 - C.gemm.head_block0) % (SACX_FWD2_HEAD_NW / 4) != 0) return false;
+                        rb = (rb + SACX_FWD2_HEAD_NW / 4 - 1) / (SACX_FWD2_HEAD_NW / 4);
+                    }
                     C.grid += rb - C.gemm.row_blocks;
                     C.gemm.row_blocks = rb;
                 }
@@ -1936,7 +1942,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
 // -- with the alpha branch of the previous speculative update (slot `prev`, -1: none) folded in
 // and the update's own alpha branch left out (deferred to the next one, or to settle()).
 int get_spec_graph(sacx_handle* h, int slot, int prev, hipGraphExec_t* out) {
-    const auto key = std::make_tuple(1, 16 + 64 * slot + (prev + 1), -1);
+    const auto key = std::make_tuple(-1, 64 * slot + (prev + 1), -1);   // < 0: never a get_graph key
     auto it = h->graphs.find(key);
     if (it != h->graphs.end()) {
         *out = it->second;
@@ -1982,7 +1988,8 @@ int get_spec_graph(sacx_handle* h, int slot, int prev, hipGraphExec_t* out) {
 // branch, ends the call).
 int get_seg_graph(sacx_handle* h, int s0, int n, bool has_prev, bool is_last, hipGraphExec_t* out) {
     const int nslot = h->nslot;
-    const auto key = std::make_tuple(4, (s0 % nslot) * 1024 + n, (has_prev ? 2 : 0) + (is_last ? 1 : 0));
+    // (first element -4: get_graph's keys start with G > 0, so a segment never replays a G-update graph)
+    const auto key = std::make_tuple(-4, (s0 % nslot) * 1024 + n, (has_prev ? 2 : 0) + (is_last ? 1 : 0));
     auto it = h->graphs.find(key);
     if (it != h->graphs.end()) {
         *out = it->second;
@@ -2140,7 +2147,7 @@ int step_graph_list(sacx_handle* h, int64_t n_steps, bool ext, std::vector<std::
     if (r == 0) return 0;
     int n_rem = 0;
     for (const auto& kv : h->graphs)
-        if (std::get<0>(kv.first) != h->graph_steps && std::get<2>(kv.first) < 0) ++n_rem;
+        if (std::get<0>(kv.first) > 0 && std::get<0>(kv.first) != h->graph_steps && std::get<2>(kv.first) < 0) ++n_rem;
     const bool exact = h->graphs.count(std::make_tuple((int)r, ext ? 0 : 1, -1)) > 0 || n_rem < kMaxRemGraphs;
     if (exact) {
         hipGraphExec_t g;
@@ -2931,20 +2938,31 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
     int32_t* ring = h->ptr<int32_t>("mfit.idx");
     // every step's launches read their minibatch rows from the index ring at ctl->mfit_seq, so a
     // graph of several steps replays them back to back (one graph launch per MFIT_GRAPH steps)
-    auto graph_of = [&](int n) -> hipGraphExec_t {
+    // (every HIP failure is reported with its error text; the capture is ended and the captured graph
+    // destroyed on every exit path, so a failed capture leaves the stream usable for the next fit)
+    auto graph_of = [&](int n, hipGraphExec_t* out) -> int {
         auto it = h->mgraphs[k].find(n);
-        if (it != h->mgraphs[k].end()) return it->second;
-        hipGraphExec_t ex = nullptr;
-        if (hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return nullptr;
+        if (it != h->mgraphs[k].end()) {
+            *out = it->second;
+            return 0;
+        }
+        HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
         for (int j = 0; j < n; ++j)
             for (const Launch& L : mplan) enqueue(L, h, h->cap_stream);
-        hipGraph_t graph;
-        if (hipStreamEndCapture(h->cap_stream, &graph) != hipSuccess) return nullptr;
-        const hipError_t e = hipGraphInstantiateWithFlags(&ex, graph, 0);
+        const hipError_t le = hipGetLastError();
+        hipGraph_t graph = nullptr;
+        const hipError_t ee = hipStreamEndCapture(h->cap_stream, &graph);
+        if (le != hipSuccess || ee != hipSuccess) {
+            if (graph) (void)hipGraphDestroy(graph);
+            return fail(h, std::string("model-fit graph capture: ") + hipGetErrorString(le != hipSuccess ? le : ee));
+        }
+        hipGraphExec_t ex = nullptr;
+        const hipError_t ie = hipGraphInstantiateWithFlags(&ex, graph, 0);
         (void)hipGraphDestroy(graph);
-        if (e != hipSuccess) return nullptr;
+        if (ie != hipSuccess) return fail(h, std::string("model-fit graph instantiate: ") + hipGetErrorString(ie));
         h->mgraphs[k][n] = ex;
-        return ex;
+        *out = ex;
+        return 0;
     };
     for (int64_t done = 0; done < n_steps;) {
         const int64_t chunk = std::min<int64_t>(n_steps - done, h->mfit_cap);
@@ -2963,8 +2981,8 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
         } else {
             for (int64_t j = 0; j < chunk;) {
                 const int n = chunk - j >= MFIT_GRAPH ? MFIT_GRAPH : chunk - j >= 8 ? 8 : 1;
-                hipGraphExec_t ex = graph_of(n);
-                if (!ex) return fail(h, "model-fit graph capture");
+                hipGraphExec_t ex = nullptr;
+                if (graph_of(n, &ex)) return -1;
                 HIPCHK(h, hipGraphLaunch(ex, h->stream));
                 j += n;
             }

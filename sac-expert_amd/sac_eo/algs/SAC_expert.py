@@ -34,8 +34,10 @@ class SAC_exp(SACBase):
                          mf_update_kwargs)
         if self.env_buffer_size:
             # the world models fit the last model_buffer_size rows of the replay ring; a smaller ring
-            # would have dropped some of them by the time the run holds that many rows
-            most = max(self.total_timesteps, self.env_batch_size_init)
+            # would have dropped some of them by the time the run holds that many rows.  Collection
+            # overshoots total_timesteps by up to one trajectory, so the bound is the one an unbounded
+            # ring is sized by (base.py _capacity)
+            most = self.total_timesteps + self.env_batch_size_init + self.env_horizon
             if int(self.env_buffer_size) < min(self.model_buffer_size, most):
                 raise NotImplementedError(
                     f"--model_buffer_size {self.model_buffer_size} larger than --env_buffer_size "

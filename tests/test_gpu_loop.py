@@ -116,6 +116,9 @@ def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
                     init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(MH, MH),
                     model_act="relu", lr_model=ak["model_lr"])
     st = _oracle_state(alg_obj, ocfg)
+    # the fp32 envelope starts from the SAME initial state: sac_update / model_fit_step advance
+    # the state they are given in place, so it is copied before the fp64 run trains st
+    st32 = st.astype(np.float32) if fp32_envelope else None
     expert = None
     if alg == "sac_imit":
         ex = alg_obj.expert.get_weights()
@@ -141,7 +144,7 @@ def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
         # the drift a faithful fp32 execution has: the same loop in fp32 against the fp64 one
         e32 = _fresh_envs(shape)
         ex32 = None if expert is None else ([w.astype(np.float32) for w in expert[0]], expert[1].astype(np.float32))
-        o32 = LoopOracle(alg, ocfg, st.astype(np.float32), e32[0], e32[2], ex32, ok, rs_state, ak["alg_seed"],
+        o32 = LoopOracle(alg, ocfg, st32, e32[0], e32[2], ex32, ok, rs_state, ak["alg_seed"],
                          max_episode_steps=1000).train(total)
         r32 = np.array([[u["q1_loss"], u["q2_loss"], u["p_loss"], u["alpha_loss"]] for u in o32.update_stats])
         env32 = [_series_err(r32[:, c], ref[:, c]) for c in range(4)]
@@ -152,9 +155,10 @@ def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
     return alg_obj, ak, name, dev, dev_rng, orc, ref, env32
 
 
-def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, env32=None):
-    """env32 (bench shapes): the diagnostics and fit losses may differ from the fp64 loop by what a
-    faithful fp32 execution of the same loop does (2x its drift), at least 1e-4 relative."""
+def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, tol=LOSS_TOL):
+    """``tol``: the bar for the per-episode expert diagnostics and last model-fit losses (relative to
+    each value): 1e-4 at the small shapes, 1e-3 at the bench shapes (three episodes of 300 updates
+    and 3 x 6 model-fit epochs of 512-wide nets between the diagnostics)."""
     assert len(dev_rng) == len(orc.episode_rng)
     for i, (a, b) in enumerate(zip(dev_rng, orc.episode_rng)):
         assert _same_stream(a, b), f"global stream differs at episode boundary {i}"
@@ -176,8 +180,7 @@ def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, env32=No
         dc = np.asarray(log["train"]["model_MSE_on_expert_counterfactual_action"], np.float64)
         od = np.array(orc.diag)
         assert len(dd) == len(od)
-        tol_d = 1e-4 if env32 is None else max(1e-4, 2 * env32[4])
-        tol_f = 1e-4 if env32 is None else max(1e-4, 2 * env32[5])
+        tol_d = tol_f = tol
         print(f"diagnostics: rel err {_rel_drift(np.stack([dd, dc], 1), od[:, :2]):.2e} (tol {tol_d:.2e}), "
               f"fit loss {_rel_drift(np.asarray(log['train']['model_loss_last'], np.float64), np.array(orc.fit_last)):.2e} "
               f"(tol {tol_f:.2e})")
@@ -207,8 +210,7 @@ def test_train_loop_matches_oracle(gpu_available, alg, flags):
     print(f"{alg} {flags}: {dev.shape[0]} updates, errors q1 {errs[0]:.2e} q2 {errs[1]:.2e} p {errs[2]:.2e} "
           f"alpha {errs[3]:.2e}")
     _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc)
-    assert max(errs[:3]) < LOSS_TOL, errs
-    assert errs[3] < 10 * LOSS_TOL, errs
+    assert max(errs) < LOSS_TOL, errs            # all four series, alpha loss included
     alg_obj.engine.close()
 
 
@@ -221,18 +223,20 @@ def test_train_loop_matches_oracle(gpu_available, alg, flags):
 def test_train_loop_bench_config(gpu_available, alg, act, flags):
     """The loops at the metric's shapes (256x2, B = 256, 512x2 models, minibatch 200, three
     100-step episodes after a 400-step collection): the global stream bit for bit at every episode
-    boundary; every update's losses within 1e-4 relative over the first 100 updates and, over the
-    whole run, within the drift a faithful fp32 execution has (2x the fp32-vs-fp64 oracle error
-    + 1e-5 per series)."""
+    boundary; every update's four losses within 1e-4 relative over the first 100 updates (north_star)
+    and within 1e-3 over the whole run; the expert diagnostics and model-fit losses within 1e-3.
+
+    The drift of a faithful fp32 execution (the same oracle loop in fp32 from the same start against
+    the fp64 one) is printed beside the errors as a diagnostic, and must itself be small (< 1e-2):
+    an envelope that wide would mean the two oracle loops do not run the same loop."""
     alg_obj, ak, name, dev, dev_rng, orc, ref, env32 = _run(alg, flags, shape=BENCH, act=act, fp32_envelope=True)
     assert dev.shape[0] == ref.shape[0] >= 200, (dev.shape, ref.shape)
     head = [_series_err(dev[:100, c], ref[:100, c]) for c in range(4)]
     full = [_series_err(dev[:, c], ref[:, c]) for c in range(4)]
     print(f"{alg} {act} {flags}: {dev.shape[0]} updates; first 100: {['%.2e' % e for e in head]}; "
           f"all: {['%.2e' % e for e in full]}; fp32 oracle drift {['%.2e' % e for e in env32]}")
-    _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, env32)
-    assert max(head[:3]) < LOSS_TOL, head
-    assert head[3] < 10 * LOSS_TOL, head
-    for c in range(4):
-        assert full[c] <= 2 * env32[c] + 1e-5 or full[c] < LOSS_TOL, (c, full, env32)
+    assert max(env32) < 1e-2, ("fp32 oracle loop diverges from the fp64 one: mis-specified envelope", env32)
+    _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, tol=1e-3)
+    assert max(head) < LOSS_TOL, head
+    assert max(full) < 1e-3, full
     alg_obj.engine.close()

@@ -23,6 +23,7 @@ import numpy as np
 import pytest
 
 import sac_oracle as O
+from sac_eo import _native as N
 from helpers import load_learner, make_learner, make_pair, oracle_step
 
 pytestmark = pytest.mark.gpu
@@ -203,6 +204,32 @@ def test_short_graphs_equal_eager(gpu_available, monkeypatch, n, nslot):
             eng.step(n, eager=eager)
         eng.sync()
         outs.append((eng.stats(2 * n).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state()[1].copy()))
+        eng.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_segment_graphs_never_replay_timing_graphs(gpu_available):
+    """The graph cache holds the G-update graphs of sacx_time_graph (keyed by G and the skipped
+    kernel) beside the single-stream segment graphs of step(n); with graph_steps = 4 the 4-update
+    graph without the sampler once shared its key with step(2)'s first one-update segment, which then
+    replayed the timing graph.  A time_graph ablation, the arena restored, then step(2) == a fresh
+    engine's step(2), bit for bit."""
+    outs = []
+    for timed in (True, False):
+        eng, *_ = make_pair(act="relu", B=256, seed=33, graph_steps=4)
+        eng.rng_set_state(np.random.RandomState(14).get_state())
+        eng.sync()
+        if timed:
+            saved = eng.arena_all.clone()
+            eng.time_graph(1, "k_rng")
+            eng.sync()
+            eng.arena_all.copy_(saved)
+            eng.sync()
+            N.check(eng.lib.sacx_resync(eng.h), eng.h, "resync")    # the restored counters are authoritative
+        eng.step(2)
+        eng.sync()
+        outs.append((eng.stats(2).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state()[1].copy()))
         eng.close()
     for a, b in zip(*outs):
         assert np.array_equal(a, b)

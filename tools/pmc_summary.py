@@ -23,7 +23,7 @@ from collections import defaultdict
 
 def family(name):
     n = name.replace("void ", "")
-    m = re.search(r"sacx::(k_[a-z_]+)", n)
+    m = re.search(r"sacx::(k_[a-z_0-9]+)", n)      # (digits: k_fwd2 is not k_fwd)
     if not m:
         return None
     # k_gemm_head is k_gemm with the actor-head prologue, k_fwd2 two forward layers in one launch:
