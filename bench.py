@@ -497,17 +497,123 @@ def packed_leg(cfgd, config, rep, k, steps, with_roofline):
     return out
 
 
-def spawn_ranks(n):
-    """Runs this script as n ranks under torch.distributed.run (127.0.0.1 rendezvous) in a
-    child process; returns its exit status.  The parent never initialises the GPU."""
+def _ranks_cmd(n, argv):
     import socket
-    import subprocess
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(n):
+    """Runs this script as n ranks under torch.distributed.run (127.0.0.1 rendezvous) in a
+    child process; returns its exit status.  The parent never initialises the GPU."""
+    import subprocess
+    return subprocess.call(_ranks_cmd(n, sys.argv[1:]))
+
+
+DP_CHECK_UPDATES = 64
+
+
+def dp_check(cfgd, rep, n_check=DP_CHECK_UPDATES, n_time=512):
+    """Config C4 over RCCL (``--mode dpcheck``, run by the N > 1 bench as a child launch): one
+    learner over the ws ranks of a fresh RCCL group (sacx_dp_init: ncclAllReduce of the critic,
+    actor and alpha gradients inside the captured update graph), each rank sampling B / ws rows of
+    its own replica of the replay ring (identical rows and initial weights on every rank) from its
+    own stream.
+      1. ``n_check`` updates from host-drawn randoms (SACX_STEP_EXTERNAL_RANDOMS, each rank its own
+         RandomState): every rank's parameters, targets and Adam moments must be bit-identical
+         (sha256 over the arena's PARAM / STATE prefix, gathered), and equal, within 1e-4 relative
+         to each tensor's max, a single learner's updates on the concatenated B-row batches (rank 0
+         replays them with the gathered indices and noise);
+      2. ``n_time`` graph-replayed updates with the device samplers: updates/s of the one learner.
+    Returns rank 0's result dict (None elsewhere)."""
+    import hashlib
+    import torch
+    from sac_eo.common.seeding import derive_seeds
+    from sac_eo.engine import Engine
+    ws, rank, device = rep.world_size, rep.rank, rep.device
+    S, A, B = cfgd["S"], cfgd["A"], cfgd["B"]
+    if cfgd["use_expert"] or B % ws:
+        raise SystemExit("dpcheck: plain SAC configs with batch divisible by the GPU count")
+    Bl, N = B // ws, cfgd["buffer"]
+    shared = {k: int(v[0]) for k, v in derive_seeds(0, runs=1).items()}   # rows and weights of run 0
+    comm_ws = rep.dist.get_world_size() if rep.dist is not None else 1
+    uid = rep.broadcast_bytes(Engine.dp_unique_id() if rank == 0 else None)
+    eng = build_engine(cfgd, shared, device, dp=(uid, ws, rank), batch=Bl, weight_seed=shared["setup"])
+    rs = np.random.RandomState(7000 + rank)
+    idx_all, nz_all = [], []
+    for t in range(n_check):
+        idx = rs.randint(N, size=Bl)                          # buffers.py:136 on this rank's stream
+        nz = rs.normal(size=(3, Bl, A))                       # target, policy, alpha evaluate()
+        eng.v["slot0.idx"][0].copy_(torch.from_numpy(idx.astype(np.int32)))
+        eng.v["slot0.noise"][0][:3 * Bl * A].copy_(torch.from_numpy(nz.astype(np.float32).ravel()))
+        eng.step(1, num_timesteps=t, ts_increment=1, external=True)
+        idx_all.append(idx)
+        nz_all.append(nz)
+    eng.sync()
+    end = eng.segments["grad"]["offset"]                      # params, adam_m, adam_v (targets included)
+    digest = hashlib.sha256(eng.arena[:end].cpu().numpy().tobytes()).hexdigest()
+    mine = dict(digest=digest, idx=np.stack(idx_all), nz=np.stack(nz_all))
+    allr = [None] * ws
+    rep.dist.all_gather_object(allr, mine)
+    identical = all(r["digest"] == allr[0]["digest"] for r in allr)
+    dev_nets = {n: eng.get_net(n) for n in ("actor", "q0", "q1", "t0", "t1")}
+    dev_alpha = eng.alpha()
+    # timed: the device samplers, graph replays (every rank the same global update)
+    eng.step(16, num_timesteps=n_check, ts_increment=1)
+    eng.prepare(n_time)
+    rep.barrier()
+    t0 = time.perf_counter()
+    eng.step(n_time, num_timesteps=n_check + 16, ts_increment=1)
+    eng.sync()
+    el = rep.max_over_ranks(time.perf_counter() - t0)
+    eng.close()
+    rep.barrier()
+    if rank != 0:
+        return None
+    # the single learner on the concatenated batches (rank order: ranks' rows, then per draw)
+    one = build_engine(cfgd, shared, device, batch=B, weight_seed=shared["setup"])
+    for t in range(n_check):
+        idx = np.concatenate([r["idx"][t] for r in allr])
+        nz = np.concatenate([r["nz"][t] for r in allr], axis=1)      # [3, B, A]
+        one.v["slot0.idx"][0].copy_(torch.from_numpy(idx.astype(np.int32)))
+        one.v["slot0.noise"][0][:3 * B * A].copy_(torch.from_numpy(nz.astype(np.float32).ravel()))
+        one.step(1, num_timesteps=t, ts_increment=1, external=True)
+    one.sync()
+    worst = 0.0
+    for n, ws_dev in dev_nets.items():
+        for a_, b_ in zip(ws_dev, one.get_net(n)):
+            worst = max(worst, float(np.max(np.abs(a_ - b_)) / max(float(np.max(np.abs(b_))), 1e-30)))
+    d_alpha = abs(dev_alpha - one.alpha()) / max(abs(one.alpha()), 1e-5)
+    one.close()
+    return {"ranks": ws, "rccl_world_size": comm_ws, "backend": rep.backend, "local_batch": Bl,
+            "checked_updates": n_check, "dp_ranks_identical": identical,
+            "vs_single_learner_max_rel_err": worst, "alpha_rel_err": d_alpha,
+            "matches_single_learner": bool(worst < 1e-4 and d_alpha < 1e-4),
+            "timed_updates": n_time, "updates_per_s": round(n_time / el, 2),
+            "ms_per_update": round(el / n_time * 1e3, 4),
+            "note": "one learner over the ranks (strong scaling); 3 RCCL all-reduces per update inside the graph"}
+
+
+def run_dp_child(ws, config, timeout=420):
+    """The C4 leg of an N > 1 bench: a fresh ws-rank launch of ``--mode dpcheck`` (its own RCCL
+    group), started by rank 0 after every replica rank has released its GPU; a hang or failure of
+    the leg costs only its own entry, never the replicas line."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID") and not k.startswith("TORCHELASTIC")}
+    cmd = _ranks_cmd(ws, ["--mode", "dpcheck", "--gpus", str(ws), "--config", config])
+    try:
+        out = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=ROOT)
+    except subprocess.TimeoutExpired:
+        return {"ranks": ws, "error": f"timed out after {timeout} s"}
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    if out.returncode != 0 or not lines:
+        return {"ranks": ws, "error": f"exit {out.returncode}", "stderr_tail": out.stderr[-800:]}
+    return json.loads(lines[-1]).get("dp_c4")
 
 
 def plan_only(args):
@@ -516,14 +622,22 @@ def plan_only(args):
     line with every rank's entry (tests/test_replicas.py checks it for --gpus 2)."""
     from sac_eo.common.replicas import init_replica
     rep = init_replica(backend="gloo", use_cuda=False)
-    mine = {"rank": rep.rank, "world_size": rep.world_size, "seeds": replica_seeds(rep, args.seeds_per_gpu)}
+    mine = {"rank": rep.rank, "world_size": rep.world_size, "seeds": replica_seeds(rep, args.seeds_per_gpu),
+            "group_world_size": rep.dist.get_world_size() if rep.dist is not None else 1,
+            "backend_on_gpus": "nccl (RCCL)"}
     if rep.dist is not None:
         allr = [None] * rep.world_size
         rep.dist.all_gather_object(allr, mine)
     else:
         allr = [mine]
     if rep.rank == 0:
-        print(json.dumps({"plan_only": True, "n_gpus": args.gpus, "ranks": allr}), flush=True)
+        # the N > 1 line's C4 leg: a fresh launch of --mode dpcheck over all the ranks' GPUs
+        leg = None if args.gpus < 2 else {"ranks": args.gpus, "mode": "dpcheck",
+                                          "checked_updates": DP_CHECK_UPDATES,
+                                          "fields": ["dp_ranks_identical", "vs_single_learner_max_rel_err",
+                                                     "rccl_world_size", "updates_per_s"]}
+        print(json.dumps({"plan_only": True, "n_gpus": args.gpus, "ranks": allr, "dp_c4_leg": leg,
+                          "line_fields_n_gt_1": ["rank_times_s", "group_world_size", "dp_c4"]}), flush=True)
     rep.close()
 
 
@@ -536,7 +650,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=16.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "dp"],
+    ap.add_argument("--mode", default="replicas", choices=["replicas", "dp", "dpcheck"],
                     help="replicas: one independent learner per GPU (the metric); dp: one learner, "
                          "global batch split over the GPUs, gradients all-reduced by RCCL (config C4)")
     ap.add_argument("--seeds-per-gpu", type=int, default=1,
@@ -545,6 +659,8 @@ def main():
     ap.add_argument("--packed-leg", type=int, default=-1,
                     help="after the timed region, also time K packed seeds per GPU and report them as "
                          "packed_seeds (default 8 for hc, 4 for the Humanoid configs; 0 = off)")
+    ap.add_argument("--no-dp-leg", action="store_true",
+                    help="N > 1: skip the C4 data-parallel RCCL leg (a child launch of --mode dpcheck)")
     ap.add_argument("--plan-only", action="store_true",
                     help="no GPU: every rank joins a gloo group and prints its rank and seeds (launch check)")
     args = ap.parse_args()
@@ -566,6 +682,12 @@ def main():
     rep = init_replica()                      # one learner per GPU, RCCL only for barrier / max time
     ws, rank, device = rep.world_size, rep.rank, rep.device
     cfgd = CONFIGS[args.config]
+    if args.mode == "dpcheck":
+        res = dp_check(cfgd, rep)
+        if rank == 0:
+            print(json.dumps({"dp_c4": res}), flush=True)
+        rep.close()
+        return
     dp = args.mode == "dp"
     if dp:
         from sac_eo.engine import Engine
@@ -592,6 +714,10 @@ def main():
     t1 = time.perf_counter()
     barrier()
     el = rep.max_over_ranks(t1 - t0)
+    rank_times = [t1 - t0]
+    if rep.dist is not None:                  # every rank's own timed region
+        rank_times = [None] * ws
+        rep.dist.all_gather_object(rank_times, t1 - t0)
     stats = eng.stats(1)[0]
     finite = bool(np.all(np.isfinite(stats)))
     value = args.steps * (1 if dp else ws * K) / el     # dp: every rank runs the same global update
@@ -618,6 +744,25 @@ def main():
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline and not dp:
         cpu = cpu_baseline(cfgd, args.cpu_seconds)
+    group_ws = rep.dist.get_world_size() if rep.dist is not None else 1
+    dpres = None
+    if ws > 1 and not dp and not args.no_dp_leg:
+        # config C4 over RCCL: every replica rank releases its GPU, rank 0 starts the ws-rank
+        # dpcheck launch (its own group), waits for it (bounded), then prints the line
+        import torch
+        if eng is not None:
+            eng.close()
+            eng = None
+        rep.barrier()
+        rep.close()
+        torch.cuda.empty_cache()
+        if rank != 0:
+            return
+        if torch.cuda.device_count() < ws:
+            dpres = {"ranks": ws, "skipped": f"{torch.cuda.device_count()} visible GPUs for {ws} ranks "
+                                               "(RCCL needs one GPU per rank)"}
+        else:
+            dpres = run_dp_child(ws, args.config)
     if rank == 0:
         line = {
             "metric": ("SAC" + ("-EO" if cfgd["use_expert"] else "") + " gradient-steps/sec ("
@@ -642,6 +787,11 @@ def main():
                 ["q1_loss", "q2_loss", "p_loss", "alpha_loss", "alpha", "mse_loss", "nlp_mean", "step"], stats)},
             "roofline": roof, "cpu_baseline": cpu,
         }
+        if ws > 1:
+            line["group_world_size"] = group_ws            # torch.distributed group the ranks joined
+            line["process_group_backend"] = rep.backend
+            line["rank_times_s"] = [round(float(x), 6) for x in rank_times]
+            line["dp_c4"] = dpres
         if fit is not None:
             line["model_fit"], line["rollout"] = fit, roll
         if mfit is not None:

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 6
+#define SACX_ABI_VERSION 7
 
 typedef struct sacx_handle sacx_handle;
 
@@ -112,6 +112,19 @@ typedef struct sacx_config {
                                    accumulate exactly as 16x16 ones, still by the packed row count), so
                                    each is bit-identical to its one-seed run (sac_eo.train --runs in
                                    lock-step); 0 = the packed plan (separate heads from 4 seeds: faster) */
+    /* --- ABI 7 --- */
+    int32_t gaussian_model;     /* --gaussian_model: GaussianModel world models (init_world_models.py:13-16):
+                                   a trainable logstd [1, S] per model after its net (segment m<k>.logstd,
+                                   continuous_models.py:24-27), the Gaussian NLL fit loss (:101-131), and
+                                   exp(logstd) * u noise in sample(deterministic=False) / step (:36-70) */
+    int32_t scale_model_loss;   /* --scale_model_loss: GaussianModel's loss times the stop-gradient
+                                   mean(exp(logstd)^2) (:122-127) */
+    int32_t separate_reward_nn; /* --separate_reward_nn (base_world_model.py:32-37): the model net has S
+                                   outputs and a reward net r<k> ([S+A] -> reward_hidden -> 1) predicts
+                                   the reward (:72-74), fitted in the same step */
+    int32_t reward_hidden[2];   /* --reward_layers (2 hidden layers; 0 -> 512) */
+    int32_t reward_act_layers[2]; /* --reward_activations per hidden layer (sacx_activation) */
+    int32_t critic_hidden[2];   /* --critic_layers when they differ from --actor_layers (0: = hidden) */
 } sacx_config;
 
 typedef struct sacx_segment {
@@ -246,10 +259,19 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
  * Requires use_expert. */
 int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n, float delta_clip,
                        float reward_clip, float* pred_out, float* sp_out, float* r_out);
+/* sacx_model_forward with GaussianModel's noise (continuous_models.py:36-70, ABI 7): stochastic != 0
+ * on a gaussian_model handle draws u = np.random.normal(size=(n, S)) from the device stream and
+ * adds exp(logstd) * u to the clipped delta_n before sp_out (GaussianModel.sample(deterministic=False)
+ * and .step); pred_out stays the mean.  stochastic = 0, or an MSEModel handle: sacx_model_forward. */
+int sacx_model_sample(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n,
+                      int32_t stochastic, float delta_clip, float reward_clip, float* pred_out, float* sp_out,
+                      float* r_out);
 /* MSEModel.get_loss (continuous_models.py:280-302) of world model `model` on s, sp [n,S],
  * a [n,A], r [n]: loss_out[0] = mean_i 0.5||clip(norm(sp-s)) - delta_pred||^2 +
  * reward_loss_coef * 0.5 (clip(norm(r)) - r_pred)^2, the clips > 0 being --delta_clip_loss /
- * --reward_clip_loss.  loss_out is device memory.  Requires use_expert. */
+ * --reward_clip_loss; on a gaussian_model handle GaussianModel.get_loss (:101-131), the delta
+ * term 0.5 sum_j (((norm(sp-s) - delta_pred) / e^l)^2 + 2 l + log 2 pi) (x mean(e^{2l}) with
+ * scale_model_loss).  loss_out is device memory.  Requires use_expert. */
 int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* sp, const float* a, const float* r,
                     int64_t n, float delta_clip_loss, float reward_clip_loss, float* loss_out);
 /* batch_simtrajectory_sampler (sac_eo/common/samplers.py:73-122) with world model `model`
@@ -259,8 +281,9 @@ int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* 
  * (uint8; always 0: MSEModel.step never terminates).  Per step t: a = sample(s_t) drawing
  * np.random.normal(size=(n, A)) from the device stream (nothing when deterministic);
  * (delta_n, r_n) = model([norm s_t, norm clip(a)]), clipped to +-delta_clip / +-reward_clip
- * when > 0 (--delta_clip_pred / --reward_clip_pred); s_{t+1} = s_t + delta_n*den + mean.
- * Requires use_expert (the models exist only then). */
+ * when > 0 (--delta_clip_pred / --reward_clip_pred); a GaussianModel (ABI 7) then draws
+ * normal(size=(n, S)) and adds exp(logstd) * u (GaussianModel.step, :36-54; n <= 4096);
+ * s_{t+1} = s_t + delta_n*den + mean.  Requires use_expert (the models exist only then). */
 int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, int32_t horizon,
                  int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
                  float* r_out, float* sp_out, uint8_t* d_out);
@@ -271,6 +294,8 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
  *   from the device stream), out[2..3] / out[4..5] = per model.
  * flags & SACX_DIAG_DISC: _calc_disc (:427-460): s_disc_i = ||sp_pred0 - sp_pred1||_2 on
  *   (s_e, counterfactual a); out[0] = sum, out[1] = max, out[2] = median, out[3 + i] = ratio.
+ *   The models sample with deterministic=False: GaussianModels draw normal(size=(n, S)) each,
+ *   model 0 then model 1, after the counterfactual action's draw (:437, :446).
  * flags & SACX_DIAG_EXPERT_ACTIONS (use_expert_actions): a_e replaces the counterfactual
  *   action (no draw; out[1] = out[0]).  delta_clip > 0: --delta_clip_pred.  out: device, >= 6
  *   floats (3 + n with DISC).  The adaptive epsilon of :383-418 is scalar host arithmetic. */

@@ -20,7 +20,9 @@ from the reference sources (all citations relative to noc-lab/sac-expert):
 * actor (+ expert term) and alpha   sac_eo/algs/SAC_expert.py:262-356 (SAC.py:178-217)
 * Polyak sync                       sac_eo/algs/SAC_expert.py:362-373
 * one gradient step                 sac_eo/algs/SAC_expert.py:463-477 (SAC.py:236-250)
-* world-model sample / loss         sac_eo/models/continuous_models.py:244-302
+* world-model sample / loss         sac_eo/models/continuous_models.py:244-302 (MSEModel),
+                                    :7-131 (GaussianModel), base_world_model.py:25-87
+                                    (--separate_reward_nn reward net)
 * model-fit step                    sac_eo/algs/mbrl_onpolicy_alg.py:301-319
 * Keras Adam (legacy OptimizerV2, epsilon-hat form, eps=1e-7)
 
@@ -69,6 +71,8 @@ class Config:
     act_limit: float = 1.0
     per_state_std: bool = False
     layer_norm: bool = False      # --actor_layer_norm: Dense -> LayerNorm -> tanh (nn_utils.py:110-119)
+    # --critic_layers when they differ from --actor_layers (`hidden`); None: `hidden`
+    critic_hidden: Optional[Sequence[int]] = None
     # per-hidden-layer activations (nn_utils.py:5-22); None: `act` for every layer
     actor_acts: Optional[Sequence[str]] = None
     critic_acts: Optional[Sequence[str]] = None
@@ -79,6 +83,16 @@ class Config:
     lr_model: float = 1e-3
     reward_loss_coef: float = 1.0
     delta_clip_pred: float = 0.0  # --delta_clip_pred (base_world_model.py:80-82); 0: None
+    # --gaussian_model (init_world_models.py:13-16): GaussianModel, a trainable logstd (1, S) per
+    # model (continuous_models.py:24-27), the Gaussian NLL fit loss (:101-131) with the optional
+    # --scale_model_loss stop-gradient scale mean(exp(logstd)^2) (:122-127), noise in sample / step
+    gaussian_model: bool = False
+    scale_model_loss: bool = False
+    # --separate_reward_nn (base_world_model.py:32-37): the model net predicts the S delta columns,
+    # a second net [S+A] -> reward_hidden -> 1 the reward (:72-74)
+    separate_reward_nn: bool = False
+    reward_hidden: Sequence[int] = (512, 512)
+    reward_act: str = "relu"
 
     @property
     def aacts(self):
@@ -87,6 +101,10 @@ class Config:
     @property
     def cacts(self):
         return tuple(self.critic_acts) if self.critic_acts else (self.act, self.act)
+
+    @property
+    def chidden(self):
+        return tuple(self.critic_hidden) if self.critic_hidden else tuple(self.hidden)
 
     @property
     def target_entropy(self) -> float:
@@ -146,6 +164,10 @@ class SACState:
     opt_alpha: AdamState
     models: Optional[List[List[np.ndarray]]] = None
     opt_model: Optional[AdamState] = None
+    # GaussianModel's logstd variable (1, S) per model (continuous_models.py:24-25)
+    model_logstd: Optional[List[np.ndarray]] = None
+    # --separate_reward_nn: the reward net's Keras weight list per model (base_world_model.py:36-37)
+    reward_nets: Optional[List[List[np.ndarray]]] = None
 
     def copy(self) -> "SACState":
         cp = lambda L: [x.copy() for x in L]
@@ -154,7 +176,9 @@ class SACState:
                         [cp(x) for x in self.q_targ], self.alpha.copy(), cpo(self.opt_actor),
                         [cpo(o) for o in self.opt_q], cpo(self.opt_alpha),
                         None if self.models is None else [cp(x) for x in self.models],
-                        None if self.opt_model is None else cpo(self.opt_model))
+                        None if self.opt_model is None else cpo(self.opt_model),
+                        None if self.model_logstd is None else cp(self.model_logstd),
+                        None if self.reward_nets is None else [cp(x) for x in self.reward_nets])
 
     def astype(self, dt) -> "SACState":
         c = lambda L: [np.asarray(x, dtype=dt).copy() for x in L]
@@ -163,7 +187,23 @@ class SACState:
                         [c(x) for x in self.q_targ], np.asarray(self.alpha, dt).copy(),
                         co(self.opt_actor), [co(o) for o in self.opt_q], co(self.opt_alpha),
                         None if self.models is None else [c(x) for x in self.models],
-                        None if self.opt_model is None else co(self.opt_model))
+                        None if self.opt_model is None else co(self.opt_model),
+                        None if self.model_logstd is None else c(self.model_logstd),
+                        None if self.reward_nets is None else [c(x) for x in self.reward_nets])
+
+    def model_vars(self, k: int) -> List[np.ndarray]:
+        """model.trainable (continuous_models.py:27-32, :216-221): the model net's variables,
+        GaussianModel's logstd, then the separate reward net's -- the model optimiser's order
+        (mbrl_onpolicy_alg.py:28-30 concatenates them over the models)."""
+        out = list(self.models[k])
+        if self.model_logstd is not None:
+            out.append(self.model_logstd[k])
+        if self.reward_nets is not None:
+            out += self.reward_nets[k]
+        return out
+
+    def model_all_vars(self) -> List[np.ndarray]:
+        return [w for k in range(len(self.models)) for w in self.model_vars(k)]
 
 
 # ---------------------------------------------------------------------------
@@ -194,7 +234,7 @@ def init_mlp(rng, in_dim: int, out_dim: int, hidden: Sequence[int], gain_final: 
 
 def init_state(cfg: Config, seed: int = 1, with_models: bool = False,
                bias_scale: float = 0.0, actor_gain: float = 0.01, critic_gain: float = 1.0,
-               model_gain: float = 0.01) -> SACState:
+               model_gain: float = 0.01, model_std_mult: float = 1.0, reward_gain: float = 0.01) -> SACState:
     rng = np.random.RandomState(seed)
     out_a = 2 * cfg.A if cfg.per_state_std else cfg.A
     actor = init_mlp(rng, cfg.S, out_a, cfg.hidden, actor_gain, bias_scale)
@@ -202,7 +242,7 @@ def init_state(cfg: Config, seed: int = 1, with_models: bool = False,
         H0 = cfg.hidden[0]
         actor = actor[:2] + [(1.0 + 0.1 * rng.normal(size=H0)).astype(np.float32),
                              (0.1 * rng.normal(size=H0)).astype(np.float32)] + actor[2:]
-    q = [init_mlp(rng, cfg.S + cfg.A, 1, cfg.hidden, critic_gain, bias_scale) for _ in range(2)]
+    q = [init_mlp(rng, cfg.S + cfg.A, 1, cfg.chidden, critic_gain, bias_scale) for _ in range(2)]
     q_targ = [[w.copy() for w in net] for net in q]         # init_critic.py:34-35
     logstd = np.zeros((1, cfg.A), np.float32)
     alpha = np.asarray(np.log(cfg.init_temperature), np.float32)  # SAC_expert.py:106
@@ -210,9 +250,17 @@ def init_state(cfg: Config, seed: int = 1, with_models: bool = False,
                   AdamState.zeros_like(actor + [logstd]),
                   [AdamState.zeros_like(n) for n in q], AdamState.zeros_like([alpha]))
     if with_models:
-        st.models = [init_mlp(rng, cfg.S + cfg.A, cfg.S + 1, cfg.model_hidden, model_gain, bias_scale)
+        om = cfg.S if cfg.separate_reward_nn else cfg.S + 1
+        st.models = [init_mlp(rng, cfg.S + cfg.A, om, cfg.model_hidden, model_gain, bias_scale)
                      for _ in range(2)]
-        st.opt_model = AdamState.zeros_like(st.models[0] + st.models[1])
+        if cfg.gaussian_model:           # np.ones((1, s_dim)) * np.log(std_mult) (continuous_models.py:24)
+            # (perturbed from the uniform init so that the tests see a per-column logstd)
+            st.model_logstd = [(np.ones((1, cfg.S)) * np.log(model_std_mult)
+                                + 0.05 * rng.normal(size=(1, cfg.S))).astype(np.float32) for _ in range(2)]
+        if cfg.separate_reward_nn:
+            st.reward_nets = [init_mlp(rng, cfg.S + cfg.A, 1, cfg.reward_hidden, reward_gain, bias_scale)
+                              for _ in range(2)]
+        st.opt_model = AdamState.zeros_like(st.model_all_vars())
     return st
 
 
@@ -562,7 +610,7 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
         ne_half = diffs[0].shape[0]
         for k, (se_n, hs_e, cache_e, xm, hsm, spe, sp_hat, dpass) in enumerate(caches):
             dsp = -eps * F(1.0 / ne_half) * diffs[k]
-            dout = np.zeros((ne_half, S + 1), dt)
+            dout = np.zeros((ne_half, om.shape[1]), dt)        # S + 1, or S with the separate reward net
             dout[:, :S] = dsp * mnrm.d_den * dpass
             if keep is not None:
                 keep["clip_frac%d" % k] = float(1.0 - dpass.mean())
@@ -618,14 +666,38 @@ def sac_update(st: SACState, cfg: Config, nrm: Normalizers, batch, noise_t, nois
 # world model: loss and one fitting step (continuous_models.py:280-302,
 # mbrl_onpolicy_alg.py:301-319)
 # ---------------------------------------------------------------------------
+def model_predict(st: SACState, cfg: Config, k: int, xm):
+    """BaseWorldModel._forward before its clips (base_world_model.py:65-78): the model net's delta
+    columns and the reward -- its last column, or the separate reward net's output (:72-74).
+    Returns (delta_n [n, S], r_n [n], (out, hs, rout, rhs)) with the caches of both nets."""
+    out, hs = mlp_forward(st.models[k], xm, cfg.model_act)
+    if cfg.separate_reward_nn:
+        ro, rhs = mlp_forward(st.reward_nets[k], xm, cfg.reward_act)
+        return out[:, :cfg.S], ro[:, 0], (out, hs, ro, rhs)
+    return out[:, :cfg.S], out[:, cfg.S], (out, hs, None, None)
+
+
+def model_entropy(st: SACState, cfg: Config, k: int) -> float:
+    """model.entropy's per-row value (logged as model_ent, SAC_expert.py:486-490): GaussianModel
+    0.5 sum(2 logstd + log 2 pi + 1) (continuous_models.py:162-166); MSEModel 0 (:321-323)."""
+    if not cfg.gaussian_model:
+        return 0.0
+    dt = st.alpha.dtype.type
+    l = np.asarray(st.model_logstd[k], dt)
+    return float(_F(dt, 0.5) * np.sum(_F(dt, 2) * l + _F(dt, np.log(np.float32(2 * np.pi))) + _F(dt, 1)))
+
+
 def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches, max_grad_norm=None,
                    delta_clip_loss=0.0, reward_clip_loss=0.0):
     """``batches`` = [(s, a, sp, r)] per model (independent minibatches,
     SAC_expert.py:519-543; one entry per world model).  Sum of the per-model mean losses
-    (get_loss with the optional target clips, continuous_models.py:284-296), the optional
+    (get_loss with the optional target clips: MSEModel continuous_models.py:280-302, GaussianModel
+    :101-131 -- 0.5 sum_j (((dn - mu) / e^l)^2 + 2 l + log 2 pi), times the stop-gradient
+    mean(e^{2l}) with --scale_model_loss, plus reward_loss_coef * 0.5 (rn - r_pred)^2, the reward from
+    the separate reward net with --separate_reward_nn), the optional
     clip_by_global_norm(grads, max_grad_norm * num_models) (mbrl_onpolicy_alg.py:315-317,
-    TF clip_ops: scale = clip * min(1 / norm, 1 / clip)), one Adam over all model variables.
-    Returns the summed loss."""
+    TF clip_ops: scale = clip * min(1 / norm, 1 / clip)), one Adam over all model variables in
+    model.trainable order (SACState.model_vars).  Returns the summed loss."""
     dt = st.alpha.dtype.type
     F = lambda x: _F(dt, x)
     nrm = nrm.cast(dt)
@@ -636,8 +708,7 @@ def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches, max_gra
         s, a, sp, r = [np.asarray(x, dt) for x in (s, a, sp, r)]
         n = s.shape[0]
         xm = np.concatenate([_norm(s, nrm.s_mean, nrm.s_den), _norm(a, nrm.a_mean, nrm.a_den)], 1)
-        out, hs = mlp_forward(st.models[k], xm, cfg.model_act)
-        dpred, rpred = out[:, :S], out[:, S]
+        dpred, rpred, (out, hs, ro, rhs) = model_predict(st, cfg, k, xm)
         dn = ((sp - s) - nrm.d_mean) / nrm.d_den
         rn = (r - nrm.r_mean) / nrm.r_den
         if delta_clip_loss:
@@ -646,22 +717,50 @@ def model_fit_step(st: SACState, cfg: Config, nrm: Normalizers, batches, max_gra
             rn = np.clip(rn, -F(reward_clip_loss), F(reward_clip_loss))
         ed = dn - dpred
         er = rn - rpred
-        per = F(0.5) * (ed * ed).sum(-1) + F(cfg.reward_loss_coef) * (F(0.5) * er * er)
+        g_l = None
+        if cfg.gaussian_model:
+            l = np.asarray(st.model_logstd[k], dt)
+            e = np.exp(l)
+            q = ed / e
+            dscale = np.mean(e * e) if cfg.scale_model_loss else F(1)     # tf.stop_gradient (:122-127)
+            nlp = F(0.5) * (q * q + F(2) * l + F(np.log(np.float32(2 * np.pi)))).sum(-1)
+            per = dscale * nlp + F(cfg.reward_loss_coef) * (F(0.5) * er * er)
+            dd = -(q / e) * (dscale * F(1.0 / n))
+            g_l = ((F(1) - q * q) * (dscale * F(1.0 / n))).sum(axis=0, keepdims=True)
+        else:
+            per = F(0.5) * (ed * ed).sum(-1) + F(cfg.reward_loss_coef) * (F(0.5) * er * er)
+            dd = -ed * F(1.0 / n)
+        dr = -er * F(cfg.reward_loss_coef / n)
         loss_all = loss_all + np.mean(per)
         dout = np.zeros_like(out)
-        dout[:, :S] = -ed * F(1.0 / n)
-        dout[:, S] = -er * F(cfg.reward_loss_coef / n)
+        dout[:, :S] = dd
+        if not cfg.separate_reward_nn:
+            dout[:, S] = dr
         g, _ = mlp_backward(st.models[k], xm, hs, dout, cfg.model_act)
         grads_all += g
+        if g_l is not None:
+            grads_all.append(g_l)
+        if cfg.separate_reward_nn:
+            gr, _ = mlp_backward(st.reward_nets[k], xm, rhs, dr[:, None], cfg.reward_act)
+            grads_all += gr
     nm = len(batches)
     if max_grad_norm:
         clip = F(max_grad_norm * nm)
         norm = np.sqrt(sum(np.sum(g * g) for g in grads_all)).astype(dt)
         scale = clip * np.minimum(F(1) / norm, F(1) / clip)
         grads_all = [g * scale for g in grads_all]
-    params = [w for k in range(nm) for w in st.models[k]]
+    params = [w for k in range(nm) for w in st.model_vars(k)]
     adam_step(params, grads_all, st.opt_model, cfg.lr_model, dt)
     return float(loss_all)
+
+
+def _model_noise(st, cfg, k, dn, u):
+    """GaussianModel.sample / step (continuous_models.py:36-70): delta_n + exp(logstd) * u, u the
+    global stream's normal(size=shape(delta_n)) cast to f32 (None: deterministic / MSEModel)."""
+    if u is None or not cfg.gaussian_model:
+        return dn
+    dt = dn.dtype.type
+    return dn + np.exp(np.asarray(st.model_logstd[k], dt)) * np.asarray(u, dt)
 
 
 # ---------------------------------------------------------------------------
@@ -678,7 +777,9 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
     = MSEModel.step: (delta_n, r_n) = _forward(s, clip(a)) with the optional prediction clips
     (base_world_model.py:65-87), s <- s + delta_rms.denormalize(delta_n), r =
     r_rms.denormalize(r_n), d = (ones_like(r) == 0) = False; the last step stores
-    d = terminated (all False).  ``mnrm``: the model's normaliser (None: ``nrm``)."""
+    d = terminated (all False).  A GaussianModel adds exp(logstd) * u to delta_n (u =
+    rs.normal(size=(n, S)) after the actor's draw, continuous_models.py:36-54).  ``mnrm``: the
+    model's normaliser (None: ``nrm``)."""
     dt = st.alpha.dtype.type
     F = lambda x: _F(dt, x)
     nrm = nrm.cast(dt)
@@ -696,12 +797,13 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
         a, _ = head_sample(mu, lraw, u, cfg.act_limit, dt)
         ac = np.clip(a, -lim, lim)                                # actor.clip (continuous_actors.py:125)
         xm = np.concatenate([_norm(s, mnrm.s_mean, mnrm.s_den), _norm(ac, mnrm.a_mean, mnrm.a_den)], 1)
-        pred, _ = mlp_forward(st.models[k], xm, cfg.model_act)
-        dn, rn = pred[:, :S], pred[:, S]
+        dn, rn, _ = model_predict(st, cfg, k, xm)
         if delta_clip:
             dn = np.clip(dn, -F(delta_clip), F(delta_clip))
         if reward_clip:
             rn = np.clip(rn, -F(reward_clip), F(reward_clip))
+        if cfg.gaussian_model:        # GaussianModel.step (continuous_models.py:36-54): always noisy
+            dn = _model_noise(st, cfg, k, dn, f32_noise(rs.normal(size=dn.shape)))
         sp = s + (dn * mnrm.d_den + mnrm.d_mean)
         r = rn * mnrm.r_den + mnrm.r_mean
         for key, v in (("s", s), ("a", a), ("r", r), ("sp", sp), ("d", np.zeros(n, bool))):
@@ -713,14 +815,16 @@ def rollout(st: SACState, cfg: Config, nrm: Normalizers, s_init, horizon: int, k
 # ---------------------------------------------------------------------------
 # expert diagnostics (A17 / F3): SAC_expert.py:579-608 and _calc_disc :427-460
 # ---------------------------------------------------------------------------
-def _model_sample(st, cfg, nrm, k, s, a, delta_clip=0.0):
-    """MSEModel.sample (continuous_models.py:244-254) with _forward(clip=True)."""
+def _model_sample(st, cfg, nrm, k, s, a, delta_clip=0.0, rs=None):
+    """MSEModel.sample (continuous_models.py:244-254) / GaussianModel.sample (:56-70) with
+    _forward(clip=True); ``rs``: deterministic=False (a GaussianModel draws normal(size=(n, S)))."""
     dt = st.alpha.dtype.type
     xm = np.concatenate([_norm(s, nrm.s_mean, nrm.s_den), _norm(a, nrm.a_mean, nrm.a_den)], 1)
-    out, _ = mlp_forward(st.models[k], xm, cfg.model_act)
-    dn = out[:, :cfg.S]
+    dn, _, _ = model_predict(st, cfg, k, xm)
     if delta_clip:
         dn = np.clip(dn, -_F(dt, delta_clip), _F(dt, delta_clip))
+    if rs is not None and cfg.gaussian_model:
+        dn = _model_noise(st, cfg, k, dn, f32_noise(rs.normal(size=dn.shape)))
     return s + (dn * nrm.d_den + nrm.d_mean)
 
 
@@ -756,13 +860,16 @@ def expert_mse_diag(st, cfg, nrm, s_e, a_e, sp_e, rs=None, use_expert_actions=Fa
 
 def calc_disc(st, cfg, nrm, s_e, a_e, rs=None, use_expert_actions=False, delta_clip=0.0, mnrm=None):
     """_calc_disc: (disc_ratio, max_disc, median_disc, s_disc_total) of the two models'
-    predictions on (s_e, a) with a = a_e or a fresh actor.sample(s_e) (tf_clip: a no-op)."""
+    predictions on (s_e, a) with a = a_e or a fresh actor.sample(s_e) (tf_clip: a no-op); the
+    models sample with deterministic=False (SAC_expert.py:437, :446: a GaussianModel draws its
+    noise, model 0 then model 1, after the actor's)."""
     dt = st.alpha.dtype.type
     nrm = nrm.cast(dt)
     mnrm = nrm if mnrm is None else mnrm.cast(dt)
     s_e = np.asarray(s_e, dt)
     a = np.asarray(a_e, dt) if use_expert_actions else _actor_sample(st, cfg, nrm, s_e, rs)
-    diff = _model_sample(st, cfg, mnrm, 0, s_e, a, delta_clip) - _model_sample(st, cfg, mnrm, 1, s_e, a, delta_clip)
+    p0 = _model_sample(st, cfg, mnrm, 0, s_e, a, delta_clip, rs=rs)
+    diff = p0 - _model_sample(st, cfg, mnrm, 1, s_e, a, delta_clip, rs=rs)
     s_disc = np.sqrt((diff * diff).sum(axis=1))
     tot = np.sum(s_disc)
     return s_disc / tot, float(np.max(s_disc)), float(np.median(s_disc)), float(tot)
@@ -814,26 +921,29 @@ def critic_forward(params, cfg, nrm, s, a, value=False):
     return out[:, 0] * _F(dt, nrm.ret_den) if value else out
 
 
-def model_forward(st, cfg, nrm, k, s, a, delta_clip=0.0, reward_clip=0.0):
+def model_forward(st, cfg, nrm, k, s, a, delta_clip=0.0, reward_clip=0.0, noise=None):
     """BaseWorldModel._forward with the prediction clips (base_world_model.py:65-87) and what
     MSEModel.sample / step make of it (continuous_models.py:225-254): (pred [n, S+1] after the
-    clips, sp = s + delta_rms.denormalize(delta_n), r = r_rms.denormalize(r_n))."""
+    clips, sp = s + delta_rms.denormalize(delta_n), r = r_rms.denormalize(r_n)).  ``noise`` [n, S]:
+    GaussianModel.sample(deterministic=False) / step (:36-70), exp(logstd) * u added to delta_n
+    after the clips (pred stays the mean)."""
     dt = st.alpha.dtype.type
     nrm = nrm.cast(dt)
     s, a = np.asarray(s, dt), np.asarray(a, dt)
     xm = np.concatenate([_norm(s, nrm.s_mean, nrm.s_den), _norm(a, nrm.a_mean, nrm.a_den)], 1)
-    out, _ = mlp_forward(st.models[k], xm, cfg.model_act)
-    dn, rn = out[:, :cfg.S].copy(), out[:, cfg.S].copy()
+    dn, rn, _ = model_predict(st, cfg, k, xm)
+    dn, rn = dn.copy(), rn.copy()
     if delta_clip:
         dn = np.clip(dn, -_F(dt, delta_clip), _F(dt, delta_clip))
     if reward_clip:
         rn = np.clip(rn, -_F(dt, reward_clip), _F(dt, reward_clip))
-    return (np.concatenate([dn, rn[:, None]], 1), s + (dn * nrm.d_den + nrm.d_mean), rn * nrm.r_den + nrm.r_mean)
+    dns = _model_noise(st, cfg, k, dn, None if noise is None else f32_noise(noise))
+    return (np.concatenate([dn, rn[:, None]], 1), s + (dns * nrm.d_den + nrm.d_mean), rn * nrm.r_den + nrm.r_mean)
 
 
 def model_loss(st, cfg, nrm, k, s, sp, a, r, delta_clip_loss=0.0, reward_clip_loss=0.0):
-    """MSEModel.get_loss (continuous_models.py:280-302): _forward(clip=False), the loss clips
-    on the normalised targets, mean over rows."""
+    """MSEModel.get_loss (continuous_models.py:280-302) / GaussianModel.get_loss (:101-131):
+    _forward(clip=False), the loss clips on the normalised targets, mean over rows."""
     dt = st.alpha.dtype.type
     nrm = nrm.cast(dt)
     s, sp, a, r = [np.asarray(x, dt) for x in (s, sp, a, r)]
@@ -844,8 +954,16 @@ def model_loss(st, cfg, nrm, k, s, sp, a, r, delta_clip_loss=0.0, reward_clip_lo
     rn = (r - nrm.r_mean) / nrm.r_den
     if reward_clip_loss:
         rn = np.clip(rn, -_F(dt, reward_clip_loss), _F(dt, reward_clip_loss))
-    per = _F(dt, 0.5) * ((dn - pred[:, :cfg.S]) ** 2).sum(-1) + _F(dt, cfg.reward_loss_coef) * (
-        _F(dt, 0.5) * (rn - pred[:, cfg.S]) ** 2)
+    ed = dn - pred[:, :cfg.S]
+    if cfg.gaussian_model:
+        l = np.asarray(st.model_logstd[k], dt)
+        e = np.exp(l)
+        q = ed / e
+        dscale = np.mean(e * e) if cfg.scale_model_loss else _F(dt, 1)
+        dl = dscale * (_F(dt, 0.5) * (q * q + _F(dt, 2) * l + _F(dt, np.log(np.float32(2 * np.pi)))).sum(-1))
+    else:
+        dl = _F(dt, 0.5) * (ed ** 2).sum(-1)
+    per = dl + _F(dt, cfg.reward_loss_coef) * (_F(dt, 0.5) * (rn - pred[:, cfg.S]) ** 2)
     return float(np.mean(per))
 
 

@@ -644,14 +644,35 @@ __device__ __forceinline__ void load_b(__amdgpu_buffer_rsrc_t rb, const GemmProb
 // (reduce_mean over its minibatch) into the stats ring, loss_all = their sum, and the optimiser
 // step / fit sequence advanced.  k_mfinal (one wave, per-row losses of k_mloss) or one extra
 // workgroup of a later launch of the step (256 threads, the fit-loss epilogue's tile partials).
-__device__ void mfit_final(const MFinalArgs& f) {
+// block sum of v over all threads (nw waves); every thread gets the result
+__device__ __forceinline__ float mfit_block_sum(float v, float* sh, int nw) {
+    v = wave_sum(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+    __syncthreads();
+    float a = sh[0];
+    for (int w = 1; w < nw; ++w) a += sh[w];
+    return a;
+}
+
+__device__ void mfit_final(const MFinalArgs& f, const AdamConsts* adam = nullptr, int64_t p_stride = 0) {
     __shared__ float mred[2][4];
+    __shared__ float lred[4];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
+    const int64_t t_model = f.ctl->t_model;      // read by every thread before thread 0 advances it
     const int n = f.nt > 0 ? f.mb * f.nt : f.mb;
     float s0 = 0.f, s1 = 0.f;
     for (int i = t; i < n; i += blockDim.x) {
         s0 += f.loss_rows[i];
         if (f.nm > 1) s1 += f.loss_rows[n + i];
+    }
+    if (f.nt2 > 0) {                             // the separate reward heads' partials
+        const int n2 = f.mb * f.nt2;
+        const float* r2 = f.loss_rows + (size_t)f.nm * n;
+        for (int i = t; i < n2; i += blockDim.x) {
+            s0 += r2[i];
+            if (f.nm > 1) s1 += r2[n2 + i];
+        }
     }
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
@@ -660,6 +681,34 @@ __device__ void mfit_final(const MFinalArgs& f) {
         mred[1][wave] = s1;
     }
     __syncthreads();
+    if (f.lgpart != nullptr && adam != nullptr) {
+        // GaussianModel's logstd (continuous_models.py:101-131): d loss / d l_j = (ds / mb) sum_i
+        // (1 - q_ij^2) from the fit epilogue's per-tile partials, then Keras Adam at the step this
+        // finalisation advances to (model.adam's t_adv), or the gradient stored for the global-norm clip
+        const int S = f.S;
+        const float lr_t = adam_lr(*adam, GRP_MODEL, t_model + 1);
+        for (int k = 0; k < f.nm; ++k) {
+            float* L = f.logstd[k];
+            float ds = 1.f;
+            if (f.lscale) {                      // tf.stop_gradient(reduce_mean(square(exp(logstd))))
+                float q = 0.f;
+                for (int j = t; j < S; j += blockDim.x) {
+                    const float e = expf(L[j]);
+                    q += e * e;
+                }
+                ds = mfit_block_sum(q, lred, nw) / (float)S;
+            }
+            __syncthreads();                     // every read of L before any update of it
+            const float* P = f.lgpart + (size_t)k * f.ntm * S;
+            for (int j = t; j < S; j += blockDim.x) {
+                float sum = 0.f;
+                for (int i = 0; i < f.ntm; ++i) sum += P[(size_t)i * S + j];
+                const float gr = sum * (ds / (float)f.mb);
+                if (f.gstore) L[j + 3 * p_stride] = gr;
+                else adam_update(L + j, L + j + p_stride, L + j + 2 * p_stride, gr, lr_t);
+            }
+        }
+    }
     if (t == 0) {
         float a0 = mred[0][0], a1 = mred[1][0];
         for (int w = 1; w < nw; ++w) {
@@ -674,7 +723,7 @@ __device__ void mfit_final(const MFinalArgs& f) {
         const int64_t seq = f.ctl->mfit_seq;
         f.mstats[(size_t)(seq % f.mstats_cap) * 2] = f.nm > 1 ? l0 + l1 : l0;     // loss_all (:305-312)
         f.mstats[(size_t)(seq % f.mstats_cap) * 2 + 1] = (float)seq;
-        f.ctl->t_model += 1;
+        f.ctl->t_model = t_model + 1;
         f.ctl->mfit_seq = seq + 1;
     }
 }
@@ -912,7 +961,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         if constexpr (MODE == GM_FWD) {
             e0[s] = g.bias[nnc];
             if constexpr (MSE) {   // launches with world-model head rows only (the registers cost occupancy)
-                e1[s] = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
+                e1[s] = bload(rs(g.se_raw), boff(g.mse != 0, mmc * ((g.mse & MSE_FIT) ? g.ldp : g.N) + nnc));
                 e2[s] = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
                 e3[s] = bload(rs(g.dmean), boff(g.mse != 0, nnc));
                 e4[s] = bload(rs(g.dden), boff(g.mse != 0, nnc));
@@ -1114,7 +1163,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         }
         if constexpr (MODE == GM_FWD && MSE) {
             if (g.mse) {          // uniform: the expert MSE / fit-loss epilogue (all 256 threads take part)
-                const bool fit = g.mse == 2;
+                const bool fit = (g.mse & MSE_FIT) != 0;
                 float pred = v + e0[s];
                 // --delta_clip_pred (base_world_model.py:80-82): clip, no gradient outside [-c, c]
                 const bool pass = g.dclip <= 0.f || (pred >= -g.dclip && pred <= g.dclip);
@@ -1122,7 +1171,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
                 const float sp_hat = e1[s] + (pred * e4[s] + e3[s]);
                 const float diff = fit ? e1[s] - pred : e2[s] - sp_hat;
                 const float gscale = -es.eps * g.grad_scale;
-                const float cf = (fit && nn == g.N - 1) ? g.fcoef : 1.f;     // the reward column
+                const float cf = (fit && !(g.mse & MSE_NOREW) && nn == g.N - 1) ? g.fcoef : 1.f;     // the reward column
                 float sq = out_ok ? diff * diff * cf : 0.f;
                 sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's sub-tile row
                 sq += __shfl_xor(sq, 4, 16);
@@ -1212,7 +1261,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         if constexpr (ROWK > 0 && ROWK < 3) {   // horizontally fused Q-head rows
             qhead_block<ROWK - 1, NQ>(ga.qh, tile - total_tiles, so);
         } else if constexpr (ROWK == 0 || ROWK == 7) {
-            if (ga.has_mfinal) mfit_final(ga.mfin);   // the world-model fit step's k_mfinal
+            if (ga.has_mfinal) mfit_final(ga.mfin, &ga.adam, ga.p_stride);   // the world-model fit step's k_mfinal
         }
         return;
     }
@@ -1288,8 +1337,11 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
         e0 = g.bias[nnc];
         if constexpr (ROWK == 8) {   // launches with world-model head rows (mse problems) only
             // world-model head rows (mse): zero-sized resources when not an mse problem
-            e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * g.N + nnc));
-            e2 = bload(rs(g.spe_raw), boff(g.mse != 0, mmc * g.N + nnc));
+            e1 = bload(rs(g.se_raw), boff(g.mse != 0, mmc * ((g.mse & MSE_FIT) ? g.ldp : g.N) + nnc));
+            // (MSE_GAUSS: the model's logstd of this column; none for the reward column)
+            const bool gl = (g.mse & MSE_GAUSS) != 0;
+            e2 = bload(rs(g.spe_raw), boff(g.mse != 0 && !(gl && !(g.mse & MSE_NOREW) && nnc == g.N - 1),
+                                           gl ? nnc : mmc * g.N + nnc));
             e3 = bload(rs(g.dmean), boff(g.mse != 0, nnc));
             e4 = bload(rs(g.dden), boff(g.mse != 0, nnc));
         }
@@ -1623,7 +1675,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     v = v + red[3][R][L];
     if constexpr (MODE == GM_FWD && ROWK == 8) {
         if (g.mse) {          // uniform: the expert MSE / fit-loss epilogue (all 256 threads take part)
-            const bool fit = g.mse == 2;
+            const bool fit = (g.mse & MSE_FIT) != 0;
             float pred = v + e0;
             // --delta_clip_pred (base_world_model.py:80-82): clip, no gradient outside [-c, c]
             const bool pass = g.dclip <= 0.f || (pred >= -g.dclip && pred <= g.dclip);
@@ -1631,15 +1683,51 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
             const float sp_hat = e1 + (pred * e4 + e3);
             const float diff = fit ? e1 - pred : e2 - sp_hat;
             const float gscale = -es.eps * g.grad_scale;
-            const float cf = (fit && nn == g.N - 1) ? g.fcoef : 1.f;     // the reward column
+            const bool rcl = fit && !(g.mse & MSE_NOREW) && nn == g.N - 1;
+            const float cf = rcl ? g.fcoef : 1.f;     // the reward column
             float sq = out_ok ? diff * diff * cf : 0.f;
+            float dout = fit ? -diff * (cf * g.grad_scale) : (pass ? (gscale * diff) * e4 : 0.f);
+            if (g.mse & MSE_GAUSS) {
+                // GaussianModel.get_loss (continuous_models.py:101-131) on the delta columns:
+                // q = (T - out) / e^l; loss ds (q^2 + 2 l + log 2 pi) (x 0.5 / mb in mfit_final);
+                // d / d out = -(q / e^l) ds / mb; d / d l = ds / mb (1 - q^2), summed over rows
+                __shared__ float lg_sh[4][16];
+                __shared__ float ds_sh[4];
+                const int Sd = (g.mse & MSE_NOREW) ? g.N : g.N - 1;     // the logstd columns
+                float ds = 1.f;
+                if (g.mse & MSE_SCALE) {     // --scale_model_loss: stop_gradient(mean(exp(logstd)^2)) (:122-127)
+                    const __amdgpu_buffer_rsrc_t rl = rs(g.spe_raw);
+                    float q2 = 0.f;
+                    for (int j = t; j < Sd; j += 256) {
+                        const float e = expf(bload(rl, (uint32_t)j * 4u));
+                        q2 += e * e;
+                    }
+                    q2 = wave_sum(q2);
+                    if ((t & 63) == 0) ds_sh[t >> 6] = q2;
+                    __syncthreads();
+                    ds = ((ds_sh[0] + ds_sh[1]) + (ds_sh[2] + ds_sh[3])) / (float)Sd;
+                }
+                float lg = 0.f;
+                if (!rcl) {
+                    const float el = expf(e2);
+                    const float q = diff / el;
+                    sq = out_ok ? ds * ((q * q + 2.f * e2) + LOG2PI_F) : 0.f;
+                    dout = -(q / el) * (ds * g.grad_scale);
+                    lg = out_ok ? 1.f - q * q : 0.f;
+                }
+                lg += __shfl_xor(lg, 16);      // the wave's 4 rows of this column
+                lg += __shfl_xor(lg, 32);
+                if ((t & 63) < 16) lg_sh[t >> 6][col] = lg;
+                __syncthreads();
+                if (t < 16 && n0 + t < Sd)
+                    st_out(&g.ppart[(size_t)tm * Sd + n0 + t], (lg_sh[0][t] + lg_sh[1][t]) + (lg_sh[2][t] + lg_sh[3][t]));
+            }
             sq += __shfl_xor(sq, 8, 16);   // the 16 columns of this thread's tile row
             sq += __shfl_xor(sq, 4, 16);
             sq += __shfl_xor(sq, 2, 16);
             sq += __shfl_xor(sq, 1, 16);
             if (!out_ok) return;
-            st_out(&g.C[(size_t)mm * g.ldc + nn],
-                   fit ? -diff * (cf * g.grad_scale) : (pass ? (gscale * diff) * e4 : 0.f));
+            st_out(&g.C[(size_t)mm * g.ldc + nn], dout);
             if (col == 0) st_out(&g.part[(size_t)mm * g.tiles_n + tn], sq);
             return;
         }
@@ -3858,6 +3946,8 @@ void launch_obs_norm(const float* obs, int64_t n, int S, const float* mean, cons
 __device__ __forceinline__ float diag_pred(const DiagArgs& g, int k, int i, int j) {
     float dn = g.O[((int64_t)k * g.n + i) * (g.S + 1) + j];
     if (g.clip_d > 0.f) dn = fminf(fmaxf(dn, -g.clip_d), g.clip_d);
+    if (g.mnoise != nullptr)        // GaussianModel.sample(deterministic=False) (continuous_models.py:60-62)
+        dn = dn + expf(g.mlogstd[k][j]) * g.mnoise[((int64_t)k * g.n + i) * g.S + j];
     return g.s_e[(int64_t)i * g.S + j] + (dn * g.d_den[j] + g.d_mean[j]);   // MSEModel.sample
 }
 
@@ -4056,6 +4146,8 @@ __global__ __launch_bounds__(256) void k_roll(RollArgs g) {
     for (int j = lane; j < S; j += 64) {
         float dn = Oi[j];
         if (g.clip_d > 0.f) dn = fminf(fmaxf(dn, -g.clip_d), g.clip_d);
+        if (g.mnoise != nullptr)    // GaussianModel.step (continuous_models.py:38-41)
+            dn = dn + expf(g.mlogstd[j]) * g.mnoise[(int64_t)i * S + j];
         const float sp = g.s_out[o * S + j] + (dn * g.d_den[j] + g.d_mean[j]);
         g.sp_out[o * S + j] = sp;
         if (g.t + 1 < g.H) g.s_out[(o + 1) * S + j] = sp;
@@ -4116,6 +4208,8 @@ __global__ __launch_bounds__(256) void k_net_io_rows(NetIOArgs g) {
             if (cl > 0.f) v = fminf(fmaxf(v, -cl), cl);
             if (g.out0 != nullptr) g.out0[i * O + j] = v;
             if (j < S) {
+                if (g.mnoise != nullptr)    // GaussianModel.sample(deterministic=False) / step (:36-70)
+                    v = v + expf(g.mlogstd[j]) * g.mnoise[i * S + j];
                 if (g.out1 != nullptr) g.out1[i * S + j] = g.s[i * S + j] + (v * g.d_den[j] + g.d_mean[j]);
             } else if (g.out2 != nullptr) {
                 g.out2[i] = v * g.r_norm[1] + g.r_norm[0];
@@ -4124,7 +4218,17 @@ __global__ __launch_bounds__(256) void k_net_io_rows(NetIOArgs g) {
         return;
     }
     // mode 3: 0.5 ||clip(norm(sp - s)) - delta_pred||^2 + coef * 0.5 (clip(norm(r)) - r_pred)^2
+    // (GaussianModel: ds * 0.5 sum_j (((dn - pred) / e^l)^2 + 2 l + log 2 pi), continuous_models.py:111-129)
     __shared__ float part[4];
+    float ds = 1.f;
+    if (g.mlogstd != nullptr && g.lscale) {      // stop_gradient(reduce_mean(square(exp(logstd))))
+        float q2 = 0.f;
+        for (int j = lane; j < S; j += 64) {
+            const float e = expf(g.mlogstd[j]);
+            q2 += e * e;
+        }
+        ds = wave_sum(q2) / (float)S;
+    }
     float acc = 0.f;
     for (int64_t i = wave; i < g.n; i += 4) {
         const float* Oi = g.O + i * g.ldO;
@@ -4133,9 +4237,14 @@ __global__ __launch_bounds__(256) void k_net_io_rows(NetIOArgs g) {
             float dn = ((g.sp[i * S + j] - g.s[i * S + j]) - g.d_mean[j]) / g.d_den[j];
             if (g.clip_d > 0.f) dn = fminf(fmaxf(dn, -g.clip_d), g.clip_d);
             const float e = dn - Oi[j];
-            sq = sq + e * e;
+            if (g.mlogstd != nullptr) {
+                const float l = g.mlogstd[j], q = e / expf(l);
+                sq = sq + ((q * q + 2.f * l) + LOG2PI_F);
+            } else {
+                sq = sq + e * e;
+            }
         }
-        const float tot = wave_sum(sq);
+        const float tot = g.mlogstd != nullptr ? ds * wave_sum(sq) : wave_sum(sq);
         float rn = (g.r[i] - g.r_norm[0]) / g.r_norm[1];
         if (g.clip_r > 0.f) rn = fminf(fmaxf(rn, -g.clip_r), g.clip_r);
         const float er = rn - Oi[S];

@@ -117,6 +117,7 @@ struct sacx_handle {
     std::string err;
     // dims
     int S = 0, A = 0, H0 = 0, H1 = 0, B = 0, Aout = 0, ne = 0, Hm0 = 0, Hm1 = 0, ecap = 0;
+    int Hc0 = 0, Hc1 = 0;     // the critics' hidden sizes (--critic_layers; H0 / H1 are the actor's)
     int ldS = 0, ldQ = 0, stride = 0, Ra = 0, Rb = 0, n_norm = 0;
     // hidden-layer activations per net and layer (nn_utils.py:5-22 create_activations): actor,
     // critics, world models
@@ -124,6 +125,12 @@ struct sacx_handle {
     int64_t cap = 0;
     int graph_steps = 128, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
     int nm = 0;               // SAC-EO world models (--num_models: 1 or 2)
+    // world-model variants (ABI 7): GaussianModel (a logstd per model, the NLL fit loss, noise in
+    // sample / step) and --separate_reward_nn (a reward net r<k> beside each model net m<k>)
+    bool gm = false, srn = false, lscale = false;
+    int Om = 0;               // model-net outputs: S + 1 (the reward as the last column), or S (srn)
+    int Hr0 = 0, Hr1 = 0;     // the reward nets' hidden sizes (srn)
+    int racts[2] = {0, 0};    // their hidden-layer activations
     bool ln = false;          // --actor_layer_norm: Dense -> LayerNorm -> tanh on the actor's layer 0
     // layout
     std::vector<SegInfo> segs;
@@ -301,14 +308,21 @@ void build_layout(sacx_handle* h) {
     net("actor", S, h->Aout, SACX_ROLE_PARAM, H0, H1);
     if (h->ln) h->add("actor.ln", 2, H0, F, SACX_ROLE_PARAM);     // LayerNormalization gamma ; beta
     h->add("actor.logstd", 1, A, F, SACX_ROLE_PARAM);
-    net("q0", S + A, 1, SACX_ROLE_PARAM, H0, H1);
-    net("q1", S + A, 1, SACX_ROLE_PARAM, H0, H1);
-    net("t0", S + A, 1, SACX_ROLE_TARGET, H0, H1);
-    net("t1", S + A, 1, SACX_ROLE_TARGET, H0, H1);
+    const int Hc0 = h->Hc0, Hc1 = h->Hc1;      // the critics' (--critic_layers)
+    net("q0", S + A, 1, SACX_ROLE_PARAM, Hc0, Hc1);
+    net("q1", S + A, 1, SACX_ROLE_PARAM, Hc0, Hc1);
+    net("t0", S + A, 1, SACX_ROLE_TARGET, Hc0, Hc1);
+    net("t1", S + A, 1, SACX_ROLE_TARGET, Hc0, Hc1);
     h->add("alpha", 1, 1, F, SACX_ROLE_PARAM);
     if (h->cfg.use_expert) {
-        net("m0", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
-        if (h->nm > 1) net("m1", S + A, S + 1, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
+        // per model, in model.trainable order (continuous_models.py:27-32, :216-221): the model net,
+        // GaussianModel's logstd, the separate reward net -- one contiguous range (the global-norm clip)
+        for (int k = 0; k < h->nm; ++k) {
+            const std::string m = "m" + std::to_string(k);
+            net(m, S + A, h->Om, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
+            if (h->gm) h->add(m + ".logstd", 1, S, F, SACX_ROLE_PARAM);
+            if (h->srn) net("r" + std::to_string(k), S + A, 1, SACX_ROLE_PARAM, h->Hr0, h->Hr1);
+        }
     }
     const uint64_t pbytes = (h->arena_bytes + 255) & ~uint64_t(255);
     h->param_off = 0;
@@ -333,9 +347,10 @@ void build_layout(sacx_handle* h) {
     if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 2)) {
         const char* nets[] = {"actor", "q0", "q1", "t0", "t1"};
         for (const char* n : nets) {
-            const int in = std::string(n) == "actor" ? S : S + A;
+            const bool act = std::string(n) == "actor";
+            const int in = act ? S : S + A, h0 = act ? H0 : Hc0, h1 = act ? H1 : Hc1;
             for (int l = 0; l < 2; ++l) {
-                const int K = l == 0 ? in : H0, N = l == 0 ? H0 : H1;
+                const int K = l == 0 ? in : h0, N = l == 0 ? h0 : h1;
                 const std::string w = std::string(n) + ".l" + std::to_string(l);
                 h->add("wbf." + w, N, wbf_ld_of(K) / 2, SACX_U32, SACX_ROLE_WORK);
                 h->wbf_mats.push_back({w, K, N});
@@ -424,18 +439,18 @@ void build_layout(sacx_handle* h) {
     h->add("ws.nlp_t", 1, B, F, 0);
     h->add("ws.nlp_p", 1, B, F, 0);
     h->add("ws.nlp3", 1, B, F, 0);
-    h->add("ws.Hq1", 4 * B, H0, F, 0);
-    h->add("ws.Hq2", 4 * B, H1, F, 0);
-    h->add("ws.Dq2", 2 * B, H1, F, 0);
-    h->add("ws.Dq1", 2 * B, H0, F, 0);
+    h->add("ws.Hq1", 4 * B, Hc0, F, 0);
+    h->add("ws.Hq2", 4 * B, Hc1, F, 0);
+    h->add("ws.Dq2", 2 * B, Hc1, F, 0);
+    h->add("ws.Dq1", 2 * B, Hc0, F, 0);
     h->add("ws.gq", 2, B, F, 0);
     h->add("ws.lq", 2, B, F, 0);
-    h->add("ws.Hp1", 2 * B, H0, F, 0);
-    h->add("ws.Hp2", 2 * B, H1, F, 0);
-    h->add("ws.Dp1", 2 * B, H0, F, 0);
+    h->add("ws.Hp1", 2 * B, Hc0, F, 0);
+    h->add("ws.Hp2", 2 * B, Hc1, F, 0);
+    h->add("ws.Dp1", 2 * B, Hc0, F, 0);
     h->add("ws.lp", 1, B, F, 0);
     h->add("ws.gp", 2, B, F, 0);                 // policy-row output gradients of q0, q1
-    h->add("ws.apart", 2 * B, ((H0 + 15) / 16) * A, F, 0);   // their action-gradient partials (folded head bwd)
+    h->add("ws.apart", 2 * B, ((Hc0 + 15) / 16) * A, F, 0);  // their action-gradient partials (folded head bwd)
     h->add("ws.mpart", ne1, ((Hm0 + 15) / 16) * A, F, 0);       // the expert rows' ones (SAC-EO, model.bwd1)
     h->add("ws.ones", 1, std::max(std::max(Rb, B), std::max(1, h->mb)) + 4, F, SACX_ROLE_STATE);
     h->add("ws.Hm1", ne1, Hm0, F, 0);
@@ -454,16 +469,19 @@ void build_layout(sacx_handle* h) {
     // (H0 a multiple of 128: every shadow position holds a k < H0; not under the layer norm,
     // which rewrites the actor's layer-0 output after the GEMM)
     h->abf_segs.clear();
-    if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 3) && H0 % 128 == 0 && !h->ln)
+    if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 3))
         for (const char* n : {"ws.Ha1", "ws.Hq1", "ws.Hp1"}) {
+            const bool act = std::string(n) == "ws.Ha1";
+            const int w = act ? H0 : Hc0;
+            if (w % 128 != 0 || (act && h->ln)) continue;
             const auto& sg = h->seg(n);
-            h->add(std::string("abf.") + n, sg.rows, H0 / 2, SACX_U32, SACX_ROLE_WORK);
+            h->add(std::string("abf.") + n, sg.rows, w / 2, SACX_U32, SACX_ROLE_WORK);
             h->abf_segs.push_back(n);
         }
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
-    h->add("act.H1", ACT_CAP, H0, F, 0);
-    h->add("act.H2", ACT_CAP, H1, F, 0);
+    h->add("act.H1", ACT_CAP, std::max(H0, Hc0), F, 0);   // (sacx_critic_forward's too)
+    h->add("act.H2", ACT_CAP, std::max(H1, Hc1), F, 0);
     h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
     if (h->ln) {                      // layer-norm caches of the update's actor rows
         h->add("ws.ln_xhat", h->Ra, H0, F, 0);
@@ -486,7 +504,22 @@ void build_layout(sacx_handle* h) {
         h->add("ws.Df3", R2, r4(O), F, 0);    // float4 rows: model.bwd2's A operand
         h->add("ws.Df2", R2, Hm1, F, 0);
         h->add("ws.Df1", R2, Hm0, F, 0);
-        h->add("ws.lf", 1, (int64_t)R2 * ((O + 15) / 16), F, 0);   // fit-loss partials (per row: k_mloss)
+        // fit-loss partials (per row: k_mloss); --separate_reward_nn: then one per row of the reward heads
+        h->add("ws.lf", 1, (int64_t)R2 * ((O + 15) / 16) + (h->srn ? R2 : 0), F, 0);
+        if (h->srn) {                 // the reward nets' fit activations / deltas
+            const int Hr0 = h->Hr0, Hr1 = h->Hr1;
+            h->add("ws.Hrf1", R2, Hr0, F, 0);
+            h->add("ws.Hrf2", R2, Hr1, F, 0);
+            h->add("ws.Drf3", R2, 4, F, 0);         // d loss / d reward (float4 rows)
+            h->add("ws.Drf2", R2, Hr1, F, 0);
+            h->add("ws.Drf1", R2, Hr0, F, 0);
+            h->add("roll.R1", ROLL_CAP, Hr0, F, 0);
+            h->add("roll.R2", ROLL_CAP, Hr1, F, 0);
+        }
+        if (h->gm) {                  // logstd-gradient partials per model, 16-row tile and column
+            h->add("ws.lgp", h->nm * ((h->mb + 15) / 16), S, F, 0);
+            h->add("roll.mnoise", 1, (int64_t)ROLL_CAP * S, F, 0);   // exp(logstd) * u noise (sample / step)
+        }
         // model rollout (sacx_rollout), up to ROLL_CAP trajectories per launch chain
         h->add("roll.X", ROLL_CAP, h->ldS, F, 0);
         h->add("roll.H1", ROLL_CAP, H0, F, 0);
@@ -818,6 +851,7 @@ void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string&
     for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
     const std::string base = G.name.substr(0, G.name.find(".adam"));
     G.name = base + ".grad";
+    const AdamConsts gadam = G.gemm.adam;       // (G dangles once the plan grows below)
     const uint64_t o0 = h->off_of(first);
     const SegInfo& sl = h->seg(last);
     const int64_t n = (int64_t)((sl.off + (uint64_t)(sl.rows * sl.cols) * 4 - o0) / 4);
@@ -838,7 +872,7 @@ void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string&
     a.t_off = targ.empty() ? 0 : (int64_t)(h->off_of(targ) - o0) / 4;
     a.grad_scale = (float)(1.0 / (double)h->dp_ranks);
     a.ctl = h->ctl();
-    a.adam = G.gemm.adam;
+    a.adam = gadam;
     U.grid = (int)((n + 255) / 256);
     U.bytes = 4.0 * n * (targ.empty() ? 7 : 9);
     plan.push_back(U);
@@ -850,6 +884,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     h->probs_cursor = 0;
     const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
     const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
+    const int Hc0 = h->Hc0, Hc1 = h->Hc1;   // the critics' hidden sizes (--critic_layers; H0 / H1: the actor's)
     // expert rows of world model k: [k * half, (k + 1) * half) with 2 models, all with one
     const int nm = h->nm, mrows = nm == 1 ? ne : half;
     const int ldS = h->ldS, ldQ = h->ldQ;
@@ -990,13 +1025,13 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // the row kernel): pi.q.bwd1 writes per-tile partial action gradients, actor.bwd1's tiles
     // finish them.  SACX_FOLD_HBW=0 keeps the separate launch (A/B measurement).
     const char* fhb = std::getenv("SACX_FOLD_HBW");
-    const int tq = (H0 + 15) / 16;
+    const int tq = (Hc0 + 15) / 16;        // action-gradient partials per row (the critics' layer-0 tiles)
     // The folded launch itself keeps 16x16 tiles (its prologue and generated A operand); the
     // partial-writing launches may take 32x32 tiles.  On 32x32 (packed) plans both folds are off
     // by default: there the launches are bound by workgroup residency, not by their number, and
     // the folds' extra work loses (HC 8 seeds, A/B x2: both on 42.3k, hbw fold only 43.4k, head
     // partials only 43.1k, both off 43.9k updates/s; tools/pk_ab.sh).
-    const bool fold_hbw = Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && H0 <= 256 && H0 % 64 == 0 &&
+    const bool fold_hbw = Aout <= 8 && H1 <= 256 && H1 % 16 == 0 && Hc0 <= 256 && Hc0 % 64 == 0 &&
                           (!eo || (Hm0 <= 512 && Hm0 % 64 == 0)) &&
                           (fhb ? std::atoi(fhb) != 0 : h->tile32_plan == 0);
     // ---- actor head
@@ -1054,9 +1089,9 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
-            GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, c0);
+            GemmProb q0 = prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), Hc0, Hq1 + (size_t)k * B * Hc0, c0);
             q0.headp = k < 2;
-            GemmProb q1 = prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, c1);
+            GemmProb q1 = prob_fwd(Hq1 + (size_t)k * B * Hc0, Hc0, B, Hc0, W(n + ".l1"), Hc1, Hq2 + (size_t)k * B * Hc1, c1);
             p0.push_back(q0);
             p1.push_back(q1);
         }
@@ -1083,8 +1118,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 4; ++k) {
             const std::string n = qn[k];
-            p0.push_back(prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), H0, Hq1 + (size_t)k * B * H0, c0));
-            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hq2 + (size_t)k * B * H1, c1));
+            p0.push_back(prob_fwd(k < 2 ? Xt : Xq, ldQ, B, S + A, W(n + ".l0"), Hc0, Hq1 + (size_t)k * B * Hc0, c0));
+            p1.push_back(prob_fwd(Hq1 + (size_t)k * B * Hc0, Hc0, B, Hc0, W(n + ".l1"), Hc1, Hq2 + (size_t)k * B * Hc1, c1));
         }
         if (eo) {
             for (int k = 0; k < nm; ++k) {
@@ -1103,7 +1138,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     // critic.adam applies g to layer 0 (row-scaled B).
     {
         QHeadArgs q{};
-        q.mode = 0; q.B = B; q.H1 = H1; q.H2 = Hq2;
+        q.mode = 0; q.B = B; q.H1 = Hc1; q.H2 = Hq2;
         for (int k = 0; k < 4; ++k) q.W3[k] = W(std::string(qn[k]) + ".l2");
         q.act = c1; q.D2 = Dq2; q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
         q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = r_in; q.d = d_in;
@@ -1114,8 +1149,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> pb;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
-            GemmProb p = prob_dx(Hq2 + (size_t)(2 + k) * B * H1, B, H1, W(n + ".l1"), H0,
-                                 Hq1 + (size_t)(2 + k) * B * H0, Dq1 + (size_t)k * B * H0, c0);
+            GemmProb p = prob_dx(Hq2 + (size_t)(2 + k) * B * Hc1, B, Hc1, W(n + ".l1"), Hc0,
+                                 Hq1 + (size_t)(2 + k) * B * Hc0, Dq1 + (size_t)k * B * Hc0, c0);
             p.wgen = W(n + ".l2");             // w3 column of W3_ext
             p.gen_act = c1;                    // act'(Hq2); the epilogue takes act'(Hq1)
             pb.push_back(p);
@@ -1126,17 +1161,17 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.gemm.row_blocks = (B + 3) / 4;
         L.gemm.qh = q;
         L.grid += L.gemm.row_blocks;
-        L.flops += 2.0 * B * H1 * 4 + 2.0 * B * H1 * 2;
-        L.bytes += 4.0 * (4.0 * B * H1 + 2.0 * B * H1 * 2);
+        L.flops += 2.0 * B * Hc1 * 4 + 2.0 * B * Hc1 * 2;
+        L.bytes += 4.0 * (4.0 * B * Hc1 + 2.0 * B * Hc1 * 2);
         std::vector<GemmProb> pw;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k), t = "t" + std::to_string(k);
-            GemmProb p0 = prob_dw(Xq, ldQ, S + A, B, Dq1 + (size_t)k * B * H0, H0, W(n + ".l0"), W(t + ".l0"), GRP_Q);
+            GemmProb p0 = prob_dw(Xq, ldQ, S + A, B, Dq1 + (size_t)k * B * Hc0, Hc0, W(n + ".l0"), W(t + ".l0"), GRP_Q);
             p0.bscale = W("ws.gq") + (size_t)k * B;   // Dq1 = g (.) M1
             pw.push_back(p0);
-            pw.push_back(prob_dw(Hq1 + (size_t)(2 + k) * B * H0, H0, H0, B, Dq2 + (size_t)k * B * H1, H1, W(n + ".l1"),
+            pw.push_back(prob_dw(Hq1 + (size_t)(2 + k) * B * Hc0, Hc0, Hc0, B, Dq2 + (size_t)k * B * Hc1, Hc1, W(n + ".l1"),
                                  W(t + ".l1"), GRP_Q));
-            pw.push_back(prob_dw(Hq2 + (size_t)(2 + k) * B * H1, H1, H1, B, W("ws.gq") + (size_t)k * B, 1,
+            pw.push_back(prob_dw(Hq2 + (size_t)(2 + k) * B * Hc1, Hc1, Hc1, B, W("ws.gq") + (size_t)k * B, 1,
                                  W(n + ".l2"), W(t + ".l2"), GRP_Q));
         }
         add_gemm(h, plan, "critic.adam", pw, record_probs, !fuse_head);
@@ -1166,21 +1201,21 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> p0, p1;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
-            p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), H0, Hp1 + (size_t)k * B * H0, c0));
-            p1.push_back(prob_fwd(Hp1 + (size_t)k * B * H0, H0, B, H0, W(n + ".l1"), H1, Hp2 + (size_t)k * B * H1, c1));
+            p0.push_back(prob_fwd(Xp, ldQ, B, S + A, W(n + ".l0"), Hc0, Hp1 + (size_t)k * B * Hc0, c0));
+            p1.push_back(prob_fwd(Hp1 + (size_t)k * B * Hc0, Hc0, B, Hc0, W(n + ".l1"), Hc1, Hp2 + (size_t)k * B * Hc1, c1));
         }
         // SAC-EO: world-model layer 2 on the expert rows + MSE epilogue (needs Hm2 from q.fwd1),
         // riding in the pi.q.fwd0 launch (a launch of its own when that one is fused)
         std::vector<GemmProb> pm;
-        const int O = S + 1, mtn = (S + 15) / 16;
+        const int mtn = (S + 15) / 16;
         if (eo) {
             for (int k = 0; k < nm; ++k) {
                 const std::string n = "m" + std::to_string(k);
                 GemmProb p{};
                 p.A = Hm2b + (size_t)k * half * Hm1; p.lda = Hm1; p.a_kc = 1; p.ones_row = -1;
-                p.B = W(n + ".l2"); p.ldb = O; p.b_kc = 0;           // W_ext [(Hm1+1) x (S+1)]
+                p.B = W(n + ".l2"); p.ldb = h->Om; p.b_kc = 0;       // W_ext [(Hm1+1) x Om], Om = S (+1)
                 p.M = mrows; p.N = S; p.K = Hm1;                     // delta-s columns only
-                p.bias = W(n + ".l2") + (size_t)Hm1 * O;
+                p.bias = W(n + ".l2") + (size_t)Hm1 * h->Om;
                 p.C = W("ws.dout") + (size_t)k * half * S; p.ldc = S;
                 p.epi = EPI_FWD; p.act = ACT_NONE;
                 p.mse = 1; p.grad_scale = 1.f / (float)mrows;       // MSE_loss = mean over the rows
@@ -1213,7 +1248,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             F0.bytes += one[0].bytes;
         }
         QHeadArgs q{};
-        q.mode = 1; q.B = B; q.H1 = H1; q.H2 = Hp2;
+        q.mode = 1; q.B = B; q.H1 = Hc1; q.H2 = Hp2;
         q.W3[0] = W("q0.l2"); q.W3[1] = W("q1.l2"); q.W3[2] = nullptr; q.W3[3] = nullptr;
         q.act = c1; q.D2 = nullptr; q.g = W("ws.gp"); q.loss_rows = W("ws.lp");
         q.alpha = W("alpha"); q.nlp = W("ws.nlp_p");
@@ -1223,8 +1258,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         std::vector<GemmProb> pb;
         for (int k = 0; k < 2; ++k) {
             const std::string n = "q" + std::to_string(k);
-            GemmProb p = prob_dx(Hp2 + (size_t)k * B * H1, B, H1, W(n + ".l1"), H0, Hp1 + (size_t)k * B * H0,
-                                 Dp1 + (size_t)k * B * H0, c0);
+            GemmProb p = prob_dx(Hp2 + (size_t)k * B * Hc1, B, Hc1, W(n + ".l1"), Hc0, Hp1 + (size_t)k * B * Hc0,
+                                 Dp1 + (size_t)k * B * Hc0, c0);
             p.wgen = W(n + ".l2");
             p.gen_act = c1;
             pb.push_back(p);
@@ -1234,15 +1269,15 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
                 const std::string n = "m" + std::to_string(k);
                 GemmProb p = prob_dx(W("ws.dout") + (size_t)k * half * S, mrows, S, W(n + ".l2"), Hm1,
                                      Hm2b + (size_t)k * half * Hm1, Dm2 + (size_t)k * half * Hm1, m1);
-                p.ldb = O;                           // B[n][k] = W_ext[n][k], row stride S+1
+                p.ldb = h->Om;                       // B[n][k] = W_ext[n][k], row stride Om
                 pb.push_back(p);
             }
         }
         if (fold_hbw) {                      // partial action gradients instead of Dp1 (read by no one else)
             for (int k = 0; k < 2; ++k) {
                 GemmProb& p = pb[k];
-                p.pw = W("q" + std::to_string(k) + ".l0") + (size_t)S * H0;   // action rows of W_ext
-                p.pw_ld = H0;
+                p.pw = W("q" + std::to_string(k) + ".l0") + (size_t)S * Hc0;   // action rows of W_ext
+                p.pw_ld = Hc0;
                 p.pw_cs = 1;
                 p.pw_n = A;
                 p.ppart = W("ws.apart") + (size_t)k * B * tq * A;
@@ -1256,8 +1291,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             L.gemm.row_blocks = (B + 3) / 4;
             L.gemm.qh = q;
             L.grid += L.gemm.row_blocks;
-            L.flops += 2.0 * B * H1 * 2 * 2;
-            L.bytes += 4.0 * (2.0 * B * H1 * 2);
+            L.flops += 2.0 * B * Hc1 * 2 * 2;
+            L.bytes += 4.0 * (2.0 * B * Hc1 * 2);
         }
         if (eo) {                            // Dm1 = Dm2 . Wm1^T (.) act'(Hm1), for actor.head.bwd
             std::vector<GemmProb> pd;
@@ -1302,7 +1337,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
         b.Da3 = Da3; b.E = E; b.Da2 = Da2;
         b.ne = ne; b.tqm = (Hm0 + 15) / 16; b.mpart = eo ? W("ws.mpart") : nullptr; b.ctl = eo ? h->ctl() : nullptr;
-        L.flops += 2.0 * B * 2 * H0 * A + 2.0 * Rb * H1 * Aout;
+        L.flops += 2.0 * B * 2 * Hc0 * A + 2.0 * Rb * H1 * Aout;
         L.bytes += 4.0 * (2.0 * B * tq * A + 2.0 * Rb * H1);
     }
     {
@@ -1310,7 +1345,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.kind = Launch::ABWD;
         L.name = "actor.head.bwd";
         ActorBwdArgs& b = L.ab;
-        b.B = B; b.ne = ne; b.S = S; b.A = A; b.Aout = Aout; b.H0 = H0; b.H1 = H1; b.Hm0 = Hm0;
+        b.B = B; b.ne = ne; b.S = S; b.A = A; b.Aout = Aout; b.H0 = Hc0; b.H1 = H1; b.Hm0 = Hm0;   // Dp1 / Wq1: critic
         b.per_state_std = h->cfg.per_state_std; b.lim = h->cfg.act_limit;
         b.Dp1 = Dp1; b.Wq1[0] = W("q0.l0"); b.Wq1[1] = W("q1.l0");
         b.Dm1 = Dm1; b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W(nm > 1 ? "m1.l0" : "m0.l0") : nullptr;
@@ -1321,8 +1356,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         b.Da3 = Da3; b.Da2 = Da2; b.E = E;
         b.gpol = W("ws.gp");
         L.grid = (h->Rb + 3) / 4;
-        L.flops = 2.0 * B * 2 * H0 * A + 2.0 * ne * Hm0 * A + 2.0 * h->Rb * H1 * Aout;
-        L.bytes = 4.0 * (2.0 * B * H0 + ne * Hm0 + 2.0 * h->Rb * H1);
+        L.flops = 2.0 * B * 2 * Hc0 * A + 2.0 * ne * Hm0 * A + 2.0 * h->Rb * H1 * Aout;
+        L.bytes = 4.0 * (2.0 * B * Hc0 + ne * Hm0 + 2.0 * h->Rb * H1);
         const int Rb = h->Rb;
         if (!fold_hbw) {
             plan.push_back(L);
@@ -1460,11 +1495,14 @@ void build_model_plan(sacx_handle* h) {
     const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ;
     const int m0 = h->macts[0], m1 = h->macts[1];
     const int nm = h->nm;
-    const bool fuse = h->mfuse != 0;
-    const int nt = (O + 15) / 16;     // fit-loss partials per row (16-column tiles of model.fwd2)
+    // GaussianModel / --separate_reward_nn fits exist only in the folded form (their loss epilogues)
+    const bool fuse = h->mfuse != 0 || h->gm || h->srn;
+    const int Om = h->Om;             // model-net outputs (S + 1, or S beside a reward net)
+    const int nt = (Om + 15) / 16;    // fit-loss partials per row (16-column tiles of model.fwd2)
     const int ldO = (int)r4(O);       // D3 row stride
+    const int ntm = (mb + 15) / 16;   // GaussianModel: logstd-gradient partials per column (row tiles)
     // model.bwd2 generated on model.bwd1's operand loads (rowk 7) for narrow heads (S + 1 <= 32)
-    const bool bfold = fuse && h->mfuse >= 3 && O <= 32 && h->mtile != 2 && h->unaligned_b;
+    const bool bfold = fuse && h->mfuse >= 3 && O <= 32 && h->mtile != 2 && h->unaligned_b && !h->gm && !h->srn;
     auto W = [&](const std::string& n) { return h->f(n); };
     float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Hf1 = W("ws.Hf1"), *Hf2 = W("ws.Hf2"), *Of = W("ws.Of");
     float *Df3 = W("ws.Df3"), *Df2 = W("ws.Df2"), *Df1 = W("ws.Df1");
@@ -1475,8 +1513,9 @@ void build_model_plan(sacx_handle* h) {
     mg.a_den = W("mnorm.a_den"); mg.d_mean = W("mnorm.d_mean"); mg.d_den = W("mnorm.d_den"); mg.r_norm = W("mnorm.r");
     mg.X = Xf; mg.ldQ = ldQ; mg.T = Tf; mg.nm = nm;
     mg.clip_d = h->cfg.delta_clip_loss; mg.clip_r = h->cfg.reward_clip_loss;
-    // the gather on model.fwd0's operand loads (rowk 6: 16x16 tiles, whose rows are whole records)
-    const bool gfold = fuse && h->mfuse >= 2 && h->mtile != 2 && h->stride % 4 == 0 && ldQ % 4 == 0;
+    // the gather on model.fwd0's operand loads (rowk 6: 16x16 tiles, whose rows are whole records; the
+    // reward nets' layer 0 reads the gathered X, so --separate_reward_nn keeps the gather launch)
+    const bool gfold = fuse && h->mfuse >= 2 && h->mtile != 2 && h->stride % 4 == 0 && ldQ % 4 == 0 && !h->srn;
     if (!gfold) {
         Launch L{};
         L.kind = Launch::MGATHER;
@@ -1486,21 +1525,26 @@ void build_model_plan(sacx_handle* h) {
         L.bytes = 4.0 * nm * mb * (2.0 * S + A + 1 + ldQ + O);
         plan.push_back(L);
     }
-    std::vector<GemmProb> f0, f1, f2, b2, b1, w;
+    std::vector<GemmProb> f0, f1, f2, b2, b1, w, wr;
     for (int k = 0; k < nm; ++k) {
         const std::string n = "m" + std::to_string(k);
         const size_t r0 = (size_t)k * mb;
         f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, m0));
         f1.push_back(prob_fwd(Hf1 + r0 * Hm0, Hm0, mb, Hm0, W(n + ".l1"), Hm1, Hf2 + r0 * Hm1, m1));
-        f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), O, fuse ? Df3 + r0 * ldO : Of + r0 * O,
+        f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), Om, fuse ? Df3 + r0 * ldO : Of + r0 * O,
                               ACT_NONE));
-        if (fuse) {   // MSEModel.get_loss as the head's epilogue: C = d loss / d out, per-tile partials
+        if (fuse) {   // MSEModel / GaussianModel.get_loss as the head's epilogue: C = d loss / d out, partials
             GemmProb& p = f2.back();
             p.ldc = ldO;
-            p.mse = 2; p.se_raw = Tf + r0 * O; p.part = W("ws.lf") + r0 * nt;
-            p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;
+            p.mse = MSE_FIT | (h->gm ? MSE_GAUSS : 0) | (h->lscale ? MSE_SCALE : 0) | (h->srn ? MSE_NOREW : 0);
+            p.se_raw = Tf + r0 * O; p.ldp = O; p.part = W("ws.lf") + r0 * nt;
+            p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;   // the reward column's
+            if (h->gm) {
+                p.spe_raw = W(n + ".logstd");
+                p.ppart = W("ws.lgp") + (size_t)k * ntm * S;
+            }
         }
-        b2.push_back(prob_dx(Df3 + r0 * ldO, mb, O, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, m1));
+        b2.push_back(prob_dx(Df3 + r0 * ldO, mb, Om, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, m1));
         b2.back().lda = ldO;
         b1.push_back(prob_dx(Df2 + r0 * Hm1, mb, Hm1, W(n + ".l1"), Hm0, Hf1 + r0 * Hm0, Df1 + r0 * Hm0, m0));
         if (bfold) {   // A = D2 generated from H2, D3 and W2 on load; column tile 0 stores it for model.adam
@@ -1510,8 +1554,34 @@ void build_model_plan(sacx_handle* h) {
         }
         w.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Df1 + r0 * Hm0, Hm0, W(n + ".l0"), nullptr, GRP_MODEL));
         w.push_back(prob_dw(Hf1 + r0 * Hm0, Hm0, Hm0, mb, Df2 + r0 * Hm1, Hm1, W(n + ".l1"), nullptr, GRP_MODEL));
-        w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * ldO, O, W(n + ".l2"), nullptr, GRP_MODEL));
+        w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * ldO, Om, W(n + ".l2"), nullptr, GRP_MODEL));
         w.back().ldb = ldO;
+    }
+    if (h->srn) {
+        // --separate_reward_nn (base_world_model.py:32-37, :72-74): the reward nets ride in the same
+        // launches -- layers 0 / 1 beside the model nets', the 1-wide head with the MSE loss epilogue on
+        // the targets' reward column, their dX and (own launch: > GEMM_MAXP problems) dW + Adam
+        const int Hr0 = h->Hr0, Hr1 = h->Hr1, r0a = h->racts[0], r1a = h->racts[1];
+        float *Hr1f = W("ws.Hrf1"), *Hr2f = W("ws.Hrf2"), *Dr3 = W("ws.Drf3"), *Dr2 = W("ws.Drf2"), *Dr1 = W("ws.Drf1");
+        for (int k = 0; k < nm; ++k) {
+            const std::string n = "r" + std::to_string(k);
+            const size_t r0 = (size_t)k * mb;
+            f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hr0, Hr1f + r0 * Hr0, r0a));
+            f1.push_back(prob_fwd(Hr1f + r0 * Hr0, Hr0, mb, Hr0, W(n + ".l1"), Hr1, Hr2f + r0 * Hr1, r1a));
+            f2.push_back(prob_fwd(Hr2f + r0 * Hr1, Hr1, mb, Hr1, W(n + ".l2"), 1, Dr3 + r0 * 4, ACT_NONE));
+            GemmProb& p = f2.back();
+            p.ldc = 4;
+            p.mse = MSE_FIT;                                // N = 1: column 0 is the reward column
+            p.se_raw = Tf + r0 * O + S; p.ldp = O; p.part = W("ws.lf") + (size_t)nm * mb * nt + r0;
+            p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;
+            b2.push_back(prob_dx(Dr3 + r0 * 4, mb, 1, W(n + ".l2"), Hr1, Hr2f + r0 * Hr1, Dr2 + r0 * Hr1, r1a));
+            b2.back().lda = 4;
+            b1.push_back(prob_dx(Dr2 + r0 * Hr1, mb, Hr1, W(n + ".l1"), Hr0, Hr1f + r0 * Hr0, Dr1 + r0 * Hr0, r0a));
+            wr.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Dr1 + r0 * Hr0, Hr0, W(n + ".l0"), nullptr, GRP_MODEL));
+            wr.push_back(prob_dw(Hr1f + r0 * Hr0, Hr0, Hr0, mb, Dr2 + r0 * Hr1, Hr1, W(n + ".l1"), nullptr, GRP_MODEL));
+            wr.push_back(prob_dw(Hr2f + r0 * Hr1, Hr1, Hr1, mb, Dr3 + r0 * 4, 1, W(n + ".l2"), nullptr, GRP_MODEL));
+            wr.back().ldb = 4;
+        }
     }
     // the fit's own tile shapes (SACX_MTILE): its 2 x 200 rows want 16x16 forward / dX tiles
     // (832 workgroups at 512 wide, against 224 as 32x32) whatever the update's batch made
@@ -1545,6 +1615,12 @@ void build_model_plan(sacx_handle* h) {
     MFinalArgs mf{};
     mf.ctl = h->ctl(); mf.loss_rows = W("ws.lf"); mf.mb = mb; mf.nm = nm;
     mf.mstats = W("mstats"); mf.mstats_cap = h->stats_cap; mf.nt = fuse ? nt : 0;
+    if (h->srn) mf.nt2 = 1;            // the reward heads' partials follow the model heads' in ws.lf
+    if (h->gm) {                       // the logstd gradient and Adam (or its store for the global-norm clip)
+        mf.lgpart = W("ws.lgp"); mf.ntm = ntm; mf.S = S; mf.lscale = h->lscale ? 1 : 0;
+        mf.gstore = h->cfg.model_max_grad_norm > 0.f ? 1 : 0;
+        for (int k = 0; k < nm; ++k) mf.logstd[k] = W("m" + std::to_string(k) + ".logstd");
+    }
     if (!bfold) {
         add_gemm(h, plan, "model.bwd2", b2, false);
         if (fuse) {
@@ -1566,15 +1642,33 @@ void build_model_plan(sacx_handle* h) {
     }
     if (h->mtile == 1) h->tile32 = 2;
     add_gemm(h, plan, "model.adam", w, false);
-    h->tile32 = tile32_h;
     plan.back().gemm.t_adv = fuse ? 1 : 0;
+    const size_t n_adam = wr.empty() ? 1 : 2;
+    if (!wr.empty()) {
+        add_gemm(h, plan, "reward.adam", wr, false);
+        plan.back().gemm.t_adv = 1;
+    }
+    h->tile32 = tile32_h;
+    for (Launch& L : plan)           // GaussianModel fits: the head epilogue has the 16x16 form only
+        if (L.kind == Launch::GEMM && L.gemm.t32)
+            for (int i = 0; i < L.gemm.nprob; ++i)
+                if (L.gemm.probs[i].mse & (MSE_GAUSS | MSE_NOREW)) {
+                    fprintf(stderr, "sacx: GaussianModel / reward-net fit heads need 16x16 tiles\n");
+                    abort();
+                }
     if (h->cfg.model_max_grad_norm > 0.f) {
-        // --model_max_grad_norm (mbrl_onpolicy_alg.py:315-317): the dW launch stores the
-        // gradients (+3 p_stride); their global norm gives one scale; Adam applies g * scale
-        Launch& G = plan.back();
-        for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
-        G.name = "model.grad";
-        const std::string last = nm > 1 ? "m1.l2" : "m0.l2";
+        // --model_max_grad_norm (mbrl_onpolicy_alg.py:315-317): the dW launches store the
+        // gradients (+3 p_stride; GaussianModel's logstd gradient from mfit_final); their global
+        // norm gives one scale; Adam applies g * scale over the models' whole contiguous range
+        for (size_t a = 0; a < n_adam; ++a) {
+            Launch& G = plan[plan.size() - 1 - a];
+            for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
+            G.name = a + 1 == n_adam ? "model.grad" : "reward.grad";
+        }
+        const AdamConsts gadam = plan[plan.size() - n_adam].gemm.adam;   // (plan grows below)
+        std::string last = "m" + std::to_string(nm - 1) + ".l2";
+        if (h->gm) last = "m" + std::to_string(nm - 1) + ".logstd";
+        if (h->srn) last = "r" + std::to_string(nm - 1) + ".l2";
         const uint64_t o0 = h->off_of("m0.l0");
         const SegInfo& sl = h->seg(last);
         const int64_t n = (int64_t)((sl.off + (uint64_t)(sl.rows * sl.cols) * 4 - o0) / 4);
@@ -1594,7 +1688,7 @@ void build_model_plan(sacx_handle* h) {
         AdamApplyArgs& a = U.ap;
         a.P = P; a.n = n; a.p_stride = h->p_stride; a.group = GRP_MODEL; a.t_off = 0;
         a.grad_scale = 1.f; a.scale_dev = N.gn.scale_out;
-        a.ctl = h->ctl(); a.adam = G.gemm.adam; a.t_adv = fuse ? 1 : 0;
+        a.ctl = h->ctl(); a.adam = gadam; a.t_adv = fuse ? 1 : 0;
         U.grid = (int)((n + 255) / 256);
         U.bytes = 4.0 * n * 7;
         plan.push_back(U);
@@ -2196,7 +2290,18 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
         if (cfg->model_hidden[0] > 512 || cfg->model_hidden[1] > 512) return bad("model hidden sizes > 512 unsupported");
         if (cfg->model_activation < 0 || cfg->model_activation > 2) return bad("model activation invalid");
         if (cfg->s_dim + 1 > 512) return bad("s_dim > 511 unsupported by the model MSE head");
+        if (cfg->separate_reward_nn) {
+            const int r0 = cfg->reward_hidden[0] > 0 ? cfg->reward_hidden[0] : 512;
+            const int r1 = cfg->reward_hidden[1] > 0 ? cfg->reward_hidden[1] : 512;
+            if (r0 > 512 || r1 > 512) return bad("reward hidden sizes > 512 unsupported");
+            for (int l = 0; l < 2; ++l)
+                if (cfg->reward_act_layers[l] < 0 || cfg->reward_act_layers[l] > 2)
+                    return bad("reward activations must be relu/tanh/elu");
+        }
     }
+    if (cfg->critic_hidden[0] < 0 || cfg->critic_hidden[1] < 0 || cfg->critic_hidden[0] > 512 ||
+        cfg->critic_hidden[1] > 512)
+        return bad("critic hidden sizes must be in [1, 512] (0: the actor's)");
     if (cfg->num_models < 0 || cfg->num_models > 2) return bad("num_models must be 1 or 2 (0 -> 2)");
     if (cfg->act_per_layer)
         for (int n = 0; n < 3; ++n)
@@ -2209,6 +2314,8 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->A = cfg->a_dim;
     h->H0 = cfg->hidden[0];
     h->H1 = cfg->hidden[1];
+    h->Hc0 = cfg->critic_hidden[0] > 0 ? cfg->critic_hidden[0] : h->H0;   // --critic_layers (nn_utils.py:86-138)
+    h->Hc1 = cfg->critic_hidden[1] > 0 ? cfg->critic_hidden[1] : h->H1;
     h->B = cfg->batch;
     h->cap = cfg->buffer_capacity;
     for (int l = 0; l < 2; ++l) {           // per-layer activations, or the one of each net
@@ -2221,6 +2328,16 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     h->ecap = cfg->use_expert ? cfg->expert_capacity : 0;
     h->Hm0 = cfg->use_expert ? cfg->model_hidden[0] : 0;
     h->Hm1 = cfg->use_expert ? cfg->model_hidden[1] : 0;
+    h->gm = cfg->use_expert && cfg->gaussian_model;
+    h->lscale = h->gm && cfg->scale_model_loss;
+    h->srn = cfg->use_expert && cfg->separate_reward_nn;
+    h->Om = h->srn ? h->S : h->S + 1;
+    if (h->srn) {
+        h->Hr0 = cfg->reward_hidden[0] > 0 ? cfg->reward_hidden[0] : 512;
+        h->Hr1 = cfg->reward_hidden[1] > 0 ? cfg->reward_hidden[1] : 512;
+        h->racts[0] = cfg->reward_act_layers[0];
+        h->racts[1] = cfg->reward_act_layers[1];
+    }
     h->mb = cfg->use_expert ? (cfg->model_batch > 0 ? cfg->model_batch : 200) : 0;
     h->nm = cfg->use_expert ? (cfg->num_models > 0 ? cfg->num_models : 2) : 0;
     h->ln = cfg->actor_layer_norm != 0;
@@ -3203,7 +3320,7 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
     if (settle(h)) return -1;
     if (net < 0 || net > 3) return fail(h, "net must be 0..3 (q0, q1, t0, t1)");
     if (n < 0 || (n > 0 && (!s || !a || !out))) return fail(h, "bad arguments");
-    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, ldQ = h->ldQ;
+    const int S = h->S, A = h->A, H0 = h->Hc0, H1 = h->Hc1, ldQ = h->ldQ;   // the critics' sizes
     auto W = [&](const std::string& nm) { return h->f(nm); };
     static const char* names[4] = {"q0", "q1", "t0", "t1"};
     const std::string nm = names[net];
@@ -3227,45 +3344,96 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
     return 0;
 }
 
-// the model net on rows [c0, c0 + m) of (s, a): roll.Xm -> roll.M1 -> roll.M2 -> roll.O
-static void model_net_chunk(sacx_handle* h, int32_t model, const float* s, const float* a, int m) {
-    const int S = h->S, A = h->A, ldQ = h->ldQ, Hm0 = h->Hm0, Hm1 = h->Hm1;
+// The world model's GEMM launches on the m rows of roll.Xm (stream st): the model net roll.Xm ->
+// M1 -> M2 -> roll.O [m, S+1] (its Om columns), and with --separate_reward_nn the reward net
+// (base_world_model.py:72-74) in the same launches into roll.O's reward column.  Model k's rows
+// start at row k * rstride of M1 / M2 / O / R1 / R2 (nk models on the same inputs: the diagnostics)
+static void model_gemms(sacx_handle* h, const std::vector<int>& models, int m, int64_t rstride, hipStream_t st,
+                        const char* tag) {
+    const int S = h->S, A = h->A, ldQ = h->ldQ, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
-    const std::string mn = "m" + std::to_string(model);
-    NetIOArgs g = netio_base(h, true);
-    g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s; g.a = a; g.X = W("roll.Xm");
-    launch_net_io(g, h->stream);
+    std::vector<GemmProb> p0, p1, p2;
+    for (size_t i = 0; i < models.size(); ++i) {
+        const std::string mn = "m" + std::to_string(models[i]);
+        float* M1 = W("roll.M1") + (size_t)i * rstride * Hm0;
+        float* M2 = W("roll.M2") + (size_t)i * rstride * Hm1;
+        float* Oo = W("roll.O") + (size_t)i * rstride * O;
+        p0.push_back(prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, M1, h->macts[0]));
+        p1.push_back(prob_fwd(M1, Hm0, m, Hm0, W(mn + ".l1"), Hm1, M2, h->macts[1]));
+        p2.push_back(prob_fwd(M2, Hm1, m, Hm1, W(mn + ".l2"), h->Om, Oo, ACT_NONE));
+        p2.back().ldc = O;
+        if (h->srn) {
+            const std::string rn = "r" + std::to_string(models[i]);
+            const int Hr0 = h->Hr0, Hr1 = h->Hr1;
+            float* R1 = W("roll.R1") + (size_t)i * rstride * Hr0;
+            float* R2 = W("roll.R2") + (size_t)i * rstride * Hr1;
+            p0.push_back(prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(rn + ".l0"), Hr0, R1, h->racts[0]));
+            p1.push_back(prob_fwd(R1, Hr0, m, Hr0, W(rn + ".l1"), Hr1, R2, h->racts[1]));
+            p2.push_back(prob_fwd(R2, Hr1, m, Hr1, W(rn + ".l2"), 1, Oo + S, ACT_NONE));
+            p2.back().ldc = O;
+        }
+    }
     std::vector<Launch> pl;
-    add_gemm(h, pl, "model.fwd0", {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->macts[0])},
-             false);
-    add_gemm(h, pl, "model.fwd1", {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->macts[1])},
-             false);
-    add_gemm(h, pl, "model.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), S + 1, W("roll.O"), ACT_NONE)}, false);
-    for (auto& L : pl) launch_gemm(L.gemm, h->stream);
-    h->probs_cursor -= 3;
+    const std::string t(tag);
+    add_gemm(h, pl, t + ".fwd0", p0, false);
+    add_gemm(h, pl, t + ".fwd1", p1, false);
+    add_gemm(h, pl, t + ".fwd2", p2, false);
+    for (auto& L : pl) launch_gemm(L.gemm, st);
+    h->probs_cursor -= (int)(p0.size() + p1.size() + p2.size());   // add_gemm's table (not a plan)
 }
 
-int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n, float delta_clip,
-                       float reward_clip, float* pred_out, float* sp_out, float* r_out) {
+// the model net on rows [c0, c0 + m) of (s, a): roll.Xm -> roll.M1 -> roll.M2 -> roll.O
+static void model_net_chunk(sacx_handle* h, int32_t model, const float* s, const float* a, int m) {
+    NetIOArgs g = netio_base(h, true);
+    g.mode = 0; g.n = m; g.ldX = h->ldQ; g.s = s; g.a = a; g.X = h->f("roll.Xm");
+    launch_net_io(g, h->stream);
+    model_gemms(h, {model}, m, 0, h->stream, "model");
+}
+
+// GaussianModel noise (continuous_models.py:40, :61): np.random.normal(size=(m, S)) from the device
+// stream into roll.mnoise (+ offset rows)
+static void model_noise_draw(sacx_handle* h, int64_t rows, int64_t row0, hipStream_t st) {
+    RngArgs r{};
+    r.st = h->ptr<RngState>("rng"); r.ctl = h->ctl();
+    r.n_int = 0; r.n_norm = (int32_t)(rows * h->S); r.out_idx = nullptr;
+    r.out_norm = h->f("roll.mnoise") + row0 * h->S;
+    r.slot = -1; r.reset_seq = 0; r.nupd = 1;
+    launch_rng(r, st);
+}
+
+int sacx_model_sample(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n,
+                      int32_t stochastic, float delta_clip, float reward_clip, float* pred_out, float* sp_out,
+                      float* r_out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (settle(h)) return -1;
     if (!h->cfg.use_expert) return fail(h, "the world models exist only with use_expert");
     if (model < 0 || model >= h->nm) return fail(h, "model index out of range (num_models)");
     if (n < 0 || (n > 0 && (!s || !a))) return fail(h, "bad arguments");
     const int S = h->S;
+    const bool noisy = stochastic && h->gm;
     for (int64_t done = 0; done < n; done += ROLL_CAP) {
         const int m = (int)std::min<int64_t>(ROLL_CAP, n - done);
         model_net_chunk(h, model, s + done * S, a + done * h->A, m);
+        if (noisy) model_noise_draw(h, m, 0, h->stream);   // chunks in row order: one draw of (n, S)
         NetIOArgs g = netio_base(h, true);
         g.mode = 2; g.n = m; g.s = s + done * S; g.O = h->f("roll.O"); g.ldO = S + 1;
         g.clip_d = delta_clip; g.clip_r = reward_clip;
         g.out0 = pred_out ? pred_out + done * (S + 1) : nullptr;
         g.out1 = sp_out ? sp_out + done * S : nullptr;
         g.out2 = r_out ? r_out + done : nullptr;
+        if (noisy) {
+            g.mlogstd = h->f("m" + std::to_string(model) + ".logstd");
+            g.mnoise = h->f("roll.mnoise");
+        }
         launch_net_io(g, h->stream);
     }
     HIPCHK(h, hipGetLastError());
     return 0;
+}
+
+int sacx_model_forward(sacx_handle* h, int32_t model, const float* s, const float* a, int64_t n, float delta_clip,
+                       float reward_clip, float* pred_out, float* sp_out, float* r_out) {
+    return sacx_model_sample(h, model, s, a, n, 0, delta_clip, reward_clip, pred_out, sp_out, r_out);
 }
 
 int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* sp, const float* a, const float* r,
@@ -3285,6 +3453,10 @@ int sacx_model_loss(sacx_handle* h, int32_t model, const float* s, const float* 
         g.clip_d = delta_clip_loss; g.clip_r = reward_clip_loss;
         g.out0 = h->f("roll.noise");           // running sum (workspace scalar)
         g.out1 = loss_out;
+        if (h->gm) {                           // GaussianModel.get_loss (continuous_models.py:101-131)
+            g.mlogstd = h->f("m" + std::to_string(model) + ".logstd");
+            g.lscale = h->lscale ? 1 : 0;
+        }
         g.first = done == 0; g.last = done + m >= n; g.n_total = n;
         launch_net_io(g, h->stream);
     }
@@ -3297,7 +3469,6 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
                      int32_t deterministic, float delta_clip, float reward_clip, float* s_out, float* a_out,
                      float* r_out, float* sp_out, uint8_t* d_out, hipStream_t st) {
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
-    const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     const std::string mn = "m" + std::to_string(model);
     // steps outer, chunks inner: each step draws normal(size=(n, A)) in row order, exactly the
@@ -3315,6 +3486,10 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
             ra.ms_mean = W("mnorm.s_mean"); ra.ms_den = W("mnorm.s_den");      // the model's
             ra.d_mean = W("mnorm.d_mean"); ra.d_den = W("mnorm.d_den"); ra.r_norm = W("mnorm.r");
             ra.clip_d = delta_clip; ra.clip_r = reward_clip;
+            if (h->gm) {               // GaussianModel.step: exp(logstd) * u (continuous_models.py:38-41)
+                ra.mlogstd = W(mn + ".logstd");
+                ra.mnoise = W("roll.mnoise");
+            }
             ra.mode = 0;
             launch_roll(ra, st);
             float* noise = deterministic ? nullptr : W("roll.noise");
@@ -3341,13 +3516,8 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
             a.alpha_mode = 0;
             FinalArgs f{};
             launch_actor_head(a, f, st);
-            add_gemm(h, pl, "roll.m.fwd0",
-                     {prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, W("roll.M1"), h->macts[0])}, false);
-            add_gemm(h, pl, "roll.m.fwd1",
-                     {prob_fwd(W("roll.M1"), Hm0, m, Hm0, W(mn + ".l1"), Hm1, W("roll.M2"), h->macts[1])}, false);
-            add_gemm(h, pl, "roll.m.fwd2", {prob_fwd(W("roll.M2"), Hm1, m, Hm1, W(mn + ".l2"), O, W("roll.O"), ACT_NONE)}, false);
-            for (auto& L : pl) launch_gemm(L.gemm, st);
-            h->probs_cursor -= 3;      // host table bookkeeping of add_gemm (these launches are not in a plan)
+            model_gemms(h, {model}, m, 0, st, "roll.m");
+            if (h->gm) model_noise_draw(h, m, 0, st);    // after the actor's draw (samplers.py:93-95)
             ra.mode = 1;
             launch_roll(ra, st);
         }
@@ -3363,6 +3533,8 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
     if (n < 0 || horizon < 0) return fail(h, "bad arguments");
     if (n == 0 || horizon == 0) return 0;
     if (!s_init || !s_out || !a_out || !r_out || !sp_out || !d_out) return fail(h, "null output");
+    if (h->gm && n > ROLL_CAP)   // one step's draws: the actor's (n, A), then the model's (n, S)
+        return fail(h, "GaussianModel rollout: at most 4096 trajectories per call (the draws of a step interleave)");
     if (settle(h)) return -1;
     // one captured graph per (model, shape, clips, pointers): the Python host keeps its
     // staging / output buffers per shape, so repeated calls replay (SACX_ROLL_GRAPH=0: eager)
@@ -3406,7 +3578,6 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
     if (settle(h)) return -1;
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
-    const int Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
     DiagArgs d{};
     d.n = n; d.S = S; d.A = A; d.ldS = ldS; d.ldQ = ldQ;
@@ -3416,23 +3587,8 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     d.a_mean = W("mnorm.a_mean"); d.a_den = W("mnorm.a_den");
     d.d_mean = W("mnorm.d_mean"); d.d_den = W("mnorm.d_den"); d.clip_d = delta_clip; d.out = out;
     // both models on the same n input rows: model k's rows land at [k n, (k+1) n)
-    auto models = [&]() {
-        std::vector<Launch> pl;
-        std::vector<GemmProb> p0, p1, p2;
-        for (int k = 0; k < 2; ++k) {             // one model: its MSE twice (the mean is exact)
-            const std::string mn = h->nm > 1 ? "m" + std::to_string(k) : std::string("m0");
-            float* M1 = W("roll.M1") + (size_t)k * n * Hm0;
-            float* M2 = W("roll.M2") + (size_t)k * n * Hm1;
-            p0.push_back(prob_fwd(W("roll.Xm"), ldQ, n, S + A, W(mn + ".l0"), Hm0, M1, h->macts[0]));
-            p1.push_back(prob_fwd(M1, Hm0, n, Hm0, W(mn + ".l1"), Hm1, M2, h->macts[1]));
-            p2.push_back(prob_fwd(M2, Hm1, n, Hm1, W(mn + ".l2"), O, W("roll.O") + (size_t)k * n * O, ACT_NONE));
-        }
-        add_gemm(h, pl, "diag.m.fwd0", p0, false);
-        add_gemm(h, pl, "diag.m.fwd1", p1, false);
-        add_gemm(h, pl, "diag.m.fwd2", p2, false);
-        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
-        h->probs_cursor -= 6;
-    };
+    // (one model: its MSE twice, the mean is exact)
+    auto models = [&]() { model_gemms(h, {0, h->nm > 1 ? 1 : 0}, n, n, h->stream, "diag.m"); };
     // actor.sample(s_e, deterministic=False) (continuous_actors.py:270-306) into the action columns
     auto counterfactual = [&]() {
         RngArgs r{};
@@ -3459,6 +3615,12 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     if (disc) {                      // _calc_disc (SAC_expert.py:427-460)
         if (!ea) counterfactual();
         models();
+        if (h->gm) {                 // model.sample(deterministic=False): model 0's (n, S), then model 1's
+            model_noise_draw(h, 2 * (int64_t)n, 0, h->stream);
+            d.mlogstd[0] = W("m0.logstd");
+            d.mlogstd[1] = W("m1.logstd");
+            d.mnoise = W("roll.mnoise");
+        }
         d.mode = 3;
         launch_diag(d, h->stream);
     } else {                         // SAC_expert.py:579-608

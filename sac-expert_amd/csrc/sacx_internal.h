@@ -64,6 +64,7 @@ enum GemmMode { GM_FWD = 0, GM_DX = 1, GM_DW = 2, GM_FWD2 = 3 };
 // so the 256 tiles and the head rows run in one round; its head rows take NW / 4 blocks of 4 rows each
 #define SACX_FWD2_HEAD_NW 8
 
+enum { MSE_EXPERT = 1, MSE_FIT = 2, MSE_GAUSS = 4, MSE_SCALE = 8, MSE_NOREW = 16 };
 struct GemmProb {
     const float* A;        // a_kc: A[m*lda + k]   else A[k*lda + m] (row ones_row = 1.0)
     const float* B;        // b_kc: B[n*ldb + k]   else B[k*ldb + n]
@@ -94,6 +95,14 @@ struct GemmProb {
     // model.fwd2 epilogue): se_raw = the normalised targets T [M, N]; C = d loss / d out =
     // -(T - out) * (cf / mb) with cf = fcoef (reward_loss_coef) on column N - 1, else 1
     // (grad_scale = 1 / mb); part[row * tiles + tn] = sum over the tile's columns of cf (T - out)^2
+    // Fit heads are mse = MSE_FIT | flags (ABI 7): the targets' row stride is ldp (T is [rows, S+1]
+    // whatever the head's N); the reward column N - 1 takes fcoef, none with MSE_NOREW (the model
+    // net beside a separate reward net); MSE_GAUSS: GaussianModel.get_loss (continuous_models.py:
+    // 101-131) on the delta columns, spe_raw = the model's logstd [Sd] (Sd = N - 1, or N with
+    // MSE_NOREW), with MSE_SCALE times the stop-gradient ds = mean(exp(2 logstd)) of
+    // --scale_model_loss: q = (T - out) / e^l, C = -(q / e^l) (ds / mb), part sums ds (q^2 + 2 l +
+    // log 2 pi), and ppart[tm * Sd + n] = sum over the tile's rows of 1 - q^2 (the logstd gradient's
+    // partials, x ds / mb in mfit_final; a fit head has no partial dots, so ppart is free)
     int32_t mse;
     float fcoef;
     float dclip;            // --delta_clip_pred on `out` (clipped, zero gradient outside); 0: off
@@ -312,6 +321,15 @@ struct MFinalArgs {
     // nt > 0: loss_rows holds nt partials per row (the fit-loss epilogue's, sums of cf e^2 over a
     // column tile: the loss is 0.5 x their sum); 0: one loss per row (k_mloss)
     int32_t nt;
+    // --separate_reward_nn: the reward heads' loss partials, nt2 per row (same 0.5 x sum), right after
+    // the nm * mb * nt of loss_rows; 0: none
+    int32_t nt2;
+    // GaussianModel: the logstd gradient, (ds / mb) x the sum over the ntm row tiles of lgpart (model k
+    // at lgpart + k ntm S), then Keras Adam on logstd[k] (m / v at +p_stride / +2 p_stride) at the
+    // advanced step, or (gstore, --model_max_grad_norm) the gradient stored at +3 p_stride for the
+    // global-norm clip; ds = mean(exp(2 logstd)) with lscale, else 1
+    const float* lgpart; int32_t ntm, S, lscale, gstore;
+    float* logstd[2];
 };
 
 #define GEMM_MAXP 8
@@ -482,6 +500,10 @@ struct NetIOArgs {
     float* out2;                   // mode 2: r [n]
     int32_t first, last;           // mode 3: first / last chunk of the call
     int64_t n_total;               // mode 3: rows of the whole call (reduce_mean)
+    // GaussianModel (ABI 7): mode 2 adds exp(mlogstd) * mnoise[i * S + j] to the clipped delta_n when
+    // mnoise is set (sample(deterministic=False) / step); mode 3 takes the Gaussian NLL of
+    // continuous_models.py:101-131 for the delta columns (x mean(exp(2 l)) with lscale)
+    const float* mlogstd; const float* mnoise; int32_t lscale;
 };
 
 struct MLossArgs {
@@ -560,6 +582,9 @@ struct RollArgs {
     const float *s_mean, *s_den, *d_mean, *d_den, *r_norm;   // r_norm = (mean, den); d / r: the model's
     const float *ms_mean, *ms_den;   // the model's state normaliser (Xm); s_*: the actor's (X)
     float clip_d, clip_r;       // > 0: clip_by_value(-clip, clip) (delta_clip_pred / reward_clip_pred)
+    // GaussianModel.step (continuous_models.py:36-54): exp(mlogstd) * mnoise [n, S] added to the clipped
+    // delta_n (mode 1); null: MSEModel
+    const float* mlogstd; const float* mnoise;
 };
 
 // ---------------------------------------------------------------- expert diagnostics (F3)
@@ -576,6 +601,9 @@ struct DiagArgs {
     const float *ms_mean, *ms_den;   // the models' state normaliser (Xm)
     float clip_d;
     float* out;
+    // mode 3 (_calc_disc, deterministic=False) with GaussianModels: model k's delta_n gets
+    // exp(mlogstd[k]) * mnoise[(k n + i) * S + j] (null: MSEModel)
+    const float* mlogstd[2]; const float* mnoise;
 };
 
 // sacx_actor_act on a few rows (the env loop's one observation): one workgroup per row runs

@@ -11,7 +11,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 6
+SACX_ABI_VERSION = 7
 STAGE_FLOATS = 65536            # SACX_STAGE_FLOATS (include/sacx.h)
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
@@ -31,7 +31,7 @@ EXPORTS = [
     "sacx_time_graph", "sacx_actor_act", "sacx_time_kernels", "sacx_rollout",
     "sacx_dp_unique_id", "sacx_dp_init", "sacx_dp_init_local", "sacx_dp_local_step", "sacx_expert_diag", "sacx_resync", "sacx_seed_stride",
     "sacx_seed_select", "sacx_prepare", "sacx_actor_evaluate", "sacx_critic_forward", "sacx_model_forward",
-    "sacx_model_loss", "sacx_spec_hits", "sacx_settle",
+    "sacx_model_loss", "sacx_spec_hits", "sacx_settle", "sacx_model_sample",
 ]
 
 
@@ -80,6 +80,13 @@ class Config(ctypes.Structure):
         ("act_layers", (ctypes.c_int32 * 2) * 3),
         ("delta_clip_pred", ctypes.c_float),
         ("single_seed_plan", ctypes.c_int32),
+        # ABI 7
+        ("gaussian_model", ctypes.c_int32),
+        ("scale_model_loss", ctypes.c_int32),
+        ("separate_reward_nn", ctypes.c_int32),
+        ("reward_hidden", ctypes.c_int32 * 2),
+        ("reward_act_layers", ctypes.c_int32 * 2),
+        ("critic_hidden", ctypes.c_int32 * 2),
     ]
 
 
@@ -153,6 +160,7 @@ def lib():
         "sacx_actor_evaluate": (ctypes.c_int, [vp, vp, i64, vp, vp]),
         "sacx_critic_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, i32, vp]),
         "sacx_model_forward": (ctypes.c_int, [vp, i32, vp, vp, i64, f32, f32, vp, vp, vp]),
+        "sacx_model_sample": (ctypes.c_int, [vp, i32, vp, vp, i64, i32, f32, f32, vp, vp, vp]),
         "sacx_model_loss": (ctypes.c_int, [vp, i32, vp, vp, vp, vp, i64, f32, f32, vp]),
         "sacx_time_kernels": (ctypes.c_int, [vp, ctypes.c_char_p, i32, P(f64), P(f64), P(i64)]),
         "sacx_dp_unique_id": (ctypes.c_int, [vp, i32]),

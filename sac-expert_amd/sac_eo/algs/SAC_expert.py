@@ -227,8 +227,12 @@ class SAC_exp(SACBase):
         d = self._diag(disc=False)
         self.model_MSE_on_expert_data.append(d["mse_expert_data"])
         self.model_MSE_on_expert_counterfactual_action.append(d["mse_counterfactual"])
+        # model_ent: mean of model.entropy over the model data (SAC_expert.py:486-490) -- a constant
+        # per row (GaussianModel: 0.5 sum(2 logstd + log 2 pi + 1), continuous_models.py:162-166; MSEModel 0)
+        ent = np.array([np.float32(m.entropy(self.s_expert[:1], None)[0]) for m in self.models], np.float32)
         self.logger.log_train({"model_MSE_on_expert_data": d["mse_expert_data"],
                                "model_MSE_on_expert_counterfactual_action": d["mse_counterfactual"],
+                               "model_ent": ent,
                                "time_model_fit": time.time() - t0, "model_loss_epochs": ep + 1,
                                "model_updates": num_updates,
                                "model_loss_last": float(self.engine.model_stats(1)[0].sum())})

@@ -127,11 +127,12 @@ class SACBase:
     def _engine_config(self, k):
         if not getattr(self.actor, "squash", False):
             raise ValueError("SAC trains the squashed Gaussian actor (--actor_squash)")
-        hidden = self.actor.layers
-        if len(hidden) != 2 or list(self.q_critics[0].layers) != list(hidden):
-            raise NotImplementedError("the device engine runs 2 hidden layers shared by actor and critics")
+        hidden, chidden = self.actor.layers, self.q_critics[0].layers
+        if len(hidden) != 2 or len(chidden) != 2:
+            raise NotImplementedError("the device engine runs 2 hidden layers per net (--actor_layers / --critic_layers)")
         cfg = EngineConfig(
             s_dim=self.s_dim, a_dim=self.a_dim, hidden=tuple(hidden), activation=self.actor.activation,
+            critic_hidden=tuple(chidden),
             batch=int(self.sac_batch_size), buffer_capacity=self._capacity(), per_state_std=self.actor.per_state_std,
             use_expert=self.use_expert, expert_capacity=self.expert_buffer_size,
             expert_batch=int(self.expert_batch_size or self.expert_buffer_size),
@@ -150,6 +151,16 @@ class SACBase:
             delta_clip_loss=float(self.models[0].delta_clip_loss or 0.0) if self.use_expert else 0.0,
             reward_clip_loss=float(self.models[0].reward_clip_loss or 0.0) if self.use_expert else 0.0,
             delta_clip_pred=float(self.models[0].delta_clip_pred or 0.0) if self.use_expert else 0.0)
+        if self.use_expert:
+            m = self.models[0]
+            cfg.gaussian_model = bool(getattr(m, "gaussian", False))
+            cfg.scale_model_loss = bool(m.scale_model_loss) and cfg.gaussian_model   # GaussianModel only (:122-127)
+            cfg.separate_reward_nn = bool(m.separate_reward_nn)
+            if cfg.separate_reward_nn:
+                if len(m.reward_layers) != 2:
+                    raise NotImplementedError("the device reward net runs 2 hidden layers (--reward_layers)")
+                cfg.reward_hidden = tuple(m.reward_layers)
+                cfg.reward_activations = tuple(m.reward_activations)
         return cfg
 
     # ------------------------------------------------------------------ RNG sharing
@@ -337,7 +348,7 @@ class SACBase:
                  "alpha": self.engine.alpha()}
         if self.use_expert:
             final["model_weights"] = [m.get_weights() for m in self.models]
-            final["reward_weights"] = [None for _ in self.models]
+            final["reward_weights"] = [m.get_reward_weights() for m in self.models]   # mbrl_onpolicy_alg.py:326-327
         return final
 
     def _dump_and_save(self, params):

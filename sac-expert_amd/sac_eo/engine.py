@@ -29,8 +29,9 @@ CTL = {"t_sac": 0, "t_model": 1, "num_timesteps": 2, "ts_increment": 3, "cur_siz
 class EngineConfig:
     s_dim: int
     a_dim: int
-    hidden: Sequence[int] = (256, 256)
+    hidden: Sequence[int] = (256, 256)       # --actor_layers (and the critics' unless critic_hidden)
     activation: str = "relu"
+    critic_hidden: Optional[Sequence[int]] = None   # --critic_layers when they differ from the actor's
     batch: int = 256
     buffer_capacity: int = 1_000_000
     per_state_std: bool = False
@@ -72,12 +73,24 @@ class EngineConfig:
     actor_activations: Optional[Sequence[str]] = None
     critic_activations: Optional[Sequence[str]] = None
     model_activations: Optional[Sequence[str]] = None
+    # world-model variants (ABI 7): --gaussian_model (GaussianModel: a trainable logstd per model,
+    # the Gaussian NLL fit, noise in sample / step), --scale_model_loss, --separate_reward_nn (a
+    # reward net of reward_hidden beside each model net)
+    gaussian_model: bool = False
+    scale_model_loss: bool = False
+    separate_reward_nn: bool = False
+    reward_hidden: Sequence[int] = (512, 512)
+    reward_activations: Optional[Sequence[str]] = None
 
     def to_c(self) -> N.Config:
         c = N.Config()
         c.abi_version = N.SACX_ABI_VERSION
         c.s_dim, c.a_dim = int(self.s_dim), int(self.a_dim)
         c.hidden[0], c.hidden[1] = int(self.hidden[0]), int(self.hidden[1])
+        if self.critic_hidden is not None:
+            if len(self.critic_hidden) != 2:
+                raise NotImplementedError("the device critics run 2 hidden layers (--critic_layers)")
+            c.critic_hidden[0], c.critic_hidden[1] = int(self.critic_hidden[0]), int(self.critic_hidden[1])
         c.activation = N.ACT[self.activation]
         c.batch = int(self.batch)
         c.buffer_capacity = int(self.buffer_capacity)
@@ -120,6 +133,18 @@ class EngineConfig:
                 if len(lst) != 2:
                     raise ValueError("two hidden layers: one or two activation names per net")
                 c.act_layers[n][0], c.act_layers[n][1] = N.ACT[lst[0]], N.ACT[lst[1]]
+        c.gaussian_model = int(bool(self.gaussian_model))
+        c.scale_model_loss = int(bool(self.scale_model_loss))
+        c.separate_reward_nn = int(bool(self.separate_reward_nn))
+        if self.separate_reward_nn:
+            if len(self.reward_hidden) != 2:
+                raise NotImplementedError("the reward net runs 2 hidden layers (--reward_layers)")
+            c.reward_hidden[0], c.reward_hidden[1] = int(self.reward_hidden[0]), int(self.reward_hidden[1])
+            lst = list(self.reward_activations or ["relu"])
+            lst = lst * 2 if len(lst) == 1 else lst
+            if len(lst) != 2:
+                raise ValueError("two hidden layers: one or two reward activation names")
+            c.reward_act_layers[0], c.reward_act_layers[1] = N.ACT[lst[0]], N.ACT[lst[1]]
         return c
 
 
@@ -289,6 +314,13 @@ class Engine:
 
     def set_logstd(self, logstd):
         self.v["actor.logstd"].copy_(torch.as_tensor(np.asarray(logstd, np.float32).reshape(1, -1)))
+
+    def set_model_logstd(self, model: int, logstd):
+        """GaussianModel's logstd variable [1, S] of world model `model` (continuous_models.py:24-25)."""
+        self.v[f"m{int(model)}.logstd"].copy_(torch.as_tensor(np.asarray(logstd, np.float32).reshape(1, -1)))
+
+    def get_model_logstd(self, model: int) -> np.ndarray:
+        return self.v[f"m{int(model)}.logstd"].detach().cpu().numpy().copy()
 
     def set_alpha(self, alpha: float):
         self.v["alpha"].fill_(float(np.float32(alpha)))
@@ -466,23 +498,28 @@ class Engine:
         self._keep_q = (x, u)
         return out if value else out.reshape(n, 1)
 
-    def model_forward(self, model: int, s, a, delta_clip: float = 0.0, reward_clip: float = 0.0):
+    def model_forward(self, model: int, s, a, delta_clip: float = 0.0, reward_clip: float = 0.0,
+                      stochastic: bool = False):
         """BaseWorldModel._forward + MSEModel.sample / step (base_world_model.py:65-87,
         continuous_models.py:225-254): -> (pred [n, S+1] = [delta_n | r_n] after the clips,
-        sp [n, S] = s + denormalised delta, r [n] = denormalised reward)."""
+        sp [n, S] = s + denormalised delta, r [n] = denormalised reward).  stochastic on a
+        gaussian_model engine: GaussianModel.sample(deterministic=False) / step (:36-70), sp from
+        delta_n + exp(logstd) * u with u = normal(size=(n, S)) from the device stream."""
         S, A = self.cfg.s_dim, self.cfg.a_dim
         x, u = self._dev(s, (-1, S)), self._dev(a, (-1, A))
         n = int(x.shape[0])
         kw = dict(dtype=torch.float32, device=self.device)
         pred, sp, r = torch.empty((n, S + 1), **kw), torch.empty((n, S), **kw), torch.empty((n,), **kw)
         p = lambda t: ctypes.c_void_p(t.data_ptr())
-        N.check(self.lib.sacx_model_forward(self.h, int(model), p(x), p(u), n, float(delta_clip or 0.0),
-                                            float(reward_clip or 0.0), p(pred), p(sp), p(r)), self.h, "model_forward")
+        N.check(self.lib.sacx_model_sample(self.h, int(model), p(x), p(u), n, int(bool(stochastic)),
+                                           float(delta_clip or 0.0), float(reward_clip or 0.0), p(pred), p(sp), p(r)),
+                self.h, "model_forward")
         self._keep_m = (x, u)
         return pred, sp, r
 
     def model_loss(self, model: int, s, sp, a, r, delta_clip_loss: float = 0.0, reward_clip_loss: float = 0.0):
-        """MSEModel.get_loss (continuous_models.py:280-302) on the device -> float."""
+        """MSEModel.get_loss (continuous_models.py:280-302) / GaussianModel.get_loss (:101-131) on
+        the device -> float."""
         S, A = self.cfg.s_dim, self.cfg.a_dim
         x, y, u = self._dev(s, (-1, S)), self._dev(sp, (-1, S)), self._dev(a, (-1, A))
         n = int(x.shape[0])

@@ -30,13 +30,18 @@ def nontrivial_normalizers(rs, S, A):
 
 def make_learner(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
                  use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
-                 bias_scale=0.05, actor_gain=0.5, epsilon=0.1, layer_norm=False, actor_acts=None, critic_acts=None):
-    """The seeded inputs of one learner: (oracle_cfg, oracle_state_f32, buffer, normalizers, expert)."""
+                 bias_scale=0.05, actor_gain=0.5, epsilon=0.1, layer_norm=False, actor_acts=None, critic_acts=None,
+                 wm=None):
+    """The seeded inputs of one learner: (oracle_cfg, oracle_state_f32, buffer, normalizers, expert).
+    ``wm``: world-model variant flags (gaussian_model, scale_model_loss, separate_reward_nn,
+    reward_hidden, reward_act) of O.Config."""
+    wm = dict(wm or {})
     ocfg = O.Config(S=S, A=A, hidden=hidden, act=act, B=B, per_state_std=per_state_std,
+                    critic_hidden=wm.pop("critic_hidden", None),
                     model_hidden=model_hidden, epsilon=epsilon, layer_norm=layer_norm, actor_acts=actor_acts,
-                    critic_acts=critic_acts)
+                    critic_acts=critic_acts, **wm)
     st = O.init_state(ocfg, seed=seed + 1, with_models=use_expert, bias_scale=bias_scale,
-                      actor_gain=actor_gain, model_gain=0.3)
+                      actor_gain=actor_gain, model_gain=0.3, model_std_mult=0.7, reward_gain=0.3)
     rs = np.random.RandomState(seed + 100)
     buf = synthetic_buffer(rs, N, S, A, done_p)
     nrm = O.Normalizers.identity(S, A) if normalizers == "identity" else nontrivial_normalizers(rs, S, A)
@@ -60,6 +65,10 @@ def load_learner(eng, st, buf, nrm, expert, epsilon):
         for k in range(2):
             if f"m{k}.l0" in eng.segments:      # --num_models 1: model 0 only
                 eng.set_net(f"m{k}", st.models[k])
+                if st.model_logstd is not None:
+                    eng.set_model_logstd(k, st.model_logstd[k])
+                if st.reward_nets is not None:
+                    eng.set_net(f"r{k}", st.reward_nets[k])
     eng.set_alpha(float(st.alpha))
     eng.set_normalizers(nrm.s_mean, nrm.s_den, nrm.a_mean, nrm.a_den, nrm.d_mean, nrm.d_den,
                         nrm.r_mean, nrm.r_den, nrm.ret_den)
@@ -71,12 +80,18 @@ def load_learner(eng, st, buf, nrm, expert, epsilon):
 def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
               use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
               graph_steps=8, bias_scale=0.05, actor_gain=0.5, epsilon=0.1, dp=None, gemm_bf16=False, layer_norm=False,
-              actor_acts=None, critic_acts=None, **ekw):
+              actor_acts=None, critic_acts=None, wm=None, **ekw):
     """Returns (engine, oracle_cfg, oracle_state_fp64, buffer, normalizers, expert)."""
     from sac_eo.engine import Engine, EngineConfig
     ocfg, st, buf, nrm, expert = make_learner(S, A, hidden, B, act, N, seed, per_state_std, use_expert, ne,
                                               model_hidden, normalizers, done_p, bias_scale, actor_gain, epsilon,
-                                              layer_norm, actor_acts, critic_acts)
+                                              layer_norm, actor_acts, critic_acts, wm)
+    if wm:                                 # the oracle's world-model flags -> the engine's
+        ekw = dict(ekw, gaussian_model=ocfg.gaussian_model, scale_model_loss=ocfg.scale_model_loss,
+                   separate_reward_nn=ocfg.separate_reward_nn, reward_hidden=tuple(ocfg.reward_hidden),
+                   reward_activations=(ocfg.reward_act,))
+    if ocfg.critic_hidden is not None:
+        ekw = dict(ekw, critic_hidden=tuple(ocfg.critic_hidden))
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=hidden, activation=act, batch=B, buffer_capacity=N,
                         per_state_std=per_state_std, use_expert=use_expert, expert_capacity=max(ne, 2),
                         expert_batch=ne, model_hidden=model_hidden, graph_steps=graph_steps, epsilon=epsilon,

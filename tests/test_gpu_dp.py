@@ -65,3 +65,25 @@ def test_dp_two_local_ranks_equal_global_batch(gpu_available, act):
     assert worst < 1e-4 and q_err < 1e-4, (worst, q_err)
     for e in engs:
         e.close()
+
+
+def test_dp_rccl_two_processes(gpu_available):
+    """Config C4 over RCCL between two fresh processes (bench.py --mode dpcheck --gpus 2: one GPU per
+    rank, ncclAllReduce inside the captured update graph): the ranks' parameters and Adam state
+    bit-identical after 64 updates, and equal to the single learner's updates on the concatenated
+    batches.  RCCL refuses two ranks on one device, so a one-GPU box skips."""
+    import json
+    import os
+    import subprocess
+    import sys
+    if torch.cuda.device_count() < 2:
+        pytest.skip("RCCL data-parallel ranks need one GPU each: fewer than 2 visible")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--mode", "dpcheck", "--gpus", "2"],
+                         capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])["dp_c4"]
+    print(res)
+    assert res["ranks"] == 2 and res["rccl_world_size"] == 2
+    assert res["dp_ranks_identical"] and res["matches_single_learner"], res

@@ -78,8 +78,15 @@ def _oracle_state(alg_obj, ocfg):
     st = O.SACState(aw[:-1], aw[-1], q, qt, alpha, O.AdamState.zeros_like(aw),
                     [O.AdamState.zeros_like(n) for n in q], O.AdamState.zeros_like([alpha]))
     if alg_obj.use_expert:
-        st.models = [m.get_weights() for m in alg_obj.models]
-        st.opt_model = O.AdamState.zeros_like([w for m in st.models for w in m])
+        ws = [m.get_weights() for m in alg_obj.models]
+        if ocfg.gaussian_model:            # GaussianModel.get_weights: the net's weights + [logstd]
+            st.models = [w[:-1] for w in ws]
+            st.model_logstd = [w[-1] for w in ws]
+        else:
+            st.models = ws
+        if ocfg.separate_reward_nn:
+            st.reward_nets = [m.get_reward_weights() for m in alg_obj.models]
+        st.opt_model = O.AdamState.zeros_like(st.model_all_vars())
     return st.astype(np.float64)
 
 
@@ -111,10 +118,16 @@ def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
     alg_obj, d, ak, total, oenvs, rs_state = _build(alg, flags, shape=shape, act=act)
     S, A = alg_obj.s_dim, alg_obj.a_dim
     H, MH = shape["hidden"], shape["model_hidden"]
+    mk, msk = d["model_kwargs"], d["model_setup_kwargs"]
     ocfg = O.Config(S=S, A=A, hidden=(H, H), act=act, B=shape["B"], gamma=ak["gamma"], tau=ak["soft_tau"],
                     lr_q=ak["q_crit_lr"], lr_pi=ak["mbpo_actor_lr"], lr_alpha=ak["mbpo_alpha_lr"],
                     init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(MH, MH),
-                    model_act="relu", lr_model=ak["model_lr"])
+                    model_act="relu", lr_model=ak["model_lr"], reward_loss_coef=msk["reward_loss_coef"],
+                    gaussian_model=bool(mk["gaussian_model"]),
+                    scale_model_loss=bool(msk["scale_model_loss"]) and bool(mk["gaussian_model"]),
+                    separate_reward_nn=bool(msk["separate_reward_nn"]), reward_hidden=tuple(mk["reward_layers"]),
+                    reward_act=mk["reward_activations"][0],
+                    critic_hidden=tuple(d["critic_kwargs"]["critic_layers"]))
     st = _oracle_state(alg_obj, ocfg)
     # the fp32 envelope starts from the SAME initial state: sac_update / model_fit_step advance
     # the state they are given in place, so it is copied before the fp64 run trains st
@@ -199,9 +212,15 @@ def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, tol=LOSS
     ("sac_imit", ["--model_holdout_ratio", "0.2"]),
     ("sac_imit", ["--update_normalizers", "--s_noise_std", "0.3"]),
     ("sac_imit", ["--update_normalizers", "--s_noise_std", "0.3", "--s_noise_type", "next"]),
+    ("sac_imit", ["--gaussian_model", "--model_std_mult", "0.5"]),
+    ("sac_imit", ["--gaussian_model", "--scale_model_loss", "--separate_reward_nn", "--reward_layers", "48", "32",
+                  "--reward_activations", "tanh"]),
+    ("sac_imit", ["--separate_reward_nn", "--reward_layers", "64", "64", "--num_models", "1"]),
     ("sac", []),
     ("sac", ["--update_normalizers"]),
     ("sac", ["--update_normalizers", "--s_noise_std", "0.5"]),
+    ("sac", ["--critic_layers", "96", "48"]),                 # critics wider / narrower than the actor
+    ("sac_imit", ["--critic_layers", "40", "72"]),
 ])
 def test_train_loop_matches_oracle(gpu_available, alg, flags):
     alg_obj, ak, name, dev, dev_rng, orc, ref, _ = _run(alg, flags)
@@ -219,6 +238,7 @@ def test_train_loop_matches_oracle(gpu_available, alg, flags):
     ("sac_imit", "relu", ["--num_models", "1"]),
     ("sac", "tanh", []),
     ("sac", "relu", []),
+    ("sac", "relu", ["--critic_layers", "400", "300"]),       # --actor_layers 256 256 --critic_layers 400 300
 ])
 def test_train_loop_bench_config(gpu_available, alg, act, flags):
     """The loops at the metric's shapes (256x2, B = 256, 512x2 models, minibatch 200, three

@@ -248,3 +248,44 @@ def test_delta_clip_pred_update(gpu_available, nm, dcp):
         assert relerr(gd[:-1], keep["actor_grads"][2 * i]) < 2e-4
         assert relerr(gd[-1], keep["actor_grads"][2 * i + 1]) < 2e-4
     eng.close()
+
+
+@pytest.mark.parametrize("chid,use_expert", [((96, 48), False), ((400, 300), False), ((64, 128), True)])
+def test_critic_hidden_sizes(gpu_available, chid, use_expert):
+    """--critic_layers different from --actor_layers (nn_utils.py:86-138 builds each net from its own
+    list; train_parser.py:56-59, :80-84): one update per stage against the oracle, then 19 graph-replayed
+    updates equal to eager launches bit for bit."""
+    B = 128
+    ne = 12 if use_expert else 20
+    eng, ocfg, st, buf, nrm, expert = make_pair(act="relu", B=B, seed=29, use_expert=use_expert, ne=ne,
+                                                normalizers="random", model_hidden=(64, 64), wm=dict(critic_hidden=chid))
+    assert eng.segments["q0.l0"]["cols"] == chid[0] and eng.segments["t1.l1"]["cols"] == chid[1]
+    N = buf["r"].shape[0]
+    rs = np.random.RandomState(95)
+    eng.rng_set_state(rs.get_state())
+    gen = np.random.default_rng(3) if use_expert else None
+    R = O.draw_step_randoms(rs, N, B, ocfg.A, n_expert=ne if use_expert else 0, gen=gen)
+    if use_expert:
+        eng.push_perms(R["perm"][None])
+    ref = oracle_step(st, ocfg, nrm, buf, R, expert)
+    eng.step(1, eager=True)
+    eng.sync()
+    row = eng.stats(1)[0]
+    for i, k in enumerate(("q1_loss", "q2_loss", "p_loss", "alpha_loss")):
+        assert abs(row[i] - ref[k]) <= 2e-5 * abs(ref[k]) + 1e-7, (k, row[i], ref[k])
+    for n, nets in (("q0", st.q[0]), ("t1", st.q_targ[1]), ("actor", st.actor)):
+        for a_, b_ in zip(eng.get_net(n), nets):
+            assert relerr(a_, b_) < 2e-4, n
+    eng.close()
+    outs = []
+    for eager in (True, False):
+        eng, *_ = make_pair(act="relu", B=B, seed=29, use_expert=use_expert, ne=ne, normalizers="random",
+                            model_hidden=(64, 64), graph_steps=8, wm=dict(critic_hidden=chid))
+        eng.rng_set_state(np.random.RandomState(96).get_state())
+        if use_expert:
+            eng.push_perms(np.stack([np.random.RandomState(j).permutation(ne) for j in range(19)]))
+        eng.step(19, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy()))
+        eng.close()
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])

@@ -355,6 +355,94 @@ def test_model_fit_clips_and_global_norm(nmodels, max_norm, dclip, rclip):
         assert st.opt_model.t == 1
 
 
+@pytest.mark.parametrize("gauss,sep,scale,max_norm,dclip", [
+    (True, False, False, None, 0.0), (True, False, True, None, 0.4), (False, True, False, None, 0.0),
+    (True, True, True, 0.05, 0.0), (True, True, False, None, 0.3)])
+def test_model_fit_gaussian_and_reward_net_match_autograd(gauss, sep, scale, max_norm, dclip):
+    """GaussianModel.get_loss (continuous_models.py:101-131: the NLL with the trainable logstd,
+    --scale_model_loss as a stop-gradient factor) and --separate_reward_nn (base_world_model.py:32-37,
+    :72-74: the model net predicts the S deltas, the reward net the reward) against autograd, with
+    one Adam over model.trainable (nn, logstd, reward nn per model) and the global-norm clip."""
+    cfg = O.Config(S=4, A=2, hidden=(8, 8), B=16, model_hidden=(10, 12), gaussian_model=gauss,
+                   separate_reward_nn=sep, scale_model_loss=scale, reward_hidden=(7, 9), reward_act="tanh",
+                   reward_loss_coef=0.7)
+    st = O.init_state(cfg, seed=8, with_models=True, bias_scale=0.1, model_gain=0.5, model_std_mult=0.8,
+                      reward_gain=0.4).astype(np.float64)
+    rs = np.random.RandomState(3)
+    nrm = O.Normalizers(rs.normal(size=4) * .1, rs.uniform(.5, 2, 4), rs.normal(size=2) * .1,
+                        rs.uniform(.5, 2, 2), rs.normal(size=4) * .1, rs.uniform(.5, 2, 4), 0.2, 1.5, 1.0)
+    batches = [(rs.normal(size=(9, 4)), rs.uniform(-1, 1, (9, 2)), rs.normal(size=(9, 4)) * 2,
+                rs.normal(size=9) * 2) for _ in range(2)]
+    V = [[_t(w).requires_grad_() for w in st.model_vars(k)] for k in range(2)]
+    tot = 0
+    for k, (s, a, sp, r) in enumerate(batches):
+        x = torch.cat([(_t(s) - _t(nrm.s_mean)) / _t(nrm.s_den), (_t(a) - _t(nrm.a_mean)) / _t(nrm.a_den)], 1)
+        nn = V[k][:6]
+        out = _mlp(nn, x, "relu")
+        rp = _mlp(V[k][-6:], x, "tanh")[:, 0] if sep else out[:, 4]
+        dn = ((_t(sp) - _t(s)) - _t(nrm.d_mean)) / _t(nrm.d_den)
+        if dclip:
+            dn = torch.clamp(dn, -dclip, dclip)
+        rn = (_t(r) - nrm.r_mean) / nrm.r_den
+        if gauss:
+            l = V[k][6]
+            q = (dn - out[:, :4]) / torch.exp(l)
+            sc = torch.mean(torch.exp(l) ** 2).detach() if scale else 1.0
+            dl = sc * 0.5 * (q * q + 2 * l + float(np.log(np.float32(2 * np.pi)))).sum(-1)   # TF: a float32 constant
+        else:
+            dl = 0.5 * ((dn - out[:, :4]) ** 2).sum(-1)
+        tot = tot + torch.mean(dl + 0.7 * 0.5 * (rn - rp) ** 2)
+        if k == 0:
+            assert abs(O.model_loss(st, cfg, nrm, 0, s, sp, a, r, delta_clip_loss=dclip)
+                       - torch.mean(dl + 0.7 * 0.5 * (rn - rp) ** 2).item()) < 1e-12
+    flat = [w for vs in V for w in vs]
+    g = [x.numpy() for x in torch.autograd.grad(tot, flat)]
+    if max_norm:
+        clip = max_norm * 2
+        norm = np.sqrt(sum(np.sum(x * x) for x in g))
+        g = [x * (clip * min(1.0 / norm, 1.0 / clip)) for x in g]
+    ref = st.copy()
+    O.adam_step(ref.model_all_vars(), g, ref.opt_model, cfg.lr_model, np.float64)
+    loss = O.model_fit_step(st, cfg, nrm, batches, max_grad_norm=max_norm, delta_clip_loss=dclip)
+    assert abs(loss - tot.item()) < 1e-12
+    for w1, w2 in zip(st.model_all_vars(), ref.model_all_vars()):
+        np.testing.assert_allclose(w1, w2, rtol=1e-12, atol=1e-14)
+    if gauss:                         # the logstd variables moved (they are trained)
+        assert not np.array_equal(st.model_logstd[0], O.init_state(cfg, seed=8, with_models=True,
+                                  model_std_mult=0.8).model_logstd[0])
+
+
+def test_gaussian_model_noise_order():
+    """GaussianModel draws normal(size=(n, S)) in sample(deterministic=False) and in every step
+    (continuous_models.py:36-70): the rollout draws the actor's (n, A) then the model's (n, S) per
+    step; _calc_disc the actor's, then model 0's, then model 1's (SAC_expert.py:442-446)."""
+    cfg = O.Config(S=3, A=2, hidden=(8, 8), act="tanh", B=4, model_hidden=(8, 8), gaussian_model=True)
+    st = O.init_state(cfg, seed=3, with_models=True).astype(np.float64)
+    nrm = O.Normalizers.identity(3, 2)
+    s0 = np.random.RandomState(1).normal(size=(5, 3))
+    rs = np.random.RandomState(7)
+    s, a, r, sp, d = O.rollout(st, cfg, nrm, s0, 2, 0, rs)
+    ref = np.random.RandomState(7)
+    for _ in range(2):
+        ref.normal(size=(5, 2))
+        ref.normal(size=(5, 3))
+    assert rs.get_state()[2] == ref.get_state()[2] and np.array_equal(rs.get_state()[1], ref.get_state()[1])
+    rs2 = np.random.RandomState(9)
+    O.rollout(st, cfg, nrm, s0, 2, 0, rs2, deterministic=True)      # the model still draws
+    ref2 = np.random.RandomState(9)
+    ref2.normal(size=(5, 3))
+    ref2.normal(size=(5, 3))
+    assert rs2.get_state()[2] == ref2.get_state()[2]
+    rs3 = np.random.RandomState(4)
+    O.calc_disc(st, cfg, nrm, s0, None, rs=rs3)
+    ref3 = np.random.RandomState(4)
+    ref3.normal(size=(5, 2))
+    ref3.normal(size=(5, 3))
+    ref3.normal(size=(5, 3))
+    assert rs3.get_state()[2] == ref3.get_state()[2]
+    assert abs(O.model_entropy(st, cfg, 0) - 0.5 * np.sum(2 * st.model_logstd[0] + np.log(2 * np.pi) + 1)) < 1e-5
+
+
 @pytest.mark.parametrize("use_expert", [False, True])
 def test_oracle_layer_norm_actor_matches_autograd(use_expert):
     """--actor_layer_norm (nn_utils.py:110-119): Dense -> LayerNormalization(eps 1e-3) -> tanh

@@ -88,6 +88,11 @@ def test_bench_gpus_flag_spawns_ranks():
     for r in ranks:
         for k, v in r["seeds"].items():
             assert v == int(ref[k][r["rank"]])
+        assert r["group_world_size"] == 2                 # the process group the ranks joined
+    # the N > 1 line carries every rank's time, the group size and the C4 RCCL leg
+    assert {"rank_times_s", "group_world_size", "dp_c4"} <= set(line["line_fields_n_gt_1"])
+    leg = line["dp_c4_leg"]
+    assert leg["ranks"] == 2 and leg["mode"] == "dpcheck" and "dp_ranks_identical" in leg["fields"]
 
 
 def test_bench_gpus_mismatch_fails_loudly():
