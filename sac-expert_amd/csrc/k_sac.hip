@@ -731,13 +731,13 @@ __device__ void mfit_final(const MFinalArgs& f, const AdamConsts* adam = nullptr
 // MODE: GM_FWD (A k-contig, B=W n-contig, bias+act), GM_DX (A k-contig, B=W^T k-contig,
 // act'), GM_DW (A=X^T and B=delta both mn-contig, Keras Adam [+Polyak]).  VEC: float4 along k.
 template <int MODE, int NQ>
-__device__ __forceinline__ void qhead_block(const QHeadArgs& q, int block, int64_t so);
-template <int NQ, int OW = 0, bool TICKET = false>
+__device__ __forceinline__ void qhead_block(const QHeadArgs& q, int block, int64_t so, const FinalArgs* fin = nullptr);
+template <int NQ, int OW = 0, int FIN = 0>
 __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so,
                                                 const FinalArgs& ffin);
 template <int NQ, int OW = 0>
 __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so) {
-    actor_head_body<NQ, OW, false>(h, f, block, so, f);
+    actor_head_body<NQ, OW, 0>(h, f, block, so, f);
 }
 
 // Workgroups are dealt round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup dispatch),
@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     }
     if (tile >= total_tiles) {
         if constexpr (ROWK > 0 && ROWK < 3) {   // horizontally fused Q-head rows
-            qhead_block<ROWK - 1, NQ>(ga.qh, tile - total_tiles, so);
+            qhead_block<ROWK - 1, NQ>(ga.qh, tile - total_tiles, so, ROWK == 1 ? &ga.fin : nullptr);
         } else if constexpr (ROWK == 0 || ROWK == 7) {
             if (ga.has_mfinal) mfit_final(ga.mfin, &ga.adam, ga.p_stride);   // the world-model fit step's k_mfinal
         }
@@ -2323,21 +2323,25 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 // rows (4 waves each: the previous update's alpha rows, whose last block then finalises that update's
 // alpha, k_alpha_final's work, when has_final), and the target nets' tiles (headp) compute their 16
 // rows' evaluate() actions in a prologue (head_prologue, actor.fwd1's partial dots) into the LDS A tile
-template <int VEC, int NW, bool HEAD>
+// H0X: the largest layer-0 width of the variant (256, or 512: the world-model fit's model.fwd0/1 pair).
+// GATHER (rowk 6, the fit): layer 0's A rows are replay records gathered by the step's minibatch indices
+// and normalised on load (k_gemm rowk 6's arithmetic); wave 0 of column group 0 stores them to X and the
+// group's threads store the rows' targets T (get_loss :286-296) -- model.gather+fwd0+fwd1 in one launch
+template <int VEC, int NW, bool HEAD, int FIN = 0, int H0X = 256, bool GATHER = false>
 __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArgs ga) {   // (min waves per SIMD)
-    // NW waves: layer 0 by column tiles (wave w: tiles w, w + NW, ... of H0 <= 256), layer 1 as
+    // (FIN: ga.has_final as a template parameter -- each variant holds one finalisation form)
+    // NW waves: layer 0 by column tiles (wave w: tiles w, w + NW, ... of H0 <= H0X), layer 1 as
     // k_gemm's four-way K split (wave w: quarter w & 3) for CTW of the group's four column tiles
-    constexpr int L0T = 16 / NW, CTW = 16 / NW;
+    constexpr int L0T = (H0X / 16) / NW, CTW = 16 / NW, PU = H0X / 64;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    __shared__ float hs[16][256 + 4];
+    __shared__ float hs[16][H0X + 4];
     __shared__ float red2[4][4][4][64];    // [K quarter][column tile][q][lane]
     const int nnet = ga.nprob >> 1;
     int tile = (int)blockIdx.x;
     if constexpr (HEAD) {
         if (tile < ga.row_blocks) {           // actor-head rows, dispatched first: NW / 4 blocks of 4
             const int blk = ga.head_block0 + (NW / 4) * tile;
-            if (ga.has_final) actor_head_body<4, 0, true>(ga.head, ga.hfin, blk, 0, ga.fin);
-            else actor_head_body<4, 0, false>(ga.head, ga.hfin, blk, 0, ga.fin);
+            actor_head_body<4, 0, FIN>(ga.head, ga.hfin, blk, 0, ga.fin);
             if (ga.ktime != nullptr) {
                 __syncthreads();
                 if (threadIdx.x == 0) {
@@ -2372,9 +2376,51 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
     const __amdgpu_buffer_rsrc_t rw1 = make_rsrc(g1.B, 0x7fffffffu);
     const __amdgpu_buffer_rsrc_t rnull = rs(nullptr);
     float xa[2][4];
+    const float* trec = nullptr;             // GATHER: the record of this thread's target row
+    if constexpr (GATHER) {
+        // k_gemm rowk 6: row m of problem p is record start + idx_ring[seq][p][m] of the replay ring
+        const MGatherArgs& mg = ga.mg;
+        const int64_t seq = mg.ctl->mfit_seq, start = mg.ctl->start;
+        const int32_t* ir = mg.idx_ring + (seq % mg.idx_cap) * (int64_t)(mg.nm * mg.mb) + (int64_t)p * mg.mb;
+        auto rec_of = [&](int rr) {
+            int64_t phys = start + ir[min(rr, g0.M - 1)];
+            phys = phys >= mg.cap ? phys - mg.cap : phys;
+            return mg.replay + phys * (int64_t)mg.stride;
+        };
+        const float* grow = rec_of(m);
+        trec = rec_of(m0 + ((threadIdx.x & 255) >> 4));
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2)
-        load_a<true, VEC == 1, false>(rx, g0, m, mok && !headp, s2 < nIt0 ? s2 * 16 + grp * 4 : (1 << 30), xa[s2], rnull);
+        for (int s2 = 0; s2 < 2; ++s2) {
+            const int k0 = s2 < nIt0 ? s2 * 16 + grp * 4 : (1 << 30);
+            const bool live = mok && k0 < g0.K;
+            const int kb = k0 < g0.K ? k0 : 0;
+            float raw[4];
+            if constexpr (VEC == 1) {        // 16-B aligned records (host: stride and ldQ multiples of 4)
+                const float4 q = *reinterpret_cast<const float4*>(grow + kb);
+                raw[0] = q.x; raw[1] = q.y; raw[2] = q.z; raw[3] = q.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) raw[j] = grow[min(kb + j, g0.K - 1)];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int kc = min(kb + j, g0.K - 1);
+                const float* mu = kc < mg.S ? mg.s_mean + kc : mg.a_mean + (kc - mg.S);
+                const float* den = kc < mg.S ? mg.s_den + kc : mg.a_den + (kc - mg.S);
+                float x = (raw[j] - *mu) / *den;          // k_mgather's normalisation
+                asm("" : "+v"(x));
+                xa[s2][j] = (live && kb + j < g0.K) ? x : 0.f;
+            }
+            // X for model.adam's layer-0 dW (zero pad columns): one wave of column group 0
+            if (cg == 0 && wave == 0 && mok && k0 < g0.lda)
+                *reinterpret_cast<float4*>(const_cast<float*>(g0.A) + (size_t)m * g0.lda + k0) =
+                    float4{xa[s2][0], xa[s2][1], xa[s2][2], xa[s2][3]};
+        }
+    } else {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+            load_a<true, VEC == 1, false>(rx, g0, m, mok && !headp, s2 < nIt0 ? s2 * 16 + grp * 4 : (1 << 30), xa[s2], rnull);
+    }
     float w0[L0T][2][4], b0[L0T];
 #pragma unroll
     for (int i = 0; i < L0T; ++i) {
@@ -2385,14 +2431,14 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
         for (int s2 = 0; s2 < 2; ++s2) load_b<false, false>(rw0, g0, nc, cok, s2 < nIt0 && cok ? s2 * 16 + grp * 4 : (1 << 30), w0[i][s2]);
         b0[i] = bload(rs(g0.bias), boff(cok, nc));
     }
-    float w1[CTW][4][4];
+    float w1[CTW][PU][4];
 #pragma unroll
     for (int j2 = 0; j2 < CTW; ++j2) {
         const int ct = CTW * ch + j2;
         const int n1 = 64 * cg + 16 * ct + r;
         const bool nok = n1 < N1;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PU; ++u) {
             const int it = kq * per1 + u;
             load_b<false, false>(rw1, g1, n1, nok, u < per1 ? it * 16 + grp * 4 : (1 << 30), w1[j2][u]);
         }
@@ -2415,6 +2461,24 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
         }
     }
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (GATHER) {
+        // the targets T[row][c] (get_loss :286-296): c < S the normalised delta sp - s, c == S the
+        // reward, clipped by --delta_clip_loss / --reward_clip_loss; column group 0, 16 columns per
+        // 256 threads (k_gemm rowk 6's arithmetic)
+        const MGatherArgs& mg = ga.mg;
+        const int S = mg.S, A = mg.A, tcol = 16 * eh + col, mmr = m0 + row;
+        if (cg == 0 && mmr < g0.M && tcol <= S) {
+            const int c = tcol;
+            const float traw0 = c < S ? trec[S + A + c] : trec[2 * S + A];
+            const float traw1 = c < S ? trec[c] : 0.f;
+            const float tmu = c < S ? mg.d_mean[c] : mg.r_norm[0];
+            const float tden = c < S ? mg.d_den[c] : mg.r_norm[1];
+            float y = c < S ? ((traw0 - traw1) - tmu) / tden : (traw0 - tmu) / tden;
+            const float cl = c < S ? mg.clip_d : mg.clip_r;
+            if (cl > 0.f) y = fminf(fmaxf(y, -cl), cl);
+            mg.T[(size_t)(p * mg.mb + mmr) * (S + 1) + c] = y;
+        }
+    }
     if constexpr (HEAD) {
         // the target rows' A tile [sp_n | evaluate() actions], as k_gemm_head's tile prologue; column
         // group 0 stores the rows' neglogp for q.head (host: the head's partial dots exist, so the
@@ -2463,9 +2527,9 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
     __syncthreads();
 
     // ---- layer 1: K quarter kq (slabs kq * per1 + u), A from LDS, CTW column tiles
-    float a1[4][4];
+    float a1[PU][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < PU; ++u) {
         const int k0 = (kq * per1 + u) * 16 + grp * 4;
         const float4 q4 = u < per1 ? *reinterpret_cast<const float4*>(&hs[r][k0]) : float4{0.f, 0.f, 0.f, 0.f};
         a1[u][0] = q4.x; a1[u][1] = q4.y; a1[u][2] = q4.z; a1[u][3] = q4.w;
@@ -2474,7 +2538,7 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
     for (int j2 = 0; j2 < CTW; ++j2) {
         floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < PU; ++u) {
             if (u >= per1) break;             // uniform (k_gemm's zero slabs add +0)
             acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][0], w1[j2][u][0], acc0, 0, 0, 0);
             acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[u][1], w1[j2][u][1], acc1, 0, 0, 0);
@@ -2532,8 +2596,14 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         const dim3 block(SACX_FWD2_NW * 64);
         if (a.rowk == 3) {          // the target / critic pair with the actor-head rows
             const dim3 grid(a.total_tiles + a.row_blocks), hblock(SACX_FWD2_HEAD_NW * 64);
-            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_HEAD_NW, true>), grid, hblock, 0, s, a);
-            else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_HEAD_NW, true>), grid, hblock, 0, s, a);
+#define SACX_F2H(V, F) hipLaunchKernelGGL((k_fwd2<V, SACX_FWD2_HEAD_NW, true, F>), grid, hblock, 0, s, a)
+            if (a.has_final == 2) { if (a.vec) SACX_F2H(1, 2); else SACX_F2H(0, 2); }
+            else if (a.has_final) { if (a.vec) SACX_F2H(1, 1); else SACX_F2H(0, 1); }
+            else { if (a.vec) SACX_F2H(1, 0); else SACX_F2H(0, 0); }
+#undef SACX_F2H
+        } else if (a.rowk == 6) {   // the world-model fit's gather + two layers (16 waves, H0 <= 512)
+            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, 16, false, 0, 512, true>), dim3(a.total_tiles), dim3(1024), 0, s, a);
+            else hipLaunchKernelGGL((k_fwd2<0, 16, false, 0, 512, true>), dim3(a.total_tiles), dim3(1024), 0, s, a);
         } else {
             if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW, false>), dim3(a.total_tiles), block, 0, s, a);
             else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW, false>), dim3(a.total_tiles), block, 0, s, a);
@@ -3060,9 +3130,12 @@ void launch_alpha_final(const FinalArgs& f, hipStream_t s) {
 // ==================================================================== k_actor_head
 // one wave per actor row: mu = h2 . W3 + b, then evaluate()/sample() per column.
 // The wave sums are broadcast, so lane j keeps output j in a register.
-// TICKET (k_fwd2's fused q launch): the alpha blocks take a ticket after storing their partial, and
-// the last of them runs the previous update's alpha finalisation (ffin) in the same launch
-template <int NQ, int OW, bool TICKET>
+// FIN (k_fwd2's fused q launch, the previous update's alpha finalisation ffin): 1 (TICKET) the alpha
+// blocks take a ticket after storing their partial, and the last of them finalises in the same
+// launch; 2 (split, SACX_AFIN) the alpha blocks store their partials only and the first one snapshots
+// the finalisation's other operands (ffin.pre) and writes the update's loss statistics: the next
+// launch's target rows finish the alpha step (qhead_block)
+template <int NQ, int OW, int FIN>
 __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalArgs& f, int block, int64_t so,
                                                 const FinalArgs& ffin) {
     // a workgroup of 4 G waves runs G blocks of 4 rows (block + wave >> 2): per block the same partial
@@ -3084,7 +3157,12 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
         __syncthreads();
     }
     const int wave = wave_id() & 3, lane = threadIdx.x & 63, g4 = wave_id() >> 2;
+    constexpr bool TICKET = FIN == 1;
     FinPre fpre;
+    if constexpr (FIN == 2) {
+        // the first alpha block's wave 0 requests the snapshot's operands under the rows' own loads
+        if (threadIdx.x < 64 && h.alpha_mode && block * 4 == h.alpha_row0) fin_prefetch(ffin, fpre);
+    }
     if constexpr (TICKET && SACX_FIN_PRE) {
         // wave 0 of a workgroup holding alpha blocks (the one that may finalise) requests the
         // finalisation's other operands now, under the rows' own loads
@@ -3205,6 +3283,25 @@ __device__ __forceinline__ void actor_head_body(const HeadArgs& h, const FinalAr
     }
     // (a group whose block is past the rows -- the last workgroup of k_fwd2's rows -- ends here too)
     if (!h.alpha_mode || block * 4 < h.alpha_row0 || block * 4 >= h.total_rows) return;
+    if constexpr (FIN == 2) {
+        if (threadIdx.x < 64 && block * 4 == h.alpha_row0) {
+            // (the first alpha block is group 0 of its workgroup: the host aligns alpha_row0 to one)
+            // the update's loss statistics (finalize_update's sums, same order) and the snapshot
+            const float q1 = wave_sum(fpre.ps[0]) / (float)ffin.B;
+            const float q2 = wave_sum(fpre.ps[1]) / (float)ffin.B;
+            const float pl = wave_sum(fpre.ps[2]) / (float)ffin.B;
+            if (lane == 0) {
+                float* st = ffin.stats + (size_t)(fpre.seq0 % ffin.stats_cap) * 8;
+                st[0] = q1;
+                st[1] = q2;
+                st[2] = pl;
+                st[5] = 0.f;
+                AfinPre* P = ffin.pre;
+                P->a_old = fpre.a_old; P->a_m = fpre.a_m; P->a_v = fpre.a_v;
+                P->t_sac = fpre.t_sac; P->seq0 = fpre.seq0; P->nts = fpre.nts; P->tsi = fpre.tsi;
+            }
+        }
+    }
     // ---- alpha: block partial of sum(-nlp + H); k_alpha_final reduces them
     if (lane == 0) red_s[4 * g4 + wave] = row_ent;
     if constexpr (TICKET) {
@@ -3507,7 +3604,7 @@ void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s)
 
 // ==================================================================== k_qhead
 template <int MODE, int NQ>
-__device__ __forceinline__ void qhead_block(const QHeadArgs& q_in, int block, int64_t so) {
+__device__ __forceinline__ void qhead_block(const QHeadArgs& q_in, int block, int64_t so, const FinalArgs* fin) {
     __shared__ float buf[4][512];
     QHeadArgs q = q_in;
     reloc(q, so);
@@ -3516,7 +3613,46 @@ __device__ __forceinline__ void qhead_block(const QHeadArgs& q_in, int block, in
     const int B = q.B, H1 = q.H1;
     if (row < B) {
         constexpr int nnet = (MODE == 0) ? 4 : 2;
-        const float alpha = *q.alpha;
+        float alpha;
+        if (MODE == 0 && fin != nullptr && fin->pre != nullptr) {
+            // the split alpha finalisation (one seed: no relocation): the previous update's alpha step
+            // from its partials and the snapshot its first alpha block took -- finalize_update's
+            // arithmetic, so every row block computes the same alpha; block 0 stores the results
+            const FinalArgs& f = *fin;
+            const AfinPre* P = f.pre;
+            const float* const xs[1] = {f.red};
+            const int ns[1] = {f.nred};
+            float p0[1];
+            strided_sums<1>(xs, ns, p0);
+            const float a_old = P->a_old, a_m = P->a_m, a_v = P->a_v;
+            const int64_t t_sac = P->t_sac, seq = P->seq0, nts = P->nts, tsi = P->tsi;
+            const float m_ent = wave_sum(p0[0]) / (float)f.B;   // reduce_mean(-nlp + H)
+            const int64_t tnew = t_sac + 1;
+            const float g = -m_ent;
+            const float lr_t = adam_lr(f.adam, GRP_ALPHA, tnew);
+            const float b1 = 0.9f, b2 = 0.999f, eps = 1e-7f;
+            const float mm = a_m + (g - a_m) * (1.f - b1);
+            const float vv = a_v + (g * g - a_v) * (1.f - b2);
+            float an = a_old - (mm * lr_t) / (sqrtf(vv) + eps);
+            an = fmaxf(an, 1e-5f);                  // SAC_expert.py:348
+            alpha = an;
+            if (block == 0 && wave == 0 && lane == 0) {
+                *f.alpha_m = mm;
+                *f.alpha_v = vv;
+                *f.alpha = an;
+                float* st = f.stats + (size_t)(seq % f.stats_cap) * 8;
+                st[3] = -a_old * m_ent;
+                st[4] = an;
+                st[6] = -(m_ent - f.target_entropy);
+                st[7] = (float)seq;
+                Ctl* ctl = f.ctl;
+                ctl->t_sac = tnew;
+                ctl->num_timesteps = nts + tsi;
+                ctl->step_seq = seq + 1;
+            }
+        } else {
+            alpha = *q.alpha;
+        }
         const float nlp_r = q.nlp[row];
         float r_r = 0.f, d_r = 0.f, rd = 1.f;
         if (MODE == 0) {

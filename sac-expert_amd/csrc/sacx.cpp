@@ -179,6 +179,8 @@ struct sacx_handle {
     int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
+    int afin = 1;             // k_fwd2's folded alpha finalisation split over q.head's rows (SACX_AFIN; 0: ticket)
+    int mfwd2 = 1;            // the fit's gather + model.fwd0 + model.fwd1 as one k_fwd2 launch (SACX_MFWD2)
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
     // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
     int dp_ranks = 0, dp_rank = 0;
@@ -423,6 +425,7 @@ void build_layout(sacx_handle* h) {
     h->add("perm", h->perm_cap, ne1, SACX_I32, SACX_ROLE_STATE);
     h->add("stats", h->stats_cap, 8, F, SACX_ROLE_STATE);
     h->add("red", 1, std::max(1024, (B + 3) / 4), F, SACX_ROLE_WORK);
+    h->add("ws.afin", 1, sizeof(AfinPre) / 4, F, SACX_ROLE_WORK);   // the split alpha finalisation's snapshot
     // ---------------- workspace
     const int Ra = h->Ra, Rb = h->Rb, Hm0 = std::max(1, h->Hm0), Hm1 = std::max(1, h->Hm1);
     // actor activations; rows [Ra4, Ra4 + B) hold the alpha evaluate() of an update
@@ -749,14 +752,17 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     // layer 0 may carry the actor head (rowk 3: target tile prologues from the head's partial dots,
     // which keep the prologue free of barriers, and head rows as extra workgroups)
     const bool head = a0.rowk == 3;
-    if ((a0.rowk != 0 && !head) || (a1.rowk != 0 && a1.rowk != 5) || (head && a1.rowk != 0) || a0.has_final ||
-        a1.has_final || a0.nprob != a1.nprob || a0.nprob > 4)
+    // or layer 0 gathers its rows from the replay ring (rowk 6: the world-model fit's model.fwd0)
+    const bool gather = a0.rowk == 6;
+    if ((a0.rowk != 0 && !head && !gather) || (a1.rowk != 0 && a1.rowk != 5) || ((head || gather) && a1.rowk != 0) ||
+        a0.has_final || a1.has_final || a0.nprob != a1.nprob || a0.nprob > 4)
         return false;
     if (head && (a0.head.part == nullptr || a0.head.H1 > 256 || a0.head.A > 16)) return false;
     bool vec = true;
     for (int i = 0; i < a0.nprob; ++i) {
         const GemmProb &p0 = a0.probs[i], &p1 = a1.probs[i];
-        if (p0.mse || p1.mse || (p0.headp && !head) || p1.headp || p0.K > 32 || p0.N % 64 != 0 || p0.N > 256 ||
+        if (p0.mse || p1.mse || (p0.headp && !head) || p1.headp || p0.K > 32 || p0.N % 64 != 0 ||
+            p0.N > (gather ? 512 : 256) ||
             p1.K != p0.N || p1.A != p0.C || p1.lda != p0.ldc || p1.M != p0.M || p1.N % 16 != 0)
             return false;
         vec = vec && p0.vec;
@@ -778,7 +784,8 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     g.mode = GM_FWD2;
     g.vec = vec ? 1 : 0;
     g.total_tiles = tiles;
-    g.rowk = head ? 3 : a1.rowk;
+    g.rowk = head ? 3 : gather ? 6 : a1.rowk;
+    if (gather) g.mg = a0.mg;
     if (head) {
         g.head = a0.head;
         g.hfin = a0.hfin;
@@ -788,7 +795,7 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     g.row_blocks = 0;
     F.grid = tiles;
     F.frees_slot = L0.frees_slot || L1.frees_slot;
-    F.block = head ? SACX_FWD2_HEAD_NW * 64 : 1024;     // k_fwd2 waves
+    F.block = head ? SACX_FWD2_HEAD_NW * 64 : 1024;     // k_fwd2 waves (16; the fit's gather variant too)
     F.flops = L0.flops + L1.flops;
     F.bytes = L0.bytes + L1.bytes;
     F.gemm_first = L0.gemm_first;
@@ -1599,6 +1606,8 @@ void build_model_plan(sacx_handle* h) {
         F.bytes += 4.0 * nm * mb * (2.0 * S + A + 1 + O);
     }
     add_gemm(h, plan, "model.fwd1", f1, false);
+    // the gathered layer 0 and layer 1 as ONE k_fwd2 launch (SACX_MFWD2, default; K0 = S + A <= 32)
+    if (gfold && h->mfwd2) fuse_fwd2(h, plan, "model.gather+fwd01");
     add_gemm(h, plan, "model.fwd2", f2, false);
     if (fuse) plan.back().name = "model.fwd2+loss";
     if (!fuse) {
@@ -1780,6 +1789,7 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
         }
     size_t gi = 0;
     bool head_done = prev_slot < 0, final_done = prev_slot < 0, ln_done = pln == nullptr;
+    bool afin_next = false;    // the split alpha finalisation still has its q.head half to place
     for (const Launch& L : h->plan[slot]) {
         if (is_prologue(L) || L.alpha_branch) continue;
         Launch C = L;
@@ -1827,12 +1837,25 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                 C.name += "+alpha";
                 head_done = true;
                 if (C.kind == Launch::GEMM && C.gemm.mode == GM_FWD2 && pf) {
-                    // k_fwd2 has no later forward launch to take it: the last alpha block finalises
-                    C.gemm.has_final = 1;
+                    // k_fwd2 has no later forward launch to take it.  Split (SACX_AFIN, default): its
+                    // first alpha block snapshots the finalisation's operands and the next launch's
+                    // target rows finish the alpha step; else the last alpha block finalises (ticket)
+                    C.gemm.has_final = h->afin ? 2 : 1;
                     C.gemm.fin = pf->fin;
-                    C.name += ".final";
+                    if (h->afin) {
+                        C.gemm.fin.pre = h->ptr<AfinPre>("ws.afin");
+                        afin_next = true;
+                    } else {
+                        C.name += ".final";
+                    }
                     final_done = true;
                 }
+            } else if (afin_next && C.kind == Launch::GEMM && C.gemm.mode == GM_DX && C.gemm.rowk == 1) {
+                // q.head+critic.bwd1: every target row block finishes the previous update's alpha step
+                C.gemm.fin = pf->fin;
+                C.gemm.fin.pre = h->ptr<AfinPre>("ws.afin");
+                C.name += "+alpha.final";
+                afin_next = false;
             } else if (C.kind == Launch::GEMM && head_done && !final_done && pf &&
                        C.gemm.mode == GM_FWD) {
                 C.gemm.has_final = 1;
@@ -1843,7 +1866,7 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
         }
         out.push_back(C);
     }
-    return gi == pg.size() && head_done && final_done && ln_done;
+    return gi == pg.size() && head_done && final_done && ln_done && !afin_next;
 }
 
 // Captured chain of G updates on two streams (see the fork branch below):
@@ -1996,7 +2019,11 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             for (const Launch& L : body) {
                 if ((int)L.kind == skip_kind) {
                     // ablation: the alpha.final folded into a skipped GEMM still runs
-                    if (L.kind == Launch::GEMM && L.gemm.has_final) launch_alpha_final(L.gemm.fin, cs);
+                    if (L.kind == Launch::GEMM && L.gemm.has_final) {
+                        FinalArgs f = L.gemm.fin;
+                        f.pre = nullptr;                 // (the split form's snapshot: finalise in place)
+                        launch_alpha_final(f, cs);
+                    }
                     continue;
                 }
                 emit(L, cs);
@@ -2451,6 +2478,8 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (const char* e = std::getenv("SACX_MTILE")) h->mtile = std::atoi(e);
     if (const char* e = std::getenv("SACX_UNALIGNED")) h->unaligned_b = std::atoi(e);
     if (const char* e = std::getenv("SACX_FWD2")) h->fwd2 = std::atoi(e);
+    if (const char* e = std::getenv("SACX_AFIN")) h->afin = std::atoi(e);
+    if (const char* e = std::getenv("SACX_MFWD2")) h->mfwd2 = std::atoi(e);
     if (const char* e = std::getenv("SACX_DWL_NH")) h->dwl_nh = std::atoi(e) == 2 ? 2 : 1;
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);

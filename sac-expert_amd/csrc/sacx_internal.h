@@ -198,6 +198,15 @@ struct HeadBwdArgs {
     const float* ma_den;    // the world models' action normaliser (expert rows; --only_model_normalizer)
 };
 
+// The split alpha finalisation of k_fwd2's fused q launch (SACX_AFIN, default): the first alpha block
+// of that launch snapshots what finalize_update reads besides the alpha partials, so that the NEXT
+// launch (q.head+critic.bwd1) can finish the alpha step in every one of its target row blocks (the
+// same arithmetic, the same value) while its block 0 alone stores the results
+struct AfinPre {
+    float a_old, a_m, a_v, pad;
+    int64_t t_sac, seq0, nts, tsi;
+};
+
 struct FinalArgs {
     float* alpha; float* alpha_m; float* alpha_v;
     Ctl* ctl;
@@ -213,8 +222,12 @@ struct FinalArgs {
     int32_t mse_tiles;      // partials per expert row in mse_rows
     float* stats; int32_t stats_cap;
     // data-parallel mode: the local alpha gradient goes here (then an all-reduce and
-    // k_alpha_apply do the Adam, clamp, stats[4] and counters); null: all in place
-    float* alpha_g;
+    // k_alpha_apply do the Adam, clamp, stats[4] and counters); null: all in place.
+    // The split finalisation (never in the data-parallel modes, which do not fold): the snapshot
+    union {
+        float* alpha_g;
+        AfinPre* pre;
+    };
     float grad_scale;       // k_alpha_apply: 1 / ranks
     // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride

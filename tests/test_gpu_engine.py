@@ -287,8 +287,9 @@ def test_fused_forward_pair_bit_identical(gpu_available, monkeypatch, act, B, ea
     finalisation by the last alpha block -- the updates equal the k_gemm chain's bit for bit, eager
     and graph."""
     outs = []
-    for fused in ("0", "1"):
+    for fused, afin in (("0", "1"), ("1", "0"), ("1", "1")):
         monkeypatch.setenv("SACX_FWD2", fused)
+        monkeypatch.setenv("SACX_AFIN", afin)     # the folded alpha finalisation: ticket (0) or split (1)
         eng, ocfg, st, buf, nrm, _ = make_pair(act=act, B=B, seed=41, normalizers="random", graph_steps=8)
         names = [L["name"] for L in eng.plan_info()]
         for pair in ("pi.q.fwd01", "actor.fwd01", "alpha.fwd01", "q.fwd01+actor.head"):
@@ -298,8 +299,9 @@ def test_fused_forward_pair_bit_identical(gpu_available, monkeypatch, act, B, ea
         eng.sync()
         outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy()))
         eng.close()
-    for a, b in zip(outs[0], outs[1]):
-        assert np.array_equal(a, b)
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("S,A,B,clip", [(17, 6, 256, 0.0), (376, 17, 1024, 0.0), (17, 6, 64, 5.0)])
@@ -307,17 +309,22 @@ def test_model_fit_folds_bit_identical(gpu_available, monkeypatch, S, A, B, clip
     """The folded world-model fit chain (the loss and its gradient in model.fwd2's epilogue,
     k_mfinal as an extra workgroup of model.bwd2: SACX_MFUSE=1; the rows gathered on model.fwd0's
     operand loads: 2; model.bwd2 generated on model.bwd1's operand loads for heads of <= 32
-    outputs: 3, the default; the fit's own tile shapes: SACX_MTILE=1, the default, or 16x16
+    outputs: 3, the default; the gathered layer 0 and layer 1 as one k_fwd2 launch: SACX_MFWD2=1,
+    the default, when S + A <= 32; the fit's own tile shapes: SACX_MTILE=1, the default, or 16x16
     everywhere: 0) leaves the weights and Adam state of the unfolded chain
     (SACX_MFUSE=0, SACX_MTILE=2) bit for bit, eager and graph; the loss statistic sums the
     same squares in another order (<= 1e-6 relative)."""
     outs = []
     steps = 12
-    for fuse, tile in (("0", "2"), ("1", "1"), ("2", "1"), ("3", "1"), ("3", "0")):
+    for fuse, tile, f2 in (("0", "2", "0"), ("1", "1", "0"), ("2", "1", "0"), ("2", "1", "1"), ("3", "1", "0"),
+                           ("3", "1", "1"), ("3", "0", "1")):
         monkeypatch.setenv("SACX_MFUSE", fuse)
         monkeypatch.setenv("SACX_MTILE", tile)
+        monkeypatch.setenv("SACX_MFWD2", f2)
         eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, B=B, act="tanh", N=3000, seed=33, use_expert=True,
                                                normalizers="random", model_max_grad_norm=clip)
+        names = [L["name"] for L in eng.model_plan_info()]
+        assert ("model.gather+fwd01" in names) == (f2 == "1" and fuse != "1" and S + A <= 32), names
         mb = eng.cfg.model_batch
         idx = np.random.RandomState(4).randint(buf["r"].shape[0], size=(steps, 2, mb))
         eng.model_fit(idx[:3], eager=True)

@@ -64,6 +64,12 @@ for step in "$@"; do
     overhead)   # fixed cost of one step(n) call (sampler start-up, alpha tail, launch + wake-up)
       timeout -k 10 200 python tools/step_overhead.py $arg > "$log" 2>&1
       rc=$?; echo "[$n overhead] rc=$rc"; cat "$log" ;;
+    mtbench)    # twist-only MT19937 variants (tools/mt_bench.hip, built on the CPU side)
+      timeout -k 10 120 ./tools/mt_bench > "$log" 2>&1
+      rc=$?; echo "[$n mtbench] rc=$rc"; cat "$log" ;;
+    rngbench)
+      timeout -k 10 120 ./tools/rng_bench > "$log" 2>&1
+      rc=$?; echo "[$n rngbench] rc=$rc"; cat "$log" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
