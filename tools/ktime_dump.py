@@ -23,6 +23,8 @@ def main():
     eng.sync()
     path = os.path.join(tempfile.mkdtemp(), "kt.csv")
     os.environ["SACX_KTIME_DUMP"] = path
+    cpath = os.path.join(os.path.dirname(path), "kc.csv")
+    os.environ["SACX_KTIME_CLASSES"] = cpath
     eng.time_kernels("k_gemm", 2)
     rows = [l.strip().split(",") for l in open(path)]
     G = eng.cfg.graph_steps
@@ -42,6 +44,17 @@ def main():
         v = np.array(v).mean(0)
         print(f"{name:34s} {len(agg[name]):5d} {v[0]:6.2f} {v[1]:6.2f} {v[2]:6.2f} {v[3]:6.2f} {v[4]:6.2f} "
               f"{v[5]:7.2f} {v[6]:7.2f}")
+    # k_fwd2 launches: workgroups per problem pair (n:mean:max us), averaged over the graph's updates
+    cls = {}
+    if os.path.exists(cpath):
+        for l in open(cpath):
+            f = l.strip().split(",")
+            cls.setdefault(f[0], []).append([[float(x) for x in c.split(":")[1:]] for c in f[1:]])
+    if cls:
+        print(f"\n{'k_fwd2 launch: tiles per problem pair':34s} n / mean / max us")
+        for name, v in cls.items():
+            v = np.array(v).mean(0)
+            print(f"{name:34s} " + "  ".join(f"p{i}: {int(c[0])} / {c[1]:.2f} / {c[2]:.2f}" for i, c in enumerate(v)))
     a = np.array([[float(x) for x in r[2:]] for r in rows])
     print(f"mean over {len(rows)} launches: span {a[:, 0].mean():.2f} wg_avg {a[:, 1].mean():.2f} "
           f"wg_max {a[:, 2].mean():.2f} skew {a[:, 3].mean():.2f} gap {a[:, 4].mean():.2f} us")

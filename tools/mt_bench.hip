@@ -24,7 +24,7 @@ __device__ __forceinline__ void lds_barrier() {
 // NT threads, RUN consecutive words per thread, LDS ring of RW words (+ 1080 mirrored), STORE:
 // every word to out[n - 624]; LB: lds-only barriers.  Words [624, 624 + nwords) of the stream
 // whose first block is key.
-template <int NT, int RUN, int RW, bool STORE, bool LB>
+template <int NT, int RUN, int RW, bool STORE, bool LB, bool LIN = false>
 __global__ __launch_bounds__(NT) void k_tw(const uint32_t* __restrict__ key, uint32_t* __restrict__ out, int nwords) {
     constexpr int MIR = 1080;
     __shared__ uint32_t ring[RW + MIR];
@@ -67,7 +67,12 @@ __global__ __launch_bounds__(NT) void k_tw(const uint32_t* __restrict__ key, uin
 #pragma unroll
             for (int i = 0; i < RUN; ++i)
                 if (RUN == 1 || n + i < n1) {
-                    const uint32_t v = e[i] ^ mt_g(f[i], f[i + 1]) ^ mt_g(c[i], c[i + 1]) ^ mt_g(a[i], a[i + 1]);
+                    uint32_t v;
+                    if (LIN) {   // g is GF(2)-linear in its two operands: one g of the xors
+                        v = e[i] ^ mt_g(f[i] ^ c[i] ^ a[i], f[i + 1] ^ c[i + 1] ^ a[i + 1]);
+                    } else {
+                        v = e[i] ^ mt_g(f[i], f[i + 1]) ^ mt_g(c[i], c[i + 1]) ^ mt_g(a[i], a[i + 1]);
+                    }
                     put(n + i, v);
                     if (STORE) out[n + i - 624] = v;
                 }
@@ -90,10 +95,10 @@ struct HostMT {
     }
 };
 
-template <int NT, int RUN, int RW, bool STORE, bool LB>
+template <int NT, int RUN, int RW, bool STORE, bool LB, bool LIN = false>
 int run(const char* name, const uint32_t* dkey, uint32_t* dout, const std::vector<uint32_t>& ref, int nwords, hipStream_t s) {
     CK(hipMemsetAsync(dout, 0, (size_t)nwords * 4, s));
-    hipLaunchKernelGGL((k_tw<NT, RUN, RW, STORE, LB>), dim3(1), dim3(NT), 0, s, dkey, dout, nwords);
+    hipLaunchKernelGGL((k_tw<NT, RUN, RW, STORE, LB, LIN>), dim3(1), dim3(NT), 0, s, dkey, dout, nwords);
     CK(hipStreamSynchronize(s));
     std::vector<uint32_t> got(nwords);
     CK(hipMemcpy(got.data(), dout, (size_t)nwords * 4, hipMemcpyDeviceToHost));
@@ -102,10 +107,10 @@ int run(const char* name, const uint32_t* dkey, uint32_t* dout, const std::vecto
     for (int i = from; i < nwords; ++i) bad += got[i] != ref[624 + i];
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
-    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tw<NT, RUN, RW, STORE, LB>), dim3(1), dim3(NT), 0, s, dkey, dout, nwords);
+    for (int w = 0; w < 3; ++w) hipLaunchKernelGGL((k_tw<NT, RUN, RW, STORE, LB, LIN>), dim3(1), dim3(NT), 0, s, dkey, dout, nwords);
     const int reps = 20;
     CK(hipEventRecord(e0, s));
-    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tw<NT, RUN, RW, STORE, LB>), dim3(1), dim3(NT), 0, s, dkey, dout, nwords);
+    for (int r = 0; r < reps; ++r) hipLaunchKernelGGL((k_tw<NT, RUN, RW, STORE, LB, LIN>), dim3(1), dim3(NT), 0, s, dkey, dout, nwords);
     CK(hipEventRecord(e1, s));
     CK(hipEventSynchronize(e1));
     float ms = 0;
@@ -135,6 +140,10 @@ int main() {
     CK(hipMemcpy(dkey, ref.data(), 624 * 4, hipMemcpyHostToDevice));
     int bad = 0;
     bad += run<1024, 1, 32768, false, false>("1024 thr, 1 w/thr, 32K ring", dkey, dout, ref, nwords, s);
+    bad += run<1024, 1, 32768, false, false, true>("linear g, 1024 thr, 32K ring", dkey, dout, ref, nwords, s);
+    bad += run<640, 1, 2048, false, false, true>("linear g, 640 thr, 2K ring", dkey, dout, ref, nwords, s);
+    bad += run<320, 2, 2048, false, true, true>("linear g, 320 thr, 2 w/thr, ldsbar", dkey, dout, ref, nwords, s);
+    bad += run<640, 1, 2048, true, true, true>("linear g, 640 thr, 2K, store, ldsbar", dkey, dout, ref, nwords, s);
     bad += run<640, 1, 32768, false, false>("640 thr, 1 w/thr, 32K ring", dkey, dout, ref, nwords, s);
     bad += run<640, 1, 2048, false, false>("640 thr, 1 w/thr, 2K ring", dkey, dout, ref, nwords, s);
     bad += run<640, 1, 2048, false, true>("640 thr, 1 w/thr, 2K ring, ldsbar", dkey, dout, ref, nwords, s);
