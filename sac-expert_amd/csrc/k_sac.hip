@@ -755,42 +755,99 @@ __device__ __forceinline__ int xcd_tile(int b, int T) {
 // over the 4 waves) -- and the A tile [state columns of A | normalised actions] is staged in
 // LDS for the main loop.  Column tile 0 stores the rows' neglogp for q.head.  The same
 // arithmetic as k_actor_head, with the 16-lane row sums of the MFMA layout.
+// The prologue's operands, requested as one batch (head_pre_load) before anything else of the
+// launch so its arithmetic (head_pre_finish) can start while the GEMM operands are in flight
+struct HeadPre {
+    float xs[4], u, ls, am, ad, bias;
+    float4 pv[4];      // actor.fwd1's partial dots of the row's output `col` (parts)
+};
+__device__ __forceinline__ void head_pre_load(const HeadArgs& hd, const GemmProb& g, int m0, int64_t so, bool parts,
+                                              HeadPre& p) {
+    const int t = threadIdx.x, row = t >> 4, col = t & 15;
+    const int A = hd.A, Aout = hd.Aout, H1 = hd.H1, S = g.K - A;
+    HeadSeg sg = hd.seg[0];
+    reloc(sg, so);
+    const bool rok = m0 + row < g.M;
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.A, 0x7fffffffu);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p.xs[q] = bload(rx, boff(rok && col + 16 * q < S, (m0 + row) * g.lda + col + 16 * q));
+    const bool jok = col < A;
+    p.u = bload(rs(sg.noise), boff(jok && rok, (m0 + row - sg.r0) * A + col));
+    p.ls = bload(rs(sr(hd.logstd, so)), boff(jok && !hd.per_state_std, col));
+    p.am = bload(rs(sr(hd.a_mean, so)), boff(jok, col));
+    p.ad = bload(rs(sr(hd.a_den, so)), boff(jok, col));
+    const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(sr(hd.W3, so), 0x7fffffffu);
+    p.bias = bload(rw3, boff(col < Aout, H1 * Aout + col));
+    if (parts) {
+        // Ha2 . W3 from actor.fwd1's per-column-tile partials: 4 float4 per (row, output)
+        const __amdgpu_buffer_rsrc_t rp = rs(sr(hd.part, so));
+        const bool pok = rok && col < Aout;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p.pv[i] = bload4(rp, boff(pok && 4 * i < hd.tq, ((m0 + row) * Aout + col) * hd.tq + 4 * i));
+    }
+}
+__device__ __forceinline__ float head_pre_mu(const HeadPre& p) {
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        v = v + p.pv[i].x; v = v + p.pv[i].y; v = v + p.pv[i].z; v = v + p.pv[i].w;
+    }
+    return v + p.bias;
+}
+// evaluate() of the row's action col from mu, the neglogp store and the A tile in LDS
+__device__ __forceinline__ void head_pre_finish(const HeadArgs& hd, const GemmProb& g, int m0, int tn,
+                                                float (&As)[16][68], const HeadPre& p, float mu, int64_t so) {
+    const int t = threadIdx.x, lane = t & 63;
+    const int row = t >> 4, col = t & 15;
+    const int A = hd.A, S = g.K - A;
+    HeadSeg sg = hd.seg[0];
+    reloc(sg, so);
+    const bool rok = m0 + row < g.M;
+    const bool jok = col < A;
+    // per_state_std: logstd_raw of action j sits in column A + j of the same row (same 16 lanes)
+    const float lv = __shfl(mu, (lane & ~15) | min(col + A, 15), 64);
+    const float lraw = hd.per_state_std ? lv : p.ls;
+    float nv = 0.f, nc = 0.f, pin = 0.f;
+    if (jok) {
+        const float l = fminf(fmaxf(lraw, -5.f), 2.f);
+        const float sd = expf(l);
+        const float x = mu + sd * p.u;
+        const float th = tanhf(x);
+        const float pi = hd.lim * th;
+        const float z = (x - mu) / expf(l);
+        nv = z * z + 2.f * l + LOG2PI_F;
+        nc = 2.f * ((LN2_F - x) - softplus_f(-2.f * x));
+        pin = (pi - p.am) / p.ad;
+    }
+    nv += __shfl_xor(nv, 8, 16);
+    nv += __shfl_xor(nv, 4, 16);
+    nv += __shfl_xor(nv, 2, 16);
+    nv += __shfl_xor(nv, 1, 16);
+    nc += __shfl_xor(nc, 8, 16);
+    nc += __shfl_xor(nc, 4, 16);
+    nc += __shfl_xor(nc, 2, 16);
+    nc += __shfl_xor(nc, 1, 16);
+    if (tn == 0 && col == 0 && rok && sg.nlp_out != nullptr) sg.nlp_out[m0 + row - sg.r0] = 0.5f * nv + nc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        if (col + 16 * q < S) As[row][col + 16 * q] = p.xs[q];
+    if (jok) As[row][S + col] = pin;
+}
+
 template <bool SYNC = true>
 __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb& g, int m0, int tn,
                                               float (&As)[16][68], float (&red)[4][4][64], int64_t so) {
     const int t = threadIdx.x, wave = t >> 6, lane = t & 63, r = lane & 15, grp = lane >> 4;
     const int row = t >> 4, col = t & 15;
-    const int A = hd.A, Aout = hd.Aout, H1 = hd.H1, S = g.K - A;
-    HeadSeg sg = hd.seg[0];
-    reloc(sg, so);
-    const bool rok = m0 + row < g.M;
+    const int Aout = hd.Aout, H1 = hd.H1;
     // everything the prologue reads is requested first
-    const __amdgpu_buffer_rsrc_t rx = make_rsrc(g.A, 0x7fffffffu);
-    float xs[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) xs[q] = bload(rx, boff(rok && col + 16 * q < S, (m0 + row) * g.lda + col + 16 * q));
-    const bool jok = col < A;
-    const float u = bload(rs(sg.noise), boff(jok && rok, (m0 + row - sg.r0) * A + col));
-    const float ls = bload(rs(sr(hd.logstd, so)), boff(jok && !hd.per_state_std, col));
-    const float am = bload(rs(sr(hd.a_mean, so)), boff(jok, col));
-    const float ad = bload(rs(sr(hd.a_den, so)), boff(jok, col));
-    const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(sr(hd.W3, so), 0x7fffffffu);
-    const float bias = bload(rw3, boff(col < Aout, H1 * Aout + col));
+    HeadPre p;
+    head_pre_load(hd, g, m0, so, hd.part != nullptr, p);
     float mu;
     if (hd.part != nullptr) {
-        // Ha2 . W3 from actor.fwd1's per-column-tile partials: 4 float4 per (row, output)
-        const __amdgpu_buffer_rsrc_t rp = rs(sr(hd.part, so));
-        const bool pok = rok && col < Aout;
-        float4 pv[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) pv[i] = bload4(rp, boff(pok && 4 * i < hd.tq, ((m0 + row) * Aout + col) * hd.tq + 4 * i));
-        float v = 0.f;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            v = v + pv[i].x; v = v + pv[i].y; v = v + pv[i].z; v = v + pv[i].w;
-        }
-        mu = v + bias;
+        mu = head_pre_mu(p);
     } else {
+        const __amdgpu_buffer_rsrc_t rw3 = make_rsrc(sr(hd.W3, so), 0x7fffffffu);
         const __amdgpu_buffer_rsrc_t rh = make_rsrc(sr(hd.H2, so), 0x7fffffffu);
         const int nIt = H1 >> 4, per = (nIt + 3) >> 2, i0 = wave * per, i1 = min(nIt, i0 + per);
         const bool hm = m0 + r < g.M, wn = r < Aout;
@@ -823,37 +880,10 @@ __device__ __forceinline__ void head_prologue(const HeadArgs& hd, const GemmProb
         float v = red[0][R][L] + red[1][R][L];
         v = v + red[2][R][L];
         v = v + red[3][R][L];
-        mu = v + bias;
+        mu = v + p.bias;
     }
-    // per_state_std: logstd_raw of action j sits in column A + j of the same row (same 16 lanes)
-    const float lv = __shfl(mu, (lane & ~15) | min(col + A, 15), 64);
-    const float lraw = hd.per_state_std ? lv : ls;
-    float nv = 0.f, nc = 0.f, pin = 0.f;
-    if (jok) {
-        const float l = fminf(fmaxf(lraw, -5.f), 2.f);
-        const float sd = expf(l);
-        const float x = mu + sd * u;
-        const float th = tanhf(x);
-        const float pi = hd.lim * th;
-        const float z = (x - mu) / expf(l);
-        nv = z * z + 2.f * l + LOG2PI_F;
-        nc = 2.f * ((LN2_F - x) - softplus_f(-2.f * x));
-        pin = (pi - am) / ad;
-    }
-    nv += __shfl_xor(nv, 8, 16);
-    nv += __shfl_xor(nv, 4, 16);
-    nv += __shfl_xor(nv, 2, 16);
-    nv += __shfl_xor(nv, 1, 16);
-    nc += __shfl_xor(nc, 8, 16);
-    nc += __shfl_xor(nc, 4, 16);
-    nc += __shfl_xor(nc, 2, 16);
-    nc += __shfl_xor(nc, 1, 16);
-    if (tn == 0 && col == 0 && rok && sg.nlp_out != nullptr) sg.nlp_out[m0 + row - sg.r0] = 0.5f * nv + nc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        if (col + 16 * q < S) As[row][col + 16 * q] = xs[q];
-    if (jok) As[row][S + col] = pin;
-    if constexpr (SYNC) __syncthreads();   // else the caller's (k_fwd2: threads >= 256 skip the body)
+    head_pre_finish(hd, g, m0, tn, As, p, mu, so);
+    if constexpr (SYNC) __syncthreads();
 }
 
 // actor.head.bwd folded into actor.bwd1 (rowk 4): the policy-row work of k_actor_bwd for the
@@ -2327,6 +2357,23 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 // GATHER (rowk 6, the fit): layer 0's A rows are replay records gathered by the step's minibatch indices
 // and normalised on load (k_gemm rowk 6's arithmetic); wave 0 of column group 0 stores them to X and the
 // group's threads store the rows' targets T (get_loss :286-296) -- model.gather+fwd0+fwd1 in one launch
+// SACX_FWD2_STAMP (diagnostic builds): the end stamp of each workgroup is taken after phase P
+// instead -- 1: layer 0 done (its operands and, for target tiles, the head prologue), 2: layer 1's
+// MFMAs reduced
+#ifndef SACX_FWD2_STAMP
+#define SACX_FWD2_STAMP 0
+#endif
+
+#define F2_STAMP(P)                                                                          \
+    do {                                                                                     \
+        if (SACX_FWD2_STAMP == (P) && ga.ktime != nullptr) {                                 \
+            __syncthreads();                                                                 \
+            if (threadIdx.x == 0) {                                                          \
+                ga.ktime[2 * ktime_wg()] = t0;                                               \
+                ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();             \
+            }                                                                                \
+        }                                                                                    \
+    } while (0)
 template <int VEC, int NW, bool HEAD, int FIN = 0, int H0X = 256, bool GATHER = false>
 __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArgs ga) {   // (min waves per SIMD)
     // (FIN: ga.has_final as a template parameter -- each variant holds one finalisation form)
@@ -2370,7 +2417,11 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
     const int nIt0 = (g0.K + 15) >> 4;       // <= 2 (host)
     const int per1 = (H0 + 63) >> 6;         // layer-1 slabs per K quarter (H0 = 64 per1)
 
-    // ---- every operand requested up front
+    // ---- every operand requested up front: the target tiles' head prologue first (its arithmetic
+    // then overlaps the weights' round trip)
+    HeadPre hpre;
+    if constexpr (HEAD)
+        if (headp && threadIdx.x < 256) head_pre_load(ga.head, g0, m0, 0, true, hpre);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(g0.A, 0x7fffffffu);
     const __amdgpu_buffer_rsrc_t rw0 = make_rsrc(g0.B, 0x7fffffffu);
     const __amdgpu_buffer_rsrc_t rw1 = make_rsrc(g1.B, 0x7fffffffu);
@@ -2484,9 +2535,8 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
         // group 0 stores the rows' neglogp for q.head (host: the head's partial dots exist, so the
         // prologue has no barrier of its own)
         __shared__ float As[16][68];
-        __shared__ float hred[4][4][64];
         if (headp) {                          // uniform
-            if (threadIdx.x < 256) head_prologue<false>(ga.head, g0, m0, cg, As, hred, 0);
+            if (threadIdx.x < 256) head_pre_finish(ga.head, g0, m0, cg, As, hpre, head_pre_mu(hpre), 0);
             __syncthreads();
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
@@ -2524,6 +2574,7 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
             if (cg == 0 && mm < g0.M && nc < H0) st_out(&g0.C[(size_t)mm * g0.ldc + nc], h);
         }
     }
+    F2_STAMP(1);
     __syncthreads();
 
     // ---- layer 1: K quarter kq (slabs kq * per1 + u), A from LDS, CTW column tiles
@@ -2550,6 +2601,7 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
         for (int q = 0; q < 4; ++q) red2[kq][CTW * ch + j2][q][lane] = acc[q];
     }
     __syncthreads();
+    F2_STAMP(2);
     // (row, col) lives in lane (row >> 2) * 16 + col, register row & 3 of each quarter's tile
     const int L = ((row >> 2) << 4) | col, R = row & 3;
     const int mm = m0 + row;
@@ -2582,7 +2634,7 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
         }
         if (mm < g1.M && nn < N1 && g1.C != nullptr) st_out(&g1.C[(size_t)mm * g1.ldc + nn], x);
     }
-    if (ga.ktime != nullptr) {
+    if (SACX_FWD2_STAMP == 0 && ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
             ga.ktime[2 * ktime_wg()] = t0;
@@ -2707,7 +2759,9 @@ __device__ __forceinline__ void block_rank2(bool fa, bool fb, int* wtot, int& ra
 // the state's key) sits at ring[q % RNG_RW].  MT19937 as a word recurrence is
 //   x[n] = x[n-227] ^ g(n-624),   g(m) = twist(x[m], x[m+1])      (n >= 624)
 // and unrolled three times
-//   x[n] = x[n-681] ^ g(n-624) ^ g(n-851) ^ g(n-1078),
+//   x[n] = x[n-681] ^ g(n-624) ^ g(n-851) ^ g(n-1078)
+//        = x[n-681] ^ twist(x[n-624] ^ x[n-851] ^ x[n-1078], x[n-623] ^ x[n-850] ^ x[n-1077])
+// (twist is linear over GF(2) in its two words, so the three are one twist of the xors),
 // whose operands all lie below n-622: 623 consecutive words are independent, so the whole
 // workgroup produces 623 words per step with one barrier (the first 454 words after the key
 // use the 227-wide form, which needs no history before it).  Consumption is one candidate
@@ -2779,7 +2833,8 @@ __device__ void rng_twist(RngShared& S, int w0, int w1) {
 #pragma unroll
             for (int i = 0; i < RNG_RUN; ++i)
                 if (RNG_RUN == 1 || n + i < n1)
-                    rng_put(S, n + i, e[i] ^ mt_g(f[i], f[i + 1]) ^ mt_g(c[i], c[i + 1]) ^ mt_g(a[i], a[i + 1]));
+                    // g is GF(2)-linear in its two words: the three twists as one of the xors
+                    rng_put(S, n + i, e[i] ^ mt_g(f[i] ^ c[i] ^ a[i], f[i + 1] ^ c[i + 1] ^ a[i + 1]));
         }
         __syncthreads();
         n0 = n1;

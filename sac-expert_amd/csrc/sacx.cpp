@@ -1882,6 +1882,7 @@ struct KTimeMap {
     std::vector<std::string> names;
     std::vector<char> is_gemm;
     std::vector<std::pair<int, int>> rowspan;   // [first, end) workgroups that run row kernels
+    std::vector<std::vector<int>> cls;          // k_fwd2: first workgroup of each problem pair's tiles
     bool rows = false;      // also stamp the row kernels (k_actor_head, k_actor_bwd): dump only
 };
 
@@ -1929,6 +1930,12 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 if (L.kind != Launch::GEMM) kt->rowspan.push_back({0, 0});
                 else if (C.gemm.rowk == 3) kt->rowspan.push_back({fin_wg, fin_wg + C.gemm.row_blocks});
                 else kt->rowspan.push_back({C.gemm.total_tiles + fin_wg, nwg1});
+                std::vector<int> cb;
+                if (L.kind == Launch::GEMM && C.gemm.mode == GM_FWD2) {
+                    const int nn = C.gemm.nprob / 2, r0 = C.gemm.rowk == 3 ? C.gemm.row_blocks : 0;
+                    for (int i = 0; i < nn; ++i) cb.push_back(r0 + C.gemm.probs[nn + i].tile_begin);
+                }
+                kt->cls.push_back(cb);
                 kt->used += 2 * nwg;
             }
             enqueue(C, h, st);
@@ -3729,6 +3736,29 @@ int sacx_time_kernels(sacx_handle* h, const char* kernel, int32_t n_replays, dou
             prev_hi = hi;
         }
         if (dump) std::fclose(dump);
+        // SACX_KTIME_CLASSES=<file>: k_fwd2 launches' workgroups by problem pair (mean / max us)
+        if (const char* path = std::getenv("SACX_KTIME_CLASSES"); path && r == n_replays - 1 && h->seeds == 1) {
+            if (FILE* f = std::fopen(path, "a")) {
+                for (size_t si = 0; si < kt.spans.size(); ++si) {
+                    const auto& cb = kt.cls[si];
+                    if (cb.empty()) continue;
+                    const auto& sp = kt.spans[si];
+                    std::fprintf(f, "%s", kt.names[si].c_str());
+                    for (size_t c = 0; c < cb.size(); ++c) {
+                        const int b0 = cb[c], b1 = c + 1 < cb.size() ? cb[c + 1] : sp.second;
+                        double su = 0.0, mx = 0.0;
+                        for (int b = b0; b < b1; ++b) {
+                            const double d = (double)(host[sp.first + 2 * b + 1] - host[sp.first + 2 * b]) * 0.01;
+                            su += d;
+                            mx = std::max(mx, d);
+                        }
+                        std::fprintf(f, ",p%zu:%d:%.2f:%.2f", c, b1 - b0, su / std::max(1, b1 - b0), mx);
+                    }
+                    std::fprintf(f, "\n");
+                }
+                std::fclose(f);
+            }
+        }
     }
     if (g) (void)hipGraphExecDestroy(g);
     (void)hipFree(kt.base);

@@ -162,9 +162,9 @@ __host__ __device__ inline int wbf_pos(int k, int per) {
     return (w * ((per + 1) >> 1) + (i >> 1)) * 32 + ((k >> 2) & 3) * 8 + (i & 1) * 4 + (k & 3);
 }
 
+#define WBF_MAXM 12
 // k_wbf_refresh: every shadow rebuilt from its fp32 weights (at each sacx_sac_step entry, so host
 // writes of the parameters reach it; the Adam epilogues keep it current inside a step)
-#define WBF_MAXM 12
 struct WbfArgs {
     const float* W[WBF_MAXM];    // [K x N] row-major (the first K rows of W_ext)
     uint16_t* S[WBF_MAXM];       // [N x ld]

@@ -296,8 +296,14 @@ def test_fused_forward_pair_bit_identical(gpu_available, monkeypatch, act, B, ea
             assert (pair in names) == (fused == "1"), names
         eng.rng_set_state(np.random.RandomState(6).get_state())
         eng.step(19, eager=eager)
+        # a host write of the weights between calls
+        for net in ("actor", "q1", "t0"):
+            w = eng.get_net(net)
+            w[1] = w[1] * np.float32(0.75)
+            eng.set_net(net, w)
+        eng.step(6, eager=eager)
         eng.sync()
-        outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy()))
+        outs.append((eng.stats(25).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy()))
         eng.close()
     for o in outs[1:]:
         for a, b in zip(outs[0], o):

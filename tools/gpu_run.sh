@@ -17,9 +17,16 @@ for step in "$@"; do
   log=$OUT/$n-$name.log
   case $name in
     tests)
-      sel=${arg:-tests}
-      timeout -k 10 1100 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
-          ${sel//,/ } > "$log" 2>&1
+      # tests=<comma-separated paths / options>[|<-k expression, spaces allowed>]
+      sel=${arg:-tests}; kx=""
+      case $sel in *"|"*) kx=${sel#*|}; sel=${sel%%|*} ;; esac
+      if [ -n "$kx" ]; then
+        timeout -k 10 1100 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+            ${sel//,/ } -k "$kx" > "$log" 2>&1
+      else
+        timeout -k 10 1100 python -u -m pytest -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider \
+            ${sel//,/ } > "$log" 2>&1
+      fi
       rc=$?; echo "[$n tests] rc=$rc $(tail -n 1 "$log")" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1
@@ -70,6 +77,10 @@ for step in "$@"; do
     rngbench)
       timeout -k 10 120 ./tools/rng_bench > "$log" 2>&1
       rc=$?; echo "[$n rngbench] rc=$rc"; cat "$log" ;;
+    ktimev)     # ktime with a variant library: ktimev=<config>:<tools/libvar name>
+      cfg=${arg%%:*}; var=${arg#*:}
+      SACX_LIBPATH=$PWD/tools/libvar/libsacx_$var.so timeout -k 10 200 python tools/ktime_dump.py "$cfg" > "$log" 2>&1
+      rc=$?; echo "[$n ktimev $arg] rc=$rc $(tail -n 1 "$log")" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;

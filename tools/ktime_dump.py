@@ -39,11 +39,12 @@ def main():
     for r in rows:
         agg.setdefault(r[0], []).append([float(x) for x in r[2:]])
     print(f"\n{'launch (mean over updates)':34s} {'n':>5s} {'span':>6s} {'wg_avg':>6s} {'wg_max':>6s} {'skew':>6s} "
-          f"{'gap':>6s} {'row_avg':>7s} {'row_max':>7s}")
+          f"{'gap':>6s} {'row_avg':>7s} {'row_max':>7s} {'gap_med':>7s} {'gap_p90':>7s}")
     for name, v in agg.items():
-        v = np.array(v).mean(0)
+        va = np.array(v)
+        v = va.mean(0)
         print(f"{name:34s} {len(agg[name]):5d} {v[0]:6.2f} {v[1]:6.2f} {v[2]:6.2f} {v[3]:6.2f} {v[4]:6.2f} "
-              f"{v[5]:7.2f} {v[6]:7.2f}")
+              f"{v[5]:7.2f} {v[6]:7.2f} {np.median(va[:, 4]):7.2f} {np.percentile(va[:, 4], 90):7.2f}")
     # k_fwd2 launches: workgroups per problem pair (n:mean:max us), averaged over the graph's updates
     cls = {}
     if os.path.exists(cpath):
