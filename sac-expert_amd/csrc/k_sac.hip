@@ -1251,7 +1251,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
 }
 
 template <int MODE, int VEC, int ROWK, int NQ, bool BF = false, bool PK = false, bool T32 = false>
-__device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
+__device__ __forceinline__ void gemm_core(const KHdr kh, const GemmArgs& ga) {
     constexpr bool AKC = (MODE != GM_DW);
     constexpr bool BKC = (MODE == GM_DX);
     __shared__ float red[T32 ? 16 : 4][4][64];
@@ -1260,15 +1260,28 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
     // Every scalar that decides this workgroup's role and problem is read in ONE batch of
     // kernarg loads: left alone, the compiler loads each behind its own branch, a chain of
     // dependent scalar round trips in front of the first operand load.
-    const int has_final = ga.has_final, row_blocks = ga.row_blocks, total_tiles = ga.total_tiles;
-    const int xcd_map = ga.xcd_map, nprob = ga.nprob;
-    const int64_t p_stride = ga.p_stride;
+    // With a valid launch header (KHdr) they are already in SGPRs at dispatch.
+    int has_final, row_blocks, total_tiles, xcd_map, nprob;
     int tb[GEMM_MAXP];
-#pragma unroll
-    for (int i = 0; i < GEMM_MAXP; ++i) tb[i] = ga.probs[i].tile_begin;
     static_assert(GEMM_MAXP == 8, "one pin per problem's tile_begin");
-    asm volatile("" ::"s"(has_final), "s"(row_blocks), "s"(total_tiles), "s"(xcd_map), "s"(nprob), "s"(p_stride),
-                 "s"(tb[1]), "s"(tb[2]), "s"(tb[3]), "s"(tb[4]), "s"(tb[5]), "s"(tb[6]), "s"(tb[7]));
+    const uint32_t kf = khdr_flags(kh);
+    if (kf & 0x80u) {
+        total_tiles = (int)khdr_field(kh, 0);
+        row_blocks = (int)khdr_field(kh, 1);
+        tb[0] = 0;
+#pragma unroll
+        for (int i = 1; i < GEMM_MAXP; ++i) tb[i] = (int)khdr_field(kh, i + 1);
+        nprob = (int)(kf & 15u);
+        has_final = (int)((kf >> 4) & 3u);
+        xcd_map = (int)((kf >> 6) & 1u);
+    } else {
+        has_final = ga.has_final; row_blocks = ga.row_blocks; total_tiles = ga.total_tiles;
+        xcd_map = ga.xcd_map; nprob = ga.nprob;
+#pragma unroll
+        for (int i = 0; i < GEMM_MAXP; ++i) tb[i] = ga.probs[i].tile_begin;
+        asm volatile("" ::"s"(has_final), "s"(row_blocks), "s"(total_tiles), "s"(xcd_map), "s"(nprob),
+                     "s"(tb[1]), "s"(tb[2]), "s"(tb[3]), "s"(tb[4]), "s"(tb[5]), "s"(tb[6]), "s"(tb[7]));
+    }
     // the folded alpha.final of the previous update is workgroup 0: dispatched first, its
     // serial reductions overlap the tiles instead of trailing them
     int tile = (int)blockIdx.x - (has_final ? 1 : 0);
@@ -1856,12 +1869,13 @@ __device__ __forceinline__ void gemm_core(const GemmArgs& ga) {
                           : SACX_T32_DW_WGS)                                                                 \
          : 1)
 template <int MODE, int VEC, int ROWK = 0, int NQ = 4, bool BF = false, bool PK = false, bool T32 = false>
-__global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(GemmArgs ga) {
+__global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3,
+                                                           GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SACX_GEMM_PHASES
     if (threadIdx.x == 0) g_gemm_ph[blockIdx.x][0] = t0;
 #endif
-    gemm_core<MODE, VEC, ROWK, NQ, BF, PK, T32>(ga);
+    gemm_core<MODE, VEC, ROWK, NQ, BF, PK, T32>(KHdr{{h0, h1, h2, h3}}, ga);
     GEMM_PH(4);
     if (ga.ktime != nullptr) {
         __syncthreads();
@@ -1875,9 +1889,9 @@ __global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(GemmArgs ga) {
 // q.fwd0 with the actor head folded in: 1,024 tiles + 128 head-row workgroups must be
 // resident at once (5 workgroups per CU), so registers are capped at 96 per lane
 template <int VEC, int NQ, bool BF, bool PK = false>
-__global__ __launch_bounds__(256, 5) void k_gemm_head(GemmArgs ga) {
+__global__ __launch_bounds__(256, 5) void k_gemm_head(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3, GemmArgs ga) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    gemm_core<GM_FWD, VEC, 3, NQ, BF, PK>(ga);
+    gemm_core<GM_FWD, VEC, 3, NQ, BF, PK>(KHdr{{h0, h1, h2, h3}}, ga);
     if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1974,7 +1988,7 @@ __device__ __forceinline__ void dwl_issue(const float* base, int ld, int k0, int
 // NH: 16-column halves per tile -- 2: 32x32 tiles, 1: 32x16 (twice the workgroups, two or three
 // per CU: more waves per SIMD to hide each slab's non-MFMA instructions)
 template <bool BF, bool PK, int NH>
-__global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
+__global__ __launch_bounds__(256, 2) void k_dwl(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3, GemmArgs ga) {
     constexpr int STG = dwl_stg<NH>(), NS = 2 * NH;     // stage floats; sub-tiles per thread
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef SACX_GEMM_PHASES
@@ -1982,12 +1996,24 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
 #endif
     __shared__ float lds[4 * SACX_DWL_NST * STG];    // the one LDS object (staging, then reduction)
     const int64_t so = PK ? seed_off(ga.sstride) : 0;
-    const int total_tiles = ga.total_tiles, xcd_map = ga.xcd_map, nprob = ga.nprob;
+    const KHdr kh{{h0, h1, h2, h3}};
+    int total_tiles, xcd_map, nprob;
     int tb[GEMM_MAXP];
+    const uint32_t kf = khdr_flags(kh);
+    if (kf & 0x80u) {            // the launch header (gemm_core)
+        total_tiles = (int)khdr_field(kh, 0);
+        tb[0] = 0;
 #pragma unroll
-    for (int i = 0; i < GEMM_MAXP; ++i) tb[i] = ga.probs[i].tile_begin;
-    asm volatile("" ::"s"(total_tiles), "s"(xcd_map), "s"(nprob), "s"(tb[1]), "s"(tb[2]), "s"(tb[3]), "s"(tb[4]),
-                 "s"(tb[5]), "s"(tb[6]), "s"(tb[7]));
+        for (int i = 1; i < GEMM_MAXP; ++i) tb[i] = (int)khdr_field(kh, i + 1);
+        nprob = (int)(kf & 15u);
+        xcd_map = (int)((kf >> 6) & 1u);
+    } else {
+        total_tiles = ga.total_tiles; xcd_map = ga.xcd_map; nprob = ga.nprob;
+#pragma unroll
+        for (int i = 0; i < GEMM_MAXP; ++i) tb[i] = ga.probs[i].tile_begin;
+        asm volatile("" ::"s"(total_tiles), "s"(xcd_map), "s"(nprob), "s"(tb[1]), "s"(tb[2]), "s"(tb[3]), "s"(tb[4]),
+                     "s"(tb[5]), "s"(tb[6]), "s"(tb[7]));
+    }
     int tile = (int)blockIdx.x;
     if (xcd_map) tile = xcd_tile(tile, total_tiles);
     int p = 0;
@@ -2225,8 +2251,11 @@ __global__ __launch_bounds__(256, 2) void k_dwl(GemmArgs ga) {
     }
 }
 
+#define KH_ARGS kh.h[0], kh.h[1], kh.h[2], kh.h[3], a
+
 template <bool PK, bool T32>
 static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
+    const KHdr kh = khdr_of(a);
     const unsigned z = seeds_z(a.nseeds);
     const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0) + (a.has_mfinal ? 1 : 0), 1, z), block(256);
     switch (a.mode) {
@@ -2236,44 +2265,44 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
             const bool h8 = a.head.H1 > 256;
 #define SACX_FH(V, Q)                                                                               \
     do {                                                                                           \
-        if (a.bf16) hipLaunchKernelGGL((k_gemm_head<V, Q, true, PK>), gh, block, 0, s, a);              \
-        else hipLaunchKernelGGL((k_gemm_head<V, Q, false, PK>), gh, block, 0, s, a);                   \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm_head<V, Q, true, PK>), gh, block, 0, s, KH_ARGS);              \
+        else hipLaunchKernelGGL((k_gemm_head<V, Q, false, PK>), gh, block, 0, s, KH_ARGS);                   \
     } while (0)
             if (a.vec) { if (h8) SACX_FH(1, 8); else SACX_FH(1, 4); }
             else { if (h8) SACX_FH(0, 8); else SACX_FH(0, 4); }
 #undef SACX_FH
         } else if (a.rowk == 5) {          // actor.fwd1 (+alpha) writing the head partials
             if (a.bf16) {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, true, PK, T32>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, true, PK, T32>), grid, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
             } else {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, false, PK, T32>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, false, PK, T32>), grid, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 5, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 5, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
             }
         } else if (a.rowk == 6) {          // model.fwd0 of the fit, gathering its rows (one seed, 16x16)
             if constexpr (!PK && !T32) {
                 if (a.bf16) {
-                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, true, false, false>), grid, block, 0, s, a);
-                    else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, true, false, false>), grid, block, 0, s, a);
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, true, false, false>), grid, block, 0, s, KH_ARGS);
+                    else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, true, false, false>), grid, block, 0, s, KH_ARGS);
                 } else {
-                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, false, false, false>), grid, block, 0, s, a);
-                    else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, false, false, false>), grid, block, 0, s, a);
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 6, 4, false, false, false>), grid, block, 0, s, KH_ARGS);
+                    else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 6, 4, false, false, false>), grid, block, 0, s, KH_ARGS);
                 }
             }
         } else if (a.rowk == 8) {          // with world-model head rows (mse problems)
             if (a.bf16) {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 8, 4, true, PK, T32>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 8, 4, true, PK, T32>), grid, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 8, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 8, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
             } else {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 8, 4, false, PK, T32>), grid, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 8, 4, false, PK, T32>), grid, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 8, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 8, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
             }
         } else if (a.bf16) {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK, T32>), grid, block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
         } else {
-            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, false, PK, T32>), grid, block, 0, s, a);
-            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, false, PK, T32>), grid, block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_gemm<GM_FWD, 1, 0, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
+            else hipLaunchKernelGGL((k_gemm<GM_FWD, 0, 0, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
         }
         break;
     case GM_DX: {
@@ -2281,26 +2310,26 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
         const bool q8 = a.rowk && a.qh.H1 > 256;
 #define SACX_DX(V, R, Q)                                                                            \
     do {                                                                                           \
-        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK, T32>), gx, block, 0, s, a);          \
-        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK, T32>), gx, block, 0, s, a);                      \
+        if (a.bf16) hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, true, PK, T32>), gx, block, 0, s, KH_ARGS);          \
+        else hipLaunchKernelGGL((k_gemm<GM_DX, V, R, Q, false, PK, T32>), gx, block, 0, s, KH_ARGS);                      \
     } while (0)
         if (a.rowk == 7) {                 // model.bwd1 with model.bwd2 folded in (one seed, 16x16)
             if constexpr (!PK && !T32) {
                 if (a.bf16) {
-                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 7, 4, true, false, false>), gx, block, 0, s, a);
-                    else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 7, 4, true, false, false>), gx, block, 0, s, a);
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 7, 4, true, false, false>), gx, block, 0, s, KH_ARGS);
+                    else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 7, 4, true, false, false>), gx, block, 0, s, KH_ARGS);
                 } else {
-                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 7, 4, false, false, false>), gx, block, 0, s, a);
-                    else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 7, 4, false, false, false>), gx, block, 0, s, a);
+                    if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 7, 4, false, false, false>), gx, block, 0, s, KH_ARGS);
+                    else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 7, 4, false, false, false>), gx, block, 0, s, KH_ARGS);
                 }
             }
         } else if (a.rowk == 4) {                 // actor.bwd1 with actor.head.bwd folded in (16x16 only)
             if (a.bf16) {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, true, PK, false>), gx, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, true, PK, false>), gx, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, true, PK, false>), gx, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, true, PK, false>), gx, block, 0, s, KH_ARGS);
             } else {
-                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, false, PK, false>), gx, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, false, PK, false>), gx, block, 0, s, a);
+                if (a.vec) hipLaunchKernelGGL((k_gemm<GM_DX, 1, 4, 4, false, PK, false>), gx, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_DX, 0, 4, 4, false, PK, false>), gx, block, 0, s, KH_ARGS);
             }
         } else if (a.rowk == 1) {
             if (a.vec) { if (q8) SACX_DX(1, 1, 8); else SACX_DX(1, 1, 4); }
@@ -2320,16 +2349,16 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
             const dim3 gh(a.total_tiles + a.row_blocks, 1, z);
             const bool h8 = a.head.H1 > 256;
             if (a.bf16) {
-                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true, PK, T32>), gh, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true, PK, T32>), gh, block, 0, s, a);
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, true, PK, T32>), gh, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, true, PK, T32>), gh, block, 0, s, KH_ARGS);
             } else {
-                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, false, PK, T32>), gh, block, 0, s, a);
-                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, false, PK, T32>), gh, block, 0, s, a);
+                if (h8) hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 8, false, PK, T32>), gh, block, 0, s, KH_ARGS);
+                else hipLaunchKernelGGL((k_gemm<GM_DW, 0, 3, 4, false, PK, T32>), gh, block, 0, s, KH_ARGS);
             }
         } else if (a.bf16) {
-            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true, PK, T32>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, true, PK, T32>), grid, block, 0, s, KH_ARGS);
         } else {
-            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, false, PK, T32>), grid, block, 0, s, a);
+            hipLaunchKernelGGL((k_gemm<GM_DW, 0, 0, 4, false, PK, T32>), grid, block, 0, s, KH_ARGS);
         }
     }
 }
@@ -2359,7 +2388,7 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 // group's threads store the rows' targets T (get_loss :286-296) -- model.gather+fwd0+fwd1 in one launch
 // SACX_FWD2_STAMP (diagnostic builds): the end stamp of each workgroup is taken after phase P
 // instead -- 1: layer 0 done (its operands and, for target tiles, the head prologue), 2: layer 1's
-// MFMAs reduced
+// MFMAs reduced, 3: the problem's kernel arguments loaded
 #ifndef SACX_FWD2_STAMP
 #define SACX_FWD2_STAMP 0
 #endif
@@ -2369,11 +2398,15 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
         if (SACX_FWD2_STAMP == (P) && ga.ktime != nullptr) {                                 \
             __syncthreads();                                                                 \
             if (threadIdx.x == 0) {                                                          \
-                ga.ktime[2 * ktime_wg()] = t0;                                               \
-                ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();             \
+                ga.ktime[2 * f2_slot(ga, g1, lt, HEAD)] = t0;                                \
+                ga.ktime[2 * f2_slot(ga, g1, lt, HEAD) + 1] = __builtin_amdgcn_s_memrealtime(); \
             }                                                                                \
         }                                                                                    \
     } while (0)
+// k_fwd2's timestamp slot of tile lt of a pair (the host's linear order: head rows, then each pair's tiles)
+__device__ __forceinline__ int f2_slot(const GemmArgs& ga, const GemmProb& g1, int lt, bool head) {
+    return (head ? ga.row_blocks : 0) + g1.tile_begin + lt;
+}
 template <int VEC, int NW, bool HEAD, int FIN = 0, int H0X = 256, bool GATHER = false>
 __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArgs ga) {   // (min waves per SIMD)
     // (FIN: ga.has_final as a template parameter -- each variant holds one finalisation form)
@@ -2383,29 +2416,34 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     __shared__ float hs[16][H0X + 4];
     __shared__ float red2[4][4][4][64];    // [K quarter][column tile][q][lane]
-    const int nnet = ga.nprob >> 1;
-    int tile = (int)blockIdx.x;
+    // grid (tiles of the largest pair, pairs (+ 1)): the problem pair is blockIdx.y and launch_gemm
+    // interleaves the pairs' problems (layer 0 of pair p at 2p, layer 1 at 2p + 1), so a workgroup's
+    // arguments arrive in ONE scalar round trip (no tile-range table to read first)
+    int p = (int)blockIdx.y;
     if constexpr (HEAD) {
-        if (tile < ga.row_blocks) {           // actor-head rows, dispatched first: NW / 4 blocks of 4
+        if (p == 0) {                         // actor-head rows, dispatched first: NW / 4 blocks of 4
+            const int tile = (int)blockIdx.x;
+            if (tile >= ga.row_blocks) return;
             const int blk = ga.head_block0 + (NW / 4) * tile;
             actor_head_body<4, 0, FIN>(ga.head, ga.hfin, blk, 0, ga.fin);
             if (ga.ktime != nullptr) {
                 __syncthreads();
                 if (threadIdx.x == 0) {
-                    ga.ktime[2 * ktime_wg()] = t0;
-                    ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
+                    ga.ktime[2 * tile] = t0;
+                    ga.ktime[2 * tile + 1] = __builtin_amdgcn_s_memrealtime();
                 }
             }
             return;
         }
-        tile -= ga.row_blocks;
+        --p;
     }
-    int p = 0;
-#pragma unroll
-    for (int i = 1; i < 4; ++i)
-        if (i < nnet && tile >= ga.probs[nnet + i].tile_begin) p = i;
-    const GemmProb g0 = ga.probs[p], g1 = ga.probs[nnet + p];
-    const int lt = tile - g1.tile_begin;
+    const GemmProb g0 = ga.probs[2 * p], g1 = ga.probs[2 * p + 1];
+    const int lt = (int)blockIdx.x;
+    if (lt >= ((g1.M + 15) >> 4) * g1.tiles_n) return;   // (a pair with fewer tiles than the grid's x)
+    if (SACX_FWD2_STAMP == 3) {               // diagnostic: the problem's arguments have arrived
+        asm volatile("" ::"s"(g0.N), "s"(g1.N), "s"(g0.A), "s"(g1.B));
+        F2_STAMP(3);
+    }
     const int tm = lt / g1.tiles_n, cg = lt - tm * g1.tiles_n;
     const int m0 = tm * 16;
     const int wave = wave_id(), lane = threadIdx.x & 63, r = lane & 15, grp = lane >> 4;
@@ -2637,41 +2675,52 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
     if (SACX_FWD2_STAMP == 0 && ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            ga.ktime[2 * ktime_wg()] = t0;
-            ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime();
+            ga.ktime[2 * f2_slot(ga, g1, lt, HEAD)] = t0;
+            ga.ktime[2 * f2_slot(ga, g1, lt, HEAD) + 1] = __builtin_amdgcn_s_memrealtime();
         }
     }
 }
 
 void launch_gemm(const GemmArgs& a, hipStream_t s) {
     if (a.mode == GM_FWD2) {       // two forward layers in one launch (host: one seed, fp32, 16x16)
-        const dim3 block(SACX_FWD2_NW * 64);
+        // the kernel's layout: pair p's problems at 2p / 2p + 1, grid (tiles of the largest pair,
+        // pairs, + a plane of head rows first for HEAD)
+        GemmArgs b = a;
+        const int np = a.nprob / 2;
+        int most = 1;
+        for (int i = 0; i < np; ++i) {
+            b.probs[2 * i] = a.probs[i];
+            b.probs[2 * i + 1] = a.probs[np + i];
+            most = std::max(most, ((a.probs[np + i].M + 15) / 16) * a.probs[np + i].tiles_n);
+        }
+        const dim3 block(SACX_FWD2_NW * 64), grid2(most, np);
         if (a.rowk == 3) {          // the target / critic pair with the actor-head rows
-            const dim3 grid(a.total_tiles + a.row_blocks), hblock(SACX_FWD2_HEAD_NW * 64);
-#define SACX_F2H(V, F) hipLaunchKernelGGL((k_fwd2<V, SACX_FWD2_HEAD_NW, true, F>), grid, hblock, 0, s, a)
+            const dim3 grid(std::max(most, a.row_blocks), np + 1), hblock(SACX_FWD2_HEAD_NW * 64);
+#define SACX_F2H(V, F) hipLaunchKernelGGL((k_fwd2<V, SACX_FWD2_HEAD_NW, true, F>), grid, hblock, 0, s, b)
             if (a.has_final == 2) { if (a.vec) SACX_F2H(1, 2); else SACX_F2H(0, 2); }
             else if (a.has_final) { if (a.vec) SACX_F2H(1, 1); else SACX_F2H(0, 1); }
             else { if (a.vec) SACX_F2H(1, 0); else SACX_F2H(0, 0); }
 #undef SACX_F2H
         } else if (a.rowk == 6) {   // the world-model fit's gather + two layers (16 waves, H0 <= 512)
-            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, 16, false, 0, 512, true>), dim3(a.total_tiles), dim3(1024), 0, s, a);
-            else hipLaunchKernelGGL((k_fwd2<0, 16, false, 0, 512, true>), dim3(a.total_tiles), dim3(1024), 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, 16, false, 0, 512, true>), grid2, dim3(1024), 0, s, b);
+            else hipLaunchKernelGGL((k_fwd2<0, 16, false, 0, 512, true>), grid2, dim3(1024), 0, s, b);
         } else {
-            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW, false>), dim3(a.total_tiles), block, 0, s, a);
-            else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW, false>), dim3(a.total_tiles), block, 0, s, a);
+            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW, false>), grid2, block, 0, s, b);
+            else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW, false>), grid2, block, 0, s, b);
         }
         return;
     }
     if (a.dwl) {   // dW + Adam with LDS-staged rows: plain problems only (no fused rows, no alpha.final)
         const dim3 grid(a.total_tiles, 1, seeds_z(a.nseeds)), block(256);
+        const KHdr kh = khdr_of(a);
 #define SACX_DWLL(NH)                                                                                  \
     do {                                                                                              \
         if (a.nseeds > 1) {                                                                           \
-            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, true, NH>), grid, block, 0, s, a);            \
-            else hipLaunchKernelGGL((k_dwl<false, true, NH>), grid, block, 0, s, a);                  \
+            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, true, NH>), grid, block, 0, s, KH_ARGS);            \
+            else hipLaunchKernelGGL((k_dwl<false, true, NH>), grid, block, 0, s, KH_ARGS);                  \
         } else {                                                                                      \
-            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, false, NH>), grid, block, 0, s, a);           \
-            else hipLaunchKernelGGL((k_dwl<false, false, NH>), grid, block, 0, s, a);                 \
+            if (a.bf16) hipLaunchKernelGGL((k_dwl<true, false, NH>), grid, block, 0, s, KH_ARGS);           \
+            else hipLaunchKernelGGL((k_dwl<false, false, NH>), grid, block, 0, s, KH_ARGS);                 \
         }                                                                                             \
     } while (0)
         if (a.dwl == 2) SACX_DWLL(1);      // 32x16 tiles

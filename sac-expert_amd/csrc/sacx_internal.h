@@ -392,7 +392,49 @@ struct GemmArgs {
     // the problem's A (X, read by model.adam) and each tile stores its 16 columns of the targets
     MGatherArgs mg;
 };
-static_assert(sizeof(GemmArgs) <= 4096, "GemmArgs travels as kernel arguments");
+static_assert(sizeof(GemmArgs) <= 4096 - 16, "GemmArgs travels as kernel arguments, behind a KHdr");
+
+// The scalars that pick a k_gemm / k_dwl workgroup's role and problem (total_tiles, row_blocks,
+// the problems' first tiles, nprob, has_final, xcd_map), packed as 9 x 12-bit fields + 8 flag bits
+// into 4 dwords that travel AHEAD of GemmArgs as plain kernel arguments and are preloaded into
+// SGPRs at dispatch (gfx950 kernarg preload, hipcc -mllvm -amdgpu-kernarg-preload-count=4): the
+// workgroup then reads its problem's fields in ONE scalar round trip instead of two.  valid = 0
+// (a value past 12 bits) falls back to reading them from GemmArgs.
+struct KHdr {
+    uint32_t h[4];
+};
+__host__ __device__ inline uint32_t khdr_field(const KHdr& k, int i) {   // 12-bit field i (i <= 9)
+    const int b = 12 * i, w = b >> 5, o = b & 31;
+    const uint64_t v = ((uint64_t)(w + 1 < 4 ? k.h[w + 1] : 0u) << 32) | k.h[w];
+    return (uint32_t)(v >> o) & 0xfffu;
+}
+// flags: bits 108.. : nprob (4), has_final (2), xcd_map (1), valid (1)
+__host__ __device__ inline uint32_t khdr_flags(const KHdr& k) { return (k.h[3] >> 12) & 0xffu; }
+// The launch header of a k_gemm / k_dwl launch (sacx_internal.h: KHdr); invalid (all zero) when a
+// value does not fit 12 bits, and the kernel then reads the same values from GemmArgs
+inline KHdr khdr_of(const GemmArgs& a) {
+    KHdr k{};
+    uint32_t v[9];
+    v[0] = (uint32_t)a.total_tiles;
+    v[1] = (uint32_t)a.row_blocks;
+    for (int i = 1; i < GEMM_MAXP; ++i) v[i + 1] = i < a.nprob ? (uint32_t)a.probs[i].tile_begin : 0xfffu;
+    bool ok = a.nprob <= 15 && a.has_final >= 0 && a.has_final <= 3 && (a.xcd_map & ~1) == 0;
+    for (int i = 0; i < 9; ++i) ok = ok && v[i] <= 0xfffu;
+    // (problems past nprob never match: the selection loop checks i < nprob first)
+    if (!ok) return k;
+    uint64_t bits[2] = {0, 0};
+    for (int i = 0; i < 9; ++i) {
+        const int b = 12 * i;
+        bits[b >> 6] |= (uint64_t)v[i] << (b & 63);
+        if ((b & 63) + 12 > 64) bits[(b >> 6) + 1] |= (uint64_t)v[i] >> (64 - (b & 63));
+    }
+    const uint32_t flags = (uint32_t)a.nprob | ((uint32_t)a.has_final << 4) | ((uint32_t)a.xcd_map << 6) | 0x80u;
+    bits[1] |= (uint64_t)flags << (108 - 64);
+    k.h[0] = (uint32_t)bits[0]; k.h[1] = (uint32_t)(bits[0] >> 32);
+    k.h[2] = (uint32_t)bits[1]; k.h[3] = (uint32_t)(bits[1] >> 32);
+    return k;
+}
+
 
 // ---------------------------------------------------------------- sampler + gather
 struct RngArgs {

@@ -127,3 +127,21 @@ def test_config_layout_matches_gcc(tmp_path):
     got = [int(x) for x in subprocess.check_output([str(exe)], text=True).split()]
     want = [getattr(N.Config, n).offset for n in names] + [ctypes.sizeof(N.Config)]
     assert got == want, list(zip(names + ["sizeof"], got, want))
+
+
+def test_launch_header_round_trip(tmp_path):
+    """The k_gemm / k_dwl launch header (sacx_internal.h KHdr: the workgroup-role scalars packed
+    into 4 preloaded dwords) decodes to the GemmArgs values it was built from, and is marked
+    invalid when a value does not fit (the kernels then read GemmArgs)."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not on PATH")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = tmp_path / "khdr"
+    subprocess.check_call(["g++", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                           "-I", os.path.join(root, "include"), "-I", os.path.join(root, "sac-expert_amd", "csrc"),
+                           os.path.join(root, "tests", "khdr_check.cpp"), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)], text=True)
+    assert "0 mismatches" in out, out
