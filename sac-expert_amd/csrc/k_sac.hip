@@ -2388,7 +2388,8 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 // group's threads store the rows' targets T (get_loss :286-296) -- model.gather+fwd0+fwd1 in one launch
 // SACX_FWD2_STAMP (diagnostic builds): the end stamp of each workgroup is taken after phase P
 // instead -- 1: layer 0 done (its operands and, for target tiles, the head prologue), 2: layer 1's
-// MFMAs reduced, 3: the problem's kernel arguments loaded
+// MFMAs reduced, 3: the problem's kernel arguments loaded, 5 / 6 (target tiles of the HEAD variant):
+// the head prologue done / its operands arrived
 #ifndef SACX_FWD2_STAMP
 #define SACX_FWD2_STAMP 0
 #endif
@@ -2574,8 +2575,14 @@ __global__ __launch_bounds__(NW * 64, HEAD ? 2 * NW / 4 : 1) void k_fwd2(GemmArg
         // prologue has no barrier of its own)
         __shared__ float As[16][68];
         if (headp) {                          // uniform
+            if (SACX_FWD2_STAMP == 6) {       // diagnostic: the prologue's operands have arrived
+                const float mu6 = head_pre_mu(hpre);
+                asm volatile("" ::"v"(mu6), "v"(hpre.xs[3]), "v"(hpre.u));
+                F2_STAMP(6);
+            }
             if (threadIdx.x < 256) head_pre_finish(ga.head, g0, m0, cg, As, hpre, head_pre_mu(hpre), 0);
             __syncthreads();
+            F2_STAMP(5);                      // diagnostic: the prologue is done
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
