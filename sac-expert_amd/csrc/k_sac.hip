@@ -170,6 +170,19 @@ __device__ __forceinline__ void st_out(float* p, float v) {
 #endif
 }
 
+// The Adam moments: read again only by the next update's same epilogue, so SACX_NT_MOMENTS stores
+// them non-temporal (they need not sit dirty in the XCD L2 that the launch boundary writes back)
+#ifndef SACX_NT_MOMENTS
+#define SACX_NT_MOMENTS 0
+#endif
+__device__ __forceinline__ void st_mom(float* p, float v) {
+#if SACX_NT_MOMENTS
+    __builtin_nontemporal_store(v, p);
+#else
+    st_out(p, v);
+#endif
+}
+
 // Raw buffer loads.  Out-of-range elements get an offset past the resource's
 // num_records and the hardware returns 0, so every load is unconditional and no
 // select follows it (a select on a load result is turned back into a branch
@@ -1038,6 +1051,37 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             load_b<BKC, V && BKC, MODE == GM_DW>(rb, g, nb, nbok, k0e, b[u][1]);
         }
     };
+#if SACX_DW_DIAG_XBF   // diagnostic timing builds only: the dW A operand as one bf16x8 per sub-row and
+                      // slab pair (reinterpreted fp32 rows: wrong values, the shadow's load shape)
+    if constexpr (BF && MODE == GM_DW) {
+        const __amdgpu_buffer_rsrc_t rab = make_rsrc(g.A, 0x7fffffffu);
+        for (int it = it0; it < it1; it += 2) {
+            float b[2][2][4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int k0 = (it + u) * 16 + grp * 4;
+                const int k0e = (it + u < it1) ? k0 : (1 << 30);
+                load_b<false, false, true>(rb, g, na, naok, k0e, b[u][0]);
+                load_b<false, false, true>(rb, g, nb, nbok, k0e, b[u][1]);
+            }
+            const int po = (it >> 1) * 32 + grp * 8;
+            bf16x8_t aw[2], bw[2];
+            aw[0] = wbf_load(rab, maok, (ma * 512 + po) & 0xffff);
+            aw[1] = wbf_load(rab, mbok, (mb * 512 + po) & 0xffff);
+            bw[0] = pack_bf16(b[0][0], b[1][0]);
+            bw[1] = pack_bf16(b[0][1], b[1][1]);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                if (((it - it0) >> 1) & 1)
+                    acc1[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s >> 1], bw[s & 1], acc1[s], 0, 0, 0);
+                else
+                    acc0[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s >> 1], bw[s & 1], acc0[s], 0, 0, 0);
+            }
+        }
+        return;
+    }
+#endif
     for (int it = it0; it < it1; it += NS) {
         float a[NS][2][4], b[NS][2][4];
         load_group(it, a, b);
@@ -1238,8 +1282,8 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
             if (out_ok) {
                 st_out(&g.P[pidx], pn);
-                st_out(&g.P[pidx + ga.p_stride], mm1);
-                st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+                st_mom(&g.P[pidx + ga.p_stride], mm1);
+                st_mom(&g.P[pidx + 2 * ga.p_stride], vv1);
                 wbf_store(g.wbf, g, mm, nn, pn);
                 if (g.T != nullptr && polyak) {
                     st_out(&g.T[pidx], tv);
@@ -1819,8 +1863,8 @@ __device__ __forceinline__ void gemm_core(const KHdr kh, const GemmArgs& ga) {
         const float pn = e0 - (mm1 * lr_t) / (sqrtf(vv1) + eps);
         if (out_ok) {
             st_out(&g.P[pidx], pn);
-            st_out(&g.P[pidx + ga.p_stride], mm1);
-            st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+            st_mom(&g.P[pidx + ga.p_stride], mm1);
+            st_mom(&g.P[pidx + 2 * ga.p_stride], vv1);
             wbf_store(g.wbf, g, mm, nn, pn);
         }
         if (g.T != nullptr) {
@@ -2232,8 +2276,8 @@ __global__ __launch_bounds__(256, 2) void k_dwl(uint32_t h0, uint32_t h1, uint32
         const float tv = e3[s] * ga.adam.tau_keep + pn * ga.adam.tau_take;
         if (ok) {
             st_out(&g.P[pidx], pn);
-            st_out(&g.P[pidx + ga.p_stride], mm1);
-            st_out(&g.P[pidx + 2 * ga.p_stride], vv1);
+            st_mom(&g.P[pidx + ga.p_stride], mm1);
+            st_mom(&g.P[pidx + 2 * ga.p_stride], vv1);
             wbf_store(g.wbf, g, mm, nn, pn);
             if (g.T != nullptr && polyak) {
                 st_out(&g.T[pidx], tv);
@@ -2386,6 +2430,9 @@ static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
 // GATHER (rowk 6, the fit): layer 0's A rows are replay records gathered by the step's minibatch indices
 // and normalised on load (k_gemm rowk 6's arithmetic); wave 0 of column group 0 stores them to X and the
 // group's threads store the rows' targets T (get_loss :286-296) -- model.gather+fwd0+fwd1 in one launch
+#ifndef SACX_DW_DIAG_XBF
+#define SACX_DW_DIAG_XBF 0
+#endif
 // SACX_FWD2_STAMP (diagnostic builds): the end stamp of each workgroup is taken after phase P
 // instead -- 1: layer 0 done (its operands and, for target tiles, the head prologue), 2: layer 1's
 // MFMAs reduced, 3: the problem's kernel arguments loaded, 5 / 6 (target tiles of the HEAD variant):

@@ -87,6 +87,9 @@ for step in "$@"; do
     benchenv)   # the 2,000-update bench under one extra environment setting: benchenv=VAR=VALUE
       env "$arg" timeout -k 10 300 python bench.py --steps 2000 --warmup 200 --no-cpu-baseline > "$log" 2>&1
       rc=$?; echo "[$n benchenv $arg] rc=$rc $(value "$log")" ;;
+    benchv)     # the 2,000-update HC bench with a variant library: benchv=<tools/libvar name>
+      SACX_LIBPATH=$PWD/tools/libvar/libsacx_$arg.so timeout -k 10 300 python bench.py --steps 2000 --warmup 200 --no-cpu-baseline > "$log" 2>&1
+      rc=$?; echo "[$n benchv $arg] rc=$rc $(value "$log")" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
