@@ -41,6 +41,16 @@ for step in "$@"; do
       { timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
         timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
       rc=$?; echo "[$n mfit] rc=$rc"; cat "$log" ;;
+    driverenv)  # the driver's command under one extra environment setting: driverenv=VAR=VALUE
+      env "$arg" timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > "$log" 2>&1
+      rc=$?; echo "[$n driverenv $arg] rc=$rc $(value "$log")" ;;
+    overheadenv)  # step-overhead table under one extra environment setting
+      env "$arg" timeout -k 10 200 python tools/step_overhead.py > "$log" 2>&1
+      rc=$?; echo "[$n overheadenv $arg] rc=$rc"; grep -E "n=  20 launch|fit:" "$log" ;;
+    mfitenv)    # the HC / Humanoid fit timing under one extra environment setting: mfitenv=VAR=VALUE
+      { env "$arg" timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
+        env "$arg" timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
+      rc=$?; echo "[$n mfitenv $arg] rc=$rc"; grep graph "$log" ;;
     mtrace)     # kernel trace of the model fit of config $arg: one step's launches, durations, gaps
       cfg=${arg:-hc_eo}
       timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$PWD/$OUT/mtrace_$cfg" -o m \
