@@ -597,7 +597,7 @@ def dp_check(cfgd, rep, n_check=DP_CHECK_UPDATES, n_time=512):
             "note": "one learner over the ranks (strong scaling); 3 RCCL all-reduces per update inside the graph"}
 
 
-def run_dp_child(ws, config, timeout=420):
+def run_dp_child(ws, config, timeout=180):
     """The C4 leg of an N > 1 bench: a fresh ws-rank launch of ``--mode dpcheck`` (its own RCCL
     group), started by rank 0 after every replica rank has released its GPU; a hang or failure of
     the leg costs only its own entry, never the replicas line."""
