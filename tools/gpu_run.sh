@@ -47,6 +47,10 @@ for step in "$@"; do
     overheadenv)  # step-overhead table under one extra environment setting
       env "$arg" timeout -k 10 200 python tools/step_overhead.py > "$log" 2>&1
       rc=$?; echo "[$n overheadenv $arg] rc=$rc"; grep -E "n=  20 launch|fit:" "$log" ;;
+    n2shared)   # bench --gpus 2 with both ranks on the one visible GPU (gloo replicas; the C4 leg skips)
+      SACX_SHARE_DEVICE=1 SACX_REPLICA_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 400 --warmup 50 \
+          --no-cpu-baseline > "$log" 2>&1
+      rc=$?; echo "[$n n2shared] rc=$rc $(value "$log")"; grep -o '"dp_c4": {[^}]*}' "$log" || true ;;
     mfitenv)    # the HC / Humanoid fit timing under one extra environment setting: mfitenv=VAR=VALUE
       { env "$arg" timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
         env "$arg" timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
