@@ -19,6 +19,7 @@
 // fmaf).  GEMM accumulation is the exact-f32 MFMA (k-ordered fmaf chain).
 #include <hip/hip_runtime.h>
 #include <cstddef>
+#include <cstdlib>
 #include <type_traits>
 #include <math.h>
 #include "sacx_internal.h"
@@ -2296,10 +2297,15 @@ __global__ __launch_bounds__(256, 2) void k_dwl(uint32_t h0, uint32_t h1, uint32
 }
 
 #define KH_ARGS kh.h[0], kh.h[1], kh.h[2], kh.h[3], a
+// SACX_KHDR=0: launch headers marked invalid (the kernels' GemmArgs path; tests compare both)
+static bool khdr_enabled() {            // (read at every launch enqueue: graph captures are rare)
+    const char* e = std::getenv("SACX_KHDR");
+    return !(e && std::atoi(e) == 0);
+}
 
 template <bool PK, bool T32>
 static void launch_gemm_t(const GemmArgs& a, hipStream_t s) {
-    const KHdr kh = khdr_of(a);
+    const KHdr kh = khdr_of(a, khdr_enabled());
     const unsigned z = seeds_z(a.nseeds);
     const dim3 grid(a.total_tiles + (a.has_final ? 1 : 0) + (a.has_mfinal ? 1 : 0), 1, z), block(256);
     switch (a.mode) {
@@ -2766,7 +2772,7 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
     }
     if (a.dwl) {   // dW + Adam with LDS-staged rows: plain problems only (no fused rows, no alpha.final)
         const dim3 grid(a.total_tiles, 1, seeds_z(a.nseeds)), block(256);
-        const KHdr kh = khdr_of(a);
+        const KHdr kh = khdr_of(a, khdr_enabled());
 #define SACX_DWLL(NH)                                                                                  \
     do {                                                                                              \
         if (a.nseeds > 1) {                                                                           \

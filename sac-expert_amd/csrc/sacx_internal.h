@@ -412,8 +412,9 @@ __host__ __device__ inline uint32_t khdr_field(const KHdr& k, int i) {   // 12-b
 __host__ __device__ inline uint32_t khdr_flags(const KHdr& k) { return (k.h[3] >> 12) & 0xffu; }
 // The launch header of a k_gemm / k_dwl launch (sacx_internal.h: KHdr); invalid (all zero) when a
 // value does not fit 12 bits, and the kernel then reads the same values from GemmArgs
-inline KHdr khdr_of(const GemmArgs& a) {
+inline KHdr khdr_of(const GemmArgs& a, bool enabled = true) {
     KHdr k{};
+    if (!enabled) return k;              // (SACX_KHDR=0: every launch reads GemmArgs)
     uint32_t v[9];
     v[0] = (uint32_t)a.total_tiles;
     v[1] = (uint32_t)a.row_blocks;

@@ -639,3 +639,24 @@ def test_packed_seeds_equal_single(gpu_available, monkeypatch, K, use_expert, ea
     assert np.all(np.isfinite(got[0][0]))
     assert not np.array_equal(got[0][1], got[1][1])     # the seeds are different learners
 
+
+
+@pytest.mark.parametrize("act,S,A,B,graph,bf16", [("relu", 17, 6, 256, True, False), ("tanh", 17, 6, 100, False, False),
+                                                  ("relu", 376, 17, 1024, True, False),
+                                                  ("relu", 376, 17, 1024, True, True)])
+def test_launch_header_fallback_bit_identical(gpu_available, monkeypatch, act, S, A, B, graph, bf16):
+    """k_gemm / k_dwl take the scalars that pick a workgroup's role from a launch header preloaded
+    into SGPRs (sacx_internal.h KHdr); SACX_KHDR=0 marks every header invalid, so the kernels read
+    the same values from GemmArgs.  Both paths give the same updates bit for bit."""
+    outs = []
+    for kh in ("1", "0"):
+        monkeypatch.setenv("SACX_KHDR", kh)
+        eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, act=act, B=B, N=4000, seed=17, normalizers="random",
+                                               graph_steps=8, gemm_bf16=bf16)
+        eng.rng_set_state(np.random.RandomState(3).get_state())
+        eng.step(19, eager=not graph)
+        eng.sync()
+        outs.append((eng.stats(19).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy()))
+        eng.close()
+    for a, b in zip(outs[0], outs[1]):
+        assert np.array_equal(a, b)

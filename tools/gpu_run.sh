@@ -51,6 +51,11 @@ for step in "$@"; do
       SACX_SHARE_DEVICE=1 SACX_REPLICA_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 400 --warmup 50 \
           --no-cpu-baseline > "$log" 2>&1
       rc=$?; echo "[$n n2shared] rc=$rc $(value "$log")"; grep -o '"dp_c4": {[^}]*}' "$log" || true ;;
+    cfgenv)     # bench of config C under one extra environment setting: cfgenv=C:VAR=VALUE (VAR=VALUE may be -)
+      cfg=${arg%%:*}; ev=${arg#*:}
+      if [ "$ev" = "-" ]; then ev="SACX_NOP=1"; fi
+      env "$ev" timeout -k 10 300 python bench.py --config $cfg --steps 1000 --warmup 100 --no-cpu-baseline > "$log" 2>&1
+      rc=$?; echo "[$n cfgenv $arg] rc=$rc $(value "$log")" ;;
     mfitenv)    # the HC / Humanoid fit timing under one extra environment setting: mfitenv=VAR=VALUE
       { env "$arg" timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
         env "$arg" timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
