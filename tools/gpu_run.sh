@@ -56,6 +56,10 @@ for step in "$@"; do
       if [ "$ev" = "-" ]; then ev="SACX_NOP=1"; fi
       env "$ev" timeout -k 10 300 python bench.py --config $cfg --steps 1000 --warmup 100 --no-cpu-baseline > "$log" 2>&1
       rc=$?; echo "[$n cfgenv $arg] rc=$rc $(value "$log")" ;;
+    mfitv)      # the fit timing with a variant library: mfitv=<tools/libvar name>
+      { SACX_LIBPATH=$PWD/tools/libvar/libsacx_$arg.so timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
+        SACX_LIBPATH=$PWD/tools/libvar/libsacx_$arg.so timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
+      rc=$?; echo "[$n mfitv $arg] rc=$rc"; grep graph "$log" ;;
     mfitenv)    # the HC / Humanoid fit timing under one extra environment setting: mfitenv=VAR=VALUE
       { env "$arg" timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
         env "$arg" timeout -k 10 200 python tools/model_fit_time.py humanoid_eo 256; } > "$log" 2>&1
