@@ -2953,7 +2953,7 @@ __device__ void rng_twist(RngShared& S, int w0, int w1) {
 // tools/rng_bench.hip builds with SACX_RNG_PROF: thread 0 accumulates 100 MHz ticks of the
 // twist bursts [0], randint chunks [1], gauss chunks [2], whole kernel [3], bursts [4], chunks [5]
 #ifdef SACX_RNG_PROF
-__device__ unsigned long long g_rng_prof[8];
+__device__ unsigned long long g_rng_prof[16];
 #define RNG_PROF_T(v) const uint64_t v = __builtin_amdgcn_s_memrealtime()
 #define RNG_PROF_ADD(i, v) do { if (threadIdx.x == 0) g_rng_prof[i] += (v); } while (0)
 #else
@@ -3190,7 +3190,656 @@ __global__ __launch_bounds__(256) void k_polar(RngArgs a) {
     }
 }
 
-void launch_rng(const RngArgs& a, hipStream_t s) {
+// ==================================================================== segmented sampler (k_mtj_*)
+// The same draws as k_rng (bit-exact), for batches of many words (Humanoid: ~134k words per
+// update), without k_rng's two serial limits -- one workgroup twisting 623-word rounds and
+// ranking the candidates with block-wide ballots:
+//   k_mtj_head     key block -> words [0, MTJ_HEAD) of the batch's raw stream (one WG)
+//   k_mtj_jump     the 624-word windows at k*L + 1, k = 1 .. S-1, as XORs of head words
+//                  selected by x^(kL) mod phi (mt_jump.h), 63 partial XORs each
+//   k_mtj_seg      S workgroups twist S segments of L words at once
+//   k_mtj_flags    per word: randint acceptance and polar acceptance of the 4-word group starting
+//                  there, as bitmaps, with per-chunk counts (per residue mod 4 for the groups)
+//   k_mtj_resolve  chunk prefixes, then per update the position of its n-th accepted word /
+//                  group from the current position (binary search + one wave), the state
+//                  (a batch that outran the generated words -- never at the sizes used, forced in
+//                  tests -- is redrawn there by rng_body from the unchanged state)
+//   k_mtj_emit     every accepted candidate -> its output slot (rank = prefix difference),
+//                  the polar transform in place
+// Stream words are numbered from the key block (words 0 .. 623 = st->key), as in rng_body.
+#define MTJ_RW 4096
+
+__device__ __forceinline__ bool polar_acc(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, double& x1,
+                                          double& x2, double& r2) {
+    const double u1 = ((double)(int32_t)(w0 >> 5) * 67108864.0 + (double)(int32_t)(w1 >> 6)) / 9007199254740992.0;
+    const double u2 = ((double)(int32_t)(w2 >> 5) * 67108864.0 + (double)(int32_t)(w3 >> 6)) / 9007199254740992.0;
+    x1 = 2.0 * u1 - 1.0;
+    x2 = 2.0 * u2 - 1.0;
+    r2 = x1 * x1 + x2 * x2;
+    return (r2 < 1.0) && (r2 != 0.0);
+}
+
+__device__ __forceinline__ void mtj_put(uint32_t* ring, int q, uint32_t v) {
+    const unsigned p = (unsigned)q & (MTJ_RW - 1u);
+    ring[p] = v;
+    if (p < RNG_MIR) ring[MTJ_RW + p] = v;
+}
+
+// words [n0, n1) into the LDS ring and sw.  The words from `base` on are resident (a 624-word
+// window at base, or the 1,078 before n0); words below base + 1078 take the 227-wide form
+__device__ void mtj_twist(uint32_t* ring, uint32_t* __restrict__ sw, int base, int n0, int n1) {
+    const int t = threadIdx.x;
+    while (n0 < n1 && n0 < base + 1078) {
+        const int e = min(min(n1, base + 1078), n0 + 227);
+        const int n = n0 + t;
+        if (n < e) {
+            const uint32_t v = ring[(unsigned)(n - 227) & (MTJ_RW - 1u)] ^
+                               mt_g(ring[(unsigned)(n - 624) & (MTJ_RW - 1u)], ring[(unsigned)(n - 623) & (MTJ_RW - 1u)]);
+            mtj_put(ring, n, v);
+            sw[n] = v;
+        }
+        __syncthreads();
+        n0 = e;
+    }
+    while (n0 < n1) {
+        const int e = min(n1, n0 + 623);
+        const int n = n0 + t;
+        if (n < e) {
+            const unsigned p = (unsigned)n & (MTJ_RW - 1u);
+            const uint32_t* b = ring + (p >= 1078u ? p : p + MTJ_RW) - 1078u;   // b[i] = word n - 1078 + i
+            const uint32_t v = b[397] ^ mt_g(b[454] ^ b[227] ^ b[0], b[455] ^ b[228] ^ b[1]);
+            mtj_put(ring, n, v);
+            sw[n] = v;
+        }
+        __syncthreads();
+        n0 = e;
+    }
+}
+
+struct MtjPtrs {
+    uint32_t* sw;
+    uint32_t* fi;
+    uint32_t* fp;
+    int32_t* cnt;
+    int32_t* pre;
+    int32_t* res;
+    uint32_t* part;
+    int32_t* ptag;
+    uint32_t* pfbm;
+};
+__device__ __forceinline__ MtjPtrs mtj_ptrs(const RngArgs& a, int64_t so) {
+    uint32_t* jw = sr(a.jw, so);
+    const MtjLayout y = mtj_layout(a.jL, a.jsmax);
+    MtjPtrs p;
+    p.sw = jw + y.sw; p.fi = jw + y.fi; p.fp = jw + y.fp;
+    p.cnt = (int32_t*)(jw + y.cnt); p.pre = (int32_t*)(jw + y.pre); p.res = (int32_t*)(jw + y.res);
+    p.part = jw + y.part;
+    p.ptag = (int32_t*)(jw + y.ptag);
+    p.pfbm = jw + y.pfbm;
+    return p;
+}
+__device__ __forceinline__ uint64_t mtj_u64(const int32_t* r) { return ((uint64_t)(uint32_t)r[1] << 32) | (uint32_t)r[0]; }
+
+// The key block of a batch that followed a segmented batch is (normally) a block of that batch's
+// stream, and the words [0, MTJ_HEAD) it needs were generated there too (the estimate keeps
+// MTJ_HEAD words of margin): copied instead of twisted when the key still equals them (res[8]:
+// the block's offset, res[9]: the words of that batch, res[10]: MTJ_CHAIN while valid).
+#define MTJ_CHAIN 0x6d746a31
+__global__ __launch_bounds__(1024) void k_mtj_head(RngArgs a) {
+    __shared__ uint32_t ring[MTJ_RW + RNG_MIR];
+    __shared__ int reuse;
+    const int64_t so = seed_off(a.sstride);
+    const RngState* st = sr(a.st, so);
+    const Ctl* ctl = sr(a.ctl, so);
+    RngState* bk = sr(a.backup, so);
+    const MtjPtrs p = mtj_ptrs(a, so);
+    const int t = threadIdx.x;
+    const int off = p.res[8];
+    if (t == 0) {
+        const int64_t wcap = mtj_layout(a.jL, a.jsmax).wcap;
+        reuse = p.res[10] == MTJ_CHAIN && off >= MTJ_HEAD && off % 624 == 0 && (int64_t)off + MTJ_HEAD <= p.res[9] &&
+                p.res[9] <= wcap;
+    }
+    __syncthreads();
+    const bool chained = reuse;
+    if (chained)
+        for (int i = t; i < 624; i += 1024)
+            if (st->key[i] != p.sw[off + i]) reuse = 0;   // the state was set from outside
+    __syncthreads();
+    const bool copy = reuse;
+    for (int i = t; i < 624; i += 1024) {
+        const uint32_t v = st->key[i];
+        if (!copy) {
+            mtj_put(ring, i, v);
+            p.sw[i] = v;
+        }
+        if (bk) bk->key[i] = v;      // the state before this draw (undo of a speculative draw)
+    }
+    if (t == 0) {
+        // randint's bound, read once for the whole batch (ctl->cur_size may move meanwhile)
+        const uint64_t high = a.size_fixed > 0 ? (uint64_t)a.size_fixed : (uint64_t)ctl->cur_size;
+        const uint64_t rng = high > 0 ? high - 1 : 0;
+        uint64_t mask = rng;
+        mask |= mask >> 1; mask |= mask >> 2; mask |= mask >> 4;
+        mask |= mask >> 8; mask |= mask >> 16; mask |= mask >> 32;
+        p.res[0] = 0;
+        p.res[1] = a.jS * a.jL + 1;
+        p.res[2] = st->pos;
+        p.res[3] = st->pos;
+        p.res[4] = (int32_t)(uint32_t)rng; p.res[5] = (int32_t)(uint32_t)(rng >> 32);
+        p.res[6] = (int32_t)(uint32_t)mask; p.res[7] = (int32_t)(uint32_t)(mask >> 32);
+        p.res[10] = 0;               // k_mtj_resolve re-validates
+        // the chunks within 3 of each update's expected randint / polar end (the resolve walk's
+        // searches land within a few hundred words of them), in increasing order
+        const int nchk = (a.jS * a.jL + 1 + MTJ_CHK - 1) / MTJ_CHK;
+        int n = 0, last = -1;
+        auto window = [&](double pos) {
+            const int c = (int)(pos / MTJ_CHK);
+            for (int k = max(last + 1, c - 3); k <= min(c + 3, nchk - 1) && n < MTJ_PF; ++k) p.ptag[n++] = last = k;
+        };
+        double q = st->pos;
+        window(q);
+        for (int u = 0; u < a.nupd; ++u) {
+            if (a.n_int > 0 && rng > 0) {
+                q += (double)a.n_int * ((double)(mask + 1) / (double)(rng + 1));
+                window(q);
+            }
+            q += (double)((a.n_norm + 1) >> 1) * (4.0 / 0.78539816339744831);
+            window(q);
+        }
+        while (n < MTJ_PF) p.ptag[n++] = -1;
+        if (bk) {
+            bk->pos = st->pos;
+            bk->has_gauss = st->has_gauss;
+            bk->gauss = st->gauss;
+        }
+    }
+    if (copy) {
+        for (int i = t; i < MTJ_HEAD; i += 1024) p.sw[i] = p.sw[off + i];   // off >= MTJ_HEAD: disjoint
+        return;
+    }
+    __syncthreads();
+    mtj_twist(ring, p.sw, 0, 624, MTJ_HEAD);
+}
+
+// window k (words k L + 1 .. k L + 624) = XOR_{c_i = 1} words i + 1 .. i + 624, i < 19937:
+// workgroup (c, k) takes coefficients [c MTJ_CH, (c + 1) MTJ_CH), as the host-built list of their
+// set bits (mt_jump_lists), eight at a time (24 independent LDS reads per step), and writes its
+// partial XOR
+__global__ __launch_bounds__(256) void k_mtj_jump(RngArgs a) {
+    __shared__ uint32_t win[MTJ_CH + 624];
+    const int64_t so = seed_off(a.sstride);
+    const MtjPtrs p = mtj_ptrs(a, so);
+    const int c = blockIdx.x, k = blockIdx.y + 1;
+    const int i0 = c * MTJ_CH;
+    const int nb = min(MTJ_CH, 19937 - i0);
+    for (int l = threadIdx.x; l < nb + 623; l += 256) win[l] = p.sw[i0 + 1 + l];
+    __shared__ int ents[MTJ_CH];
+    const int32_t* jl = reinterpret_cast<const int32_t*>(sr(a.jc, so));
+    const int g = (k - 1) * MTJ_NC + c;
+    const int e0 = jl[g], ne = jl[g + 1] - e0;
+    const int32_t* ent = jl + (a.jsmax - 1) * MTJ_NC + 1 + e0;
+    for (int l = threadIdx.x; l < ne; l += 256) ents[l] = ent[l];   // the list, in the window's round
+    __syncthreads();
+    const int j0 = threadIdx.x, j1 = j0 + 256, j2 = min(j0 + 512, 623);   // j2 > 623: computed, not stored
+    uint32_t s0 = 0, s1 = 0, s2 = 0;
+    int e = 0;
+    for (; e + 8 <= ne; e += 8) {
+        int ii[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) ii[r] = ents[e + r];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            s0 ^= win[ii[r] + j0];
+            s1 ^= win[ii[r] + j1];
+            s2 ^= win[ii[r] + j2];
+        }
+    }
+    for (; e < ne; ++e) {
+        const int i = ents[e];
+        s0 ^= win[i + j0];
+        s1 ^= win[i + j1];
+        s2 ^= win[i + j2];
+    }
+    uint32_t* out = p.part + ((size_t)(k - 1) * MTJ_NC + c) * 624;
+    out[j0] = s0;
+    out[j1] = s1;
+    if (j0 + 512 < 624) out[j2] = s2;
+}
+
+// segment k: words [k L + 1, (k + 1) L + 1) (segment 0: [0, L + 1), its head from k_mtj_head)
+__global__ __launch_bounds__(1024) void k_mtj_seg(RngArgs a) {
+    __shared__ uint32_t ring[MTJ_RW + RNG_MIR];
+    const int64_t so = seed_off(a.sstride);
+    const MtjPtrs p = mtj_ptrs(a, so);
+    const int k = blockIdx.x, t = threadIdx.x;
+    const int n1 = (k + 1) * a.jL + 1;
+    int base, n0;
+    if (k == 0) {
+        if (n1 <= MTJ_HEAD) return;
+        base = 0;
+        n0 = MTJ_HEAD;
+        for (int q = n0 - 1078 + t; q < n0; q += 1024) mtj_put(ring, q, p.sw[q]);
+    } else {
+        base = k * a.jL + 1;
+        n0 = base + 624;
+        const uint32_t* pt = p.part + (size_t)(k - 1) * MTJ_NC * 624;
+        for (int j = t; j < 624; j += 1024) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int c = 0; c < MTJ_NC; ++c) v ^= pt[c * 624 + j];   // all 63 loads in one round
+            mtj_put(ring, base + j, v);
+            p.sw[base + j] = v;
+        }
+    }
+    __syncthreads();
+    mtj_twist(ring, p.sw, base, n0, n1);
+}
+
+// chunk c: acceptance bitmaps of its MTJ_CHK words and the counts [randint, group at residue 0..3]
+__global__ __launch_bounds__(256) void k_mtj_flags(RngArgs a) {
+    __shared__ int wc[4][5];
+    __shared__ uint32_t bmw[2][MTJ_CHK / 32];
+    const int64_t so = seed_off(a.sstride);
+    const MtjPtrs p = mtj_ptrs(a, so);
+    const int W = a.jS * a.jL + 1;
+    const uint64_t rng = mtj_u64(p.res + 4), mask = mtj_u64(p.res + 6);
+    const int c = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int cnt[5] = {0, 0, 0, 0, 0};
+    uint32_t wd[MTJ_CHK / 256][4];   // the eight positions' 4-word groups, loaded before any use
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        const int m = c * MTJ_CHK + i * 256 + t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wd[i][r] = m + r < W ? p.sw[m + r] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        const int m = c * MTJ_CHK + i * 256 + t;
+        bool fi = false, fp = false;
+        if (m < W) {
+            const uint32_t w0 = mt_temper(wd[i][0]);
+            fi = rng == 0xFFFFFFFFULL || (uint64_t)(w0 & (uint32_t)mask) <= rng;
+            if (m + 3 < W) {
+                double x1, x2, r2;
+                fp = polar_acc(w0, mt_temper(wd[i][1]), mt_temper(wd[i][2]), mt_temper(wd[i][3]), x1, x2, r2);
+            }
+        }
+        const uint64_t bi = __ballot(fi), bp = __ballot(fp);
+        if (lane == 0) {
+            const int w32 = (m - lane) >> 5;
+            p.fi[w32] = (uint32_t)bi; p.fi[w32 + 1] = (uint32_t)(bi >> 32);
+            p.fp[w32] = (uint32_t)bp; p.fp[w32 + 1] = (uint32_t)(bp >> 32);
+            const int l32 = w32 - c * (MTJ_CHK / 32);
+            bmw[0][l32] = (uint32_t)bi; bmw[0][l32 + 1] = (uint32_t)(bi >> 32);
+            bmw[1][l32] = (uint32_t)bp; bmw[1][l32 + 1] = (uint32_t)(bp >> 32);
+        }
+        cnt[0] += __popcll(bi);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) cnt[1 + r] += __popcll(bp & (0x1111111111111111ULL << r));
+    }
+    if (lane == 0)
+        for (int k = 0; k < 5; ++k) wc[wv][k] = cnt[k];
+    __syncthreads();
+    if (t < 5) p.cnt[c * 8 + t] = wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];
+    if (wv == 0) {   // a predicted chunk: its bitmaps also to its k_mtj_resolve prefetch slot
+        const unsigned long long b0 = __ballot(p.ptag[lane] == c), b1 = __ballot(p.ptag[64 + lane] == c);
+        if (b0 | b1) {
+            const int sl = b0 ? (int)__builtin_ctzll(b0) : 64 + (int)__builtin_ctzll(b1);
+            p.pfbm[sl * 128 + lane] = bmw[0][lane];
+            p.pfbm[sl * 128 + 64 + lane] = bmw[1][lane];
+        }
+    }
+}
+
+// Wave-wide integer scans on DPP lane moves (row_shr within 16-lane rows, then the row
+// broadcasts), a few cycles each instead of ds_bpermute's LDS round trip; all 64 lanes active
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+__device__ __forceinline__ int wave_isum(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
+__device__ __forceinline__ uint32_t mtj_rmask(int kind) { return kind == 0 ? 0xFFFFFFFFu : (0x11111111u << (kind - 1)); }
+
+// Wave 0 of k_mtj_resolve walks the updates holding one chunk's two bitmaps in registers (lane l:
+// word l of the chunk), so that the prefix at the position a search ended needs no load.
+struct MtjWalk {
+    const int* pre;      // LDS: exclusive chunk prefixes [chunk][kind], [nchk] = totals
+    const int* ctag;     // LDS: the prefetched chunks (-1: empty slot)
+    const uint32_t (*cbm)[2][64];
+    MtjPtrs p;
+    int nchk;
+    int cc = -1;         // the chunk held
+    uint32_t fiw = 0, fpw = 0;
+
+    __device__ void hold(int c) {
+        if (c == cc) return;
+        const int lane = threadIdx.x & 63;
+        const unsigned long long b0 = __ballot(ctag[lane] == c), b1 = __ballot(ctag[64 + lane] == c);
+        if (b0 | b1) {
+            const int s = b0 ? (int)__builtin_ctzll(b0) : 64 + (int)__builtin_ctzll(b1);
+            fiw = cbm[s][0][lane];
+            fpw = cbm[s][1][lane];
+        } else {     // outside the predicted windows: one global round trip
+            fiw = p.fi[c * (MTJ_CHK / 32) + lane];
+            fpw = p.fp[c * (MTJ_CHK / 32) + lane];
+        }
+        cc = c;
+    }
+    // candidates of `kind` accepted at positions < m (kind 0: randint words; 1 + r: groups at r mod 4)
+    __device__ int prefix(int kind, int m) {
+        const int c = m / MTJ_CHK;
+        if (c >= nchk) return pre[nchk * 5 + kind];
+        hold(c);
+        const int lane = threadIdx.x & 63;
+        const int o = m - c * MTJ_CHK;
+        uint32_t w = (kind == 0 ? fiw : fpw) & mtj_rmask(kind);
+        const int lw = o >> 5;
+        if (lane > lw) w = 0;
+        else if (lane == lw) w &= (1u << (o & 31)) - 1u;
+        return pre[c * 5 + kind] + wave_isum(__popc(w));
+    }
+    // the position of the T-th (1-based) accepted candidate of `kind`; -1 past the generated words
+    __device__ int find(int kind, int T) {
+        if (T > pre[nchk * 5 + kind]) return -1;
+        const int lane = threadIdx.x & 63;
+        // the last chunk whose exclusive prefix is < T: among 16-chunk groups, then within one
+        const int g = lane * 16;
+        const int l1 = 63 - __clzll(__ballot(g < nchk && pre[g * 5 + kind] < T));
+        const int c2 = l1 * 16 + lane;
+        const int c = l1 * 16 + 63 - __clzll(__ballot(lane < 16 && c2 < nchk && pre[c2 * 5 + kind] < T));
+        hold(c);
+        const int rem = T - 1 - pre[c * 5 + kind];
+        uint32_t w = (kind == 0 ? fiw : fpw) & mtj_rmask(kind);
+        const int n = __popc(w);
+        const int incl = wave_incl_scan(n);
+        const bool mine = incl - n <= rem && rem < incl;
+        int pos = 0;
+        if (mine) {
+            for (int i = incl - n; i < rem; ++i) w &= w - 1u;
+            pos = c * MTJ_CHK + lane * 32 + __builtin_ctz(w);
+        }
+        return __shfl(pos, (int)__builtin_ctzll(__ballot(mine)));
+    }
+};
+
+// the chunk prefixes (phase 1) share LDS with rng_body's ring (the fallback, after phase 2)
+union MtjResolveShared {
+    struct {
+        int pre[(MTJ_MAXCHK + 1) * 5];
+        int wsum[16][5];
+        int ctag[MTJ_PF];
+        uint32_t cbm[MTJ_PF][2][64];
+    } r;
+    RngShared fb;
+};
+
+__global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
+    __shared__ MtjResolveShared U;
+    __shared__ int sh_q, sh_ovf, sh_has;
+    __shared__ double sh_gauss;
+    int* const pre = U.r.pre;
+    const int64_t so = seed_off(a.sstride);
+    const MtjPtrs p = mtj_ptrs(a, so);
+    RngState* st = sr(a.st, so);
+    Ctl* ctl = sr(a.ctl, so);
+    const int W = a.jS * a.jL + 1;
+    const int nchk = (W + MTJ_CHK - 1) / MTJ_CHK;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    RNG_PROF_T(r0);
+    const uint64_t rng = mtj_u64(p.res + 4);
+    const int pos0 = p.res[3];
+
+    // ---- exclusive prefixes of the chunk counts (nchk <= MTJ_MAXCHK = blockDim); the predicted
+    // chunks' bitmaps (k_mtj_head's list, copied by k_mtj_flags) into LDS in the same round
+    int v[5], incl[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) v[k] = t < nchk ? p.cnt[t * 8 + k] : 0;
+    if (t < MTJ_PF) U.r.ctag[t] = p.ptag[t];
+    for (int i = t; i < MTJ_PF * 128; i += 1024) U.r.cbm[i >> 7][(i >> 6) & 1][i & 63] = p.pfbm[i];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        incl[k] = wave_incl_scan(v[k]);
+        if (lane == 63) U.r.wsum[wv][k] = incl[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        int off = 0;
+        for (int i = 0; i < wv; ++i) off += U.r.wsum[i][k];
+        if (t < nchk) pre[t * 5 + k] = off + incl[k] - v[k];
+        if (t == nchk - 1) pre[nchk * 5 + k] = off + incl[k];
+    }
+    __syncthreads();
+    for (int i = t; i < (nchk + 1) * 5; i += 1024) p.pre[(i / 5) * 8 + i % 5] = pre[i];
+    RNG_PROF_T(r1);
+    RNG_PROF_ADD(8, r1 - r0);
+
+    // ---- the updates in stream order (wave 0)
+    if (wv == 0) {
+        MtjWalk wk;
+        wk.pre = pre; wk.ctag = U.r.ctag; wk.cbm = U.r.cbm; wk.p = p; wk.nchk = nchk;
+        int q = pos0, ovf = 0;
+        int has = st->has_gauss;
+        double gauss = st->gauss;
+        for (int u = 0; u < a.nupd && !ovf; ++u) {
+            int32_t* const out_idx = a.out_idx ? (int32_t*)((char*)sr(a.out_idx, so) + u * a.slot_bytes) : nullptr;
+            float* const out_norm = (float*)((char*)sr(a.out_norm, so) + u * a.slot_bytes);
+            int* ru = p.res + 16 + 16 * u;
+            int ib = q, ie = q, ibase = 0;
+            if (a.n_int > 0) {
+                if (rng == 0) {
+                    for (int i = lane; i < a.n_int; i += 64) out_idx[i] = 0;
+                } else {
+                    ibase = wk.prefix(0, q);
+                    const int m = wk.find(0, ibase + a.n_int);
+                    if (m < 0) { ovf = 1; break; }
+                    ie = q = m + 1;
+                }
+            }
+            int oi = 0;
+            if (a.n_norm > 0 && has) {
+                if (lane == 0) out_norm[0] = (float)gauss;
+                has = 0;
+                gauss = 0.0;     // NumPy clears the cached value with the flag
+                oi = 1;
+            }
+            const int need = (a.n_norm - oi + 1) >> 1;
+            int pb = q, pe = q, pbase = 0;
+            if (need > 0) {
+                const int kind = 1 + (q & 3);
+                pbase = wk.prefix(kind, q);
+                const int m = wk.find(kind, pbase + need);
+                if (m < 0) { ovf = 1; break; }
+                pe = q = m + 4;
+                if ((a.n_norm - oi) & 1) {   // the last pair's second normal is cached
+                    double x1, x2, r2;
+                    polar_acc(mt_temper(p.sw[m]), mt_temper(p.sw[m + 1]), mt_temper(p.sw[m + 2]), mt_temper(p.sw[m + 3]),
+                              x1, x2, r2);
+                    gauss = sqrt(-2.0 * log(r2) / r2) * x1;
+                    has = 1;
+                }
+            }
+            if (lane == 0) {
+                ru[0] = ib; ru[1] = ie; ru[2] = ibase;
+                ru[3] = pb; ru[4] = pe; ru[5] = pbase; ru[6] = oi;
+            }
+        }
+        if (!ovf && q > pos0 && 624 * ((q - 1) / 624 + 1) > W) ovf = 1;   // the state block must exist
+        if (lane == 0) {
+            sh_q = q; sh_ovf = ovf; sh_has = has; sh_gauss = gauss;
+            p.res[0] = ovf;
+            p.res[2] = q;
+        }
+    }
+    __syncthreads();
+    RNG_PROF_T(r2);
+    RNG_PROF_ADD(9, r2 - r1);
+    if (sh_ovf) {   // the batch outran the generated words: rng_body redraws it from the unchanged state
+        RngArgs b = a;
+        b.pairs = nullptr;
+        b.backup = nullptr;     // k_mtj_head saved it
+        rng_body(b, U.fb);
+        return;
+    }
+    const int q = sh_q;
+    if (q > pos0) {
+        const int b = (q - 1) / 624;
+        for (int i = t; i < 624; i += 1024) st->key[i] = p.sw[624 * b + i];
+        if (t == 0) {
+            st->pos = q - b * 624;
+            p.res[8] = 624 * b;      // the next batch's head may copy its words from here
+            p.res[9] = W;
+            p.res[10] = MTJ_CHAIN;
+        }
+    }
+    if (t == 0) {
+        st->has_gauss = sh_has;
+        st->gauss = sh_gauss;
+        if (a.slot >= 0) {
+            const int64_t seq = a.reset_seq ? ctl->step_seq + (a.reset_seq - 1) : ctl->rng_seq;
+            for (int u = 0; u < a.nupd; ++u) ctl->pseq[a.slot + u] = seq + u;
+            ctl->rng_seq = seq + a.nupd;
+        }
+    }
+    RNG_PROF_T(r3);
+    RNG_PROF_ADD(10, r3 - r2);
+    RNG_PROF_ADD(11, 1);
+}
+
+// Chunk c's randint values are stored directly; its accepted polar groups are first compacted
+// into an LDS list, so that the fp64 transform runs on every lane (one in four positions of a
+// range is a candidate)
+#define MTJ_EMIT_CAP (MTJ_CHK / 4 + NBATCH_MAX + 8)
+__global__ __launch_bounds__(256) void k_mtj_emit(RngArgs a) {
+    __shared__ uint32_t bm[2][64];
+    __shared__ int wpre[64][5];
+    __shared__ int ru[NBATCH_MAX][8];
+    __shared__ uint32_t lw[MTJ_EMIT_CAP][4];
+    __shared__ int lo[MTJ_EMIT_CAP], lu[MTJ_EMIT_CAP];
+    __shared__ int ln;
+    const int64_t so = seed_off(a.sstride);
+    RNG_PROF_T(e0);
+    const MtjPtrs p = mtj_ptrs(a, so);
+    if (p.res[0]) return;
+    const int c = blockIdx.x, t = threadIdx.x;
+    const int qf = p.res[2];
+    if (c * MTJ_CHK >= qf) return;
+    const uint64_t rng = mtj_u64(p.res + 4), mask = mtj_u64(p.res + 6);
+    uint32_t wd[MTJ_CHK / 256][4];   // the positions' 4-word groups, loaded before any use
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        const int m = c * MTJ_CHK + i * 256 + t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wd[i][r] = m < qf ? p.sw[m + r] : 0u;
+    }
+    if (t < 64) {      // wave 0: the bitmaps and their exclusive prefix over the chunk's words, per kind
+        const uint32_t fi = p.fi[c * (MTJ_CHK / 32) + t], fp = p.fp[c * (MTJ_CHK / 32) + t];
+        bm[0][t] = fi;
+        bm[1][t] = fp;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            const int n = __popc((k == 0 ? fi : fp) & mtj_rmask(k));
+            wpre[t][k] = p.pre[c * 8 + k] + wave_incl_scan(n) - n;
+        }
+    }
+    if (t < a.nupd * 8) ru[t >> 3][t & 7] = p.res[16 + 16 * (t >> 3) + (t & 7)];
+    if (t == 0) ln = 0;
+    __syncthreads();
+    RNG_PROF_T(e1);
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        const int m = c * MTJ_CHK + i * 256 + t;
+        if (m >= qf) break;
+        const int wl = (m - c * MTJ_CHK) >> 5;
+        const uint32_t below = (1u << (m & 31)) - 1u;
+        for (int u = 0; u < a.nupd; ++u) {
+            if (m >= ru[u][0] && m < ru[u][1]) {
+                if ((bm[0][wl] >> (m & 31)) & 1u) {
+                    const int rank = wpre[wl][0] + __popc(bm[0][wl] & below) - ru[u][2];
+                    const uint32_t w = mt_temper(wd[i][0]);
+                    int32_t* out_idx = (int32_t*)((char*)sr(a.out_idx, so) + u * a.slot_bytes);
+                    if ((unsigned)rank < (unsigned)a.n_int) out_idx[rank] = (int32_t)(rng == 0xFFFFFFFFULL ? w : (w & (uint32_t)mask));
+                }
+                break;
+            }
+            if (m >= ru[u][3] && m < ru[u][4]) {
+                const int kind = 1 + (m & 3);
+                if (((m - ru[u][3]) & 3) == 0 && ((bm[1][wl] >> (m & 31)) & 1u)) {
+                    const int rank = wpre[wl][kind] + __popc(bm[1][wl] & mtj_rmask(kind) & below) - ru[u][5];
+                    const int e = atomicAdd(&ln, 1);
+                    if (e < MTJ_EMIT_CAP) {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) lw[e][r] = wd[i][r];
+                        lo[e] = ru[u][6] + 2 * rank;
+                        lu[e] = u;
+                    }
+                }
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    RNG_PROF_T(e2);
+    const int n = min(ln, MTJ_EMIT_CAP);
+    for (int e = t; e < n; e += 256) {
+        double x1, x2, r2;
+        polar_acc(mt_temper(lw[e][0]), mt_temper(lw[e][1]), mt_temper(lw[e][2]), mt_temper(lw[e][3]), x1, x2, r2);
+        const double f = sqrt(-2.0 * log(r2) / r2);
+        float* out = (float*)((char*)sr(a.out_norm, so) + lu[e] * a.slot_bytes);
+        const int o = lo[e];
+        if ((unsigned)o < (unsigned)a.n_norm) out[o] = (float)(f * x2);
+        if ((unsigned)(o + 1) < (unsigned)a.n_norm) out[o + 1] = (float)(f * x1);
+    }
+    RNG_PROF_T(e3);
+#ifdef SACX_RNG_PROF
+    if (t == 0) {    // per workgroup: loads, ranks, transforms (sums) and the span's first start / last end
+        atomicAdd(&g_rng_prof[12], e1 - e0);
+        atomicAdd(&g_rng_prof[13], e2 - e1);
+        atomicAdd(&g_rng_prof[14], e3 - e2);
+        atomicAdd(&g_rng_prof[15], 1ULL);
+    }
+#endif
+}
+
+// words a launch of `a` expects to draw (randint at acceptance >= 1/2) and whether it takes the
+// segmented path, with its segment count
+static int mtj_segments(const RngArgs& a) {
+    if (a.jw == nullptr || a.jL < MTJ_HEAD || a.nupd > NBATCH_MAX) return 0;
+    const double per = 2.0 * a.n_int + (double)((a.n_norm + 1) >> 1) * (4.0 / 0.78539816339744831);
+    const double words = a.nupd * per;
+    if (words < (double)a.jmin) return 0;
+    // + MTJ_HEAD: the next batch's head words (k_mtj_head copies them)
+    const double est = 624.0 + 1.02 * words + 8.0 * sqrt(words) + 64.0 * a.nupd + 1024.0 + MTJ_HEAD;
+    int S = (int)ceil((est - 1.0) / a.jL);
+    const char* ue = std::getenv("SACX_MTJ_UNDER");
+    const int under = ue ? std::atoi(ue) : 0;
+    if (under > 0) S = std::max(1, std::min(S, under));   // tests: too few segments (the fallback)
+    const int64_t W = (int64_t)S * a.jL + 1;
+    if (S > a.jsmax || (W + MTJ_CHK - 1) / MTJ_CHK > MTJ_MAXCHK) return 0;
+    return S;
+}
+
+void launch_rng(const RngArgs& a0, hipStream_t s) {
+    if (const int S = mtj_segments(a0)) {
+        RngArgs a = a0;
+        a.jS = S;
+        const int z = seeds_z(a.nseeds);
+        const int nchk = (int)(((int64_t)S * a.jL + 1 + MTJ_CHK - 1) / MTJ_CHK);
+        hipLaunchKernelGGL(k_mtj_head, dim3(1, 1, z), dim3(1024), 0, s, a);
+        if (S > 1) hipLaunchKernelGGL(k_mtj_jump, dim3(MTJ_NC, S - 1, z), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mtj_seg, dim3(S, 1, z), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_mtj_flags, dim3(nchk, 1, z), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_mtj_resolve, dim3(1, 1, z), dim3(1024), 0, s, a);
+        hipLaunchKernelGGL(k_mtj_emit, dim3(nchk, 1, z), dim3(256), 0, s, a);
+        return;
+    }
+    const RngArgs& a = a0;
     hipLaunchKernelGGL(k_rng, dim3(1, 1, seeds_z(a.nseeds)), dim3(RNG_THREADS), 0, s, a);
     if (a.pairs != nullptr && a.n_norm > 0)
         hipLaunchKernelGGL(k_polar, dim3(std::min((a.pcap + 255) / 256, SACX_POLAR_WGS), a.nupd, seeds_z(a.nseeds)),

@@ -21,6 +21,7 @@
 //   alpha.head     evaluate + alpha loss + Adam + clamp + stats   [SAC_expert.py:345-356]
 #include "sacx.h"
 #include "sacx_internal.h"
+#include "mt_jump.h"
 
 #include <rccl/rccl.h>
 
@@ -165,6 +166,10 @@ struct sacx_handle {
     std::vector<std::pair<const float*, const float*>> abf_written;   // plan build: ranges a wired producer stores
     bool rng_split = false;   // k_rng + k_polar (rng.pairs): the polar transform spread over the GPU
     int pcap = 0;             // polar pairs per update (rng.pairs rows per update)
+    bool rng_jump = false;    // segmented sampler (k_mtj_*): the update sampler's launches
+    int jL = 0;               // its segment length (words)
+    int jsmax = 0;            // segments its work area holds
+    int mtj_ramp = 3;         // a graph's first mtj_ramp sampler batches take it (SACX_MTJ_RAMP), the rest k_rng
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
     int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
     int dwl = 0;              // dW + Adam launches on k_dwl: 0 never, 1 when K >= 512, 2 always (SACX_DWL)
@@ -385,6 +390,29 @@ void build_layout(sacx_handle* h) {
         h->pcap = (h->n_norm + 1) / 2;
         h->add("rng.pairs", (int64_t)NBATCH_MAX * h->pcap, 4, SACX_U32, SACX_ROLE_WORK);
         h->add("rng.pairs_oi", 1, NBATCH_MAX, SACX_I32, SACX_ROLE_WORK);
+    }
+    // Segmented sampler (k_mtj_*): a sampler batch of many words (Humanoid: ~135k per update)
+    // is twisted as ~16 segments of L words from jumped-ahead windows and ranked over the GPU
+    // instead of on one workgroup.  L: a 4-update batch in ~16 segments, >= the 20,561 words
+    // every jump reads; the work area holds a batch of NBATCH_MAX updates
+    {
+        const double per = 2.0 * h->B + (double)((h->n_norm + 1) >> 1) * (4.0 / 0.78539816339744831);
+        h->rng_jump = per >= 40000.0;
+        if (const char* e = std::getenv("SACX_RNG_JUMP")) h->rng_jump = std::atoi(e) != 0;
+        if (h->rng_jump) {
+            int64_t L = ((int64_t)std::ceil(per * 1.02 / 4.0) + 63) / 64 * 64;
+            if (const char* e = std::getenv("SACX_MTJ_L")) L = std::atoll(e);
+            L = std::max<int64_t>(L, MTJ_HEAD);
+            const double words = NBATCH_MAX * per;
+            const double est = 624.0 + 1.02 * words + 8.0 * std::sqrt(words) + 64.0 * NBATCH_MAX + 1024.0 + MTJ_HEAD;
+            int smax = (int)std::ceil((est - 1.0) / (double)L) + 1;
+            smax = (int)std::max<int64_t>(2, std::min<int64_t>(smax, ((int64_t)MTJ_MAXCHK * MTJ_CHK - 9) / L));
+            h->jL = (int)L;
+            h->jsmax = smax;
+            h->add("rng.jw", 1, mtj_layout(L, smax).total, SACX_U32, SACX_ROLE_WORK);
+            // x^(kL) mod phi as per-chunk set-bit lists (mt_jump_lists), uploaded at bind
+            h->add("rng.jc", 1, mt_jump_lists_words(smax - 1, MTJ_CH), SACX_I32, SACX_ROLE_STATE);
+        }
     }
     // per-slot update inputs: the sampler + gather run ahead of the updates on a side stream,
     // so everything they write rotates over a ring of slots.  A cheap sampler (HC: 1,536 normals
@@ -934,6 +962,12 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             L.rng.pairs = h->ptr<uint32_t>("rng.pairs");
             L.rng.pairs_oi = h->ptr<int32_t>("rng.pairs_oi");
             L.rng.pcap = h->pcap;
+        }
+        if (h->rng_jump) {
+            L.rng.jw = h->ptr<uint32_t>("rng.jw");
+            L.rng.jc = h->ptr<uint32_t>("rng.jc");
+            L.rng.jL = h->jL;
+            L.rng.jsmax = h->jsmax;
         }
         L.grid = 1;
         L.block = 1024;
@@ -1989,6 +2023,10 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 if (C.kind == Launch::RNG) {
                     C.rng.reset_seq = (b == 0);
                     C.rng.nupd = n;
+                    // the segmented sampler (k_mtj_*) where the chain waits for the draw: the ramp's
+                    // batches; the batches drawn ahead stay on k_rng's one CU, which the chain's
+                    // launches never miss (the segmented launches take CUs: Humanoid bf16 -2 %)
+                    if (b >= h->mtj_ramp) C.rng.jmin = INT32_MAX;
                 } else {
                     C.gather.nupd = n;
                 }
@@ -2468,6 +2506,14 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
             HIPCHK(h, hipMemcpy(h->arena0 + (uint64_t)k * h->seed_bytes + so.off, ones.data(), ones.size() * sizeof(float),
                                 hipMemcpyHostToDevice));
     }
+    if (h->rng_jump) {   // rng.jc: the segmented sampler's jump coefficients
+        const SegInfo& sj = h->seg("rng.jc");
+        std::vector<int32_t> jc((size_t)mt_jump_lists_words(h->jsmax - 1, MTJ_CH));
+        const int64_t used = mt_jump_lists(h->jL, h->jsmax - 1, MTJ_CH, jc.data());
+        for (int k = 0; k < h->seeds; ++k)
+            HIPCHK(h, hipMemcpy(h->arena0 + (uint64_t)k * h->seed_bytes + sj.off, jc.data(), (size_t)used * sizeof(int32_t),
+                                hipMemcpyHostToDevice));
+    }
     // 32x32 forward / dX tiles once the launches are wide: seeds x batch >= 1024 rows (packed
     // seeds; Humanoid B = 1024: SAC-EO +5.6 %, model fit +8 %, SAC +1 %); a handle-level rule, so
     // the launches merged_body folds together always agree.  From 4,096 rows the dW + Adam
@@ -2494,6 +2540,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // ramp and the sampler's lead over the chain favour smaller batches (5.80k vs 5.62k at 8)
     h->nbatch = h->n_norm <= 16384 ? 8 : 4;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
+    if (const char* e = std::getenv("SACX_MTJ_RAMP")) h->mtj_ramp = std::atoi(e);
     while (h->nslot % h->nbatch || h->nslot < 2 * h->nbatch) --h->nbatch;   // the ring holds whole batches
     if (h->dp_ranks > 0) {
         if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");

@@ -464,7 +464,50 @@ struct RngArgs {
     uint32_t* pairs;
     int32_t* pairs_oi;
     int32_t pcap;
+    // segmented sampler (launch_rng: a batch of many words): the batch's raw stream is generated
+    // as jS segments of jL words, each but the first started from a window jumped to from the
+    // key block (mt_jump.h), then consumed by flag / prefix / resolve / emit launches over the
+    // GPU (k_mtj_*).  jw: the work area (mtj_layout, per seed); nullptr: the one-workgroup k_rng
+    uint32_t* jw;
+    const uint32_t* jc;    // jump coefficients x^(k jL) mod phi, k = 1 .. jsmax - 1 (624 words each)
+    int32_t jL;
+    int32_t jsmax;         // segments the work area holds
+    int32_t jS;            // segments of this launch (launch_rng)
+    int32_t jmin;          // launches expecting fewer words stay on k_rng
 };
+
+// ---------------------------------------------------------------- segmented sampler layout
+#define MTJ_CH 320                                   // jump coefficient bits per workgroup
+#define MTJ_NC ((19937 + MTJ_CH - 1) / MTJ_CH)       // jump workgroups per window (63)
+#define MTJ_HEAD (19937 + 624)                       // words [0, MTJ_HEAD) feed every jump
+#define MTJ_CHK 2048                                 // flag chunk (words)
+#define MTJ_MAXCHK 1024                              // chunks the resolve workgroup scans
+#define MTJ_RES_WORDS (16 + 16 * NBATCH_MAX)
+#define MTJ_PF 128                                   // chunks k_mtj_resolve finds in LDS
+// res words: [0] overflow, [1] words generated, [2] final position, [3] pos0, [4..5] rng,
+// [6..7] mask; update u at 16 + 16 u: [0] ib [1] ie [2] ibase [3] pb [4] pe [5] pbase [6] oi
+// ptag: the chunks around each update's predicted boundaries (k_mtj_head), pfbm: their two
+// bitmaps, copied there by k_mtj_flags
+struct MtjLayout {
+    int64_t sw, part, fi, fp, cnt, pre, res, ptag, pfbm, total, wcap;
+    int32_t nchk;
+};
+__host__ __device__ inline MtjLayout mtj_layout(int64_t L, int smax) {
+    MtjLayout y{};
+    y.wcap = ((smax * L + 1 + 8 + MTJ_CHK - 1) / MTJ_CHK) * MTJ_CHK;
+    y.nchk = (int32_t)(y.wcap / MTJ_CHK);
+    y.sw = 0;
+    y.part = y.wcap;
+    y.fi = y.part + (int64_t)(smax - 1) * MTJ_NC * 624;
+    y.fp = y.fi + y.wcap / 32;
+    y.cnt = y.fp + y.wcap / 32;
+    y.pre = y.cnt + (int64_t)y.nchk * 8;
+    y.res = y.pre + (int64_t)(y.nchk + 1) * 8;
+    y.ptag = y.res + MTJ_RES_WORDS;
+    y.pfbm = y.ptag + MTJ_PF;
+    y.total = y.pfbm + (int64_t)MTJ_PF * 128;
+    return y;
+}
 
 struct GatherArgs {
     const float* replay;   // [cap, stride]

@@ -145,3 +145,22 @@ def test_launch_header_round_trip(tmp_path):
                            os.path.join(root, "tests", "khdr_check.cpp"), "-o", str(exe)])
     out = subprocess.check_output([str(exe)], text=True)
     assert "0 mismatches" in out, out
+
+
+def test_mt_jump_windows(tmp_path):
+    """The segmented sampler's jump-ahead (csrc/mt_jump.cpp: MT19937's characteristic polynomial
+    by Berlekamp-Massey, x^(kL) mod phi): the 624-word windows k L + 1 .. k L + 624 rebuilt as
+    XORs of the words after a key block equal the directly generated stream (3 segment lengths,
+    k = 1 .. 4)."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("g++") is None:
+        pytest.skip("g++ not on PATH")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    csrc = os.path.join(root, "sac-expert_amd", "csrc")
+    exe = tmp_path / "mtj"
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-I", csrc, os.path.join(root, "tests", "mtjump_check.cpp"),
+                           os.path.join(csrc, "mt_jump.cpp"), "-o", str(exe)])
+    out = subprocess.check_output([str(exe)], text=True)
+    assert " 0 mismatches" in out, out

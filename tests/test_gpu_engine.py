@@ -56,6 +56,48 @@ def test_rng_big_draws(gpu_available):
     eng.close()
 
 
+@pytest.mark.parametrize("mode", ["segmented", "fallback", "k_rng"])
+def test_rng_segmented_batches(gpu_available, monkeypatch, mode):
+    """Humanoid-sized draws (~135k MT words per update) take the segmented sampler (k_mtj_*:
+    jumped-ahead segments, flag / prefix / resolve / emit over the GPU).  Over a captured graph
+    (two batches of 4 updates after a cached gaussian) and then eager updates, the draws and the
+    final state equal NumPy's stream -- on the segmented path, on its fallback (forced: one
+    segment, too few words, rng_body redraws the batch) and on the one-workgroup k_rng."""
+    if mode == "fallback":
+        monkeypatch.setenv("SACX_MTJ_UNDER", "1")
+    if mode == "k_rng":
+        monkeypatch.setenv("SACX_RNG_JUMP", "0")
+    S, A, B, N = 4, 17, 1024, (1 << 20) + 3
+    eng, *_ = make_pair(S=S, A=A, hidden=(16, 16), B=B, N=N, graph_steps=8)
+    rs = np.random.RandomState(2024)
+    rs.normal(size=1)                                    # a cached gaussian (has_gauss)
+    eng.rng_set_state(rs.get_state())
+    eng.step(8)
+    eng.sync()
+    ctl = eng.v["ctl"][0].cpu().numpy()
+    seq0 = int(ctl[6]) - 8                               # step_seq before the call
+    for u in range(8):
+        idx = rs.randint(N, size=B)
+        nz = rs.normal(size=3 * B * A).astype(np.float32)
+        slots = [k for k in range(8) if int(ctl[16 + k]) == seq0 + u]
+        assert len(slots) == 1, (u, ctl[16:24])
+        k = slots[0]
+        assert np.array_equal(eng.v[f"slot{k}.idx"][0].cpu().numpy(), idx), (mode, u)
+        assert np.array_equal(eng.v[f"slot{k}.noise"][0].cpu().numpy(), nz), (mode, u)
+    rs.normal(size=3)                                    # an odd draw: the next update starts cached
+    eng.rng_set_state(rs.get_state())
+    for _ in range(2):
+        eng.step(1, eager=True)
+        eng.sync()
+        idx = rs.randint(N, size=B)
+        nz = rs.normal(size=3 * B * A).astype(np.float32)
+        assert np.array_equal(eng.v["slot0.idx"][0].cpu().numpy(), idx), mode
+        assert np.array_equal(eng.v["slot0.noise"][0].cpu().numpy(), nz), mode
+    got, ref = eng.rng_get_state(), rs.get_state()
+    assert np.array_equal(got[1], ref[1]) and got[2] == ref[2] and got[3] == ref[3] and got[4] == ref[4]
+    eng.close()
+
+
 @pytest.mark.parametrize("host", [True, False])
 def test_replay_ring_fifo(gpu_available, host):
     """TrajectoryBuffer.add truncation (buffers.py:60-66) on the device ring, from host rows

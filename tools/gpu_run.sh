@@ -54,7 +54,7 @@ for step in "$@"; do
     cfgenv)     # bench of config C under one extra environment setting: cfgenv=C:VAR=VALUE (VAR=VALUE may be -)
       cfg=${arg%%:*}; ev=${arg#*:}
       if [ "$ev" = "-" ]; then ev="SACX_NOP=1"; fi
-      env "$ev" timeout -k 10 300 python bench.py --config $cfg --steps 1000 --warmup 100 --no-cpu-baseline > "$log" 2>&1
+      env $ev timeout -k 10 300 python bench.py --config $cfg --steps 1000 --warmup 100 --no-cpu-baseline > "$log" 2>&1
       rc=$?; echo "[$n cfgenv $arg] rc=$rc $(value "$log")" ;;
     mfitv)      # the fit timing with a variant library: mfitv=<tools/libvar name>
       { SACX_LIBPATH=$PWD/tools/libvar/libsacx_$arg.so timeout -k 10 200 python tools/model_fit_time.py hc_eo 512 && \
@@ -100,6 +100,13 @@ for step in "$@"; do
     rngbench)
       timeout -k 10 120 ./tools/rng_bench > "$log" 2>&1
       rc=$?; echo "[$n rngbench] rc=$rc"; cat "$log" ;;
+    rngenv)     # rng_bench "humanoid segmented" under one extra environment setting: rngenv=VAR=VALUE
+      env "$arg" timeout -k 10 120 ./tools/rng_bench "humanoid segmented" > "$log" 2>&1
+      rc=$?; echo "[$n rngenv $arg] rc=$rc $(grep 'us/update' "$log" | tail -n 1)" ;;
+    rngprof)    # rocprofv3 kernel-trace (+ stats) of the rng_bench configurations matching $arg
+      timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/rngprof_$n" -o r \
+          -- ./tools/rng_bench "$arg" > "$log" 2>&1
+      rc=$?; echo "[$n rngprof $arg] rc=$rc"; tail -n 4 "$log" ;;
     ktimev)     # ktime with a variant library: ktimev=<config>:<tools/libvar name>
       cfg=${arg%%:*}; var=${arg#*:}
       SACX_LIBPATH=$PWD/tools/libvar/libsacx_$var.so timeout -k 10 200 python tools/ktime_dump.py "$cfg" > "$log" 2>&1
