@@ -3583,6 +3583,8 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
     __shared__ MtjResolveShared U;
     __shared__ int sh_q, sh_ovf, sh_has;
     __shared__ double sh_gauss;
+    __shared__ int sh_ru[NBATCH_MAX][8];     // the walk's per-update results (stored after it)
+    __shared__ float sh_g0[NBATCH_MAX];      // update u's leading cached normal (sh_ru[u][6] = 1)
     int* const pre = U.r.pre;
     const int64_t so = seed_off(a.sstride);
     const MtjPtrs p = mtj_ptrs(a, so);
@@ -3629,8 +3631,6 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
         double gauss = st->gauss;
         for (int u = 0; u < a.nupd && !ovf; ++u) {
             int32_t* const out_idx = a.out_idx ? (int32_t*)((char*)sr(a.out_idx, so) + u * a.slot_bytes) : nullptr;
-            float* const out_norm = (float*)((char*)sr(a.out_norm, so) + u * a.slot_bytes);
-            int* ru = p.res + 16 + 16 * u;
             int ib = q, ie = q, ibase = 0;
             if (a.n_int > 0) {
                 if (rng == 0) {
@@ -3644,7 +3644,7 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
             }
             int oi = 0;
             if (a.n_norm > 0 && has) {
-                if (lane == 0) out_norm[0] = (float)gauss;
+                if (lane == 0) sh_g0[u] = (float)gauss;
                 has = 0;
                 gauss = 0.0;     // NumPy clears the cached value with the flag
                 oi = 1;
@@ -3665,9 +3665,9 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
                     has = 1;
                 }
             }
-            if (lane == 0) {
-                ru[0] = ib; ru[1] = ie; ru[2] = ibase;
-                ru[3] = pb; ru[4] = pe; ru[5] = pbase; ru[6] = oi;
+            if (lane == 0) {   // LDS: a global store here would be waited for by the next search's loads
+                sh_ru[u][0] = ib; sh_ru[u][1] = ie; sh_ru[u][2] = ibase;
+                sh_ru[u][3] = pb; sh_ru[u][4] = pe; sh_ru[u][5] = pbase; sh_ru[u][6] = oi;
             }
         }
         if (!ovf && q > pos0 && 624 * ((q - 1) / 624 + 1) > W) ovf = 1;   // the state block must exist
@@ -3687,6 +3687,8 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
         rng_body(b, U.fb);
         return;
     }
+    if (t < a.nupd * 7) p.res[16 + 16 * (t / 7) + t % 7] = sh_ru[t / 7][t % 7];
+    if (t < a.nupd && sh_ru[t][6]) *(float*)((char*)sr(a.out_norm, so) + t * a.slot_bytes) = sh_g0[t];
     const int q = sh_q;
     if (q > pos0) {
         const int b = (q - 1) / 624;
@@ -3719,7 +3721,6 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
 __global__ __launch_bounds__(256) void k_mtj_emit(RngArgs a) {
     __shared__ uint32_t bm[2][64];
     __shared__ int wpre[64][5];
-    __shared__ int ru[NBATCH_MAX][8];
     __shared__ uint32_t lw[MTJ_EMIT_CAP][4];
     __shared__ int lo[MTJ_EMIT_CAP], lu[MTJ_EMIT_CAP];
     __shared__ int ln;
@@ -3731,13 +3732,6 @@ __global__ __launch_bounds__(256) void k_mtj_emit(RngArgs a) {
     const int qf = p.res[2];
     if (c * MTJ_CHK >= qf) return;
     const uint64_t rng = mtj_u64(p.res + 4), mask = mtj_u64(p.res + 6);
-    uint32_t wd[MTJ_CHK / 256][4];   // the positions' 4-word groups, loaded before any use
-#pragma unroll
-    for (int i = 0; i < MTJ_CHK / 256; ++i) {
-        const int m = c * MTJ_CHK + i * 256 + t;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) wd[i][r] = m < qf ? p.sw[m + r] : 0u;
-    }
     if (t < 64) {      // wave 0: the bitmaps and their exclusive prefix over the chunk's words, per kind
         const uint32_t fi = p.fi[c * (MTJ_CHK / 32) + t], fp = p.fp[c * (MTJ_CHK / 32) + t];
         bm[0][t] = fi;
@@ -3748,39 +3742,76 @@ __global__ __launch_bounds__(256) void k_mtj_emit(RngArgs a) {
             wpre[t][k] = p.pre[c * 8 + k] + wave_incl_scan(n) - n;
         }
     }
-    if (t < a.nupd * 8) ru[t >> 3][t & 7] = p.res[16 + 16 * (t >> 3) + (t & 7)];
     if (t == 0) ln = 0;
     __syncthreads();
     RNG_PROF_T(e1);
+    const int lane = t & 63;
+    // what each of the thread's eight positions is: 1 an accepted randint word of update uu
+    // (output o = its rank), 2 an accepted polar group (o = its first output), 0 neither.  The
+    // update ranges are uniform (scalar loads), the bitmap words and prefixes of all eight
+    // positions are read from LDS in one batch: no dependent LDS round trips per position
+    const int kp = 1 + (t & 3);          // a position's residue class (chunk and step are multiples of 4)
+    int rr[NBATCH_MAX][7];
+#pragma unroll
+    for (int u = 0; u < NBATCH_MAX; ++u)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) rr[u][k] = u < a.nupd ? p.res[16 + 16 * u + k] : 0;
+    uint32_t b0[MTJ_CHK / 256], b1[MTJ_CHK / 256];
+    int w0[MTJ_CHK / 256], w1[MTJ_CHK / 256];
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        const int wl = (i * 256 + t) >> 5;
+        b0[i] = bm[0][wl]; b1[i] = bm[1][wl];
+        w0[i] = wpre[wl][0]; w1[i] = wpre[wl][kp];
+    }
+    int what[MTJ_CHK / 256], uu[MTJ_CHK / 256], o[MTJ_CHK / 256];
 #pragma unroll
     for (int i = 0; i < MTJ_CHK / 256; ++i) {
         const int m = c * MTJ_CHK + i * 256 + t;
-        if (m >= qf) break;
-        const int wl = (m - c * MTJ_CHK) >> 5;
-        const uint32_t below = (1u << (m & 31)) - 1u;
-        for (int u = 0; u < a.nupd; ++u) {
-            if (m >= ru[u][0] && m < ru[u][1]) {
-                if ((bm[0][wl] >> (m & 31)) & 1u) {
-                    const int rank = wpre[wl][0] + __popc(bm[0][wl] & below) - ru[u][2];
-                    const uint32_t w = mt_temper(wd[i][0]);
-                    int32_t* out_idx = (int32_t*)((char*)sr(a.out_idx, so) + u * a.slot_bytes);
-                    if ((unsigned)rank < (unsigned)a.n_int) out_idx[rank] = (int32_t)(rng == 0xFFFFFFFFULL ? w : (w & (uint32_t)mask));
-                }
-                break;
-            }
-            if (m >= ru[u][3] && m < ru[u][4]) {
-                const int kind = 1 + (m & 3);
-                if (((m - ru[u][3]) & 3) == 0 && ((bm[1][wl] >> (m & 31)) & 1u)) {
-                    const int rank = wpre[wl][kind] + __popc(bm[1][wl] & mtj_rmask(kind) & below) - ru[u][5];
-                    const int e = atomicAdd(&ln, 1);
-                    if (e < MTJ_EMIT_CAP) {
+        const uint32_t bit = 1u << (m & 31), below = bit - 1u;
+        what[i] = 0; uu[i] = 0; o[i] = 0;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) lw[e][r] = wd[i][r];
-                        lo[e] = ru[u][6] + 2 * rank;
-                        lu[e] = u;
-                    }
-                }
-                break;
+        for (int u = 0; u < NBATCH_MAX; ++u) {
+            if (u >= a.nupd || m >= qf) break;
+            if (m >= rr[u][0] && m < rr[u][1] && (b0[i] & bit)) {
+                what[i] = 1; uu[i] = u;
+                o[i] = w0[i] + __popc(b0[i] & below) - rr[u][2];
+            }
+            if (m >= rr[u][3] && m < rr[u][4] && ((m - rr[u][3]) & 3) == 0 && (b1[i] & bit)) {
+                what[i] = 2; uu[i] = u;
+                o[i] = rr[u][6] + 2 * (w1[i] + __popc(b1[i] & mtj_rmask(kp) & below) - rr[u][5]);
+            }
+        }
+    }
+    // the candidates' words, all requested in one round
+    uint32_t wd[MTJ_CHK / 256][4];
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        const int m = c * MTJ_CHK + i * 256 + t;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wd[i][r] = (what[i] == 2 || (what[i] == 1 && r == 0)) ? p.sw[m + r] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < MTJ_CHK / 256; ++i) {
+        if (what[i] == 1) {
+            const uint32_t w = mt_temper(wd[i][0]);
+            int32_t* out_idx = (int32_t*)((char*)sr(a.out_idx, so) + uu[i] * a.slot_bytes);
+            if ((unsigned)o[i] < (unsigned)a.n_int) out_idx[o[i]] = (int32_t)(rng == 0xFFFFFFFFULL ? w : (w & (uint32_t)mask));
+        }
+        // the wave's accepted groups appended to the list: one LDS atomic per wave
+        const bool take = what[i] == 2;
+        const unsigned long long bal = __ballot(take);
+        if (bal) {
+            const int first = (int)__builtin_ctzll(bal);
+            int base = 0;
+            if (lane == first) base = atomicAdd(&ln, __popcll(bal));
+            base = __builtin_amdgcn_readlane(base, first);
+            const int e = base + __popcll(bal & ((1ULL << lane) - 1ULL));
+            if (take && e < MTJ_EMIT_CAP) {
+#pragma unroll
+                for (int r = 0; r < 4; ++r) lw[e][r] = wd[i][r];
+                lo[e] = o[i];
+                lu[e] = uu[i];
             }
         }
     }

@@ -100,9 +100,9 @@ for step in "$@"; do
     rngbench)
       timeout -k 10 120 ./tools/rng_bench > "$log" 2>&1
       rc=$?; echo "[$n rngbench] rc=$rc"; cat "$log" ;;
-    rngenv)     # rng_bench "humanoid segmented" under one extra environment setting: rngenv=VAR=VALUE
-      env "$arg" timeout -k 10 120 ./tools/rng_bench "humanoid segmented" > "$log" 2>&1
-      rc=$?; echo "[$n rngenv $arg] rc=$rc $(grep 'us/update' "$log" | tail -n 1)" ;;
+    rngenv)     # rng_bench's segmented Humanoid cases under extra environment settings: rngenv=VAR=VALUE[ VAR=VALUE]
+      env $arg timeout -k 10 120 ./tools/rng_bench "humanoid seg" > "$log" 2>&1
+      rc=$?; echo "[$n rngenv $arg] rc=$rc"; grep 'us/update\|emit per' "$log" ;;
     rngprof)    # rocprofv3 kernel-trace (+ stats) of the rng_bench configurations matching $arg
       timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/rngprof_$n" -o r \
           -- ./tools/rng_bench "$arg" > "$log" 2>&1
