@@ -3208,6 +3208,9 @@ __global__ __launch_bounds__(256) void k_polar(RngArgs a) {
 //                  the polar transform in place
 // Stream words are numbered from the key block (words 0 .. 623 = st->key), as in rng_body.
 #define MTJ_RW 4096
+// global-address-space pointers: global_load / global_store (a pointer loaded from the kernel
+// arguments is otherwise generic, and its accesses flat ones that also wait on the LDS counter)
+#define MTJ_G __attribute__((address_space(1)))
 
 __device__ __forceinline__ bool polar_acc(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, double& x1,
                                           double& x2, double& r2) {
@@ -3227,7 +3230,7 @@ __device__ __forceinline__ void mtj_put(uint32_t* ring, int q, uint32_t v) {
 
 // words [n0, n1) into the LDS ring and sw.  The words from `base` on are resident (a 624-word
 // window at base, or the 1,078 before n0); words below base + 1078 take the 227-wide form
-__device__ void mtj_twist(uint32_t* ring, uint32_t* __restrict__ sw, int base, int n0, int n1) {
+__device__ void mtj_twist(uint32_t* ring, MTJ_G uint32_t* __restrict__ sw, int base, int n0, int n1) {
     const int t = threadIdx.x;
     while (n0 < n1 && n0 < base + 1078) {
         const int e = min(min(n1, base + 1078), n0 + 227);
@@ -3256,29 +3259,30 @@ __device__ void mtj_twist(uint32_t* ring, uint32_t* __restrict__ sw, int base, i
     }
 }
 
+// the work area's pointers are in the global address space (MTJ_G)
 struct MtjPtrs {
-    uint32_t* sw;
-    uint32_t* fi;
-    uint32_t* fp;
-    int32_t* cnt;
-    int32_t* pre;
-    int32_t* res;
-    uint32_t* part;
-    int32_t* ptag;
-    uint32_t* pfbm;
+    MTJ_G uint32_t* sw;
+    MTJ_G uint32_t* fi;
+    MTJ_G uint32_t* fp;
+    MTJ_G int32_t* cnt;
+    MTJ_G int32_t* pre;
+    MTJ_G int32_t* res;
+    MTJ_G uint32_t* part;
+    MTJ_G int32_t* ptag;
+    MTJ_G uint32_t* pfbm;
 };
 __device__ __forceinline__ MtjPtrs mtj_ptrs(const RngArgs& a, int64_t so) {
     uint32_t* jw = sr(a.jw, so);
     const MtjLayout y = mtj_layout(a.jL, a.jsmax);
     MtjPtrs p;
-    p.sw = jw + y.sw; p.fi = jw + y.fi; p.fp = jw + y.fp;
-    p.cnt = (int32_t*)(jw + y.cnt); p.pre = (int32_t*)(jw + y.pre); p.res = (int32_t*)(jw + y.res);
-    p.part = jw + y.part;
-    p.ptag = (int32_t*)(jw + y.ptag);
-    p.pfbm = jw + y.pfbm;
+    p.sw = (MTJ_G uint32_t*)(jw + y.sw); p.fi = (MTJ_G uint32_t*)(jw + y.fi); p.fp = (MTJ_G uint32_t*)(jw + y.fp);
+    p.cnt = (MTJ_G int32_t*)(jw + y.cnt); p.pre = (MTJ_G int32_t*)(jw + y.pre); p.res = (MTJ_G int32_t*)(jw + y.res);
+    p.part = (MTJ_G uint32_t*)(jw + y.part);
+    p.ptag = (MTJ_G int32_t*)(jw + y.ptag);
+    p.pfbm = (MTJ_G uint32_t*)(jw + y.pfbm);
     return p;
 }
-__device__ __forceinline__ uint64_t mtj_u64(const int32_t* r) { return ((uint64_t)(uint32_t)r[1] << 32) | (uint32_t)r[0]; }
+__device__ __forceinline__ uint64_t mtj_u64(const MTJ_G int32_t* r) { return ((uint64_t)(uint32_t)r[1] << 32) | (uint32_t)r[0]; }
 
 // The key block of a batch that followed a segmented batch is (normally) a block of that batch's
 // stream, and the words [0, MTJ_HEAD) it needs were generated there too (the estimate keeps
@@ -3401,7 +3405,7 @@ __global__ __launch_bounds__(256) void k_mtj_jump(RngArgs a) {
         s1 ^= win[i + j1];
         s2 ^= win[i + j2];
     }
-    uint32_t* out = p.part + ((size_t)(k - 1) * MTJ_NC + c) * 624;
+    MTJ_G uint32_t* out = p.part + ((size_t)(k - 1) * MTJ_NC + c) * 624;
     out[j0] = s0;
     out[j1] = s1;
     if (j0 + 512 < 624) out[j2] = s2;
@@ -3423,7 +3427,7 @@ __global__ __launch_bounds__(1024) void k_mtj_seg(RngArgs a) {
     } else {
         base = k * a.jL + 1;
         n0 = base + 624;
-        const uint32_t* pt = p.part + (size_t)(k - 1) * MTJ_NC * 624;
+        const MTJ_G uint32_t* pt = p.part + (size_t)(k - 1) * MTJ_NC * 624;
         for (int j = t; j < 624; j += 1024) {
             uint32_t v = 0;
 #pragma unroll
@@ -3506,68 +3510,6 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 __device__ __forceinline__ int wave_isum(int v) { return __builtin_amdgcn_readlane(wave_incl_scan(v), 63); }
 __device__ __forceinline__ uint32_t mtj_rmask(int kind) { return kind == 0 ? 0xFFFFFFFFu : (0x11111111u << (kind - 1)); }
 
-// Wave 0 of k_mtj_resolve walks the updates holding one chunk's two bitmaps in registers (lane l:
-// word l of the chunk), so that the prefix at the position a search ended needs no load.
-struct MtjWalk {
-    const int* pre;      // LDS: exclusive chunk prefixes [chunk][kind], [nchk] = totals
-    const int* ctag;     // LDS: the prefetched chunks (-1: empty slot)
-    const uint32_t (*cbm)[2][64];
-    MtjPtrs p;
-    int nchk;
-    int cc = -1;         // the chunk held
-    uint32_t fiw = 0, fpw = 0;
-
-    __device__ void hold(int c) {
-        if (c == cc) return;
-        const int lane = threadIdx.x & 63;
-        const unsigned long long b0 = __ballot(ctag[lane] == c), b1 = __ballot(ctag[64 + lane] == c);
-        if (b0 | b1) {
-            const int s = b0 ? (int)__builtin_ctzll(b0) : 64 + (int)__builtin_ctzll(b1);
-            fiw = cbm[s][0][lane];
-            fpw = cbm[s][1][lane];
-        } else {     // outside the predicted windows: one global round trip
-            fiw = p.fi[c * (MTJ_CHK / 32) + lane];
-            fpw = p.fp[c * (MTJ_CHK / 32) + lane];
-        }
-        cc = c;
-    }
-    // candidates of `kind` accepted at positions < m (kind 0: randint words; 1 + r: groups at r mod 4)
-    __device__ int prefix(int kind, int m) {
-        const int c = m / MTJ_CHK;
-        if (c >= nchk) return pre[nchk * 5 + kind];
-        hold(c);
-        const int lane = threadIdx.x & 63;
-        const int o = m - c * MTJ_CHK;
-        uint32_t w = (kind == 0 ? fiw : fpw) & mtj_rmask(kind);
-        const int lw = o >> 5;
-        if (lane > lw) w = 0;
-        else if (lane == lw) w &= (1u << (o & 31)) - 1u;
-        return pre[c * 5 + kind] + wave_isum(__popc(w));
-    }
-    // the position of the T-th (1-based) accepted candidate of `kind`; -1 past the generated words
-    __device__ int find(int kind, int T) {
-        if (T > pre[nchk * 5 + kind]) return -1;
-        const int lane = threadIdx.x & 63;
-        // the last chunk whose exclusive prefix is < T: among 16-chunk groups, then within one
-        const int g = lane * 16;
-        const int l1 = 63 - __clzll(__ballot(g < nchk && pre[g * 5 + kind] < T));
-        const int c2 = l1 * 16 + lane;
-        const int c = l1 * 16 + 63 - __clzll(__ballot(lane < 16 && c2 < nchk && pre[c2 * 5 + kind] < T));
-        hold(c);
-        const int rem = T - 1 - pre[c * 5 + kind];
-        uint32_t w = (kind == 0 ? fiw : fpw) & mtj_rmask(kind);
-        const int n = __popc(w);
-        const int incl = wave_incl_scan(n);
-        const bool mine = incl - n <= rem && rem < incl;
-        int pos = 0;
-        if (mine) {
-            for (int i = incl - n; i < rem; ++i) w &= w - 1u;
-            pos = c * MTJ_CHK + lane * 32 + __builtin_ctz(w);
-        }
-        return __shfl(pos, (int)__builtin_ctzll(__ballot(mine)));
-    }
-};
-
 // the chunk prefixes (phase 1) share LDS with rng_body's ring (the fallback, after phase 2)
 union MtjResolveShared {
     struct {
@@ -3622,10 +3564,58 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
     RNG_PROF_T(r1);
     RNG_PROF_ADD(8, r1 - r0);
 
-    // ---- the updates in stream order (wave 0)
+    // ---- the updates in stream order (wave 0).  The wave holds one chunk's two bitmaps in
+    // registers (lane l: word l of the chunk), so the prefix where a search ended needs no load;
+    // LDS is addressed through U directly (ds_read), the work area through MTJ_G pointers
     if (wv == 0) {
-        MtjWalk wk;
-        wk.pre = pre; wk.ctag = U.r.ctag; wk.cbm = U.r.cbm; wk.p = p; wk.nchk = nchk;
+        int cc = -1;
+        uint32_t fiw = 0, fpw = 0;
+        auto hold = [&](int c) {
+            if (c == cc) return;
+            const unsigned long long b0 = __ballot(U.r.ctag[lane] == c), b1 = __ballot(U.r.ctag[64 + lane] == c);
+            if (b0 | b1) {
+                const int sl = b0 ? (int)__builtin_ctzll(b0) : 64 + (int)__builtin_ctzll(b1);
+                fiw = U.r.cbm[sl][0][lane];
+                fpw = U.r.cbm[sl][1][lane];
+            } else {     // outside the predicted windows: one global round trip
+                fiw = p.fi[c * (MTJ_CHK / 32) + lane];
+                fpw = p.fp[c * (MTJ_CHK / 32) + lane];
+            }
+            cc = c;
+        };
+        // candidates of `kind` accepted at positions < m (kind 0: randint words; 1 + r: groups at r mod 4)
+        auto prefix = [&](int kind, int m) -> int {
+            const int c = m / MTJ_CHK;
+            if (c >= nchk) return U.r.pre[nchk * 5 + kind];
+            hold(c);
+            const int o = m - c * MTJ_CHK;
+            uint32_t w = (kind == 0 ? fiw : fpw) & mtj_rmask(kind);
+            const int lw = o >> 5;
+            if (lane > lw) w = 0;
+            else if (lane == lw) w &= (1u << (o & 31)) - 1u;
+            return U.r.pre[c * 5 + kind] + wave_isum(__popc(w));
+        };
+        // the position of the T-th (1-based) accepted candidate of `kind`; -1 past the generated words
+        auto find = [&](int kind, int T) -> int {
+            if (T > U.r.pre[nchk * 5 + kind]) return -1;
+            // the last chunk whose exclusive prefix is < T: among 16-chunk groups, then within one
+            const int g = lane * 16;
+            const int l1 = 63 - __clzll(__ballot(g < nchk && U.r.pre[g * 5 + kind] < T));
+            const int c2 = l1 * 16 + lane;
+            const int c = l1 * 16 + 63 - __clzll(__ballot(lane < 16 && c2 < nchk && U.r.pre[c2 * 5 + kind] < T));
+            hold(c);
+            const int rem = T - 1 - U.r.pre[c * 5 + kind];
+            uint32_t w = (kind == 0 ? fiw : fpw) & mtj_rmask(kind);
+            const int n = __popc(w);
+            const int incl = wave_incl_scan(n);
+            const bool mine = incl - n <= rem && rem < incl;
+            int pos = 0;
+            if (mine) {
+                for (int i = incl - n; i < rem; ++i) w &= w - 1u;
+                pos = c * MTJ_CHK + lane * 32 + __builtin_ctz(w);
+            }
+            return __builtin_amdgcn_readlane(pos, (int)__builtin_ctzll(__ballot(mine)));
+        };
         int q = pos0, ovf = 0;
         int has = st->has_gauss;
         double gauss = st->gauss;
@@ -3636,8 +3626,8 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
                 if (rng == 0) {
                     for (int i = lane; i < a.n_int; i += 64) out_idx[i] = 0;
                 } else {
-                    ibase = wk.prefix(0, q);
-                    const int m = wk.find(0, ibase + a.n_int);
+                    ibase = prefix(0, q);
+                    const int m = find(0, ibase + a.n_int);
                     if (m < 0) { ovf = 1; break; }
                     ie = q = m + 1;
                 }
@@ -3653,8 +3643,8 @@ __global__ __launch_bounds__(1024) void k_mtj_resolve(RngArgs a) {
             int pb = q, pe = q, pbase = 0;
             if (need > 0) {
                 const int kind = 1 + (q & 3);
-                pbase = wk.prefix(kind, q);
-                const int m = wk.find(kind, pbase + need);
+                pbase = prefix(kind, q);
+                const int m = find(kind, pbase + need);
                 if (m < 0) { ovf = 1; break; }
                 pe = q = m + 4;
                 if ((a.n_norm - oi) & 1) {   // the last pair's second normal is cached

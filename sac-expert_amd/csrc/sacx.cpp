@@ -181,6 +181,7 @@ struct sacx_handle {
     int unaligned_b = 1;      // dX launches: float4 loads of W_ext rows at any 4-B offset (SACX_UNALIGNED)
     int fwd2 = 1;             // two-layer forward pairs as one k_fwd2 launch where they qualify (SACX_FWD2)
     int mtile = 1;            // model fit tiles: 0 16x16, 1 16x16 + wide dW on 32x32, 2 the handle's (SACX_MTILE)
+    int mt32 = 1;             // fit launches moved to 32x32 tiles under mtile 1 (SACX_MT32): 1 model.bwd1, 2 model.fwd1
     int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
@@ -1639,7 +1640,12 @@ void build_model_plan(sacx_handle* h) {
         F.name = "model.gather+fwd0";
         F.bytes += 4.0 * nm * mb * (2.0 * S + A + 1 + O);
     }
-    add_gemm(h, plan, "model.fwd1", f1, false);
+    {   // model.fwd1 on 32x32 tiles (mt32 bit 2) when it stays its own launch (no k_fwd2 pair)
+        const int t32_fit = h->tile32;
+        if (h->mtile == 1 && (h->mt32 & 2) && !(gfold && h->mfwd2 && S + A <= 32)) h->tile32 = 2;
+        add_gemm(h, plan, "model.fwd1", f1, false);
+        h->tile32 = t32_fit;
+    }
     // the gathered layer 0 and layer 1 as ONE k_fwd2 launch (SACX_MFWD2, default; K0 = S + A <= 32)
     if (gfold && h->mfwd2) fuse_fwd2(h, plan, "model.gather+fwd01");
     add_gemm(h, plan, "model.fwd2", f2, false);
@@ -1673,7 +1679,13 @@ void build_model_plan(sacx_handle* h) {
             B2.gemm.mfin = mf;
         }
     }
-    add_gemm(h, plan, "model.bwd1", b1, false);
+    {   // model.bwd1 (K = H1) on 32x32 dX tiles (mt32 bit 1): half the operand re-reads of the
+        // 16x16 ones at the same k order (bit-identical)
+        const int t32_fit = h->tile32;
+        if (h->mtile == 1 && (h->mt32 & 1) && !bfold) h->tile32 = 2;
+        add_gemm(h, plan, "model.bwd1", b1, false);
+        h->tile32 = t32_fit;
+    }
     if (bfold) {
         Launch& B1 = plan.back();
         if (B1.gemm.t32 || B1.gemm.dwl) { fprintf(stderr, "sacx: model.bwd1 generation needs 16x16 tiles\n"); abort(); }
@@ -2529,6 +2541,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (const char* e = std::getenv("SACX_DW_ROUND")) h->dw_round_tiles = std::atoi(e);
     if (const char* e = std::getenv("SACX_MFUSE")) h->mfuse = std::atoi(e);
     if (const char* e = std::getenv("SACX_MTILE")) h->mtile = std::atoi(e);
+    if (const char* e = std::getenv("SACX_MT32")) h->mt32 = std::atoi(e);
     if (const char* e = std::getenv("SACX_UNALIGNED")) h->unaligned_b = std::atoi(e);
     if (const char* e = std::getenv("SACX_FWD2")) h->fwd2 = std::atoi(e);
     if (const char* e = std::getenv("SACX_AFIN")) h->afin = std::atoi(e);

@@ -364,11 +364,13 @@ def test_model_fit_folds_bit_identical(gpu_available, monkeypatch, S, A, B, clip
     same squares in another order (<= 1e-6 relative)."""
     outs = []
     steps = 12
-    for fuse, tile, f2 in (("0", "2", "0"), ("1", "1", "0"), ("2", "1", "0"), ("2", "1", "1"), ("3", "1", "0"),
-                           ("3", "1", "1"), ("3", "0", "1")):
+    for fuse, tile, f2, mt32 in (("0", "2", "0", "1"), ("1", "1", "0", "1"), ("2", "1", "0", "1"), ("2", "1", "1", "1"),
+                                 ("2", "1", "1", "0"), ("2", "1", "0", "3"), ("3", "1", "0", "1"), ("3", "1", "1", "1"),
+                                 ("3", "0", "1", "1")):
         monkeypatch.setenv("SACX_MFUSE", fuse)
         monkeypatch.setenv("SACX_MTILE", tile)
         monkeypatch.setenv("SACX_MFWD2", f2)
+        monkeypatch.setenv("SACX_MT32", mt32)
         eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, B=B, act="tanh", N=3000, seed=33, use_expert=True,
                                                normalizers="random", model_max_grad_norm=clip)
         names = [L["name"] for L in eng.model_plan_info()]
