@@ -181,7 +181,7 @@ struct sacx_handle {
     int unaligned_b = 1;      // dX launches: float4 loads of W_ext rows at any 4-B offset (SACX_UNALIGNED)
     int fwd2 = 1;             // two-layer forward pairs as one k_fwd2 launch where they qualify (SACX_FWD2)
     int mtile = 1;            // model fit tiles: 0 16x16, 1 16x16 + wide dW on 32x32, 2 the handle's (SACX_MTILE)
-    int mt32 = 1;             // fit launches moved to 32x32 tiles under mtile 1 (SACX_MT32): 1 model.bwd1, 2 model.fwd1
+    int mt32 = 5;             // fit launches on 32x32 tiles under mtile 1 (SACX_MT32): 1 model.bwd1, 2 model.fwd1, 4 model.bwd2, 8 model.fwd2
     int dw_round_tiles = 1280;  // 16x16 dW tiles resident at once (SACX_DW_ROUND)
                               // (32x32 tiles accumulate as 16x16 ones: only the folds change sums)
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
@@ -1648,7 +1648,12 @@ void build_model_plan(sacx_handle* h) {
     }
     // the gathered layer 0 and layer 1 as ONE k_fwd2 launch (SACX_MFWD2, default; K0 = S + A <= 32)
     if (gfold && h->mfwd2) fuse_fwd2(h, plan, "model.gather+fwd01");
-    add_gemm(h, plan, "model.fwd2", f2, false);
+    {   // model.fwd2 (+ the MSE loss epilogue) on 32x32 tiles (mt32 bit 8; MSE heads only)
+        const int t32_fit = h->tile32;
+        if (h->mtile == 1 && (h->mt32 & 8) && !h->gm && !h->srn) h->tile32 = 2;
+        add_gemm(h, plan, "model.fwd2", f2, false);
+        h->tile32 = t32_fit;
+    }
     if (fuse) plan.back().name = "model.fwd2+loss";
     if (!fuse) {
         Launch L{};
@@ -1671,7 +1676,10 @@ void build_model_plan(sacx_handle* h) {
         for (int k = 0; k < nm; ++k) mf.logstd[k] = W("m" + std::to_string(k) + ".logstd");
     }
     if (!bfold) {
+        const int t32_fit = h->tile32;   // model.bwd2 (+ k_mfinal's workgroup) on 32x32 tiles (mt32 bit 4)
+        if (h->mtile == 1 && (h->mt32 & 4)) h->tile32 = 2;
         add_gemm(h, plan, "model.bwd2", b2, false);
+        h->tile32 = t32_fit;
         if (fuse) {
             Launch& B2 = plan.back();
             B2.name = "model.bwd2+final";

@@ -364,9 +364,10 @@ def test_model_fit_folds_bit_identical(gpu_available, monkeypatch, S, A, B, clip
     same squares in another order (<= 1e-6 relative)."""
     outs = []
     steps = 12
-    for fuse, tile, f2, mt32 in (("0", "2", "0", "1"), ("1", "1", "0", "1"), ("2", "1", "0", "1"), ("2", "1", "1", "1"),
-                                 ("2", "1", "1", "0"), ("2", "1", "0", "3"), ("3", "1", "0", "1"), ("3", "1", "1", "1"),
-                                 ("3", "0", "1", "1")):
+    for fuse, tile, f2, mt32 in (("0", "2", "0", "5"), ("1", "1", "0", "5"), ("2", "1", "0", "5"), ("2", "1", "1", "5"),
+                                 ("2", "1", "1", "0"), ("2", "1", "0", "3"), ("2", "1", "1", "15"), ("2", "1", "0", "15"),
+                                 ("3", "1", "0", "5"), ("3", "1", "1", "5"),
+                                 ("3", "0", "1", "5")):
         monkeypatch.setenv("SACX_MFUSE", fuse)
         monkeypatch.setenv("SACX_MTILE", tile)
         monkeypatch.setenv("SACX_MFWD2", f2)
