@@ -3838,9 +3838,7 @@ static int mtj_segments(const RngArgs& a) {
     // + MTJ_HEAD: the next batch's head words (k_mtj_head copies them)
     const double est = 624.0 + 1.02 * words + 8.0 * sqrt(words) + 64.0 * a.nupd + 1024.0 + MTJ_HEAD;
     int S = (int)ceil((est - 1.0) / a.jL);
-    const char* ue = std::getenv("SACX_MTJ_UNDER");
-    const int under = ue ? std::atoi(ue) : 0;
-    if (under > 0) S = std::max(1, std::min(S, under));   // tests: too few segments (the fallback)
+    if (a.junder > 0) S = std::max(1, std::min(S, a.junder));   // tests: too few segments (the fallback)
     const int64_t W = (int64_t)S * a.jL + 1;
     if (S > a.jsmax || (W + MTJ_CHK - 1) / MTJ_CHK > MTJ_MAXCHK) return 0;
     return S;

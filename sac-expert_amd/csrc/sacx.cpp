@@ -33,6 +33,7 @@
 #include <chrono>
 #include <cstring>
 #include <map>
+#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <vector>
@@ -170,6 +171,7 @@ struct sacx_handle {
     int jL = 0;               // its segment length (words)
     int jsmax = 0;            // segments its work area holds
     int mtj_ramp = 3;         // a graph's first mtj_ramp sampler batches take it (SACX_MTJ_RAMP), the rest k_rng
+    int mtj_under = 0;        // tests: cap its segment count (SACX_MTJ_UNDER: forces the redraw fallback)
     int tile32 = 0;           // plan GEMMs on 32x32 workgroup tiles: 1 all, 2 FWD / DX only (SACX_T32)
     int tile32_plan = 0;      // the tile32 a plan of plan_seeds seeds would take: the folds follow it
     int dwl = 0;              // dW + Adam launches on k_dwl: 0 never, 1 when K >= 512, 2 always (SACX_DWL)
@@ -969,6 +971,7 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
             L.rng.jc = h->ptr<uint32_t>("rng.jc");
             L.rng.jL = h->jL;
             L.rng.jsmax = h->jsmax;
+            L.rng.junder = h->mtj_under;
         }
         L.grid = 1;
         L.block = 1024;
@@ -1894,9 +1897,12 @@ bool merged_body(sacx_handle* h, int slot, int prev_slot, std::vector<Launch>& o
                     // k_fwd2 has no later forward launch to take it.  Split (SACX_AFIN, default): its
                     // first alpha block snapshots the finalisation's operands and the next launch's
                     // target rows finish the alpha step; else the last alpha block finalises (ticket)
-                    C.gemm.has_final = h->afin ? 2 : 1;
+                    // (qhead_block reads the snapshot unrelocated, and FinalArgs::pre shares its slot with
+                    // the data-parallel alpha_g: one seed, no data-parallel ranks)
+                    const bool split = h->afin && h->seeds == 1 && h->dp_ranks == 0 && !h->dp_local;
+                    C.gemm.has_final = split ? 2 : 1;
                     C.gemm.fin = pf->fin;
-                    if (h->afin) {
+                    if (split) {
                         C.gemm.fin.pre = h->ptr<AfinPre>("ws.afin");
                         afin_next = true;
                     } else {
@@ -2081,6 +2087,7 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             for (int b = 0; b < (int)batches.size(); ++b)
                 if (emit_after[b] == j) due.push_back(b);
             bool recorded = false;
+            bool afin_skipped = false;          // ablation: the split finalisation's snapshot was never taken
             for (const Launch& L : body) {
                 if ((int)L.kind == skip_kind) {
                     // ablation: the alpha.final folded into a skipped GEMM still runs
@@ -2088,7 +2095,15 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                         FinalArgs f = L.gemm.fin;
                         f.pre = nullptr;                 // (the split form's snapshot: finalise in place)
                         launch_alpha_final(f, cs);
+                        afin_skipped = afin_skipped || L.gemm.has_final == 2;
                     }
+                    continue;
+                }
+                if (afin_skipped && L.kind == Launch::GEMM && L.gemm.rowk == 1 && L.gemm.fin.pre != nullptr) {
+                    Launch C = L;                        // its q.head half: alpha is already final in place
+                    C.gemm.fin.pre = nullptr;
+                    afin_skipped = false;
+                    emit(C, cs);
                     continue;
                 }
                 emit(L, cs);
@@ -2528,8 +2543,14 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     }
     if (h->rng_jump) {   // rng.jc: the segmented sampler's jump coefficients
         const SegInfo& sj = h->seg("rng.jc");
-        std::vector<int32_t> jc((size_t)mt_jump_lists_words(h->jsmax - 1, MTJ_CH));
-        const int64_t used = mt_jump_lists(h->jL, h->jsmax - 1, MTJ_CH, jc.data());
+        std::vector<int32_t> jc;
+        int64_t used = 0;
+        try {   // (a C entry point: no exception may leave it -- bad_alloc, or the charpoly search failing)
+            jc.resize((size_t)mt_jump_lists_words(h->jsmax - 1, MTJ_CH));
+            used = mt_jump_lists(h->jL, h->jsmax - 1, MTJ_CH, jc.data());
+        } catch (const std::exception& e) {
+            return fail(h, std::string("segmented sampler jump coefficients: ") + e.what());
+        }
         for (int k = 0; k < h->seeds; ++k)
             HIPCHK(h, hipMemcpy(h->arena0 + (uint64_t)k * h->seed_bytes + sj.off, jc.data(), (size_t)used * sizeof(int32_t),
                                 hipMemcpyHostToDevice));
@@ -2562,6 +2583,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->nbatch = h->n_norm <= 16384 ? 8 : 4;
     if (const char* e = std::getenv("SACX_NBATCH")) h->nbatch = std::max(1, std::min(NBATCH_MAX, std::atoi(e)));
     if (const char* e = std::getenv("SACX_MTJ_RAMP")) h->mtj_ramp = std::atoi(e);
+    if (const char* e = std::getenv("SACX_MTJ_UNDER")) h->mtj_under = std::atoi(e);
     while (h->nslot % h->nbatch || h->nslot < 2 * h->nbatch) --h->nbatch;   // the ring holds whole batches
     if (h->dp_ranks > 0) {
         if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");

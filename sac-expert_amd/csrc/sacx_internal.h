@@ -474,6 +474,8 @@ struct RngArgs {
     int32_t jsmax;         // segments the work area holds
     int32_t jS;            // segments of this launch (launch_rng)
     int32_t jmin;          // launches expecting fewer words stay on k_rng
+    int32_t junder;        // > 0: at most this many segments (tests: forces the redraw fallback;
+                           // SACX_MTJ_UNDER, read once at sacx_bind)
 };
 
 // ---------------------------------------------------------------- segmented sampler layout

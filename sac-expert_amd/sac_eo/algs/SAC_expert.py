@@ -188,6 +188,10 @@ class SAC_exp(SACBase):
         if n_model == 0:
             return
         base = int(self.engine.ctl()["cur_size"]) - n_model
+        # model_ent: mean of model.entropy over the model data, taken BEFORE the epoch loop
+        # (SAC_expert.py:486-490, logged at :615) -- a constant per row (GaussianModel: 0.5 sum(2 logstd
+        # + log 2 pi + 1) of the pre-fit logstd, continuous_models.py:162-166; MSEModel 0)
+        ent = np.array([np.float32(m.entropy(self.s_expert[:1], None)[0]) for m in self.models], np.float32)
         batches = []
         num_updates = 0
         with self._host_rng():
@@ -227,9 +231,6 @@ class SAC_exp(SACBase):
         d = self._diag(disc=False)
         self.model_MSE_on_expert_data.append(d["mse_expert_data"])
         self.model_MSE_on_expert_counterfactual_action.append(d["mse_counterfactual"])
-        # model_ent: mean of model.entropy over the model data (SAC_expert.py:486-490) -- a constant
-        # per row (GaussianModel: 0.5 sum(2 logstd + log 2 pi + 1), continuous_models.py:162-166; MSEModel 0)
-        ent = np.array([np.float32(m.entropy(self.s_expert[:1], None)[0]) for m in self.models], np.float32)
         self.logger.log_train({"model_MSE_on_expert_data": d["mse_expert_data"],
                                "model_MSE_on_expert_counterfactual_action": d["mse_counterfactual"],
                                "model_ent": ent,

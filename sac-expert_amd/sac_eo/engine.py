@@ -675,14 +675,20 @@ class Engine:
         return st[[(seq - n_last + i) % cap for i in range(n_last)], 0]
 
     def reset_model_optimizer(self):
-        """--reset_model_optimizer (SAC_expert.py:553-555): fresh Adam state for the models."""
-        for k in range(int(self.cfg.num_models or 2)):
-            net = f"m{k}"
-            for i in range(3):
-                seg = self.segments[f"{net}.l{i}"]
-                o, n = seg["offset"] // 4, seg["rows"] * seg["cols"]
-                self.v["adam_m"][0, o:o + n] = 0
-                self.v["adam_v"][0, o:o + n] = 0
+        """--reset_model_optimizer (SAC_expert.py:553-555): a fresh Keras Adam for the models, so
+        no slot survives for ANY model trainable -- the model nets m<k>.l*, GaussianModel's
+        m<k>.logstd and the separate reward nets r<k>.l* (build_layout keeps them one contiguous
+        parameter range, the model optimiser's variable list)."""
+        lo, hi = None, None
+        for name, d in self.segments.items():
+            if d["role"] != N.ROLE_PARAM or not (name[:1] in ("m", "r") and name[1:2].isdigit()):
+                continue
+            o = d["offset"] // 4
+            lo = o if lo is None else min(lo, o)
+            hi = max(hi or 0, o + d["rows"] * d["cols"])
+        if lo is not None:
+            self.v["adam_m"][0, lo:hi] = 0
+            self.v["adam_v"][0, lo:hi] = 0
         self.v["ctl"][0, CTL["t_model"]] = 0
 
     def sync(self):

@@ -106,6 +106,40 @@ def test_model_fit_variant(gpu_available, variant, nm, max_norm, dclip):
     eng.close()
 
 
+def test_reset_model_optimizer_every_model_trainable(gpu_available):
+    """--reset_model_optimizer (SAC_expert.py:553-555) builds a fresh Keras Adam: no moment survives
+    for any model trainable -- the model nets, GaussianModel's logstd AND the separate reward nets.
+    Fit 2 steps, reset, fit 2 more: every variable against the oracle with a fresh AdamState."""
+    eng, ocfg, st, buf, nrm, _ = make_pair(act="relu", B=64, seed=35, use_expert=True, normalizers="random",
+                                           num_models=2, model_hidden=(96, 64), wm=VARIANTS["gauss_reward_scale"])
+    N = buf["r"].shape[0]
+    mb = eng.cfg.model_batch
+    idx = np.random.RandomState(17).randint(N, size=(4, 2, mb))
+    dev = []
+    for half in (0, 1):
+        eng.model_fit(idx[2 * half: 2 * half + 2], eager=True)
+        if half == 0:
+            eng.reset_model_optimizer()
+    eng.sync()
+    dev = eng.model_stats(4)
+    ref = []
+    for j in range(4):
+        if j == 2:
+            st.opt_model = O.AdamState.zeros_like(st.model_all_vars())
+        batches = [(buf["s"][idx[j, k]], buf["a"][idx[j, k]], buf["sp"][idx[j, k]], buf["r"][idx[j, k]])
+                   for k in range(2)]
+        ref.append(O.model_fit_step(st, ocfg, nrm, batches))
+    ref = np.array(ref)
+    assert np.max(np.abs(dev - ref) / np.abs(ref)) < 1e-4, (dev, ref)
+    for k in range(2):
+        for a_, b_ in zip(eng.get_net(f"m{k}"), st.models[k]):
+            assert np.max(np.abs(a_ - b_)) < 5e-5
+        assert np.max(np.abs(eng.get_model_logstd(k) - st.model_logstd[k])) < 5e-5
+        for a_, b_ in zip(eng.get_net(f"r{k}"), st.reward_nets[k]):
+            assert np.max(np.abs(a_ - b_)) < 5e-5
+    eng.close()
+
+
 @pytest.mark.parametrize("variant", ["gauss", "gauss_reward_scale", "reward_nn"])
 def test_model_forward_sample_loss(gpu_available, variant):
     """_forward / sample(deterministic and not) / get_loss on the device vs the oracle; the
