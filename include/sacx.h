@@ -36,7 +36,9 @@
 extern "C" {
 #endif
 
-#define SACX_ABI_VERSION 7
+#define SACX_ABI_VERSION 8
+#define SACX_MAX_DEPTH 4    /* hidden layers per net (create_nn's layers list, nn_utils.py:100-138) */
+#define SACX_MAX_MODELS 8   /* --num_models */
 
 typedef struct sacx_handle sacx_handle;
 
@@ -93,7 +95,9 @@ typedef struct sacx_config {
     int32_t actor_output_norm;  /* --actor_output_norm (GaussianActor mean normalisation) */
     int32_t actor_layer_norm;   /* --actor_layer_norm: Dense -> LayerNormalization -> tanh on layer 0
                                    (nn_utils.py:110-119) */
-    int32_t num_models;         /* --num_models for SAC-EO: 1 or 2 world models (0 -> 2) */
+    int32_t num_models;         /* --num_models for SAC-EO: 1 .. SACX_MAX_MODELS world models (0 -> 2); all are
+                                   fitted in one model-Adam step, the expert term uses the first two sections of
+                                   array_split(perm, num_models) (SAC_expert.py:297-336) */
     float model_max_grad_norm;  /* --model_max_grad_norm: clip_by_global_norm(grads, max_norm * num_models)
                                    of the model fit (mbrl_onpolicy_alg.py:315-317); <= 0: None */
     float delta_clip_loss;      /* --delta_clip_loss of MSEModel.get_loss in the model fit; <= 0: None */
@@ -125,6 +129,15 @@ typedef struct sacx_config {
     int32_t reward_hidden[2];   /* --reward_layers (2 hidden layers; 0 -> 512) */
     int32_t reward_act_layers[2]; /* --reward_activations per hidden layer (sacx_activation) */
     int32_t critic_hidden[2];   /* --critic_layers when they differ from --actor_layers (0: = hidden) */
+    /* --- ABI 8 --- */
+    int32_t net_depth[4];       /* hidden layers of [actor | critics | world models | reward nets]: 0 -> the two of
+                                   hidden / critic_hidden / model_hidden / reward_hidden (and their activations);
+                                   1..SACX_MAX_DEPTH -> net_hidden / net_acts below give every layer (the
+                                   --actor_layers / --critic_layers / --model_layers / --reward_layers lists,
+                                   train_parser.py:56-57, :107-108, of any length).  Any net not of 2 layers runs
+                                   the generic launch plan (unfused, every layer its own GEMM problem) */
+    int32_t net_hidden[4][SACX_MAX_DEPTH];   /* widths, [1, 512] */
+    int32_t net_acts[4][SACX_MAX_DEPTH];     /* per-layer sacx_activation */
 } sacx_config;
 
 typedef struct sacx_segment {
@@ -289,16 +302,18 @@ int sacx_rollout(sacx_handle* h, int32_t model, const float* s_init, int64_t n, 
                  float* r_out, float* sp_out, uint8_t* d_out);
 /* Expert diagnostics on the device, n <= 2048 expert rows (device).
  * flags = 0: model_MSE_on_expert_data and _counterfactual_action (SAC_expert.py:579-608):
- *   out[0] = mean over the 2 models of mean_i 0.5||model.sample(s_e, a_e) - sp_e||^2,
+ *   out[0] = mean over the nm models of mean_i 0.5||model.sample(s_e, a_e) - sp_e||^2,
  *   out[1] = the same with a = actor.sample(s_e, deterministic=False) (draws n*A normals
- *   from the device stream), out[2..3] / out[4..5] = per model.
+ *   from the device stream), out[2 .. 2+nm) / out[2+nm .. 2+2nm) = per model (nm = 1: model 0
+ *   twice).  n * max(nm, 2) <= 4096.
  * flags & SACX_DIAG_DISC: _calc_disc (:427-460): s_disc_i = ||sp_pred0 - sp_pred1||_2 on
  *   (s_e, counterfactual a); out[0] = sum, out[1] = max, out[2] = median, out[3 + i] = ratio.
  *   The models sample with deterministic=False: GaussianModels draw normal(size=(n, S)) each,
- *   model 0 then model 1, after the counterfactual action's draw (:437, :446).
+ *   every model in order (only models 0 and 1 enter the distance), after the counterfactual
+ *   action's draw (:437, :446).
  * flags & SACX_DIAG_EXPERT_ACTIONS (use_expert_actions): a_e replaces the counterfactual
- *   action (no draw; out[1] = out[0]).  delta_clip > 0: --delta_clip_pred.  out: device, >= 6
- *   floats (3 + n with DISC).  The adaptive epsilon of :383-418 is scalar host arithmetic. */
+ *   action (no draw; out[1] = out[0]).  delta_clip > 0: --delta_clip_pred.  out: device, >= 2 + 2
+ *   max(nm, 2) floats (3 + n with DISC).  The adaptive epsilon of :383-418 is scalar host arithmetic. */
 enum { SACX_DIAG_DISC = 1, SACX_DIAG_EXPERT_ACTIONS = 2 };
 int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const float* sp_e, int32_t n,
                      int32_t flags, float delta_clip, float* out);

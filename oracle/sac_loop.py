@@ -279,7 +279,7 @@ class LoopOracle:
             else:
                 perm = np.arange(len(s_e))
                 self.gen.shuffle(perm)                                       # :301-303
-                sec = np.array_split(perm, 2)
+                sec = np.array_split(perm, int(self.k.get("num_models", 2)))    # sections 0 and 1 (:303-309)
                 n1 = O.f32_noise(rs.normal(size=(len(sec[0]), A)))
                 n2 = O.f32_noise(rs.normal(size=(len(sec[1]), A)))
                 ex = O.Expert(s_e[sec[0]], sp_e[sec[0]], s_e[sec[1]], sp_e[sec[1]], n1, n2, self.eps)

@@ -94,13 +94,16 @@ class Config:
     reward_hidden: Sequence[int] = (512, 512)
     reward_act: str = "relu"
 
+    # SAC-EO world models (--num_models): all are fitted, the expert term uses models 0 and 1
+    num_models: int = 2
+
     @property
     def aacts(self):
-        return tuple(self.actor_acts) if self.actor_acts else (self.act, self.act)
+        return tuple(self.actor_acts) if self.actor_acts else (self.act,) * len(self.hidden)
 
     @property
     def cacts(self):
-        return tuple(self.critic_acts) if self.critic_acts else (self.act, self.act)
+        return tuple(self.critic_acts) if self.critic_acts else (self.act,) * len(self.chidden)
 
     @property
     def chidden(self):
@@ -252,14 +255,15 @@ def init_state(cfg: Config, seed: int = 1, with_models: bool = False,
     if with_models:
         om = cfg.S if cfg.separate_reward_nn else cfg.S + 1
         st.models = [init_mlp(rng, cfg.S + cfg.A, om, cfg.model_hidden, model_gain, bias_scale)
-                     for _ in range(2)]
+                     for _ in range(max(2, cfg.num_models))]
         if cfg.gaussian_model:           # np.ones((1, s_dim)) * np.log(std_mult) (continuous_models.py:24)
             # (perturbed from the uniform init so that the tests see a per-column logstd)
             st.model_logstd = [(np.ones((1, cfg.S)) * np.log(model_std_mult)
-                                + 0.05 * rng.normal(size=(1, cfg.S))).astype(np.float32) for _ in range(2)]
+                                + 0.05 * rng.normal(size=(1, cfg.S))).astype(np.float32)
+                               for _ in range(max(2, cfg.num_models))]
         if cfg.separate_reward_nn:
             st.reward_nets = [init_mlp(rng, cfg.S + cfg.A, 1, cfg.reward_hidden, reward_gain, bias_scale)
-                              for _ in range(2)]
+                              for _ in range(max(2, cfg.num_models))]
         st.opt_model = AdamState.zeros_like(st.model_all_vars())
     return st
 
@@ -382,8 +386,8 @@ def actor_backward(params, x, hs, dout, cfg):
     """Gradients of the actor weight list (same order as params)."""
     if not cfg.layer_norm:
         return mlp_backward(params, x, hs, dout, cfg.aacts)[0]
-    h1, h2, xh, rstd = hs
-    g_rest, dh1 = mlp_backward(params[4:], h1, [h2], dout, cfg.aacts[1:], need_dx=True)
+    h1, rest, xh, rstd = hs[0], hs[1:-2], hs[-2], hs[-1]
+    g_rest, dh1 = mlp_backward(params[4:], h1, rest, dout, cfg.aacts[1:], need_dx=True)
     one = np.ones((), h1.dtype)
     dy = dh1 * (one - h1 * h1)
     gg = dy * params[2]
@@ -870,6 +874,8 @@ def calc_disc(st, cfg, nrm, s_e, a_e, rs=None, use_expert_actions=False, delta_c
     a = np.asarray(a_e, dt) if use_expert_actions else _actor_sample(st, cfg, nrm, s_e, rs)
     p0 = _model_sample(st, cfg, mnrm, 0, s_e, a, delta_clip, rs=rs)
     diff = p0 - _model_sample(st, cfg, mnrm, 1, s_e, a, delta_clip, rs=rs)
+    for k in range(2, len(st.models)):          # every model samples (and draws); sp_pred[0] - sp_pred[1]
+        _model_sample(st, cfg, mnrm, k, s_e, a, delta_clip, rs=rs)
     s_disc = np.sqrt((diff * diff).sum(axis=1))
     tot = np.sum(s_disc)
     return s_disc / tot, float(np.max(s_disc)), float(np.median(s_disc)), float(tot)
@@ -984,7 +990,7 @@ def draw_step_randoms(rs, cur_size: int, B: int, A: int, n_expert: int = 0, gen=
     elif n_expert:
         perm = np.arange(n_expert)
         gen.shuffle(perm)                                       # SAC_expert.py:301-303
-        sec = np.array_split(perm, 2)
+        sec = np.array_split(perm, n_models)                    # the expert term takes sections 0 and 1
         out["perm"] = perm
         out["sections"] = sec
         out["noise_e1"] = rs.normal(size=(len(sec[0]), A))      # sample(s_expert_one)

@@ -670,29 +670,21 @@ __device__ __forceinline__ float mfit_block_sum(float v, float* sh, int nw) {
 }
 
 __device__ void mfit_final(const MFinalArgs& f, const AdamConsts* adam = nullptr, int64_t p_stride = 0) {
-    __shared__ float mred[2][4];
+    __shared__ float mred[MAX_MODELS][4];
     __shared__ float lred[4];
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6, nw = blockDim.x >> 6;
     const int64_t t_model = f.ctl->t_model;      // read by every thread before thread 0 advances it
     const int n = f.nt > 0 ? f.mb * f.nt : f.mb;
-    float s0 = 0.f, s1 = 0.f;
-    for (int i = t; i < n; i += blockDim.x) {
-        s0 += f.loss_rows[i];
-        if (f.nm > 1) s1 += f.loss_rows[n + i];
-    }
-    if (f.nt2 > 0) {                             // the separate reward heads' partials
-        const int n2 = f.mb * f.nt2;
-        const float* r2 = f.loss_rows + (size_t)f.nm * n;
-        for (int i = t; i < n2; i += blockDim.x) {
-            s0 += r2[i];
-            if (f.nm > 1) s1 += r2[n2 + i];
+    for (int k = 0; k < f.nm; ++k) {             // model k's loss partials, then its reward head's
+        float sk = 0.f;
+        for (int i = t; i < n; i += blockDim.x) sk += f.loss_rows[(size_t)k * n + i];
+        if (f.nt2 > 0) {                         // the separate reward heads' partials
+            const int n2 = f.mb * f.nt2;
+            const float* r2 = f.loss_rows + (size_t)f.nm * n;
+            for (int i = t; i < n2; i += blockDim.x) sk += r2[(size_t)k * n2 + i];
         }
-    }
-    s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    if (lane == 0) {
-        mred[0][wave] = s0;
-        mred[1][wave] = s1;
+        sk = wave_sum(sk);
+        if (lane == 0) mred[k][wave] = sk;
     }
     __syncthreads();
     if (f.lgpart != nullptr && adam != nullptr) {
@@ -702,7 +694,7 @@ __device__ void mfit_final(const MFinalArgs& f, const AdamConsts* adam = nullptr
         const int S = f.S;
         const float lr_t = adam_lr(*adam, GRP_MODEL, t_model + 1);
         for (int k = 0; k < f.nm; ++k) {
-            float* L = f.logstd[k];
+            float* L = f.logstd + (size_t)k * f.lstride;
             float ds = 1.f;
             if (f.lscale) {                      // tf.stop_gradient(reduce_mean(square(exp(logstd))))
                 float q = 0.f;
@@ -724,18 +716,16 @@ __device__ void mfit_final(const MFinalArgs& f, const AdamConsts* adam = nullptr
         }
     }
     if (t == 0) {
-        float a0 = mred[0][0], a1 = mred[1][0];
-        for (int w = 1; w < nw; ++w) {
-            a0 += mred[0][w];
-            a1 += mred[1][w];
+        float tot = 0.f;
+        for (int k = 0; k < f.nm; ++k) {
+            float ak = mred[k][0];
+            for (int w = 1; w < nw; ++w) ak += mred[k][w];
+            if (f.nt > 0) ak = 0.5f * ak;        // partials of e^2: get_loss's 0.5 factor
+            const float lk = ak / (float)f.mb;
+            tot = k == 0 ? lk : tot + lk;        // loss_all (:305-312), in model order
         }
-        if (f.nt > 0) {        // partials of e^2: get_loss's 0.5 factor
-            a0 = 0.5f * a0;
-            a1 = 0.5f * a1;
-        }
-        const float l0 = a0 / (float)f.mb, l1 = a1 / (float)f.mb;
         const int64_t seq = f.ctl->mfit_seq;
-        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = f.nm > 1 ? l0 + l1 : l0;     // loss_all (:305-312)
+        f.mstats[(size_t)(seq % f.mstats_cap) * 2] = tot;
         f.mstats[(size_t)(seq % f.mstats_cap) * 2 + 1] = (float)seq;
         f.ctl->t_model = t_model + 1;
         f.ctl->mfit_seq = seq + 1;
@@ -3918,10 +3908,11 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
         }
     } else if (row < g.B + g.ne) {
         const int e = row - g.B;
-        // 2 models: the update's self.rng.shuffle permutation (SAC_expert.py:301-303); one model
-        // takes the expert rows in order (:290-295, no perm ring)
+        // 2+ models: the update's self.rng.shuffle permutation (SAC_expert.py:301-303), whose first ne
+        // entries are array_split's first two sections; one model takes the expert rows in order
+        // (:290-295, no perm ring)
         const int64_t slot = g.ctl->pseq[g.slot] % g.perm_cap;
-        const int src = g.perm_ring != nullptr ? g.perm_ring[slot * g.ne + e] : e;
+        const int src = g.perm_ring != nullptr ? g.perm_ring[slot * g.perm_ld + e] : e;
         const __amdgpu_buffer_rsrc_t rse = rs(g.exp_s + (size_t)src * S), rspe = rs(g.exp_sp + (size_t)src * S);
         // the actor row takes the actor's normaliser, the world-model row the models' (the same
         // values unless --only_model_normalizer, SAC_expert.py:139-144)
@@ -4951,9 +4942,11 @@ __global__ __launch_bounds__(DIAG_THREADS) void k_diag(DiagArgs g) {
     __shared__ float red[DIAG_THREADS / 64];
     const int n = g.n, S = g.S;
     if (g.mode == 1 || g.mode == 2) {
-        // per model: mean_i 0.5 sum_j (sp_pred - sp_e)^2; then the mean of the two
-        float m[2];
-        for (int k = 0; k < 2; ++k) {
+        // per model: mean_i 0.5 sum_j (sp_pred - sp_e)^2; then np.mean over the models' f32 values
+        // (sequential below 8 values, numpy's 8-way pairwise block at 8)
+        const int nmod = g.nmod;
+        float m[MAX_MODELS];
+        for (int k = 0; k < nmod; ++k) {
             float acc = 0.f;
             for (int i = threadIdx.x; i < n; i += DIAG_THREADS) {
                 float se = 0.f;
@@ -4963,13 +4956,20 @@ __global__ __launch_bounds__(DIAG_THREADS) void k_diag(DiagArgs g) {
                 }
                 acc += 0.5f * se;
             }
-            m[k] = block_sum_1024(acc, red) / (float)n;
+            const float mk = block_sum_1024(acc, red) / (float)n;
+            if (threadIdx.x == 0) m[k] = mk;
         }
         if (threadIdx.x == 0) {
+            float sum;
+            if (nmod >= 8) {
+                sum = ((m[0] + m[1]) + (m[2] + m[3])) + ((m[4] + m[5]) + (m[6] + m[7]));
+            } else {
+                sum = m[0];
+                for (int k = 1; k < nmod; ++k) sum += m[k];
+            }
             const int o = g.mode == 1 ? 0 : 1;
-            g.out[o] = (m[0] + m[1]) * 0.5f;
-            g.out[2 + 2 * (g.mode - 1)] = m[0];
-            g.out[3 + 2 * (g.mode - 1)] = m[1];
+            g.out[o] = sum / (float)nmod;
+            for (int k = 0; k < nmod; ++k) g.out[2 + nmod * (g.mode - 1) + k] = m[k];
         }
         return;
     }

@@ -114,6 +114,12 @@ const char* kernel_family(Launch::Kind k) {
 
 }  // namespace
 
+// One net's hidden layers: create_nn's layers list and its activations (nn_utils.py:100-138)
+struct NetDims {
+    std::vector<int> h, act;
+    int D() const { return (int)h.size(); }
+};
+
 struct sacx_handle {
     sacx_config cfg{};
     std::string err;
@@ -126,7 +132,13 @@ struct sacx_handle {
     int aact[2] = {0, 0}, cact[2] = {0, 0}, macts[2] = {0, 0};
     int64_t cap = 0;
     int graph_steps = 128, stats_cap = 4096, perm_cap = 4096, mb = 0, mfit_cap = 1024;
-    int nm = 0;               // SAC-EO world models (--num_models: 1 or 2)
+    int nm = 0;               // SAC-EO world models (--num_models: 1 .. SACX_MAX_MODELS)
+    int ne_perm = 0;          // expert rows per update permutation (expert_batch); ne = the rows the update
+                              // uses: all of them (1 or 2 models), else the first two array_split sections
+    // hidden layers of [actor, critics, world models, reward nets]; H0 / H1 (Hc*, Hm*, Hr*) and the act
+    // pairs above are the first and the last hidden layer of each
+    NetDims nd[4];
+    bool deep = false;        // a net of other than 2 hidden layers: the generic plans (build_plan_generic)
     // world-model variants (ABI 7): GaussianModel (a logstd per model, the NLL fit loss, noise in
     // sample / step) and --separate_reward_nn (a reward net r<k> beside each model net m<k>)
     bool gm = false, srn = false, lscale = false;
@@ -269,6 +281,9 @@ std::string mnorm(const sacx_handle* h, const char* x) {
     return std::string(h->cfg.use_expert ? "mnorm." : "norm.") + x;
 }
 
+// the actor's output head (the Dense layer after its last hidden one)
+std::string actor_head_name(const sacx_handle* h) { return "actor.l" + std::to_string(h->nd[0].D()); }
+
 int fail(sacx_handle* h, const std::string& msg) {
     if (h) h->err = msg;
     return -1;
@@ -310,28 +325,32 @@ void build_layout(sacx_handle* h) {
     const int F = SACX_F32;
     // ---------------- parameters (Keras W_ext = [W ; b] per Dense layer)
     h->arena_bytes = 0;
-    auto net = [&](const std::string& n, int in, int out, int role, int h0, int h1) {
-        h->add(n + ".l0", in + 1, h0, F, role);
-        h->add(n + ".l1", h0 + 1, h1, F, role);
-        h->add(n + ".l2", h1 + 1, out, F, role);
+    // Keras Dense layers l0 .. l<D> (the last one the output head) of a net with hidden widths w
+    auto net = [&](const std::string& n, int in, int out, int role, const std::vector<int>& w) {
+        int k = in;
+        for (size_t l = 0; l < w.size(); ++l) {
+            h->add(n + ".l" + std::to_string(l), k + 1, w[l], F, role);
+            k = w[l];
+        }
+        h->add(n + ".l" + std::to_string(w.size()), k + 1, out, F, role);
     };
-    net("actor", S, h->Aout, SACX_ROLE_PARAM, H0, H1);
+    net("actor", S, h->Aout, SACX_ROLE_PARAM, h->nd[0].h);
     if (h->ln) h->add("actor.ln", 2, H0, F, SACX_ROLE_PARAM);     // LayerNormalization gamma ; beta
     h->add("actor.logstd", 1, A, F, SACX_ROLE_PARAM);
     const int Hc0 = h->Hc0, Hc1 = h->Hc1;      // the critics' (--critic_layers)
-    net("q0", S + A, 1, SACX_ROLE_PARAM, Hc0, Hc1);
-    net("q1", S + A, 1, SACX_ROLE_PARAM, Hc0, Hc1);
-    net("t0", S + A, 1, SACX_ROLE_TARGET, Hc0, Hc1);
-    net("t1", S + A, 1, SACX_ROLE_TARGET, Hc0, Hc1);
+    net("q0", S + A, 1, SACX_ROLE_PARAM, h->nd[1].h);
+    net("q1", S + A, 1, SACX_ROLE_PARAM, h->nd[1].h);
+    net("t0", S + A, 1, SACX_ROLE_TARGET, h->nd[1].h);
+    net("t1", S + A, 1, SACX_ROLE_TARGET, h->nd[1].h);
     h->add("alpha", 1, 1, F, SACX_ROLE_PARAM);
     if (h->cfg.use_expert) {
         // per model, in model.trainable order (continuous_models.py:27-32, :216-221): the model net,
         // GaussianModel's logstd, the separate reward net -- one contiguous range (the global-norm clip)
         for (int k = 0; k < h->nm; ++k) {
             const std::string m = "m" + std::to_string(k);
-            net(m, S + A, h->Om, SACX_ROLE_PARAM, h->Hm0, h->Hm1);
+            net(m, S + A, h->Om, SACX_ROLE_PARAM, h->nd[2].h);
             if (h->gm) h->add(m + ".logstd", 1, S, F, SACX_ROLE_PARAM);
-            if (h->srn) net("r" + std::to_string(k), S + A, 1, SACX_ROLE_PARAM, h->Hr0, h->Hr1);
+            if (h->srn) net("r" + std::to_string(k), S + A, 1, SACX_ROLE_PARAM, h->nd[3].h);
         }
     }
     const uint64_t pbytes = (h->arena_bytes + 255) & ~uint64_t(255);
@@ -354,7 +373,7 @@ void build_layout(sacx_handle* h) {
     // bf16 shadows of the SAC nets' hidden-layer weights (config C5, 32x32 forward tiles): the
     // forward launches read B from them (wbf_pos layout), the Adam epilogues keep them current
     h->wbf_mats.clear();
-    if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 2)) {
+    if (h->cfg.gemm_bf16 && !h->deep && (h->wbf_enabled == 1 || h->wbf_enabled == 2)) {
         const char* nets[] = {"actor", "q0", "q1", "t0", "t1"};
         for (const char* n : nets) {
             const bool act = std::string(n) == "actor";
@@ -453,7 +472,7 @@ void build_layout(sacx_handle* h) {
     const int ecap = std::max(1, h->ecap);
     h->add("expert.s", ecap, S, F, SACX_ROLE_STATE);
     h->add("expert.sp", ecap, S, F, SACX_ROLE_STATE);
-    h->add("perm", h->perm_cap, ne1, SACX_I32, SACX_ROLE_STATE);
+    h->add("perm", h->perm_cap, std::max(1, h->ne_perm), SACX_I32, SACX_ROLE_STATE);
     h->add("stats", h->stats_cap, 8, F, SACX_ROLE_STATE);
     h->add("red", 1, std::max(1024, (B + 3) / 4), F, SACX_ROLE_WORK);
     h->add("ws.afin", 1, sizeof(AfinPre) / 4, F, SACX_ROLE_WORK);   // the split alpha finalisation's snapshot
@@ -462,8 +481,21 @@ void build_layout(sacx_handle* h) {
     // actor activations; rows [Ra4, Ra4 + B) hold the alpha evaluate() of an update
     // (aliased ws.Hl1 / ws.Hl2) so one grouped head launch can serve both
     const int Ra4 = (Ra + 3) & ~3;
+    // a chain's per-layer buffers: <p>1 = hidden layer 0, <p>2 = the last hidden layer -- one segment
+    // each at two layers (the fused plans' layout), with one layer <p>2 aliases <p>1; the middle layers
+    // <p>m<i> of deeper nets (the generic plans) are added at the end of the workspace (mids)
+    auto last = [&](const std::string& n2, const std::string& n1, int64_t rows, int w2, int D) -> uint64_t {
+        if (D >= 2) return h->add(n2, rows, w2, F, 0);
+        const SegInfo& s1 = h->seg(n1);
+        h->alias(n2, s1.off, s1.rows, s1.cols, F, 0);
+        return s1.off;
+    };
+    struct Mid { std::string p; int64_t rows; int net; };
+    std::vector<Mid> mids;
+    const int Da = h->nd[0].D(), Dc = h->nd[1].D(), Dm = h->nd[2].D(), Dr = h->nd[3].D();
     const uint64_t oHa1 = h->add("ws.Ha1", Ra4 + B, H0, F, 0);
-    const uint64_t oHa2 = h->add("ws.Ha2", Ra4 + B, H1, F, 0);
+    const uint64_t oHa2 = last("ws.Ha2", "ws.Ha1", Ra4 + B, H1, Da);
+    mids.push_back({"ws.Ham", Ra4 + B, 0});
     // Ha2 . W3 per 16-column tile of actor.fwd1 (rows as ws.Ha2), summed by the head rows
     h->add("ws.hpart", Ra4 + B, (int64_t)h->Aout * ((H1 + 15) / 16), F, 0);
     h->add("ws.c_t", Rb, A, F, 0);
@@ -474,28 +506,43 @@ void build_layout(sacx_handle* h) {
     h->add("ws.nlp_p", 1, B, F, 0);
     h->add("ws.nlp3", 1, B, F, 0);
     h->add("ws.Hq1", 4 * B, Hc0, F, 0);
-    h->add("ws.Hq2", 4 * B, Hc1, F, 0);
-    h->add("ws.Dq2", 2 * B, Hc1, F, 0);
+    last("ws.Hq2", "ws.Hq1", 4 * B, Hc1, Dc);
+    if (Dc >= 2) h->add("ws.Dq2", 2 * B, Hc1, F, 0);
     h->add("ws.Dq1", 2 * B, Hc0, F, 0);
+    if (Dc < 2) last("ws.Dq2", "ws.Dq1", 2 * B, Hc1, Dc);
+    mids.push_back({"ws.Hqm", 4 * B, 1});
+    mids.push_back({"ws.Dqm", 2 * B, 1});
     h->add("ws.gq", 2, B, F, 0);
     h->add("ws.lq", 2, B, F, 0);
     h->add("ws.Hp1", 2 * B, Hc0, F, 0);
-    h->add("ws.Hp2", 2 * B, Hc1, F, 0);
+    last("ws.Hp2", "ws.Hp1", 2 * B, Hc1, Dc);
     h->add("ws.Dp1", 2 * B, Hc0, F, 0);
+    if (h->deep) {                    // the generic plan's policy-row deltas (the fused one keeps partials)
+        last("ws.Dp2", "ws.Dp1", 2 * B, Hc1, Dc);
+        mids.push_back({"ws.Hpm", 2 * B, 1});
+        mids.push_back({"ws.Dpm", 2 * B, 1});
+    }
     h->add("ws.lp", 1, B, F, 0);
     h->add("ws.gp", 2, B, F, 0);                 // policy-row output gradients of q0, q1
     h->add("ws.apart", 2 * B, ((Hc0 + 15) / 16) * A, F, 0);  // their action-gradient partials (folded head bwd)
     h->add("ws.mpart", ne1, ((Hm0 + 15) / 16) * A, F, 0);       // the expert rows' ones (SAC-EO, model.bwd1)
     h->add("ws.ones", 1, std::max(std::max(Rb, B), std::max(1, h->mb)) + 4, F, SACX_ROLE_STATE);
     h->add("ws.Hm1", ne1, Hm0, F, 0);
-    h->add("ws.Hm2", ne1, Hm1, F, 0);
-    h->add("ws.Dm2", ne1, Hm1, F, 0);
+    last("ws.Hm2", "ws.Hm1", ne1, Hm1, Dm);
+    if (Dm >= 2) h->add("ws.Dm2", ne1, Hm1, F, 0);
     h->add("ws.Dm1", ne1, Hm0, F, 0);
+    if (Dm < 2) last("ws.Dm2", "ws.Dm1", ne1, Hm1, Dm);
+    if (h->cfg.use_expert) {
+        mids.push_back({"ws.Hmm", ne1, 2});
+        mids.push_back({"ws.Dmm", ne1, 2});
+    }
     h->add("ws.mse", ne1, (S + 15) / 16, F, 0);       // per-column-tile partials of the expert MSE
     h->add("ws.dout", ne1, S, F, 0);                  // d loss / d model output (expert rows)
     h->add("ws.Da3", Rb, h->Aout, F, 0);
-    h->add("ws.Da2", Rb, H1, F, 0);
+    if (Da >= 2) h->add("ws.Da2", Rb, H1, F, 0);
     h->add("ws.Da1", Rb, H0, F, 0);
+    if (Da < 2) last("ws.Da2", "ws.Da1", Rb, H1, Da);
+    mids.push_back({"ws.Dam", Rb, 0});
     h->add("ws.E", Rb, A, F, 0);
     h->alias("ws.Hl1", oHa1 + (uint64_t)Ra4 * H0 * 4, B, H0, F, 0);
     h->alias("ws.Hl2", oHa2 + (uint64_t)Ra4 * H1 * 4, B, H1, F, 0);
@@ -503,7 +550,7 @@ void build_layout(sacx_handle* h) {
     // (H0 a multiple of 128: every shadow position holds a k < H0; not under the layer norm,
     // which rewrites the actor's layer-0 output after the GEMM)
     h->abf_segs.clear();
-    if (h->cfg.gemm_bf16 && (h->wbf_enabled == 1 || h->wbf_enabled == 3))
+    if (h->cfg.gemm_bf16 && !h->deep && (h->wbf_enabled == 1 || h->wbf_enabled == 3))
         for (const char* n : {"ws.Ha1", "ws.Hq1", "ws.Hp1"}) {
             const bool act = std::string(n) == "ws.Ha1";
             const int w = act ? H0 : Hc0;
@@ -514,8 +561,10 @@ void build_layout(sacx_handle* h) {
         }
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
-    h->add("act.H1", ACT_CAP, std::max(H0, Hc0), F, 0);   // (sacx_critic_forward's too)
-    h->add("act.H2", ACT_CAP, std::max(H1, Hc1), F, 0);
+    // (sacx_critic_forward's too; the generic plans' nets alternate between the two: any layer's width)
+    auto wmax = [&](int n) { return *std::max_element(h->nd[n].h.begin(), h->nd[n].h.end()); };
+    h->add("act.H1", ACT_CAP, h->deep ? std::max(wmax(0), wmax(1)) : std::max(H0, Hc0), F, 0);
+    h->add("act.H2", ACT_CAP, h->deep ? std::max(wmax(0), wmax(1)) : std::max(H1, Hc1), F, 0);
     h->add("act.noise", 1, (int64_t)ACT_CAP * A, F, 0);
     if (h->ln) {                      // layer-norm caches of the update's actor rows
         h->add("ws.ln_xhat", h->Ra, H0, F, 0);
@@ -527,44 +576,56 @@ void build_layout(sacx_handle* h) {
     h->add("act.Q", ACT_CAP, 1, F, 0);                // sacx_critic_forward output
     if (h->cfg.use_expert) {          // world-model fitting (A16)
         const int R2 = h->nm * h->mb, O = S + 1;
+        // the models' output rows: a rollout chunk, or every model on the diagnostics' <= 2048 rows
+        const int64_t RR = std::max<int64_t>(ROLL_CAP, (int64_t)h->nm * 2048);
         h->add("mfit.idx", h->mfit_cap, R2, SACX_I32, SACX_ROLE_WORK);
         h->add("ws.gnorm", 1, GNORM_PARTS + 1, F, 0);   // clip_by_global_norm partials + scale
         h->add("mstats", h->stats_cap, 2, F, SACX_ROLE_STATE);
         h->add("ws.Xf", R2, h->ldQ, F, 0);
         h->add("ws.Tf", R2, O, F, 0);
         h->add("ws.Hf1", R2, Hm0, F, 0);
-        h->add("ws.Hf2", R2, Hm1, F, 0);
+        last("ws.Hf2", "ws.Hf1", R2, Hm1, Dm);
         h->add("ws.Of", R2, O, F, 0);
         h->add("ws.Df3", R2, r4(O), F, 0);    // float4 rows: model.bwd2's A operand
-        h->add("ws.Df2", R2, Hm1, F, 0);
+        if (Dm >= 2) h->add("ws.Df2", R2, Hm1, F, 0);
         h->add("ws.Df1", R2, Hm0, F, 0);
+        if (Dm < 2) last("ws.Df2", "ws.Df1", R2, Hm1, Dm);
+        mids.push_back({"ws.Hfm", R2, 2});
+        mids.push_back({"ws.Dfm", R2, 2});
         // fit-loss partials (per row: k_mloss); --separate_reward_nn: then one per row of the reward heads
         h->add("ws.lf", 1, (int64_t)R2 * ((O + 15) / 16) + (h->srn ? R2 : 0), F, 0);
         if (h->srn) {                 // the reward nets' fit activations / deltas
             const int Hr0 = h->Hr0, Hr1 = h->Hr1;
             h->add("ws.Hrf1", R2, Hr0, F, 0);
-            h->add("ws.Hrf2", R2, Hr1, F, 0);
+            last("ws.Hrf2", "ws.Hrf1", R2, Hr1, Dr);
             h->add("ws.Drf3", R2, 4, F, 0);         // d loss / d reward (float4 rows)
-            h->add("ws.Drf2", R2, Hr1, F, 0);
+            if (Dr >= 2) h->add("ws.Drf2", R2, Hr1, F, 0);
             h->add("ws.Drf1", R2, Hr0, F, 0);
-            h->add("roll.R1", ROLL_CAP, Hr0, F, 0);
-            h->add("roll.R2", ROLL_CAP, Hr1, F, 0);
+            if (Dr < 2) last("ws.Drf2", "ws.Drf1", R2, Hr1, Dr);
+            mids.push_back({"ws.Hrfm", R2, 3});
+            mids.push_back({"ws.Drfm", R2, 3});
+            h->add("roll.R1", RR, h->deep ? wmax(3) : Hr0, F, 0);
+            h->add("roll.R2", RR, h->deep ? wmax(3) : Hr1, F, 0);
         }
         if (h->gm) {                  // logstd-gradient partials per model, 16-row tile and column
             h->add("ws.lgp", h->nm * ((h->mb + 15) / 16), S, F, 0);
-            h->add("roll.mnoise", 1, (int64_t)ROLL_CAP * S, F, 0);   // exp(logstd) * u noise (sample / step)
+            h->add("roll.mnoise", 1, RR * S, F, 0);   // exp(logstd) * u noise (sample / step, every model's)
         }
         // model rollout (sacx_rollout), up to ROLL_CAP trajectories per launch chain
         h->add("roll.X", ROLL_CAP, h->ldS, F, 0);
-        h->add("roll.H1", ROLL_CAP, H0, F, 0);
-        h->add("roll.H2", ROLL_CAP, H1, F, 0);
+        h->add("roll.H1", ROLL_CAP, h->deep ? wmax(0) : H0, F, 0);
+        h->add("roll.H2", ROLL_CAP, h->deep ? wmax(0) : H1, F, 0);
         h->add("roll.noise", 1, (int64_t)ROLL_CAP * A, F, 0);
         h->add("roll.A", ROLL_CAP, A, F, 0);
         h->add("roll.Xm", ROLL_CAP, h->ldQ, F, 0);
-        h->add("roll.M1", ROLL_CAP, Hm0, F, 0);
-        h->add("roll.M2", ROLL_CAP, Hm1, F, 0);
-        h->add("roll.O", ROLL_CAP, O, F, 0);
+        h->add("roll.M1", RR, h->deep ? wmax(2) : Hm0, F, 0);
+        h->add("roll.M2", RR, h->deep ? wmax(2) : Hm1, F, 0);
+        h->add("roll.O", RR, O, F, 0);
     }
+    // the middle hidden layers (1 .. D-2) of nets deeper than two layers: <p>m<i>
+    for (const Mid& m : mids)
+        for (int i = 1; i + 1 < h->nd[m.net].D(); ++i)
+            h->add(m.p + std::to_string(i), m.rows, h->nd[m.net].h[i], F, 0);
     h->arena_bytes = (h->arena_bytes + 255) & ~uint64_t(255);
 }
 
@@ -655,6 +716,18 @@ void wbf_wire(sacx_handle* h, GemmProb& p, int mode, bool t32) {
         p.wbf_k = m->K;
         if (const auto* t = find(p.T)) p.obf = h->ptr<uint16_t>("wbf." + t->name);
     }
+}
+
+AdamConsts adam_consts(const sacx_handle* h) {
+    AdamConsts c{};
+    c.lr[GRP_Q] = h->cfg.lr_q;
+    c.lr[GRP_PI] = h->cfg.lr_pi;
+    c.lr[GRP_ALPHA] = h->cfg.lr_alpha;
+    c.lr[GRP_MODEL] = h->cfg.lr_model;
+    c.tau_keep = (float)(1.0 - (double)h->cfg.tau);
+    c.tau_take = h->cfg.tau;
+    c.target_update_int = h->cfg.target_update_int;
+    return c;
 }
 
 void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name, std::vector<GemmProb> ps,
@@ -756,13 +829,7 @@ void add_gemm(sacx_handle* h, std::vector<Launch>& plan, const std::string& name
     L.gemm.bf16 = h->cfg.gemm_bf16 != 0;
     L.gemm.p_stride = h->p_stride;
     L.gemm.ctl = h->ctl();
-    L.gemm.adam.lr[GRP_Q] = h->cfg.lr_q;
-    L.gemm.adam.lr[GRP_PI] = h->cfg.lr_pi;
-    L.gemm.adam.lr[GRP_ALPHA] = h->cfg.lr_alpha;
-    L.gemm.adam.lr[GRP_MODEL] = h->cfg.lr_model;
-    L.gemm.adam.tau_keep = (float)(1.0 - (double)h->cfg.tau);
-    L.gemm.adam.tau_take = h->cfg.tau;
-    L.gemm.adam.target_update_int = h->cfg.target_update_int;
+    L.gemm.adam = adam_consts(h);
     L.grid = tiles;
     plan.push_back(L);
 }
@@ -884,12 +951,15 @@ void pack_seeds(Launch& L, int64_t stride, int n) {
 // running Adam; RCCL sums the contiguous gradient range [first, last] over the ranks and
 // k_adam_apply runs the Adam (and Polyak into the same range at `targ`) with scale 1/ranks.
 void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string& first, const std::string& last,
-                   const std::string& targ, int group) {
-    Launch& G = plan.back();
-    for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
-    const std::string base = G.name.substr(0, G.name.find(".adam"));
-    G.name = base + ".grad";
-    const AdamConsts gadam = G.gemm.adam;       // (G dangles once the plan grows below)
+                   const std::string& targ, int group, int nlaunch = 1) {
+    std::string base;
+    for (int j = 0; j < nlaunch; ++j) {        // the last nlaunch dW launches (add_gemm_split's)
+        Launch& G = plan[plan.size() - 1 - j];
+        for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
+        base = G.name.substr(0, G.name.find(".adam"));
+        G.name = base + ".grad" + G.name.substr(G.name.find(".adam") + 5);
+    }
+    const AdamConsts gadam = adam_consts(h);
     const uint64_t o0 = h->off_of(first);
     const SegInfo& sl = h->seg(last);
     const int64_t n = (int64_t)((sl.off + (uint64_t)(sl.rows * sl.cols) * 4 - o0) / 4);
@@ -916,36 +986,18 @@ void dp_split_adam(sacx_handle* h, std::vector<Launch>& plan, const std::string&
     plan.push_back(U);
 }
 
-void build_plan(sacx_handle* h, int slot, bool record_probs) {
-    std::vector<Launch>& plan = h->plan[slot];
-    plan.clear();
-    h->probs_cursor = 0;
-    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
-    const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
-    const int Hc0 = h->Hc0, Hc1 = h->Hc1;   // the critics' hidden sizes (--critic_layers; H0 / H1: the actor's)
-    // expert rows of world model k: [k * half, (k + 1) * half) with 2 models, all with one
-    const int nm = h->nm, mrows = nm == 1 ? ne : half;
+// The update's inputs in slot `slot`: the sampler (randint + every normal of the update,
+// buffers.py:136, continuous_actors.py:351) and the gather of the replay / expert rows into the
+// normalised staging slabs (buffers.py:137-141, normalizer.py:36-41).  Every plan starts with them.
+void plan_inputs(sacx_handle* h, std::vector<Launch>& plan, int slot) {
+    const int S = h->S, A = h->A, B = h->B, ne = h->ne;
     const int ldS = h->ldS, ldQ = h->ldQ;
-    const int a0 = h->aact[0], a1 = h->aact[1], c0 = h->cact[0], c1 = h->cact[1], m0 = h->macts[0], m1 = h->macts[1];
-    const bool eo = h->cfg.use_expert != 0;
     const std::string sl = "slot" + std::to_string(slot);
+    auto W = [&](const std::string& n) { return h->f(n); };
     int32_t* idx = h->ptr<int32_t>(sl + ".idx");
     float* noise = h->f(sl + ".noise");
-    float* noise_t = noise;
-    float* noise_pi = noise + (size_t)B * A;
-    float* noise_e = noise + (size_t)2 * B * A;
-    float* noise_al = noise + (size_t)(2 * B + ne) * A;
-    auto W = [&](const std::string& n) { return h->f(n); };
     float *Xa = W(sl + ".Xa"), *Xq = W(sl + ".Xq"), *Xt = W(sl + ".Xt"), *Xp = W(sl + ".Xp"), *Xm = W(sl + ".Xm");
     float *r_in = W(sl + ".r"), *d_in = W(sl + ".d"), *se_raw = W(sl + ".se_raw"), *spe_raw = W(sl + ".spe_raw");
-    float *Ha1 = W("ws.Ha1"), *Ha2 = W("ws.Ha2");
-    float *Hq1 = W("ws.Hq1"), *Hq2 = W("ws.Hq2"), *Dq1 = W("ws.Dq1"), *Dq2 = W("ws.Dq2");
-    float *Hp1 = W("ws.Hp1"), *Hp2 = W("ws.Hp2"), *Dp1 = W("ws.Dp1");
-    float *Hm1b = W("ws.Hm1"), *Hm2b = W("ws.Hm2"), *Dm1 = W("ws.Dm1"), *Dm2 = W("ws.Dm2");
-    float *Da1 = W("ws.Da1"), *Da2 = W("ws.Da2"), *Da3 = W("ws.Da3"), *E = W("ws.E");
-    float *Hl1 = W("ws.Hl1"), *Hl2 = W("ws.Hl2");
-    const char* qn[4] = {"t0", "t1", "q0", "q1"};
-
     // ---- sampler
     {
         Launch L{};
@@ -993,11 +1045,94 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         g.r = r_in; g.d = d_in; g.slot = slot; g.nupd = 1; g.slot_bytes = h->slot_bytes;
         g.exp_s = W("expert.s"); g.exp_sp = W("expert.sp");
         g.perm_ring = h->nm == 1 ? nullptr : h->ptr<int32_t>("perm"); g.perm_cap = h->perm_cap;
+        g.perm_ld = h->ne_perm;
         g.se_raw = se_raw; g.spe_raw = spe_raw;
         L.grid = (B + ne + 3) / 4;
         L.bytes = 4.0 * (B * (2.0 * S + A + 2) + ne * 2.0 * S) + 4.0 * (B * (2.0 * ldS + 3.0 * ldQ + 2));
         plan.push_back(L);
     }
+}
+
+// alpha.final (k_alpha_final: the alpha loss / Adam / clamp, SAC_expert.py:340-356, and the update's
+// statistics row) behind the alpha.head launch that ends `plan`; in the data-parallel mode the local
+// alpha gradient, its all-reduce and k_alpha_apply
+void plan_alpha_final(sacx_handle* h, std::vector<Launch>& plan, int nm) {
+    const int B = h->B, ne = h->ne, S = h->S;
+    const bool eo = h->cfg.use_expert != 0;
+    auto W = [&](const std::string& n) { return h->f(n); };
+    {
+        const Launch& AH = plan.back();
+        Launch L{};
+        L.kind = Launch::FINAL;
+        L.name = "alpha.final";
+        FinalArgs& f = L.fin;
+        f.nred = AH.grid;
+        f.alpha = W("alpha"); f.alpha_m = f.alpha + h->p_stride; f.alpha_v = f.alpha + 2 * h->p_stride;
+        f.ctl = h->ctl();
+        f.adam = adam_consts(h);
+        f.target_entropy = h->cfg.target_entropy;
+        f.B = B; f.ne = ne; f.use_expert = eo; f.nm = nm;
+        f.lq = W("ws.lq"); f.lp = W("ws.lp"); f.mse_rows = W("ws.mse"); f.red = W("red");
+        f.mse_tiles = (S + 15) / 16;
+        f.stats = W("stats"); f.stats_cap = h->stats_cap;
+        L.grid = 1;
+        L.block = 64;
+        L.bytes = 4.0 * (f.nred + 3.0 * B + ne);
+        if (h->dp_ranks > 0) {              // alpha gradient: local -> all-reduce -> Adam + counters
+            f.alpha_g = W("alpha") + 3 * h->p_stride;
+            f.grad_scale = (float)(1.0 / (double)h->dp_ranks);
+            L.name = "alpha.grad";
+            plan.push_back(L);
+            Launch R{};
+            R.kind = Launch::ALLREDUCE;
+            R.name = "alpha.allreduce";
+            R.ar_buf = f.alpha_g;
+            R.ar_count = 1;
+            plan.push_back(R);
+            Launch U{};
+            U.kind = Launch::AAPPLY;
+            U.name = "alpha.adam";
+            U.fin = f;
+            U.grid = 1;
+            U.block = 64;
+            plan.push_back(U);
+        } else {
+            plan.push_back(L);
+        }
+    }
+}
+
+void build_plan(sacx_handle* h, int slot, bool record_probs) {
+    std::vector<Launch>& plan = h->plan[slot];
+    plan.clear();
+    h->probs_cursor = 0;
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
+    const int Hm0 = h->Hm0, Hm1 = h->Hm1, half = ne / 2;
+    const int Hc0 = h->Hc0, Hc1 = h->Hc1;   // the critics' hidden sizes (--critic_layers; H0 / H1: the actor's)
+    // expert rows of world model k: [k * half, (k + 1) * half) with 2 or more models (the expert term
+    // takes models 0 and 1, SAC_expert.py:325-326), all with one
+    const int nm = std::min(h->nm, 2), mrows = nm == 1 ? ne : half;
+    const int ldS = h->ldS, ldQ = h->ldQ;
+    const int a0 = h->aact[0], a1 = h->aact[1], c0 = h->cact[0], c1 = h->cact[1], m0 = h->macts[0], m1 = h->macts[1];
+    const bool eo = h->cfg.use_expert != 0;
+    const std::string sl = "slot" + std::to_string(slot);
+    float* noise = h->f(sl + ".noise");
+    float* noise_t = noise;
+    float* noise_pi = noise + (size_t)B * A;
+    float* noise_e = noise + (size_t)2 * B * A;
+    float* noise_al = noise + (size_t)(2 * B + ne) * A;
+    auto W = [&](const std::string& n) { return h->f(n); };
+    float *Xa = W(sl + ".Xa"), *Xq = W(sl + ".Xq"), *Xt = W(sl + ".Xt"), *Xp = W(sl + ".Xp"), *Xm = W(sl + ".Xm");
+    float *r_in = W(sl + ".r"), *d_in = W(sl + ".d"), *se_raw = W(sl + ".se_raw"), *spe_raw = W(sl + ".spe_raw");
+    float *Ha1 = W("ws.Ha1"), *Ha2 = W("ws.Ha2");
+    float *Hq1 = W("ws.Hq1"), *Hq2 = W("ws.Hq2"), *Dq1 = W("ws.Dq1"), *Dq2 = W("ws.Dq2");
+    float *Hp1 = W("ws.Hp1"), *Hp2 = W("ws.Hp2"), *Dp1 = W("ws.Dp1");
+    float *Hm1b = W("ws.Hm1"), *Hm2b = W("ws.Hm2"), *Dm1 = W("ws.Dm1"), *Dm2 = W("ws.Dm2");
+    float *Da1 = W("ws.Da1"), *Da2 = W("ws.Da2"), *Da3 = W("ws.Da3"), *E = W("ws.E");
+    float *Hl1 = W("ws.Hl1"), *Hl2 = W("ws.Hl2");
+    const char* qn[4] = {"t0", "t1", "q0", "q1"};
+
+    plan_inputs(h, plan, slot);
     // ---- actor forward on [sp ; s ; s_e]
     // the two forward layers of a net as two launches (a fused two-layer tile recomputing
     // layer 0 per column tile measured slower once the alpha branch and the heads share
@@ -1481,51 +1616,344 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
         L.bytes = 4.0 * B * H1;
         plan.push_back(L);
     }
-    {
-        const Launch& AH = plan.back();
-        Launch L{};
-        L.kind = Launch::FINAL;
-        L.name = "alpha.final";
-        FinalArgs& f = L.fin;
-        f.nred = AH.grid;
-        f.alpha = W("alpha"); f.alpha_m = f.alpha + h->p_stride; f.alpha_v = f.alpha + 2 * h->p_stride;
-        f.ctl = h->ctl();
-        f.adam = plan[plan.size() - 2].gemm.adam;   // alpha.fwd's Adam constants
-        f.target_entropy = h->cfg.target_entropy;
-        f.B = B; f.ne = ne; f.use_expert = eo; f.nm = nm;
-        f.lq = W("ws.lq"); f.lp = W("ws.lp"); f.mse_rows = W("ws.mse"); f.red = W("red");
-        f.mse_tiles = (S + 15) / 16;
-        f.stats = W("stats"); f.stats_cap = h->stats_cap;
-        L.grid = 1;
-        L.block = 64;
-        L.bytes = 4.0 * (f.nred + 3.0 * B + ne);
-        if (h->dp_ranks > 0) {              // alpha gradient: local -> all-reduce -> Adam + counters
-            f.alpha_g = W("alpha") + 3 * h->p_stride;
-            f.grad_scale = (float)(1.0 / (double)h->dp_ranks);
-            L.name = "alpha.grad";
-            plan.push_back(L);
-            Launch R{};
-            R.kind = Launch::ALLREDUCE;
-            R.name = "alpha.allreduce";
-            R.ar_buf = f.alpha_g;
-            R.ar_count = 1;
-            plan.push_back(R);
-            Launch U{};
-            U.kind = Launch::AAPPLY;
-            U.name = "alpha.adam";
-            U.fin = f;
-            U.grid = 1;
-            U.block = 64;
-            plan.push_back(U);
-        } else {
-            plan.push_back(L);
-        }
-    }
+    plan_alpha_final(h, plan, nm);
     // alpha.fwd .. alpha.final only feed the next update's q.head
     for (size_t i = alpha_first; i < plan.size(); ++i) plan[i].alpha_branch = true;
     for (Launch& L : plan) pack_seeds(L, (int64_t)h->seed_bytes, h->seeds);
     {
     }
+}
+
+// Appends one GEMM launch per GEMM_MAXP problems (a launch's problems travel by value): `name`,
+// then name.1, name.2, ...  Returns the launches added.
+int add_gemm_split(sacx_handle* h, std::vector<Launch>& plan, const std::string& name, const std::vector<GemmProb>& ps,
+                   bool record_probs) {
+    int n = 0;
+    for (size_t i = 0; i < ps.size(); i += GEMM_MAXP, ++n) {
+        std::vector<GemmProb> part(ps.begin() + i, ps.begin() + std::min(ps.size(), i + GEMM_MAXP));
+        add_gemm(h, plan, n == 0 ? name : name + "." + std::to_string(n), part, record_probs);
+    }
+    return n;
+}
+
+// ---------------------------------------------------------------- the generic update plan
+// Nets of any depth (create_nn's layers list, nn_utils.py:100-138; SACX_GENERIC=1 also at two layers,
+// the parity check of this plan against the fused one): the update of build_plan in the reference's
+// order, with every Dense layer a problem of its depth level's forward, dX or dW + Adam launch and the
+// heads on the row kernels -- k_actor_head (evaluate / sample), k_qhead (twin-Q target, critic loss and
+// policy-loss gradients, writing the delta at the critics' last hidden layer), k_actor_bwd (the action
+// gradient through the first layer of the critics / world models, the tanh-Gaussian backward, the
+// delta at the actor's last hidden layer).  No folds and no linearity fusion: each delta is the
+// loss-scaled one, the dW launches take unscaled rows.  merged_body folds the alpha branch exactly
+// as in the fused plan (alpha.fwd<i> into actor.fwd<i>, alpha.head into actor.head, alpha.final into
+// the first forward launch after it).
+void build_plan_generic(sacx_handle* h, int slot, bool record_probs) {
+    std::vector<Launch>& plan = h->plan[slot];
+    plan.clear();
+    h->probs_cursor = 0;
+    const int S = h->S, A = h->A, H0 = h->H0, H1 = h->H1, B = h->B, ne = h->ne, Aout = h->Aout;
+    const int Hm1 = h->Hm1, half = ne / 2, Hc1 = h->Hc1;
+    const int nm = std::min(h->nm, 2), mrows = nm == 1 ? ne : half;   // the expert term's models
+    const int ldS = h->ldS, ldQ = h->ldQ, Rb = h->Rb;
+    const bool eo = h->cfg.use_expert != 0;
+    const NetDims &na = h->nd[0], &nc = h->nd[1], &nmd = h->nd[2];
+    const int Da = na.D(), Dc = nc.D(), Dm = eo ? nmd.D() : 0;
+    const std::string sl = "slot" + std::to_string(slot);
+    auto W = [&](const std::string& n) { return h->f(n); };
+    auto L_ = [](const std::string& net, int i) { return net + ".l" + std::to_string(i); };
+    // hidden-layer buffer i of a chain of D layers: <p>1 (layer 0), <p>2 (the last), <p>m<i>
+    auto ch = [&](const std::string& p, int i, int D) -> float* {
+        if (i == 0) return W(p + "1");
+        if (i == D - 1) return W(p + "2");
+        return W(p + "m" + std::to_string(i));
+    };
+    float* noise = h->f(sl + ".noise");
+    float* noise_t = noise;
+    float* noise_pi = noise + (size_t)B * A;
+    float* noise_e = noise + (size_t)2 * B * A;
+    float* noise_al = noise + (size_t)(2 * B + ne) * A;
+    float *Xa = W(sl + ".Xa"), *Xq = W(sl + ".Xq"), *Xt = W(sl + ".Xt"), *Xp = W(sl + ".Xp"), *Xm = W(sl + ".Xm");
+    float *r_in = W(sl + ".r"), *d_in = W(sl + ".d"), *se_raw = W(sl + ".se_raw"), *spe_raw = W(sl + ".spe_raw");
+    const char* qn[4] = {"t0", "t1", "q0", "q1"};
+    const int Ra4 = (h->Ra + 3) & ~3;       // first row of the alpha rows in the actor chain's buffers
+
+    plan_inputs(h, plan, slot);
+    // ---- actor forward on rows [r0, r0 + M) of its chain from X: --actor_layer_norm puts Dense ->
+    // LayerNorm -> tanh on layer 0 (k_ln on the pre-norm output, nn_utils.py:110-119)
+    auto actor_fwd = [&](const std::string& name, const float* X, int r0, int M, bool alpha) {
+        for (int i = 0; i < Da; ++i) {
+            const float* in = i == 0 ? X : ch("ws.Ha", i - 1, Da) + (size_t)r0 * na.h[i - 1];
+            const int ldi = i == 0 ? ldS : na.h[i - 1], K = i == 0 ? S : na.h[i - 1];
+            const int act = (i == 0 && h->ln) ? ACT_NONE : na.act[i];
+            add_gemm(h, plan, name + std::to_string(i),
+                     {prob_fwd(in, ldi, M, K, W(L_("actor", i)), na.h[i], ch("ws.Ha", i, Da) + (size_t)r0 * na.h[i], act)},
+                     record_probs);
+            if (i == 0 && h->ln) {
+                Launch L{};
+                L.kind = Launch::LNORM;
+                L.name = alpha ? "alpha.ln" : "actor.ln";
+                LNArgs& a = L.ln;
+                a.mode = 0; a.H = H0; a.Z = W("ws.Ha1"); a.nrange = 1; a.r[0] = r0; a.r[1] = r0 + M;
+                a.gamma = W("actor.ln"); a.xhat = W("ws.ln_xhat"); a.rstd = W("ws.ln_rstd"); a.cache_rows = h->Ra;
+                L.grid = (M + 3) / 4;
+                L.flops = 8.0 * M * H0;
+                L.bytes = 4.0 * M * H0 * 3;
+                plan.push_back(L);
+            }
+        }
+    };
+    actor_fwd("actor.fwd", Xa, 0, h->Ra, false);
+    float* Ha_last = W("ws.Ha2");
+    auto head_base = [&](HeadArgs& a, const float* H2) {
+        a.H2 = H2; a.ldh = H1; a.W3 = W(L_("actor", Da)); a.logstd = W("actor.logstd");
+        a.part = nullptr; a.tq = (H1 + 15) / 16;
+        a.H1 = H1; a.A = A; a.Aout = Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
+        a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
+        a.ma_mean = W(mnorm(h, "a_mean")); a.ma_den = W(mnorm(h, "a_den"));
+    };
+    {   // ---- actor head: evaluate(sp) -> target rows, evaluate(s) -> policy rows, sample(s_e) -> model rows
+        Launch L{};
+        L.kind = Launch::AHEAD;
+        L.name = "actor.head";
+        L.frees_slot = true;
+        HeadArgs& a = L.head;
+        head_base(a, Ha_last);
+        a.nseg = eo ? 3 : 2;
+        a.seg[0] = {0, B, 0, 0, noise_t, Xt, W("ws.nlp_t")};
+        a.seg[1] = {B, 2 * B, 0, 0, noise_pi, Xp, W("ws.nlp_p")};
+        a.seg[2] = {2 * B, 2 * B + ne, 1, 0, noise_e, Xm, nullptr};
+        a.total_rows = h->Ra;
+        a.cache_row0 = B;
+        a.cache_row1 = h->Ra;
+        a.c_t = W("ws.c_t"); a.c_std = W("ws.c_std"); a.c_u = W("ws.c_u"); a.c_mask = W("ws.c_mask");
+        a.alpha_mode = 0;
+        L.grid = (h->Ra + 3) / 4;
+        L.flops = 2.0 * h->Ra * H1 * Aout;
+        L.bytes = 4.0 * h->Ra * (H1 + 6.0 * A);
+        plan.push_back(L);
+    }
+    // ---- target / critic forward (t0, t1 on [sp | pi(sp)], q0, q1 on [s | a]; the world models' hidden
+    // layers on the expert rows [s_e | pi(s_e)]), one launch per depth level
+    for (int i = 0; i < std::max(Dc, Dm); ++i) {
+        std::vector<GemmProb> ps;
+        if (i < Dc)
+            for (int k = 0; k < 4; ++k) {
+                const float* in = i == 0 ? (k < 2 ? Xt : Xq) : ch("ws.Hq", i - 1, Dc) + (size_t)k * B * nc.h[i - 1];
+                ps.push_back(prob_fwd(in, i == 0 ? ldQ : nc.h[i - 1], B, i == 0 ? S + A : nc.h[i - 1], W(L_(qn[k], i)),
+                                      nc.h[i], ch("ws.Hq", i, Dc) + (size_t)k * B * nc.h[i], nc.act[i]));
+            }
+        if (i < Dm)
+            for (int k = 0; k < nm; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                const float* in = i == 0 ? Xm + (size_t)k * half * ldQ : ch("ws.Hm", i - 1, Dm) + (size_t)k * half * nmd.h[i - 1];
+                ps.push_back(prob_fwd(in, i == 0 ? ldQ : nmd.h[i - 1], mrows, i == 0 ? S + A : nmd.h[i - 1], W(L_(n, i)),
+                                      nmd.h[i], ch("ws.Hm", i, Dm) + (size_t)k * half * nmd.h[i], nmd.act[i]));
+            }
+        add_gemm(h, plan, "q.fwd" + std::to_string(i), ps, record_probs);
+    }
+    const int mtn = (S + 15) / 16;
+    if (eo) {   // the world models' head on the expert rows + the expert MSE (SAC_expert.py:319-332)
+        std::vector<GemmProb> pm;
+        for (int k = 0; k < nm; ++k) {
+            const std::string n = "m" + std::to_string(k);
+            GemmProb p{};
+            p.A = W("ws.Hm2") + (size_t)k * half * Hm1; p.lda = Hm1; p.a_kc = 1; p.ones_row = -1;
+            p.B = W(L_(n, Dm)); p.ldb = h->Om; p.b_kc = 0;       // W_ext [(Hm1+1) x Om], Om = S (+1)
+            p.M = mrows; p.N = S; p.K = Hm1;                     // delta-s columns only
+            p.bias = W(L_(n, Dm)) + (size_t)Hm1 * h->Om;
+            p.C = W("ws.dout") + (size_t)k * half * S; p.ldc = S;
+            p.epi = EPI_FWD; p.act = ACT_NONE;
+            p.mse = 1; p.grad_scale = 1.f / (float)mrows;       // MSE_loss = mean over the rows
+            p.dclip = h->cfg.delta_clip_pred > 0.f ? h->cfg.delta_clip_pred : 0.f;
+            p.se_raw = se_raw + (size_t)k * half * S; p.spe_raw = spe_raw + (size_t)k * half * S;
+            p.dmean = W("mnorm.d_mean"); p.dden = W("mnorm.d_den");
+            p.part = W("ws.mse") + (size_t)k * half * mtn;
+            pm.push_back(p);
+        }
+        add_gemm(h, plan, "model.head", pm, record_probs);
+    }
+    {   // ---- q.head: min target, TD target, critic losses and the delta at the critics' last hidden layer
+        Launch L{};
+        L.kind = Launch::QHEAD;
+        L.name = "q.head";
+        QHeadArgs& q = L.qh;
+        q.mode = 0; q.B = B; q.H1 = Hc1; q.H2 = W("ws.Hq2");
+        for (int k = 0; k < 4; ++k) q.W3[k] = W(L_(qn[k], Dc));
+        q.act = nc.act[Dc - 1]; q.D2 = W("ws.Dq2"); q.g = W("ws.gq"); q.loss_rows = W("ws.lq");
+        q.alpha = W("alpha"); q.nlp = W("ws.nlp_t"); q.r = r_in; q.d = d_in;
+        q.gamma = h->cfg.gamma; q.ret_den = W("norm.ret_den"); q.w_sac = 1.f;
+        q.ne = 0; q.ctl = h->ctl();
+        L.grid = (B + 3) / 4;
+        L.flops = 2.0 * B * Hc1 * 4;
+        L.bytes = 4.0 * (4.0 * B * Hc1 + 2.0 * B * Hc1);
+        plan.push_back(L);
+    }
+    // ---- critic backward (dX down to layer 0's output), then dW + Keras Adam + Polyak into t0 / t1
+    for (int i = Dc - 1; i >= 1; --i) {
+        std::vector<GemmProb> pb;
+        for (int k = 0; k < 2; ++k)
+            pb.push_back(prob_dx(ch("ws.Dq", i, Dc) + (size_t)k * B * nc.h[i], B, nc.h[i], W(L_(qn[2 + k], i)), nc.h[i - 1],
+                                 ch("ws.Hq", i - 1, Dc) + (size_t)(2 + k) * B * nc.h[i - 1],
+                                 ch("ws.Dq", i - 1, Dc) + (size_t)k * B * nc.h[i - 1], nc.act[i - 1]));
+        add_gemm(h, plan, "critic.bwd" + std::to_string(i), pb, record_probs);
+    }
+    {
+        std::vector<GemmProb> pw;
+        for (int k = 0; k < 2; ++k) {
+            const std::string n = "q" + std::to_string(k), t = "t" + std::to_string(k);
+            for (int i = 0; i < Dc; ++i) {
+                const float* X = i == 0 ? Xq : ch("ws.Hq", i - 1, Dc) + (size_t)(2 + k) * B * nc.h[i - 1];
+                const int K = i == 0 ? S + A : nc.h[i - 1];
+                pw.push_back(prob_dw(X, i == 0 ? ldQ : K, K, B, ch("ws.Dq", i, Dc) + (size_t)k * B * nc.h[i], nc.h[i],
+                                     W(L_(n, i)), W(L_(t, i)), GRP_Q));
+            }
+            pw.push_back(prob_dw(W("ws.Hq2") + (size_t)(2 + k) * B * Hc1, Hc1, Hc1, B, W("ws.gq") + (size_t)k * B, 1,
+                                 W(L_(n, Dc)), W(L_(t, Dc)), GRP_Q));
+        }
+        const int n = add_gemm_split(h, plan, "critic.adam", pw, record_probs);
+        if (h->dp_ranks > 0) dp_split_adam(h, plan, "q0.l0", L_("q1", Dc), "t0.l0", GRP_Q, n);
+    }
+    // ---- policy loss through the updated critics
+    for (int i = 0; i < Dc; ++i) {
+        std::vector<GemmProb> ps;
+        for (int k = 0; k < 2; ++k) {
+            const float* in = i == 0 ? Xp : ch("ws.Hp", i - 1, Dc) + (size_t)k * B * nc.h[i - 1];
+            ps.push_back(prob_fwd(in, i == 0 ? ldQ : nc.h[i - 1], B, i == 0 ? S + A : nc.h[i - 1],
+                                  W(L_("q" + std::to_string(k), i)), nc.h[i], ch("ws.Hp", i, Dc) + (size_t)k * B * nc.h[i],
+                                  nc.act[i]));
+        }
+        add_gemm(h, plan, "pi.q.fwd" + std::to_string(i), ps, record_probs);
+    }
+    {   // min, tie split, policy loss rows, the delta at the critics' last hidden layer (x d p / d Q_k)
+        Launch L{};
+        L.kind = Launch::QHEAD;
+        L.name = "pi.q.head";
+        QHeadArgs& q = L.qh;
+        q.mode = 1; q.B = B; q.H1 = Hc1; q.H2 = W("ws.Hp2");
+        q.W3[0] = W(L_("q0", Dc)); q.W3[1] = W(L_("q1", Dc)); q.W3[2] = nullptr; q.W3[3] = nullptr;
+        q.act = nc.act[Dc - 1]; q.D2 = W("ws.Dp2"); q.g = W("ws.gp"); q.loss_rows = W("ws.lp");
+        q.alpha = W("alpha"); q.nlp = W("ws.nlp_p");
+        q.w_sac = eo ? (float)(1.0 - (double)h->cfg.epsilon) : 1.f;
+        q.ret_den = W("norm.ret_den");
+        q.ne = 0; q.ctl = h->ctl();
+        L.grid = (B + 3) / 4;
+        L.flops = 2.0 * B * Hc1 * 2;
+        L.bytes = 4.0 * (4.0 * B * Hc1);
+        plan.push_back(L);
+    }
+    for (int i = Dc - 1; i >= 1; --i) {
+        std::vector<GemmProb> pb;
+        for (int k = 0; k < 2; ++k)
+            pb.push_back(prob_dx(ch("ws.Dp", i, Dc) + (size_t)k * B * nc.h[i], B, nc.h[i], W(L_("q" + std::to_string(k), i)),
+                                 nc.h[i - 1], ch("ws.Hp", i - 1, Dc) + (size_t)k * B * nc.h[i - 1],
+                                 ch("ws.Dp", i - 1, Dc) + (size_t)k * B * nc.h[i - 1], nc.act[i - 1]));
+        add_gemm(h, plan, "pi.q.bwd" + std::to_string(i), pb, record_probs);
+    }
+    if (eo)     // the world models' backward to their layer-0 output (the expert rows' action gradient)
+        for (int i = Dm; i >= 1; --i) {
+            std::vector<GemmProb> pb;
+            for (int k = 0; k < nm; ++k) {
+                const std::string n = "m" + std::to_string(k);
+                const float* D = i == Dm ? W("ws.dout") + (size_t)k * half * S : ch("ws.Dm", i, Dm) + (size_t)k * half * nmd.h[i];
+                GemmProb p = prob_dx(D, mrows, i == Dm ? S : nmd.h[i], W(L_(n, i)), nmd.h[i - 1],
+                                     ch("ws.Hm", i - 1, Dm) + (size_t)k * half * nmd.h[i - 1],
+                                     ch("ws.Dm", i - 1, Dm) + (size_t)k * half * nmd.h[i - 1], nmd.act[i - 1]);
+                if (i == Dm) p.ldb = h->Om;          // the head's delta-s columns: B[n][k] = W_ext[n][k], stride Om
+                pb.push_back(p);
+            }
+            add_gemm(h, plan, "model.bwd" + std::to_string(i), pb, record_probs);
+        }
+    // ---- actor backward: action gradients -> tanh-Gaussian backward -> the delta at the last hidden
+    // layer (k_actor_bwd, from the loss-scaled deltas: gpol = null), dX to layer 0, dW + Adam
+    {
+        Launch L{};
+        L.kind = Launch::ABWD;
+        L.name = "actor.head.bwd";
+        ActorBwdArgs& b = L.ab;
+        b.B = B; b.ne = ne; b.S = S; b.A = A; b.Aout = Aout; b.H0 = h->Hc0; b.H1 = H1; b.Hm0 = h->Hm0;
+        b.per_state_std = h->cfg.per_state_std; b.lim = h->cfg.act_limit;
+        b.Dp1 = W("ws.Dp1"); b.Wq1[0] = W("q0.l0"); b.Wq1[1] = W("q1.l0");
+        b.Dm1 = W("ws.Dm1"); b.Wm1[0] = eo ? W("m0.l0") : nullptr; b.Wm1[1] = eo ? W(nm > 1 ? "m1.l0" : "m0.l0") : nullptr;
+        b.a_den = W("norm.a_den"); b.ma_den = W(mnorm(h, "a_den")); b.alpha = W("alpha"); b.ctl = h->ctl();
+        b.use_expert = eo;
+        b.c_t = W("ws.c_t"); b.c_std = W("ws.c_std"); b.c_u = W("ws.c_u"); b.c_mask = W("ws.c_mask");
+        b.W3a = W(L_("actor", Da)); b.Ha2 = Ha_last + (size_t)B * H1;
+        b.act = (Da == 1 && h->ln) ? ACT_TANH : na.act[Da - 1];   // layer norm: tanh' at the norm's output
+        b.Da3 = W("ws.Da3"); b.Da2 = W("ws.Da2"); b.E = W("ws.E");
+        b.gpol = nullptr;
+        L.grid = (Rb + 3) / 4;
+        L.flops = 2.0 * B * 2 * h->Hc0 * A + 2.0 * ne * h->Hm0 * A + 2.0 * Rb * H1 * Aout;
+        L.bytes = 4.0 * (2.0 * B * h->Hc0 + ne * h->Hm0 + 2.0 * Rb * H1);
+        plan.push_back(L);
+    }
+    for (int i = Da - 1; i >= 1; --i)
+        add_gemm(h, plan, "actor.bwd" + std::to_string(i),
+                 {prob_dx(ch("ws.Da", i, Da), Rb, na.h[i], W(L_("actor", i)), na.h[i - 1],
+                          ch("ws.Ha", i - 1, Da) + (size_t)B * na.h[i - 1], ch("ws.Da", i - 1, Da),
+                          (i == 1 && h->ln) ? ACT_TANH : na.act[i - 1])},
+                 record_probs);
+    if (h->ln) {                          // dY -> dZ through the norm; dY*xhat, dY for gamma / beta
+        Launch N{};
+        N.kind = Launch::LNORM;
+        N.name = "actor.ln.bwd";
+        LNArgs& a = N.ln;
+        a.mode = 1; a.H = H0; a.Z = W("ws.Da1"); a.r[1] = Rb; a.gamma = W("actor.ln");
+        a.xhat = W("ws.ln_xhat"); a.rstd = W("ws.ln_rstd"); a.xrow0 = B;
+        a.gy = W("ws.ln_gy"); a.gb = W("ws.ln_gb");
+        N.grid = (Rb + 3) / 4;
+        N.flops = 8.0 * Rb * H0;
+        N.bytes = 4.0 * Rb * H0 * 5;
+        plan.push_back(N);
+    }
+    {
+        std::vector<GemmProb> pw;
+        for (int i = 0; i < Da; ++i) {
+            const float* X = i == 0 ? Xa + (size_t)B * ldS : ch("ws.Ha", i - 1, Da) + (size_t)B * na.h[i - 1];
+            const int K = i == 0 ? S : na.h[i - 1];
+            pw.push_back(prob_dw(X, i == 0 ? ldS : K, K, Rb, ch("ws.Da", i, Da), na.h[i], W(L_("actor", i)), nullptr, GRP_PI));
+        }
+        pw.push_back(prob_dw(Ha_last + (size_t)B * H1, H1, H1, Rb, W("ws.Da3"), Aout, W(L_("actor", Da)), nullptr, GRP_PI));
+        if (!h->cfg.per_state_std) {
+            GemmProb p = prob_dw(W("ws.E"), 1, 0, Rb, W("ws.E"), A, W("actor.logstd"), nullptr, GRP_PI);
+            p.ones_row = 0;   // single all-ones row: column sums of E
+            pw.push_back(p);
+        }
+        if (h->ln) {          // gamma, beta: column sums of dY*xhat and dY
+            for (int k = 0; k < 2; ++k) {
+                float* gsrc = W(k ? "ws.ln_gb" : "ws.ln_gy");
+                GemmProb p = prob_dw(gsrc, 1, 0, Rb, gsrc, H0, W("actor.ln") + (size_t)k * H0, nullptr, GRP_PI);
+                p.ones_row = 0;
+                pw.push_back(p);
+            }
+        }
+        const int n = add_gemm_split(h, plan, "actor.adam", pw, record_probs);
+        if (h->dp_ranks > 0) dp_split_adam(h, plan, "actor.l0", "actor.logstd", "", GRP_PI, n);
+    }
+    // ---- alpha: the updated actor on s, evaluate, Adam on alpha, statistics
+    const size_t alpha_first = plan.size();
+    actor_fwd("alpha.fwd", Xa + (size_t)B * ldS, Ra4, B, true);
+    {
+        Launch L{};
+        L.kind = Launch::AHEAD;
+        L.name = "alpha.head";
+        HeadArgs& a = L.head;
+        head_base(a, W("ws.Hl2"));
+        a.nseg = 1;
+        a.seg[0] = {0, B, 0, 0, noise_al, nullptr, W("ws.nlp3")};
+        a.total_rows = B;
+        a.cache_row0 = 1 << 30;
+        a.c_t = nullptr;
+        a.alpha_mode = 1;
+        L.fin.red = W("red");                       // per-workgroup partials of sum(-nlp + H)
+        L.fin.target_entropy = h->cfg.target_entropy;
+        L.grid = (B + 3) / 4;
+        L.flops = 2.0 * B * H1 * Aout;
+        L.bytes = 4.0 * B * H1;
+        plan.push_back(L);
+    }
+    plan_alpha_final(h, plan, nm);
+    for (size_t i = alpha_first; i < plan.size(); ++i) plan[i].alpha_branch = true;
+    for (Launch& L : plan) pack_seeds(L, (int64_t)h->seed_bytes, h->seeds);
 }
 
 // one world-model fitting step: gather -> 3 fwd GEMMs -> loss grads -> 2 dX GEMMs -> dW + Adam -> finalize
@@ -1537,9 +1965,12 @@ void build_model_plan(sacx_handle* h) {
     std::vector<Launch>& plan = h->mplans[h->sel];
     plan.clear();
     if (!h->cfg.use_expert) return;
-    const int S = h->S, A = h->A, mb = h->mb, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1, ldQ = h->ldQ;
-    const int m0 = h->macts[0], m1 = h->macts[1];
+    const int S = h->S, A = h->A, mb = h->mb, O = S + 1, ldQ = h->ldQ;
     const int nm = h->nm;
+    const NetDims& nmd = h->nd[2];
+    const NetDims& nrd = h->nd[3];
+    const int Dm = nmd.D(), Dr = h->srn ? nrd.D() : 0;
+    const int Lf = std::max(Dm, Dr);          // forward levels 0 .. Lf (a net's head at its own depth)
     // GaussianModel / --separate_reward_nn fits exist only in the folded form (their loss epilogues)
     const bool fuse = h->mfuse != 0 || h->gm || h->srn;
     const int Om = h->Om;             // model-net outputs (S + 1, or S beside a reward net)
@@ -1547,10 +1978,18 @@ void build_model_plan(sacx_handle* h) {
     const int ldO = (int)r4(O);       // D3 row stride
     const int ntm = (mb + 15) / 16;   // GaussianModel: logstd-gradient partials per column (row tiles)
     // model.bwd2 generated on model.bwd1's operand loads (rowk 7) for narrow heads (S + 1 <= 32)
-    const bool bfold = fuse && h->mfuse >= 3 && O <= 32 && h->mtile != 2 && h->unaligned_b && !h->gm && !h->srn;
+    const bool bfold = fuse && h->mfuse >= 3 && O <= 32 && h->mtile != 2 && h->unaligned_b && !h->gm && !h->srn &&
+                       Dm == 2;
     auto W = [&](const std::string& n) { return h->f(n); };
-    float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Hf1 = W("ws.Hf1"), *Hf2 = W("ws.Hf2"), *Of = W("ws.Of");
-    float *Df3 = W("ws.Df3"), *Df2 = W("ws.Df2"), *Df1 = W("ws.Df1");
+    auto L_ = [](const std::string& net, int i) { return net + ".l" + std::to_string(i); };
+    // hidden-layer buffer i of a chain of D layers: <p>1 (layer 0), <p>2 (the last), <p>m<i>
+    auto ch = [&](const std::string& p, int i, int D) -> float* {
+        if (i == 0) return W(p + "1");
+        if (i == D - 1) return W(p + "2");
+        return W(p + "m" + std::to_string(i));
+    };
+    float *Xf = W("ws.Xf"), *Tf = W("ws.Tf"), *Of = W("ws.Of");
+    float *Df3 = W("ws.Df3");
     MGatherArgs mg{};
     mg.replay = W("replay"); mg.cap = h->cap; mg.stride = h->stride; mg.S = S; mg.A = A; mg.mb = mb;
     mg.idx_ring = h->ptr<int32_t>("mfit.idx"); mg.idx_cap = h->mfit_cap; mg.ctl = h->ctl();
@@ -1570,62 +2009,95 @@ void build_model_plan(sacx_handle* h) {
         L.bytes = 4.0 * nm * mb * (2.0 * S + A + 1 + ldQ + O);
         plan.push_back(L);
     }
-    std::vector<GemmProb> f0, f1, f2, b2, b1, w, wr;
+    // forward levels (f[i]: every net's layer i, the head at its depth), backward steps from the heads
+    // (b[t]: the dX through layer D - t of each net of depth D > t), dW + Adam per net
+    std::vector<std::vector<GemmProb>> f(Lf + 1), b(Lf);
+    std::vector<GemmProb> w, wr;
     for (int k = 0; k < nm; ++k) {
         const std::string n = "m" + std::to_string(k);
         const size_t r0 = (size_t)k * mb;
-        f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hm0, Hf1 + r0 * Hm0, m0));
-        f1.push_back(prob_fwd(Hf1 + r0 * Hm0, Hm0, mb, Hm0, W(n + ".l1"), Hm1, Hf2 + r0 * Hm1, m1));
-        f2.push_back(prob_fwd(Hf2 + r0 * Hm1, Hm1, mb, Hm1, W(n + ".l2"), Om, fuse ? Df3 + r0 * ldO : Of + r0 * O,
-                              ACT_NONE));
-        if (fuse) {   // MSEModel / GaussianModel.get_loss as the head's epilogue: C = d loss / d out, partials
-            GemmProb& p = f2.back();
-            p.ldc = ldO;
-            p.mse = MSE_FIT | (h->gm ? MSE_GAUSS : 0) | (h->lscale ? MSE_SCALE : 0) | (h->srn ? MSE_NOREW : 0);
-            p.se_raw = Tf + r0 * O; p.ldp = O; p.part = W("ws.lf") + r0 * nt;
-            p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;   // the reward column's
-            if (h->gm) {
-                p.spe_raw = W(n + ".logstd");
-                p.ppart = W("ws.lgp") + (size_t)k * ntm * S;
+        for (int i = 0; i <= Dm; ++i) {
+            const bool head = i == Dm;
+            const float* in = i == 0 ? Xf + r0 * ldQ : ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1];
+            const int K = i == 0 ? S + A : nmd.h[i - 1];
+            if (!head) {
+                f[i].push_back(prob_fwd(in, i == 0 ? ldQ : K, mb, K, W(L_(n, i)), nmd.h[i],
+                                        ch("ws.Hf", i, Dm) + r0 * nmd.h[i], nmd.act[i]));
+            } else {
+                f[i].push_back(prob_fwd(in, K, mb, K, W(L_(n, i)), Om, fuse ? Df3 + r0 * ldO : Of + r0 * O, ACT_NONE));
+                if (fuse) {   // MSEModel / GaussianModel.get_loss as the head's epilogue: C = d loss / d out, partials
+                    GemmProb& p = f[i].back();
+                    p.ldc = ldO;
+                    p.mse = MSE_FIT | (h->gm ? MSE_GAUSS : 0) | (h->lscale ? MSE_SCALE : 0) | (h->srn ? MSE_NOREW : 0);
+                    p.se_raw = Tf + r0 * O; p.ldp = O; p.part = W("ws.lf") + r0 * nt;
+                    p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;   // the reward column's
+                    if (h->gm) {
+                        p.spe_raw = W(n + ".logstd");
+                        p.ppart = W("ws.lgp") + (size_t)k * ntm * S;
+                    }
+                }
             }
         }
-        b2.push_back(prob_dx(Df3 + r0 * ldO, mb, Om, W(n + ".l2"), Hm1, Hf2 + r0 * Hm1, Df2 + r0 * Hm1, m1));
-        b2.back().lda = ldO;
-        b1.push_back(prob_dx(Df2 + r0 * Hm1, mb, Hm1, W(n + ".l1"), Hm0, Hf1 + r0 * Hm0, Df1 + r0 * Hm0, m0));
-        if (bfold) {   // A = D2 generated from H2, D3 and W2 on load; column tile 0 stores it for model.adam
-            GemmProb& q = b1.back();
-            q.A = Hf2 + r0 * Hm1; q.wgen = W(n + ".l2"); q.gen_act = m1;
-            q.gd = Df3 + r0 * ldO; q.gd_ld = ldO; q.g_o = O; q.gst = Df2 + r0 * Hm1; q.gst_ld = Hm1;
+        for (int i = Dm; i >= 1; --i) {
+            const bool head = i == Dm;
+            GemmProb p = prob_dx(head ? Df3 + r0 * ldO : ch("ws.Df", i, Dm) + r0 * nmd.h[i], mb, head ? Om : nmd.h[i],
+                                 W(L_(n, i)), nmd.h[i - 1], ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1],
+                                 ch("ws.Df", i - 1, Dm) + r0 * nmd.h[i - 1], nmd.act[i - 1]);
+            if (head) p.lda = ldO;
+            if (bfold && i == 1) {   // A = D2 generated from H2, D3 and W2 on load; column tile 0 stores it for model.adam
+                p.A = W("ws.Hf2") + r0 * nmd.h[1]; p.wgen = W(L_(n, 2)); p.gen_act = nmd.act[1];
+                p.gd = Df3 + r0 * ldO; p.gd_ld = ldO; p.g_o = O; p.gst = W("ws.Df2") + r0 * nmd.h[1]; p.gst_ld = nmd.h[1];
+            }
+            b[Lf - i - (Lf - Dm)].push_back(p);
         }
-        w.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Df1 + r0 * Hm0, Hm0, W(n + ".l0"), nullptr, GRP_MODEL));
-        w.push_back(prob_dw(Hf1 + r0 * Hm0, Hm0, Hm0, mb, Df2 + r0 * Hm1, Hm1, W(n + ".l1"), nullptr, GRP_MODEL));
-        w.push_back(prob_dw(Hf2 + r0 * Hm1, Hm1, Hm1, mb, Df3 + r0 * ldO, Om, W(n + ".l2"), nullptr, GRP_MODEL));
-        w.back().ldb = ldO;
+        for (int i = 0; i <= Dm; ++i) {
+            const bool head = i == Dm;
+            const float* X = i == 0 ? Xf + r0 * ldQ : ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1];
+            const int K = i == 0 ? S + A : nmd.h[i - 1];
+            w.push_back(prob_dw(X, i == 0 ? ldQ : K, K, mb, head ? Df3 + r0 * ldO : ch("ws.Df", i, Dm) + r0 * nmd.h[i],
+                                head ? Om : nmd.h[i], W(L_(n, i)), nullptr, GRP_MODEL));
+            if (head) w.back().ldb = ldO;
+        }
     }
     if (h->srn) {
         // --separate_reward_nn (base_world_model.py:32-37, :72-74): the reward nets ride in the same
-        // launches -- layers 0 / 1 beside the model nets', the 1-wide head with the MSE loss epilogue on
-        // the targets' reward column, their dX and (own launch: > GEMM_MAXP problems) dW + Adam
-        const int Hr0 = h->Hr0, Hr1 = h->Hr1, r0a = h->racts[0], r1a = h->racts[1];
-        float *Hr1f = W("ws.Hrf1"), *Hr2f = W("ws.Hrf2"), *Dr3 = W("ws.Drf3"), *Dr2 = W("ws.Drf2"), *Dr1 = W("ws.Drf1");
+        // launches -- their hidden layers beside the model nets', the 1-wide head with the MSE loss
+        // epilogue on the targets' reward column, their dX and (own launch) dW + Adam
+        float* Dr3 = W("ws.Drf3");
         for (int k = 0; k < nm; ++k) {
             const std::string n = "r" + std::to_string(k);
             const size_t r0 = (size_t)k * mb;
-            f0.push_back(prob_fwd(Xf + r0 * ldQ, ldQ, mb, S + A, W(n + ".l0"), Hr0, Hr1f + r0 * Hr0, r0a));
-            f1.push_back(prob_fwd(Hr1f + r0 * Hr0, Hr0, mb, Hr0, W(n + ".l1"), Hr1, Hr2f + r0 * Hr1, r1a));
-            f2.push_back(prob_fwd(Hr2f + r0 * Hr1, Hr1, mb, Hr1, W(n + ".l2"), 1, Dr3 + r0 * 4, ACT_NONE));
-            GemmProb& p = f2.back();
-            p.ldc = 4;
-            p.mse = MSE_FIT;                                // N = 1: column 0 is the reward column
-            p.se_raw = Tf + r0 * O + S; p.ldp = O; p.part = W("ws.lf") + (size_t)nm * mb * nt + r0;
-            p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;
-            b2.push_back(prob_dx(Dr3 + r0 * 4, mb, 1, W(n + ".l2"), Hr1, Hr2f + r0 * Hr1, Dr2 + r0 * Hr1, r1a));
-            b2.back().lda = 4;
-            b1.push_back(prob_dx(Dr2 + r0 * Hr1, mb, Hr1, W(n + ".l1"), Hr0, Hr1f + r0 * Hr0, Dr1 + r0 * Hr0, r0a));
-            wr.push_back(prob_dw(Xf + r0 * ldQ, ldQ, S + A, mb, Dr1 + r0 * Hr0, Hr0, W(n + ".l0"), nullptr, GRP_MODEL));
-            wr.push_back(prob_dw(Hr1f + r0 * Hr0, Hr0, Hr0, mb, Dr2 + r0 * Hr1, Hr1, W(n + ".l1"), nullptr, GRP_MODEL));
-            wr.push_back(prob_dw(Hr2f + r0 * Hr1, Hr1, Hr1, mb, Dr3 + r0 * 4, 1, W(n + ".l2"), nullptr, GRP_MODEL));
-            wr.back().ldb = 4;
+            for (int i = 0; i <= Dr; ++i) {
+                const float* in = i == 0 ? Xf + r0 * ldQ : ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1];
+                const int K = i == 0 ? S + A : nrd.h[i - 1];
+                if (i < Dr) {
+                    f[i].push_back(prob_fwd(in, i == 0 ? ldQ : K, mb, K, W(L_(n, i)), nrd.h[i],
+                                            ch("ws.Hrf", i, Dr) + r0 * nrd.h[i], nrd.act[i]));
+                } else {
+                    f[i].push_back(prob_fwd(in, K, mb, K, W(L_(n, i)), 1, Dr3 + r0 * 4, ACT_NONE));
+                    GemmProb& p = f[i].back();
+                    p.ldc = 4;
+                    p.mse = MSE_FIT;                                // N = 1: column 0 is the reward column
+                    p.se_raw = Tf + r0 * O + S; p.ldp = O; p.part = W("ws.lf") + (size_t)nm * mb * nt + r0;
+                    p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;
+                }
+            }
+            for (int i = Dr; i >= 1; --i) {
+                const bool head = i == Dr;
+                GemmProb p = prob_dx(head ? Dr3 + r0 * 4 : ch("ws.Drf", i, Dr) + r0 * nrd.h[i], mb, head ? 1 : nrd.h[i],
+                                     W(L_(n, i)), nrd.h[i - 1], ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1],
+                                     ch("ws.Drf", i - 1, Dr) + r0 * nrd.h[i - 1], nrd.act[i - 1]);
+                if (head) p.lda = 4;
+                b[Dr - i].push_back(p);
+            }
+            for (int i = 0; i <= Dr; ++i) {
+                const bool head = i == Dr;
+                const float* X = i == 0 ? Xf + r0 * ldQ : ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1];
+                const int K = i == 0 ? S + A : nrd.h[i - 1];
+                wr.push_back(prob_dw(X, i == 0 ? ldQ : K, K, mb, head ? Dr3 + r0 * 4 : ch("ws.Drf", i, Dr) + r0 * nrd.h[i],
+                                     head ? 1 : nrd.h[i], W(L_(n, i)), nullptr, GRP_MODEL));
+                if (head) wr.back().ldb = 4;
+            }
         }
     }
     // the fit's own tile shapes (SACX_MTILE): its 2 x 200 rows want 16x16 forward / dX tiles
@@ -1634,30 +2106,38 @@ void build_model_plan(sacx_handle* h) {
     // residency (HC 2,372 -> 610 tiles), the rule of add_gemm at tile32 = 2.  2: the handle's.
     const int tile32_h = h->tile32;
     if (h->mtile != 2) h->tile32 = 0;
-    add_gemm(h, plan, "model.fwd0", f0, false);
-    if (gfold) {
-        Launch& F = plan.back();
-        if (F.gemm.t32 || F.gemm.dwl) { fprintf(stderr, "sacx: model.fwd0 gather needs 16x16 tiles\n"); abort(); }
-        F.gemm.rowk = 6;
-        F.gemm.mg = mg;
-        F.name = "model.gather+fwd0";
-        F.bytes += 4.0 * nm * mb * (2.0 * S + A + 1 + O);
-    }
-    {   // model.fwd1 on 32x32 tiles (mt32 bit 2) when it stays its own launch (no k_fwd2 pair)
+    auto has_head = [](const std::vector<GemmProb>& ps) {
+        for (const auto& p : ps)
+            if (p.mse) return true;
+        return false;
+    };
+    for (int i = 0; i <= Lf; ++i) {
+        const std::string name = "model.fwd" + std::to_string(i);
         const int t32_fit = h->tile32;
-        if (h->mtile == 1 && (h->mt32 & 2) && !(gfold && h->mfwd2 && S + A <= 32)) h->tile32 = 2;
-        add_gemm(h, plan, "model.fwd1", f1, false);
+        if (i == 0) {
+            add_gemm(h, plan, name, f[0], false);    // (<= SACX_MAX_MODELS problems: one launch)
+            if (gfold) {
+                Launch& F = plan.back();
+                if (F.gemm.t32 || F.gemm.dwl) { fprintf(stderr, "sacx: model.fwd0 gather needs 16x16 tiles\n"); abort(); }
+                F.gemm.rowk = 6;
+                F.gemm.mg = mg;
+                F.name = "model.gather+fwd0";
+                F.bytes += 4.0 * nm * mb * (2.0 * S + A + 1 + O);
+            }
+            continue;
+        }
+        if (!has_head(f[i])) {
+            // hidden levels on 32x32 tiles (mt32 bit 2) when not inside the k_fwd2 pair
+            if (h->mtile == 1 && (h->mt32 & 2) && !(i == 1 && gfold && h->mfwd2 && S + A <= 32)) h->tile32 = 2;
+        } else if (i == Lf && h->mtile == 1 && (h->mt32 & 8) && !h->gm && !h->srn) {
+            h->tile32 = 2;     // the heads (+ the MSE loss epilogue) on 32x32 tiles (mt32 bit 8; MSE heads only)
+        }
+        add_gemm_split(h, plan, name, f[i], false);
         h->tile32 = t32_fit;
+        // the gathered layer 0 and layer 1 as ONE k_fwd2 launch (SACX_MFWD2, default; K0 = S + A <= 32)
+        if (i == 1 && gfold && h->mfwd2) fuse_fwd2(h, plan, "model.gather+fwd01");
+        if (i == Lf && fuse) plan.back().name = "model.fwd" + std::to_string(i) + "+loss";
     }
-    // the gathered layer 0 and layer 1 as ONE k_fwd2 launch (SACX_MFWD2, default; K0 = S + A <= 32)
-    if (gfold && h->mfwd2) fuse_fwd2(h, plan, "model.gather+fwd01");
-    {   // model.fwd2 (+ the MSE loss epilogue) on 32x32 tiles (mt32 bit 8; MSE heads only)
-        const int t32_fit = h->tile32;
-        if (h->mtile == 1 && (h->mt32 & 8) && !h->gm && !h->srn) h->tile32 = 2;
-        add_gemm(h, plan, "model.fwd2", f2, false);
-        h->tile32 = t32_fit;
-    }
-    if (fuse) plan.back().name = "model.fwd2+loss";
     if (!fuse) {
         Launch L{};
         L.kind = Launch::MLOSS;
@@ -1676,43 +2156,47 @@ void build_model_plan(sacx_handle* h) {
     if (h->gm) {                       // the logstd gradient and Adam (or its store for the global-norm clip)
         mf.lgpart = W("ws.lgp"); mf.ntm = ntm; mf.S = S; mf.lscale = h->lscale ? 1 : 0;
         mf.gstore = h->cfg.model_max_grad_norm > 0.f ? 1 : 0;
-        for (int k = 0; k < nm; ++k) mf.logstd[k] = W("m" + std::to_string(k) + ".logstd");
+        mf.logstd = W("m0.logstd");
+        mf.lstride = nm > 1 ? (int64_t)(h->off_of("m1.logstd") - h->off_of("m0.logstd")) / 4 : 0;
+        for (int k = 1; k < nm; ++k)      // (build_layout gives every model the same block)
+            if ((int64_t)(h->off_of("m" + std::to_string(k) + ".logstd") - h->off_of("m0.logstd")) / 4 != k * mf.lstride) {
+                fprintf(stderr, "sacx: model parameter blocks differ\n");
+                abort();
+            }
     }
-    if (!bfold) {
-        const int t32_fit = h->tile32;   // model.bwd2 (+ k_mfinal's workgroup) on 32x32 tiles (mt32 bit 4)
-        if (h->mtile == 1 && (h->mt32 & 4)) h->tile32 = 2;
-        add_gemm(h, plan, "model.bwd2", b2, false);
+    for (int t = 0; t < Lf; ++t) {
+        const std::string name = "model.bwd" + std::to_string(Lf - t);
+        if (t == Lf - 1 && bfold) {      // model.bwd2 folded: model.bwd1 generates its A operand
+            add_gemm(h, plan, name, b[t], false);
+            Launch& B1 = plan.back();
+            if (B1.gemm.t32 || B1.gemm.dwl) { fprintf(stderr, "sacx: model.bwd1 generation needs 16x16 tiles\n"); abort(); }
+            B1.name = "model.bwd2+bwd1+final";
+            B1.gemm.rowk = 7;
+            B1.gemm.has_mfinal = 1;
+            B1.gemm.mfin = mf;
+            for (const GemmProb& q : b[0]) { B1.flops += gemm_flops(q); B1.bytes += gemm_bytes(q); }
+            continue;
+        }
+        if (t == 0 && bfold) continue;   // (in the launch above)
+        const int t32_fit = h->tile32;   // the heads' dX (+ k_mfinal's workgroup): mt32 bit 4; the others bit 1
+        if (h->mtile == 1 && (h->mt32 & (t == 0 ? 4 : 1))) h->tile32 = 2;
+        const size_t first = plan.size();
+        add_gemm_split(h, plan, name, b[t], false);
         h->tile32 = t32_fit;
-        if (fuse) {
-            Launch& B2 = plan.back();
-            B2.name = "model.bwd2+final";
+        if (t == 0 && fuse) {
+            Launch& B2 = plan[first];
+            B2.name += "+final";
             B2.gemm.has_mfinal = 1;
             B2.gemm.mfin = mf;
         }
     }
-    {   // model.bwd1 (K = H1) on 32x32 dX tiles (mt32 bit 1): half the operand re-reads of the
-        // 16x16 ones at the same k order (bit-identical)
-        const int t32_fit = h->tile32;
-        if (h->mtile == 1 && (h->mt32 & 1) && !bfold) h->tile32 = 2;
-        add_gemm(h, plan, "model.bwd1", b1, false);
-        h->tile32 = t32_fit;
-    }
-    if (bfold) {
-        Launch& B1 = plan.back();
-        if (B1.gemm.t32 || B1.gemm.dwl) { fprintf(stderr, "sacx: model.bwd1 generation needs 16x16 tiles\n"); abort(); }
-        B1.name = "model.bwd2+bwd1+final";
-        B1.gemm.rowk = 7;
-        B1.gemm.has_mfinal = 1;
-        B1.gemm.mfin = mf;
-        for (const GemmProb& q : b2) { B1.flops += gemm_flops(q); B1.bytes += gemm_bytes(q); }
-    }
     if (h->mtile == 1) h->tile32 = 2;
-    add_gemm(h, plan, "model.adam", w, false);
-    plan.back().gemm.t_adv = fuse ? 1 : 0;
-    const size_t n_adam = wr.empty() ? 1 : 2;
+    int n_adam = add_gemm_split(h, plan, "model.adam", w, false);
+    for (int j = 0; j < n_adam; ++j) plan[plan.size() - 1 - j].gemm.t_adv = fuse ? 1 : 0;
     if (!wr.empty()) {
-        add_gemm(h, plan, "reward.adam", wr, false);
-        plan.back().gemm.t_adv = 1;
+        const int nr = add_gemm_split(h, plan, "reward.adam", wr, false);
+        for (int j = 0; j < nr; ++j) plan[plan.size() - 1 - j].gemm.t_adv = 1;
+        n_adam += nr;
     }
     h->tile32 = tile32_h;
     for (Launch& L : plan)           // GaussianModel fits: the head epilogue has the 16x16 form only
@@ -1726,15 +2210,16 @@ void build_model_plan(sacx_handle* h) {
         // --model_max_grad_norm (mbrl_onpolicy_alg.py:315-317): the dW launches store the
         // gradients (+3 p_stride; GaussianModel's logstd gradient from mfit_final); their global
         // norm gives one scale; Adam applies g * scale over the models' whole contiguous range
-        for (size_t a = 0; a < n_adam; ++a) {
+        for (int a = 0; a < n_adam; ++a) {
             Launch& G = plan[plan.size() - 1 - a];
             for (int i = 0; i < G.gemm.nprob; ++i) G.gemm.probs[i].epi = EPI_STORE;
-            G.name = a + 1 == n_adam ? "model.grad" : "reward.grad";
+            const size_t at = G.name.find(".adam");
+            G.name = G.name.substr(0, at) + ".grad" + G.name.substr(at + 5);
         }
-        const AdamConsts gadam = plan[plan.size() - n_adam].gemm.adam;   // (plan grows below)
-        std::string last = "m" + std::to_string(nm - 1) + ".l2";
+        const AdamConsts gadam = adam_consts(h);
+        std::string last = L_("m" + std::to_string(nm - 1), Dm);
         if (h->gm) last = "m" + std::to_string(nm - 1) + ".logstd";
-        if (h->srn) last = "r" + std::to_string(nm - 1) + ".l2";
+        if (h->srn) last = L_("r" + std::to_string(nm - 1), Dr);
         const uint64_t o0 = h->off_of("m0.l0");
         const SegInfo& sl = h->seg(last);
         const int64_t n = (int64_t)((sl.off + (uint64_t)(sl.rows * sl.cols) * 4 - o0) / 4);
@@ -2384,69 +2869,104 @@ int sacx_create(const sacx_config* cfg, sacx_handle** out) {
     if (cfg->abi_version != SACX_ABI_VERSION) return bad("abi_version mismatch");
     if (cfg->seeds < 0 || cfg->seeds > 64) return bad("seeds must be in [0, 64]");
     if (cfg->s_dim <= 0 || cfg->a_dim <= 0 || cfg->a_dim > 32) return bad("s_dim/a_dim out of range (a_dim <= 32)");
-    if (cfg->hidden[0] <= 0 || cfg->hidden[1] <= 0) return bad("hidden sizes must be positive");
-    if (cfg->hidden[0] > 512 || cfg->hidden[1] > 512) return bad("hidden sizes > 512 unsupported (row kernels hold a row in 8 regs/lane)");
     if (cfg->activation < 0 || cfg->activation > 2) return bad("activation must be relu/tanh/elu");
     if (cfg->batch <= 0 || cfg->buffer_capacity <= 0) return bad("batch/buffer_capacity must be positive");
     if (cfg->buffer_capacity >= (int64_t(1) << 31)) return bad("buffer_capacity must be < 2^31");
+    if (cfg->num_models < 0 || cfg->num_models > SACX_MAX_MODELS) return bad("num_models must be in [1, 8] (0 -> 2)");
     if (cfg->use_expert) {
-        if (cfg->expert_batch <= 0 || ((cfg->expert_batch & 1) && cfg->num_models != 1))
-            return bad("expert_batch must be positive and even with 2 models (SAC_expert.py:329-332 adds equal halves)");
+        const int nmc = cfg->num_models > 0 ? cfg->num_models : 2;
+        if (cfg->expert_batch <= 0) return bad("expert_batch must be positive");
+        // the expert term adds model 0's and model 1's rows elementwise (SAC_expert.py:329-332): the
+        // first two sections of np.array_split(perm, num_models) must hold the same number of rows
+        if (nmc == 2 && (cfg->expert_batch & 1))
+            return bad("expert_batch must be even with 2 models (SAC_expert.py:329-332 adds equal halves)");
+        if (nmc > 2 && cfg->expert_batch % nmc == 1)
+            return bad("expert_batch % num_models == 1: the two array_split sections of the expert term differ in length");
+        if (nmc >= 2 && cfg->expert_batch < nmc) return bad("expert_batch < num_models");
         if (cfg->expert_capacity < cfg->expert_batch) return bad("expert_capacity < expert_batch");
-        if (cfg->model_hidden[0] <= 0 || cfg->model_hidden[1] <= 0) return bad("model sizes must be positive");
-        if (cfg->model_hidden[0] > 512 || cfg->model_hidden[1] > 512) return bad("model hidden sizes > 512 unsupported");
         if (cfg->model_activation < 0 || cfg->model_activation > 2) return bad("model activation invalid");
         if (cfg->s_dim + 1 > 512) return bad("s_dim > 511 unsupported by the model MSE head");
-        if (cfg->separate_reward_nn) {
-            const int r0 = cfg->reward_hidden[0] > 0 ? cfg->reward_hidden[0] : 512;
-            const int r1 = cfg->reward_hidden[1] > 0 ? cfg->reward_hidden[1] : 512;
-            if (r0 > 512 || r1 > 512) return bad("reward hidden sizes > 512 unsupported");
-            for (int l = 0; l < 2; ++l)
-                if (cfg->reward_act_layers[l] < 0 || cfg->reward_act_layers[l] > 2)
-                    return bad("reward activations must be relu/tanh/elu");
-        }
     }
-    if (cfg->critic_hidden[0] < 0 || cfg->critic_hidden[1] < 0 || cfg->critic_hidden[0] > 512 ||
-        cfg->critic_hidden[1] > 512)
-        return bad("critic hidden sizes must be in [1, 512] (0: the actor's)");
-    if (cfg->num_models < 0 || cfg->num_models > 2) return bad("num_models must be 1 or 2 (0 -> 2)");
+    for (int n = 0; n < 4; ++n)
+        if (cfg->net_depth[n] < 0 || cfg->net_depth[n] > SACX_MAX_DEPTH) return bad("net_depth must be in [0, 4]");
     if (cfg->act_per_layer)
         for (int n = 0; n < 3; ++n)
             for (int l = 0; l < 2; ++l)
                 if (cfg->act_layers[n][l] < 0 || cfg->act_layers[n][l] > 2) return bad("act_layers must be relu/tanh/elu");
+    // every net's hidden layers: the ABI-8 lists, or the two of the older fields
+    NetDims nd[4];
+    {
+        const int leg_w[4][2] = {{cfg->hidden[0], cfg->hidden[1]},
+                                 {cfg->critic_hidden[0] > 0 ? cfg->critic_hidden[0] : cfg->hidden[0],
+                                  cfg->critic_hidden[1] > 0 ? cfg->critic_hidden[1] : cfg->hidden[1]},
+                                 {cfg->model_hidden[0], cfg->model_hidden[1]},
+                                 {cfg->reward_hidden[0] > 0 ? cfg->reward_hidden[0] : 512,
+                                  cfg->reward_hidden[1] > 0 ? cfg->reward_hidden[1] : 512}};
+        for (int n = 0; n < 4; ++n) {
+            if (cfg->net_depth[n] > 0) {
+                for (int l = 0; l < cfg->net_depth[n]; ++l) {
+                    nd[n].h.push_back(cfg->net_hidden[n][l]);
+                    nd[n].act.push_back(cfg->net_acts[n][l]);
+                }
+                continue;
+            }
+            for (int l = 0; l < 2; ++l) {
+                nd[n].h.push_back(leg_w[n][l]);
+                int a = n == 3 ? cfg->reward_act_layers[l]
+                               : cfg->act_per_layer ? cfg->act_layers[n][l] : (n == 2 ? cfg->model_activation : cfg->activation);
+                nd[n].act.push_back(a);
+            }
+        }
+        const bool used[4] = {true, true, cfg->use_expert != 0, cfg->use_expert && cfg->separate_reward_nn};
+        for (int n = 0; n < 4; ++n) {
+            if (!used[n]) continue;
+            for (int l = 0; l < nd[n].D(); ++l) {
+                if (nd[n].h[l] <= 0 || nd[n].h[l] > 512)
+                    return bad("hidden sizes must be in [1, 512] (row kernels hold a row in 8 regs/lane)");
+                if (nd[n].act[l] < 0 || nd[n].act[l] > 2) return bad("activations must be relu/tanh/elu");
+            }
+        }
+    }
     if (cfg->actor_gaussian && cfg->actor_std_mult < 0.f) return bad("actor_std_mult must be positive");
     auto* h = new sacx_handle();
     h->cfg = *cfg;
     h->S = cfg->s_dim;
     h->A = cfg->a_dim;
-    h->H0 = cfg->hidden[0];
-    h->H1 = cfg->hidden[1];
-    h->Hc0 = cfg->critic_hidden[0] > 0 ? cfg->critic_hidden[0] : h->H0;   // --critic_layers (nn_utils.py:86-138)
-    h->Hc1 = cfg->critic_hidden[1] > 0 ? cfg->critic_hidden[1] : h->H1;
+    for (int n = 0; n < 4; ++n) h->nd[n] = nd[n];
+    // the first and the last hidden layer of each net (one layer: both the same)
+    h->H0 = nd[0].h.front();
+    h->H1 = nd[0].h.back();
+    h->Hc0 = nd[1].h.front();   // --critic_layers (nn_utils.py:86-138)
+    h->Hc1 = nd[1].h.back();
     h->B = cfg->batch;
     h->cap = cfg->buffer_capacity;
-    for (int l = 0; l < 2; ++l) {           // per-layer activations, or the one of each net
-        h->aact[l] = cfg->act_per_layer ? cfg->act_layers[0][l] : cfg->activation;
-        h->cact[l] = cfg->act_per_layer ? cfg->act_layers[1][l] : cfg->activation;
-        h->macts[l] = cfg->act_per_layer ? cfg->act_layers[2][l] : cfg->model_activation;
-    }
+    h->aact[0] = nd[0].act.front(); h->aact[1] = nd[0].act.back();
+    h->cact[0] = nd[1].act.front(); h->cact[1] = nd[1].act.back();
+    h->macts[0] = nd[2].act.front(); h->macts[1] = nd[2].act.back();
     h->Aout = cfg->per_state_std ? 2 * h->A : h->A;
-    h->ne = cfg->use_expert ? cfg->expert_batch : 0;
+    h->nm = cfg->use_expert ? (cfg->num_models > 0 ? cfg->num_models : 2) : 0;
+    h->ne_perm = cfg->use_expert ? cfg->expert_batch : 0;
+    // the update's expert rows: every row with one model, else the first two array_split sections
+    // (each ceil(ne / nm) rows here: their lengths agree, checked above)
+    h->ne = h->nm <= 1 ? h->ne_perm : 2 * ((h->ne_perm + h->nm - 1) / h->nm);
     h->ecap = cfg->use_expert ? cfg->expert_capacity : 0;
-    h->Hm0 = cfg->use_expert ? cfg->model_hidden[0] : 0;
-    h->Hm1 = cfg->use_expert ? cfg->model_hidden[1] : 0;
+    h->Hm0 = cfg->use_expert ? nd[2].h.front() : 0;
+    h->Hm1 = cfg->use_expert ? nd[2].h.back() : 0;
     h->gm = cfg->use_expert && cfg->gaussian_model;
     h->lscale = h->gm && cfg->scale_model_loss;
     h->srn = cfg->use_expert && cfg->separate_reward_nn;
     h->Om = h->srn ? h->S : h->S + 1;
     if (h->srn) {
-        h->Hr0 = cfg->reward_hidden[0] > 0 ? cfg->reward_hidden[0] : 512;
-        h->Hr1 = cfg->reward_hidden[1] > 0 ? cfg->reward_hidden[1] : 512;
-        h->racts[0] = cfg->reward_act_layers[0];
-        h->racts[1] = cfg->reward_act_layers[1];
+        h->Hr0 = nd[3].h.front();
+        h->Hr1 = nd[3].h.back();
+        h->racts[0] = nd[3].act.front();
+        h->racts[1] = nd[3].act.back();
     }
+    // the fused plans are built for two hidden layers per net; any other depth takes the generic
+    // plans (SACX_GENERIC=1 forces them at two layers too: their parity test)
+    h->deep = nd[0].D() != 2 || nd[1].D() != 2 || (cfg->use_expert && nd[2].D() != 2) || (h->srn && nd[3].D() != 2);
+    if (const char* e = std::getenv("SACX_GENERIC")) h->deep = h->deep || std::atoi(e) != 0;
     h->mb = cfg->use_expert ? (cfg->model_batch > 0 ? cfg->model_batch : 200) : 0;
-    h->nm = cfg->use_expert ? (cfg->num_models > 0 ? cfg->num_models : 2) : 0;
     h->ln = cfg->actor_layer_norm != 0;
     h->ldS = (int)r4(h->S);
     h->ldQ = (int)r4(h->S + h->A);
@@ -2588,9 +3108,10 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (h->dp_ranks > 0) {
         if (h->cfg.use_expert) return fail(h, "data-parallel mode covers plain SAC (use_expert = 0)");
         const int64_t d = (int64_t)(h->off_of("t0.l0") - h->off_of("q0.l0"));
-        for (const char* l : {".l0", ".l1", ".l2"})
+        for (int l = 0; l <= h->nd[1].D(); ++l)
             for (int k = 0; k < 2; ++k)
-                if ((int64_t)(h->off_of("t" + std::to_string(k) + l) - h->off_of("q" + std::to_string(k) + l)) != d)
+                if ((int64_t)(h->off_of("t" + std::to_string(k) + ".l" + std::to_string(l)) -
+                              h->off_of("q" + std::to_string(k) + ".l" + std::to_string(l))) != d)
                     return fail(h, "internal: target layout is not a fixed shift of the critics");
     }
     // the weight shadows feed the update plans' 32x32 bf16 forward tiles; the Adam epilogues
@@ -2599,7 +3120,8 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     h->wbf_live = h->wbf_attach;
     for (int sl = 0; sl < h->nslot; ++sl) {
         h->abf_written.clear();
-        build_plan(h, sl, sl == 0);
+        if (h->deep) build_plan_generic(h, sl, sl == 0);
+        else build_plan(h, sl, sl == 0);
     }
     h->abf_written.clear();
     h->wbf_attach = false;
@@ -2882,7 +3404,7 @@ static ActRowArgs act_rows_args(sacx_handle* h, const float* obs, float* noise, 
 static int actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out,
                      uint32_t* done);
 static bool act_rows_ok(const sacx_handle* h, int64_t n) {
-    return n > 0 && n <= ACT_ROWS_MAX && !h->ln && h->S <= ACT_ROWS_DIM && h->H0 <= ACT_ROWS_DIM &&
+    return n > 0 && n <= ACT_ROWS_MAX && !h->ln && h->nd[0].D() == 2 && h->S <= ACT_ROWS_DIM && h->H0 <= ACT_ROWS_DIM &&
            h->H1 <= ACT_ROWS_DIM && h->Aout <= 64;
 }
 
@@ -2968,8 +3490,10 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
     if (!h || !h->bound) return fail(h, "not bound");
     if (n <= 0 || !obs || !act_out) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, K = h->seeds;
-    if (n > ACT_ROWS_MAX || h->ln || S > ACT_ROWS_DIM || h->H0 > ACT_ROWS_DIM || h->H1 > ACT_ROWS_DIM || h->Aout > 64)
-        return fail(h, "sacx_actor_act_host_seeds: n <= 16 rows per seed, no layer norm (use per-seed calls)");
+    if (n > ACT_ROWS_MAX || h->ln || h->nd[0].D() != 2 || S > ACT_ROWS_DIM || h->H0 > ACT_ROWS_DIM ||
+        h->H1 > ACT_ROWS_DIM || h->Aout > 64)
+        return fail(h, "sacx_actor_act_host_seeds: n <= 16 rows per seed, two hidden layers, no layer norm "
+                       "(use per-seed calls)");
     const int64_t tot = (int64_t)K * n;
     if (tot * (S + A) > STAGE_CAP) return fail(h, "rows exceed the pinned staging buffer (act per seed)");
     if (stage_alloc(h)) return -1;
@@ -3029,7 +3553,7 @@ int sacx_expert_set(sacx_handle* h, const float* s_e, const float* sp_e, int32_t
     if (!h || !h->bound) return fail(h, "not bound");
     if (settle(h)) return -1;             // alpha.final reads the epsilon this sets
     if (!h->cfg.use_expert) return fail(h, "handle was created without use_expert");
-    if (n != h->ne) return fail(h, "expert rows must equal expert_batch");
+    if (n != h->ne_perm) return fail(h, "expert rows must equal expert_batch");
     const size_t bytes = sizeof(float) * (size_t)n * h->S;
     HIPCHK(h, hipMemcpyAsync(h->f("expert.s"), s_e, bytes, hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(h->f("expert.sp"), sp_e, bytes, hipMemcpyDeviceToDevice, h->stream));
@@ -3049,7 +3573,8 @@ int sacx_perm_push(sacx_handle* h, const int32_t* perms, int64_t n_steps) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     for (int64_t j = 0; j < n_steps; ++j) {
         const int64_t slot = (h->seq_host + j) % h->perm_cap;
-        HIPCHK(h, hipMemcpy(ring + slot * h->ne, perms + j * h->ne, sizeof(int32_t) * h->ne, hipMemcpyHostToDevice));
+        HIPCHK(h, hipMemcpy(ring + slot * h->ne_perm, perms + j * h->ne_perm, sizeof(int32_t) * h->ne_perm,
+                            hipMemcpyHostToDevice));
     }
     return 0;
 }
@@ -3315,22 +3840,35 @@ int sacx_profile(sacx_handle* h, int64_t n_steps, double* ms_per_launch, int32_t
     return 0;
 }
 
-// The actor's hidden layers on m rows of X (row stride ldX) into H1b [m, H0] and H2b [m, H1]:
-// Dense + activation, or with --actor_layer_norm Dense -> LayerNorm -> tanh on layer 0
-// (nn_utils.py:110-119).  Eager launches on st (or captured by the caller).
-static void actor_hidden(sacx_handle* h, const float* X, int ldX, int m, float* H1b, float* H2b, hipStream_t st) {
-    std::vector<Launch> pl;
-    add_gemm(h, pl, "a.fwd0", {prob_fwd(X, ldX, m, h->S, h->f("actor.l0"), h->H0, H1b, h->ln ? ACT_NONE : h->aact[0])},
-             false);
-    add_gemm(h, pl, "a.fwd1", {prob_fwd(H1b, h->H0, m, h->H0, h->f("actor.l1"), h->H1, H2b, h->aact[1])}, false);
-    h->probs_cursor -= 2;          // host table bookkeeping of add_gemm (these launches are not in a plan)
-    launch_gemm(pl[0].gemm, st);
-    if (h->ln) {
-        LNArgs a{};
-        a.mode = 0; a.H = h->H0; a.Z = H1b; a.nrange = 1; a.r[1] = m; a.gamma = h->f("actor.ln");
-        launch_ln(a, st);
+// The hidden layers of net `net` (nd: its widths / activations) on m rows of X (row stride ldX, K0
+// inputs), alternating between H1b and H2b (layer 0 -> H1b, layer 1 -> H2b, ...); returns the
+// buffer holding the last hidden layer.  The actor's --actor_layer_norm puts Dense -> LayerNorm ->
+// tanh on layer 0 (nn_utils.py:110-119).  Eager launches on st (or captured by the caller).
+static float* net_hidden(sacx_handle* h, const std::string& net, const NetDims& nd, const float* X, int ldX, int K0,
+                         int m, float* H1b, float* H2b, hipStream_t st, bool ln = false) {
+    const float* in = X;
+    int ld = ldX, K = K0;
+    float* out = H1b;
+    for (int i = 0; i < nd.D(); ++i) {
+        out = (i & 1) ? H2b : H1b;
+        std::vector<Launch> pl;
+        add_gemm(h, pl, net + ".fwd", {prob_fwd(in, ld, m, K, h->f(net + ".l" + std::to_string(i)), nd.h[i], out,
+                                                (i == 0 && ln) ? ACT_NONE : nd.act[i])}, false);
+        h->probs_cursor -= 1;      // host table bookkeeping of add_gemm (these launches are not in a plan)
+        launch_gemm(pl[0].gemm, st);
+        if (i == 0 && ln) {
+            LNArgs a{};
+            a.mode = 0; a.H = nd.h[0]; a.Z = out; a.nrange = 1; a.r[1] = m; a.gamma = h->f("actor.ln");
+            launch_ln(a, st);
+        }
+        in = out;
+        ld = K = nd.h[i];
     }
-    launch_gemm(pl[1].gemm, st);
+    return out;
+}
+
+static float* actor_hidden(sacx_handle* h, const float* X, int ldX, int m, float* H1b, float* H2b, hipStream_t st) {
+    return net_hidden(h, "actor", h->nd[0], X, ldX, h->S, m, H1b, H2b, st, h->ln);
 }
 
 static int actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out,
@@ -3373,9 +3911,9 @@ static int actor_act(sacx_handle* h, const float* obs, int64_t n, int32_t determ
             launch_rng(r, h->stream);
         }
         launch_obs_norm(obs + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
-        actor_hidden(h, W("act.X"), ldS, m, W("act.H1"), W("act.H2"), h->stream);
         HeadArgs a{};
-        a.H2 = W("act.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H2 = actor_hidden(h, W("act.X"), ldS, m, W("act.H1"), W("act.H2"), h->stream);
+        a.ldh = H1; a.W3 = W(actor_head_name(h)); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         a.nseg = 1;
@@ -3424,9 +3962,9 @@ int sacx_actor_evaluate(sacx_handle* h, const float* s, int64_t n, float* pi_out
         r.slot = -1; r.reset_seq = 0; r.nupd = 1;
         launch_rng(r, h->stream);
         launch_obs_norm(s + done * S, m, S, W("norm.s_mean"), W("norm.s_den"), W("act.X"), ldS, h->stream);
-        actor_hidden(h, W("act.X"), ldS, m, W("act.H1"), W("act.H2"), h->stream);
         HeadArgs a{};
-        a.H2 = W("act.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H2 = actor_hidden(h, W("act.X"), ldS, m, W("act.H1"), W("act.H2"), h->stream);
+        a.ldh = H1; a.W3 = W(actor_head_name(h)); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = h->ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         a.nseg = 1;
@@ -3446,7 +3984,7 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
     if (settle(h)) return -1;
     if (net < 0 || net > 3) return fail(h, "net must be 0..3 (q0, q1, t0, t1)");
     if (n < 0 || (n > 0 && (!s || !a || !out))) return fail(h, "bad arguments");
-    const int S = h->S, A = h->A, H0 = h->Hc0, H1 = h->Hc1, ldQ = h->ldQ;   // the critics' sizes
+    const int S = h->S, A = h->A, H1 = h->Hc1, ldQ = h->ldQ;   // the critics' sizes
     auto W = [&](const std::string& nm) { return h->f(nm); };
     static const char* names[4] = {"q0", "q1", "t0", "t1"};
     const std::string nm = names[net];
@@ -3455,14 +3993,12 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
         NetIOArgs g = netio_base(h);
         g.mode = 0; g.n = m; g.ldX = ldQ; g.s = s + done * S; g.a = a + done * A; g.X = W("act.Xq");
         launch_net_io(g, h->stream);
+        float* Hl = net_hidden(h, nm, h->nd[1], W("act.Xq"), ldQ, S + A, m, W("act.H1"), W("act.H2"), h->stream);
         std::vector<Launch> pl;
-        add_gemm(h, pl, "critic.fwd0", {prob_fwd(W("act.Xq"), ldQ, m, S + A, W(nm + ".l0"), H0, W("act.H1"), h->cact[0])},
-                 false);
-        add_gemm(h, pl, "critic.fwd1", {prob_fwd(W("act.H1"), H0, m, H0, W(nm + ".l1"), H1, W("act.H2"), h->cact[1])},
-                 false);
-        add_gemm(h, pl, "critic.fwd2", {prob_fwd(W("act.H2"), H1, m, H1, W(nm + ".l2"), 1, W("act.Q"), ACT_NONE)}, false);
-        for (auto& L : pl) launch_gemm(L.gemm, h->stream);
-        h->probs_cursor -= 3;
+        add_gemm(h, pl, "critic.head", {prob_fwd(Hl, H1, m, H1, W(nm + ".l" + std::to_string(h->nd[1].D())), 1, W("act.Q"),
+                                                 ACT_NONE)}, false);
+        launch_gemm(pl[0].gemm, h->stream);
+        h->probs_cursor -= 1;
         g.mode = 1; g.O = W("act.Q"); g.ldO = 1; g.value = value ? 1 : 0; g.out0 = out + done;
         launch_net_io(g, h->stream);
     }
@@ -3476,36 +4012,55 @@ int sacx_critic_forward(sacx_handle* h, int32_t net, const float* s, const float
 // start at row k * rstride of M1 / M2 / O / R1 / R2 (nk models on the same inputs: the diagnostics)
 static void model_gemms(sacx_handle* h, const std::vector<int>& models, int m, int64_t rstride, hipStream_t st,
                         const char* tag) {
-    const int S = h->S, A = h->A, ldQ = h->ldQ, Hm0 = h->Hm0, Hm1 = h->Hm1, O = S + 1;
+    const int S = h->S, A = h->A, ldQ = h->ldQ, O = S + 1;
     auto W = [&](const std::string& nm) { return h->f(nm); };
-    std::vector<GemmProb> p0, p1, p2;
-    for (size_t i = 0; i < models.size(); ++i) {
-        const std::string mn = "m" + std::to_string(models[i]);
-        float* M1 = W("roll.M1") + (size_t)i * rstride * Hm0;
-        float* M2 = W("roll.M2") + (size_t)i * rstride * Hm1;
-        float* Oo = W("roll.O") + (size_t)i * rstride * O;
-        p0.push_back(prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(mn + ".l0"), Hm0, M1, h->macts[0]));
-        p1.push_back(prob_fwd(M1, Hm0, m, Hm0, W(mn + ".l1"), Hm1, M2, h->macts[1]));
-        p2.push_back(prob_fwd(M2, Hm1, m, Hm1, W(mn + ".l2"), h->Om, Oo, ACT_NONE));
-        p2.back().ldc = O;
-        if (h->srn) {
-            const std::string rn = "r" + std::to_string(models[i]);
-            const int Hr0 = h->Hr0, Hr1 = h->Hr1;
-            float* R1 = W("roll.R1") + (size_t)i * rstride * Hr0;
-            float* R2 = W("roll.R2") + (size_t)i * rstride * Hr1;
-            p0.push_back(prob_fwd(W("roll.Xm"), ldQ, m, S + A, W(rn + ".l0"), Hr0, R1, h->racts[0]));
-            p1.push_back(prob_fwd(R1, Hr0, m, Hr0, W(rn + ".l1"), Hr1, R2, h->racts[1]));
-            p2.push_back(prob_fwd(R2, Hr1, m, Hr1, W(rn + ".l2"), 1, Oo + S, ACT_NONE));
-            p2.back().ldc = O;
+    const NetDims& nmd = h->nd[2];
+    const NetDims& nrd = h->nd[3];
+    const int Dm = nmd.D(), Dr = h->srn ? nrd.D() : 0, Lf = std::max(Dm, Dr);
+    // the hidden layers alternate between the two buffers of each net (layer 0 -> M1 / R1, layer 1 ->
+    // M2 / R2, ...): their row stride is the layer's width, so model i's rows start at i * rstride * width
+    auto hb = [&](const char* b1, const char* b2, int i, int w, size_t mi) {
+        return W((i & 1) ? b2 : b1) + mi * rstride * w;
+    };
+    std::vector<std::vector<GemmProb>> lv(Lf + 1);
+    for (size_t mi = 0; mi < models.size(); ++mi) {
+        const std::string mn = "m" + std::to_string(models[mi]);
+        float* Oo = W("roll.O") + mi * rstride * O;
+        for (int i = 0; i <= Dm; ++i) {
+            const float* in = i == 0 ? W("roll.Xm") : hb("roll.M1", "roll.M2", i - 1, nmd.h[i - 1], mi);
+            const int K = i == 0 ? S + A : nmd.h[i - 1];
+            if (i < Dm) {
+                lv[i].push_back(prob_fwd(in, i == 0 ? ldQ : K, m, K, W(mn + ".l" + std::to_string(i)), nmd.h[i],
+                                         hb("roll.M1", "roll.M2", i, nmd.h[i], mi), nmd.act[i]));
+            } else {
+                lv[i].push_back(prob_fwd(in, K, m, K, W(mn + ".l" + std::to_string(i)), h->Om, Oo, ACT_NONE));
+                lv[i].back().ldc = O;
+            }
+        }
+        if (h->srn) {     // the reward net into roll.O's reward column (base_world_model.py:72-74)
+            const std::string rn = "r" + std::to_string(models[mi]);
+            for (int i = 0; i <= Dr; ++i) {
+                const float* in = i == 0 ? W("roll.Xm") : hb("roll.R1", "roll.R2", i - 1, nrd.h[i - 1], mi);
+                const int K = i == 0 ? S + A : nrd.h[i - 1];
+                if (i < Dr) {
+                    lv[i].push_back(prob_fwd(in, i == 0 ? ldQ : K, m, K, W(rn + ".l" + std::to_string(i)), nrd.h[i],
+                                             hb("roll.R1", "roll.R2", i, nrd.h[i], mi), nrd.act[i]));
+                } else {
+                    lv[i].push_back(prob_fwd(in, K, m, K, W(rn + ".l" + std::to_string(i)), 1, Oo + S, ACT_NONE));
+                    lv[i].back().ldc = O;
+                }
+            }
         }
     }
     std::vector<Launch> pl;
     const std::string t(tag);
-    add_gemm(h, pl, t + ".fwd0", p0, false);
-    add_gemm(h, pl, t + ".fwd1", p1, false);
-    add_gemm(h, pl, t + ".fwd2", p2, false);
+    int np = 0;
+    for (int i = 0; i <= Lf; ++i) {
+        add_gemm_split(h, pl, t + ".fwd" + std::to_string(i), lv[i], false);
+        np += (int)lv[i].size();
+    }
     for (auto& L : pl) launch_gemm(L.gemm, st);
-    h->probs_cursor -= (int)(p0.size() + p1.size() + p2.size());   // add_gemm's table (not a plan)
+    h->probs_cursor -= np;   // add_gemm's table (not a plan)
 }
 
 // the model net on rows [c0, c0 + m) of (s, a): roll.Xm -> roll.M1 -> roll.M2 -> roll.O
@@ -3626,10 +4181,9 @@ static void enqueue_rollout(sacx_handle* h, int32_t model, const float* s_init, 
                 r.slot = -1; r.reset_seq = 0; r.nupd = 1;
                 launch_rng(r, st);
             }
-            actor_hidden(h, W("roll.X"), ldS, m, W("roll.H1"), W("roll.H2"), st);
-            std::vector<Launch> pl;
             HeadArgs a{};
-            a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+            a.H2 = actor_hidden(h, W("roll.X"), ldS, m, W("roll.H1"), W("roll.H2"), st);
+            a.ldh = H1; a.W3 = W(actor_head_name(h)); a.logstd = W("actor.logstd");
             a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
             a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
             a.ma_mean = W("mnorm.a_mean"); a.ma_den = W("mnorm.a_den");
@@ -3698,9 +4252,9 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
                      int32_t flags, float delta_clip, float* out) {
     if (!h || !h->bound) return fail(h, "not bound");
     if (!h->cfg.use_expert) return fail(h, "expert diagnostics need the world models (use_expert)");
-    if (n <= 0 || n > ROLL_CAP / 2) return fail(h, "expert rows must be in [1, 2048]");
+    if (n <= 0 || n > 2048) return fail(h, "expert rows must be in [1, 2048]");
     const bool disc = (flags & SACX_DIAG_DISC) != 0, ea = (flags & SACX_DIAG_EXPERT_ACTIONS) != 0;
-    if (disc && h->nm < 2) return fail(h, "_calc_disc compares two world models (num_models = 2)");
+    if (disc && h->nm < 2) return fail(h, "_calc_disc compares two world models (num_models >= 2)");
     if (!s_e || !sp_e || !out || (ea && !a_e) || (!disc && !a_e)) return fail(h, "null argument");
     if (settle(h)) return -1;
     const int S = h->S, A = h->A, H1 = h->H1, ldS = h->ldS, ldQ = h->ldQ;
@@ -3712,9 +4266,14 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     d.ms_mean = W("mnorm.s_mean"); d.ms_den = W("mnorm.s_den");             // the models'
     d.a_mean = W("mnorm.a_mean"); d.a_den = W("mnorm.a_den");
     d.d_mean = W("mnorm.d_mean"); d.d_den = W("mnorm.d_den"); d.clip_d = delta_clip; d.out = out;
-    // both models on the same n input rows: model k's rows land at [k n, (k+1) n)
-    // (one model: its MSE twice, the mean is exact)
-    auto models = [&]() { model_gemms(h, {0, h->nm > 1 ? 1 : 0}, n, n, h->stream, "diag.m"); };
+    // every model on the same n input rows: model k's rows land at [k n, (k+1) n)
+    // (one model: its MSE twice, the mean is exact); _calc_disc reads models 0 and 1
+    std::vector<int> all;
+    for (int k = 0; k < std::max(2, h->nm); ++k) all.push_back(h->nm > 1 ? k : 0);
+    d.nmod = (int)all.size();
+    auto models = [&](bool two) {
+        model_gemms(h, two ? std::vector<int>{0, 1} : all, n, n, h->stream, "diag.m");
+    };
     // actor.sample(s_e, deterministic=False) (continuous_actors.py:270-306) into the action columns
     auto counterfactual = [&]() {
         RngArgs r{};
@@ -3722,9 +4281,9 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
         r.n_int = 0; r.n_norm = n * A; r.out_idx = nullptr; r.out_norm = W("roll.noise");
         r.slot = -1; r.reset_seq = 0; r.nupd = 1;
         launch_rng(r, h->stream);
-        actor_hidden(h, W("roll.X"), ldS, n, W("roll.H1"), W("roll.H2"), h->stream);
         HeadArgs a{};
-        a.H2 = W("roll.H2"); a.ldh = H1; a.W3 = W("actor.l2"); a.logstd = W("actor.logstd");
+        a.H2 = actor_hidden(h, W("roll.X"), ldS, n, W("roll.H1"), W("roll.H2"), h->stream);
+        a.ldh = H1; a.W3 = W(actor_head_name(h)); a.logstd = W("actor.logstd");
         a.H1 = H1; a.A = A; a.Aout = h->Aout; a.S = S; a.ldQ = ldQ; a.per_state_std = h->cfg.per_state_std;
         a.lim = h->cfg.act_limit; a.a_mean = W("norm.a_mean"); a.a_den = W("norm.a_den");
         a.ma_mean = W("mnorm.a_mean"); a.ma_den = W("mnorm.a_den");
@@ -3740,9 +4299,9 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
     launch_diag(d, h->stream);
     if (disc) {                      // _calc_disc (SAC_expert.py:427-460)
         if (!ea) counterfactual();
-        models();
-        if (h->gm) {                 // model.sample(deterministic=False): model 0's (n, S), then model 1's
-            model_noise_draw(h, 2 * (int64_t)n, 0, h->stream);
+        models(true);
+        if (h->gm) {                 // model.sample(deterministic=False): (n, S) for every model in order
+            model_noise_draw(h, (int64_t)h->nm * n, 0, h->stream);
             d.mlogstd[0] = W("m0.logstd");
             d.mlogstd[1] = W("m1.logstd");
             d.mnoise = W("roll.mnoise");
@@ -3750,12 +4309,12 @@ int sacx_expert_diag(sacx_handle* h, const float* s_e, const float* a_e, const f
         d.mode = 3;
         launch_diag(d, h->stream);
     } else {                         // SAC_expert.py:579-608
-        models();
+        models(false);
         d.mode = 1;
         launch_diag(d, h->stream);
         if (!ea) {
             counterfactual();
-            models();
+            models(false);
         }
         d.mode = 2;                  // use_expert_actions: the counterfactual MSE is the data MSE
         launch_diag(d, h->stream);

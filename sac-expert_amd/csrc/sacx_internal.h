@@ -13,6 +13,7 @@ enum Act { ACT_RELU = 0, ACT_TANH = 1, ACT_ELU = 2, ACT_NONE = 3 };
 // ahead of the updates that consume them (and an update's alpha rows are read one update
 // later by the folded launches); the ring holds at least two batches (sacx_handle::nslot)
 #define NBATCH_MAX 8
+#define MAX_MODELS 8        // world models (--num_models, sacx.h SACX_MAX_MODELS)
 #define NSLOT 32
 #define CTL_WORDS 48
 
@@ -342,7 +343,8 @@ struct MFinalArgs {
     // advanced step, or (gstore, --model_max_grad_norm) the gradient stored at +3 p_stride for the
     // global-norm clip; ds = mean(exp(2 logstd)) with lscale, else 1
     const float* lgpart; int32_t ntm, S, lscale, gstore;
-    float* logstd[2];
+    float* logstd;          // model 0's; model k's at + k * lstride floats (equal per-model parameter blocks)
+    int64_t lstride;
 };
 
 #define GEMM_MAXP 8
@@ -527,6 +529,7 @@ struct GatherArgs {
     float* Xq;  float* Xt; float* Xp; float* Xm; int32_t ldQ;
     float* r; float* d;
     const float* exp_s; const float* exp_sp; const int32_t* perm_ring; int32_t perm_cap;
+    int32_t perm_ld;            // permutation length (expert_batch; ne = the rows used, <= perm_ld)
     float* se_raw; float* spe_raw;
     // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
@@ -705,6 +708,7 @@ struct DiagArgs {
     // mode 3 (_calc_disc, deterministic=False) with GaussianModels: model k's delta_n gets
     // exp(mlogstd[k]) * mnoise[(k n + i) * S + j] (null: MSEModel)
     const float* mlogstd[2]; const float* mnoise;
+    int32_t nmod;               // modes 1 / 2: models whose outputs O holds (rows [k n, (k+1) n)), 2 .. MAX_MODELS
 };
 
 // sacx_actor_act on a few rows (the env loop's one observation): one workgroup per row runs

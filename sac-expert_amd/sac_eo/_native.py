@@ -11,7 +11,9 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SACX_LIBPATH") or os.path.join(os.path.dirname(_HERE), "lib", "libsacx.so")
 
-SACX_ABI_VERSION = 7
+SACX_ABI_VERSION = 8
+MAX_DEPTH = 4                   # SACX_MAX_DEPTH: hidden layers per net
+MAX_MODELS = 8                  # SACX_MAX_MODELS: --num_models
 STAGE_FLOATS = 65536            # SACX_STAGE_FLOATS (include/sacx.h)
 ACT = {"relu": 0, "tanh": 1, "elu": 2}
 DTYPES = {0: "f32", 1: "i32", 2: "i64", 3: "u32", 4: "f64"}
@@ -87,6 +89,10 @@ class Config(ctypes.Structure):
         ("reward_hidden", ctypes.c_int32 * 2),
         ("reward_act_layers", ctypes.c_int32 * 2),
         ("critic_hidden", ctypes.c_int32 * 2),
+        # ABI 8: every net's hidden layers [actor, critics, world models, reward nets] (0: the fields above)
+        ("net_depth", ctypes.c_int32 * 4),
+        ("net_hidden", (ctypes.c_int32 * 4) * 4),
+        ("net_acts", (ctypes.c_int32 * 4) * 4),
     ]
 
 

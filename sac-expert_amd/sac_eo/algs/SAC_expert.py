@@ -28,8 +28,10 @@ class SAC_exp(SACBase):
 
     def __init__(self, idx, env, env_eval, env_expert, actor, expert, init_expert_rms_stats, v_critic, q_targets,
                  q_critics, models, alg_kwargs, mf_update_kwargs):
-        if len(models) not in (1, 2):
-            raise ValueError("SAC-EO uses one or two world models (SAC_expert.py:271-336)")
+        if not 1 <= len(models) <= 8:
+            # every model is fitted (mbrl_onpolicy_alg.py:305-319); the expert term uses the first two
+            # array_split sections and models 0 / 1 (SAC_expert.py:297-336)
+            raise ValueError("SAC-EO runs 1 to 8 world models on the device")
         super().__init__(idx, env, env_eval, actor, v_critic, q_targets, q_critics, models, alg_kwargs,
                          mf_update_kwargs)
         if self.env_buffer_size:

@@ -127,9 +127,9 @@ class SACBase:
     def _engine_config(self, k):
         if not getattr(self.actor, "squash", False):
             raise ValueError("SAC trains the squashed Gaussian actor (--actor_squash)")
+        # --actor_layers / --critic_layers / --model_layers / --reward_layers of any length up to 4
+        # (create_nn, nn_utils.py:100-138); other than two, the engine runs its generic plans
         hidden, chidden = self.actor.layers, self.q_critics[0].layers
-        if len(hidden) != 2 or len(chidden) != 2:
-            raise NotImplementedError("the device engine runs 2 hidden layers per net (--actor_layers / --critic_layers)")
         cfg = EngineConfig(
             s_dim=self.s_dim, a_dim=self.a_dim, hidden=tuple(hidden), activation=self.actor.activation,
             critic_hidden=tuple(chidden),
@@ -157,8 +157,6 @@ class SACBase:
             cfg.scale_model_loss = bool(m.scale_model_loss) and cfg.gaussian_model   # GaussianModel only (:122-127)
             cfg.separate_reward_nn = bool(m.separate_reward_nn)
             if cfg.separate_reward_nn:
-                if len(m.reward_layers) != 2:
-                    raise NotImplementedError("the device reward net runs 2 hidden layers (--reward_layers)")
                 cfg.reward_hidden = tuple(m.reward_layers)
                 cfg.reward_activations = tuple(m.reward_activations)
         return cfg

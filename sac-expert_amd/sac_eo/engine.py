@@ -29,7 +29,7 @@ CTL = {"t_sac": 0, "t_model": 1, "num_timesteps": 2, "ts_increment": 3, "cur_siz
 class EngineConfig:
     s_dim: int
     a_dim: int
-    hidden: Sequence[int] = (256, 256)       # --actor_layers (and the critics' unless critic_hidden)
+    hidden: Sequence[int] = (256, 256)       # --actor_layers (and the critics' unless critic_hidden); 1-4 layers
     activation: str = "relu"
     critic_hidden: Optional[Sequence[int]] = None   # --critic_layers when they differ from the actor's
     batch: int = 256
@@ -63,7 +63,7 @@ class EngineConfig:
     actor_std_mult: float = 1.0
     actor_output_norm: bool = False
     actor_layer_norm: bool = False  # Dense -> LayerNorm -> tanh on the actor's layer 0
-    num_models: int = 2             # SAC-EO world models (1 or 2)
+    num_models: int = 2             # SAC-EO world models (1 .. 8; the expert term uses models 0 and 1)
     model_max_grad_norm: float = 0.0    # <= 0: None
     delta_clip_loss: float = 0.0        # <= 0: None
     reward_clip_loss: float = 0.0       # <= 0: None
@@ -82,15 +82,43 @@ class EngineConfig:
     reward_hidden: Sequence[int] = (512, 512)
     reward_activations: Optional[Sequence[str]] = None
 
+    @staticmethod
+    def _acts(lst, dflt: str, depth: int, what: str) -> List[str]:
+        """create_activations (nn_utils.py:5-22): one name for every layer, or one per layer."""
+        lst = list(lst) if lst is not None else [dflt]
+        lst = lst * depth if len(lst) == 1 else lst
+        if len(lst) != depth:                               # create_nn's assert (nn_utils.py:106-107)
+            raise ValueError(f"{what}: activations must be list of length len(layers) ({depth})")
+        return lst
+
+    def nets(self):
+        """[(hidden widths, activation names)] of the actor, the critics, the world models and the
+        reward nets (create_nn's layers / activations lists, nn_utils.py:86-138)."""
+        hid = [tuple(self.hidden), tuple(self.critic_hidden if self.critic_hidden is not None else self.hidden),
+               tuple(self.model_hidden), tuple(self.reward_hidden)]
+        acts = [self._acts(self.actor_activations, self.activation, len(hid[0]), "actor"),
+                self._acts(self.critic_activations, self.activation, len(hid[1]), "critic"),
+                self._acts(self.model_activations, self.model_activation, len(hid[2]), "model"),
+                self._acts(self.reward_activations, "relu", len(hid[3]), "reward")]
+        return list(zip(hid, acts))
+
     def to_c(self) -> N.Config:
         c = N.Config()
         c.abi_version = N.SACX_ABI_VERSION
         c.s_dim, c.a_dim = int(self.s_dim), int(self.a_dim)
-        c.hidden[0], c.hidden[1] = int(self.hidden[0]), int(self.hidden[1])
+        nets = self.nets()
+        for n, (hid, acts) in enumerate(nets):
+            if not 1 <= len(hid) <= N.MAX_DEPTH:
+                raise NotImplementedError(f"the device nets run 1 to {N.MAX_DEPTH} hidden layers (got {list(hid)})")
+            # ABI 8: every layer of every net (the legacy two-layer fields below stay filled as well)
+            c.net_depth[n] = len(hid)
+            for l, (w, a) in enumerate(zip(hid, acts)):
+                c.net_hidden[n][l] = int(w)
+                c.net_acts[n][l] = N.ACT[a]
+        two = lambda x: (list(x) + list(x))[:2]             # the legacy fields of a net (any depth: unused)
+        c.hidden[0], c.hidden[1] = [int(x) for x in two(self.hidden)]
         if self.critic_hidden is not None:
-            if len(self.critic_hidden) != 2:
-                raise NotImplementedError("the device critics run 2 hidden layers (--critic_layers)")
-            c.critic_hidden[0], c.critic_hidden[1] = int(self.critic_hidden[0]), int(self.critic_hidden[1])
+            c.critic_hidden[0], c.critic_hidden[1] = [int(x) for x in two(self.critic_hidden)]
         c.activation = N.ACT[self.activation]
         c.batch = int(self.batch)
         c.buffer_capacity = int(self.buffer_capacity)
@@ -98,7 +126,7 @@ class EngineConfig:
         c.use_expert = int(bool(self.use_expert))
         c.expert_capacity = int(self.expert_capacity)
         c.expert_batch = int(self.expert_batch)
-        c.model_hidden[0], c.model_hidden[1] = int(self.model_hidden[0]), int(self.model_hidden[1])
+        c.model_hidden[0], c.model_hidden[1] = [int(x) for x in two(self.model_hidden)]
         c.model_activation = N.ACT[self.model_activation]
         c.model_batch = int(self.model_batch)
         c.target_update_int = int(self.target_update_int)
@@ -119,32 +147,24 @@ class EngineConfig:
         c.actor_std_mult = float(self.actor_std_mult)
         c.actor_output_norm = int(bool(self.actor_output_norm))
         c.actor_layer_norm = int(bool(self.actor_layer_norm))
+        if not 1 <= int(self.num_models) <= N.MAX_MODELS:
+            raise ValueError(f"num_models must be in [1, {N.MAX_MODELS}]")
         c.num_models = int(self.num_models)
         c.model_max_grad_norm = float(self.model_max_grad_norm or 0.0)
         c.delta_clip_loss = float(self.delta_clip_loss or 0.0)
         c.reward_clip_loss = float(self.reward_clip_loss or 0.0)
         c.delta_clip_pred = float(self.delta_clip_pred or 0.0)
-        lists = (self.actor_activations, self.critic_activations, self.model_activations)
-        if any(x is not None for x in lists):
-            c.act_per_layer = 1
-            for n, (lst, dflt) in enumerate(zip(lists, (self.activation, self.activation, self.model_activation))):
-                lst = list(lst) if lst is not None else [dflt]
-                lst = lst * 2 if len(lst) == 1 else lst          # nn_utils.py:7-8: one name for all layers
-                if len(lst) != 2:
-                    raise ValueError("two hidden layers: one or two activation names per net")
-                c.act_layers[n][0], c.act_layers[n][1] = N.ACT[lst[0]], N.ACT[lst[1]]
+        c.act_per_layer = 1
+        for n in range(3):
+            a2 = two(nets[n][1])
+            c.act_layers[n][0], c.act_layers[n][1] = N.ACT[a2[0]], N.ACT[a2[1]]
         c.gaussian_model = int(bool(self.gaussian_model))
         c.scale_model_loss = int(bool(self.scale_model_loss))
         c.separate_reward_nn = int(bool(self.separate_reward_nn))
         if self.separate_reward_nn:
-            if len(self.reward_hidden) != 2:
-                raise NotImplementedError("the reward net runs 2 hidden layers (--reward_layers)")
-            c.reward_hidden[0], c.reward_hidden[1] = int(self.reward_hidden[0]), int(self.reward_hidden[1])
-            lst = list(self.reward_activations or ["relu"])
-            lst = lst * 2 if len(lst) == 1 else lst
-            if len(lst) != 2:
-                raise ValueError("two hidden layers: one or two reward activation names")
-            c.reward_act_layers[0], c.reward_act_layers[1] = N.ACT[lst[0]], N.ACT[lst[1]]
+            c.reward_hidden[0], c.reward_hidden[1] = [int(x) for x in two(self.reward_hidden)]
+            a2 = two(nets[3][1])
+            c.reward_act_layers[0], c.reward_act_layers[1] = N.ACT[a2[0]], N.ACT[a2[1]]
         return c
 
 
@@ -285,7 +305,11 @@ class Engine:
 
     # ------------------------------------------------------------------ weights
     def _layers(self, net: str) -> List[torch.Tensor]:
-        return [self.v[f"{net}.l{i}"] for i in range(3)]
+        """The Dense layers l0 .. l<D> of `net` (D hidden layers, then the output head)."""
+        out = []
+        while f"{net}.l{len(out)}" in self._v:
+            out.append(self.v[f"{net}.l{len(out)}"])
+        return out
 
     def set_net(self, net: str, weights: Sequence[np.ndarray]):
         """Keras get_weights() list [W0, b0, W1, b1, W2, b2] -> W_ext views; the actor with
@@ -447,12 +471,20 @@ class Engine:
     def act_host_seeds(self, obs, deterministic: bool = True) -> np.ndarray:
         """act_host for EVERY seed of a packed handle in one launch chain: obs [seeds, n, S]
         (or [seeds, S]) -> actions [seeds, n, A] (or [seeds, A]); each seed draws from its own
-        stream (sacx_actor_act_host_seeds)."""
+        stream (sacx_actor_act_host_seeds).  Actors the one-launch rows kernel does not cover
+        (layer norm, other than two hidden layers) act seed by seed."""
         S, A, K = self.cfg.s_dim, self.cfg.a_dim, self.seeds
         o = np.ascontiguousarray(np.asarray(obs, np.float32))
         one = o.ndim == 2
         o = o.reshape(K, -1, S)
         out = np.empty((K, o.shape[1], A), dtype=np.float32)
+        if self.cfg.actor_layer_norm or len(self.cfg.hidden) != 2 or o.shape[1] > 16:
+            sel = self.seed_index
+            for k in range(K):
+                self.select_seed(k)
+                out[k] = self.act_host(o[k], deterministic)
+            self.select_seed(sel)
+            return out[:, 0] if one else out
         N.check(self.lib.sacx_actor_act_host_seeds(self.h, o.ctypes.data, int(o.shape[1]), int(bool(deterministic)),
                                                    out.ctypes.data), self.h, "actor_act_host_seeds")
         return out[:, 0] if one else out
@@ -570,7 +602,8 @@ class Engine:
         s0, sp0 = self._dev(s_e, (-1, S)), self._dev(sp_e, (-1, S))
         n = int(s0.shape[0])
         a0 = self._dev(a_e, (n, A)) if a_e is not None else None
-        out = torch.zeros(3 + n if disc else 6, dtype=torch.float32, device=self.device)
+        nmod = max(2, int(self.cfg.num_models or 2))       # every model (one model: twice)
+        out = torch.zeros(3 + n if disc else 2 + 2 * nmod, dtype=torch.float32, device=self.device)
         flags = (N.DIAG_DISC if disc else 0) | (N.DIAG_EXPERT_ACTIONS if use_expert_actions else 0)
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None
         N.check(self.lib.sacx_expert_diag(self.h, p(s0), p(a0), p(sp0), n, flags, float(delta_clip or 0.0),
@@ -580,7 +613,8 @@ class Engine:
             return dict(s_disc_total=float(o[0]), max_disc=float(o[1]), median_disc=float(o[2]),
                         disc_ratio=o[3:].copy())
         return dict(mse_expert_data=float(o[0]), mse_counterfactual=float(o[1]),
-                    mse_expert_data_per_model=o[2:4].copy(), mse_counterfactual_per_model=o[4:6].copy())
+                    mse_expert_data_per_model=o[2:2 + nmod].copy(),
+                    mse_counterfactual_per_model=o[2 + nmod:2 + 2 * nmod].copy())
 
     # ------------------------------------------------------------------ snapshot (F4)
     def _state_ranges(self):

@@ -31,7 +31,7 @@ def nontrivial_normalizers(rs, S, A):
 def make_learner(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, per_state_std=False,
                  use_expert=False, ne=20, model_hidden=(512, 512), normalizers="identity", done_p=0.0,
                  bias_scale=0.05, actor_gain=0.5, epsilon=0.1, layer_norm=False, actor_acts=None, critic_acts=None,
-                 wm=None):
+                 wm=None, num_models=2):
     """The seeded inputs of one learner: (oracle_cfg, oracle_state_f32, buffer, normalizers, expert).
     ``wm``: world-model variant flags (gaussian_model, scale_model_loss, separate_reward_nn,
     reward_hidden, reward_act) of O.Config."""
@@ -39,7 +39,7 @@ def make_learner(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0
     ocfg = O.Config(S=S, A=A, hidden=hidden, act=act, B=B, per_state_std=per_state_std,
                     critic_hidden=wm.pop("critic_hidden", None),
                     model_hidden=model_hidden, epsilon=epsilon, layer_norm=layer_norm, actor_acts=actor_acts,
-                    critic_acts=critic_acts, **wm)
+                    critic_acts=critic_acts, num_models=num_models, **wm)
     st = O.init_state(ocfg, seed=seed + 1, with_models=use_expert, bias_scale=bias_scale,
                       actor_gain=actor_gain, model_gain=0.3, model_std_mult=0.7, reward_gain=0.3)
     rs = np.random.RandomState(seed + 100)
@@ -62,7 +62,7 @@ def load_learner(eng, st, buf, nrm, expert, epsilon):
         eng.set_net(f"q{k}", st.q[k])
         eng.set_net(f"t{k}", st.q_targ[k])
     if expert is not None:
-        for k in range(2):
+        for k in range(len(st.models)):
             if f"m{k}.l0" in eng.segments:      # --num_models 1: model 0 only
                 eng.set_net(f"m{k}", st.models[k])
                 if st.model_logstd is not None:
@@ -85,7 +85,7 @@ def make_pair(S=17, A=6, hidden=(256, 256), B=256, act="relu", N=5000, seed=0, p
     from sac_eo.engine import Engine, EngineConfig
     ocfg, st, buf, nrm, expert = make_learner(S, A, hidden, B, act, N, seed, per_state_std, use_expert, ne,
                                               model_hidden, normalizers, done_p, bias_scale, actor_gain, epsilon,
-                                              layer_norm, actor_acts, critic_acts, wm)
+                                              layer_norm, actor_acts, critic_acts, wm, ekw.get("num_models", 2))
     if wm:                                 # the oracle's world-model flags -> the engine's
         ekw = dict(ekw, gaussian_model=ocfg.gaussian_model, scale_model_loss=ocfg.scale_model_loss,
                    separate_reward_nn=ocfg.separate_reward_nn, reward_hidden=tuple(ocfg.reward_hidden),

@@ -29,7 +29,7 @@ def test_struct_layouts():
     from sac_eo import _native as N
     # offsets fixed by include/sacx.h (natural alignment)
     assert N.Config.buffer_capacity.offset == 32
-    assert ctypes.sizeof(N.Config) == 248          # gcc: sizeof(sacx_config) (ABI 7)
+    assert ctypes.sizeof(N.Config) == 392          # gcc: sizeof(sacx_config) (ABI 8)
     assert N.Config.gaussian_model.offset == 208 and N.Config.reward_hidden.offset == 220
     assert N.Config.reward_act_layers.offset == 228 and N.Config.critic_hidden.offset == 236
     assert N.Config.act_per_layer.offset == 172 and N.Config.act_layers.offset == 176

@@ -117,11 +117,13 @@ def _run(alg, flags, shape=SMALL, act="relu", fp32_envelope=False):
     """The device loop and the fp64 oracle loop from the same start; returns everything compared."""
     alg_obj, d, ak, total, oenvs, rs_state = _build(alg, flags, shape=shape, act=act)
     S, A = alg_obj.s_dim, alg_obj.a_dim
-    H, MH = shape["hidden"], shape["model_hidden"]
     mk, msk = d["model_kwargs"], d["model_setup_kwargs"]
-    ocfg = O.Config(S=S, A=A, hidden=(H, H), act=act, B=shape["B"], gamma=ak["gamma"], tau=ak["soft_tau"],
-                    lr_q=ak["q_crit_lr"], lr_pi=ak["mbpo_actor_lr"], lr_alpha=ak["mbpo_alpha_lr"],
-                    init_temperature=ak["init_temperature"], epsilon=ak["epsilon"], model_hidden=(MH, MH),
+    # the parsed layer lists (a flag given again in `flags` replaces the shape's: nargs='+')
+    ocfg = O.Config(S=S, A=A, hidden=tuple(d["actor_kwargs"]["actor_layers"]), act=act, B=shape["B"], gamma=ak["gamma"],
+                    tau=ak["soft_tau"], lr_q=ak["q_crit_lr"], lr_pi=ak["mbpo_actor_lr"], lr_alpha=ak["mbpo_alpha_lr"],
+                    init_temperature=ak["init_temperature"], epsilon=ak["epsilon"],
+                    model_hidden=tuple(mk["model_layers"]), num_models=int(mk["num_models"]),
+                    layer_norm=bool(d["actor_kwargs"].get("actor_layer_norm", False)),
                     model_act="relu", lr_model=ak["model_lr"], reward_loss_coef=msk["reward_loss_coef"],
                     gaussian_model=bool(mk["gaussian_model"]),
                     scale_model_loss=bool(msk["scale_model_loss"]) and bool(mk["gaussian_model"]),
@@ -221,6 +223,16 @@ def _check_stream_and_diag(alg, flags, alg_obj, ak, name, dev_rng, orc, tol=LOSS
     ("sac", ["--update_normalizers", "--s_noise_std", "0.5"]),
     ("sac", ["--critic_layers", "96", "48"]),                 # critics wider / narrower than the actor
     ("sac_imit", ["--critic_layers", "40", "72"]),
+    # round 6: nets of any depth (create_nn's layers list, nn_utils.py:100-138) and more world models
+    ("sac", ["--actor_layers", "256", "256", "256"]),
+    ("sac", ["--critic_layers", "400", "300", "200"]),
+    ("sac_imit", ["--model_layers", "200", "200", "200"]),
+    ("sac_imit", ["--actor_layers", "64"]),
+    ("sac", ["--critic_layers", "96", "--actor_layers", "48", "80", "64", "32"]),
+    ("sac_imit", ["--num_models", "3"]),
+    ("sac_imit", ["--num_models", "4", "--gaussian_model", "--model_layers", "48", "64", "48"]),
+    ("sac_imit", ["--separate_reward_nn", "--reward_layers", "48", "32", "40", "--model_layers", "64"]),
+    ("sac", ["--actor_layer_norm", "--actor_layers", "64", "48", "64"]),
 ])
 def test_train_loop_matches_oracle(gpu_available, alg, flags):
     alg_obj, ak, name, dev, dev_rng, orc, ref, _ = _run(alg, flags)
