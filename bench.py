@@ -115,8 +115,10 @@ def build_engine(cfgd, seeds, device, dp=None, batch=None, weight_seed=None):
 
 def pmc_traffic(kernel, config):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this config
-    (tools/pmc_summary.py over tools/gpu_pmc.sh output: 2 x FETCH_SIZE + WRITE_SIZE,
-    the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md section HBM), or None."""
+    (tools/pmc_summary.py over tools/gpu_pmc.sh output: f x FETCH_SIZE + WRITE_SIZE, with the
+    fetch factor f calibrated per access shape -- 2 for coalesced streaming reads, the gfx950
+    correction of MI355X_MICROARCH.md section HBM, but 1 for k_gemm's MFMA-fragment loads,
+    profiles/r03_fetch_calib_v1.txt; pmc_<config>.json records the factor per kernel), or None."""
     path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
     try:
         with open(path) as fh:

@@ -3742,7 +3742,58 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
         if (chunk > first)
             HIPCHK(h, hipMemcpy(ring, idx + (done + first) * R2, sizeof(int32_t) * R2 * (chunk - first),
                                 hipMemcpyHostToDevice));
-        if (flags & SACX_STEP_EAGER) {
+        const char* kdump = std::getenv("SACX_MFIT_KTIME");
+        if ((flags & SACX_STEP_EAGER) && kdump) {
+            // diagnostics: per-workgroup start / end stamps of every GEMM launch of each step, appended
+            // to <file> as one line per launch and step: name, workgroups, span, mean / max workgroup,
+            // last-start offset, gap to the previous launch's end (us)
+            std::vector<int> nwg;
+            int64_t tot = 0;
+            for (const Launch& L : mplan) {
+                const int n = L.kind == Launch::GEMM ? L.grid + (L.gemm.has_mfinal ? 1 : 0) : 0;
+                nwg.push_back(n);
+                tot += 2 * n;
+            }
+            uint64_t* kb = nullptr;
+            HIPCHK(h, hipMalloc(&kb, sizeof(uint64_t) * std::max<int64_t>(1, tot)));
+            std::vector<uint64_t> host((size_t)std::max<int64_t>(1, tot));
+            FILE* f = std::fopen(kdump, "a");
+            for (int64_t j = 0; j < chunk; ++j) {
+                HIPCHK(h, hipMemsetAsync(kb, 0, sizeof(uint64_t) * std::max<int64_t>(1, tot), h->stream));
+                int64_t o = 0;
+                for (size_t i = 0; i < mplan.size(); ++i) {
+                    Launch C = mplan[i];
+                    if (nwg[i] > 0) {
+                        C.gemm.ktime = kb + o;
+                        o += 2 * nwg[i];
+                    }
+                    enqueue(C, h, h->stream);
+                }
+                HIPCHK(h, hipStreamSynchronize(h->stream));
+                HIPCHK(h, hipMemcpy(host.data(), kb, sizeof(uint64_t) * host.size(), hipMemcpyDeviceToHost));
+                o = 0;
+                uint64_t prev = 0;
+                for (size_t i = 0; f && i < mplan.size(); ++i) {
+                    if (nwg[i] == 0) continue;
+                    uint64_t lo = UINT64_MAX, hi = 0, ls = 0, wmax = 0;
+                    double wsum = 0.0;
+                    int cnt = 0;
+                    for (int b = 0; b < nwg[i]; ++b) {
+                        const uint64_t t0 = host[o + 2 * b], t1 = host[o + 2 * b + 1];
+                        if (t0 == 0 || t1 == 0) continue;           // (workgroups that return early stamp nothing)
+                        lo = std::min(lo, t0); hi = std::max(hi, t1); ls = std::max(ls, t0);
+                        wmax = std::max(wmax, t1 - t0); wsum += (double)(t1 - t0); ++cnt;
+                    }
+                    std::fprintf(f, "%s,%d,%.2f,%.2f,%.2f,%.2f,%.2f\n", mplan[i].name.c_str(), cnt, (hi - lo) * 0.01,
+                                 wsum / std::max(1, cnt) * 0.01, wmax * 0.01, (ls - lo) * 0.01,
+                                 prev ? ((double)lo - (double)prev) * 0.01 : 0.0);
+                    prev = hi;
+                    o += 2 * nwg[i];
+                }
+            }
+            if (f) std::fclose(f);
+            (void)hipFree(kb);
+        } else if (flags & SACX_STEP_EAGER) {
             for (int64_t j = 0; j < chunk; ++j)
                 for (const Launch& L : mplan) enqueue(L, h, h->stream);
             HIPCHK(h, hipGetLastError());

@@ -74,6 +74,9 @@ for step in "$@"; do
         python tools/trace_view.py "$f" 24 "k_mgather,k_gemm<0, 1, 6,k_gemm<0, 0, 6" > "$OUT/$n-mtrace_$cfg.txt" 2>&1; cat "$OUT/$n-mtrace_$cfg.txt"
       fi
       echo "[$n mtrace $cfg] rc=$rc" ;;
+    mktime)     # per-launch workgroup timing of the fit (eager steps, SACX_MFIT_KTIME): mktime=<config>
+      timeout -k 10 200 python tools/mfit_ktime.py ${arg:-hc_eo} > "$log" 2>&1
+      rc=$?; echo "[$n mktime ${arg:-hc_eo}] rc=$rc"; cat "$log" | grep -v amdgpu.ids ;;
     mprof)      # rocprofv3 kernel-trace stats of the HC model fit (graph replay only) -> profiles r*_mfit_hc_kernel_stats
       MFT_GRAPH_ONLY=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/mprof" -o m \
           -- python tools/model_fit_time.py hc_eo 2048 > "$log" 2>&1
