@@ -201,7 +201,7 @@ class LoopOracle:
         dt = self.dt
         n = nrm.cast(dt)
         x = ((np.asarray(s, dt) - n.s_mean) / n.s_den)[None]
-        out, _ = O.mlp_forward(params, x, self.cfg.aacts)
+        out, _ = O.actor_forward(params, x, self.cfg)            # (Dense -> LayerNorm -> tanh with the norm)
         mu, lraw = O.split_head(out, np.asarray(logstd, dt), self.cfg)
         u = np.zeros_like(mu) if deterministic else O.f32_noise(self.rs.normal(size=mu.shape)).astype(dt)
         a, _ = O.head_sample(mu, lraw, u, self.cfg.act_limit, dt)
