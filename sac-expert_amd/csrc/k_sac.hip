@@ -972,6 +972,20 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
 #ifndef SACX_T32_DW_NS
 #define SACX_T32_DW_NS 1   // the same for the dW + Adam tiles (uncapped registers)
 #endif
+// SACX_T32_STAMP (diagnostic builds): a 32x32 dW + Adam workgroup's end stamp is taken after phase P
+// instead -- 1: its epilogue operands (P, m, v, T) have arrived, 2: its main-loop MFMAs are done,
+// 3: the K-quarter reduction is in LDS (k_gemm skips its own end stamp for these launches)
+#ifndef SACX_T32_STAMP
+#define SACX_T32_STAMP 0
+#endif
+#define T32_STAMP(P, ...)                                                                   \
+    do {                                                                                     \
+        if (MODE == GM_DW && SACX_T32_STAMP == (P) && ga.ktime != nullptr) {                 \
+            asm volatile("" ::__VA_ARGS__);                                                  \
+            __syncthreads();                                                                 \
+            if (threadIdx.x == 0) ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                    \
+    } while (0)
 template <int MODE, int VEC, bool BF, bool PART = false, bool MSE = false>
 __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& g, int lt, int64_t so,
                                             float (&red)[16][4][64]) {
@@ -1011,6 +1025,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
     }
     EpiScalars es{};
     if constexpr (MODE == GM_DW || MSE) es = epi_scalars(sr(ga.ctl, so), g.group);
+    T32_STAMP(1, "v"(e0[0]), "v"(e1[1]), "v"(e2[2]), "v"(e3[3]));
 
     const int nIt = (g.K + 15) >> 4;
     const int per = (nIt + 3) >> 2;
@@ -1171,6 +1186,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
     } else {
         main_loop(std::false_type{});
     }
+    T32_STAMP(2, "v"(acc0[0]), "v"(acc1[3]));
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
         const floatx4 acc = acc0[s] + acc1[s];
@@ -1178,6 +1194,7 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         for (int q = 0; q < 4; ++q) red[wave * 4 + s][q][lane] = acc[q];
     }
     __syncthreads();
+    T32_STAMP(3, "v"(red[0][0][lane]));
 
     const int L = ((row >> 2) << 4) | col, R = row & 3;
     // the Polyak gate once per workgroup, as a scalar (a per-lane 64-bit modulo per sub-tile
@@ -1912,7 +1929,9 @@ __global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(uint32_t h0, uint32_
 #endif
     gemm_core<MODE, VEC, ROWK, NQ, BF, PK, T32>(KHdr{{h0, h1, h2, h3}}, ga);
     GEMM_PH(4);
-    if (ga.ktime != nullptr) {
+    if (SACX_T32_STAMP && T32 && MODE == GM_DW) {   // (diagnostic: the phase stamp is the end stamp)
+        if (ga.ktime != nullptr && threadIdx.x == 0) ga.ktime[2 * ktime_wg()] = t0;
+    } else if (ga.ktime != nullptr) {
         __syncthreads();
         if (threadIdx.x == 0) {
             ga.ktime[2 * ktime_wg()] = t0;
@@ -2754,6 +2773,9 @@ void launch_gemm(const GemmArgs& a, hipStream_t s) {
         } else if (a.rowk == 6) {   // the world-model fit's gather + two layers (16 waves, H0 <= 512)
             if (a.vec) hipLaunchKernelGGL((k_fwd2<1, 16, false, 0, 512, true>), grid2, dim3(1024), 0, s, b);
             else hipLaunchKernelGGL((k_fwd2<0, 16, false, 0, 512, true>), grid2, dim3(1024), 0, s, b);
+        } else if (a.rowk == 9) {   // the fit's two layers on pre-gathered rows (16 waves, H0 <= 512)
+            if (a.vec) hipLaunchKernelGGL((k_fwd2<1, 16, false, 0, 512, false>), grid2, dim3(1024), 0, s, b);
+            else hipLaunchKernelGGL((k_fwd2<0, 16, false, 0, 512, false>), grid2, dim3(1024), 0, s, b);
         } else {
             if (a.vec) hipLaunchKernelGGL((k_fwd2<1, SACX_FWD2_NW, false>), grid2, block, 0, s, b);
             else hipLaunchKernelGGL((k_fwd2<0, SACX_FWD2_NW, false>), grid2, block, 0, s, b);
@@ -5314,17 +5336,22 @@ namespace sacx {
 __global__ __launch_bounds__(256) void k_mgather(MGatherArgs g) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
-    if (row >= g.nm * g.mb) return;
+    const int R2 = g.nm * g.mb;
+    if (row >= R2) return;
     const int S = g.S, A = g.A;
-    const int64_t slot = g.ctl->mfit_seq % g.idx_cap;
-    const int64_t li = g.idx_ring[slot * g.nm * g.mb + row];
+    // one step (grid y = 1), or step j = blockIdx.y of a pre-gathered block into staging slot j
+    const int j = (int)blockIdx.y;
+    float* X = g.X + (size_t)j * R2 * g.ldQ;
+    float* T = g.T + (size_t)j * R2 * (S + 1);
+    const int64_t slot = (g.ctl->mfit_seq + j) % g.idx_cap;
+    const int64_t li = g.idx_ring[slot * R2 + row];
     const int64_t phys = (g.ctl->start + li) % g.cap;
     const float* rec = g.replay + phys * (int64_t)g.stride;
     for (int c = lane; c < g.ldQ; c += 64) {
         float x = 0.f;
         if (c < S) x = (rec[c] - g.s_mean[c]) / g.s_den[c];
         else if (c < S + A) x = (rec[c] - g.a_mean[c - S]) / g.a_den[c - S];
-        g.X[(size_t)row * g.ldQ + c] = x;
+        X[(size_t)row * g.ldQ + c] = x;
     }
     for (int c = lane; c <= S; c += 64) {
         float y;
@@ -5332,7 +5359,7 @@ __global__ __launch_bounds__(256) void k_mgather(MGatherArgs g) {
         else y = (rec[2 * S + A] - g.r_norm[0]) / g.r_norm[1];
         const float cl = c < S ? g.clip_d : g.clip_r;
         if (cl > 0.f) y = fminf(fmaxf(y, -cl), cl);
-        g.T[(size_t)row * (S + 1) + c] = y;
+        T[(size_t)row * (S + 1) + c] = y;
     }
 }
 
@@ -5360,8 +5387,8 @@ __global__ __launch_bounds__(256) void k_mloss(MLossArgs g) {
 
 __global__ __launch_bounds__(64) void k_mfinal(MFinalArgs f) { mfit_final(f); }
 
-void launch_mgather(const MGatherArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL(k_mgather, dim3((a.nm * a.mb + 3) / 4), dim3(256), 0, s, a);
+void launch_mgather(const MGatherArgs& a, hipStream_t s, int nsteps) {
+    hipLaunchKernelGGL(k_mgather, dim3((a.nm * a.mb + 3) / 4, std::max(1, nsteps)), dim3(256), 0, s, a);
 }
 void launch_mloss(const MLossArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_mloss, dim3((a.nm * a.mb + 3) / 4), dim3(256), 0, s, a);

@@ -83,6 +83,7 @@ struct Launch {
     float* ar_buf = nullptr;   // ALLREDUCE: in-place sum over the data-parallel ranks
     int64_t ar_count = 0;
     int grid = 0, block = 256;
+    int pre_steps = 0;         // MGATHER: > 0 the pre-gather of that many fit steps (launch_mgather)
     double flops = 0, bytes = 0;
     int gemm_first = 0;  // index of the first problem in the host table (GEMM)
     bool after_final = false;  // graph: waits for the previous update's alpha branch
@@ -201,6 +202,8 @@ struct sacx_handle {
     int xcd_map = 1;          // GEMM tiles XCD-contiguous (xcd_tile)
     int afin = 1;             // k_fwd2's folded alpha finalisation split over q.head's rows (SACX_AFIN; 0: ticket)
     int mfwd2 = 1;            // the fit's gather + model.fwd0 + model.fwd1 as one k_fwd2 launch (SACX_MFWD2)
+    int mpre = 1;             // the fit's minibatch rows pre-gathered for a block of steps (SACX_MPRE): the
+                              // steps read the staging slots mfit.Xs / mfit.Ts instead of gathering on load
     // data-parallel mode (sacx_dp_init): each rank's local-batch gradients are summed over
     // dp_ranks by RCCL inside the update graph, then every rank applies the same Adam
     int dp_ranks = 0, dp_rank = 0;
@@ -209,6 +212,7 @@ struct sacx_handle {
     bool nccl_failed = false;
     // world-model fitting, per seed (packed seeds fit one seed at a time: its arena block's plan)
     std::vector<std::vector<Launch>> mplans;
+    std::vector<Launch> mpres;   // per seed: the pre-gather launch of its fit plan (kind RNG: none)
     std::vector<std::map<int, hipGraphExec_t>> mgraphs;   // per seed: fit steps per graph -> graph
     std::vector<int64_t> mfit_hosts;   // model steps issued per seed (mirror ctl->mfit_seq)
     std::vector<GemmProb> probs;
@@ -317,6 +321,7 @@ bool spec_mode(const sacx_handle* h) {
 
 constexpr int ACT_CAP = 1024;   // rows per sacx_actor_act launch chain
 constexpr int MFIT_GRAPH = 64;      // model-fit steps per captured graph (then 8, then 1)
+static_assert(MFIT_GRAPH <= MFIT_PRE, "a fit graph's steps fit one pre-gather block");
 constexpr int STAGE_CAP = SACX_STAGE_FLOATS;   // floats in the pinned host staging buffer of the _host entry points
 constexpr int ROLL_CAP = 4096;  // trajectories per sacx_rollout launch chain
 
@@ -583,6 +588,8 @@ void build_layout(sacx_handle* h) {
         h->add("mstats", h->stats_cap, 2, F, SACX_ROLE_STATE);
         h->add("ws.Xf", R2, h->ldQ, F, 0);
         h->add("ws.Tf", R2, O, F, 0);
+        h->add("mfit.Xs", MFIT_PRE, (int64_t)R2 * h->ldQ, F, 0);   // pre-gathered rows / targets of a block of steps
+        h->add("mfit.Ts", MFIT_PRE, (int64_t)R2 * O, F, 0);
         h->add("ws.Hf1", R2, Hm0, F, 0);
         last("ws.Hf2", "ws.Hf1", R2, Hm1, Dm);
         h->add("ws.Of", R2, O, F, 0);
@@ -850,8 +857,9 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     // layer 0 may carry the actor head (rowk 3: target tile prologues from the head's partial dots,
     // which keep the prologue free of barriers, and head rows as extra workgroups)
     const bool head = a0.rowk == 3;
-    // or layer 0 gathers its rows from the replay ring (rowk 6: the world-model fit's model.fwd0)
-    const bool gather = a0.rowk == 6;
+    // or layer 0 gathers its rows from the replay ring (rowk 6: the world-model fit's model.fwd0), or
+    // reads them pre-gathered (rowk 9): the fit's layer 0, up to 512 wide
+    const bool gather = a0.rowk == 6 || a0.rowk == 9;
     if ((a0.rowk != 0 && !head && !gather) || (a1.rowk != 0 && a1.rowk != 5) || ((head || gather) && a1.rowk != 0) ||
         a0.has_final || a1.has_final || a0.nprob != a1.nprob || a0.nprob > 4)
         return false;
@@ -882,8 +890,8 @@ bool fuse_fwd2(sacx_handle* h, std::vector<Launch>& plan, const std::string& nam
     g.mode = GM_FWD2;
     g.vec = vec ? 1 : 0;
     g.total_tiles = tiles;
-    g.rowk = head ? 3 : gather ? 6 : a1.rowk;
-    if (gather) g.mg = a0.mg;
+    g.rowk = head ? 3 : gather ? a0.rowk : a1.rowk;
+    if (a0.rowk == 6) g.mg = a0.mg;
     if (head) {
         g.head = a0.head;
         g.hfin = a0.hfin;
@@ -1997,10 +2005,30 @@ void build_model_plan(sacx_handle* h) {
     mg.a_den = W("mnorm.a_den"); mg.d_mean = W("mnorm.d_mean"); mg.d_den = W("mnorm.d_den"); mg.r_norm = W("mnorm.r");
     mg.X = Xf; mg.ldQ = ldQ; mg.T = Tf; mg.nm = nm;
     mg.clip_d = h->cfg.delta_clip_loss; mg.clip_r = h->cfg.reward_clip_loss;
-    // the gather on model.fwd0's operand loads (rowk 6: 16x16 tiles, whose rows are whole records; the
-    // reward nets' layer 0 reads the gathered X, so --separate_reward_nn keeps the gather launch)
-    const bool gfold = fuse && h->mfuse >= 2 && h->mtile != 2 && h->stride % 4 == 0 && ldQ % 4 == 0 && !h->srn;
-    if (!gfold) {
+    // The minibatch rows: pre-gathered (SACX_MPRE, default) -- one k_mgather per block of <= MFIT_PRE steps
+    // writes step j's normalised rows / targets into staging slot j before the block's steps, whose
+    // launches read slot j (enqueue_fit_step moves their slot-0 pointers); or gathered per step, on
+    // model.fwd0's operand loads (rowk 6: 16x16 tiles, whose rows are whole records; the reward nets'
+    // layer 0 reads the gathered X, so --separate_reward_nn keeps the gather launch) or by its own launch
+    const bool pre = h->mpre != 0;
+    float* Xin = pre ? W("mfit.Xs") : Xf;     // what the steps read: slot 0 of the staging, or X / T
+    float* Tin = pre ? W("mfit.Ts") : Tf;
+    h->mpres[h->sel] = Launch{};
+    h->mpres[h->sel].kind = Launch::RNG;      // (none)
+    if (pre) {
+        Launch L{};
+        L.kind = Launch::MGATHER;
+        L.name = "model.pregather";
+        L.mg = mg;
+        L.mg.X = Xin;
+        L.mg.T = Tin;
+        L.pre_steps = 1;                      // (the block's step count, set at enqueue)
+        L.grid = (nm * mb + 3) / 4;
+        L.bytes = 4.0 * nm * mb * (2.0 * S + A + 1 + ldQ + O);
+        h->mpres[h->sel] = L;
+    }
+    const bool gfold = !pre && fuse && h->mfuse >= 2 && h->mtile != 2 && h->stride % 4 == 0 && ldQ % 4 == 0 && !h->srn;
+    if (!gfold && !pre) {
         Launch L{};
         L.kind = Launch::MGATHER;
         L.name = "model.gather";
@@ -2018,7 +2046,7 @@ void build_model_plan(sacx_handle* h) {
         const size_t r0 = (size_t)k * mb;
         for (int i = 0; i <= Dm; ++i) {
             const bool head = i == Dm;
-            const float* in = i == 0 ? Xf + r0 * ldQ : ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1];
+            const float* in = i == 0 ? Xin + r0 * ldQ : ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1];
             const int K = i == 0 ? S + A : nmd.h[i - 1];
             if (!head) {
                 f[i].push_back(prob_fwd(in, i == 0 ? ldQ : K, mb, K, W(L_(n, i)), nmd.h[i],
@@ -2029,7 +2057,7 @@ void build_model_plan(sacx_handle* h) {
                     GemmProb& p = f[i].back();
                     p.ldc = ldO;
                     p.mse = MSE_FIT | (h->gm ? MSE_GAUSS : 0) | (h->lscale ? MSE_SCALE : 0) | (h->srn ? MSE_NOREW : 0);
-                    p.se_raw = Tf + r0 * O; p.ldp = O; p.part = W("ws.lf") + r0 * nt;
+                    p.se_raw = Tin + r0 * O; p.ldp = O; p.part = W("ws.lf") + r0 * nt;
                     p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;   // the reward column's
                     if (h->gm) {
                         p.spe_raw = W(n + ".logstd");
@@ -2052,7 +2080,7 @@ void build_model_plan(sacx_handle* h) {
         }
         for (int i = 0; i <= Dm; ++i) {
             const bool head = i == Dm;
-            const float* X = i == 0 ? Xf + r0 * ldQ : ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1];
+            const float* X = i == 0 ? Xin + r0 * ldQ : ch("ws.Hf", i - 1, Dm) + r0 * nmd.h[i - 1];
             const int K = i == 0 ? S + A : nmd.h[i - 1];
             w.push_back(prob_dw(X, i == 0 ? ldQ : K, K, mb, head ? Df3 + r0 * ldO : ch("ws.Df", i, Dm) + r0 * nmd.h[i],
                                 head ? Om : nmd.h[i], W(L_(n, i)), nullptr, GRP_MODEL));
@@ -2068,7 +2096,7 @@ void build_model_plan(sacx_handle* h) {
             const std::string n = "r" + std::to_string(k);
             const size_t r0 = (size_t)k * mb;
             for (int i = 0; i <= Dr; ++i) {
-                const float* in = i == 0 ? Xf + r0 * ldQ : ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1];
+                const float* in = i == 0 ? Xin + r0 * ldQ : ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1];
                 const int K = i == 0 ? S + A : nrd.h[i - 1];
                 if (i < Dr) {
                     f[i].push_back(prob_fwd(in, i == 0 ? ldQ : K, mb, K, W(L_(n, i)), nrd.h[i],
@@ -2078,7 +2106,7 @@ void build_model_plan(sacx_handle* h) {
                     GemmProb& p = f[i].back();
                     p.ldc = 4;
                     p.mse = MSE_FIT;                                // N = 1: column 0 is the reward column
-                    p.se_raw = Tf + r0 * O + S; p.ldp = O; p.part = W("ws.lf") + (size_t)nm * mb * nt + r0;
+                    p.se_raw = Tin + r0 * O + S; p.ldp = O; p.part = W("ws.lf") + (size_t)nm * mb * nt + r0;
                     p.grad_scale = 1.f / (float)mb; p.fcoef = h->cfg.reward_loss_coef;
                 }
             }
@@ -2092,7 +2120,7 @@ void build_model_plan(sacx_handle* h) {
             }
             for (int i = 0; i <= Dr; ++i) {
                 const bool head = i == Dr;
-                const float* X = i == 0 ? Xf + r0 * ldQ : ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1];
+                const float* X = i == 0 ? Xin + r0 * ldQ : ch("ws.Hrf", i - 1, Dr) + r0 * nrd.h[i - 1];
                 const int K = i == 0 ? S + A : nrd.h[i - 1];
                 wr.push_back(prob_dw(X, i == 0 ? ldQ : K, K, mb, head ? Dr3 + r0 * 4 : ch("ws.Drf", i, Dr) + r0 * nrd.h[i],
                                      head ? 1 : nrd.h[i], W(L_(n, i)), nullptr, GRP_MODEL));
@@ -2128,7 +2156,7 @@ void build_model_plan(sacx_handle* h) {
         }
         if (!has_head(f[i])) {
             // hidden levels on 32x32 tiles (mt32 bit 2) when not inside the k_fwd2 pair
-            if (h->mtile == 1 && (h->mt32 & 2) && !(i == 1 && gfold && h->mfwd2 && S + A <= 32)) h->tile32 = 2;
+            if (h->mtile == 1 && (h->mt32 & 2) && !(i == 1 && (gfold || pre) && h->mfwd2 && S + A <= 32)) h->tile32 = 2;
         } else if (i == Lf && h->mtile == 1 && (h->mt32 & 8) && !h->gm && !h->srn) {
             h->tile32 = 2;     // the heads (+ the MSE loss epilogue) on 32x32 tiles (mt32 bit 8; MSE heads only)
         }
@@ -2136,13 +2164,21 @@ void build_model_plan(sacx_handle* h) {
         h->tile32 = t32_fit;
         // the gathered layer 0 and layer 1 as ONE k_fwd2 launch (SACX_MFWD2, default; K0 = S + A <= 32)
         if (i == 1 && gfold && h->mfwd2) fuse_fwd2(h, plan, "model.gather+fwd01");
+        // or, pre-gathered, layer 0 (rowk 9: H0 <= 512, plain A) and layer 1 the same way
+        if (i == 1 && pre && h->mfwd2 && h->mtile != 2 && S + A <= 32) {
+            Launch& F0 = plan[plan.size() - 2];
+            if (F0.kind == Launch::GEMM && F0.gemm.rowk == 0 && !F0.gemm.t32) {
+                F0.gemm.rowk = 9;
+                if (!fuse_fwd2(h, plan, "model.fwd01")) plan[plan.size() - 2].gemm.rowk = 0;
+            }
+        }
         if (i == Lf && fuse) plan.back().name = "model.fwd" + std::to_string(i) + "+loss";
     }
     if (!fuse) {
         Launch L{};
         L.kind = Launch::MLOSS;
         L.name = "model.loss";
-        L.ml.S = S; L.ml.mb = mb; L.ml.nm = nm; L.ml.T = Tf; L.ml.O = Of; L.ml.D3 = Df3; L.ml.ldD = ldO;
+        L.ml.S = S; L.ml.mb = mb; L.ml.nm = nm; L.ml.T = Tin; L.ml.O = Of; L.ml.D3 = Df3; L.ml.ldD = ldO;
         L.ml.loss_rows = W("ws.lf");
         L.ml.reward_coef = h->cfg.reward_loss_coef;
         L.grid = (nm * mb + 3) / 4;
@@ -2264,7 +2300,7 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::QHEAD: launch_qhead(L.qh, s); break;
         case Launch::ABWD: launch_actor_bwd(L.ab, s); break;
         case Launch::FINAL: launch_alpha_final(L.fin, s); break;
-        case Launch::MGATHER: launch_mgather(L.mg, s); break;
+        case Launch::MGATHER: launch_mgather(L.mg, s, L.pre_steps); break;
         case Launch::MLOSS: launch_mloss(L.ml, s); break;
         case Launch::MFINAL: launch_mfinal(L.mf, s); break;
         case Launch::ALLREDUCE:
@@ -2277,6 +2313,38 @@ void enqueue(const Launch& L, sacx_handle* h, hipStream_t s) {
         case Launch::GNORM: launch_gnorm(L.gn, s); break;
         case Launch::LNORM: launch_ln(L.ln, s); break;
     }
+}
+
+// A fit step's launches as step j of a pre-gathered block (SACX_MPRE): the pointers into slot 0 of the
+// staging (the rows mfit.Xs the first layers and the layer-0 dW read, the targets mfit.Ts of the loss)
+// moved to slot j
+Launch fit_step_launch(const sacx_handle* h, const Launch& L, int j) {
+    Launch C = L;
+    if (!h->mpre || j == 0) return C;
+    const float* x0 = h->f("mfit.Xs");
+    const float* t0 = h->f("mfit.Ts");
+    const int64_t xs = h->seg("mfit.Xs").cols, ts = h->seg("mfit.Ts").cols;
+    auto mv = [&](const float*& p) {
+        if (p >= x0 && p < x0 + xs) p += (size_t)j * xs;
+        else if (p >= t0 && p < t0 + ts) p += (size_t)j * ts;
+    };
+    if (C.kind == Launch::GEMM) {
+        for (int i = 0; i < C.gemm.nprob; ++i) {
+            mv(C.gemm.probs[i].A);
+            mv(C.gemm.probs[i].se_raw);
+        }
+    } else if (C.kind == Launch::MLOSS) {
+        mv(C.ml.T);
+    }
+    return C;
+}
+
+// The pre-gather of a block of n fit steps (none without SACX_MPRE)
+void enqueue_fit_pre(sacx_handle* h, int n, hipStream_t s) {
+    if (!h->mpre || h->mpres[h->sel].kind != Launch::MGATHER) return;
+    Launch P = h->mpres[h->sel];
+    P.pre_steps = n;
+    enqueue(P, h, s);
 }
 
 // Rebuilds every bf16 weight shadow from the fp32 weights (all seeds): at each entry point that
@@ -3095,6 +3163,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     if (const char* e = std::getenv("SACX_FWD2")) h->fwd2 = std::atoi(e);
     if (const char* e = std::getenv("SACX_AFIN")) h->afin = std::atoi(e);
     if (const char* e = std::getenv("SACX_MFWD2")) h->mfwd2 = std::atoi(e);
+    if (const char* e = std::getenv("SACX_MPRE")) h->mpre = std::atoi(e);
     if (const char* e = std::getenv("SACX_DWL_NH")) h->dwl_nh = std::atoi(e) == 2 ? 2 : 1;
     // Sampler batch: each batch start is a cross-stream wait on the chain (~1 us of gap), so a
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
@@ -3134,6 +3203,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
                 return fail(h, "internal: GEMM problem table mismatch");
     }
     h->mplans.assign(h->seeds, {});
+    h->mpres.assign(h->seeds, Launch{});
     h->mgraphs.assign(h->seeds, {});
     h->mfit_hosts.assign(h->seeds, 0);
     {
@@ -3715,8 +3785,9 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
             return 0;
         }
         HIPCHK(h, hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal));
+        enqueue_fit_pre(h, n, h->cap_stream);     // (n <= MFIT_PRE)
         for (int j = 0; j < n; ++j)
-            for (const Launch& L : mplan) enqueue(L, h, h->cap_stream);
+            for (const Launch& L : mplan) enqueue(fit_step_launch(h, L, j), h, h->cap_stream);
         const hipError_t le = hipGetLastError();
         hipGraph_t graph = nullptr;
         const hipError_t ee = hipStreamEndCapture(h->cap_stream, &graph);
@@ -3760,9 +3831,10 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
             FILE* f = std::fopen(kdump, "a");
             for (int64_t j = 0; j < chunk; ++j) {
                 HIPCHK(h, hipMemsetAsync(kb, 0, sizeof(uint64_t) * std::max<int64_t>(1, tot), h->stream));
+                if (j % MFIT_PRE == 0) enqueue_fit_pre(h, (int)std::min<int64_t>(MFIT_PRE, chunk - j), h->stream);
                 int64_t o = 0;
                 for (size_t i = 0; i < mplan.size(); ++i) {
-                    Launch C = mplan[i];
+                    Launch C = fit_step_launch(h, mplan[i], (int)(j % MFIT_PRE));
                     if (nwg[i] > 0) {
                         C.gemm.ktime = kb + o;
                         o += 2 * nwg[i];
@@ -3794,12 +3866,14 @@ int sacx_model_fit(sacx_handle* h, const int32_t* idx, int64_t n_steps, int32_t 
             if (f) std::fclose(f);
             (void)hipFree(kb);
         } else if (flags & SACX_STEP_EAGER) {
-            for (int64_t j = 0; j < chunk; ++j)
-                for (const Launch& L : mplan) enqueue(L, h, h->stream);
+            for (int64_t j = 0; j < chunk; ++j) {
+                if (j % MFIT_PRE == 0) enqueue_fit_pre(h, (int)std::min<int64_t>(MFIT_PRE, chunk - j), h->stream);
+                for (const Launch& L : mplan) enqueue(fit_step_launch(h, L, (int)(j % MFIT_PRE)), h, h->stream);
+            }
             HIPCHK(h, hipGetLastError());
         } else {
             for (int64_t j = 0; j < chunk;) {
-                const int n = chunk - j >= MFIT_GRAPH ? MFIT_GRAPH : chunk - j >= 8 ? 8 : 1;
+                const int n = chunk - j >= MFIT_GRAPH ? MFIT_GRAPH : chunk - j >= 8 ? 8 : 1;   // (<= MFIT_PRE)
                 hipGraphExec_t ex = nullptr;
                 if (graph_of(n, &ex)) return -1;
                 HIPCHK(h, hipGraphLaunch(ex, h->stream));

@@ -326,6 +326,7 @@ struct MGatherArgs {        // rows [0, 2*mb): model k = row / mb
     int32_t nm;                 // world models fitted (rows [0, nm*mb))
     float clip_d, clip_r;       // > 0: --delta_clip_loss / --reward_clip_loss on T (get_loss :286-296)
 };
+#define MFIT_PRE 64                 // fit steps one pre-gather block holds (= the steps of a fit graph)
 
 // end of a world-model fitting step (k_mfinal, or folded into a launch of the step)
 struct MFinalArgs {
@@ -746,7 +747,10 @@ void launch_actor_head(const HeadArgs& a, const FinalArgs& f, hipStream_t s);
 void launch_qhead(const QHeadArgs& a, hipStream_t s);
 void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s);
 void launch_append(const AppendArgs& a, hipStream_t s);
-void launch_mgather(const MGatherArgs& a, hipStream_t s);
+// nsteps > 0: the pre-gather of a block of fit steps (SACX_MPRE): step j of the block (ctl->mfit_seq + j)
+// into slot j of the staging that a.X / a.T point to ([MFIT_PRE, 2mb, ldQ] / [MFIT_PRE, 2mb, S+1]), which
+// that step's launches read; 0: this step's rows into X / T
+void launch_mgather(const MGatherArgs& a, hipStream_t s, int nsteps = 0);
 void launch_mloss(const MLossArgs& a, hipStream_t s);
 void launch_mfinal(const MFinalArgs& a, hipStream_t s);
 void launch_set_ctl(Ctl* ctl, int64_t num_timesteps, int64_t ts_increment, int64_t sstride, int nseeds, hipStream_t s);

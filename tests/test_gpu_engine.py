@@ -363,19 +363,24 @@ def test_model_fit_folds_bit_identical(gpu_available, monkeypatch, S, A, B, clip
     (SACX_MFUSE=0, SACX_MTILE=2) bit for bit, eager and graph; the loss statistic sums the
     same squares in another order (<= 1e-6 relative)."""
     outs = []
-    steps = 12
-    for fuse, tile, f2, mt32 in (("0", "2", "0", "5"), ("1", "1", "0", "5"), ("2", "1", "0", "5"), ("2", "1", "1", "5"),
-                                 ("2", "1", "1", "0"), ("2", "1", "0", "3"), ("2", "1", "1", "15"), ("2", "1", "0", "15"),
-                                 ("3", "1", "0", "5"), ("3", "1", "1", "5"),
-                                 ("3", "0", "1", "5")):
+    steps = 12      # (> 8: a graph block of 8 steps reads pre-gather slots 0 .. 7, then 1-step blocks slot 0)
+    for fuse, tile, f2, mt32, pre in (("0", "2", "0", "5", "0"), ("1", "1", "0", "5", "0"), ("2", "1", "0", "5", "0"),
+                                      ("2", "1", "1", "5", "0"), ("2", "1", "1", "0", "0"), ("2", "1", "0", "3", "0"),
+                                      ("2", "1", "1", "15", "0"), ("2", "1", "0", "15", "0"), ("3", "1", "0", "5", "0"),
+                                      ("3", "1", "1", "5", "0"), ("3", "0", "1", "5", "0"),
+                                      # SACX_MPRE=1 (default): the rows of a block of steps pre-gathered
+                                      ("0", "2", "0", "5", "1"), ("2", "1", "1", "5", "1"), ("2", "1", "0", "5", "1"),
+                                      ("2", "1", "1", "15", "1"), ("3", "1", "0", "5", "1")):
         monkeypatch.setenv("SACX_MFUSE", fuse)
         monkeypatch.setenv("SACX_MTILE", tile)
         monkeypatch.setenv("SACX_MFWD2", f2)
         monkeypatch.setenv("SACX_MT32", mt32)
+        monkeypatch.setenv("SACX_MPRE", pre)
         eng, ocfg, st, buf, nrm, _ = make_pair(S=S, A=A, B=B, act="tanh", N=3000, seed=33, use_expert=True,
                                                normalizers="random", model_max_grad_norm=clip)
         names = [L["name"] for L in eng.model_plan_info()]
-        assert ("model.gather+fwd01" in names) == (f2 == "1" and fuse != "1" and S + A <= 32), names
+        pair = f2 == "1" and S + A <= 32 and (fuse != "1" if pre == "0" else tile != "2")
+        assert (("model.gather+fwd01" if pre == "0" else "model.fwd01") in names) == pair, names
         mb = eng.cfg.model_batch
         idx = np.random.RandomState(4).randint(buf["r"].shape[0], size=(steps, 2, mb))
         eng.model_fit(idx[:3], eager=True)

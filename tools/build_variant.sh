@@ -9,7 +9,8 @@ H=/opt/rocm/bin/hipcc
 F="-O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Iinclude -Isac-expert_amd/csrc"
 $H $F $flags -mllvm -amdgpu-kernarg-preload-count=4 -c -o tools/libvar/k_sac_$name.o sac-expert_amd/csrc/k_sac.hip
 $H $F $flags -c -o tools/libvar/sacx_$name.o sac-expert_amd/csrc/sacx.cpp
+$H $F $flags -c -o tools/libvar/mtj_$name.o sac-expert_amd/csrc/mt_jump.cpp
 $H --offload-arch=gfx950 -shared -o tools/libvar/libsacx_$name.so tools/libvar/k_sac_$name.o tools/libvar/sacx_$name.o \
-    -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
-rm -f tools/libvar/k_sac_$name.o tools/libvar/sacx_$name.o
+    tools/libvar/mtj_$name.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+rm -f tools/libvar/k_sac_$name.o tools/libvar/sacx_$name.o tools/libvar/mtj_$name.o
 echo tools/libvar/libsacx_$name.so

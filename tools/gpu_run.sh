@@ -77,6 +77,10 @@ for step in "$@"; do
     mktime)     # per-launch workgroup timing of the fit (eager steps, SACX_MFIT_KTIME): mktime=<config>
       timeout -k 10 200 python tools/mfit_ktime.py ${arg:-hc_eo} > "$log" 2>&1
       rc=$?; echo "[$n mktime ${arg:-hc_eo}] rc=$rc"; cat "$log" | grep -v amdgpu.ids ;;
+    mktimev)    # mktime with a variant library: mktimev=<config>:<tools/libvar name>
+      cfg=${arg%%:*}; var=${arg#*:}
+      SACX_LIBPATH=$PWD/tools/libvar/libsacx_$var.so timeout -k 10 200 python tools/mfit_ktime.py $cfg > "$log" 2>&1
+      rc=$?; echo "[$n mktimev $arg] rc=$rc"; cat "$log" | grep -v amdgpu.ids ;;
     mprof)      # rocprofv3 kernel-trace stats of the HC model fit (graph replay only) -> profiles r*_mfit_hc_kernel_stats
       MFT_GRAPH_ONLY=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/mprof" -o m \
           -- python tools/model_fit_time.py hc_eo 2048 > "$log" 2>&1
