@@ -972,15 +972,15 @@ __device__ __forceinline__ void head_bwd_prologue(HeadBwdArgs hb, int m0, int tn
 #ifndef SACX_T32_DW_NS
 #define SACX_T32_DW_NS 1   // the same for the dW + Adam tiles (uncapped registers)
 #endif
-// SACX_T32_STAMP (diagnostic builds): a 32x32 dW + Adam workgroup's end stamp is taken after phase P
-// instead -- 1: its epilogue operands (P, m, v, T) have arrived, 2: its main-loop MFMAs are done,
-// 3: the K-quarter reduction is in LDS (k_gemm skips its own end stamp for these launches)
+// SACX_T32_STAMP (diagnostic builds): a 32x32-tile workgroup's end stamp is taken after phase P
+// instead -- 1: its epilogue operands (bias / act' input / P, m, v, T) have arrived, 2: its main-loop
+// MFMAs are done, 3: the K-quarter reduction is in LDS (k_gemm skips its own end stamp for these launches)
 #ifndef SACX_T32_STAMP
 #define SACX_T32_STAMP 0
 #endif
 #define T32_STAMP(P, ...)                                                                   \
     do {                                                                                     \
-        if (MODE == GM_DW && SACX_T32_STAMP == (P) && ga.ktime != nullptr) {                 \
+        if (SACX_T32_STAMP == (P) && ga.ktime != nullptr) {                                  \
             asm volatile("" ::__VA_ARGS__);                                                  \
             __syncthreads();                                                                 \
             if (threadIdx.x == 0) ga.ktime[2 * ktime_wg() + 1] = __builtin_amdgcn_s_memrealtime(); \
@@ -1929,7 +1929,7 @@ __global__ __launch_bounds__(256, SACX_T32_OCC) void k_gemm(uint32_t h0, uint32_
 #endif
     gemm_core<MODE, VEC, ROWK, NQ, BF, PK, T32>(KHdr{{h0, h1, h2, h3}}, ga);
     GEMM_PH(4);
-    if (SACX_T32_STAMP && T32 && MODE == GM_DW) {   // (diagnostic: the phase stamp is the end stamp)
+    if (SACX_T32_STAMP && T32) {   // (diagnostic: the phase stamp is the end stamp)
         if (ga.ktime != nullptr && threadIdx.x == 0) ga.ktime[2 * ktime_wg()] = t0;
     } else if (ga.ktime != nullptr) {
         __syncthreads();
