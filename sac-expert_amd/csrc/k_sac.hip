@@ -241,6 +241,19 @@ __device__ __forceinline__ void abf_store4(uint16_t* S, int N, int m, bool mok, 
     o.y = bf16_bits(v2) | (bf16_bits(v3) << 16);
     *reinterpret_cast<uint2*>(S + (size_t)m * N + wbf_pos(n, wbf_per_of(N))) = o;
 }
+// A transposed image's 4 consecutive rows m .. m + 3 (m % 4 == 0) of column n: a 32x32 tile's lanes
+// l, l + 16, l + 32, l + 48 hold them (rows 4 wave + 0 .. 3 of a 16-row sub-tile); lane l < 16
+// stores them as one 8-B piece of row n (wbf_pos positions of K = M, the consumer's reduction).
+// Every lane calls it.
+__device__ __forceinline__ void tbf_store4(uint16_t* S, int M, int m, int n, bool nok, float v) {
+    const int lane = threadIdx.x & 63;
+    const float v1 = __shfl_down(v, 16, 64), v2 = __shfl_down(v, 32, 64), v3 = __shfl_down(v, 48, 64);
+    if (lane >= 16 || !nok || m >= M) return;
+    uint2 o;
+    o.x = bf16_bits(v) | (bf16_bits(v1) << 16);
+    o.y = bf16_bits(v2) | (bf16_bits(v3) << 16);
+    *reinterpret_cast<uint2*>(S + (size_t)n * wbf_ld_of(M) + wbf_pos(m, wbf_per_of(M))) = o;
+}
 // The control-block scalars a GEMM epilogue needs (the optimiser step, the Polyak gate, the
 // expert weight), requested with the epilogue operands before the main loop: read after the
 // tile reduction they were two more dependent memory round trips (the kernarg ctl pointer,
@@ -1164,9 +1177,55 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
         }
     }
     };
+    // bf16 dW + Adam with X^T from its transposed image (abf, wbf_ld_of(K) positions per row m):
+    // one bf16x8 per lane, sub-tile row and slab pair; the ones row (bias gradient) generated as
+    // the converting path makes it; B converted (its per-row scale is produced in the launch before)
+    auto xbf_loop = [&]() {
+    const __amdgpu_buffer_rsrc_t rab = make_rsrc(reinterpret_cast<const float*>(g.abf), 0x7fffffffu);
+    const int pb = wave * ((per + 1) >> 1);
+    const int ld = 4 * ((per + 1) >> 1) * 32;        // wbf_ld_of(K)
+    const bool aone = ma == g.ones_row, bone = mb == g.ones_row;
+    for (int it = it0; it < it1; it += 2) {
+        float b[2][2][4];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int k0 = (it + u) * 16 + grp * 4;
+            const int k0e = (it + u < it1) ? k0 : (1 << 30);
+            load_b<false, false, true>(rb, g, na, naok, k0e, b[u][0]);
+            load_b<false, false, true>(rb, g, nb, nbok, k0e, b[u][1]);
+        }
+        const int po = (pb + ((it - it0) >> 1)) * 32 + grp * 8;
+        bf16x8_t aw[2], bw[2];
+        aw[0] = wbf_load(rab, maok && !aone, ma * ld + po);
+        aw[1] = wbf_load(rab, mbok && !bone, mb * ld + po);
+        if (aone || bone) {
+            float o0[4], o1[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                o0[j] = it * 16 + grp * 4 + j < g.K ? 1.f : 0.f;
+                o1[j] = (it + 1 < it1 && (it + 1) * 16 + grp * 4 + j < g.K) ? 1.f : 0.f;
+            }
+            const bf16x8_t ones = pack_bf16(o0, o1);
+            if (aone) aw[0] = ones;
+            if (bone) aw[1] = ones;
+        }
+        bw[0] = pack_bf16(b[0][0], b[1][0]);
+        bw[1] = pack_bf16(b[0][1], b[1][1]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if (((it - it0) >> 1) & 1)
+                acc1[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s >> 1], bw[s & 1], acc1[s], 0, 0, 0);
+            else
+                acc0[s] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(aw[s >> 1], bw[s & 1], acc0[s], 0, 0, 0);
+        }
+    }
+    };
     bool shadow = false;
     if constexpr (MODE == GM_FWD && BF) shadow = g.wbf != nullptr || g.abf != nullptr;
+    if constexpr (MODE == GM_DW && BF) shadow = g.abf != nullptr;
     if (shadow) {
+        if constexpr (MODE == GM_DW && BF) xbf_loop();
         if constexpr (MODE == GM_FWD && BF) {
             using T_ = std::true_type;
             using F_ = std::false_type;
@@ -1272,6 +1331,8 @@ __device__ __forceinline__ void gemm_tile32(const GemmArgs& ga, const GemmProb& 
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], o);
             if constexpr (BF) {     // the next layer's bf16 A operand (its K = this N)
                 if (g.obf != nullptr) abf_store4(g.obf, g.N, mm, mm < g.M, nn, o);
+                // and the dW + Adam tiles' (the transposed image: K = this M)
+                if (g.tbf != nullptr) tbf_store4(sr(g.tbf, so), g.M, mm, nn, nn < g.N, o);
             }
         } else if constexpr (MODE == GM_DX) {
             if (out_ok) st_out(&g.C[(size_t)mm * g.ldc + nn], v * dact_f(e0[s], g.act));
@@ -3890,6 +3951,7 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
         auto sh = [off](auto* p) { return p ? (decltype(p))((char*)p + off) : p; };
         g.idx = sh(ga.idx); g.Xa = sh(ga.Xa); g.Xq = sh(ga.Xq); g.Xt = sh(ga.Xt); g.Xp = sh(ga.Xp);
         g.Xm = sh(ga.Xm); g.r = sh(ga.r); g.d = sh(ga.d); g.se_raw = sh(ga.se_raw); g.spe_raw = sh(ga.spe_raw);
+        g.xbfq = sh(ga.xbfq);
         g.slot = ga.slot + (int)blockIdx.y;
         g.replay = sr(ga.replay, so); g.ctl = sr(ga.ctl, so);
         g.s_mean = sr(ga.s_mean, so); g.s_den = sr(ga.s_den, so); g.a_mean = sr(ga.a_mean, so); g.a_den = sr(ga.a_den, so);
@@ -3919,6 +3981,8 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
                 g.Xa[(size_t)(g.B + row) * g.ldS + c] = sn;
             }
             g.Xq[(size_t)row * g.ldQ + c] = cs ? sn : an;
+            if (g.xbfq != nullptr && c < S + A)     // (critic.adam's layer-0 A operand, transposed)
+                g.xbfq[(size_t)c * wbf_ld_of(g.B) + wbf_pos(row, wbf_per_of(g.B))] = (uint16_t)bf16_bits(cs ? sn : an);
             if (!ca) {
                 g.Xt[(size_t)row * g.ldQ + c] = spn;
                 g.Xp[(size_t)row * g.ldQ + c] = sn;

@@ -173,6 +173,8 @@ struct sacx_handle {
     struct WbfMat { std::string name; int K, N; };
     std::vector<WbfMat> wbf_mats;
     int wbf_enabled = 3;      // SACX_WBF: 0 off, 1 weights + layer-0 activations, 2 weights only, 3 activations only
+    int xbf = 0;              // transposed bf16 images of critic.adam's X operands (SACX_XBF; C5, B % 128 == 0):
+                              // 0 off, 1 the critic rows (k_gather) and layer-0 outputs (q.fwd0), 2 the rows only
     bool wbf_attach = false;
     bool wbf_live = false;    // the update plans read / maintain the shadows (refreshed per step call)
     hipEvent_t seg_start = nullptr;   // run_segments: the call's start on the bound stream (before set_ctl)
@@ -451,6 +453,12 @@ void build_layout(sacx_handle* h) {
     h->nslot = h->n_norm <= 16384 ? NSLOT : 8;
     if (const char* e = std::getenv("SACX_NSLOT")) h->nslot = std::max(2, std::min(NSLOT, std::atoi(e)));
     const int ne1 = std::max(1, h->ne);
+    // config C5: critic.adam's bf16 32x32 tiles read X^T (the critic rows, the critics' layer-0
+    // outputs) from transposed images their producers write (k_gather, q.fwd0's epilogue) instead
+    // of converting strided fp32 columns; B % 128 == 0, so the images have no pad positions
+    h->xbf = 0;
+    if (const char* e = std::getenv("SACX_XBF"))
+        if (h->cfg.gemm_bf16 && !h->deep && B % 128 == 0) h->xbf = std::max(0, std::min(2, std::atoi(e)));
     for (int s = 0; s < h->nslot; ++s) {
         const std::string sl = "slot" + std::to_string(s);
         h->add(sl + ".idx", 1, B, SACX_I32, SACX_ROLE_WORK);
@@ -464,11 +472,13 @@ void build_layout(sacx_handle* h) {
         h->add(sl + ".d", 1, B, F, 0);
         h->add(sl + ".se_raw", ne1, S, F, 0);
         h->add(sl + ".spe_raw", ne1, S, F, 0);
+        if (h->xbf) h->add(sl + ".xbfq", S + A, wbf_ld_of(B) / 2, SACX_U32, SACX_ROLE_WORK);
     }
     h->slot_bytes = (int64_t)(h->off_of("slot1.idx") - h->off_of("slot0.idx"));
     for (int k = 1; k < h->nslot; ++k)   // the batched sampler / gather address slot k as slot 0 + k * slot_bytes
-        for (const char* nm : {".idx", ".noise", ".Xa", ".Xq", ".Xt", ".Xp", ".Xm", ".r", ".d", ".se_raw", ".spe_raw"})
-            if (h->off_of("slot" + std::to_string(k) + nm) != h->off_of(std::string("slot0") + nm) + k * (uint64_t)h->slot_bytes) {
+        for (const char* nm : {".idx", ".noise", ".Xa", ".Xq", ".Xt", ".Xp", ".Xm", ".r", ".d", ".se_raw", ".spe_raw", ".xbfq"})
+            if ((std::string(nm) != ".xbfq" || h->xbf) &&
+                (h->off_of("slot" + std::to_string(k) + nm) != h->off_of(std::string("slot0") + nm) + k * (uint64_t)h->slot_bytes)) {
                 fprintf(stderr, "sacx: slot layout is not uniform\n");
                 abort();
             }
@@ -564,6 +574,8 @@ void build_layout(sacx_handle* h) {
             h->add(std::string("abf.") + n, sg.rows, w / 2, SACX_U32, SACX_ROLE_WORK);
             h->abf_segs.push_back(n);
         }
+    // (config C5) the critics' layer-0 outputs transposed: one image per q.fwd0 problem (t0 t1 q0 q1)
+    if (h->xbf == 1) h->add("xbf.ws.Hq1", 4 * (int64_t)Hc0, wbf_ld_of(B) / 2, SACX_U32, SACX_ROLE_WORK);
     // behaviour-policy inference (sacx_actor_act), up to ACT_CAP rows per launch chain
     h->add("act.X", ACT_CAP, h->ldS, F, 0);
     // (sacx_critic_forward's too; the generic plans' nets alternate between the two: any layer's width)
@@ -1110,6 +1122,50 @@ void plan_alpha_final(sacx_handle* h, std::vector<Launch>& plan, int nm) {
     }
 }
 
+// Config C5: the bf16 32x32 dW + Adam problems whose X is the slot's critic rows (Xq) or a critic's
+// layer-0 output (ws.Hq1, written by a bf16 32x32 forward problem earlier in the plan) read X^T
+// from a transposed image instead (GemmProb::abf); its producer -- k_gather (xbfq) or that
+// forward problem's epilogue (tbf) -- is told to write it.  Bit-identical: the image holds the
+// bf16 values the converting loads make, in the order they pack them.
+void xbf_wire(sacx_handle* h, std::vector<Launch>& plan, int slot) {
+    if (!h->xbf || !h->wbf_attach) return;
+    const int S = h->S, A = h->A, B = h->B, Hc0 = h->Hc0, ld = wbf_ld_of(B);
+    const std::string sl = "slot" + std::to_string(slot);
+    const float* Xq = h->f(sl + ".Xq");
+    const float* Hq1 = h->f("ws.Hq1");
+    Launch* gather = nullptr;
+    for (Launch& L : plan)
+        if (L.kind == Launch::GATHER) gather = &L;
+    for (size_t i = 0; i < plan.size(); ++i) {
+        Launch& L = plan[i];
+        if (L.kind != Launch::GEMM || L.gemm.mode != GM_DW || !L.gemm.t32 || L.gemm.dwl || !L.gemm.bf16) continue;
+        for (int j = 0; j < L.gemm.nprob; ++j) {
+            GemmProb& p = L.gemm.probs[j];
+            if (p.K != B || p.a_kc != 0) continue;
+            if (p.A == Xq && p.ones_row == S + A && gather != nullptr) {
+                p.abf = h->ptr<uint16_t>(sl + ".xbfq");
+                gather->gather.xbfq = h->ptr<uint16_t>(sl + ".xbfq");
+                continue;
+            }
+            const int64_t d = p.A - Hq1;
+            if (h->xbf != 1 || d < 0 || d % ((int64_t)B * Hc0) != 0 || d / ((int64_t)B * Hc0) >= 4 || p.lda != Hc0 || p.ones_row != Hc0)
+                continue;
+            uint16_t* img = h->ptr<uint16_t>("xbf.ws.Hq1") + (size_t)(d / ((int64_t)B * Hc0)) * Hc0 * ld;
+            for (size_t q = 0; q < i && p.abf == nullptr; ++q) {
+                Launch& F = plan[q];
+                if (F.kind != Launch::GEMM || F.gemm.mode != GM_FWD || !F.gemm.t32 || !F.gemm.bf16 || F.gemm.rowk != 0) continue;
+                for (int c = 0; c < F.gemm.nprob; ++c) {
+                    GemmProb& f = F.gemm.probs[c];
+                    if (f.C == p.A && f.M == B && f.N == Hc0 && f.ldc == Hc0 && f.mse == 0 && f.ppart == nullptr) {
+                        f.tbf = img;
+                        p.abf = img;
+                    }
+                }
+            }
+        }
+    }
+}
+
 void build_plan(sacx_handle* h, int slot, bool record_probs) {
     std::vector<Launch>& plan = h->plan[slot];
     plan.clear();
@@ -1627,9 +1683,8 @@ void build_plan(sacx_handle* h, int slot, bool record_probs) {
     plan_alpha_final(h, plan, nm);
     // alpha.fwd .. alpha.final only feed the next update's q.head
     for (size_t i = alpha_first; i < plan.size(); ++i) plan[i].alpha_branch = true;
+    xbf_wire(h, plan, slot);
     for (Launch& L : plan) pack_seeds(L, (int64_t)h->seed_bytes, h->seeds);
-    {
-    }
 }
 
 // Appends one GEMM launch per GEMM_MAXP problems (a launch's problems travel by value): `name`,

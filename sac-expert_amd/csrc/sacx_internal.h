@@ -133,14 +133,23 @@ struct GemmProb {
     // with model.bwd2's exact MFMA sequence (16-wide output slabs t, j = 0 2 / 1 3 pairs, the
     // slabs as waves summed in order; g_o <= 32); column tile 0 stores D2 to gst (ld gst_ld)
     const float* gd;
-    float* gst;
+    union {
+        float* gst;
+        // config C5, GM_FWD on 32x32 tiles: the output's transposed bf16 image, rows n of C^T in the
+        // wbf_pos layout of K = M (one 8-B piece per 4 consecutive rows) -- a later dW problem's A
+        // operand (abf of GM_DW below; M % 4 == 0)
+        uint16_t* tbf;
+    };
     int32_t gd_ld, g_o, gst_ld;
     // config C5 (bf16 GEMMs) with 32x32 forward tiles: bf16 shadows of operands in the MFMA pair
     // layout of wbf_pos, read as one bf16x8 per lane and k-slab pair (null: the fp32 operand,
     // converted on load).  Weights: each row n of W^T; GM_FWD reads B from wbf, GM_DW + Adam stores
     // the updated rows k < wbf_k of P into wbf and the Polyak target into obf.  Activations (the
     // hidden layer-0 outputs, K = H0 a multiple of 128: rows of K positions): GM_FWD reads A from
-    // abf (row stride K) and stores its own output into obf (row stride N) beside C.
+    // abf (row stride K) and stores its own output into obf (row stride N) beside C.  GM_DW on
+    // 32x32 tiles reads its A (= X^T) from abf when set: rows m < ones_row of wbf_ld_of(K)
+    // positions (the ones row generated), written by the producer of X (tbf above, or k_gather's
+    // xbfq for the critic input rows).
     uint16_t* wbf;
     uint16_t* obf;
     const uint16_t* abf;
@@ -532,6 +541,9 @@ struct GatherArgs {
     const float* exp_s; const float* exp_sp; const int32_t* perm_ring; int32_t perm_cap;
     int32_t perm_ld;            // permutation length (expert_batch; ne = the rows used, <= perm_ld)
     float* se_raw; float* spe_raw;
+    // config C5: the critic rows' transposed bf16 image (columns c < S + A of Xq as rows of
+    // wbf_ld_of(B) positions, wbf_pos layout): critic.adam's layer-0 A operand; null: not written
+    uint16_t* xbfq;
     // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
     int64_t sstride;

@@ -132,11 +132,16 @@ def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
     (SACX_WBF=0) bit for bit over 2 x 24 Humanoid updates at B = 1,024, with a host write of the
     parameters in between (the weight shadows are rebuilt at the next step call); after each run
     every weight shadow equals the bf16 image of its fp32 weights in the wbf_pos layout, and the
-    critics' layer-0 output shadow that of the last update's activations."""
+    critics' layer-0 output shadow that of the last update's activations.  critic.adam reading X^T
+    from transposed images (opt-in SACX_XBF=1: critic rows and layer-0 outputs, 2: the rows only)
+    equals it too, and the images equal the bf16 transposes of every slot's critic rows and of the
+    last update's q0 / q1 layer-0 outputs."""
     B, n = 1024, 24
+    S, A = HUM["S"], HUM["A"]
     outs = []
-    for wbf in ("0", "3", "2", "1"):
+    for wbf, xbf in (("0", "1"), ("3", "0"), ("3", "1"), ("3", "2"), ("2", "1"), ("1", "1")):
         monkeypatch.setenv("SACX_WBF", wbf)
+        monkeypatch.setenv("SACX_XBF", xbf)
         eng, *_ = make_pair(act="relu", B=B, N=6000, seed=41, done_p=0.01, gemm_bf16=True, graph_steps=8, **HUM)
         eng.rng_set_state(np.random.RandomState(8).get_state())
         eng.step(n, eager=eager)
@@ -160,6 +165,21 @@ def test_bf16_weight_shadows_bit_identical(gpu_available, monkeypatch, eager):
             exp = _wbf_expected(hq.T)
             got = eng.v["abf.ws.Hq1"].cpu().numpy().view(np.uint16).reshape(exp.shape[0], -1)
             assert np.array_equal(got, exp)
+        assert ("xbf.ws.Hq1" in eng.v) == (xbf == "1")
+        if wbf != "0" and xbf != "0":
+            names = [nm for nm in eng.v if nm.startswith("slot") and nm.endswith(".xbfq")]
+            assert len(names) == 8                   # Humanoid: an 8-slot ring
+            for nm in names:
+                xq = eng.v[nm.replace(".xbfq", ".Xq")].cpu().numpy()[:B, :S + A]
+                exp = _wbf_expected(xq)
+                got = eng.v[nm].cpu().numpy().view(np.uint16).reshape(exp.shape[0], -1)
+                assert np.array_equal(got, exp), nm
+        if wbf != "0" and xbf == "1":
+            hq = eng.v["ws.Hq1"].cpu().numpy()
+            img = eng.v["xbf.ws.Hq1"].cpu().numpy().view(np.uint16)
+            img = img.reshape(4, hq.shape[1], -1)
+            for k in (2, 3):                         # q0, q1 (critic.adam's consumers; t0 / t1 unwritten)
+                assert np.array_equal(img[k], _wbf_expected(hq[k * B:(k + 1) * B])), k
         eng.close()
     for o in outs[1:]:
         for i, (a, b) in enumerate(zip(outs[0], o)):

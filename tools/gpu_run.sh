@@ -121,6 +121,10 @@ for step in "$@"; do
     ktimeenv)   # ktime (hc) under one extra environment setting: ktimeenv=VAR=VALUE
       env "$arg" timeout -k 10 200 python tools/ktime_dump.py hc > "$log" 2>&1
       rc=$?; echo "[$n ktimeenv $arg] rc=$rc $(tail -n 1 "$log")" ;;
+    ktimecfgenv)  # ktime of config C under one extra environment setting: ktimecfgenv=C:VAR=VALUE
+      cfg=${arg%%:*}; ev=${arg#*:}
+      env "$ev" timeout -k 10 200 python tools/ktime_dump.py "$cfg" > "$log" 2>&1
+      rc=$?; echo "[$n ktimecfgenv $arg] rc=$rc $(tail -n 1 "$log")" ;;
     benchenv)   # the 2,000-update bench under one extra environment setting: benchenv=VAR=VALUE
       env "$arg" timeout -k 10 300 python bench.py --steps 2000 --warmup 200 --no-cpu-baseline > "$log" 2>&1
       rc=$?; echo "[$n benchenv $arg] rc=$rc $(value "$log")" ;;
