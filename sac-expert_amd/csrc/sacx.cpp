@@ -249,6 +249,13 @@ struct sacx_handle {
     // the next act needs the updated actor, not alpha.  alpha_pending = that update's slot, or -1;
     // every entry point that could observe or disturb it runs it first (settle).
     int alpha_pending = -1;
+    // k_set_ctl skipped when the control block already holds the values: a speculative step(1)
+    // right after another with num_timesteps advanced by ts_increment (the folded alpha.final's
+    // add) -- the drop-in loop's cadence.  settle() and resync forget it.
+    bool ctl_skip = true;     // SACX_CTL_SKIP=0: always launch it
+    bool ctl_known = false;
+    int64_t ctl_nts = 0;
+    int32_t ctl_inc = 0;
     int64_t cur_size_host = 0; // mirrors ctl->cur_size (appends, resync)
     int64_t n_appends = 0;     // sacx_buffer_append calls (a full ring changes content, not size)
     int64_t spec_appends = 0;  // n_appends when the speculative draw was queued
@@ -457,6 +464,7 @@ void build_layout(sacx_handle* h) {
     // outputs) from transposed images their producers write (k_gather, q.fwd0's epilogue) instead
     // of converting strided fp32 columns; B % 128 == 0, so the images have no pad positions
     h->xbf = 0;
+    if (const char* e = std::getenv("SACX_CTL_SKIP")) h->ctl_skip = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_XBF"))
         if (h->cfg.gemm_bf16 && !h->deep && B % 128 == 0) h->xbf = std::max(0, std::min(2, std::atoi(e)));
     for (int s = 0; s < h->nslot; ++s) {
@@ -2925,6 +2933,7 @@ int run_segments(sacx_handle* h, int n, bool run) {
 // a queued speculative draw: the state every entry point but act / append / the speculative
 // step(1) starts from.
 int settle(sacx_handle* h, bool keep_rng_state = false) {
+    h->ctl_known = false;
     if (h->alpha_pending >= 0) {
         const int slot = h->alpha_pending;
         h->alpha_pending = -1;
@@ -3284,6 +3293,7 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
 int sacx_resync(sacx_handle* h) {
     if (!h || !h->bound) return fail(h, "not bound");
     h->alpha_pending = -1;                   // the restored state is authoritative
+    h->ctl_known = false;
     if (spec_cancel(h, true)) return -1;
     Ctl c{};
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -3772,8 +3782,10 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
         HIPCHK(h, hipEventRecord(h->seg_start, h->stream));
     }
     wbf_refresh(h, h->stream);
-    launch_set_ctl(h->ctl0(), num_timesteps - (prev >= 0 ? ts_increment : 0), ts_increment,
-                   (int64_t)h->seed_bytes, h->seeds, h->stream);
+    const int64_t nts_set = num_timesteps - (prev >= 0 ? ts_increment : 0);
+    if (!(use_spec && h->ctl_skip && h->ctl_known && h->ctl_nts == nts_set && h->ctl_inc == ts_increment))
+        launch_set_ctl(h->ctl0(), nts_set, ts_increment, (int64_t)h->seed_bytes, h->seeds, h->stream);
+    h->ctl_known = false;
     const bool ext = (flags & SACX_STEP_EXTERNAL_RANDOMS) != 0;
     if (use_spec) {
         h->spec_live = false;
@@ -3782,6 +3794,11 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
         if (get_spec_graph(h, h->spec_slot, prev, &g)) return -1;
         HIPCHK(h, hipGraphLaunch(g, h->stream));
         h->alpha_pending = h->spec_slot;
+        // the control block after this chain: num_timesteps (the folded alpha.final added
+        // ts_increment; this update's own is deferred into the next step)
+        h->ctl_known = true;
+        h->ctl_nts = num_timesteps;
+        h->ctl_inc = ts_increment;
     } else if (flags & SACX_STEP_EAGER) {
         for (int64_t j = 0; j < n_steps; ++j) enqueue_step(h, 0, !ext, h->stream);
         HIPCHK(h, hipGetLastError());

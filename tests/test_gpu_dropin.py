@@ -13,8 +13,11 @@ from helpers import load_learner, make_learner
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("full", [False, True])
-def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full):
+@pytest.mark.parametrize("full,tui", [(False, 1), (True, 1), (False, 2)])
+def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full, tui):
+    """tui = 2: the Polyak gate reads num_timesteps, which the speculative steps leave to the
+    control block when it already holds the value (k_set_ctl skipped); the timesteps jump now and
+    then, so a stale value would gate the wrong updates."""
     from sac_eo.engine import Engine, EngineConfig
     B, N, n = 64, 600, 48
     outs, hits = [], []
@@ -22,7 +25,8 @@ def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full):
         monkeypatch.setenv("SACX_SPEC", spec)
         ocfg, st, buf, nrm, _ = make_learner(act="relu", B=B, N=N, seed=5, done_p=0.05)
         cap = N if full else N + 200          # full: every append drops the oldest row
-        eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=cap, graph_steps=1))
+        eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=cap, graph_steps=1,
+                                  target_update_int=tui))
         load_learner(eng, st, buf, nrm, None, 0.1)
         eng.rng_set_state(np.random.RandomState(12).get_state())
         rs = np.random.RandomState(3)
@@ -32,7 +36,7 @@ def test_speculative_sampler_equals_plain(gpu_available, monkeypatch, full):
             late = j % 9 == 4                                     # now and then the add before the update
             if late:
                 eng.append(o[None], a[None], np.array([0.5], np.float32), o2[None], np.zeros(1, np.float32))
-            eng.step(1, num_timesteps=j, ts_increment=1)
+            eng.step(1, num_timesteps=j + j // 7, ts_increment=1)
             if j % 13 == 5:
                 eng.append(np.stack([o, o2]), np.stack([a, a]), np.zeros(2), np.stack([o2, o]), np.zeros(2))  # 2 rows
             elif not late:
