@@ -4474,22 +4474,67 @@ __global__ __launch_bounds__(1024) void k_act_rows(ActRowArgs g) {
     act_rows_done(g.done);
 }
 
+// TrajectoryBuffer.add (buffers.py:41-71) as a device ring, by one workgroup so the control-block
+// update is ordered after every row write (k_append; k_act_rng's append workgroup)
+__device__ void append_body(const AppendArgs& a_in) {
+    __shared__ int64_t cur_s, start_s;
+    AppendArgs a = a_in;
+    if (a_in.nseeds > 1) {          // packed seeds: seed z's ring and counters, its n source rows
+        const int64_t so = seed_off(a_in.sstride), z = blockIdx.z;
+        a.replay = sr(a.replay, so); a.ctl = sr(a.ctl, so);
+        a.s = a.s + z * a.n * a.S; a.a = a.a + z * a.n * a.A; a.sp = a.sp + z * a.n * a.S;
+        a.r = a.r + z * a.n; a.d = a.d + z * a.n;
+    }
+    if (threadIdx.x == 0) {
+        cur_s = a.ctl->cur_size;
+        start_s = a.ctl->start;
+    }
+    __syncthreads();
+    const int64_t cur = cur_s, start = start_s, cap = a.cap, n = a.n;
+    const int64_t first = n > cap ? n - cap : 0;   // rows that survive truncation
+    const int S = a.S, A = a.A, W = 2 * S + A + 2;
+    for (int64_t e = (int64_t)threadIdx.x + first * W; e < n * W; e += blockDim.x) {
+        const int64_t i = e / W;
+        const int c = (int)(e - i * W);
+        const int64_t phys = (start + cur + i) % cap;
+        float v;
+        if (c < S) v = a.s[i * S + c];
+        else if (c < S + A) v = a.a[i * A + (c - S)];
+        else if (c < 2 * S + A) v = a.sp[i * S + (c - S - A)];
+        else if (c == 2 * S + A) v = a.r[i];
+        else v = a.d[i];
+        a.replay[phys * a.stride + c] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int64_t tot = cur + n;
+        const int64_t drop = tot > cap ? tot - cap : 0;
+        a.ctl->start = (start + drop) % cap;
+        a.ctl->cur_size = tot - drop;
+    }
+}
+
 // The drop-in loop's deterministic act with the next update's sampler draw beside it: the
 // action rows are workgroups 0 .. m - 1 and k_rng's draw is workgroup m, so the draw (one CU,
 // ~13 us at HC shapes) runs while the rows run instead of after them.  One LDS image, either
-// role's.  (A deterministic act reads no randoms: the two are independent.)
+// role's.  (A deterministic act reads no randoms: the two are independent.)  APP: the previous
+// call's deferred 1-row append is workgroup m + 1 (the draw then takes the ring size from the
+// host, r.size_fixed, instead of reading it beside the append)
 union ActRngShared {
     RngShared r;
     ActShared a;
 };
-template <bool PF>
-__global__ __launch_bounds__(1024) void k_act_rng(ActRowArgs g, RngArgs r) {
+template <bool PF, bool APP>
+__global__ __launch_bounds__(1024) void k_act_rng(ActRowArgs g, RngArgs r, AppendArgs app) {
     __shared__ ActRngShared U;
-    if (blockIdx.x + 1 < gridDim.x) {
+    const int m = (int)gridDim.x - 1 - (APP ? 1 : 0);
+    if ((int)blockIdx.x < m) {
         act_rows_body<PF>(g, blockIdx.x, U.a);
         act_rows_done(g.done);
-    } else {
+    } else if ((int)blockIdx.x == m) {
         rng_body(r, U.r);
+    } else if constexpr (APP) {
+        append_body(app);
     }
 }
 
@@ -4501,11 +4546,17 @@ void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s) {
     else hipLaunchKernelGGL(k_act_rows<false>, grid, dim3(1024), 0, s, a);
 }
 
-void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s) {
+void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s, const AppendArgs* app) {
     const bool pf = a.S <= 128 && a.H0 <= 256 && a.H1 <= 256 && a.Aout <= 16;
-    const dim3 grid(m + 1, 1, seeds_z(a.nseeds));
-    if (pf) hipLaunchKernelGGL(k_act_rng<true>, grid, dim3(1024), 0, s, a, r);
-    else hipLaunchKernelGGL(k_act_rng<false>, grid, dim3(1024), 0, s, a, r);
+    const dim3 grid(m + 1 + (app ? 1 : 0), 1, seeds_z(a.nseeds));
+    const AppendArgs none{};
+    if (app) {
+        if (pf) hipLaunchKernelGGL((k_act_rng<true, true>), grid, dim3(1024), 0, s, a, r, *app);
+        else hipLaunchKernelGGL((k_act_rng<false, true>), grid, dim3(1024), 0, s, a, r, *app);
+    } else {
+        if (pf) hipLaunchKernelGGL((k_act_rng<true, false>), grid, dim3(1024), 0, s, a, r, none);
+        else hipLaunchKernelGGL((k_act_rng<false, false>), grid, dim3(1024), 0, s, a, r, none);
+    }
     if (r.pairs != nullptr && r.n_norm > 0)     // the split sampler's polar transform, as launch_rng
         hipLaunchKernelGGL(k_polar, dim3(std::min((r.pcap + 255) / 256, SACX_POLAR_WGS), r.nupd, seeds_z(r.nseeds)),
                            dim3(256), 0, s, r);
@@ -4906,45 +4957,8 @@ void launch_actor_bwd(const ActorBwdArgs& a, hipStream_t s) {
 }
 
 // ==================================================================== k_append
-// TrajectoryBuffer.add (buffers.py:41-71) as a device ring: one workgroup so the
-// control-block update is ordered after every row write.
-__global__ __launch_bounds__(256) void k_append(AppendArgs a_in) {
-    __shared__ int64_t cur_s, start_s;
-    AppendArgs a = a_in;
-    if (a_in.nseeds > 1) {          // packed seeds: seed z's ring and counters, its n source rows
-        const int64_t so = seed_off(a_in.sstride), z = blockIdx.z;
-        a.replay = sr(a.replay, so); a.ctl = sr(a.ctl, so);
-        a.s = a.s + z * a.n * a.S; a.a = a.a + z * a.n * a.A; a.sp = a.sp + z * a.n * a.S;
-        a.r = a.r + z * a.n; a.d = a.d + z * a.n;
-    }
-    if (threadIdx.x == 0) {
-        cur_s = a.ctl->cur_size;
-        start_s = a.ctl->start;
-    }
-    __syncthreads();
-    const int64_t cur = cur_s, start = start_s, cap = a.cap, n = a.n;
-    const int64_t first = n > cap ? n - cap : 0;   // rows that survive truncation
-    const int S = a.S, A = a.A, W = 2 * S + A + 2;
-    for (int64_t e = (int64_t)threadIdx.x + first * W; e < n * W; e += blockDim.x) {
-        const int64_t i = e / W;
-        const int c = (int)(e - i * W);
-        const int64_t phys = (start + cur + i) % cap;
-        float v;
-        if (c < S) v = a.s[i * S + c];
-        else if (c < S + A) v = a.a[i * A + (c - S)];
-        else if (c < 2 * S + A) v = a.sp[i * S + (c - S - A)];
-        else if (c == 2 * S + A) v = a.r[i];
-        else v = a.d[i];
-        a.replay[phys * a.stride + c] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int64_t tot = cur + n;
-        const int64_t drop = tot > cap ? tot - cap : 0;
-        a.ctl->start = (start + drop) % cap;
-        a.ctl->cur_size = tot - drop;
-    }
-}
+// TrajectoryBuffer.add (buffers.py:41-71) as a device ring (append_body, above)
+__global__ __launch_bounds__(256) void k_append(AppendArgs a_in) { append_body(a_in); }
 
 void launch_append(const AppendArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_append, dim3(1, 1, seeds_z(a.nseeds)), dim3(256), 0, s, a);

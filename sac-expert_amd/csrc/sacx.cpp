@@ -252,6 +252,13 @@ struct sacx_handle {
     // k_set_ctl skipped when the control block already holds the values: a speculative step(1)
     // right after another with num_timesteps advanced by ts_increment (the folded alpha.final's
     // add) -- the drop-in loop's cadence.  settle() and resync forget it.
+    // Deferred append (SACX_APP_DEFER): a 1-row append_host right after a one-update step is held
+    // (its row in the pinned staging) and runs as one more workgroup of the next act's k_act_rng
+    // launch -- the drop-in cadence's act -> step(1) -> append; every other entry point queues it
+    // first (flush_append, from settle and the ring's other users)
+    bool app_defer = true;
+    bool app_pending = false;
+    AppendArgs app_args{};
     bool ctl_skip = true;     // SACX_CTL_SKIP=0: always launch it
     bool ctl_known = false;
     int64_t ctl_nts = 0;
@@ -465,6 +472,7 @@ void build_layout(sacx_handle* h) {
     // of converting strided fp32 columns; B % 128 == 0, so the images have no pad positions
     h->xbf = 0;
     if (const char* e = std::getenv("SACX_CTL_SKIP")) h->ctl_skip = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SACX_APP_DEFER")) h->app_defer = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_XBF"))
         if (h->cfg.gemm_bf16 && !h->deep && B % 128 == 0) h->xbf = std::max(0, std::min(2, std::atoi(e)));
     for (int s = 0; s < h->nslot; ++s) {
@@ -2932,7 +2940,19 @@ int run_segments(sacx_handle* h, int n, bool run) {
 // Runs a deferred alpha branch (the tail a one-update graph would have ended with), then undoes
 // a queued speculative draw: the state every entry point but act / append / the speculative
 // step(1) starts from.
+// the deferred append, queued now (sacx_handle::app_defer)
+int flush_append(sacx_handle* h) {
+    if (!h->app_pending) return 0;
+    h->app_pending = false;
+    launch_append(h->app_args, h->stream);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(h->pin_ev, h->stream) != hipSuccess)
+        return fail(h, "deferred append");
+    h->pin_pending = true;
+    return 0;
+}
+
 int settle(sacx_handle* h, bool keep_rng_state = false) {
+    if (flush_append(h)) return -1;
     h->ctl_known = false;
     if (h->alpha_pending >= 0) {
         const int slot = h->alpha_pending;
@@ -3390,6 +3410,7 @@ int sacx_buffer_append(sacx_handle* h, const float* s, const float* a, const flo
     if (!h || !h->bound) return fail(h, "not bound");
     if (n <= 0) return 0;
     if (!s || !a || !r || !sp || !d) return fail(h, "null row pointer");
+    if (flush_append(h)) return -1;           // appends stay in call order
     AppendArgs g{};
     g.replay = h->f("replay"); g.cap = h->cap; g.stride = h->stride; g.S = h->S; g.A = h->A;
     g.s = s; g.a = a; g.r = r; g.sp = sp; g.d = d; g.n = n; g.ctl = h->ctl();
@@ -3463,6 +3484,9 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
     const int S = h->S, A = h->A;
     const int64_t per = 2 * S + A + 2, chunk = STAGE_CAP / per;
     if (chunk <= 0) return fail(h, "a transition is larger than the pinned staging buffer (use sacx_buffer_append)");
+    if (flush_append(h)) return -1;           // (a held one first: appends stay in call order)
+    // the drop-in cadence: hold the row for the next act's launch (sacx_handle::app_defer)
+    const bool defer = n == 1 && h->app_defer && h->last_step_one && h->seeds == 1 && spec_mode(h) && h->act_rng;
     for (int64_t done = 0; done < n; done += chunk) {
         const int64_t m = std::min(chunk, n - done);
         if (stage_begin(h)) return -1;
@@ -3473,6 +3497,17 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
         std::memcpy(p + m * (S + A + 1), sp + done * S, sizeof(float) * m * S);
         std::memcpy(p + m * (2 * S + A + 1), d + done, sizeof(float) * m);
         const float* g = h->pin_dev;
+        if (defer) {
+            AppendArgs& ap = h->app_args;
+            ap = AppendArgs{};
+            ap.replay = h->f("replay"); ap.cap = h->cap; ap.stride = h->stride; ap.S = S; ap.A = A;
+            ap.s = g; ap.a = g + m * S; ap.r = g + m * (S + A); ap.sp = g + m * (S + A + 1); ap.d = g + m * (2 * S + A + 1);
+            ap.n = m; ap.ctl = h->ctl();
+            h->app_pending = true;
+            h->cur_size_host = std::min<int64_t>(h->cur_size_host + m, h->cap);
+            ++h->n_appends;
+            continue;
+        }
         const int rc = sacx_buffer_append(h, g, g + m * S, g + m * (S + A), g + m * (S + A + 1), g + m * (2 * S + A + 1), m);
         if (rc) return rc;
         HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
@@ -3568,15 +3603,23 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
             if (spec_rng_args(h, &r)) return -1;
             ActRowArgs a = act_rows_args(h, g, nullptr, (float*)g + m * S);
             a.done = h->done_dev;
-            launch_act_rng(a, (int)m, r, h->stream);
+            const bool app = h->app_pending;  // the held append as one more workgroup: the draw then
+            if (app) r.size_fixed = h->cur_size_host;   // takes the ring size from the host
+            h->app_pending = false;
+            launch_act_rng(a, (int)m, r, h->stream, app ? &h->app_args : nullptr);
             HIPCHK(h, hipGetLastError());
             h->done_seq += (uint32_t)m;
             HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+            if (app) {
+                HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
+                h->pin_pending = true;
+            }
             if (spec_after_rng(h)) return -1;
             if (act_rows_wait(h)) return -1;
             std::memcpy(act_out + done * A, p + m * S, sizeof(float) * m * A);
             continue;
         }
+        if (flush_append(h)) return -1;
         const bool rows = act_rows_ok(h, m);     // k_act_rows: the host polls the rows' count
         const int rc = actor_act(h, g, m, deterministic, (float*)g + m * S, rows ? h->done_dev : nullptr);
         if (rc) return rc;
@@ -3599,6 +3642,7 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
 int sacx_buffer_append_host_seeds(sacx_handle* h, const float* s, const float* a, const float* r, const float* sp,
                                   const float* d, int64_t n) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (flush_append(h)) return -1;
     if (n <= 0) return 0;
     if (!s || !a || !r || !sp || !d) return fail(h, "null row pointer");
     const int S = h->S, A = h->A, K = h->seeds;
@@ -3627,6 +3671,7 @@ int sacx_buffer_append_host_seeds(sacx_handle* h, const float* s, const float* a
 
 int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32_t deterministic, float* act_out) {
     if (!h || !h->bound) return fail(h, "not bound");
+    if (flush_append(h)) return -1;
     if (n <= 0 || !obs || !act_out) return fail(h, "bad arguments");
     const int S = h->S, A = h->A, K = h->seeds;
     if (n > ACT_ROWS_MAX || h->ln || h->nd[0].D() != 2 || S > ACT_ROWS_DIM || h->H0 > ACT_ROWS_DIM ||
@@ -3769,6 +3814,7 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     // the drop-in loop's one-update steps: the randoms drawn speculatively after the previous
     // step are valid when the ring now holds the size they assumed (nothing else drew meanwhile:
     // every other consumer of the stream undid the draw)
+    if (flush_append(h)) return -1;
     const bool spec_ok = spec_mode(h) && n_steps == 1 && flags == 0;
     const bool use_spec = spec_ok && h->spec_live && h->spec_appends == h->n_appends;
     if (!use_spec && settle(h)) return -1;

@@ -751,7 +751,8 @@ struct ActRowArgs {
 
 // launchers (defined in k_sac.hip)
 void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s);
-void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s);   // rows + the sampler draw beside them
+// rows + the sampler draw beside them (+ a deferred 1-row append as one more workgroup when app is set)
+void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s, const AppendArgs* app = nullptr);
 void launch_gemm(const GemmArgs& a, hipStream_t s);
 void launch_rng(const RngArgs& a, hipStream_t s);
 void launch_gather(const GatherArgs& a, hipStream_t s);
