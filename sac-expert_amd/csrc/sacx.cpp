@@ -3253,10 +3253,10 @@ int sacx_bind(sacx_handle* h, void* arena, uint64_t bytes, void* stream) {
     // cheap sampler takes 8 updates per launch (HC one seed, A/B x2: 13.55k vs 13.38k at 4);
     // an expensive one (Humanoid: 52k normals, 146 us per update) keeps 4, where the graph's
     // ramp and the sampler's lead over the chain favour smaller batches (5.80k vs 5.62k at 8)
-    // Round 6: the one-workgroup k_rng alone (HC) takes 16 updates per launch -- half the cross-stream
-    // waits of the chain on the sampler (HC 2,000 updates 16.22k / 16.30k against 16.15k / 16.17k at 8,
-    // alternating; profiles/r06_ab_nbatch_v1.txt)
-    h->nbatch = h->n_norm <= 16384 ? (h->rng_jump || h->rng_split ? 8 : NSLOT / 2) : 4;
+    // (16 updates per k_rng launch measured within noise of 8 -- HC 2,000 updates 16.22k / 16.30k against
+    // 16.15k / 16.17k, profiles/r06_ab_nbatch_v1.txt -- and slowed the profiled run: 10.2k updates/s
+    // and 7.73 us per k_gemm / k_fwd2 launch under rocprofv3 against 16.1k and 6.92 at 8; SACX_NBATCH=16)
+    h->nbatch = h->n_norm <= 16384 ? 8 : 4;
     if (const char* e = std::getenv("SACX_NBATCH"))   // (k_rng alone takes batches up to half the ring)
         h->nbatch = std::max(1, std::min(h->rng_jump || h->rng_split ? NBATCH_MAX : NSLOT / 2, std::atoi(e)));
     if (const char* e = std::getenv("SACX_MTJ_RAMP")) h->mtj_ramp = std::atoi(e);

@@ -95,6 +95,10 @@ for step in "$@"; do
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof_${arg:-hc}" -o s \
           -- python bench.py --config "${arg:-hc}" --steps 2000 --warmup 200 --no-cpu-baseline --no-roofline --packed-leg 0 > "$log" 2>&1
       rc=$?; echo "[$n prof ${arg:-hc}] rc=$rc $(value "$log")" ;;
+    profenv)    # prof (hc) under one extra environment setting: profenv=VAR=VALUE
+      env "$arg" timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/$OUT/prof_env_$n" -o s \
+          -- python bench.py --config hc --steps 2000 --warmup 200 --no-cpu-baseline --no-roofline --packed-leg 0 > "$log" 2>&1
+      rc=$?; echo "[$n profenv $arg] rc=$rc $(value "$log")" ;;
     pmc)
       CONFIG=${arg:-hc} bash tools/gpu_pmc.sh > "$log" 2>&1
       rc=$?; echo "[$n pmc ${arg:-hc}] rc=$rc"; tail -n 3 "$log" ;;
