@@ -177,3 +177,54 @@ def test_speculative_packed_per_seed_act(gpu_available, monkeypatch):
     assert hits[1] == 0 and hits[0] >= n // 2, hits
     for i, (a, b) in enumerate(zip(*outs)):
         assert np.array_equal(a, b), i
+
+
+def test_held_append_and_skipped_ctl_observed(gpu_available, monkeypatch):
+    """The drop-in cadence's held 1-row append (it runs inside the next act's launch) and the
+    skipped k_set_ctl must be invisible: right after an append_host the ring read through Engine.v
+    holds the row; any other entry point (a multi-update step, a stochastic act, a 2-row append,
+    get_state) queues the held row first; ts_increment changes force the control block's rewrite.
+    The whole run equals SACX_APP_DEFER=0 SACX_CTL_SKIP=0 bit for bit."""
+    from sac_eo.engine import Engine, EngineConfig
+    B, N, n = 64, 500, 40
+    outs = []
+    for opt in ("1", "0"):
+        monkeypatch.setenv("SACX_APP_DEFER", opt)
+        monkeypatch.setenv("SACX_CTL_SKIP", opt)
+        _, st, buf, nrm, _ = make_learner(act="relu", B=B, N=N, seed=6, done_p=0.05)
+        eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=N + 100,
+                                  graph_steps=1, target_update_int=3))
+        load_learner(eng, st, buf, nrm, None, 0.1)
+        eng.rng_set_state(np.random.RandomState(31).get_state())
+        rs = np.random.RandomState(9)
+        t, inc = 0, 1
+        for j in range(n):
+            o, o2 = rs.normal(size=17).astype(np.float32), rs.normal(size=17).astype(np.float32)
+            a = eng.act_host(o, deterministic=(j % 13 != 6))
+            if j == 20:
+                inc = 2                                       # a new ts_increment: the control block is rewritten
+            eng.step(1, num_timesteps=t, ts_increment=inc)
+            t += inc
+            r = np.array([0.1 * j], np.float32)
+            eng.append(o[None], a[None], r, o2[None], np.zeros(1, np.float32))
+            if j % 9 == 4:                                    # the held row is visible at once
+                c = eng.ctl()
+                row = eng.v["replay"][(c["start"] + c["cur_size"] - 1) % (N + 100)].cpu().numpy()
+                assert row[2 * 17 + 6] == r[0] and np.array_equal(row[:17], o)
+            if j == 14:
+                eng.step(2, num_timesteps=t, ts_increment=inc)
+                t += 2 * inc
+            if j == 27:
+                eng.append(np.stack([o2, o]), np.stack([a, a]), np.zeros(2), np.stack([o, o2]), np.zeros(2))
+            if j == 33:
+                eng.rng_get_state()
+        eng.sync()
+        outs.append((eng.stats(n + 2).copy(), eng.v["params"].cpu().numpy().copy(), eng.v["adam_v"].cpu().numpy().copy(),
+                     eng.v["replay"].cpu().numpy().copy(), eng.rng_get_state()[1].copy(),
+                     {k: v for k, v in eng.ctl().items() if k in ("t_sac", "num_timesteps", "cur_size", "start", "step_seq")}))
+        eng.close()
+    for i, (x, y) in enumerate(zip(*outs)):
+        if isinstance(x, dict):
+            assert x == y, (x, y)
+        else:
+            assert np.array_equal(x, y), i
