@@ -74,7 +74,7 @@ def build_engine(cfgd, seeds, device, dp=None, batch=None, weight_seed=None):
     B = batch or cfgd["B"]
     ecfg = EngineConfig(s_dim=S, a_dim=A, hidden=cfgd["hidden"], activation="relu", batch=B,
                         buffer_capacity=cfgd["buffer"], use_expert=cfgd["use_expert"], expert_batch=20,
-                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "128")),
+                        expert_capacity=20, graph_steps=int(os.environ.get("SACX_GRAPH_STEPS", "256")),
                         gemm_bf16=bool(cfgd.get("bf16", False)), seeds=len(seed_list))
     eng = Engine(ecfg, device=device, dp=dp)
     for k, sd in enumerate(seed_list):
