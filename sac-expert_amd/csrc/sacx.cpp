@@ -260,6 +260,9 @@ struct sacx_handle {
     bool app_pending = false;
     AppendArgs app_args{};
     bool ctl_skip = true;     // SACX_CTL_SKIP=0: always launch it
+    // a fork / join graph's first sampler batch (one update) on the chain's own stream, as the segment
+    // graphs do: the chain's first update then does not wait on a cross-queue edge (SACX_G_INLINE0)
+    bool g_inline0 = true;
     bool ctl_known = false;
     int64_t ctl_nts = 0;
     int32_t ctl_inc = 0;
@@ -472,6 +475,7 @@ void build_layout(sacx_handle* h) {
     // of converting strided fp32 columns; B % 128 == 0, so the images have no pad positions
     h->xbf = 0;
     if (const char* e = std::getenv("SACX_CTL_SKIP")) h->ctl_skip = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SACX_G_INLINE0")) h->g_inline0 = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_APP_DEFER")) h->app_defer = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_XBF"))
         if (h->cfg.gemm_bf16 && !h->deep && B % 128 == 0) h->xbf = std::max(0, std::min(2, std::atoi(e)));
@@ -2680,9 +2684,9 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
                 } else {
                     C.gather.nupd = n;
                 }
-                enqueue(C, h, rs);
+                enqueue(C, h, b == 0 && h->g_inline0 ? cs : rs);
             }
-            return hipEventRecord(evR[b], rs);
+            return hipEventRecord(evR[b], b == 0 && h->g_inline0 ? cs : rs);
         };
         std::vector<int> batch_of(G, -1), emit_after(batches.size(), -1);
         for (int b = 0; b < (int)batches.size(); ++b) {
@@ -2693,6 +2697,8 @@ int get_graph(sacx_handle* h, int G, bool with_rng, hipGraphExec_t* out, int ski
             if (emit_after[b] <= 0) {
                 HIPCHK(h, prologue(b));
                 emit_after[b] = -1;                             // drawn once: not again after update 0
+                // batch 0 on the chain's stream (g_inline0): the side stream's draws continue after it
+                if (b == 0 && h->g_inline0) HIPCHK(h, hipStreamWaitEvent(rs, evR[0], 0));
             }
         std::vector<Launch> body;
         for (int j = 0; j < G; ++j) {
