@@ -2988,6 +2988,9 @@ __device__ __forceinline__ uint32_t mt_g(uint32_t a, uint32_t b) {
 #define RNG_RUN 1
 #endif
 __device__ void rng_twist(RngShared& S, int w0, int w1) {
+#ifdef SACX_DIAG_NOTWIST
+    return;   // diagnostic builds only (tools/build_variant.sh): wrong words, the twist's cost removed
+#endif
     const int t = threadIdx.x;
     int n0 = w0;
     while (n0 < w1 && n0 < 1078) {               // 227-wide steps (history from the key only)
@@ -3183,7 +3186,11 @@ __device__ __forceinline__ void rng_body(const RngArgs& a_in, RngShared& S) {
                         S.has = 1;
                     }
                 } else {
+#ifdef SACX_DIAG_NOPOLAR
+                    const double f = r2[k];   // diagnostic builds only: the transform's cost removed
+#else
                     const double f = sqrt(-2.0 * log(r2[k]) / r2[k]);
+#endif
                     out_norm[o] = (float)(f * x2[k]);
                     if (o + 1 < a.n_norm) {
                         out_norm[o + 1] = (float)(f * x1[k]);
@@ -3242,14 +3249,10 @@ __global__ __launch_bounds__(RNG_THREADS) void k_rng(RngArgs a) {
 #ifndef SACX_POLAR_WGS
 #define SACX_POLAR_WGS 8
 #endif
-__global__ __launch_bounds__(256) void k_polar(RngArgs a) {
-    const int64_t so = seed_off(a.sstride);
-    const int u = blockIdx.y;
-    const int oi = sr(a.pairs_oi, so)[u];
-    const int np = (a.n_norm - oi + 1) >> 1;
-    const uint32_t* const pairs = sr(a.pairs, so) + (size_t)u * a.pcap * 4;
-    float* const out = (float*)((char*)sr(a.out_norm, so) + (int64_t)u * a.slot_bytes);
-    for (int j = blockIdx.x * 256 + threadIdx.x; j < np; j += gridDim.x * 256) {
+// pairs j = j0, j0 + stride, ... of one update: its normals from the leading cached one (oi) on
+__device__ __forceinline__ void polar_pairs(const uint32_t* pairs, int oi, int n_norm, float* out, int j0, int stride) {
+    const int np = (n_norm - oi + 1) >> 1;
+    for (int j = j0; j < np; j += stride) {
         const uint4 w = *reinterpret_cast<const uint4*>(pairs + (size_t)j * 4);
         const double u1 = ((double)(int32_t)(w.x >> 5) * 67108864.0 + (double)(int32_t)(w.y >> 6)) / 9007199254740992.0;
         const double u2 = ((double)(int32_t)(w.z >> 5) * 67108864.0 + (double)(int32_t)(w.w >> 6)) / 9007199254740992.0;
@@ -3259,8 +3262,16 @@ __global__ __launch_bounds__(256) void k_polar(RngArgs a) {
         const double f = sqrt(-2.0 * log(r2) / r2);
         const int o = oi + 2 * j;
         out[o] = (float)(f * x2);
-        if (o + 1 < a.n_norm) out[o + 1] = (float)(f * x1);
+        if (o + 1 < n_norm) out[o + 1] = (float)(f * x1);
     }
+}
+
+__global__ __launch_bounds__(256) void k_polar(RngArgs a) {
+    const int64_t so = seed_off(a.sstride);
+    const int u = blockIdx.y;
+    polar_pairs(sr(a.pairs, so) + (size_t)u * a.pcap * 4, sr(a.pairs_oi, so)[u], a.n_norm,
+                (float*)((char*)sr(a.out_norm, so) + (int64_t)u * a.slot_bytes), blockIdx.x * 256 + threadIdx.x,
+                gridDim.x * 256);
 }
 
 // ==================================================================== segmented sampler (k_mtj_*)
@@ -3941,6 +3952,12 @@ void launch_rng(const RngArgs& a0, hipStream_t s) {
 // ==================================================================== k_gather
 // one wave per sampled row (then per expert row); rows are [s | a | sp | r | d]
 __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
+    const int rwgs = (ga.B + ga.ne + 3) >> 2;
+    if ((int)blockIdx.x >= rwgs) {      // the speculative draw's polar transform (one update, one seed)
+        polar_pairs(ga.pairs, ga.pairs_oi[0], ga.n_norm, ga.norm, ((int)blockIdx.x - rwgs) * 256 + threadIdx.x,
+                    ga.polar_wgs * 256);
+        return;
+    }
     const int wave = wave_id(), lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + wave;
     // slot (ga.slot + blockIdx.y): every slot buffer sits at a fixed distance from slot 0's
@@ -4022,7 +4039,8 @@ __global__ __launch_bounds__(256) void k_gather(GatherArgs ga) {
 
 void launch_gather(const GatherArgs& a, hipStream_t s) {
     const int rows = a.B + a.ne;
-    hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4, a.nupd > 0 ? a.nupd : 1, seeds_z(a.nseeds)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gather, dim3((rows + 3) / 4 + a.polar_wgs, a.nupd > 0 ? a.nupd : 1, seeds_z(a.nseeds)),
+                       dim3(256), 0, s, a);
 }
 
 // one wave: alpha Adam + clamp and the statistics row of the update
@@ -4532,7 +4550,9 @@ __global__ __launch_bounds__(1024) void k_act_rng(ActRowArgs g, RngArgs r, Appen
         act_rows_body<PF>(g, blockIdx.x, U.a);
         act_rows_done(g.done);
     } else if ((int)blockIdx.x == m) {
+#ifndef SACX_DIAG_NODRAW
         rng_body(r, U.r);
+#endif
     } else if constexpr (APP) {
         append_body(app);
     }
@@ -4546,7 +4566,7 @@ void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s) {
     else hipLaunchKernelGGL(k_act_rows<false>, grid, dim3(1024), 0, s, a);
 }
 
-void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s, const AppendArgs* app) {
+void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s, const AppendArgs* app, bool polar) {
     const bool pf = a.S <= 128 && a.H0 <= 256 && a.H1 <= 256 && a.Aout <= 16;
     const dim3 grid(m + 1 + (app ? 1 : 0), 1, seeds_z(a.nseeds));
     const AppendArgs none{};
@@ -4557,7 +4577,7 @@ void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s,
         if (pf) hipLaunchKernelGGL((k_act_rng<true, false>), grid, dim3(1024), 0, s, a, r, none);
         else hipLaunchKernelGGL((k_act_rng<false, false>), grid, dim3(1024), 0, s, a, r, none);
     }
-    if (r.pairs != nullptr && r.n_norm > 0)     // the split sampler's polar transform, as launch_rng
+    if (polar && r.pairs != nullptr && r.n_norm > 0)   // the split sampler's polar transform, as launch_rng
         hipLaunchKernelGGL(k_polar, dim3(std::min((r.pcap + 255) / 256, SACX_POLAR_WGS), r.nupd, seeds_z(r.nseeds)),
                            dim3(256), 0, s, r);
 }

@@ -182,6 +182,12 @@ struct sacx_handle {
     std::vector<std::pair<const float*, const float*>> abf_written;   // plan build: ranges a wired producer stores
     bool rng_split = false;   // k_rng + k_polar (rng.pairs): the polar transform spread over the GPU
     int pcap = 0;             // polar pairs per update (rng.pairs rows per update)
+    // the drop-in loop's draw beside the act (k_act_rng, plain SAC, no split sampler) stores its
+    // accepted pairs' words in rng.spairs and the gather queued behind it computes the normals on
+    // spare workgroups: the fp64 log / sqrt leave the draw's one workgroup (SACX_SPEC_POLAR)
+    bool spec_polar = false;
+    bool spec_polar_live = false;   // the queued speculative draw stored pairs
+    int spcap = 0;
     bool rng_jump = false;    // segmented sampler (k_mtj_*): the update sampler's launches
     int jL = 0;               // its segment length (words)
     int jsmax = 0;            // segments its work area holds
@@ -436,6 +442,13 @@ void build_layout(sacx_handle* h) {
         h->pcap = (h->n_norm + 1) / 2;
         h->add("rng.pairs", (int64_t)NBATCH_MAX * h->pcap, 4, SACX_U32, SACX_ROLE_WORK);
         h->add("rng.pairs_oi", 1, NBATCH_MAX, SACX_I32, SACX_ROLE_WORK);
+    }
+    h->spec_polar = !h->rng_split && !h->cfg.use_expert && h->n_norm > 0;
+    if (const char* e = std::getenv("SACX_SPEC_POLAR")) h->spec_polar = h->spec_polar && std::atoi(e) != 0;
+    if (h->spec_polar) {
+        h->spcap = (h->n_norm + 1) / 2;
+        h->add("rng.spairs", h->spcap, 4, SACX_U32, SACX_ROLE_WORK);
+        h->add("rng.spairs_oi", 1, 1, SACX_I32, SACX_ROLE_WORK);
     }
     // Segmented sampler (k_mtj_*): a sampler batch of many words (Humanoid: ~135k per update)
     // is twisted as ~16 segments of L words from jumped-ahead windows and ranked over the GPU
@@ -3565,7 +3578,21 @@ static int spec_rng_args(sacx_handle* h, RngArgs* out) {
 static int spec_after_rng(sacx_handle* h) {
     if (!h->cfg.use_expert)
         for (const Launch& L : h->plan[h->spec_slot])
-            if (L.kind == Launch::GATHER) enqueue(L, h, h->stream);
+            if (L.kind == Launch::GATHER) {
+                if (!h->spec_polar_live) {
+                    enqueue(L, h, h->stream);
+                    continue;
+                }
+                Launch G = L;                  // + the draw's polar transform (sacx_handle::spec_polar)
+                G.gather.pairs = h->ptr<uint32_t>("rng.spairs");
+                G.gather.pairs_oi = h->ptr<int32_t>("rng.spairs_oi");
+                for (const Launch& R : h->plan[h->spec_slot])
+                    if (R.kind == Launch::RNG) G.gather.norm = R.rng.out_norm;
+                G.gather.n_norm = h->n_norm;
+                G.gather.polar_wgs = std::min(16, (h->spcap + 255) / 256);
+                enqueue(G, h, h->stream);
+            }
+    h->spec_polar_live = false;
     HIPCHK(h, hipGetLastError());
     h->spec_live = true;
     h->spec_size = h->cur_size_host;
@@ -3629,7 +3656,13 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
             const bool app = h->app_pending;  // the held append as one more workgroup: the draw then
             if (app) r.size_fixed = h->cur_size_host;   // takes the ring size from the host
             h->app_pending = false;
-            launch_act_rng(a, (int)m, r, h->stream, app ? &h->app_args : nullptr);
+            if (h->spec_polar) {
+                r.pairs = h->ptr<uint32_t>("rng.spairs");
+                r.pairs_oi = h->ptr<int32_t>("rng.spairs_oi");
+                r.pcap = h->spcap;
+                h->spec_polar_live = true;
+            }
+            launch_act_rng(a, (int)m, r, h->stream, app ? &h->app_args : nullptr, !h->spec_polar);
             HIPCHK(h, hipGetLastError());
             h->done_seq += (uint32_t)m;
             HIPCHK(h, hipEventRecord(h->act_ev, h->stream));

@@ -544,6 +544,14 @@ struct GatherArgs {
     // config C5: the critic rows' transposed bf16 image (columns c < S + A of Xq as rows of
     // wbf_ld_of(B) positions, wbf_pos layout): critic.adam's layer-0 A operand; null: not written
     uint16_t* xbfq;
+    // the drop-in loop's speculative draw (k_act_rng, plain SAC, one update): the draw stored its
+    // accepted polar pairs' words (pairs, pairs_oi[0]); polar_wgs more workgroups turn them into the
+    // slot's n_norm normals at norm with k_polar's arithmetic.  polar_wgs 0: none
+    const uint32_t* pairs;
+    const int32_t* pairs_oi;
+    float* norm;
+    int32_t n_norm;
+    int32_t polar_wgs;
     // packed seeds (sacx_config.seeds): grid z = nseeds independent learners whose arena blocks
     // sit sstride bytes apart; every arena pointer is relocated by blockIdx.z * sstride
     int64_t sstride;
@@ -752,7 +760,7 @@ struct ActRowArgs {
 // launchers (defined in k_sac.hip)
 void launch_act_rows(const ActRowArgs& a, int m, hipStream_t s);
 // rows + the sampler draw beside them (+ a deferred 1-row append as one more workgroup when app is set)
-void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s, const AppendArgs* app = nullptr);
+void launch_act_rng(const ActRowArgs& a, int m, const RngArgs& r, hipStream_t s, const AppendArgs* app = nullptr, bool polar = true);
 void launch_gemm(const GemmArgs& a, hipStream_t s);
 void launch_rng(const RngArgs& a, hipStream_t s);
 void launch_gather(const GatherArgs& a, hipStream_t s);

@@ -135,6 +135,10 @@ for step in "$@"; do
     benchv)     # the 2,000-update HC bench with a variant library: benchv=<tools/libvar name>
       SACX_LIBPATH=$PWD/tools/libvar/libsacx_$arg.so timeout -k 10 300 python bench.py --steps 2000 --warmup 200 --no-cpu-baseline > "$log" 2>&1
       rc=$?; echo "[$n benchv $arg] rc=$rc $(value "$log")" ;;
+    dropin)     # host time per drop-in iteration: dropin[=<tools/libvar name>]
+      if [ -n "$arg" ]; then lp=$PWD/tools/libvar/libsacx_$arg.so; else lp=$PWD/sac-expert_amd/lib/libsacx.so; fi
+      SACX_LIBPATH=$lp timeout -k 10 200 python tools/dropin_trace.py host > "$log" 2>&1
+      rc=$?; echo "[$n dropin $arg] rc=$rc $(tail -n 1 "$log")" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
