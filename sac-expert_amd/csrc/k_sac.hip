@@ -4530,6 +4530,7 @@ __device__ void append_body(const AppendArgs& a_in) {
         a.ctl->start = (start + drop) % cap;
         a.ctl->cur_size = tot - drop;
     }
+    act_rows_done(a.done);   // (uniform: every thread reaches it)
 }
 
 // The drop-in loop's deterministic act with the next update's sampler draw beside it: the

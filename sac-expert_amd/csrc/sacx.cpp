@@ -247,6 +247,12 @@ struct sacx_handle {
     bool spec_enabled = true;  // SACX_SPEC=0: off
     bool spec_live = false;    // a speculative draw is queued
     bool last_step_one = false;  // the last sacx_sac_step was a plain one-update step
+    // k_act_rng's held append signals its reads of the staging rows through done_host[1] instead of
+    // an event recorded behind it (SACX_APP_CTR); app_seq = the count the host expects
+    bool app_ctr = true;
+    bool app_ctr_pending = false;
+    uint32_t app_seq = 0;
+    bool act_ev_live = true;     // act_ev marks the last act (false: nothing recorded, poll only)
     int64_t spec_size = 0;     // the ring size it assumed
     int64_t spec_hits = 0;     // one-update steps that used a speculative draw (sacx_spec_hits)
     int spec_slot = 1;         // the slot the queued draw fills (1 or 2: never the pending alpha's)
@@ -488,6 +494,7 @@ void build_layout(sacx_handle* h) {
     // of converting strided fp32 columns; B % 128 == 0, so the images have no pad positions
     h->xbf = 0;
     if (const char* e = std::getenv("SACX_CTL_SKIP")) h->ctl_skip = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SACX_APP_CTR")) h->app_ctr = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_G_INLINE0")) h->g_inline0 = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_APP_DEFER")) h->app_defer = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_XBF"))
@@ -3469,6 +3476,7 @@ static int stage_alloc(sacx_handle* h) {
         HIPCHK(h, hipHostMalloc((void**)&h->done_host, 64, hipHostMallocMapped));
         HIPCHK(h, hipHostGetDevicePointer((void**)&h->done_dev, h->done_host, 0));
         __atomic_store_n(h->done_host, 0u, __ATOMIC_RELEASE);
+        __atomic_store_n(h->done_host + 1, 0u, __ATOMIC_RELEASE);
         h->done_seq = 0;
     }
     return 0;
@@ -3494,7 +3502,7 @@ static int act_rows_wait(sacx_handle* h) {
     for (uint32_t it = 1; !reached(); ++it) {
         cpu_relax();
         if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > ACT_SPIN) {
-            const hipError_t e = hipEventSynchronize(h->act_ev);
+            const hipError_t e = h->act_ev_live ? hipEventSynchronize(h->act_ev) : hipStreamSynchronize(h->stream);
             if (e != hipSuccess || !reached()) {
                 h->done_seq = __atomic_load_n(h->done_host, __ATOMIC_ACQUIRE);
                 return fail(h, e != hipSuccess ? "act event" : "act rows finished without their completion count");
@@ -3507,6 +3515,20 @@ static int act_rows_wait(sacx_handle* h) {
 // the append half: waits until its last reader (a k_append) has finished
 static int stage_begin(sacx_handle* h) {
     if (stage_alloc(h)) return -1;
+    if (h->app_ctr_pending) {           // the held append's workgroup has read the rows
+        const uint32_t target = h->app_seq;
+        auto reached = [&]() { return (int32_t)(__atomic_load_n(h->done_host + 1, __ATOMIC_ACQUIRE) - target) >= 0; };
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t it = 1; !reached(); ++it) {
+            cpu_relax();
+            if ((it & 255) == 0 && std::chrono::steady_clock::now() - t0 > ACT_SPIN) {
+                HIPCHK(h, hipStreamSynchronize(h->stream));
+                if (!reached()) return fail(h, "held append finished without its completion count");
+                break;
+            }
+        }
+        h->app_ctr_pending = false;
+    }
     if (h->pin_pending) HIPCHK(h, hipEventSynchronize(h->pin_ev));   // its last reader has finished
     h->pin_pending = false;
     return 0;
@@ -3662,11 +3684,21 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
                 r.pcap = h->spcap;
                 h->spec_polar_live = true;
             }
-            launch_act_rng(a, (int)m, r, h->stream, app ? &h->app_args : nullptr, !h->spec_polar);
+            AppendArgs ag = h->app_args;
+            if (app && h->app_ctr) {
+                ag.done = h->done_dev + 1;
+                ++h->app_seq;
+                h->app_ctr_pending = true;
+            }
+            launch_act_rng(a, (int)m, r, h->stream, app ? &ag : nullptr, !h->spec_polar);
             HIPCHK(h, hipGetLastError());
             h->done_seq += (uint32_t)m;
-            HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
-            if (app) {
+            // no event markers behind the launch: each one held the next kernel back ~7-10 us on the
+            // device (r06_dropin_ab_v2.txt).  The host polls the rows' count (act_poll) and the held
+            // append's own count (stage_begin)
+            if (!h->act_poll) HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+            h->act_ev_live = !h->act_poll;
+            if (app && !h->app_ctr) {
                 HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
                 h->pin_pending = true;
             }
@@ -3681,6 +3713,7 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
         if (rc) return rc;
         if (rows) h->done_seq += (uint32_t)m;    // only once the launch that counts them is queued
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+        h->act_ev_live = true;
         // the drop-in loop steps next: its randoms are drawn while the host has the action
         if (done + m >= n && spec && spec_draw(h)) return -1;
         if (rows) {
@@ -3776,12 +3809,14 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         HIPCHK(h, hipGetLastError());
         h->done_seq += (uint32_t)(n * K);
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+        h->act_ev_live = true;
         if (spec_after_rng(h)) return -1;
     } else {
         launch_act_rows(a, (int)n, h->stream);
         HIPCHK(h, hipGetLastError());
         h->done_seq += (uint32_t)(n * K);
         HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
+        h->act_ev_live = true;
         if (spec && spec_draw(h)) return -1;
     }
     if (act_rows_wait(h)) return -1;

@@ -597,6 +597,9 @@ struct AppendArgs {
     const float *s, *a, *r, *sp, *d;
     int64_t n;
     Ctl* ctl;
+    // pinned counter the workgroup bumps once it has read the source rows (k_act_rng's held
+    // append: the host reuses the staging buffer without an event marker); null: none
+    uint32_t* done;
     // packed seeds (sacx_buffer_append_host_seeds): grid z = seed; replay / ctl move by z * sstride,
     // the source rows by z * n rows (arrays [seeds, n, ...])
     int64_t sstride;

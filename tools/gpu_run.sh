@@ -139,6 +139,14 @@ for step in "$@"; do
       if [ -n "$arg" ]; then lp=$PWD/tools/libvar/libsacx_$arg.so; else lp=$PWD/sac-expert_amd/lib/libsacx.so; fi
       SACX_LIBPATH=$lp timeout -k 10 200 python tools/dropin_trace.py host > "$log" 2>&1
       rc=$?; echo "[$n dropin $arg] rc=$rc $(tail -n 1 "$log")" ;;
+    dropinenv)  # dropin under one extra environment setting: dropinenv=VAR=VALUE
+      env "$arg" timeout -k 10 200 python tools/dropin_trace.py host > "$log" 2>&1
+      rc=$?; echo "[$n dropinenv $arg] rc=$rc $(tail -n 1 "$log")" ;;
+    dropintr)   # kernel trace of the drop-in loop (tools/dropin_trace.py), optional env: dropintr=VAR=VALUE
+      ev=${arg:-SACX_NONE=0}
+      env "$ev" timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$PWD/$OUT/dtr$n" -o d \
+          -- python tools/dropin_trace.py run > "$log" 2>&1 && python tools/dropin_trace.py "$OUT/dtr$n" >> "$log" 2>&1
+      rc=$?; echo "[$n dropintr $arg] rc=$rc"; grep -A3 "iterations:" "$log" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
