@@ -178,6 +178,13 @@ struct sacx_handle {
     bool wbf_attach = false;
     bool wbf_live = false;    // the update plans read / maintain the shadows (refreshed per step call)
     hipEvent_t seg_start = nullptr;   // run_segments: the call's start on the bound stream (before set_ctl)
+    // run_segments' cross-stream edges as stream memory operations on signal memory instead of
+    // event markers (SACX_SEG_SIG: 1 the side stream's batch-ready edges, 2 (default) also batch
+    // 0's, whose marker on the bound stream held segment 0 back: the driver's command 16.00-16.03k
+    // -> 16.20-16.23k, r06_ab_seg_sig_v1.txt); 0 where the device lacks stream wait-value
+    int seg_sig = 2;
+    uint64_t* sig_mem[2] = {nullptr, nullptr};   // batches drawn (side stream), batch 0 drawn (bound stream)
+    uint64_t sig_seq[2] = {0, 0};
     std::vector<std::string> abf_segs;          // activation segments with a bf16 shadow ("abf.<name>")
     std::vector<std::pair<const float*, const float*>> abf_written;   // plan build: ranges a wired producer stores
     bool rng_split = false;   // k_rng + k_polar (rng.pairs): the polar transform spread over the GPU
@@ -495,6 +502,7 @@ void build_layout(sacx_handle* h) {
     h->xbf = 0;
     if (const char* e = std::getenv("SACX_CTL_SKIP")) h->ctl_skip = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_APP_CTR")) h->app_ctr = std::atoi(e) != 0;
+    if (const char* e = std::getenv("SACX_SEG_SIG")) h->seg_sig = std::atoi(e);
     if (const char* e = std::getenv("SACX_G_INLINE0")) h->g_inline0 = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_APP_DEFER")) h->app_defer = std::atoi(e) != 0;
     if (const char* e = std::getenv("SACX_XBF"))
@@ -2905,6 +2913,12 @@ std::vector<std::pair<int, int>> segment_batches(const sacx_handle* h, int n) {
     return batches;
 }
 
+// SACX_SEG_INLINE0 (default 1): batch 0 of a segmented call drawn on the bound stream
+static int seg_inline0() {
+    static const int v = [] { const char* e = std::getenv("SACX_SEG_INLINE0"); return e ? std::atoi(e) : 1; }();
+    return v;
+}
+
 int run_segments(sacx_handle* h, int n, bool run) {
     const auto batches = segment_batches(h, n);
     const int nb = (int)batches.size(), nslot = h->nslot;
@@ -2931,6 +2945,22 @@ int run_segments(sacx_handle* h, int n, bool run) {
     hipEvent_t* evR = h->events.data();          // batch b drawn
     hipEvent_t* evE = h->events.data() + nb;     // segment k done
     hipStream_t rs = h->rng_stream;
+    const int first_inline = seg_inline0();
+    const int sig = h->seg_sig;
+    if (sig && !h->sig_mem[0]) {
+        int dev = 0, can = 0;
+        HIPCHK(h, hipGetDevice(&dev));
+        if (hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, dev) != hipSuccess || !can) {
+            h->seg_sig = 0;
+            return run_segments(h, n, run);
+        }
+        for (int w = 0; w < 2; ++w) {
+            HIPCHK(h, hipExtMallocWithFlags((void**)&h->sig_mem[w], sizeof(uint64_t), hipMallocSignalMemory));
+            HIPCHK(h, hipStreamWriteValue64(h->stream, h->sig_mem[w], 0, 0));
+        }
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    const uint64_t base0 = h->sig_seq[0];
     auto draw = [&](int b, hipStream_t st) {
         const int j0 = batches[b].first, n_b = batches[b].second - j0;
         for (const Launch& L : h->plan[j0 % nslot]) {
@@ -2944,27 +2974,37 @@ int run_segments(sacx_handle* h, int n, bool run) {
             }
             enqueue(C, h, st);
         }
-        return hipEventRecord(evR[b], st);
+        if (sig == 0 || (b == 0 && st == h->stream && sig < 2)) return hipEventRecord(evR[b], st);
+        const int w = st == h->stream ? 1 : 0;
+        const hipError_t e = hipStreamWriteValue64(st, h->sig_mem[w], h->sig_seq[w] + 1, 0);
+        if (e == hipSuccess) ++h->sig_seq[w];   // (the waits count on every queued write)
+        return e;
+    };
+    auto wait_batch = [&](hipStream_t st, int b) {   // st waits for batch b's draw
+        if (sig == 0 || (b == 0 && st == rs && sig < 2)) return hipStreamWaitEvent(st, evR[b], 0);
+        // batch b's value: batch 0 (bound stream) is the one write of sig_mem[1] this call; side
+        // stream batch b the (b - first)-th write of sig_mem[0] after this call's base
+        const int w = b == 0 && first_inline ? 1 : 0;
+        const uint64_t v = w ? h->sig_seq[1] : base0 + (uint64_t)(b - (first_inline ? 1 : 0)) + 1;
+        return hipStreamWaitValue64(st, h->sig_mem[w], v, hipStreamWaitValueGte, ~0ull);
     };
     // the sampler follows the bound stream's earlier work but not this call's k_set_ctl (it writes
     // num_timesteps / ts_increment, which the sampler does not read): sacx_sac_step recorded
     // seg_start before launching it
     // SACX_SEG_INLINE0 (default 1): warm step(20) 1,296 vs 1,320 us, the driver's command +0.3 %
     // (r04_seg_inline0_v1.txt)
-    const char* ie = std::getenv("SACX_SEG_INLINE0");
-    const int first_inline = ie ? std::atoi(ie) : 1;
     if (first_inline) {
         // batch 0 on the bound stream itself, right before segment 0: no cross-stream hop on the
         // call's critical path; the side stream continues the draws after it
         HIPCHK(h, draw(0, h->stream));
-        HIPCHK(h, hipStreamWaitEvent(rs, evR[0], 0));
+        HIPCHK(h, wait_batch(rs, 0));
     } else {
         HIPCHK(h, hipStreamWaitEvent(rs, h->seg_start, 0));
     }
     for (int b = first_inline ? 1 : 0; b < nb; ++b)
         if (due_seg[b] < 0) HIPCHK(h, draw(b, rs));
     for (int k = 0; k < nb; ++k) {
-        if (k > 0 || !first_inline) HIPCHK(h, hipStreamWaitEvent(h->stream, evR[k], 0));
+        if (k > 0 || !first_inline) HIPCHK(h, wait_batch(h->stream, k));
         HIPCHK(h, hipGraphLaunch(gx[k], h->stream));
         bool rec = false;
         for (int b = 0; b < nb; ++b)
@@ -3192,6 +3232,8 @@ void sacx_destroy(sacx_handle* h) {
     if (h->rng_stream) (void)hipStreamSynchronize(h->rng_stream);
     if (h->act_ev) (void)hipEventDestroy(h->act_ev);
     if (h->seg_start) (void)hipEventDestroy(h->seg_start);
+    for (uint64_t* p : h->sig_mem)
+        if (p) (void)hipFree(p);
     for (auto& kv : h->graphs) (void)hipGraphExecDestroy(kv.second);
     for (auto& m : h->mgraphs)
         for (auto& kv : m) (void)hipGraphExecDestroy(kv.second);
@@ -3915,8 +3957,10 @@ int sacx_sac_step(sacx_handle* h, int64_t n_steps, int64_t num_timesteps, int32_
     const int prev = use_spec ? h->alpha_pending : -1;
     const bool segs = !use_spec && !(flags & SACX_STEP_EAGER) && use_segments(h, n_steps, flags);
     if (segs) {
+        // (only the side-stream batch 0 waits for it: a marker on the bound stream otherwise costs the
+        // call's first launches, r06_ab_seg_sig_v1.txt)
         if (!h->seg_start) HIPCHK(h, hipEventCreateWithFlags(&h->seg_start, hipEventDisableTiming));
-        HIPCHK(h, hipEventRecord(h->seg_start, h->stream));
+        if (!seg_inline0()) HIPCHK(h, hipEventRecord(h->seg_start, h->stream));
     }
     wbf_refresh(h, h->stream);
     const int64_t nts_set = num_timesteps - (prev >= 0 ? ts_increment : 0);

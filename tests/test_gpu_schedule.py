@@ -209,6 +209,25 @@ def test_short_graphs_equal_eager(gpu_available, monkeypatch, n, nslot):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("sig", ["0", "1"])
+def test_segment_edges_events_or_signals(gpu_available, monkeypatch, sig):
+    """run_segments' cross-stream edges as event markers (SACX_SEG_SIG=0), side-stream edges on
+    signal memory (1), or every edge on signal memory (2, the default, test_short_graphs_equal_eager):
+    step(20) twice == eager launches, bit for bit, RNG state included."""
+    monkeypatch.setenv("SACX_SEG_SIG", sig)
+    outs = []
+    for eager in (True, False):
+        eng, *_ = make_pair(act="relu", B=256, seed=32, graph_steps=128)
+        eng.rng_set_state(np.random.RandomState(13).get_state())
+        for _ in range(2):
+            eng.step(20, eager=eager)
+        eng.sync()
+        outs.append((eng.stats(40).copy(), eng.v["params"].cpu().numpy().copy(), eng.rng_get_state()[1].copy()))
+        eng.close()
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
 def test_segment_graphs_never_replay_timing_graphs(gpu_available):
     """The graph cache holds the G-update graphs of sacx_time_graph (keyed by G and the skipped
     kernel) beside the single-stream segment graphs of step(n); with graph_steps = 4 the 4-update
