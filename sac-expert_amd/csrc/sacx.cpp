@@ -3010,8 +3010,14 @@ int run_segments(sacx_handle* h, int n, bool run) {
         for (int b = 0; b < nb; ++b)
             if (due_seg[b] == k) {
                 if (!rec) {
-                    HIPCHK(h, hipEventRecord(evE[k], h->stream));
-                    HIPCHK(h, hipStreamWaitEvent(rs, evE[k], 0));
+                    if (sig >= 2) {     // segment k done, as a write on the bound stream
+                        HIPCHK(h, hipStreamWriteValue64(h->stream, h->sig_mem[1], h->sig_seq[1] + 1, 0));
+                        ++h->sig_seq[1];
+                        HIPCHK(h, hipStreamWaitValue64(rs, h->sig_mem[1], h->sig_seq[1], hipStreamWaitValueGte, ~0ull));
+                    } else {
+                        HIPCHK(h, hipEventRecord(evE[k], h->stream));
+                        HIPCHK(h, hipStreamWaitEvent(rs, evE[k], 0));
+                    }
                     rec = true;
                 }
                 HIPCHK(h, draw(b, rs));
