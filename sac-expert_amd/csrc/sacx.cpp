@@ -256,7 +256,7 @@ struct sacx_handle {
     bool last_step_one = false;  // the last sacx_sac_step was a plain one-update step
     // k_act_rng's held append signals its reads of the staging rows through done_host[1] instead of
     // an event recorded behind it (SACX_APP_CTR); app_seq = the count the host expects
-    bool app_ctr = true;
+    bool app_ctr = true;         // (and the acts record act_ev only when the host does not poll)
     bool app_ctr_pending = false;
     uint32_t app_seq = 0;
     bool act_ev_live = true;     // act_ev marks the last act (false: nothing recorded, poll only)
@@ -3027,14 +3027,29 @@ int run_segments(sacx_handle* h, int n, bool run) {
 }
 
 // the deferred append, queued now (sacx_handle::app_defer)
+// An append whose source rows are the pinned staging buffer: its workgroups (one per seed) bump
+// done_host[1] once they have read them, and the next staging reuse polls that count (stage_begin)
+// instead of waiting for an event marker recorded behind the launch (SACX_APP_CTR)
+static int launch_staged_append(sacx_handle* h, AppendArgs g) {
+    if (h->app_ctr) {
+        g.done = h->done_dev + 1;
+        launch_append(g, h->stream);
+        if (hipGetLastError() != hipSuccess) return fail(h, "append launch");
+        h->app_seq += (uint32_t)(g.nseeds > 1 ? g.nseeds : 1);
+        h->app_ctr_pending = true;
+        return 0;
+    }
+    launch_append(g, h->stream);
+    if (hipGetLastError() != hipSuccess || hipEventRecord(h->pin_ev, h->stream) != hipSuccess)
+        return fail(h, "append launch");
+    h->pin_pending = true;
+    return 0;
+}
+
 int flush_append(sacx_handle* h) {
     if (!h->app_pending) return 0;
     h->app_pending = false;
-    launch_append(h->app_args, h->stream);
-    if (hipGetLastError() != hipSuccess || hipEventRecord(h->pin_ev, h->stream) != hipSuccess)
-        return fail(h, "deferred append");
-    h->pin_pending = true;
-    return 0;
+    return launch_staged_append(h, h->app_args);
 }
 
 // Queues a held append, runs a deferred alpha branch (the tail a one-update graph would have ended
@@ -3614,10 +3629,13 @@ int sacx_buffer_append_host(sacx_handle* h, const float* s, const float* a, cons
             ++h->n_appends;
             continue;
         }
-        const int rc = sacx_buffer_append(h, g, g + m * S, g + m * (S + A), g + m * (S + A + 1), g + m * (2 * S + A + 1), m);
-        if (rc) return rc;
-        HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
-        h->pin_pending = true;
+        AppendArgs ag{};
+        ag.replay = h->f("replay"); ag.cap = h->cap; ag.stride = h->stride; ag.S = S; ag.A = A;
+        ag.s = g; ag.a = g + m * S; ag.r = g + m * (S + A); ag.sp = g + m * (S + A + 1); ag.d = g + m * (2 * S + A + 1);
+        ag.n = m; ag.ctl = h->ctl();
+        if (launch_staged_append(h, ag)) return -1;
+        h->cur_size_host = std::min<int64_t>(h->cur_size_host + m, h->cap);
+        ++h->n_appends;
     }
     return 0;
 }
@@ -3744,8 +3762,8 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
             // no event markers behind the launch: each one held the next kernel back ~7-10 us on the
             // device (r06_dropin_ab_v2.txt).  The host polls the rows' count (act_poll) and the held
             // append's own count (stage_begin)
-            if (!h->act_poll) HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
-            h->act_ev_live = !h->act_poll;
+            h->act_ev_live = !(h->act_poll && h->app_ctr);
+            if (h->act_ev_live) HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
             if (app && !h->app_ctr) {
                 HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
                 h->pin_pending = true;
@@ -3760,8 +3778,8 @@ int sacx_actor_act_host(sacx_handle* h, const float* obs, int64_t n, int32_t det
         const int rc = actor_act(h, g, m, deterministic, (float*)g + m * S, rows ? h->done_dev : nullptr);
         if (rc) return rc;
         if (rows) h->done_seq += (uint32_t)m;    // only once the launch that counts them is queued
-        HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
-        h->act_ev_live = true;
+        h->act_ev_live = !(rows && h->act_poll && h->app_ctr);   // (a marker holds the next launch back)
+        if (h->act_ev_live) HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         // the drop-in loop steps next: its randoms are drawn while the host has the action
         if (done + m >= n && spec && spec_draw(h)) return -1;
         if (rows) {
@@ -3797,12 +3815,9 @@ int sacx_buffer_append_host_seeds(sacx_handle* h, const float* s, const float* a
     ag.replay = h->f0("replay"); ag.cap = h->cap; ag.stride = h->stride; ag.S = S; ag.A = A;
     ag.s = g; ag.a = g + tot * S; ag.r = g + tot * (S + A); ag.sp = g + tot * (S + A + 1); ag.d = g + tot * (2 * S + A + 1);
     ag.n = n; ag.ctl = h->ctl0(); ag.sstride = (int64_t)h->seed_bytes; ag.nseeds = K;
-    launch_append(ag, h->stream);
+    if (launch_staged_append(h, ag)) return -1;
     h->cur_size_host = std::min<int64_t>(h->cur_size_host + n, h->cap);   // every seed grows alike
     ++h->n_appends;
-    HIPCHK(h, hipGetLastError());
-    HIPCHK(h, hipEventRecord(h->pin_ev, h->stream));
-    h->pin_pending = true;
     return 0;
 }
 
@@ -3856,15 +3871,15 @@ int sacx_actor_act_host_seeds(sacx_handle* h, const float* obs, int64_t n, int32
         launch_act_rng(a, (int)n, r, h->stream);
         HIPCHK(h, hipGetLastError());
         h->done_seq += (uint32_t)(n * K);
-        HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
-        h->act_ev_live = true;
+        h->act_ev_live = !(h->act_poll && h->app_ctr);
+        if (h->act_ev_live) HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         if (spec_after_rng(h)) return -1;
     } else {
         launch_act_rows(a, (int)n, h->stream);
         HIPCHK(h, hipGetLastError());
         h->done_seq += (uint32_t)(n * K);
-        HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
-        h->act_ev_live = true;
+        h->act_ev_live = !(h->act_poll && h->app_ctr);
+        if (h->act_ev_live) HIPCHK(h, hipEventRecord(h->act_ev, h->stream));
         if (spec && spec_draw(h)) return -1;
     }
     if (act_rows_wait(h)) return -1;

@@ -147,6 +147,10 @@ for step in "$@"; do
       env "$ev" timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$PWD/$OUT/dtr$n" -o d \
           -- python tools/dropin_trace.py run > "$log" 2>&1 && python tools/dropin_trace.py "$OUT/dtr$n" >> "$log" 2>&1
       rc=$?; echo "[$n dropintr $arg] rc=$rc"; grep -A3 "iterations:" "$log" ;;
+    runs)       # sac_eo.train --runs K serial vs lock-step packed: runs=<K>:<alg>:<steps>[:VAR=VALUE]
+      IFS=: read -r rk ralg rsteps renv <<< "$arg"
+      env "${renv:-SACX_NONE=0}" timeout -k 10 400 python tools/packed_runs_time.py "$rk" "$ralg" "$rsteps" 2 > "$log" 2>&1
+      rc=$?; echo "[$n runs $arg] rc=$rc"; grep -E "^(serial|packed|pool)" "$log" ;;
     ktime)
       timeout -k 10 200 python tools/ktime_dump.py "${arg:-hc}" > "$log" 2>&1
       rc=$?; echo "[$n ktime ${arg:-hc}] rc=$rc $(tail -n 1 "$log")" ;;
