@@ -184,13 +184,15 @@ def test_held_append_and_skipped_ctl_observed(gpu_available, monkeypatch):
     skipped k_set_ctl must be invisible: right after an append_host the ring read through Engine.v
     holds the row; any other entry point (a multi-update step, a stochastic act, a 2-row append,
     get_state) queues the held row first; ts_increment changes force the control block's rewrite.
-    The whole run equals SACX_APP_DEFER=0 SACX_CTL_SKIP=0 bit for bit."""
+    The gather's polar workgroups (SACX_SPEC_POLAR) and the pinned completion counts in place of
+    event markers (SACX_APP_CTR) likewise.  The whole run equals SACX_APP_DEFER=0 SACX_CTL_SKIP=0
+    SACX_SPEC_POLAR=0 SACX_APP_CTR=0 bit for bit."""
     from sac_eo.engine import Engine, EngineConfig
     B, N, n = 64, 500, 40
     outs = []
     for opt in ("1", "0"):
-        monkeypatch.setenv("SACX_APP_DEFER", opt)
-        monkeypatch.setenv("SACX_CTL_SKIP", opt)
+        for var in ("SACX_APP_DEFER", "SACX_CTL_SKIP", "SACX_SPEC_POLAR", "SACX_APP_CTR"):
+            monkeypatch.setenv(var, opt)
         _, st, buf, nrm, _ = make_learner(act="relu", B=B, N=N, seed=6, done_p=0.05)
         eng = Engine(EngineConfig(s_dim=17, a_dim=6, activation="relu", batch=B, buffer_capacity=N + 100,
                                   graph_steps=1, target_update_int=3))
